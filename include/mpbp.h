@@ -1,0 +1,207 @@
+/* libmpbp -- MI355X (gfx950) multiphase-Stokes block-preconditioner apply, C ABI.
+ *
+ * Plain pointers and sizes only.  Every pointer named "device" lives in HBM
+ * (hipMalloc / torch allocations); every `stream` is a hipStream_t passed as
+ * void*.  All functions return MPBP_OK (0) or a negative error code, with a
+ * message in mpbp_last_error().  No function allocates or synchronises unless
+ * its comment says "setup" -- the apply path is graph-capturable.
+ *
+ * Reference interfaces replaced (abarret/mp-block-preconditioners @ 2025-02-23):
+ *   mpbp_stokes_*         MultiphaseBlockPreconditioner.get_block_matrices   preconditioner.py:86-297
+ *                         MultiphaseBlockPreconditioner.get_big_A_matrix     preconditioner.py:299-341
+ *                         (thn / ths volume fractions                        preconditioner.py:9-15)
+ *   mpbp_spgemm_*         Gt_G = np.matmul(mD, G), Gt_F_G = (mD F) G          solve.py:246-249
+ *   mpbp_spmv             b_approx = np.matmul(A, u_vec)                      apply.py:72
+ *                         A @ xk in the FGMRES residual callback              solve.py:166
+ *   mpbp_jacobi_*         Jacobi(A, b, N, x)                                  solve.py:149-159
+ *   mpbp_cheb_*           inner Chebyshev sweeps (BASELINE.json configs[3])
+ *   mpbp_schur_apply      approx_schur_op(v) -- the LinearOperator matvec    solve.py:257-277
+ */
+#ifndef MPBP_H
+#define MPBP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPBP_OK 0
+#define MPBP_ERR_ARG (-1)
+#define MPBP_ERR_HIP (-2)
+#define MPBP_ERR_OVERFLOW (-3)
+#define MPBP_ERR_PATTERN (-4)
+
+/* operator ids for mpbp_stokes_{rows,cols,count,fill} */
+#define MPBP_OP_A 0    /* [[F, G], [d_div D, 0]], 5N x 5N                 preconditioner.py:339-341 */
+#define MPBP_OP_F 1    /* XI + d_u blockdiag(eta_n L_n, eta_s L_s), 4N x 4N preconditioner.py:331-337 */
+#define MPBP_OP_D 2    /* hstack(D_n, D_s) (unscaled), N x 4N             preconditioner.py:311 */
+#define MPBP_OP_G 3    /* vstack(d_p G_n, d_p G_s), 4N x N                preconditioner.py:313 */
+#define MPBP_OP_L_N 4  /* per-phase blocks of get_block_matrices(is_ths)  preconditioner.py:86-297 */
+#define MPBP_OP_L_S 5
+#define MPBP_OP_D_N 6
+#define MPBP_OP_D_S 7
+#define MPBP_OP_G_N 8
+#define MPBP_OP_G_S 9
+#define MPBP_OP_XI_N 10
+#define MPBP_OP_XI_S 11
+
+/* spmv epilogues */
+#define MPBP_SPMV_STORE 0  /* y = A x          */
+#define MPBP_SPMV_ADD 1    /* y = A x + z      */
+#define MPBP_SPMV_RESID 2  /* y = z - A x      */
+
+/* inner solvers of the approximate Schur preconditioner */
+#define MPBP_INNER_JACOBI 0
+#define MPBP_INNER_CHEBYSHEV 1
+
+/* halo callback phases / vector kinds (multi-GPU row partition) */
+#define MPBP_HALO_BEGIN 0
+#define MPBP_HALO_END 1
+#define MPBP_VEC_VELOCITY 0
+#define MPBP_VEC_PRESSURE 1
+
+typedef struct mpbp_csr {
+    int32_t nrows;
+    int32_t ncols;
+    int64_t nnz;
+    const int32_t* row_ptr; /* device, nrows + 1 */
+    const int32_t* col_idx; /* device, nnz */
+    const double* val;      /* device, nnz */
+} mpbp_csr;
+
+/* Row blocks: `count` (start, end) row pairs, device int32[2*count]; each block has at most 256
+ * rows and at most MPBP_BLOCK_NNZ nonzeros (or is a single longer row).  Built on the host by
+ * mpbp_plan_row_blocks from a host copy of row_ptr. */
+typedef struct mpbp_rowblocks {
+    const int32_t* pairs;
+    int32_t count;
+} mpbp_rowblocks;
+
+#define MPBP_BLOCK_ROWS 256
+#define MPBP_BLOCK_NNZ 4095
+
+typedef struct mpbp_stokes_params {
+    int32_t n;     /* grid is n x n, N = n*n cells, dx = dy = 1/n */
+    double xi;     /* drag coefficient */
+    double eta_n;  /* network viscosity */
+    double eta_s;  /* solvent viscosity */
+    double c;      /* c (w_thn = c * thn) */
+    double d_u;    /* d_u (viscous / drag scaling) */
+    double d_p;    /* d_p (gradient scaling) */
+    double d_div;  /* d_div (divergence scaling) */
+} mpbp_stokes_params;
+
+typedef struct mpbp_inner_solver {
+    int32_t kind;   /* MPBP_INNER_JACOBI or MPBP_INNER_CHEBYSHEV */
+    int32_t sweeps; /* >= 1 updates of x from x0 = 0 (sweeps - 1 SpMVs) */
+    double lmin;    /* Chebyshev interval of diag(A)^-1 A; ignored by Jacobi */
+    double lmax;
+} mpbp_inner_solver;
+
+typedef void (*mpbp_halo_fn)(void* ctx, int32_t vec_kind, double* x_ext, int32_t phase, void* stream);
+
+/* The apply's operands.  On one GPU every matrix's columns index the full vector and the
+ * *_bnd row blocks are empty.  Under a row partition the columns index the "ext" layout of the
+ * input vector kind (owned rows first, then ghost rows) and the halo callback fills the ghosts:
+ * BEGIN before the interior blocks are launched, END before the boundary blocks. */
+typedef struct mpbp_schur_plan {
+    int32_t nu, np;                  /* owned velocity rows (4N) and pressure rows (N) */
+    int32_t nu_ext, np_ext;          /* owned + ghost */
+    mpbp_csr F, D, G, GtG, GtFG;
+    mpbp_rowblocks F_int, F_bnd, D_int, D_bnd, G_int, G_bnd, P_int, P_bnd, Q_int, Q_bnd; /* P: GtG, Q: GtFG */
+    const double* diag_F;            /* device, nu */
+    const double* diag_P;            /* device, np (diagonal of GtG) */
+    mpbp_inner_solver inner_F, inner_P;
+    double* wu[4];                   /* device velocity work vectors, nu_ext each (Y, U0, U1, dir) */
+    double* wu_owned;                /* device, nu (W = G x_p) */
+    double* wp[7];                   /* device pressure work vectors, np_ext each */
+    mpbp_halo_fn halo;               /* NULL on one GPU */
+    void* halo_ctx;
+    void** prof_events;              /* optional: hipEvent_t pairs around every inner-F SpMV sweep */
+    int32_t prof_capacity;           /* number of event pairs available */
+    int32_t* prof_count;             /* host int: pairs recorded so far (caller resets) */
+} mpbp_schur_plan;
+
+const char* mpbp_version(void);
+const char* mpbp_last_error(void);
+
+/* ---- assembly (setup) ---------------------------------------------------------------------- */
+/* thn at cell centres / u faces / v faces, preconditioner.py:9-11 (device arrays of n*n). */
+int mpbp_stokes_theta(int32_t n, double* cell, double* uface, double* vface, void* stream);
+int64_t mpbp_stokes_rows(int32_t n, int32_t op);
+int64_t mpbp_stokes_cols(int32_t n, int32_t op);
+/* row_nnz[r] for every row of `op` (device int32[rows]). */
+int mpbp_stokes_count(const mpbp_stokes_params* prm, int32_t op, const double* cell,
+                      int32_t* row_nnz, void* stream);
+/* Fill col_idx / val given row_ptr (device).  Columns sorted within each row. */
+int mpbp_stokes_fill(const mpbp_stokes_params* prm, int32_t op, const double* cell,
+                     const double* uface, const double* vface, const int32_t* row_ptr,
+                     int32_t* col_idx, double* val, void* stream);
+/* row_ptr[0] = 0, row_ptr[i+1] = row_ptr[i] + row_nnz[i] (device); *total (host) = row_ptr[n].
+ * Setup: synchronises the stream. */
+int mpbp_exclusive_scan(const int32_t* row_nnz, int32_t* row_ptr, int64_t n, int64_t* total,
+                        void* stream);
+
+/* ---- sparse products (setup) ----------------------------------------------------------------- */
+/* C = alpha * A B with every structural product kept; row_nnz device int32[A.nrows].
+ * Setup: synchronises the stream (returns MPBP_ERR_OVERFLOW for a row wider than 64). */
+int mpbp_spgemm_count(const mpbp_csr* A, const mpbp_csr* B, int32_t* row_nnz, void* stream);
+int mpbp_spgemm_fill(const mpbp_csr* A, const mpbp_csr* B, double alpha, const int32_t* row_ptr,
+                     int32_t* col_idx, double* val, void* stream);
+
+/* ---- planning / helpers (setup) ------------------------------------------------------------ */
+/* Host-side greedy row blocking of rows [row_begin, row_end) of a HOST row_ptr; writes at most
+ * `capacity` pairs to `pairs` (host) and returns the number of blocks needed. */
+int64_t mpbp_plan_row_blocks(const int32_t* row_ptr, int32_t row_begin, int32_t row_end,
+                             int32_t* pairs, int64_t capacity);
+/* diag[r] = A[r, r + col_offset]; *missing (host) = rows without that entry.  Setup (syncs). */
+int mpbp_csr_diag(const mpbp_csr* A, int32_t col_offset, double* diag, int32_t* missing, void* stream);
+/* *lmax (host) = max_r sum_k |A[r,k]| / |diag[r]| (Gershgorin bound of diag^-1 A). Setup (syncs). */
+int mpbp_gershgorin(const mpbp_csr* A, const double* diag, double* lmax, void* stream);
+/* Row extraction for a row partition: local row i = global row rows[i]; columns mapped through
+ * colmap (global col -> local ext col, -1 = not available).  count writes row_nnz (device);
+ * fill returns MPBP_ERR_PATTERN when a needed column is unmapped.  Setup (fill syncs). */
+int mpbp_csr_extract_count(const mpbp_csr* A, const int32_t* rows, int32_t nrows_local,
+                           int32_t* row_nnz, void* stream);
+int mpbp_csr_extract_fill(const mpbp_csr* A, const int32_t* rows, int32_t nrows_local,
+                          const int32_t* colmap, const int32_t* row_ptr_local, int32_t* col_local,
+                          double* val_local, void* stream);
+
+/* ---- apply path (graph-capturable, no sync) ------------------------------------------------ */
+/* y = op(A x) over the rows of `blocks` (mode MPBP_SPMV_*; z unused for STORE). */
+int mpbp_spmv(const mpbp_csr* A, const mpbp_rowblocks* blocks, int32_t mode, const double* x,
+              const double* z, double* y, void* stream);
+/* x_out = b / diag (first Jacobi sweep from 0); x_out = sub - that when sub != NULL. */
+int mpbp_jacobi_init(int32_t nrows, const double* b, const double* diag, const double* sub,
+                     double* x_out, void* stream);
+/* x_out = x_in + (b - A x_in) / diag  (optionally sub - that). */
+int mpbp_jacobi_step(const mpbp_csr* A, const mpbp_rowblocks* blocks, const double* x_in,
+                     const double* b, const double* diag, const double* sub, double* x_out,
+                     void* stream);
+/* d = c2 * (b / diag); x_out = d (optionally sub - d). */
+int mpbp_cheb_init(int32_t nrows, const double* b, const double* diag, double c2, double* d,
+                   const double* sub, double* x_out, void* stream);
+/* z = (b - A x_in)/diag; d = c1 d + c2 z; x_out = x_in + d (optionally sub - that). */
+int mpbp_cheb_step(const mpbp_csr* A, const mpbp_rowblocks* blocks, const double* x_in,
+                   const double* b, const double* diag, double c1, double c2, double* d,
+                   const double* sub, double* x_out, void* stream);
+/* Chebyshev coefficients used by mpbp_schur_apply for sweep s (0-based): c1[s], c2[s]. Host. */
+int mpbp_cheb_coeffs(double lmin, double lmax, int32_t sweeps, double* c1, double* c2);
+/* out = M^-1 v with M the block upper-triangular approximate-commutator preconditioner
+ * (solve.py:257-277): v, out are device vectors of nu + np owned entries. */
+int mpbp_schur_apply(const mpbp_schur_plan* plan, const double* v, double* out, void* stream);
+
+/* gather: dst[i] = src[idx[i]] ; scatter: dst[idx[i]] = src[i]   (halo pack / unpack) */
+int mpbp_gather(int32_t count, const int32_t* idx, const double* src, double* dst, void* stream);
+int mpbp_scatter(int32_t count, const int32_t* idx, const double* src, double* dst, void* stream);
+
+/* hipEvent helpers for callers without a HIP binding (bench profiling). */
+int mpbp_event_create(void** ev);
+int mpbp_event_destroy(void* ev);
+int mpbp_event_elapsed_ms(void* start, void* stop, float* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPBP_H */

@@ -1,0 +1,1064 @@
+// libmpbp -- MI355X (gfx950) HIP kernels + C ABI for the multiphase-Stokes
+// block-preconditioner apply.  Header: include/mpbp.h.  Design: DESIGN.md.
+//
+// Built with -ffp-contract=off: every kernel performs the IEEE operations of the
+// sequential checker oracle/csr_oracle.c in the same order (row sums left to
+// right from 0.0, no fused multiply-add), so results are bit-identical to it.
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <vector>
+
+#include "mpbp.h"
+
+namespace {
+
+thread_local char g_err[1024] = "";
+
+int set_error(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define MPBP_HIP(call)                                                                      \
+    do {                                                                                    \
+        hipError_t e_ = (call);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return set_error(MPBP_ERR_HIP, "%s: %s", #call, hipGetErrorString(e_));         \
+    } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+constexpr int kBlock = 256;                    // 4 wave64 per workgroup, one row per thread
+constexpr int kCap = MPBP_BLOCK_NNZ + 1;       // products staged in LDS per row block (32 KiB)
+constexpr int kPairs = kCap / (2 * kBlock);    // 16-byte (2 x f64) loads per thread
+
+inline int grid_for(int64_t n, int block = kBlock) { return (int)((n + block - 1) / block); }
+
+// ================================================================== theta ====
+// thn(y, x) = 0.25 sin(2 pi x) sin(2 pi y) + 0.5 -- preconditioner.py:9-11
+__device__ inline double thn_fn(double y, double x) {
+    const double two_pi = 2.0 * 3.141592653589793;
+    return 0.25 * sin(two_pi * x) * sin(two_pi * y) + 0.5;
+}
+
+__global__ void k_theta(int n, double* cell, double* uface, double* vface) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)n * n) return;
+    const int r = (int)(i / n), c = (int)(i % n);
+    const double dx = 1.0 / n, dy = 1.0 / n;
+    cell[i] = thn_fn(-(r + 0.5) * dy, (c + 0.5) * dx);   // get_thn_vals cell centres
+    uface[i] = thn_fn(-(r + 0.5) * dy, c * dx);          // w_thn, u rows (preconditioner.py:325)
+    vface[i] = thn_fn((double)(-r) * dy, (c + 0.5) * dx);  // w_thn, v rows (preconditioner.py:326)
+}
+
+// =============================================================== stencils ====
+// The reference assigns into dense matrices; a later write to the same (row, col)
+// replaces the earlier one (n <= 2 only).  RowBuf restates that: last write wins.
+struct RowBuf {
+    int m;
+    int32_t col[16];
+    double val[16];
+};
+
+__device__ inline void put(RowBuf& w, int32_t col, double v) {
+    for (int k = 0; k < w.m; ++k)
+        if (w.col[k] == col) { w.val[k] = v; return; }
+    w.col[w.m] = col;
+    w.val[w.m] = v;
+    ++w.m;
+}
+
+__device__ inline void sort_row(RowBuf& w) {
+    for (int i = 1; i < w.m; ++i) {
+        const int32_t cj = w.col[i];
+        const double cv = w.val[i];
+        int t = i - 1;
+        while (t >= 0 && w.col[t] > cj) { w.col[t + 1] = w.col[t]; w.val[t + 1] = w.val[t]; --t; }
+        w.col[t + 1] = cj;
+        w.val[t + 1] = cv;
+    }
+}
+
+// Periodic cell-centred volume fraction of one phase (ths = 1 - thn, preconditioner.py:74-81).
+struct Phase {
+    int n;
+    const double* cell;
+    int s;
+    __device__ int wrap(int a) const { a %= n; return a < 0 ? a + n : a; }
+    __device__ int32_t idx(int r, int c) const { return wrap(r) * n + wrap(c); }
+    __device__ double T(int r, int c) const { const double v = cell[idx(r, c)]; return s ? 1.0 - v : v; }
+};
+
+// L rows of one phase (2N x 2N) and the XI diagonal entry of that row.
+// u rows: preconditioner.py:100-179 ; v rows: preconditioner.py:240-295 ; XI: :124-125.
+__device__ void phase_L_row(const Phase& g, double xi, int32_t i, RowBuf& w, double& xi_ii) {
+    const int n = g.n;
+    const int32_t N = n * n;
+    const double dx = 1.0 / n, dy = 1.0 / n;
+    w.m = 0;
+    if (i < N) {
+        const int r = i / n, c = i % n;
+        const double tij = g.T(r, c - 1), tip1j = g.T(r, c);
+        const double tijp1 = g.T(r - 1, c - 1), tip1jp1 = g.T(r - 1, c);
+        const double tijm1 = g.T(r + 1, c - 1), tip1jm1 = g.T(r + 1, c);
+        const double iph_jph = 0.25 * (tij + tijp1 + tip1jp1 + tip1j);
+        const double iph_jmh = 0.25 * (tij + tip1j + tijm1 + tip1jm1);
+        const double iph_j = 0.5 * (tij + tip1j);
+        xi_ii = xi * iph_j * (1.0 - iph_j);
+        put(w, i, 1.0 / (dx * dx) * (-tip1j - tij) + 1.0 / (dy * dy) * (-iph_jph - iph_jmh));
+        put(w, N + g.idx(r, c), 1.0 / (dx * dy) * (-tip1j + iph_jph));
+        put(w, g.idx(r, c - 1), 1.0 / (dx * dx) * (tij));
+        put(w, g.idx(r, c + 1), tip1j / (dx * dx));
+        put(w, g.idx(r - 1, c), 1.0 / (dy * dy) * (iph_jph));
+        put(w, g.idx(r + 1, c), 1.0 / (dy * dy) * (iph_jmh));
+        put(w, N + g.idx(r, c - 1), 1.0 / (dy * dx) * (tij - iph_jph));
+        put(w, N + g.idx(r + 1, c - 1), 1.0 / (dy * dx) * (iph_jmh - tij));
+        put(w, N + g.idx(r + 1, c), 1.0 / (dx * dy) * (tip1j - iph_jmh));
+    } else {
+        const int32_t k = i - N;
+        const int r = k / n, c = k % n;
+        const double ip1_jph = 0.5 * (g.T(r, c) + g.T(r - 1, c));   // set in the u loop (:125)
+        xi_ii = xi * ip1_jph * (1.0 - ip1_jph);
+        const double tij = g.T(r, c), tip1j = g.T(r, c + 1);
+        const double tijp1 = g.T(r - 1, c), tip1jp1 = g.T(r - 1, c + 1);
+        const double tim1j = g.T(r, c - 1), tim1jp1 = g.T(r - 1, c - 1);
+        const double imh_jph = 0.25 * (tim1j + tim1jp1 + tij + tijp1);
+        const double iph_jph = 0.25 * (tij + tip1j + tijp1 + tip1jp1);
+        put(w, i, -1.0 / (dy * dy) * (tijp1 + tij) - 1.0 / (dx * dx) * (iph_jph + imh_jph));
+        put(w, N + g.idx(r, c - 1), 1.0 / (dx * dx) * imh_jph);
+        put(w, N + g.idx(r, c + 1), 1.0 / (dx * dx) * iph_jph);
+        put(w, N + g.idx(r - 1, c), 1.0 / (dy * dy) * tijp1);
+        put(w, N + g.idx(r + 1, c), 1.0 / (dy * dy) * tij);
+        put(w, k, 1.0 / (dx * dy) * (imh_jph - tij));
+        put(w, g.idx(r, c + 1), 1.0 / (dy * dx) * (tij - iph_jph));
+        put(w, g.idx(r - 1, c), 1.0 / (dy * dx) * (tijp1 - imh_jph));
+        put(w, g.idx(r - 1, c + 1), 1.0 / (dy * dx) * (iph_jph - tijp1));
+    }
+    sort_row(w);
+}
+
+// G rows of one phase (2N x N), preconditioner.py:203-219.
+__device__ void phase_G_row(const Phase& g, int32_t i, RowBuf& w) {
+    const int n = g.n;
+    const int32_t N = n * n;
+    const double dx = 1.0 / n, dy = 1.0 / n;
+    w.m = 0;
+    if (i < N) {
+        const int r = i / n, c = i % n;
+        const double imh_j = 0.5 * (g.T(r, c) + g.T(r, c - 1));
+        put(w, i, (1.0 / dx) * imh_j);
+        put(w, g.idx(r, c - 1), -(1.0 / dx) * imh_j);
+    } else {
+        const int32_t k = i - N;
+        const int r = k / n, c = k % n;
+        const double i_jph = 0.5 * (g.T(r, c) + g.T(r - 1, c));
+        put(w, k, -(1.0 / dy) * i_jph);
+        put(w, g.idx(r - 1, c), (1.0 / dy) * i_jph);
+    }
+    sort_row(w);
+}
+
+// D rows of one phase (N x 2N), preconditioner.py:221-238.
+__device__ void phase_D_row(const Phase& g, int32_t k, RowBuf& w) {
+    const int n = g.n;
+    const int32_t N = n * n;
+    const double dx = 1.0 / n, dy = 1.0 / n;
+    const int r = k / n, c = k % n;
+    const double tij = g.T(r, c);
+    const double iph_j = 0.5 * (tij + g.T(r, c + 1));
+    const double imh_j = 0.5 * (tij + g.T(r, c - 1));
+    const double i_jph = 0.5 * (tij + g.T(r - 1, c));
+    const double i_jmh = 0.5 * (tij + g.T(r + 1, c));
+    w.m = 0;
+    put(w, g.idx(r, c + 1), 1.0 / dx * iph_j);
+    put(w, k, -1.0 / dx * imh_j);
+    put(w, N + k, 1.0 / dy * i_jph);
+    put(w, N + g.idx(r + 1, c), -1.0 / dy * i_jmh);
+    sort_row(w);
+}
+
+struct StokesDev {
+    int n;
+    double xi, eta_n, eta_s, c, d_u, d_p, d_div;
+    const double* cell;
+    const double* uface;
+    const double* vface;
+};
+
+__device__ inline void append(RowBuf& o, int32_t col, double v) {
+    o.col[o.m] = col;
+    o.val[o.m] = v;
+    ++o.m;
+}
+
+// F row R of [u_n, v_n, u_s, v_s]: F = XI + d_u blockdiag(eta_n L_n, eta_s L_s)
+// (preconditioner.py:310, 315-337).  Columns come out sorted.
+__device__ void F_row(const StokesDev& P, int32_t R, RowBuf& o) {
+    const int32_t N = P.n * P.n;
+    const int p = R >= 2 * N;
+    const int32_t i = R - p * 2 * N;
+    const Phase g{P.n, P.cell, p};
+    RowBuf L;
+    double xi_ii;
+    phase_L_row(g, P.xi, i, L, xi_ii);
+    // Face tables are absent when only the pattern is counted.
+    const double th = !P.uface ? 0.0 : (i < N) ? P.uface[i] : P.vface[i - N];
+    const double w = p ? P.c * (1.0 - th) : P.c * th;          // w_ths = c*ths, w_thn = c*thn
+    const double eta = p ? P.eta_s : P.eta_n;
+    const int32_t off = p * 2 * N, other = (1 - p) * 2 * N;
+    o.m = 0;
+    if (p == 1) append(o, other + i, P.d_u * xi_ii);              // d_u * XI_s (cross block)
+    for (int k = 0; k < L.m; ++k) {
+        double v = P.d_u * (eta * L.val[k]);
+        if (L.col[k] == i) v = (w - P.d_u * xi_ii) + v;           // (w - d_u XI) + d_u eta L
+        append(o, off + L.col[k], v);
+    }
+    if (p == 0) append(o, other + i, P.d_u * xi_ii);              // d_u * XI_n (cross block)
+}
+
+__device__ void build_row(const StokesDev& P, int op, int32_t R, RowBuf& o) {
+    const int32_t N = P.n * P.n;
+    RowBuf t;
+    double xi_ii;
+    o.m = 0;
+    switch (op) {
+    case MPBP_OP_A:
+        if (R < 4 * N) {
+            F_row(P, R, o);
+            const int p = R >= 2 * N;
+            phase_G_row(Phase{P.n, P.cell, p}, R - p * 2 * N, t);
+            for (int k = 0; k < t.m; ++k) append(o, 4 * N + t.col[k], P.d_p * t.val[k]);
+        } else {
+            const int32_t q = R - 4 * N;
+            phase_D_row(Phase{P.n, P.cell, 0}, q, t);
+            for (int k = 0; k < t.m; ++k) append(o, t.col[k], P.d_div * t.val[k]);
+            phase_D_row(Phase{P.n, P.cell, 1}, q, t);
+            for (int k = 0; k < t.m; ++k) append(o, 2 * N + t.col[k], P.d_div * t.val[k]);
+        }
+        break;
+    case MPBP_OP_F:
+        F_row(P, R, o);
+        break;
+    case MPBP_OP_D:
+        phase_D_row(Phase{P.n, P.cell, 0}, R, t);
+        for (int k = 0; k < t.m; ++k) append(o, t.col[k], t.val[k]);
+        phase_D_row(Phase{P.n, P.cell, 1}, R, t);
+        for (int k = 0; k < t.m; ++k) append(o, 2 * N + t.col[k], t.val[k]);
+        break;
+    case MPBP_OP_G: {
+        const int p = R >= 2 * N;
+        phase_G_row(Phase{P.n, P.cell, p}, R - p * 2 * N, t);
+        for (int k = 0; k < t.m; ++k) append(o, t.col[k], P.d_p * t.val[k]);
+        break;
+    }
+    case MPBP_OP_L_N:
+    case MPBP_OP_L_S:
+        phase_L_row(Phase{P.n, P.cell, op == MPBP_OP_L_S}, P.xi, R, o, xi_ii);
+        break;
+    case MPBP_OP_D_N:
+    case MPBP_OP_D_S:
+        phase_D_row(Phase{P.n, P.cell, op == MPBP_OP_D_S}, R, o);
+        break;
+    case MPBP_OP_G_N:
+    case MPBP_OP_G_S:
+        phase_G_row(Phase{P.n, P.cell, op == MPBP_OP_G_S}, R, o);
+        break;
+    case MPBP_OP_XI_N:
+    case MPBP_OP_XI_S:
+        phase_L_row(Phase{P.n, P.cell, op == MPBP_OP_XI_S}, P.xi, R, t, xi_ii);
+        append(o, R, xi_ii);
+        break;
+    default:
+        break;
+    }
+}
+
+__global__ void k_stokes_count(StokesDev P, int op, int64_t nrows, int32_t* row_nnz) {
+    const int64_t R = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (R >= nrows) return;
+    RowBuf o;
+    build_row(P, op, (int32_t)R, o);
+    row_nnz[R] = o.m;
+}
+
+__global__ void k_stokes_fill(StokesDev P, int op, int64_t nrows, const int32_t* rp, int32_t* ci,
+                              double* va) {
+    const int64_t R = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (R >= nrows) return;
+    RowBuf o;
+    build_row(P, op, (int32_t)R, o);
+    const int32_t base = rp[R];
+    for (int k = 0; k < o.m; ++k) {
+        ci[base + k] = o.col[k];
+        va[base + k] = o.val[k];
+    }
+}
+
+// One 1024-thread workgroup scans the whole array in 1024-element chunks (setup only).
+__global__ void __launch_bounds__(1024) k_exclusive_scan(const int32_t* in, int32_t* out, int64_t n,
+                                                         long long* total) {
+    __shared__ long long wsum[16];
+    __shared__ long long carry;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int64_t base = 0; base < n; base += 1024) {
+        const int64_t i = base + threadIdx.x;
+        const long long v = i < n ? (long long)in[i] : 0;
+        long long x = v;
+        for (int d = 1; d < 64; d <<= 1) {
+            const long long y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) wsum[wid] = x;
+        __syncthreads();
+        if (wid == 0) {
+            long long s = lane < 16 ? wsum[lane] : 0;
+            for (int d = 1; d < 16; d <<= 1) {
+                const long long y = __shfl_up(s, d, 64);
+                if (lane >= d) s += y;
+            }
+            if (lane < 16) wsum[lane] = s;
+        }
+        __syncthreads();
+        const long long excl = carry + (wid ? wsum[wid - 1] : 0) + x - v;
+        if (i < n) out[i] = (int32_t)excl;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = excl + v;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[n] = (int32_t)carry;
+        *total = carry;
+    }
+}
+
+// ================================================================ SpGEMM ====
+struct Csr {
+    const int32_t* rp;
+    const int32_t* ci;
+    const double* va;
+};
+
+constexpr int kSpgemmMaxW = 64;
+
+// Row r of A*B: first-touch order over (A row order, B row order), then sorted by column.
+// Same operation order as oracle/csr_oracle.c:row_product.
+__device__ int spgemm_row(const Csr A, const Csr B, int32_t r, int32_t* cols, double* vals) {
+    int m = 0;
+    for (int32_t ka = A.rp[r]; ka < A.rp[r + 1]; ++ka) {
+        const double a = A.va[ka];
+        const int32_t k = A.ci[ka];
+        for (int32_t kb = B.rp[k]; kb < B.rp[k + 1]; ++kb) {
+            const int32_t j = B.ci[kb];
+            const double v = a * B.va[kb];
+            int t = 0;
+            while (t < m && cols[t] != j) ++t;
+            if (t < m) {
+                vals[t] += v;
+            } else {
+                if (m == kSpgemmMaxW) return -1;
+                cols[m] = j;
+                vals[m] = v;
+                ++m;
+            }
+        }
+    }
+    for (int i = 1; i < m; ++i) {
+        const int32_t cj = cols[i];
+        const double cv = vals[i];
+        int t = i - 1;
+        while (t >= 0 && cols[t] > cj) { cols[t + 1] = cols[t]; vals[t + 1] = vals[t]; --t; }
+        cols[t + 1] = cj;
+        vals[t + 1] = cv;
+    }
+    return m;
+}
+
+__global__ void k_spgemm_count(Csr A, Csr B, int32_t nrows, int32_t* row_nnz, int* overflow) {
+    const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrows) return;
+    int32_t cols[kSpgemmMaxW];
+    double vals[kSpgemmMaxW];
+    const int m = spgemm_row(A, B, r, cols, vals);
+    if (m < 0) { atomicAdd(overflow, 1); row_nnz[r] = 0; }
+    else row_nnz[r] = m;
+}
+
+__global__ void k_spgemm_fill(Csr A, Csr B, int32_t nrows, double alpha, const int32_t* crp,
+                              int32_t* cci, double* cva) {
+    const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrows) return;
+    int32_t cols[kSpgemmMaxW];
+    double vals[kSpgemmMaxW];
+    const int m = spgemm_row(A, B, r, cols, vals);
+    const int32_t base = crp[r];
+    for (int k = 0; k < m; ++k) {
+        cci[base + k] = cols[k];
+        cva[base + k] = alpha * vals[k];
+    }
+}
+
+// ============================================================ helpers ====
+__global__ void k_csr_diag(Csr A, int32_t nrows, int32_t col_offset, double* diag, int* missing) {
+    const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrows) return;
+    double d = 0.0;
+    bool found = false;
+    for (int32_t k = A.rp[r]; k < A.rp[r + 1]; ++k)
+        if (A.ci[k] == r + col_offset) { d = A.va[k]; found = true; }
+    diag[r] = d;
+    if (!found) atomicAdd(missing, 1);
+}
+
+__global__ void k_gershgorin(Csr A, int32_t nrows, const double* diag, unsigned long long* out) {
+    const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    double q = 0.0;
+    if (r < nrows) {
+        double s = 0.0;
+        for (int32_t k = A.rp[r]; k < A.rp[r + 1]; ++k) s += fabs(A.va[k]);
+        q = s / fabs(diag[r]);
+    }
+    // non-negative doubles order like their bit patterns
+    for (int d = 32; d > 0; d >>= 1) {
+        const double o = __shfl_xor(q, d, 64);
+        q = o > q ? o : q;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(out, (unsigned long long)__double_as_longlong(q));
+}
+
+__global__ void k_extract_count(Csr A, const int32_t* rows, int32_t nloc, int32_t* row_nnz) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nloc) return;
+    const int32_t r = rows[i];
+    row_nnz[i] = A.rp[r + 1] - A.rp[r];
+}
+
+__global__ void k_extract_fill(Csr A, const int32_t* rows, int32_t nloc, const int32_t* colmap,
+                               const int32_t* lrp, int32_t* lci, double* lva, int* bad) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nloc) return;
+    const int32_t r = rows[i];
+    int32_t o = lrp[i];
+    for (int32_t k = A.rp[r]; k < A.rp[r + 1]; ++k, ++o) {   // keep the global row's order
+        const int32_t lc = colmap[A.ci[k]];
+        if (lc < 0) atomicAdd(bad, 1);
+        lci[o] = lc < 0 ? 0 : lc;
+        lva[o] = A.va[k];
+    }
+}
+
+__global__ void k_gather(int32_t count, const int32_t* idx, const double* src, double* dst) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) dst[i] = src[idx[i]];
+}
+
+__global__ void k_scatter(int32_t count, const int32_t* idx, const double* src, double* dst) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) dst[idx[i]] = src[i];
+}
+
+// ================================================================== SpMV ====
+// Row blocks are dealt round-robin over the 8 XCDs; give every XCD a contiguous run of
+// blocks instead, so the +-n stencil neighbours of a block's rows sit in the same L2.
+// Placement changes speed only, never results.
+__device__ inline int xcd_swizzle(int b, int nb) {
+    const int full = nb & ~7;
+    if (b >= full) return b;
+    const int per = full >> 3;
+    return (b & 7) * per + (b >> 3);
+}
+
+struct EpiStore {
+    double* y;
+    __device__ void operator()(int32_t r, double acc) const { y[r] = acc; }
+};
+struct EpiAdd {   // rhs = D Finv_v + v_p   (solve.py:259)
+    const double* z;
+    double* y;
+    __device__ void operator()(int32_t r, double acc) const { y[r] = acc + z[r]; }
+};
+struct EpiResid {
+    const double* z;
+    double* y;
+    __device__ void operator()(int32_t r, double acc) const { y[r] = z[r] - acc; }
+};
+struct EpiJacobi {   // x = (b - R x)/D in residual form (solve.py:158)
+    const double* xin;
+    const double* b;
+    const double* diag;
+    const double* sub;
+    double* xout;
+    __device__ void operator()(int32_t r, double acc) const {
+        const double x = xin[r] + (b[r] - acc) / diag[r];
+        xout[r] = sub ? sub[r] - x : x;
+    }
+};
+struct EpiCheb {
+    const double* xin;
+    const double* b;
+    const double* diag;
+    double* d;
+    double c1, c2;
+    const double* sub;
+    double* xout;
+    __device__ void operator()(int32_t r, double acc) const {
+        const double z = (b[r] - acc) / diag[r];
+        const double dn = c1 * d[r] + c2 * z;
+        d[r] = dn;
+        const double x = xin[r] + dn;
+        xout[r] = sub ? sub[r] - x : x;
+    }
+};
+
+// CSR SpMV over a list of row blocks.  Phase 1 streams the block's [row_ptr[r0], row_ptr[r1])
+// slice of col_idx / val with 16-byte loads (fully coalesced across the workgroup), gathers x
+// and stages the products in LDS; phase 2 gives each row to one lane, which sums its products
+// left to right (a segmented reduction with sequential order -> bit-exact with the oracle) and
+// runs the fused epilogue.
+template <class Epi>
+__global__ void __launch_bounds__(kBlock) k_csr_rows(Csr A, const double* __restrict__ x,
+                                                     const int2* __restrict__ blocks, int nblocks,
+                                                     Epi epi) {
+    __shared__ double prod[kCap];
+    const int b = xcd_swizzle(blockIdx.x, nblocks);
+    const int2 blk = blocks[b];
+    const int32_t r0 = blk.x, r1 = blk.y;
+    const int32_t s = A.rp[r0], e = A.rp[r1];
+    const int tid = threadIdx.x;
+    const int32_t base = s & ~1;
+    if (e - base <= kCap) {
+        double2 v[kPairs];
+        int2 cc[kPairs];
+#pragma unroll
+        for (int j = 0; j < kPairs; ++j) {
+            const int32_t k = base + 2 * (tid + j * kBlock);
+            if (k + 1 < e) {
+                v[j] = *reinterpret_cast<const double2*>(A.va + k);
+                cc[j] = *reinterpret_cast<const int2*>(A.ci + k);
+            } else if (k < e) {
+                v[j] = make_double2(A.va[k], 0.0);
+                cc[j] = make_int2(A.ci[k], 0);
+            } else {
+                v[j] = make_double2(0.0, 0.0);
+                cc[j] = make_int2(0, 0);
+            }
+        }
+        double x0[kPairs], x1[kPairs];
+#pragma unroll
+        for (int j = 0; j < kPairs; ++j) {
+            const int32_t k = base + 2 * (tid + j * kBlock);
+            x0[j] = (k >= s && k < e) ? x[cc[j].x] : 0.0;
+            x1[j] = (k + 1 >= s && k + 1 < e) ? x[cc[j].y] : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < kPairs; ++j) {
+            const int32_t k = base + 2 * (tid + j * kBlock);
+            if (k >= s && k < e) prod[k - s] = v[j].x * x0[j];
+            if (k + 1 >= s && k + 1 < e) prod[k + 1 - s] = v[j].y * x1[j];
+        }
+        __syncthreads();
+        const int32_t r = r0 + tid;
+        if (r < r1) {
+            const int32_t ks = A.rp[r] - s, ke = A.rp[r + 1] - s;
+            double acc = 0.0;
+            for (int32_t k = ks; k < ke; ++k) acc += prod[k];
+            epi(r, acc);
+        }
+    } else {
+        // A single row longer than the LDS stage (the planner never groups such a row).
+        // Tree-reduced: not in sequential order.
+        double part = 0.0;
+        for (int32_t k = s + tid; k < e; k += kBlock) part += A.va[k] * x[A.ci[k]];
+        prod[tid] = part;
+        __syncthreads();
+        for (int w = kBlock / 2; w > 0; w >>= 1) {
+            if (tid < w) prod[tid] += prod[tid + w];
+            __syncthreads();
+        }
+        if (tid == 0) epi(r0, prod[0]);
+    }
+}
+
+__global__ void k_jacobi_init(int32_t n, const double* b, const double* diag, const double* sub,
+                              double* xout) {
+    const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const double x = b[r] / diag[r];
+    xout[r] = sub ? sub[r] - x : x;
+}
+
+__global__ void k_cheb_init(int32_t n, const double* b, const double* diag, double c2, double* d,
+                            const double* sub, double* xout) {
+    const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const double z = b[r] / diag[r];
+    const double dn = c2 * z;
+    d[r] = dn;
+    xout[r] = sub ? sub[r] - dn : dn;
+}
+
+inline Csr to_csr(const mpbp_csr* A) { return Csr{A->row_ptr, A->col_idx, A->val}; }
+
+template <class Epi>
+int launch_rows(const mpbp_csr* A, const mpbp_rowblocks* blk, const double* x, Epi epi, hipStream_t st) {
+    if (!blk || blk->count <= 0) return MPBP_OK;
+    k_csr_rows<Epi><<<blk->count, kBlock, 0, st>>>(to_csr(A), x,
+                                                    reinterpret_cast<const int2*>(blk->pairs),
+                                                    blk->count, epi);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int check_csr(const mpbp_csr* A) {
+    if (!A || !A->row_ptr || A->nrows < 0) return set_error(MPBP_ERR_ARG, "invalid csr");
+    if (A->nnz > 0 && (!A->col_idx || !A->val)) return set_error(MPBP_ERR_ARG, "csr without entries");
+    return MPBP_OK;
+}
+
+// Chebyshev-Jacobi coefficients (Saad, Iterative Methods, Alg. 12.1 with diag(A)^-1 preconditioning).
+void cheb_coeffs(double lmin, double lmax, int sweeps, double* c1, double* c2) {
+    const double theta = (lmax + lmin) / 2.0;
+    const double delta = (lmax - lmin) / 2.0;
+    const double sigma = theta / delta;
+    double rho = 1.0 / sigma;
+    c1[0] = 0.0;
+    c2[0] = 1.0 / theta;
+    for (int s = 1; s < sweeps; ++s) {
+        const double rho_new = 1.0 / (2.0 * sigma - rho);
+        c1[s] = rho_new * rho;
+        c2[s] = 2.0 * rho_new / delta;
+        rho = rho_new;
+    }
+}
+
+}  // namespace
+
+// ================================================================ C ABI ====
+extern "C" {
+
+const char* mpbp_version(void) { return "libmpbp 0.1 (gfx950)"; }
+const char* mpbp_last_error(void) { return g_err; }
+
+int mpbp_stokes_theta(int32_t n, double* cell, double* uface, double* vface, void* stream) {
+    if (n < 1 || !cell || !uface || !vface) return set_error(MPBP_ERR_ARG, "mpbp_stokes_theta: bad args");
+    k_theta<<<grid_for((int64_t)n * n), kBlock, 0, as_stream(stream)>>>(n, cell, uface, vface);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int64_t mpbp_stokes_rows(int32_t n, int32_t op) {
+    const int64_t N = (int64_t)n * n;
+    switch (op) {
+    case MPBP_OP_A: return 5 * N;
+    case MPBP_OP_F: case MPBP_OP_G: return 4 * N;
+    case MPBP_OP_D: case MPBP_OP_D_N: case MPBP_OP_D_S: return N;
+    case MPBP_OP_L_N: case MPBP_OP_L_S: case MPBP_OP_G_N: case MPBP_OP_G_S:
+    case MPBP_OP_XI_N: case MPBP_OP_XI_S: return 2 * N;
+    default: return set_error(MPBP_ERR_ARG, "unknown operator %d", op);
+    }
+}
+
+int64_t mpbp_stokes_cols(int32_t n, int32_t op) {
+    const int64_t N = (int64_t)n * n;
+    switch (op) {
+    case MPBP_OP_A: return 5 * N;
+    case MPBP_OP_F: case MPBP_OP_D: return 4 * N;
+    case MPBP_OP_G: case MPBP_OP_G_N: case MPBP_OP_G_S: return N;
+    case MPBP_OP_L_N: case MPBP_OP_L_S: case MPBP_OP_D_N: case MPBP_OP_D_S:
+    case MPBP_OP_XI_N: case MPBP_OP_XI_S: return 2 * N;
+    default: return set_error(MPBP_ERR_ARG, "unknown operator %d", op);
+    }
+}
+
+static int make_stokes(const mpbp_stokes_params* prm, const double* cell, const double* uface,
+                       const double* vface, StokesDev* P) {
+    if (!prm || prm->n < 1 || !cell) return set_error(MPBP_ERR_ARG, "stokes: bad params");
+    if ((int64_t)prm->n * prm->n * 5 > INT32_MAX) return set_error(MPBP_ERR_OVERFLOW, "stokes: n too large");
+    *P = StokesDev{prm->n, prm->xi, prm->eta_n, prm->eta_s, prm->c, prm->d_u, prm->d_p, prm->d_div,
+                   cell, uface, vface};
+    return MPBP_OK;
+}
+
+int mpbp_stokes_count(const mpbp_stokes_params* prm, int32_t op, const double* cell,
+                      int32_t* row_nnz, void* stream) {
+    StokesDev P;
+    int rc = make_stokes(prm, cell, nullptr, nullptr, &P);
+    if (rc) return rc;
+    const int64_t rows = mpbp_stokes_rows(prm->n, op);
+    if (rows < 0) return (int)rows;
+    k_stokes_count<<<grid_for(rows), kBlock, 0, as_stream(stream)>>>(P, op, rows, row_nnz);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int mpbp_stokes_fill(const mpbp_stokes_params* prm, int32_t op, const double* cell,
+                     const double* uface, const double* vface, const int32_t* row_ptr,
+                     int32_t* col_idx, double* val, void* stream) {
+    StokesDev P;
+    int rc = make_stokes(prm, cell, uface, vface, &P);
+    if (rc) return rc;
+    if ((op == MPBP_OP_A || op == MPBP_OP_F) && (!uface || !vface))
+        return set_error(MPBP_ERR_ARG, "stokes fill: A/F need face tables");
+    const int64_t rows = mpbp_stokes_rows(prm->n, op);
+    if (rows < 0) return (int)rows;
+    k_stokes_fill<<<grid_for(rows), kBlock, 0, as_stream(stream)>>>(P, op, rows, row_ptr, col_idx, val);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int mpbp_exclusive_scan(const int32_t* row_nnz, int32_t* row_ptr, int64_t n, int64_t* total,
+                        void* stream) {
+    if (n < 0 || !row_ptr || (n > 0 && !row_nnz)) return set_error(MPBP_ERR_ARG, "scan: bad args");
+    long long* d_total = nullptr;
+    MPBP_HIP(hipMalloc(&d_total, sizeof(long long)));
+    k_exclusive_scan<<<1, 1024, 0, as_stream(stream)>>>(row_nnz, row_ptr, n, d_total);
+    hipError_t e = hipGetLastError();
+    long long h = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, d_total, sizeof(h), hipMemcpyDeviceToHost, as_stream(stream));
+    if (e == hipSuccess) e = hipStreamSynchronize(as_stream(stream));
+    (void)hipFree(d_total);
+    if (e != hipSuccess) return set_error(MPBP_ERR_HIP, "scan: %s", hipGetErrorString(e));
+    if (h > INT32_MAX) return set_error(MPBP_ERR_OVERFLOW, "scan: %lld entries exceed int32 row_ptr", h);
+    if (total) *total = h;
+    return MPBP_OK;
+}
+
+int mpbp_spgemm_count(const mpbp_csr* A, const mpbp_csr* B, int32_t* row_nnz, void* stream) {
+    int rc = check_csr(A);
+    if (!rc) rc = check_csr(B);
+    if (rc) return rc;
+    if (A->ncols != B->nrows) return set_error(MPBP_ERR_ARG, "spgemm: shape mismatch");
+    int* d_over = nullptr;
+    MPBP_HIP(hipMalloc(&d_over, sizeof(int)));
+    hipError_t e = hipMemsetAsync(d_over, 0, sizeof(int), as_stream(stream));
+    if (e == hipSuccess) {
+        k_spgemm_count<<<grid_for(A->nrows), kBlock, 0, as_stream(stream)>>>(to_csr(A), to_csr(B), A->nrows,
+                                                                          row_nnz, d_over);
+        e = hipGetLastError();
+    }
+    int h = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, d_over, sizeof(int), hipMemcpyDeviceToHost, as_stream(stream));
+    if (e == hipSuccess) e = hipStreamSynchronize(as_stream(stream));
+    (void)hipFree(d_over);
+    if (e != hipSuccess) return set_error(MPBP_ERR_HIP, "spgemm_count: %s", hipGetErrorString(e));
+    if (h) return set_error(MPBP_ERR_OVERFLOW, "spgemm: %d rows wider than %d", h, kSpgemmMaxW);
+    return MPBP_OK;
+}
+
+int mpbp_spgemm_fill(const mpbp_csr* A, const mpbp_csr* B, double alpha, const int32_t* row_ptr,
+                     int32_t* col_idx, double* val, void* stream) {
+    int rc = check_csr(A);
+    if (!rc) rc = check_csr(B);
+    if (rc) return rc;
+    k_spgemm_fill<<<grid_for(A->nrows), kBlock, 0, as_stream(stream)>>>(to_csr(A), to_csr(B), A->nrows, alpha,
+                                                                     row_ptr, col_idx, val);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int64_t mpbp_plan_row_blocks(const int32_t* row_ptr, int32_t row_begin, int32_t row_end,
+                             int32_t* pairs, int64_t capacity) {
+    if (!row_ptr || row_begin < 0 || row_end < row_begin) return set_error(MPBP_ERR_ARG, "plan: bad args");
+    int64_t nb = 0;
+    int32_t r = row_begin;
+    while (r < row_end) {
+        const int32_t s = r;
+        int32_t e = r;
+        while (e < row_end && e - s < kBlock && row_ptr[e + 1] - row_ptr[s] <= MPBP_BLOCK_NNZ) ++e;
+        if (e == s) e = s + 1;   // one row longer than the LDS stage
+        if (pairs && nb < capacity) {
+            pairs[2 * nb] = s;
+            pairs[2 * nb + 1] = e;
+        }
+        ++nb;
+        r = e;
+    }
+    return nb;
+}
+
+int mpbp_csr_diag(const mpbp_csr* A, int32_t col_offset, double* diag, int32_t* missing, void* stream) {
+    int rc = check_csr(A);
+    if (rc) return rc;
+    int* d_miss = nullptr;
+    MPBP_HIP(hipMalloc(&d_miss, sizeof(int)));
+    hipError_t e = hipMemsetAsync(d_miss, 0, sizeof(int), as_stream(stream));
+    if (e == hipSuccess) {
+        k_csr_diag<<<grid_for(A->nrows), kBlock, 0, as_stream(stream)>>>(to_csr(A), A->nrows, col_offset,
+                                                                      diag, d_miss);
+        e = hipGetLastError();
+    }
+    int h = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, d_miss, sizeof(int), hipMemcpyDeviceToHost, as_stream(stream));
+    if (e == hipSuccess) e = hipStreamSynchronize(as_stream(stream));
+    (void)hipFree(d_miss);
+    if (e != hipSuccess) return set_error(MPBP_ERR_HIP, "csr_diag: %s", hipGetErrorString(e));
+    if (missing) *missing = h;
+    return MPBP_OK;
+}
+
+int mpbp_gershgorin(const mpbp_csr* A, const double* diag, double* lmax, void* stream) {
+    int rc = check_csr(A);
+    if (rc) return rc;
+    unsigned long long* d_out = nullptr;
+    MPBP_HIP(hipMalloc(&d_out, sizeof(unsigned long long)));
+    hipError_t e = hipMemsetAsync(d_out, 0, sizeof(unsigned long long), as_stream(stream));
+    if (e == hipSuccess) {
+        k_gershgorin<<<grid_for(A->nrows), kBlock, 0, as_stream(stream)>>>(to_csr(A), A->nrows, diag, d_out);
+        e = hipGetLastError();
+    }
+    unsigned long long h = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, d_out, sizeof(h), hipMemcpyDeviceToHost, as_stream(stream));
+    if (e == hipSuccess) e = hipStreamSynchronize(as_stream(stream));
+    (void)hipFree(d_out);
+    if (e != hipSuccess) return set_error(MPBP_ERR_HIP, "gershgorin: %s", hipGetErrorString(e));
+    double v;
+    memcpy(&v, &h, sizeof(v));
+    if (lmax) *lmax = v;
+    return MPBP_OK;
+}
+
+int mpbp_csr_extract_count(const mpbp_csr* A, const int32_t* rows, int32_t nrows_local,
+                           int32_t* row_nnz, void* stream) {
+    int rc = check_csr(A);
+    if (rc) return rc;
+    if (nrows_local < 0 || (nrows_local && (!rows || !row_nnz))) return set_error(MPBP_ERR_ARG, "extract: bad args");
+    if (nrows_local == 0) return MPBP_OK;
+    k_extract_count<<<grid_for(nrows_local), kBlock, 0, as_stream(stream)>>>(to_csr(A), rows, nrows_local, row_nnz);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int mpbp_csr_extract_fill(const mpbp_csr* A, const int32_t* rows, int32_t nrows_local,
+                          const int32_t* colmap, const int32_t* row_ptr_local, int32_t* col_local,
+                          double* val_local, void* stream) {
+    int rc = check_csr(A);
+    if (rc) return rc;
+    if (nrows_local == 0) return MPBP_OK;
+    int* d_bad = nullptr;
+    MPBP_HIP(hipMalloc(&d_bad, sizeof(int)));
+    hipError_t e = hipMemsetAsync(d_bad, 0, sizeof(int), as_stream(stream));
+    if (e == hipSuccess) {
+        k_extract_fill<<<grid_for(nrows_local), kBlock, 0, as_stream(stream)>>>(
+            to_csr(A), rows, nrows_local, colmap, row_ptr_local, col_local, val_local, d_bad);
+        e = hipGetLastError();
+    }
+    int h = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, d_bad, sizeof(int), hipMemcpyDeviceToHost, as_stream(stream));
+    if (e == hipSuccess) e = hipStreamSynchronize(as_stream(stream));
+    (void)hipFree(d_bad);
+    if (e != hipSuccess) return set_error(MPBP_ERR_HIP, "extract_fill: %s", hipGetErrorString(e));
+    if (h) return set_error(MPBP_ERR_PATTERN, "extract: %d entries reference columns outside the halo", h);
+    return MPBP_OK;
+}
+
+int mpbp_spmv(const mpbp_csr* A, const mpbp_rowblocks* blocks, int32_t mode, const double* x,
+              const double* z, double* y, void* stream) {
+    int rc = check_csr(A);
+    if (rc) return rc;
+    if (!x || !y || (mode != MPBP_SPMV_STORE && !z)) return set_error(MPBP_ERR_ARG, "spmv: bad vectors");
+    const hipStream_t st = as_stream(stream);
+    switch (mode) {
+    case MPBP_SPMV_STORE: return launch_rows(A, blocks, x, EpiStore{y}, st);
+    case MPBP_SPMV_ADD: return launch_rows(A, blocks, x, EpiAdd{z, y}, st);
+    case MPBP_SPMV_RESID: return launch_rows(A, blocks, x, EpiResid{z, y}, st);
+    default: return set_error(MPBP_ERR_ARG, "spmv: unknown mode %d", mode);
+    }
+}
+
+int mpbp_jacobi_init(int32_t nrows, const double* b, const double* diag, const double* sub,
+                     double* x_out, void* stream) {
+    if (nrows < 0 || (nrows && (!b || !diag || !x_out))) return set_error(MPBP_ERR_ARG, "jacobi_init: bad args");
+    if (!nrows) return MPBP_OK;
+    k_jacobi_init<<<grid_for(nrows), kBlock, 0, as_stream(stream)>>>(nrows, b, diag, sub, x_out);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int mpbp_jacobi_step(const mpbp_csr* A, const mpbp_rowblocks* blocks, const double* x_in,
+                     const double* b, const double* diag, const double* sub, double* x_out,
+                     void* stream) {
+    int rc = check_csr(A);
+    if (rc) return rc;
+    if (!x_in || !b || !diag || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "jacobi_step: bad vectors");
+    return launch_rows(A, blocks, x_in, EpiJacobi{x_in, b, diag, sub, x_out}, as_stream(stream));
+}
+
+int mpbp_cheb_init(int32_t nrows, const double* b, const double* diag, double c2, double* d,
+                   const double* sub, double* x_out, void* stream) {
+    if (nrows < 0 || (nrows && (!b || !diag || !d || !x_out))) return set_error(MPBP_ERR_ARG, "cheb_init: bad args");
+    if (!nrows) return MPBP_OK;
+    k_cheb_init<<<grid_for(nrows), kBlock, 0, as_stream(stream)>>>(nrows, b, diag, c2, d, sub, x_out);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int mpbp_cheb_step(const mpbp_csr* A, const mpbp_rowblocks* blocks, const double* x_in,
+                   const double* b, const double* diag, double c1, double c2, double* d,
+                   const double* sub, double* x_out, void* stream) {
+    int rc = check_csr(A);
+    if (rc) return rc;
+    if (!x_in || !b || !diag || !d || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "cheb_step: bad vectors");
+    return launch_rows(A, blocks, x_in, EpiCheb{x_in, b, diag, d, c1, c2, sub, x_out}, as_stream(stream));
+}
+
+int mpbp_cheb_coeffs(double lmin, double lmax, int32_t sweeps, double* c1, double* c2) {
+    if (sweeps < 1 || !c1 || !c2 || !(lmax > lmin) || !(lmin >= 0.0))
+        return set_error(MPBP_ERR_ARG, "cheb_coeffs: need sweeps >= 1 and lmax > lmin >= 0");
+    cheb_coeffs(lmin, lmax, sweeps, c1, c2);
+    return MPBP_OK;
+}
+
+int mpbp_gather(int32_t count, const int32_t* idx, const double* src, double* dst, void* stream) {
+    if (count <= 0) return MPBP_OK;
+    k_gather<<<grid_for(count), kBlock, 0, as_stream(stream)>>>(count, idx, src, dst);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int mpbp_scatter(int32_t count, const int32_t* idx, const double* src, double* dst, void* stream) {
+    if (count <= 0) return MPBP_OK;
+    k_scatter<<<grid_for(count), kBlock, 0, as_stream(stream)>>>(count, idx, src, dst);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int mpbp_event_create(void** ev) {
+    hipEvent_t e;
+    MPBP_HIP(hipEventCreate(&e));
+    *ev = (void*)e;
+    return MPBP_OK;
+}
+
+int mpbp_event_destroy(void* ev) {
+    MPBP_HIP(hipEventDestroy((hipEvent_t)ev));
+    return MPBP_OK;
+}
+
+int mpbp_event_elapsed_ms(void* start, void* stop, float* ms) {
+    MPBP_HIP(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+    return MPBP_OK;
+}
+
+}  // extern "C"
+
+// ======================================================= Schur apply ====
+namespace {
+
+struct Ctx {
+    const mpbp_schur_plan* p;
+    hipStream_t st;
+};
+
+// Launch one sweep over interior blocks, then (after the halo is complete) boundary blocks.
+template <class Fn>
+int two_phase(const Ctx& c, int32_t kind, const double* x_ext, const mpbp_rowblocks& bi,
+              const mpbp_rowblocks& bb, Fn&& launch) {
+    const mpbp_schur_plan* p = c.p;
+    if (p->halo) p->halo(p->halo_ctx, kind, const_cast<double*>(x_ext), MPBP_HALO_BEGIN, (void*)c.st);
+    int rc = launch(&bi);
+    if (rc) return rc;
+    if (p->halo) p->halo(p->halo_ctx, kind, const_cast<double*>(x_ext), MPBP_HALO_END, (void*)c.st);
+    return launch(&bb);
+}
+
+// x = M^-1 b by `inner` sweeps from x0 = 0 (solve.py:251/254 F_inv / Gt_G_factorization roles).
+// The final iterate goes to dst (sub - iterate when sub != NULL); ping/pong hold the others.
+int inner_solve(const Ctx& c, int32_t kind, const mpbp_csr& M, const mpbp_rowblocks& bi,
+                const mpbp_rowblocks& bb, const double* diag, const mpbp_inner_solver& in,
+                int32_t nrows, const double* b, double* dst, const double* sub, double* ping,
+                double* pong, double* dir, bool profile) {
+    const int K = in.sweeps;
+    double c1[64], c2[64];
+    if (K < 1 || K > 64) return set_error(MPBP_ERR_ARG, "inner sweeps must be in [1, 64]");
+    const bool cheb = in.kind == MPBP_INNER_CHEBYSHEV;
+    if (cheb) {
+        if (!(in.lmax > in.lmin) || !(in.lmin >= 0.0)) return set_error(MPBP_ERR_ARG, "bad Chebyshev interval");
+        cheb_coeffs(in.lmin, in.lmax, K, c1, c2);
+    } else if (in.kind != MPBP_INNER_JACOBI) {
+        return set_error(MPBP_ERR_ARG, "unknown inner solver %d", in.kind);
+    }
+    double* cur = (K == 1) ? dst : ping;
+    const double* s0 = (K == 1) ? sub : nullptr;
+    int rc = cheb ? mpbp_cheb_init(nrows, b, diag, c2[0], dir, s0, cur, (void*)c.st)
+                  : mpbp_jacobi_init(nrows, b, diag, s0, cur, (void*)c.st);
+    if (rc) return rc;
+    for (int s = 1; s < K; ++s) {
+        const bool last = s == K - 1;
+        double* nxt = last ? dst : (cur == ping ? pong : ping);
+        const double* sb = last ? sub : nullptr;
+        const mpbp_schur_plan* p = c.p;
+        const bool rec = profile && p->prof_events && p->prof_count && *p->prof_count < p->prof_capacity;
+        if (rec) MPBP_HIP(hipEventRecord((hipEvent_t)p->prof_events[2 * *p->prof_count], c.st));
+        rc = two_phase(c, kind, cur, bi, bb, [&](const mpbp_rowblocks* blk) {
+            return cheb ? mpbp_cheb_step(&M, blk, cur, b, diag, c1[s], c2[s], dir, sb, nxt, (void*)c.st)
+                        : mpbp_jacobi_step(&M, blk, cur, b, diag, sb, nxt, (void*)c.st);
+        });
+        if (rc) return rc;
+        if (rec) {
+            MPBP_HIP(hipEventRecord((hipEvent_t)p->prof_events[2 * *p->prof_count + 1], c.st));
+            ++*p->prof_count;
+        }
+        cur = nxt;
+    }
+    return MPBP_OK;
+}
+
+}  // namespace
+
+extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, double* out, void* stream) {
+    if (!p || !v || !out) return set_error(MPBP_ERR_ARG, "schur_apply: bad args");
+    for (int i = 0; i < 4; ++i)
+        if (!p->wu[i]) return set_error(MPBP_ERR_ARG, "schur_apply: missing velocity workspace");
+    for (int i = 0; i < 7; ++i)
+        if (!p->wp[i]) return set_error(MPBP_ERR_ARG, "schur_apply: missing pressure workspace");
+    if (!p->wu_owned || !p->diag_F || !p->diag_P) return set_error(MPBP_ERR_ARG, "schur_apply: missing operands");
+    const Ctx c{p, as_stream(stream)};
+    const double* v_u = v;
+    const double* v_p = v + p->nu;
+    double* out_u = out;
+    double* out_p = out + p->nu;
+    double *Y = p->wu[0], *U0 = p->wu[1], *U1 = p->wu[2], *Ud = p->wu[3], *W = p->wu_owned;
+    double *Prhs = p->wp[0], *Pxa = p->wp[1], *Pxb = p->wp[2], *Pxp = p->wp[3];
+    double *P0 = p->wp[4], *P1 = p->wp[5], *Pd = p->wp[6];
+    int rc;
+    // 1. Finv_v = F_inv @ v[:F.shape[1]]                                   solve.py:258
+    rc = inner_solve(c, MPBP_VEC_VELOCITY, p->F, p->F_int, p->F_bnd, p->diag_F, p->inner_F, p->nu, v_u, Y,
+                     nullptr, U0, U1, Ud, true);
+    if (rc) return rc;
+    // 2. rhs_interim = D @ Finv_v + v[F.shape[1]:]                            solve.py:259
+    rc = two_phase(c, MPBP_VEC_VELOCITY, Y, p->D_int, p->D_bnd, [&](const mpbp_rowblocks* blk) {
+        return mpbp_spmv(&p->D, blk, MPBP_SPMV_ADD, Y, v_p, Prhs, (void*)c.st);
+    });
+    if (rc) return rc;
+    // 3. x_a = Gt_G_factorization @ rhs_interim                             solve.py:265
+    rc = inner_solve(c, MPBP_VEC_PRESSURE, p->GtG, p->P_int, p->P_bnd, p->diag_P, p->inner_P, p->np, Prhs, Pxa,
+                     nullptr, P0, P1, Pd, false);
+    if (rc) return rc;
+    // 4. x_b = Gt_F_G @ x_a                                                solve.py:267
+    rc = two_phase(c, MPBP_VEC_PRESSURE, Pxa, p->Q_int, p->Q_bnd, [&](const mpbp_rowblocks* blk) {
+        return mpbp_spmv(&p->GtFG, blk, MPBP_SPMV_STORE, Pxa, nullptr, Pxb, (void*)c.st);
+    });
+    if (rc) return rc;
+    // 5. x_p = Gt_G_factorization @ x_b                                    solve.py:271
+    rc = inner_solve(c, MPBP_VEC_PRESSURE, p->GtG, p->P_int, p->P_bnd, p->diag_P, p->inner_P, p->np, Pxb, Pxp,
+                     nullptr, P0, P1, Pd, false);
+    if (rc) return rc;
+    MPBP_HIP(hipMemcpyAsync(out_p, Pxp, sizeof(double) * (size_t)p->np, hipMemcpyDeviceToDevice, c.st));
+    // 6. G_xp = G @ x_p                                                     solve.py:273
+    rc = two_phase(c, MPBP_VEC_PRESSURE, Pxp, p->G_int, p->G_bnd, [&](const mpbp_rowblocks* blk) {
+        return mpbp_spmv(&p->G, blk, MPBP_SPMV_STORE, Pxp, nullptr, W, (void*)c.st);
+    });
+    if (rc) return rc;
+    // 7. u = Finv_v - F_inv @ G_xp                                          solve.py:274-276
+    return inner_solve(c, MPBP_VEC_VELOCITY, p->F, p->F_int, p->F_bnd, p->diag_F, p->inner_F, p->nu, W, out_u,
+                       Y, U0, U1, Ud, true);
+}
