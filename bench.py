@@ -1,0 +1,190 @@
+"""Benchmark: preconditioner applies per second on the 1024^2 multiphase-Stokes system (BASELINE.json
+configs[2]) on MI355X, with the roofline of the dominant kernel and the CPU oracle timed beside it.
+
+One step = one application of the approximate-commutator block preconditioner (solve.py:257-277,
+``mpbp_schur_apply``) to a resident random vector of 5 n^2 doubles.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 1024] ...
+
+N > 1 is launched by torch.distributed.run (one rank per GPU); see DESIGN.md for how the work is
+split.  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0    # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse_inner(s):
+    kind, _, k = s.partition(":")
+    return kind, int(k or 4)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--xi", type=float, default=1.0)
+    ap.add_argument("--eta-n", type=float, default=100.0)
+    ap.add_argument("--eta-s", type=float, default=1.0)
+    ap.add_argument("--inner-f", default="chebyshev:4")
+    ap.add_argument("--inner-p", default="chebyshev:4")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import mp_block_preconditioners_amd as mp
+
+    n = args.n
+    kf, sf = parse_inner(args.inner_f)
+    kp, spp = parse_inner(args.inner_p)
+    bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
+    A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver(kf, sf), inner_P=mp.InnerSolver(kp, spp))
+    gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
+    v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda", generator=gen)
+    out = torch.empty_like(v)
+    torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        pc.apply(v, out)
+    sweeps_per_apply = 2 * (sf - 1)
+    pc.enable_profiling(max(1, args.steps * sweeps_per_apply))
+    pc.reset_profiling()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pc.apply(v, out)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    sweep_ms = pc.profiled_ms()
+    pc.disable_profiling()
+
+    # dominant kernel: the fused Chebyshev-Jacobi CSR sweep over F (k_csr_rows<EpiCheb>)
+    nF, nnzF = F.shape[0], F.nnz
+    nblk = F.blocks.count
+    sweep_bytes = nnzF * (8 + 4) + (nF + 1) * 4 + nF * 8 * (1 + 1 + 1 + 2 + 1) + nblk * 8
+    avg_sweep_s = (sum(sweep_ms) / len(sweep_ms) / 1e3) if sweep_ms else float("nan")
+    achieved = sweep_bytes / avg_sweep_s / 1e9
+
+    # the plain A SpMV (apply.py:72) on the same device, for reference
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    x = torch.randn(A.shape[1], dtype=torch.float64, device="cuda", generator=gen)
+    y = torch.empty(A.shape[0], dtype=torch.float64, device="cuda")
+    for _ in range(3):
+        A.matvec(x, out=y)
+    ev[0].record()
+    reps = 20
+    for _ in range(reps):
+        A.matvec(x, out=y)
+    ev[1].record()
+    torch.cuda.synchronize()
+    spmv_s = ev[0].elapsed_time(ev[1]) / 1e3 / reps
+    spmv_bytes = A.nnz * 12 + (A.shape[0] + 1) * 4 + (A.shape[0] + A.shape[1]) * 8 + A.blocks.count * 8
+
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as f:
+                pm = json.load(f)
+            if int(pm.get("n", -1)) == n:
+                traffic = pm.get("cheb_F_sweep_bytes")
+        except (OSError, ValueError):
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(F, D, G, pc, v, args.cpu_seconds, kf, sf, kp, spp)
+
+    if rank == 0:
+        value = world * args.steps / dt
+        line = {
+            "metric": "precond-applies/sec",
+            "value": value,
+            "unit": "applies/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: reference operator (thn = 0.25 sin sin + 0.5), random input vector",
+            "config": {"workload": f"{n}x{n} MAC grid, approx-commutator Schur preconditioner apply "
+                                   "(BASELINE configs[2])",
+                       "n": n, "unknowns": int(pc.shape[0]), "xi": args.xi, "eta_n": args.eta_n,
+                       "eta_s": args.eta_s, "inner_F": f"{kf}:{sf}", "inner_P": f"{kp}:{spp}",
+                       "parallelism": "replicas" if world > 1 else "single"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_csr_rows<EpiCheb> (F Chebyshev sweep)",
+                         "bytes_per_launch": sweep_bytes, "avg_launch_us": avg_sweep_s * 1e6,
+                         "launches_timed": len(sweep_ms)},
+            "spmv_A": {"gbs": spmv_bytes / spmv_s / 1e9, "us": spmv_s * 1e6, "nnz": A.nnz,
+                       "bytes": spmv_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(F, D, G, pc, v, seconds, kf, sf, kp, spp):
+    """The oracle's apply (sequential C, one core) on the same matrices, bounded sample."""
+    import numpy as np
+    from oracle.schur_oracle import Inner, approx_schur_apply
+    Fh, Dh, Gh = F.to_scipy(), D.to_scipy(), G.to_scipy()
+    GtGh, GtFGh = pc.GtG.to_scipy(), pc.GtFG.to_scipy()
+    iF = Inner(kf, sf, pc.inner_F.lmin or 0.0, pc.inner_F.lmax or 0.0)
+    iP = Inner(kp, spp, pc.inner_P.lmin or 0.0, pc.inner_P.lmax or 0.0)
+    dF, dP = pc.diag_F.cpu().numpy(), pc.diag_P.cpu().numpy()
+    vh = v.cpu().numpy()
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        ref = approx_schur_apply(Fh, Dh, Gh, GtGh, GtFGh, vh, iF, iP, diag_F=dF, diag_P=dP)
+        done += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    el = time.perf_counter() - t0
+    # the GPU apply of the same vector must be bit-identical to the timed oracle output
+    gpu = pc.apply(v).cpu().numpy()
+    same = bool(np.array_equal(gpu.view(np.uint64), ref.view(np.uint64)))
+    return {"value": done / el, "unit": "applies/s", "cores": 1, "kind": "port",
+            "sample": f"{done} full applies of the same {pc.shape[0]}-unknown system in {el:.1f} s "
+                      f"(oracle/csr_oracle.c, 1 thread)", "bit_exact_vs_gpu": same}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,136 @@
+"""ctypes binding of libmpbp.so (include/mpbp.h).  Loading fails loudly: there is no CPU fallback."""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (CFUNCTYPE, POINTER, Structure, byref, c_char_p, c_double, c_int, c_int32,
+                    c_int64, c_void_p)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libmpbp.so")
+
+OP_A, OP_F, OP_D, OP_G = 0, 1, 2, 3
+OP_L_N, OP_L_S, OP_D_N, OP_D_S, OP_G_N, OP_G_S, OP_XI_N, OP_XI_S = range(4, 12)
+SPMV_STORE, SPMV_ADD, SPMV_RESID = 0, 1, 2
+INNER_JACOBI, INNER_CHEBYSHEV = 0, 1
+HALO_BEGIN, HALO_END = 0, 1
+VEC_VELOCITY, VEC_PRESSURE = 0, 1
+BLOCK_ROWS, BLOCK_NNZ = 256, 4095
+
+
+class MpbpError(RuntimeError):
+    pass
+
+
+class Csr(Structure):
+    _fields_ = [("nrows", c_int32), ("ncols", c_int32), ("nnz", c_int64),
+                ("row_ptr", c_void_p), ("col_idx", c_void_p), ("val", c_void_p)]
+
+
+class RowBlocks(Structure):
+    _fields_ = [("pairs", c_void_p), ("count", c_int32)]
+
+
+class StokesParams(Structure):
+    _fields_ = [("n", c_int32), ("xi", c_double), ("eta_n", c_double), ("eta_s", c_double),
+                ("c", c_double), ("d_u", c_double), ("d_p", c_double), ("d_div", c_double)]
+
+
+class InnerSolverC(Structure):
+    _fields_ = [("kind", c_int32), ("sweeps", c_int32), ("lmin", c_double), ("lmax", c_double)]
+
+
+HALO_FN = CFUNCTYPE(None, c_void_p, c_int32, c_void_p, c_int32, c_void_p)
+
+
+class SchurPlan(Structure):
+    _fields_ = [("nu", c_int32), ("np", c_int32), ("nu_ext", c_int32), ("np_ext", c_int32),
+                ("F", Csr), ("D", Csr), ("G", Csr), ("GtG", Csr), ("GtFG", Csr),
+                ("F_int", RowBlocks), ("F_bnd", RowBlocks), ("D_int", RowBlocks), ("D_bnd", RowBlocks),
+                ("G_int", RowBlocks), ("G_bnd", RowBlocks), ("P_int", RowBlocks), ("P_bnd", RowBlocks),
+                ("Q_int", RowBlocks), ("Q_bnd", RowBlocks),
+                ("diag_F", c_void_p), ("diag_P", c_void_p),
+                ("inner_F", InnerSolverC), ("inner_P", InnerSolverC),
+                ("wu", c_void_p * 4), ("wu_owned", c_void_p), ("wp", c_void_p * 7),
+                ("halo", HALO_FN), ("halo_ctx", c_void_p),
+                ("prof_events", c_void_p), ("prof_capacity", c_int32), ("prof_count", POINTER(c_int32))]
+
+
+_P = c_void_p
+_SIGNATURES = {
+    "mpbp_version": ([], c_char_p),
+    "mpbp_last_error": ([], c_char_p),
+    "mpbp_stokes_theta": ([c_int32, _P, _P, _P, _P], c_int),
+    "mpbp_stokes_rows": ([c_int32, c_int32], c_int64),
+    "mpbp_stokes_cols": ([c_int32, c_int32], c_int64),
+    "mpbp_stokes_count": ([POINTER(StokesParams), c_int32, _P, _P, _P], c_int),
+    "mpbp_stokes_fill": ([POINTER(StokesParams), c_int32, _P, _P, _P, _P, _P, _P, _P], c_int),
+    "mpbp_exclusive_scan": ([_P, _P, c_int64, POINTER(c_int64), _P], c_int),
+    "mpbp_spgemm_count": ([POINTER(Csr), POINTER(Csr), _P, _P], c_int),
+    "mpbp_spgemm_fill": ([POINTER(Csr), POINTER(Csr), c_double, _P, _P, _P, _P], c_int),
+    "mpbp_plan_row_blocks": ([_P, c_int32, c_int32, _P, c_int64], c_int64),
+    "mpbp_csr_diag": ([POINTER(Csr), c_int32, _P, POINTER(c_int32), _P], c_int),
+    "mpbp_gershgorin": ([POINTER(Csr), _P, POINTER(c_double), _P], c_int),
+    "mpbp_csr_extract_count": ([POINTER(Csr), _P, c_int32, _P, _P], c_int),
+    "mpbp_csr_extract_fill": ([POINTER(Csr), _P, c_int32, _P, _P, _P, _P, _P], c_int),
+    "mpbp_spmv": ([POINTER(Csr), POINTER(RowBlocks), c_int32, _P, _P, _P, _P], c_int),
+    "mpbp_jacobi_init": ([c_int32, _P, _P, _P, _P, _P], c_int),
+    "mpbp_jacobi_step": ([POINTER(Csr), POINTER(RowBlocks), _P, _P, _P, _P, _P, _P], c_int),
+    "mpbp_cheb_init": ([c_int32, _P, _P, c_double, _P, _P, _P, _P], c_int),
+    "mpbp_cheb_step": ([POINTER(Csr), POINTER(RowBlocks), _P, _P, _P, c_double, c_double, _P, _P, _P, _P],
+                       c_int),
+    "mpbp_cheb_coeffs": ([c_double, c_double, c_int32, _P, _P], c_int),
+    "mpbp_schur_apply": ([POINTER(SchurPlan), _P, _P, _P], c_int),
+    "mpbp_gather": ([c_int32, _P, _P, _P, _P], c_int),
+    "mpbp_scatter": ([c_int32, _P, _P, _P, _P], c_int),
+    "mpbp_event_create": ([POINTER(c_void_p)], c_int),
+    "mpbp_event_destroy": ([_P], c_int),
+    "mpbp_event_elapsed_ms": ([_P, _P, POINTER(ctypes.c_float)], c_int),
+}
+
+_lib = None
+
+
+def lib():
+    """The loaded libmpbp.so; raises MpbpError if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MpbpError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                            f"g.build()'` (hipcc --offload-arch=gfx950).  There is no CPU fallback.")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in _SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc < 0:
+        raise MpbpError(f"libmpbp error {rc}: {lib().mpbp_last_error().decode()}")
+    return rc
+
+
+def exported_symbols():
+    return list(_SIGNATURES)
+
+
+def ptr(t):
+    """Device (or host) address of a torch tensor / numpy array, or None."""
+    if t is None:
+        return None
+    if hasattr(t, "data_ptr"):
+        return ctypes.c_void_p(t.data_ptr())
+    return t.ctypes.data_as(ctypes.c_void_p)
+
+
+def stream_handle(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+__all__ = ["lib", "check", "ptr", "stream_handle", "MpbpError", "Csr", "RowBlocks", "StokesParams",
+           "InnerSolverC", "SchurPlan", "HALO_FN", "byref"]

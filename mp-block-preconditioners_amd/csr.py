@@ -1,0 +1,161 @@
+"""Device-resident CSR matrices (HBM) driven through libmpbp's C ABI.
+
+Layout in HBM: row_ptr int32[nrows+1], col_idx int32[nnz], val float64[nnz] -- the scipy.sparse
+CSR layout, so a scipy matrix crosses the boundary with three copies and no reformatting.  Row
+blocks (<= 256 rows, <= 4095 nonzeros each) are planned once on the host from row_ptr and kept
+on the device; every SpMV-shaped kernel walks them.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr, stream_handle
+
+
+class DeviceCSR:
+    """A CSR matrix in HBM.  ``A @ x`` (x a CUDA float64 tensor) runs the HIP SpMV."""
+
+    def __init__(self, row_ptr: torch.Tensor, col_idx: torch.Tensor, val: torch.Tensor, shape,
+                 row_ptr_host: np.ndarray | None = None):
+        assert row_ptr.dtype == torch.int32 and col_idx.dtype == torch.int32 and val.dtype == torch.float64
+        assert row_ptr.is_cuda and col_idx.is_cuda and val.is_cuda
+        self.row_ptr, self.col_idx, self.val = row_ptr, col_idx, val
+        self.shape = (int(shape[0]), int(shape[1]))
+        assert row_ptr.numel() == self.shape[0] + 1
+        self._rp_host = row_ptr_host
+        self._blocks = None
+        self._cs = None
+
+    # -- construction -------------------------------------------------------------------------
+    @classmethod
+    def from_scipy(cls, M, device=None):
+        import scipy.sparse as sp
+        M = sp.csr_matrix(M)
+        M.sort_indices()
+        dev = torch.device(device or "cuda")
+        rp = np.ascontiguousarray(M.indptr, dtype=np.int32)
+        return cls(torch.from_numpy(rp).to(dev),
+                   torch.from_numpy(np.ascontiguousarray(M.indices, dtype=np.int32)).to(dev),
+                   torch.from_numpy(np.ascontiguousarray(M.data, dtype=np.float64)).to(dev),
+                   M.shape, row_ptr_host=rp)
+
+    def to_scipy(self):
+        import scipy.sparse as sp
+        return sp.csr_matrix((self.val.cpu().numpy(), self.col_idx.cpu().numpy(), self.row_ptr.cpu().numpy()),
+                             shape=self.shape)
+
+    @property
+    def nnz(self) -> int:
+        return int(self.val.numel())
+
+    @property
+    def device(self):
+        return self.val.device
+
+    @property
+    def row_ptr_host(self) -> np.ndarray:
+        if self._rp_host is None:
+            self._rp_host = self.row_ptr.cpu().numpy()
+        return self._rp_host
+
+    def cstruct(self) -> _lib.Csr:
+        if self._cs is None:
+            self._cs = _lib.Csr(self.shape[0], self.shape[1], self.nnz, self.row_ptr.data_ptr(),
+                                self.col_idx.data_ptr(), self.val.data_ptr())
+        return self._cs
+
+    # -- row blocks -----------------------------------------------------------------------------
+    def plan_blocks(self, row_begin=0, row_end=None, rows=None):
+        """Device row-block list over [row_begin, row_end), or over sorted row ranges `rows`."""
+        rp = self.row_ptr_host
+        ranges = rows if rows is not None else [(row_begin, self.shape[0] if row_end is None else row_end)]
+        pieces = []
+        for a, b in ranges:
+            need = lib().mpbp_plan_row_blocks(rp.ctypes.data_as(ctypes.c_void_p), a, b, None, 0)
+            check(need)
+            buf = np.empty(2 * max(int(need), 1), dtype=np.int32)
+            lib().mpbp_plan_row_blocks(rp.ctypes.data_as(ctypes.c_void_p), a, b,
+                                       buf.ctypes.data_as(ctypes.c_void_p), int(need))
+            pieces.append(buf[: 2 * int(need)])
+        pairs = np.concatenate(pieces) if pieces else np.zeros(0, dtype=np.int32)
+        return RowBlockList(torch.from_numpy(pairs).to(self.device))
+
+    @property
+    def blocks(self):
+        if self._blocks is None:
+            self._blocks = self.plan_blocks()
+        return self._blocks
+
+    # -- kernels --------------------------------------------------------------------------------
+    def matvec(self, x: torch.Tensor, out: torch.Tensor | None = None, mode=_lib.SPMV_STORE,
+               z: torch.Tensor | None = None, blocks=None) -> torch.Tensor:
+        assert x.dtype == torch.float64 and x.is_cuda and x.numel() >= self.shape[1]
+        if out is None:
+            out = torch.empty(self.shape[0], dtype=torch.float64, device=self.device)
+        blk = (blocks or self.blocks).cstruct()
+        check(lib().mpbp_spmv(ctypes.byref(self.cstruct()), ctypes.byref(blk), mode, ptr(x), ptr(z), ptr(out),
+                              stream_handle()))
+        return out
+
+    def __matmul__(self, other):
+        if isinstance(other, DeviceCSR):
+            return spgemm(self, other)
+        if isinstance(other, np.ndarray):
+            return self.matvec(torch.from_numpy(np.ascontiguousarray(other, dtype=np.float64))
+                               .to(self.device)).cpu().numpy()
+        return self.matvec(other)
+
+    def diagonal(self, col_offset=0) -> torch.Tensor:
+        d = torch.empty(self.shape[0], dtype=torch.float64, device=self.device)
+        missing = ctypes.c_int32(0)
+        check(lib().mpbp_csr_diag(ctypes.byref(self.cstruct()), col_offset, ptr(d), ctypes.byref(missing),
+                                  stream_handle()))
+        if missing.value:
+            raise _lib.MpbpError(f"{missing.value} rows have no diagonal entry")
+        return d
+
+    def gershgorin(self, diag: torch.Tensor) -> float:
+        out = ctypes.c_double(0.0)
+        check(lib().mpbp_gershgorin(ctypes.byref(self.cstruct()), ptr(diag), ctypes.byref(out), stream_handle()))
+        return out.value
+
+    def __repr__(self):
+        return f"DeviceCSR(shape={self.shape}, nnz={self.nnz}, device={self.device})"
+
+
+class RowBlockList:
+    def __init__(self, pairs: torch.Tensor):
+        self.pairs = pairs
+        self.count = pairs.numel() // 2
+        self._cs = _lib.RowBlocks(pairs.data_ptr() if self.count else None, self.count)
+
+    def cstruct(self):
+        return self._cs
+
+
+def csr_from_row_nnz(row_nnz: torch.Tensor, shape, device):
+    """Allocate row_ptr/col_idx/val for the given per-row counts (device exclusive scan)."""
+    rows = row_nnz.numel()
+    row_ptr = torch.empty(rows + 1, dtype=torch.int32, device=device)
+    total = ctypes.c_int64(0)
+    check(lib().mpbp_exclusive_scan(ptr(row_nnz), ptr(row_ptr), rows, ctypes.byref(total), stream_handle()))
+    col = torch.empty(max(total.value, 1), dtype=torch.int32, device=device)[: total.value]
+    val = torch.empty(max(total.value, 1), dtype=torch.float64, device=device)[: total.value]
+    return row_ptr, col, val
+
+
+def spgemm(A: DeviceCSR, B: DeviceCSR, alpha: float = 1.0) -> DeviceCSR:
+    """alpha * A @ B keeping every structural product (solve.py:246-249 use np.matmul)."""
+    if A.shape[1] != B.shape[0]:
+        raise ValueError(f"shape mismatch {A.shape} @ {B.shape}")
+    row_nnz = torch.empty(A.shape[0], dtype=torch.int32, device=A.device)
+    check(lib().mpbp_spgemm_count(ctypes.byref(A.cstruct()), ctypes.byref(B.cstruct()), ptr(row_nnz),
+                                  stream_handle()))
+    rp, ci, va = csr_from_row_nnz(row_nnz, (A.shape[0], B.shape[1]), A.device)
+    check(lib().mpbp_spgemm_fill(ctypes.byref(A.cstruct()), ctypes.byref(B.cstruct()), float(alpha), ptr(rp),
+                                 ptr(ci), ptr(va), stream_handle()))
+    return DeviceCSR(rp, ci, va, (A.shape[0], B.shape[1]))

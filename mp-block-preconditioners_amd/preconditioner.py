@@ -1,0 +1,116 @@
+"""MultiphaseBlockPreconditioner -- the reference's operator-assembly interface, assembled in HBM.
+
+Mirrors ``preconditioner.py`` of abarret/mp-block-preconditioners:
+
+    thn(y, x), ths(y, x)                         preconditioner.py:9-15
+    MultiphaseBlockPreconditioner(n, xi, eta_n, eta_s)              :17-24
+    .get_block_matrices(is_ths) -> (L, D, XI, G)                     :86-297
+    .get_big_A_matrix(c, d_u, d_p=1.0, d_div=-1.0) -> (A, S, F, D, G) :299-349
+
+Every matrix is a ``DeviceCSR`` built on the GPU by the stencil kernels of libmpbp (one thread per
+row, last-write-wins over the reference's ordered dense assignments, columns sorted).  The
+reference also returns the exact Schur complement S = -D F^-1 G (a dense inverse, O(N^3)); that
+is not formed here (``S`` is None) -- the approximate-commutator preconditioner in
+``solve.ApproxSchurPreconditioner`` is the path the reference actually solves with.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr, stream_handle
+from .csr import DeviceCSR, csr_from_row_nnz, spgemm
+
+PI = np.pi
+
+
+def thn(y, x):
+    """Network volume fraction (host helper, preconditioner.py:9-11)."""
+    return 0.25 * np.sin(2 * PI * x) * np.sin(2 * PI * y) + 0.5
+
+
+def ths(y, x):
+    """Solvent volume fraction (preconditioner.py:13-15)."""
+    return 1.0 - thn(y, x)
+
+
+class MultiphaseBlockPreconditioner:
+    def __init__(self, n, xi, eta_n=1.0, eta_s=1.0, device=None):
+        if int(n) < 1:
+            raise ValueError("n must be >= 1")
+        self.n = int(n)
+        self.dx = 1 / self.n
+        self.dy = 1 / self.n
+        self.xi = float(xi)
+        self.eta_n = float(eta_n)
+        self.eta_s = float(eta_s)
+        self.device = torch.device(device or "cuda")
+        self._theta = None
+
+    # -- volume fraction tables (HBM) ---------------------------------------------------------------
+    def theta_tables(self):
+        """(cell, uface, vface) thn tables, n*n each, computed on the GPU."""
+        if self._theta is None:
+            N = self.n * self.n
+            t = [torch.empty(N, dtype=torch.float64, device=self.device) for _ in range(3)]
+            check(lib().mpbp_stokes_theta(self.n, ptr(t[0]), ptr(t[1]), ptr(t[2]), stream_handle()))
+            self._theta = tuple(t)
+        return self._theta
+
+    def set_theta_tables(self, cell, uface, vface):
+        """Use caller-provided thn tables (any volume-fraction field; host arrays or tensors)."""
+        N = self.n * self.n
+        tabs = []
+        for a in (cell, uface, vface):
+            a = torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64) if isinstance(a, np.ndarray) else a)
+            a = a.to(device=self.device, dtype=torch.float64).contiguous()
+            if a.numel() != N:
+                raise ValueError("theta tables must have n*n entries")
+            tabs.append(a)
+        self._theta = tuple(tabs)
+
+    def _params(self, c=1.0, d_u=-1.0, d_p=1.0, d_div=-1.0):
+        return _lib.StokesParams(self.n, self.xi, self.eta_n, self.eta_s, float(c), float(d_u), float(d_p),
+                                 float(d_div))
+
+    def assemble(self, op, c=1.0, d_u=-1.0, d_p=1.0, d_div=-1.0) -> DeviceCSR:
+        cell, uface, vface = self.theta_tables()
+        prm = self._params(c, d_u, d_p, d_div)
+        rows = check(lib().mpbp_stokes_rows(self.n, op))
+        cols = check(lib().mpbp_stokes_cols(self.n, op))
+        row_nnz = torch.empty(rows, dtype=torch.int32, device=self.device)
+        check(lib().mpbp_stokes_count(ctypes.byref(prm), op, ptr(cell), ptr(row_nnz), stream_handle()))
+        rp, ci, va = csr_from_row_nnz(row_nnz, (rows, cols), self.device)
+        check(lib().mpbp_stokes_fill(ctypes.byref(prm), op, ptr(cell), ptr(uface), ptr(vface), ptr(rp), ptr(ci),
+                                     ptr(va), stream_handle()))
+        return DeviceCSR(rp, ci, va, (rows, cols))
+
+    # -- the reference's interface ---------------------------------------------------------------
+    def get_block_matrices(self, is_ths):
+        """(L, D, XI, G) of one phase (preconditioner.py:86-297)."""
+        s = bool(is_ths)
+        return (self.assemble(_lib.OP_L_S if s else _lib.OP_L_N),
+                self.assemble(_lib.OP_D_S if s else _lib.OP_D_N),
+                self.assemble(_lib.OP_XI_S if s else _lib.OP_XI_N),
+                self.assemble(_lib.OP_G_S if s else _lib.OP_G_N))
+
+    def get_big_A_matrix(self, c, d_u, d_p: float = 1.0, d_div: float = -1.0):
+        """(A, S, F, D, G) (preconditioner.py:299-349); S (dense exact Schur complement) is None."""
+        kw = dict(c=c, d_u=d_u, d_p=d_p, d_div=d_div)
+        A = self.assemble(_lib.OP_A, **kw)
+        F = self.assemble(_lib.OP_F, **kw)
+        D = self.assemble(_lib.OP_D, **kw)
+        G = self.assemble(_lib.OP_G, **kw)
+        return A, None, F, D, G
+
+    @staticmethod
+    def commutator_products(F: DeviceCSR, D: DeviceCSR, G: DeviceCSR):
+        """Gt_G = (-D) G and Gt_F_G = ((-D) F) G (solve.py:246-249), sparse products in HBM."""
+        GtG = spgemm(D, G, alpha=-1.0)
+        GtF = spgemm(D, F, alpha=-1.0)
+        GtFG = spgemm(GtF, G, alpha=1.0)
+        del GtF
+        return GtG, GtFG

@@ -1,0 +1,299 @@
+"""The preconditioned solve -- the reference's solve.py surface, with the apply on the GPU.
+
+    ApproxSchurPreconditioner  ~ approx_schur = LinearOperator(matvec=approx_schur_op)  solve.py:240-281
+    fgmres                     ~ pyamg.krylov.fgmres (the outer Krylov loop)           solve.py:285
+    solve_with_approx_schur_pc ~ solve.py:240-286
+    Jacobi                     ~ solve.py:149-159 (as an inner solver kind)
+
+The reference factors F and Gt_G with ilupp's ILUT (solve.py:251-254; sequential triangular
+solves).  On MI355X the inner inverses are the fused Jacobi / Chebyshev-Jacobi SpMV sweeps of
+libmpbp (``InnerSolver``); the outer composition of approx_schur_op is unchanged and runs as one
+native call (``mpbp_schur_apply``) that is graph-capturable.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import scipy.sparse.linalg as spla
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr, stream_handle
+from .csr import DeviceCSR
+from .preconditioner import MultiphaseBlockPreconditioner
+
+
+@dataclass
+class InnerSolver:
+    """Approximate inverse used for F^-1 and Gt_G^-1 inside the apply.
+
+    kind   "jacobi" (solve.py:149-159) or "chebyshev" (Chebyshev-Jacobi, BASELINE configs[3])
+    sweeps updates of x from x0 = 0 (sweeps - 1 SpMVs)
+    lmax   upper bound of spec(diag(M)^-1 M); None -> Gershgorin bound computed on the GPU
+    lmin   lower end of the Chebyshev interval; None -> lmax / ratio
+    """
+    kind: str = "chebyshev"
+    sweeps: int = 4
+    lmin: float | None = None
+    lmax: float | None = None
+    ratio: float = 30.0
+
+    def resolve(self, M: DeviceCSR, diag: torch.Tensor) -> "InnerSolver":
+        if self.kind == "jacobi":
+            return InnerSolver("jacobi", int(self.sweeps), 0.0, 0.0, self.ratio)
+        if self.kind != "chebyshev":
+            raise ValueError(f"unknown inner solver {self.kind!r}")
+        lmax = float(self.lmax) if self.lmax is not None else M.gershgorin(diag)
+        lmin = float(self.lmin) if self.lmin is not None else lmax / self.ratio
+        return InnerSolver("chebyshev", int(self.sweeps), lmin, lmax, self.ratio)
+
+    def cstruct(self):
+        kind = _lib.INNER_CHEBYSHEV if self.kind == "chebyshev" else _lib.INNER_JACOBI
+        return _lib.InnerSolverC(kind, int(self.sweeps), float(self.lmin or 0.0), float(self.lmax or 0.0))
+
+
+def _device_csr(M, device):
+    return M if isinstance(M, DeviceCSR) else DeviceCSR.from_scipy(M, device)
+
+
+class ApproxSchurPreconditioner(spla.LinearOperator):
+    """M^-1 of the block upper-triangular approximate-commutator preconditioner (solve.py:257-277).
+
+    ``apply(v, out)`` works on CUDA tensors and is graph-capturable; ``matvec`` (the scipy
+    LinearOperator surface) copies a host vector in and out around the same apply.
+    """
+
+    def __init__(self, F, D, G, GtG=None, GtFG=None, inner_F: InnerSolver | None = None,
+                 inner_P: InnerSolver | None = None, device=None):
+        dev = torch.device(device or (F.device if isinstance(F, DeviceCSR) else "cuda"))
+        self.F, self.D, self.G = (_device_csr(M, dev) for M in (F, D, G))
+        if GtG is None or GtFG is None:
+            GtG, GtFG = MultiphaseBlockPreconditioner.commutator_products(self.F, self.D, self.G)
+        self.GtG, self.GtFG = _device_csr(GtG, dev), _device_csr(GtFG, dev)
+        nu, np_ = self.F.shape[0], self.GtG.shape[0]
+        if self.F.shape != (nu, nu) or self.D.shape != (np_, nu) or self.G.shape != (nu, np_) \
+                or self.GtFG.shape != (np_, np_):
+            raise ValueError("inconsistent block shapes")
+        self.nu, self.np = nu, np_
+        self.device = dev
+        self.diag_F = self.F.diagonal()
+        self.diag_P = self.GtG.diagonal()
+        self.inner_F = (inner_F or InnerSolver()).resolve(self.F, self.diag_F)
+        self.inner_P = (inner_P or InnerSolver()).resolve(self.GtG, self.diag_P)
+        f64 = dict(dtype=torch.float64, device=dev)
+        self._wu = [torch.empty(nu, **f64) for _ in range(4)]
+        self._wu_owned = torch.empty(nu, **f64)
+        self._wp = [torch.empty(np_, **f64) for _ in range(7)]
+        self._prof = None
+        self._plan = self._make_plan()
+        super().__init__(dtype=np.float64, shape=(nu + np_, nu + np_))
+
+    def _make_plan(self):
+        p = _lib.SchurPlan()
+        p.nu, p.np, p.nu_ext, p.np_ext = self.nu, self.np, self.nu, self.np
+        p.F, p.D, p.G = self.F.cstruct(), self.D.cstruct(), self.G.cstruct()
+        p.GtG, p.GtFG = self.GtG.cstruct(), self.GtFG.cstruct()
+        empty = _lib.RowBlocks(None, 0)
+        p.F_int, p.F_bnd = self.F.blocks.cstruct(), empty
+        p.D_int, p.D_bnd = self.D.blocks.cstruct(), empty
+        p.G_int, p.G_bnd = self.G.blocks.cstruct(), empty
+        p.P_int, p.P_bnd = self.GtG.blocks.cstruct(), empty
+        p.Q_int, p.Q_bnd = self.GtFG.blocks.cstruct(), empty
+        p.diag_F, p.diag_P = self.diag_F.data_ptr(), self.diag_P.data_ptr()
+        p.inner_F, p.inner_P = self.inner_F.cstruct(), self.inner_P.cstruct()
+        for i, t in enumerate(self._wu):
+            p.wu[i] = t.data_ptr()
+        p.wu_owned = self._wu_owned.data_ptr()
+        for i, t in enumerate(self._wp):
+            p.wp[i] = t.data_ptr()
+        p.halo = _lib.HALO_FN()
+        p.halo_ctx = None
+        p.prof_events = None
+        p.prof_capacity = 0
+        p.prof_count = ctypes.POINTER(ctypes.c_int32)()
+        return p
+
+    # -- profiling hook: hipEvent pairs around every inner-F SpMV sweep ------------------------------
+    def enable_profiling(self, capacity: int):
+        evs = (ctypes.c_void_p * (2 * capacity))()
+        for i in range(2 * capacity):
+            e = ctypes.c_void_p()
+            check(lib().mpbp_event_create(ctypes.byref(e)))
+            evs[i] = e
+        cnt = ctypes.c_int32(0)
+        self._prof = (evs, cnt, capacity)
+        self._plan.prof_events = ctypes.cast(evs, ctypes.c_void_p)
+        self._plan.prof_capacity = capacity
+        self._plan.prof_count = ctypes.pointer(cnt)
+
+    def reset_profiling(self):
+        if self._prof:
+            self._prof[1].value = 0
+
+    def profiled_ms(self):
+        """Durations (ms) of the recorded inner-F sweeps (call after synchronising)."""
+        if not self._prof:
+            return []
+        evs, cnt, _ = self._prof
+        out = []
+        for i in range(cnt.value):
+            ms = ctypes.c_float(0.0)
+            check(lib().mpbp_event_elapsed_ms(evs[2 * i], evs[2 * i + 1], ctypes.byref(ms)))
+            out.append(ms.value)
+        return out
+
+    def disable_profiling(self):
+        if self._prof:
+            evs, _, cap = self._prof
+            for i in range(2 * cap):
+                lib().mpbp_event_destroy(evs[i])
+        self._prof = None
+        self._plan.prof_events = None
+        self._plan.prof_capacity = 0
+        self._plan.prof_count = ctypes.POINTER(ctypes.c_int32)()
+
+    # -- the apply ---------------------------------------------------------------------------------
+    def apply(self, v: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        assert v.is_cuda and v.dtype == torch.float64 and v.numel() == self.nu + self.np
+        if out is None:
+            out = torch.empty_like(v)
+        check(lib().mpbp_schur_apply(ctypes.byref(self._plan), ptr(v), ptr(out), stream_handle()))
+        return out
+
+    def _matvec(self, x):
+        v = torch.from_numpy(np.ascontiguousarray(np.ravel(x), dtype=np.float64)).to(self.device)
+        return self.apply(v).cpu().numpy()
+
+    # reference naming (solve.py:257)
+    def approx_schur_op(self, v):
+        return self._matvec(v)
+
+
+def _as_operator(A):
+    if A is None:
+        return None
+    if isinstance(A, DeviceCSR):
+        return lambda x, out=None: A.matvec(x, out=out)
+    if isinstance(A, ApproxSchurPreconditioner):
+        return lambda x, out=None: A.apply(x, out=out)
+    if callable(A):
+        return lambda x, out=None: A(x)
+    raise TypeError(f"unsupported operator {type(A)}")
+
+
+def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=None, residuals=None):
+    """Flexible GMRES with right preconditioning, all vectors in HBM.
+
+    Same call shape as pyamg.krylov.fgmres (solve.py:207, 237, 285): convergence when the
+    residual 2-norm falls below ``tol * ||r0||``; returns (x, info) with info 0 on convergence
+    and the iteration count otherwise.  ``callback(xk)`` receives the current iterate as a CUDA
+    tensor after every inner iteration (the reference's true-residual printer, solve.py:161-170).
+    Orthogonalisation is classical Gram-Schmidt with one re-orthogonalisation pass (CGS2: two
+    batched GEMVs per iteration instead of j dependent dot products).  pyamg is not installed
+    here, so iteration counts against pyamg itself are unpinned.
+    """
+    Aop = _as_operator(A)
+    Mop = _as_operator(M)
+    b = b if isinstance(b, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(b, dtype=np.float64)).cuda()
+    n = b.numel()
+    x = torch.zeros_like(b) if x0 is None else (
+        x0.clone() if isinstance(x0, torch.Tensor) else torch.from_numpy(np.asarray(x0, dtype=np.float64)).to(b.device))
+    maxiter = int(maxiter) if maxiter is not None else min(n, 200)
+    m = int(restrt) if restrt is not None else maxiter
+    r = b - Aop(x)
+    normr = float(torch.linalg.vector_norm(r))
+    if residuals is not None:
+        residuals[:] = [normr]
+    normb = float(torch.linalg.vector_norm(b)) or 1.0
+    if normr < tol * normb:
+        return x, 0
+    target = tol * normr if normr != 0.0 else tol
+    it = 0
+    while it < maxiter:
+        beta = normr
+        V = torch.zeros(m + 1, n, dtype=b.dtype, device=b.device)
+        Z = torch.zeros(m, n, dtype=b.dtype, device=b.device)
+        H = np.zeros((m + 1, m))
+        cs, sn = np.zeros(m), np.zeros(m)
+        g = np.zeros(m + 1)
+        g[0] = beta
+        V[0] = r / beta
+        k = 0
+        for j in range(m):
+            Z[j] = Mop(V[j]) if Mop is not None else V[j]
+            w = Aop(Z[j])
+            h = V[: j + 1] @ w
+            w = w - V[: j + 1].T @ h
+            h2 = V[: j + 1] @ w
+            w = w - V[: j + 1].T @ h2
+            hcol = (h + h2).cpu().numpy()
+            hn = float(torch.linalg.vector_norm(w))
+            H[: j + 1, j] = hcol
+            H[j + 1, j] = hn
+            if hn != 0.0:
+                V[j + 1] = w / hn
+            for i in range(j):                          # apply previous Givens rotations
+                t = cs[i] * H[i, j] + sn[i] * H[i + 1, j]
+                H[i + 1, j] = -sn[i] * H[i, j] + cs[i] * H[i + 1, j]
+                H[i, j] = t
+            den = math.hypot(H[j, j], H[j + 1, j])
+            cs[j], sn[j] = (1.0, 0.0) if den == 0.0 else (H[j, j] / den, H[j + 1, j] / den)
+            H[j, j] = cs[j] * H[j, j] + sn[j] * H[j + 1, j]
+            H[j + 1, j] = 0.0
+            g[j + 1] = -sn[j] * g[j]
+            g[j] = cs[j] * g[j]
+            k = j + 1
+            it += 1
+            res = abs(g[j + 1])
+            if residuals is not None:
+                residuals.append(res)
+            if callback is not None:
+                y = np.linalg.solve(np.triu(H[:k, :k]), g[:k]) if k else np.zeros(0)
+                callback(x + Z[:k].T @ torch.from_numpy(y).to(b.device))
+            if res <= target or it >= maxiter or hn == 0.0:
+                break
+        y = np.linalg.solve(np.triu(H[:k, :k]), g[:k])
+        x = x + Z[:k].T @ torch.from_numpy(y).to(b.device)
+        r = b - Aop(x)
+        normr = float(torch.linalg.vector_norm(r))
+        if normr <= target:
+            return x, 0
+    return x, it
+
+
+def print_true_res_norm(A, b_vec):
+    """Callback printing true residual norms (solve.py:161-170)."""
+    iteration = 0
+    op = _as_operator(A)
+    nb = float(torch.linalg.vector_norm(b_vec))
+
+    def callback(xk):
+        nonlocal iteration
+        iteration += 1
+        res = float(torch.linalg.vector_norm(b_vec - op(xk)))
+        print(f"GMRES Iteration {iteration}: True residual norm = {res}, Rel residual norm: {res / nb}")
+    return callback
+
+
+def solve_with_approx_schur_pc(n, xi, etan, etas, c, d, b_vec, u_vec, inner_F=None, inner_P=None,
+                               tol=1e-8, maxiter=150, verbose=True):
+    """solve.py:240-286: FGMRES on A with the approximate-commutator preconditioner.
+
+    Returns (u_approx, info, residual history) with u_approx a host array.
+    """
+    from .utils import print_norms
+    bp = MultiphaseBlockPreconditioner(n, xi, etan, etas)
+    A, _, F, D, G = bp.get_big_A_matrix(c=c, d_u=d)
+    pc = ApproxSchurPreconditioner(F, D, G, inner_F=inner_F, inner_P=inner_P)
+    b = torch.from_numpy(np.ascontiguousarray(b_vec, dtype=np.float64)).to(pc.device)
+    hist = []
+    x, info = fgmres(A, b, M=pc, tol=tol, maxiter=maxiter,
+                     callback=print_true_res_norm(A, b) if verbose else None, residuals=hist)
+    u_approx = x.cpu().numpy()
+    if verbose:
+        print("\nPrinting error norms for solving Ax=b using fGMRES with approx schur complement as preconditioner:")
+        print_norms(u_approx, u_vec, 1 / n, 1 / n, n)
+    return u_approx, info, hist

@@ -1,0 +1,106 @@
+"""CPU checks of the C-ABI library: it loads, exports every symbol include/mpbp.h declares, and its
+host-only entry points (row-block planner, Chebyshev coefficients, operator sizes) agree with the
+oracle.  No compute kernels are launched (there is no GPU here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+def _header_symbols():
+    with open(os.path.join(ROOT, "include", "mpbp.h")) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"\b(mpbp_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    from mp_block_preconditioners_amd import _lib
+    L = _lib.lib()
+    declared = _header_symbols()
+    assert len(declared) >= 25
+    missing = [s for s in declared if not hasattr(L, s)]
+    assert not missing, missing
+    assert set(declared) == set(_lib.exported_symbols())
+    assert L.mpbp_version().decode().startswith("libmpbp")
+
+
+def test_library_is_gfx950_code_object():
+    from mp_block_preconditioners_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        blob = f.read()
+    assert b"gfx950" in blob
+
+
+def test_operator_sizes():
+    from mp_block_preconditioners_amd import _lib
+    L = _lib.lib()
+    n = 7
+    N = n * n
+    expect = {_lib.OP_A: (5 * N, 5 * N), _lib.OP_F: (4 * N, 4 * N), _lib.OP_D: (N, 4 * N),
+              _lib.OP_G: (4 * N, N), _lib.OP_L_N: (2 * N, 2 * N), _lib.OP_D_S: (N, 2 * N),
+              _lib.OP_G_N: (2 * N, N), _lib.OP_XI_S: (2 * N, 2 * N)}
+    for op, (r, c) in expect.items():
+        assert L.mpbp_stokes_rows(n, op) == r
+        assert L.mpbp_stokes_cols(n, op) == c
+    assert L.mpbp_stokes_rows(n, 99) < 0
+    assert b"unknown operator" in L.mpbp_last_error()
+
+
+def _py_plan(rp, a, b, max_rows=256, cap=4095):
+    out = []
+    r = a
+    while r < b:
+        s = e = r
+        while e < b and e - s < max_rows and rp[e + 1] - rp[s] <= cap:
+            e += 1
+        if e == s:
+            e = s + 1
+        out.append((s, e))
+        r = e
+    return out
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_row_block_planner(seed):
+    from mp_block_preconditioners_amd import _lib
+    rng = np.random.default_rng(seed)
+    lengths = rng.integers(0, 40, size=3000)
+    lengths[rng.integers(0, 3000, size=3)] = 5000          # rows longer than the LDS stage
+    rp = np.zeros(lengths.size + 1, dtype=np.int32)
+    np.cumsum(lengths, out=rp[1:])
+    L = _lib.lib()
+    for a, b in ((0, 3000), (17, 2900), (5, 5)):
+        need = L.mpbp_plan_row_blocks(rp.ctypes.data_as(ctypes.c_void_p), a, b, None, 0)
+        buf = np.zeros(2 * max(need, 1), dtype=np.int32)
+        L.mpbp_plan_row_blocks(rp.ctypes.data_as(ctypes.c_void_p), a, b, buf.ctypes.data_as(ctypes.c_void_p), need)
+        got = [tuple(p) for p in buf[: 2 * need].reshape(-1, 2)]
+        assert got == _py_plan(rp, a, b)
+        for s, e in got:
+            assert e - s <= 256 and (rp[e] - rp[s] <= 4095 or e - s == 1)
+
+
+def test_cheb_coeffs_match_oracle():
+    from mp_block_preconditioners_amd import _lib
+    from oracle.schur_oracle import cheb_coeffs
+    L = _lib.lib()
+    for lmin, lmax, k in ((0.05, 2.0, 8), (1e-3, 1.7, 3), (0.0, 1.0, 1)):
+        c1 = np.zeros(k)
+        c2 = np.zeros(k)
+        assert L.mpbp_cheb_coeffs(lmin, lmax, k, c1.ctypes.data_as(ctypes.c_void_p),
+                                  c2.ctypes.data_as(ctypes.c_void_p)) == 0
+        o1, o2 = cheb_coeffs(lmin, lmax, k)
+        assert np.array_equal(c1, o1) and np.array_equal(c2, o2)
+    c = np.zeros(2)
+    assert L.mpbp_cheb_coeffs(1.0, 1.0, 2, c.ctypes.data_as(ctypes.c_void_p), c.ctypes.data_as(ctypes.c_void_p)) < 0
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    from mp_block_preconditioners_amd import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "libmpbp.so"))
+    with pytest.raises(_lib.MpbpError, match="no CPU fallback"):
+        _lib.lib()

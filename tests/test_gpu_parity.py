@@ -1,0 +1,259 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the reference fixtures.
+
+Bars (BASELINE.json north_star):
+* CSR indexing (row_ptr, col_idx) bit-exact against the oracle;
+* values bit-exact against the oracle when both are fed the same thn tables (same IEEE operations,
+  same order, no FMA), and within 1e-12 relative infinity-norm of the reference's fp64 results;
+* at the BASELINE sizes (1024^2), where the oracle is too slow to run whole, size-independent
+  properties: linearity and determinism of the apply, the O(h^2) consistency of A on the
+  manufactured solution, and an oracle comparison on a row sample.
+"""
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from conftest import golden_csr, golden_files, golden_params, load_golden, rel_inf
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu(oracle_built):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _mp():
+    import mp_block_preconditioners_amd as mp
+    return mp
+
+
+def _oracle_system(n, tables=None, **kw):
+    from oracle.stokes_oracle import StokesSystem
+    return StokesSystem(n, tables=tables, **kw)
+
+
+def _same_csr(dev, ref):
+    got = dev.to_scipy()
+    ref = sp.csr_matrix(ref)
+    assert got.shape == ref.shape
+    assert np.array_equal(got.indptr, ref.indptr), "row_ptr differs"
+    assert np.array_equal(got.indices, ref.indices), "col_idx differs"
+    assert np.array_equal(got.data.view(np.uint64), ref.data.view(np.uint64)), \
+        f"values differ (max {np.max(np.abs(got.data - ref.data)):.3e})"
+
+
+def _cuda(x):
+    return torch.from_numpy(np.ascontiguousarray(x, dtype=np.float64)).cuda()
+
+
+def _bits_equal(a, b):
+    a = a.cpu().numpy() if hasattr(a, "cpu") else np.asarray(a)
+    return np.array_equal(np.asarray(a, dtype=np.float64).view(np.uint64), np.asarray(b, dtype=np.float64).view(np.uint64))
+
+
+PARAMS = dict(xi=1.0, eta_n=100.0, eta_s=1.0, c=1.0, d_u=-1.0, d_p=1.0, d_div=-1.0)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 16, 64])
+def test_theta_tables_match_oracle(n):
+    from oracle.stokes_oracle import theta_tables
+    bp = _mp().MultiphaseBlockPreconditioner(n, 1.0, 1.0, 1.0)
+    for got, ref in zip(bp.theta_tables(), theta_tables(n)):
+        assert rel_inf(got.cpu().numpy(), ref) <= 4e-16
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 8, 33, 128])
+def test_assembly_bit_exact(n):
+    mp = _mp()
+    from oracle.stokes_oracle import theta_tables
+    tabs = theta_tables(n)
+    osys = _oracle_system(n, tables=tabs, products=False, **PARAMS)
+    bp = mp.MultiphaseBlockPreconditioner(n, PARAMS["xi"], PARAMS["eta_n"], PARAMS["eta_s"])
+    bp.set_theta_tables(*tabs)
+    A, S, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    assert S is None
+    _same_csr(A, osys.A)
+    _same_csr(F, osys.F)
+    _same_csr(D, osys.D)
+    _same_csr(G, osys.G)
+    for is_ths in (False, True):
+        for dev, ref in zip(bp.get_block_matrices(is_ths), osys.block_matrices(is_ths)):
+            _same_csr(dev, ref)
+
+
+@pytest.mark.parametrize("path", golden_files(), ids=os.path.basename)
+def test_assembly_against_reference(path):
+    """GPU-computed thn tables + GPU assembly vs the reference's dense matrices (1e-12)."""
+    mp = _mp()
+    from test_oracle_golden import assert_matrix_matches
+    g = load_golden(path)
+    p = golden_params(g)
+    bp = mp.MultiphaseBlockPreconditioner(p["n"], p["xi"], p["eta_n"], p["eta_s"])
+    A, _, F, D, G = bp.get_big_A_matrix(c=p["c"], d_u=p["d_u"])
+    assert_matrix_matches(A.to_scipy(), golden_csr(g, "A"))
+    assert rel_inf(A.matvec(_cuda(g["u_vec"])).cpu().numpy(), g["Au"]) <= 1e-12     # apply.py:72
+    if "F_data" in g:
+        assert_matrix_matches(F.to_scipy(), golden_csr(g, "F"))
+        GtG, GtFG = bp.commutator_products(F, D, G)
+        assert_matrix_matches(GtG.to_scipy(), golden_csr(g, "GtG"))
+        assert_matrix_matches(GtFG.to_scipy(), golden_csr(g, "GtFG"))
+
+
+@pytest.mark.parametrize("n", [3, 16, 48])
+def test_spgemm_bit_exact(n):
+    mp = _mp()
+    from oracle import csr_oracle as co
+    osys = _oracle_system(n, **PARAMS)
+    F, D, G = (mp.DeviceCSR.from_scipy(M) for M in (osys.F, osys.D, osys.G))
+    GtG, GtFG = mp.MultiphaseBlockPreconditioner.commutator_products(F, D, G)
+    _same_csr(GtG, osys.GtG)
+    _same_csr(GtFG, osys.GtFG)
+    _same_csr(mp.spgemm(F, G, alpha=2.5), co.spgemm(osys.F, osys.G, alpha=2.5))
+
+
+@pytest.mark.parametrize("n", [2, 16, 100])
+def test_spmv_bit_exact(n):
+    mp = _mp()
+    from oracle import csr_oracle as co
+    osys = _oracle_system(n, products=False, **PARAMS)
+    rng = np.random.default_rng(n)
+    for M in (osys.A, osys.F, osys.D, osys.G):
+        dM = mp.DeviceCSR.from_scipy(M)
+        x = rng.standard_normal(M.shape[1])
+        z = rng.standard_normal(M.shape[0])
+        for mode in (0, 1, 2):
+            y = dM.matvec(_cuda(x), mode=mode, z=_cuda(z))
+            assert _bits_equal(y, co.spmv(M, x, z, mode=mode)), (M.shape, mode)
+
+
+def test_spmv_long_rows_and_empty_rows():
+    """Rows longer than the LDS stage (single-row blocks, tree reduction) and empty rows."""
+    mp = _mp()
+    rng = np.random.default_rng(7)
+    lengths = rng.integers(0, 30, size=2000)
+    lengths[[5, 777, 1999]] = [9000, 4096, 20000]
+    lengths[[0, 10, 11]] = 0
+    rows = np.repeat(np.arange(lengths.size), lengths)
+    cols = rng.integers(0, 50000, size=rows.size)
+    M = sp.csr_matrix((rng.standard_normal(rows.size), (rows, cols)), shape=(lengths.size, 50000))
+    M.sum_duplicates()
+    x = rng.standard_normal(50000)
+    y = mp.DeviceCSR.from_scipy(M).matvec(_cuda(x)).cpu().numpy()
+    ref = M @ x
+    assert rel_inf(y, ref) <= 1e-13
+    assert y[0] == 0.0 and y[10] == 0.0
+
+
+@pytest.mark.parametrize("n", [4, 32])
+def test_inner_steps_bit_exact(n):
+    mp = _mp()
+    from mp_block_preconditioners_amd import _lib
+    from mp_block_preconditioners_amd._lib import check, lib, ptr, stream_handle
+    from oracle import csr_oracle as co
+    import ctypes
+    osys = _oracle_system(n, **PARAMS)
+    rng = np.random.default_rng(3)
+    for M in (osys.F, osys.GtG):
+        dM = mp.DeviceCSR.from_scipy(M)
+        diag = M.diagonal().copy()
+        b, x, d0, sub = (rng.standard_normal(M.shape[0]) for _ in range(4))
+        tb, tx, tdiag, tsub = _cuda(b), _cuda(x), _cuda(diag), _cuda(sub)
+        out = torch.empty_like(tb)
+        blk = dM.blocks.cstruct()
+        check(lib().mpbp_jacobi_step(ctypes.byref(dM.cstruct()), ctypes.byref(blk), ptr(tx), ptr(tb), ptr(tdiag),
+                                     ptr(tsub), ptr(out), stream_handle()))
+        assert _bits_equal(out, co.jacobi_step(M, x, b, diag, sub))
+        td = _cuda(d0)
+        d_ref = d0.copy()
+        check(lib().mpbp_cheb_step(ctypes.byref(dM.cstruct()), ctypes.byref(blk), ptr(tx), ptr(tb), ptr(tdiag),
+                                   0.3, 1.7, ptr(td), None, ptr(out), stream_handle()))
+        ref = co.cheb_step(M, x, b, diag, 0.3, 1.7, d_ref)
+        assert _bits_equal(out, ref) and _bits_equal(td, d_ref)
+
+
+INNERS = [("jacobi", 1, "jacobi", 1), ("jacobi", 3, "jacobi", 2), ("chebyshev", 4, "chebyshev", 4),
+          ("chebyshev", 6, "jacobi", 3)]
+
+
+@pytest.mark.parametrize("n", [3, 16, 64])
+@pytest.mark.parametrize("inner", INNERS, ids=lambda t: f"{t[0]}{t[1]}-{t[2]}{t[3]}")
+def test_schur_apply_bit_exact(n, inner):
+    """mpbp_schur_apply vs the oracle's restatement of approx_schur_op (solve.py:257-277)."""
+    mp = _mp()
+    from oracle.schur_oracle import Inner, approx_schur_apply, diagonal, gershgorin
+    osys = _oracle_system(n, **PARAMS)
+    kf, sf, kp, spp = inner
+    pc = mp.ApproxSchurPreconditioner(osys.F, osys.D, osys.G, osys.GtG, osys.GtFG,
+                                      inner_F=mp.InnerSolver(kf, sf), inner_P=mp.InnerSolver(kp, spp))
+    # the oracle uses the bounds the GPU computed (Gershgorin on the GPU sums in row order too)
+    dF, dP = diagonal(osys.F), diagonal(osys.GtG)
+    assert np.array_equal(pc.diag_F.cpu().numpy(), dF) and np.array_equal(pc.diag_P.cpu().numpy(), dP)
+    if kf == "chebyshev":
+        assert abs(pc.inner_F.lmax - gershgorin(osys.F, dF)) <= 1e-14 * pc.inner_F.lmax
+    iF = Inner(kf, sf, pc.inner_F.lmin or 0.0, pc.inner_F.lmax or 0.0)
+    iP = Inner(kp, spp, pc.inner_P.lmin or 0.0, pc.inner_P.lmax or 0.0)
+    v = np.random.default_rng(n).standard_normal(pc.shape[0])
+    got = pc.apply(_cuda(v))
+    ref = approx_schur_apply(osys.F, osys.D, osys.G, osys.GtG, osys.GtFG, v, iF, iP)
+    assert _bits_equal(got, ref), rel_inf(got.cpu().numpy(), ref)
+    assert np.array_equal(pc.matvec(v), got.cpu().numpy())           # LinearOperator surface
+
+
+@pytest.mark.parametrize("path", [p for p in golden_files() if "n32" not in p], ids=os.path.basename)
+def test_schur_apply_against_reference(path):
+    """Jacobi-inner apply vs the reference composition on the reference's own matrices (1e-11)."""
+    mp = _mp()
+    g = load_golden(path)
+    p = golden_params(g)
+    bp = mp.MultiphaseBlockPreconditioner(p["n"], p["xi"], p["eta_n"], p["eta_s"])
+    A, _, F, D, G = bp.get_big_A_matrix(c=p["c"], d_u=p["d_u"])
+    for nf, npp in ((1, 1), (3, 2)):
+        pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("jacobi", nf),
+                                          inner_P=mp.InnerSolver("jacobi", npp))
+        assert rel_inf(pc.apply(_cuda(g["v"])).cpu().numpy(), g[f"schur_jacobi_{nf}_{npp}"]) <= 1e-11
+
+
+def test_full_size_properties():
+    """1024^2 (BASELINE configs[2]): linearity, determinism, O(h^2) consistency, sampled oracle rows."""
+    mp = _mp()
+    n = 1024
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    assert A.nnz == 56 * n * n and F.nnz == 40 * n * n
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("chebyshev", 4),
+                                      inner_P=mp.InnerSolver("chebyshev", 4))
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    v1 = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda", generator=gen)
+    v2 = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda", generator=gen)
+    y1, y2 = pc.apply(v1), pc.apply(v2)
+    y12 = pc.apply(2.0 * v1 - 0.5 * v2)
+    assert rel_inf((y12 - (2.0 * y1 - 0.5 * y2)).cpu().numpy() + 0, (2.0 * y1 - 0.5 * y2).cpu().numpy()) <= 1e-12
+    assert torch.equal(pc.apply(v1), y1)                                      # deterministic
+    # manufactured solution: ||A u - b||_inf / ||b||_inf is a truncation error, O(h^2)
+    u, b = mp.manufactured_problem(n, 1.0, -1.0, 1.0, 100.0, 1.0)
+    Au = A.matvec(_cuda(u)).cpu().numpy()
+    assert rel_inf(Au, b) <= 1e-3
+    # sampled rows of A x against a host CSR product of the same device matrix
+    x = np.random.default_rng(0).standard_normal(A.shape[1])
+    y = A.matvec(_cuda(x)).cpu().numpy()
+    Ah = A.to_scipy()
+    rows = np.random.default_rng(1).choice(A.shape[0], 4096, replace=False)
+    assert rel_inf(y[rows], Ah[rows] @ x) <= 1e-12
+
+
+def test_fgmres_converges_with_gpu_preconditioner():
+    mp = _mp()
+    n = 32
+    u, b = mp.manufactured_problem(n, 1.0, -1.0, 1.0, 100.0, 1.0)
+    x, info, hist = mp.solve_with_approx_schur_pc(n, 1.0, 100.0, 1.0, 1.0, -1.0, b, u,
+                                                  inner_F=mp.InnerSolver("chebyshev", 8),
+                                                  inner_P=mp.InnerSolver("chebyshev", 8),
+                                                  tol=1e-8, maxiter=400, verbose=False)
+    assert info == 0 and hist[-1] <= 1e-8 * hist[0] * 1.0001
+    # discretisation error of the converged solution (velocity components), O(h^2)
+    assert np.max(np.abs(x[: 4 * n * n] - u[: 4 * n * n])) < 5e-2
