@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--eta-s", type=float, default=1.0)
     ap.add_argument("--inner-f", default="chebyshev:4")
     ap.add_argument("--inner-p", default="chebyshev:4")
+    ap.add_argument("--layout", default="sell", choices=["sell", "csr"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -61,7 +62,8 @@ def main():
     kp, spp = parse_inner(args.inner_p)
     bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
     A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
-    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver(kf, sf), inner_P=mp.InnerSolver(kp, spp))
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver(kf, sf), inner_P=mp.InnerSolver(kp, spp),
+                                      layout=args.layout)
     gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
     v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda", generator=gen)
     out = torch.empty_like(v)
@@ -89,10 +91,17 @@ def main():
     sweep_ms = pc.profiled_ms()
     pc.disable_profiling()
 
-    # dominant kernel: the fused Chebyshev-Jacobi CSR sweep over F (k_csr_rows<EpiCheb>)
+    # dominant kernel: the fused Chebyshev-Jacobi sweep over F (k_sell_rows / k_csr_rows <EpiCheb>)
+    # algorithmic bytes: matrix entries (8 B value + 4 B column) + per-row index data + x, b, diag,
+    # d (read + write) and x_out (8 B each per row) + the row-block / slice descriptors
     nF, nnzF = F.shape[0], F.nnz
-    nblk = F.blocks.count
-    sweep_bytes = nnzF * (8 + 4) + (nF + 1) * 4 + nF * 8 * (1 + 1 + 1 + 2 + 1) + nblk * 8
+    if args.layout == "sell":
+        S = pc._sell[0]
+        sweep_bytes = nnzF * (8 + 4) + nF * 1 + nF * 8 * (1 + 1 + 1 + 2 + 1) + S.nslices * 16
+        kname = "k_sell_rows<EpiCheb> (F Chebyshev sweep, SELL-64)"
+    else:
+        sweep_bytes = nnzF * (8 + 4) + (nF + 1) * 4 + nF * 8 * (1 + 1 + 1 + 2 + 1) + F.blocks.count * 8
+        kname = "k_csr_rows<EpiCheb> (F Chebyshev sweep, CSR)"
     avg_sweep_s = (sum(sweep_ms) / len(sweep_ms) / 1e3) if sweep_ms else float("nan")
     achieved = sweep_bytes / avg_sweep_s / 1e9
 
@@ -110,6 +119,17 @@ def main():
     torch.cuda.synchronize()
     spmv_s = ev[0].elapsed_time(ev[1]) / 1e3 / reps
     spmv_bytes = A.nnz * 12 + (A.shape[0] + 1) * 4 + (A.shape[0] + A.shape[1]) * 8 + A.blocks.count * 8
+    AS = A.to_sell()
+    for _ in range(3):
+        AS.matvec(x, out=y)
+    ev[0].record()
+    for _ in range(reps):
+        AS.matvec(x, out=y)
+    ev[1].record()
+    torch.cuda.synchronize()
+    sell_s = ev[0].elapsed_time(ev[1]) / 1e3 / reps
+    sell_bytes = A.nnz * 12 + A.shape[0] * 1 + (A.shape[0] + A.shape[1]) * 8 + AS.nslices * 16
+    del AS
 
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -145,14 +165,16 @@ def main():
                                    "(BASELINE configs[2])",
                        "n": n, "unknowns": int(pc.shape[0]), "xi": args.xi, "eta_n": args.eta_n,
                        "eta_s": args.eta_s, "inner_F": f"{kf}:{sf}", "inner_P": f"{kp}:{spp}",
-                       "parallelism": "replicas" if world > 1 else "single"},
+                       "parallelism": "replicas" if world > 1 else "single",
+                       "layout": args.layout},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_csr_rows<EpiCheb> (F Chebyshev sweep)",
+                         "kernel": kname,
                          "bytes_per_launch": sweep_bytes, "avg_launch_us": avg_sweep_s * 1e6,
                          "launches_timed": len(sweep_ms)},
-            "spmv_A": {"gbs": spmv_bytes / spmv_s / 1e9, "us": spmv_s * 1e6, "nnz": A.nnz,
-                       "bytes": spmv_bytes},
+            "spmv_A": {"csr_gbs": spmv_bytes / spmv_s / 1e9, "csr_us": spmv_s * 1e6, "nnz": A.nnz,
+                       "csr_bytes": spmv_bytes, "sell_gbs": sell_bytes / sell_s / 1e9, "sell_us": sell_s * 1e6,
+                       "sell_bytes": sell_bytes},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

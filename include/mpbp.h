@@ -81,6 +81,20 @@ typedef struct mpbp_rowblocks {
 #define MPBP_BLOCK_ROWS 256
 #define MPBP_BLOCK_NNZ 4095
 
+/* SELL-64: sliced ELLPACK, one wavefront (64 rows) per slice, entries column-major in pairs.
+ * slices: device int32[4*nslices] = {row0, rows (<= 64), width, first pair-row}; row_len: device
+ * uint8[nrows]; val / col: device arrays of 128 doubles / int32 per pair-row (zero padding). */
+typedef struct mpbp_sell {
+    int32_t nrows;
+    int32_t ncols;
+    int32_t nslices;
+    int32_t reserved;
+    const int32_t* slices;
+    const uint8_t* row_len;
+    const double* val;
+    const int32_t* col;
+} mpbp_sell;
+
 typedef struct mpbp_stokes_params {
     int32_t n;     /* grid is n x n, N = n*n cells, dx = dy = 1/n */
     double xi;     /* drag coefficient */
@@ -121,6 +135,8 @@ typedef struct mpbp_schur_plan {
     void** prof_events;              /* optional: hipEvent_t pairs around every inner-F SpMV sweep */
     int32_t prof_capacity;           /* number of event pairs available */
     int32_t* prof_count;             /* host int: pairs recorded so far (caller resets) */
+    int32_t use_sell;                /* 1: run the SELL-64 copies below instead of CSR row blocks */
+    mpbp_sell Fs_int, Fs_bnd, Ds_int, Ds_bnd, Gs_int, Gs_bnd, Ps_int, Ps_bnd, Qs_int, Qs_bnd;
 } mpbp_schur_plan;
 
 const char* mpbp_version(void);
@@ -191,6 +207,22 @@ int mpbp_cheb_coeffs(double lmin, double lmax, int32_t sweeps, double* c1, doubl
 /* out = M^-1 v with M the block upper-triangular approximate-commutator preconditioner
  * (solve.py:257-277): v, out are device vectors of nu + np owned entries. */
 int mpbp_schur_apply(const mpbp_schur_plan* plan, const double* v, double* out, void* stream);
+
+/* ---- SELL-64 (the apply's HBM layout; built once from CSR) --------------------------------- */
+/* Host: slices of <= 64 rows over each row range [ranges[2q], ranges[2q+1]) of a HOST row_ptr.
+ * Writes at most `capacity` slices; returns the slice count, *pair_rows = storage in pair-rows. */
+int64_t mpbp_sell_plan(const int32_t* row_ptr, const int32_t* ranges, int32_t nranges, int32_t* slices,
+                       int64_t capacity, int64_t* pair_rows);
+/* Copy CSR entries into SELL storage (val / col zero-filled by the caller). */
+int mpbp_sell_fill(const mpbp_csr* A, const int32_t* slices, int32_t nslices, uint8_t* row_len,
+                   double* val, int32_t* col, void* stream);
+/* The CSR apply-path kernels on SELL storage; same arithmetic, same order, same results. */
+int mpbp_sell_spmv(const mpbp_sell* S, int32_t mode, const double* x, const double* z, double* y,
+                   void* stream);
+int mpbp_sell_jacobi_step(const mpbp_sell* S, const double* x_in, const double* b, const double* diag,
+                          const double* sub, double* x_out, void* stream);
+int mpbp_sell_cheb_step(const mpbp_sell* S, const double* x_in, const double* b, const double* diag,
+                        double c1, double c2, double* d, const double* sub, double* x_out, void* stream);
 
 /* gather: dst[i] = src[idx[i]] ; scatter: dst[idx[i]] = src[i]   (halo pack / unpack) */
 int mpbp_gather(int32_t count, const int32_t* idx, const double* src, double* dst, void* stream);

@@ -3,7 +3,7 @@ block preconditioner, applied by hand-written HIP kernels for gfx950 (libmpbp.so
 include/mpbp.h).  Import name: ``mp_block_preconditioners_amd`` (a symlink to this directory).
 """
 from ._lib import MpbpError, lib
-from .csr import DeviceCSR, spgemm
+from .csr import DeviceCSR, DeviceSELL, spgemm
 from .preconditioner import MultiphaseBlockPreconditioner, thn, ths
 from .solve import (ApproxSchurPreconditioner, InnerSolver, fgmres, print_true_res_norm,
                     solve_with_approx_schur_pc)
@@ -11,7 +11,7 @@ from .utils import (fill_sol_and_RHS_vecs, manufactured_problem, max_norm, print
                     weighted_L2)
 
 __all__ = [
-    "MpbpError", "lib", "DeviceCSR", "spgemm", "MultiphaseBlockPreconditioner", "thn", "ths",
+    "MpbpError", "lib", "DeviceCSR", "DeviceSELL", "spgemm", "MultiphaseBlockPreconditioner", "thn", "ths",
     "ApproxSchurPreconditioner", "InnerSolver", "fgmres", "print_true_res_norm",
     "solve_with_approx_schur_pc", "fill_sol_and_RHS_vecs", "manufactured_problem", "max_norm",
     "print_norms", "weighted_L1", "weighted_L2",

@@ -31,6 +31,11 @@ class RowBlocks(Structure):
     _fields_ = [("pairs", c_void_p), ("count", c_int32)]
 
 
+class Sell(Structure):
+    _fields_ = [("nrows", c_int32), ("ncols", c_int32), ("nslices", c_int32), ("reserved", c_int32),
+                ("slices", c_void_p), ("row_len", c_void_p), ("val", c_void_p), ("col", c_void_p)]
+
+
 class StokesParams(Structure):
     _fields_ = [("n", c_int32), ("xi", c_double), ("eta_n", c_double), ("eta_s", c_double),
                 ("c", c_double), ("d_u", c_double), ("d_p", c_double), ("d_div", c_double)]
@@ -53,7 +58,10 @@ class SchurPlan(Structure):
                 ("inner_F", InnerSolverC), ("inner_P", InnerSolverC),
                 ("wu", c_void_p * 4), ("wu_owned", c_void_p), ("wp", c_void_p * 7),
                 ("halo", HALO_FN), ("halo_ctx", c_void_p),
-                ("prof_events", c_void_p), ("prof_capacity", c_int32), ("prof_count", POINTER(c_int32))]
+                ("prof_events", c_void_p), ("prof_capacity", c_int32), ("prof_count", POINTER(c_int32)),
+                ("use_sell", c_int32),
+                ("Fs_int", Sell), ("Fs_bnd", Sell), ("Ds_int", Sell), ("Ds_bnd", Sell), ("Gs_int", Sell),
+                ("Gs_bnd", Sell), ("Ps_int", Sell), ("Ps_bnd", Sell), ("Qs_int", Sell), ("Qs_bnd", Sell)]
 
 
 _P = c_void_p
@@ -81,6 +89,11 @@ _SIGNATURES = {
                        c_int),
     "mpbp_cheb_coeffs": ([c_double, c_double, c_int32, _P, _P], c_int),
     "mpbp_schur_apply": ([POINTER(SchurPlan), _P, _P, _P], c_int),
+    "mpbp_sell_plan": ([_P, _P, c_int32, _P, c_int64, POINTER(c_int64)], c_int64),
+    "mpbp_sell_fill": ([POINTER(Csr), _P, c_int32, _P, _P, _P, _P], c_int),
+    "mpbp_sell_spmv": ([POINTER(Sell), c_int32, _P, _P, _P, _P], c_int),
+    "mpbp_sell_jacobi_step": ([POINTER(Sell), _P, _P, _P, _P, _P, _P], c_int),
+    "mpbp_sell_cheb_step": ([POINTER(Sell), _P, _P, _P, c_double, c_double, _P, _P, _P, _P], c_int),
     "mpbp_gather": ([c_int32, _P, _P, _P, _P], c_int),
     "mpbp_scatter": ([c_int32, _P, _P, _P, _P], c_int),
     "mpbp_event_create": ([POINTER(c_void_p)], c_int),
@@ -132,5 +145,5 @@ def stream_handle(stream=None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
-__all__ = ["lib", "check", "ptr", "stream_handle", "MpbpError", "Csr", "RowBlocks", "StokesParams",
+__all__ = ["lib", "check", "ptr", "stream_handle", "MpbpError", "Csr", "RowBlocks", "Sell", "StokesParams",
            "InnerSolverC", "SchurPlan", "HALO_FN", "byref"]

@@ -123,8 +123,68 @@ class DeviceCSR:
         check(lib().mpbp_gershgorin(ctypes.byref(self.cstruct()), ptr(diag), ctypes.byref(out), stream_handle()))
         return out.value
 
+    def to_sell(self, ranges=None):
+        """SELL-64 copy of the rows in `ranges` (list of [a, b) row ranges; default all rows)."""
+        return DeviceSELL.from_csr(self, ranges)
+
     def __repr__(self):
         return f"DeviceCSR(shape={self.shape}, nnz={self.nnz}, device={self.device})"
+
+
+class DeviceSELL:
+    """SELL-64 copy of (some rows of) a DeviceCSR: one wavefront per 64-row slice, entries
+    column-major in 16-byte pairs.  Row sums keep CSR order, so results equal the CSR kernels'."""
+
+    def __init__(self, csr: DeviceCSR, slices: torch.Tensor, nslices: int, row_len, val, col, pair_rows: int):
+        self.csr, self.slices, self.nslices = csr, slices, nslices
+        self.row_len, self.val, self.col, self.pair_rows = row_len, val, col, pair_rows
+        self.shape = csr.shape
+        self._cs = _lib.Sell(csr.shape[0], csr.shape[1], nslices, 0,
+                             slices.data_ptr() if nslices else None, row_len.data_ptr(),
+                             val.data_ptr(), col.data_ptr())
+
+    @classmethod
+    def from_csr(cls, A: DeviceCSR, ranges=None):
+        rp = A.row_ptr_host
+        rg = np.asarray(ranges if ranges is not None else [(0, A.shape[0])], dtype=np.int32).reshape(-1, 2)
+        rg = np.ascontiguousarray(rg)
+        pr = ctypes.c_int64(0)
+        need = check(lib().mpbp_sell_plan(rp.ctypes.data_as(ctypes.c_void_p), rg.ctypes.data_as(ctypes.c_void_p),
+                                          rg.shape[0], None, 0, ctypes.byref(pr)))
+        sl = np.zeros(4 * max(need, 1), dtype=np.int32)
+        check(lib().mpbp_sell_plan(rp.ctypes.data_as(ctypes.c_void_p), rg.ctypes.data_as(ctypes.c_void_p),
+                                   rg.shape[0], sl.ctypes.data_as(ctypes.c_void_p), need, ctypes.byref(pr)))
+        dev = A.device
+        slices = torch.from_numpy(sl).to(dev)
+        row_len = torch.zeros(max(A.shape[0], 1), dtype=torch.uint8, device=dev)
+        val = torch.zeros(max(pr.value, 1) * 128, dtype=torch.float64, device=dev)
+        col = torch.zeros(max(pr.value, 1) * 128, dtype=torch.int32, device=dev)
+        check(lib().mpbp_sell_fill(ctypes.byref(A.cstruct()), ptr(slices), int(need), ptr(row_len), ptr(val),
+                                   ptr(col), stream_handle()))
+        return cls(A, slices, int(need), row_len, val, col, int(pr.value))
+
+    def sub(self, first: int, count: int):
+        """The slices [first, first+count) as their own SELL view (shares storage)."""
+        view = object.__new__(DeviceSELL)
+        view.__dict__.update(self.__dict__)
+        view.nslices = count
+        view._cs = _lib.Sell(self.shape[0], self.shape[1], count, 0,
+                             self.slices.data_ptr() + 16 * first if count else None, self.row_len.data_ptr(),
+                             self.val.data_ptr(), self.col.data_ptr())
+        return view
+
+    def cstruct(self):
+        return self._cs
+
+    @property
+    def device(self):
+        return self.val.device
+
+    def matvec(self, x, out=None, mode=_lib.SPMV_STORE, z=None):
+        if out is None:
+            out = torch.empty(self.shape[0], dtype=torch.float64, device=self.device)
+        check(lib().mpbp_sell_spmv(ctypes.byref(self._cs), mode, ptr(x), ptr(z), ptr(out), stream_handle()))
+        return out
 
 
 class RowBlockList:

@@ -477,19 +477,27 @@ __device__ inline int xcd_swizzle(int b, int nb) {
     return (b & 7) * per + (b >> 3);
 }
 
+// Epilogues.  pre(r) issues the row's operand loads at kernel start (they overlap the matrix
+// stream); operator() finishes the row once its sum is known.
 struct EpiStore {
     double* y;
-    __device__ void operator()(int32_t r, double acc) const { y[r] = acc; }
+    struct P {};
+    __device__ P pre(int32_t) const { return {}; }
+    __device__ void operator()(int32_t r, double acc, const P&) const { y[r] = acc; }
 };
 struct EpiAdd {   // rhs = D Finv_v + v_p   (solve.py:259)
     const double* z;
     double* y;
-    __device__ void operator()(int32_t r, double acc) const { y[r] = acc + z[r]; }
+    struct P { double z; };
+    __device__ P pre(int32_t r) const { return {z[r]}; }
+    __device__ void operator()(int32_t r, double acc, const P& p) const { y[r] = acc + p.z; }
 };
 struct EpiResid {
     const double* z;
     double* y;
-    __device__ void operator()(int32_t r, double acc) const { y[r] = z[r] - acc; }
+    struct P { double z; };
+    __device__ P pre(int32_t r) const { return {z[r]}; }
+    __device__ void operator()(int32_t r, double acc, const P& p) const { y[r] = p.z - acc; }
 };
 struct EpiJacobi {   // x = (b - R x)/D in residual form (solve.py:158)
     const double* xin;
@@ -497,9 +505,11 @@ struct EpiJacobi {   // x = (b - R x)/D in residual form (solve.py:158)
     const double* diag;
     const double* sub;
     double* xout;
-    __device__ void operator()(int32_t r, double acc) const {
-        const double x = xin[r] + (b[r] - acc) / diag[r];
-        xout[r] = sub ? sub[r] - x : x;
+    struct P { double x, b, d, s; };
+    __device__ P pre(int32_t r) const { return {xin[r], b[r], diag[r], sub ? sub[r] : 0.0}; }
+    __device__ void operator()(int32_t r, double acc, const P& p) const {
+        const double x = p.x + (p.b - acc) / p.d;
+        xout[r] = sub ? p.s - x : x;
     }
 };
 struct EpiCheb {
@@ -510,12 +520,14 @@ struct EpiCheb {
     double c1, c2;
     const double* sub;
     double* xout;
-    __device__ void operator()(int32_t r, double acc) const {
-        const double z = (b[r] - acc) / diag[r];
-        const double dn = c1 * d[r] + c2 * z;
+    struct P { double x, b, dg, d, s; };
+    __device__ P pre(int32_t r) const { return {xin[r], b[r], diag[r], d[r], sub ? sub[r] : 0.0}; }
+    __device__ void operator()(int32_t r, double acc, const P& p) const {
+        const double z = (p.b - acc) / p.dg;
+        const double dn = c1 * p.d + c2 * z;
         d[r] = dn;
-        const double x = xin[r] + dn;
-        xout[r] = sub ? sub[r] - x : x;
+        const double x = p.x + dn;
+        xout[r] = sub ? p.s - x : x;
     }
 };
 
@@ -536,6 +548,15 @@ __global__ void __launch_bounds__(kBlock) k_csr_rows(Csr A, const double* __rest
     const int tid = threadIdx.x;
     const int32_t base = s & ~1;
     if (e - base <= kCap) {
+        const int32_t r = r0 + tid;
+        const bool live = r < r1;
+        int32_t ks = 0, ke = 0;
+        typename Epi::P pe{};
+        if (live) {
+            ks = A.rp[r] - s;
+            ke = A.rp[r + 1] - s;
+            pe = epi.pre(r);
+        }
         double2 v[kPairs];
         int2 cc[kPairs];
 #pragma unroll
@@ -566,12 +587,10 @@ __global__ void __launch_bounds__(kBlock) k_csr_rows(Csr A, const double* __rest
             if (k + 1 >= s && k + 1 < e) prod[k + 1 - s] = v[j].y * x1[j];
         }
         __syncthreads();
-        const int32_t r = r0 + tid;
-        if (r < r1) {
-            const int32_t ks = A.rp[r] - s, ke = A.rp[r + 1] - s;
+        if (live) {
             double acc = 0.0;
             for (int32_t k = ks; k < ke; ++k) acc += prod[k];
-            epi(r, acc);
+            epi(r, acc, pe);
         }
     } else {
         // A single row longer than the LDS stage (the planner never groups such a row).
@@ -584,7 +603,92 @@ __global__ void __launch_bounds__(kBlock) k_csr_rows(Csr A, const double* __rest
             if (tid < w) prod[tid] += prod[tid + w];
             __syncthreads();
         }
-        if (tid == 0) epi(r0, prod[0]);
+        if (tid == 0) epi(r0, prod[0], epi.pre(r0));
+    }
+}
+
+// ------------------------------------------------------------------ SELL-64 ----
+// Sliced ELLPACK with one wavefront per slice: a slice is <= 64 consecutive rows, its entries
+// stored column-major in pairs -- pair-row j of the slice holds entries (2j, 2j+1) of every row,
+// one double2 / int2 per lane -- so each wave-instruction reads 1 KiB of values and 512 B of
+// column indices contiguously, and each lane owns one row: no LDS, no barrier, no reduction
+// across lanes.  Entries keep their CSR order, so row sums stay bit-exact with the oracle.
+// slices[s] = {row0, rows, width, first pair-row}; row_len[r] = CSR length of row r (< 256).
+struct Sell {
+    const int4* slices;
+    const uint8_t* rlen;
+    const double2* val;
+    const int2* col;
+};
+
+constexpr int kSellPairs = 8;   // rows of up to 16 entries take the fully unrolled path
+
+template <class Epi>
+__global__ void __launch_bounds__(kBlock) k_sell_rows(Sell S, const double* __restrict__ x, int nslices,
+                                                      Epi epi) {
+    const int b = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int sidx = b * (kBlock / 64) + (int)(threadIdx.x >> 6);
+    if (sidx >= nslices) return;
+    const int lane = threadIdx.x & 63;
+    const int4 sl = S.slices[sidx];
+    const int32_t r = sl.x + lane;
+    const bool live = lane < sl.y;
+    const int len = live ? (int)S.rlen[r] : 0;
+    typename Epi::P pe{};
+    if (live) pe = epi.pre(r);
+    const int np = (sl.z + 1) >> 1;
+    const double2* vp = S.val + (size_t)sl.w * 64 + lane;
+    const int2* cp = S.col + (size_t)sl.w * 64 + lane;
+    double acc = 0.0;
+    if (np <= kSellPairs) {
+        double2 v[kSellPairs];
+        int2 c[kSellPairs];
+#pragma unroll
+        for (int j = 0; j < kSellPairs; ++j) {
+            if (j < np) {
+                v[j] = vp[(size_t)j * 64];
+                c[j] = cp[(size_t)j * 64];
+            } else {
+                v[j] = make_double2(0.0, 0.0);
+                c[j] = make_int2(0, 0);
+            }
+        }
+        double x0[kSellPairs], x1[kSellPairs];
+#pragma unroll
+        for (int j = 0; j < kSellPairs; ++j) {
+            x0[j] = (2 * j < len) ? x[c[j].x] : 0.0;
+            x1[j] = (2 * j + 1 < len) ? x[c[j].y] : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < kSellPairs; ++j) {
+            if (2 * j < len) acc += v[j].x * x0[j];
+            if (2 * j + 1 < len) acc += v[j].y * x1[j];
+        }
+    } else {
+        for (int j = 0; 2 * j < len; ++j) {
+            const double2 vv = vp[(size_t)j * 64];
+            const int2 cc = cp[(size_t)j * 64];
+            acc += vv.x * x[cc.x];
+            if (2 * j + 1 < len) acc += vv.y * x[cc.y];
+        }
+    }
+    if (live) epi(r, acc, pe);
+}
+
+// One thread per (slice, lane): copy the CSR row into its column-major slots.
+__global__ void k_sell_fill(Csr A, const int4* slices, int nslices, uint8_t* rlen, double* val, int32_t* col) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int sidx = (int)(t >> 6), lane = (int)(t & 63);
+    if (sidx >= nslices) return;
+    const int4 sl = slices[sidx];
+    if (lane >= sl.y) return;
+    const int32_t r = sl.x + lane;
+    const int32_t k0 = A.rp[r], len = A.rp[r + 1] - k0;
+    rlen[r] = (uint8_t)len;
+    for (int k = 0; k < len; ++k) {
+        const size_t slot = ((size_t)sl.w + (k >> 1)) * 64 + lane;
+        val[2 * slot + (k & 1)] = A.va[k0 + k];
+        col[2 * slot + (k & 1)] = A.ci[k0 + k];
     }
 }
 
@@ -614,6 +718,19 @@ int launch_rows(const mpbp_csr* A, const mpbp_rowblocks* blk, const double* x, E
     k_csr_rows<Epi><<<blk->count, kBlock, 0, st>>>(to_csr(A), x,
                                                     reinterpret_cast<const int2*>(blk->pairs),
                                                     blk->count, epi);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+template <class Epi>
+int launch_sell(const mpbp_sell* S, const double* x, Epi epi, hipStream_t st) {
+    if (!S || S->nslices <= 0) return MPBP_OK;
+    const int slices_per_block = kBlock / 64;
+    const int grid = (S->nslices + slices_per_block - 1) / slices_per_block;
+    k_sell_rows<Epi><<<grid, kBlock, 0, st>>>(
+        Sell{reinterpret_cast<const int4*>(S->slices), S->row_len, reinterpret_cast<const double2*>(S->val),
+             reinterpret_cast<const int2*>(S->col)},
+        x, S->nslices, epi);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
@@ -950,6 +1067,88 @@ int mpbp_event_elapsed_ms(void* start, void* stop, float* ms) {
 
 }  // extern "C"
 
+// ============================================================== SELL ABI ====
+extern "C" {
+
+int64_t mpbp_sell_plan(const int32_t* row_ptr, const int32_t* ranges, int32_t nranges, int32_t* slices,
+                       int64_t capacity, int64_t* pair_rows) {
+    if (!row_ptr || nranges < 0 || (nranges && !ranges)) return set_error(MPBP_ERR_ARG, "sell_plan: bad args");
+    int64_t ns = 0, pr = 0;
+    for (int32_t q = 0; q < nranges; ++q) {
+        const int32_t a = ranges[2 * q], b = ranges[2 * q + 1];
+        if (a < 0 || b < a) return set_error(MPBP_ERR_ARG, "sell_plan: bad range");
+        for (int32_t r0 = a; r0 < b; r0 += 64) {
+            const int32_t rows = (b - r0) < 64 ? (b - r0) : 64;
+            int32_t w = 0;
+            for (int32_t r = r0; r < r0 + rows; ++r) {
+                const int32_t len = row_ptr[r + 1] - row_ptr[r];
+                if (len > 255) return set_error(MPBP_ERR_OVERFLOW, "sell_plan: row %d has %d > 255 entries", r, len);
+                w = len > w ? len : w;
+            }
+            if (slices && ns < capacity) {
+                slices[4 * ns] = r0;
+                slices[4 * ns + 1] = rows;
+                slices[4 * ns + 2] = w;
+                slices[4 * ns + 3] = (int32_t)pr;
+            }
+            pr += (w + 1) / 2;
+            if (pr > INT32_MAX) return set_error(MPBP_ERR_OVERFLOW, "sell_plan: too many pair rows");
+            ++ns;
+        }
+    }
+    if (pair_rows) *pair_rows = pr;
+    return ns;
+}
+
+int mpbp_sell_fill(const mpbp_csr* A, const int32_t* slices, int32_t nslices, uint8_t* row_len, double* val,
+                   int32_t* col, void* stream) {
+    int rc = check_csr(A);
+    if (rc) return rc;
+    if (nslices <= 0) return MPBP_OK;
+    if (!slices || !row_len || !val || !col) return set_error(MPBP_ERR_ARG, "sell_fill: bad args");
+    k_sell_fill<<<grid_for((int64_t)nslices * 64), kBlock, 0, as_stream(stream)>>>(
+        to_csr(A), reinterpret_cast<const int4*>(slices), nslices, row_len, val, col);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+static int check_sell(const mpbp_sell* S) {
+    if (!S || S->nslices < 0 || (S->nslices && (!S->slices || !S->row_len || !S->val || !S->col)))
+        return set_error(MPBP_ERR_ARG, "invalid sell matrix");
+    return MPBP_OK;
+}
+
+int mpbp_sell_spmv(const mpbp_sell* S, int32_t mode, const double* x, const double* z, double* y, void* stream) {
+    int rc = check_sell(S);
+    if (rc) return rc;
+    if (!x || !y || (mode != MPBP_SPMV_STORE && !z)) return set_error(MPBP_ERR_ARG, "sell_spmv: bad vectors");
+    const hipStream_t st = as_stream(stream);
+    switch (mode) {
+    case MPBP_SPMV_STORE: return launch_sell(S, x, EpiStore{y}, st);
+    case MPBP_SPMV_ADD: return launch_sell(S, x, EpiAdd{z, y}, st);
+    case MPBP_SPMV_RESID: return launch_sell(S, x, EpiResid{z, y}, st);
+    default: return set_error(MPBP_ERR_ARG, "sell_spmv: unknown mode %d", mode);
+    }
+}
+
+int mpbp_sell_jacobi_step(const mpbp_sell* S, const double* x_in, const double* b, const double* diag,
+                          const double* sub, double* x_out, void* stream) {
+    int rc = check_sell(S);
+    if (rc) return rc;
+    if (!x_in || !b || !diag || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "sell_jacobi_step: bad vectors");
+    return launch_sell(S, x_in, EpiJacobi{x_in, b, diag, sub, x_out}, as_stream(stream));
+}
+
+int mpbp_sell_cheb_step(const mpbp_sell* S, const double* x_in, const double* b, const double* diag, double c1,
+                        double c2, double* d, const double* sub, double* x_out, void* stream) {
+    int rc = check_sell(S);
+    if (rc) return rc;
+    if (!x_in || !b || !diag || !d || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "sell_cheb_step: bad vectors");
+    return launch_sell(S, x_in, EpiCheb{x_in, b, diag, d, c1, c2, sub, x_out}, as_stream(stream));
+}
+
+}  // extern "C"
+
 // ======================================================= Schur apply ====
 namespace {
 
@@ -958,24 +1157,54 @@ struct Ctx {
     hipStream_t st;
 };
 
-// Launch one sweep over interior blocks, then (after the halo is complete) boundary blocks.
+// One operator of the apply, restricted to interior or boundary rows, in CSR or SELL form.
+struct OpRef {
+    const mpbp_csr* csr;
+    const mpbp_rowblocks* blk;
+    const mpbp_sell* sell;
+};
+
+int op_spmv(const OpRef& o, int32_t mode, const double* x, const double* z, double* y, hipStream_t st) {
+    return o.sell ? mpbp_sell_spmv(o.sell, mode, x, z, y, (void*)st)
+                  : mpbp_spmv(o.csr, o.blk, mode, x, z, y, (void*)st);
+}
+int op_jacobi(const OpRef& o, const double* xin, const double* b, const double* dg, const double* sub, double* xo,
+              hipStream_t st) {
+    return o.sell ? mpbp_sell_jacobi_step(o.sell, xin, b, dg, sub, xo, (void*)st)
+                  : mpbp_jacobi_step(o.csr, o.blk, xin, b, dg, sub, xo, (void*)st);
+}
+int op_cheb(const OpRef& o, const double* xin, const double* b, const double* dg, double c1, double c2, double* d,
+            const double* sub, double* xo, hipStream_t st) {
+    return o.sell ? mpbp_sell_cheb_step(o.sell, xin, b, dg, c1, c2, d, sub, xo, (void*)st)
+                  : mpbp_cheb_step(o.csr, o.blk, xin, b, dg, c1, c2, d, sub, xo, (void*)st);
+}
+
+struct OpPair {
+    OpRef in, bd;
+};
+
+OpPair make_op(const mpbp_schur_plan* p, const mpbp_csr& A, const mpbp_rowblocks& bi, const mpbp_rowblocks& bb,
+               const mpbp_sell& si, const mpbp_sell& sb) {
+    if (p->use_sell) return OpPair{OpRef{&A, nullptr, &si}, OpRef{&A, nullptr, &sb}};
+    return OpPair{OpRef{&A, &bi, nullptr}, OpRef{&A, &bb, nullptr}};
+}
+
+// Launch one sweep over interior rows, then (after the halo is complete) boundary rows.
 template <class Fn>
-int two_phase(const Ctx& c, int32_t kind, const double* x_ext, const mpbp_rowblocks& bi,
-              const mpbp_rowblocks& bb, Fn&& launch) {
+int two_phase(const Ctx& c, int32_t kind, const double* x_ext, const OpPair& op, Fn&& launch) {
     const mpbp_schur_plan* p = c.p;
     if (p->halo) p->halo(p->halo_ctx, kind, const_cast<double*>(x_ext), MPBP_HALO_BEGIN, (void*)c.st);
-    int rc = launch(&bi);
+    int rc = launch(op.in);
     if (rc) return rc;
     if (p->halo) p->halo(p->halo_ctx, kind, const_cast<double*>(x_ext), MPBP_HALO_END, (void*)c.st);
-    return launch(&bb);
+    return launch(op.bd);
 }
 
 // x = M^-1 b by `inner` sweeps from x0 = 0 (solve.py:251/254 F_inv / Gt_G_factorization roles).
 // The final iterate goes to dst (sub - iterate when sub != NULL); ping/pong hold the others.
-int inner_solve(const Ctx& c, int32_t kind, const mpbp_csr& M, const mpbp_rowblocks& bi,
-                const mpbp_rowblocks& bb, const double* diag, const mpbp_inner_solver& in,
-                int32_t nrows, const double* b, double* dst, const double* sub, double* ping,
-                double* pong, double* dir, bool profile) {
+int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag, const mpbp_inner_solver& in,
+                int32_t nrows, const double* b, double* dst, const double* sub, double* ping, double* pong,
+                double* dir, bool profile) {
     const int K = in.sweeps;
     double c1[64], c2[64];
     if (K < 1 || K > 64) return set_error(MPBP_ERR_ARG, "inner sweeps must be in [1, 64]");
@@ -998,9 +1227,9 @@ int inner_solve(const Ctx& c, int32_t kind, const mpbp_csr& M, const mpbp_rowblo
         const mpbp_schur_plan* p = c.p;
         const bool rec = profile && p->prof_events && p->prof_count && *p->prof_count < p->prof_capacity;
         if (rec) MPBP_HIP(hipEventRecord((hipEvent_t)p->prof_events[2 * *p->prof_count], c.st));
-        rc = two_phase(c, kind, cur, bi, bb, [&](const mpbp_rowblocks* blk) {
-            return cheb ? mpbp_cheb_step(&M, blk, cur, b, diag, c1[s], c2[s], dir, sb, nxt, (void*)c.st)
-                        : mpbp_jacobi_step(&M, blk, cur, b, diag, sb, nxt, (void*)c.st);
+        rc = two_phase(c, kind, cur, op, [&](const OpRef& o) {
+            return cheb ? op_cheb(o, cur, b, diag, c1[s], c2[s], dir, sb, nxt, c.st)
+                        : op_jacobi(o, cur, b, diag, sb, nxt, c.st);
         });
         if (rc) return rc;
         if (rec) {
@@ -1022,6 +1251,11 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
         if (!p->wp[i]) return set_error(MPBP_ERR_ARG, "schur_apply: missing pressure workspace");
     if (!p->wu_owned || !p->diag_F || !p->diag_P) return set_error(MPBP_ERR_ARG, "schur_apply: missing operands");
     const Ctx c{p, as_stream(stream)};
+    const OpPair F = make_op(p, p->F, p->F_int, p->F_bnd, p->Fs_int, p->Fs_bnd);
+    const OpPair D = make_op(p, p->D, p->D_int, p->D_bnd, p->Ds_int, p->Ds_bnd);
+    const OpPair G = make_op(p, p->G, p->G_int, p->G_bnd, p->Gs_int, p->Gs_bnd);
+    const OpPair P = make_op(p, p->GtG, p->P_int, p->P_bnd, p->Ps_int, p->Ps_bnd);
+    const OpPair Q = make_op(p, p->GtFG, p->Q_int, p->Q_bnd, p->Qs_int, p->Qs_bnd);
     const double* v_u = v;
     const double* v_p = v + p->nu;
     double* out_u = out;
@@ -1031,34 +1265,27 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
     double *P0 = p->wp[4], *P1 = p->wp[5], *Pd = p->wp[6];
     int rc;
     // 1. Finv_v = F_inv @ v[:F.shape[1]]                                   solve.py:258
-    rc = inner_solve(c, MPBP_VEC_VELOCITY, p->F, p->F_int, p->F_bnd, p->diag_F, p->inner_F, p->nu, v_u, Y,
-                     nullptr, U0, U1, Ud, true);
+    rc = inner_solve(c, MPBP_VEC_VELOCITY, F, p->diag_F, p->inner_F, p->nu, v_u, Y, nullptr, U0, U1, Ud, true);
     if (rc) return rc;
     // 2. rhs_interim = D @ Finv_v + v[F.shape[1]:]                            solve.py:259
-    rc = two_phase(c, MPBP_VEC_VELOCITY, Y, p->D_int, p->D_bnd, [&](const mpbp_rowblocks* blk) {
-        return mpbp_spmv(&p->D, blk, MPBP_SPMV_ADD, Y, v_p, Prhs, (void*)c.st);
-    });
+    rc = two_phase(c, MPBP_VEC_VELOCITY, Y, D,
+                   [&](const OpRef& o) { return op_spmv(o, MPBP_SPMV_ADD, Y, v_p, Prhs, c.st); });
     if (rc) return rc;
     // 3. x_a = Gt_G_factorization @ rhs_interim                             solve.py:265
-    rc = inner_solve(c, MPBP_VEC_PRESSURE, p->GtG, p->P_int, p->P_bnd, p->diag_P, p->inner_P, p->np, Prhs, Pxa,
-                     nullptr, P0, P1, Pd, false);
+    rc = inner_solve(c, MPBP_VEC_PRESSURE, P, p->diag_P, p->inner_P, p->np, Prhs, Pxa, nullptr, P0, P1, Pd, false);
     if (rc) return rc;
     // 4. x_b = Gt_F_G @ x_a                                                solve.py:267
-    rc = two_phase(c, MPBP_VEC_PRESSURE, Pxa, p->Q_int, p->Q_bnd, [&](const mpbp_rowblocks* blk) {
-        return mpbp_spmv(&p->GtFG, blk, MPBP_SPMV_STORE, Pxa, nullptr, Pxb, (void*)c.st);
-    });
+    rc = two_phase(c, MPBP_VEC_PRESSURE, Pxa, Q,
+                   [&](const OpRef& o) { return op_spmv(o, MPBP_SPMV_STORE, Pxa, nullptr, Pxb, c.st); });
     if (rc) return rc;
     // 5. x_p = Gt_G_factorization @ x_b                                    solve.py:271
-    rc = inner_solve(c, MPBP_VEC_PRESSURE, p->GtG, p->P_int, p->P_bnd, p->diag_P, p->inner_P, p->np, Pxb, Pxp,
-                     nullptr, P0, P1, Pd, false);
+    rc = inner_solve(c, MPBP_VEC_PRESSURE, P, p->diag_P, p->inner_P, p->np, Pxb, Pxp, nullptr, P0, P1, Pd, false);
     if (rc) return rc;
     MPBP_HIP(hipMemcpyAsync(out_p, Pxp, sizeof(double) * (size_t)p->np, hipMemcpyDeviceToDevice, c.st));
     // 6. G_xp = G @ x_p                                                     solve.py:273
-    rc = two_phase(c, MPBP_VEC_PRESSURE, Pxp, p->G_int, p->G_bnd, [&](const mpbp_rowblocks* blk) {
-        return mpbp_spmv(&p->G, blk, MPBP_SPMV_STORE, Pxp, nullptr, W, (void*)c.st);
-    });
+    rc = two_phase(c, MPBP_VEC_PRESSURE, Pxp, G,
+                   [&](const OpRef& o) { return op_spmv(o, MPBP_SPMV_STORE, Pxp, nullptr, W, c.st); });
     if (rc) return rc;
     // 7. u = Finv_v - F_inv @ G_xp                                          solve.py:274-276
-    return inner_solve(c, MPBP_VEC_VELOCITY, p->F, p->F_int, p->F_bnd, p->diag_F, p->inner_F, p->nu, W, out_u,
-                       Y, U0, U1, Ud, true);
+    return inner_solve(c, MPBP_VEC_VELOCITY, F, p->diag_F, p->inner_F, p->nu, W, out_u, Y, U0, U1, Ud, true);
 }

@@ -67,7 +67,7 @@ class ApproxSchurPreconditioner(spla.LinearOperator):
     """
 
     def __init__(self, F, D, G, GtG=None, GtFG=None, inner_F: InnerSolver | None = None,
-                 inner_P: InnerSolver | None = None, device=None):
+                 inner_P: InnerSolver | None = None, device=None, layout: str = "sell"):
         dev = torch.device(device or (F.device if isinstance(F, DeviceCSR) else "cuda"))
         self.F, self.D, self.G = (_device_csr(M, dev) for M in (F, D, G))
         if GtG is None or GtFG is None:
@@ -88,6 +88,10 @@ class ApproxSchurPreconditioner(spla.LinearOperator):
         self._wu_owned = torch.empty(nu, **f64)
         self._wp = [torch.empty(np_, **f64) for _ in range(7)]
         self._prof = None
+        if layout not in ("sell", "csr"):
+            raise ValueError("layout must be 'sell' or 'csr'")
+        self.layout = layout
+        self._sell = [M.to_sell() for M in (self.F, self.D, self.G, self.GtG, self.GtFG)] if layout == "sell" else None
         self._plan = self._make_plan()
         super().__init__(dtype=np.float64, shape=(nu + np_, nu + np_))
 
@@ -109,6 +113,12 @@ class ApproxSchurPreconditioner(spla.LinearOperator):
         p.wu_owned = self._wu_owned.data_ptr()
         for i, t in enumerate(self._wp):
             p.wp[i] = t.data_ptr()
+        p.use_sell = 1 if self._sell else 0
+        if self._sell:
+            esell = _lib.Sell(0, 0, 0, 0, None, None, None, None)
+            for name, S in zip(("Fs", "Ds", "Gs", "Ps", "Qs"), self._sell):
+                setattr(p, name + "_int", S.cstruct())
+                setattr(p, name + "_bnd", esell)
         p.halo = _lib.HALO_FN()
         p.halo_ctx = None
         p.prof_events = None

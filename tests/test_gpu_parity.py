@@ -126,9 +126,35 @@ def test_spmv_bit_exact(n):
         dM = mp.DeviceCSR.from_scipy(M)
         x = rng.standard_normal(M.shape[1])
         z = rng.standard_normal(M.shape[0])
+        dS = dM.to_sell()
         for mode in (0, 1, 2):
+            ref = co.spmv(M, x, z, mode=mode)
             y = dM.matvec(_cuda(x), mode=mode, z=_cuda(z))
-            assert _bits_equal(y, co.spmv(M, x, z, mode=mode)), (M.shape, mode)
+            assert _bits_equal(y, ref), (M.shape, mode)
+            y = dS.matvec(_cuda(x), mode=mode, z=_cuda(z))
+            assert _bits_equal(y, ref), ("sell", M.shape, mode)
+
+
+def test_sell_ragged_rows_and_partial_slices():
+    """SELL-64 with ragged rows (0..40 entries, beyond the unrolled 16), partial slices, row ranges."""
+    mp = _mp()
+    from oracle import csr_oracle as co
+    rng = np.random.default_rng(11)
+    lengths = rng.integers(0, 41, size=1000)
+    lengths[:64] = 0
+    rows = np.repeat(np.arange(lengths.size), lengths)
+    M = sp.csr_matrix((rng.standard_normal(rows.size), (rows, rng.integers(0, 3000, size=rows.size))),
+                      shape=(lengths.size, 3000))
+    M.sum_duplicates()
+    x = rng.standard_normal(3000)
+    dM = mp.DeviceCSR.from_scipy(M)
+    ref = co.spmv(M, x)
+    assert _bits_equal(dM.to_sell().matvec(_cuda(x)), ref)
+    y = torch.full((M.shape[0],), 7.0, dtype=torch.float64, device="cuda")
+    dM.to_sell([(3, 100), (500, 1000)]).matvec(_cuda(x), out=y)
+    got = y.cpu().numpy()
+    sel = np.r_[3:100, 500:1000]
+    assert _bits_equal(got[sel], ref[sel]) and np.all(got[np.r_[0:3, 100:500]] == 7.0)
 
 
 def test_spmv_long_rows_and_empty_rows():
@@ -180,16 +206,18 @@ INNERS = [("jacobi", 1, "jacobi", 1), ("jacobi", 3, "jacobi", 2), ("chebyshev", 
           ("chebyshev", 6, "jacobi", 3)]
 
 
+@pytest.mark.parametrize("layout", ["sell", "csr"])
 @pytest.mark.parametrize("n", [3, 16, 64])
 @pytest.mark.parametrize("inner", INNERS, ids=lambda t: f"{t[0]}{t[1]}-{t[2]}{t[3]}")
-def test_schur_apply_bit_exact(n, inner):
+def test_schur_apply_bit_exact(n, inner, layout):
     """mpbp_schur_apply vs the oracle's restatement of approx_schur_op (solve.py:257-277)."""
     mp = _mp()
     from oracle.schur_oracle import Inner, approx_schur_apply, diagonal, gershgorin
     osys = _oracle_system(n, **PARAMS)
     kf, sf, kp, spp = inner
     pc = mp.ApproxSchurPreconditioner(osys.F, osys.D, osys.G, osys.GtG, osys.GtFG,
-                                      inner_F=mp.InnerSolver(kf, sf), inner_P=mp.InnerSolver(kp, spp))
+                                      inner_F=mp.InnerSolver(kf, sf), inner_P=mp.InnerSolver(kp, spp),
+                                      layout=layout)
     # the oracle uses the bounds the GPU computed (Gershgorin on the GPU sums in row order too)
     dF, dP = diagonal(osys.F), diagonal(osys.GtG)
     assert np.array_equal(pc.diag_F.cpu().numpy(), dF) and np.array_equal(pc.diag_P.cpu().numpy(), dP)
@@ -232,7 +260,10 @@ def test_full_size_properties():
     v2 = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda", generator=gen)
     y1, y2 = pc.apply(v1), pc.apply(v2)
     y12 = pc.apply(2.0 * v1 - 0.5 * v2)
-    assert rel_inf((y12 - (2.0 * y1 - 0.5 * y2)).cpu().numpy() + 0, (2.0 * y1 - 0.5 * y2).cpu().numpy()) <= 1e-12
+    assert rel_inf(y12.cpu().numpy(), (2.0 * y1 - 0.5 * y2).cpu().numpy()) <= 1e-12
+    pc_csr = mp.ApproxSchurPreconditioner(F, D, G, pc.GtG, pc.GtFG, inner_F=mp.InnerSolver("chebyshev", 4),
+                                          inner_P=mp.InnerSolver("chebyshev", 4), layout="csr")
+    assert torch.equal(pc_csr.apply(v1), y1)                                  # CSR == SELL bit for bit
     assert torch.equal(pc.apply(v1), y1)                                      # deterministic
     # manufactured solution: ||A u - b||_inf / ||b||_inf is a truncation error, O(h^2)
     u, b = mp.manufactured_problem(n, 1.0, -1.0, 1.0, 100.0, 1.0)
