@@ -4,15 +4,19 @@ configs[2]) on MI355X, with the roofline of the dominant kernel and the CPU orac
 One step = one application of the approximate-commutator block preconditioner (solve.py:257-277,
 ``mpbp_schur_apply``) to a resident random vector of 5 n^2 doubles.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 1024] ...
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 1024] [--strong] ...
 
-N > 1 is launched by torch.distributed.run (one rank per GPU); see DESIGN.md for how the work is
-split.  Rank 0 prints ONE JSON line.
+N > 1 is launched by torch.distributed.run (one rank per GPU, RCCL).  The grid is row-partitioned
+over the ranks with halo all-gathers between sweeps.  Default is weak scaling: the global grid is
+n_N = round(n * sqrt(N)) so every GPU holds ~n^2 cells, and `value` counts applies of the global
+system scaled to 1024^2-cell equivalents (n_N^2 / 1024^2 per apply; exactly applies/s at N = 1).
+--strong keeps the global grid at n.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -28,12 +32,26 @@ def parse_inner(s):
     return kind, int(k or 4)
 
 
+def sweep_bytes(pc, layout):
+    """Algorithmic bytes of one F Chebyshev sweep on this rank: every entry's value (8 B) and column
+    (4 B), the per-row index data (SELL: 1 B length; CSR: 4 B row_ptr), the six row vectors
+    (x_in, b, diag, d read + d write, x_out) and the slice / row-block descriptors."""
+    F = pc.F
+    nF, nnzF = F.shape[0], F.nnz
+    if layout == "sell":
+        nsl = pc.sell_of("F").nslices
+        return nnzF * 12 + nF * 1 + nF * 8 * 6 + nsl * 16, "k_sell_rows<EpiCheb> (F Chebyshev sweep, SELL-64)"
+    return (nnzF * 12 + (nF + 1) * 4 + nF * 8 * 6 + F.blocks.count * 8,
+            "k_csr_rows<EpiCheb> (F Chebyshev sweep, CSR)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--strong", action="store_true", help="keep the global grid at n for every N")
     ap.add_argument("--xi", type=float, default=1.0)
     ap.add_argument("--eta-n", type=float, default=100.0)
     ap.add_argument("--eta-s", type=float, default=1.0)
@@ -42,9 +60,9 @@ def main():
     ap.add_argument("--layout", default="sell", choices=["sell", "csr"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-spmv", action="store_true")
     args = ap.parse_args()
 
-    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -57,13 +75,20 @@ def main():
 
     import mp_block_preconditioners_amd as mp
 
-    n = args.n
+    n = args.n if (world == 1 or args.strong) else int(round(args.n * math.sqrt(world)))
     kf, sf = parse_inner(args.inner_f)
     kp, spp = parse_inner(args.inner_p)
-    bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
-    A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
-    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver(kf, sf), inner_P=mp.InnerSolver(kp, spp),
-                                      layout=args.layout)
+    iF, iP = mp.InnerSolver(kf, sf), mp.InnerSolver(kp, spp)
+    A = None
+    if world == 1:
+        bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
+        A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+        pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, layout=args.layout)
+        del F, D, G
+    else:
+        from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
+        pc = DistributedSchurPreconditioner(n, args.xi, args.eta_n, args.eta_s, inner_F=iF, inner_P=iP,
+                                            layout=args.layout)
     gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
     v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda", generator=gen)
     out = torch.empty_like(v)
@@ -91,45 +116,14 @@ def main():
     sweep_ms = pc.profiled_ms()
     pc.disable_profiling()
 
-    # dominant kernel: the fused Chebyshev-Jacobi sweep over F (k_sell_rows / k_csr_rows <EpiCheb>)
-    # algorithmic bytes: matrix entries (8 B value + 4 B column) + per-row index data + x, b, diag,
-    # d (read + write) and x_out (8 B each per row) + the row-block / slice descriptors
-    nF, nnzF = F.shape[0], F.nnz
-    if args.layout == "sell":
-        S = pc._sell[0]
-        sweep_bytes = nnzF * (8 + 4) + nF * 1 + nF * 8 * (1 + 1 + 1 + 2 + 1) + S.nslices * 16
-        kname = "k_sell_rows<EpiCheb> (F Chebyshev sweep, SELL-64)"
-    else:
-        sweep_bytes = nnzF * (8 + 4) + (nF + 1) * 4 + nF * 8 * (1 + 1 + 1 + 2 + 1) + F.blocks.count * 8
-        kname = "k_csr_rows<EpiCheb> (F Chebyshev sweep, CSR)"
+    # dominant kernel: the fused Chebyshev-Jacobi sweep over F
+    sbytes, kname = sweep_bytes(pc, args.layout)
     avg_sweep_s = (sum(sweep_ms) / len(sweep_ms) / 1e3) if sweep_ms else float("nan")
-    achieved = sweep_bytes / avg_sweep_s / 1e9
+    achieved = sbytes / avg_sweep_s / 1e9
 
-    # the plain A SpMV (apply.py:72) on the same device, for reference
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    x = torch.randn(A.shape[1], dtype=torch.float64, device="cuda", generator=gen)
-    y = torch.empty(A.shape[0], dtype=torch.float64, device="cuda")
-    for _ in range(3):
-        A.matvec(x, out=y)
-    ev[0].record()
-    reps = 20
-    for _ in range(reps):
-        A.matvec(x, out=y)
-    ev[1].record()
-    torch.cuda.synchronize()
-    spmv_s = ev[0].elapsed_time(ev[1]) / 1e3 / reps
-    spmv_bytes = A.nnz * 12 + (A.shape[0] + 1) * 4 + (A.shape[0] + A.shape[1]) * 8 + A.blocks.count * 8
-    AS = A.to_sell()
-    for _ in range(3):
-        AS.matvec(x, out=y)
-    ev[0].record()
-    for _ in range(reps):
-        AS.matvec(x, out=y)
-    ev[1].record()
-    torch.cuda.synchronize()
-    sell_s = ev[0].elapsed_time(ev[1]) / 1e3 / reps
-    sell_bytes = A.nnz * 12 + A.shape[0] * 1 + (A.shape[0] + A.shape[1]) * 8 + AS.nslices * 16
-    del AS
+    spmv = None
+    if A is not None and not args.no_spmv:
+        spmv = spmv_bench(A, gen)
 
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -137,44 +131,41 @@ def main():
         try:
             with open(pmc_path) as f:
                 pm = json.load(f)
-            if int(pm.get("n", -1)) == n:
+            if int(pm.get("n", -1)) == n and pm.get("layout") == args.layout:
                 traffic = pm.get("cheb_F_sweep_bytes")
         except (OSError, ValueError):
             traffic = None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(F, D, G, pc, v, args.cpu_seconds, kf, sf, kp, spp)
+        cpu = cpu_baseline(pc, v, args.cpu_seconds, kf, sf, kp, spp)
 
     if rank == 0:
-        value = world * args.steps / dt
+        scale = n * n / float(1024 * 1024)
+        value = args.steps / dt * (1.0 if args.strong else scale)
         line = {
             "metric": "precond-applies/sec",
             "value": value,
-            "unit": "applies/s",
+            "unit": "applies/s" if (world == 1 or args.strong) else "applies/s (1024^2-cell equivalents)",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: reference operator (thn = 0.25 sin sin + 0.5), random input vector",
             "config": {"workload": f"{n}x{n} MAC grid, approx-commutator Schur preconditioner apply "
-                                   "(BASELINE configs[2])",
-                       "n": n, "unknowns": int(pc.shape[0]), "xi": args.xi, "eta_n": args.eta_n,
+                                   "(BASELINE configs[2]" + (")" if world == 1 else ", row-partitioned)"),
+                       "n": n, "unknowns": 5 * n * n, "xi": args.xi, "eta_n": args.eta_n,
                        "eta_s": args.eta_s, "inner_F": f"{kf}:{sf}", "inner_P": f"{kp}:{spp}",
-                       "parallelism": "replicas" if world > 1 else "single",
-                       "layout": args.layout},
+                       "parallelism": f"rows{world}" if world > 1 else "single", "layout": args.layout},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": kname,
-                         "bytes_per_launch": sweep_bytes, "avg_launch_us": avg_sweep_s * 1e6,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
+                         "bytes_per_launch": sbytes, "avg_launch_us": avg_sweep_s * 1e6,
                          "launches_timed": len(sweep_ms)},
-            "spmv_A": {"csr_gbs": spmv_bytes / spmv_s / 1e9, "csr_us": spmv_s * 1e6, "nnz": A.nnz,
-                       "csr_bytes": spmv_bytes, "sell_gbs": sell_bytes / sell_s / 1e9, "sell_us": sell_s * 1e6,
-                       "sell_bytes": sell_bytes},
+            "spmv_A": spmv,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -182,11 +173,34 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(F, D, G, pc, v, seconds, kf, sf, kp, spp):
+def spmv_bench(A, gen, reps=20):
+    """The plain operator matvec b = A u (apply.py:72) in both layouts, HIP-event timed."""
+    import torch
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    x = torch.randn(A.shape[1], dtype=torch.float64, device="cuda", generator=gen)
+    y = torch.empty(A.shape[0], dtype=torch.float64, device="cuda")
+    res = {"nnz": A.nnz}
+    AS = A.to_sell()
+    for name, M, nbytes in (
+            ("csr", A, A.nnz * 12 + (A.shape[0] + 1) * 4 + (A.shape[0] + A.shape[1]) * 8 + A.blocks.count * 8),
+            ("sell", AS, A.nnz * 12 + A.shape[0] + (A.shape[0] + A.shape[1]) * 8 + AS.nslices * 16)):
+        for _ in range(3):
+            M.matvec(x, out=y)
+        ev[0].record()
+        for _ in range(reps):
+            M.matvec(x, out=y)
+        ev[1].record()
+        torch.cuda.synchronize()
+        s = ev[0].elapsed_time(ev[1]) / 1e3 / reps
+        res.update({f"{name}_gbs": nbytes / s / 1e9, f"{name}_us": s * 1e6, f"{name}_bytes": nbytes})
+    return res
+
+
+def cpu_baseline(pc, v, seconds, kf, sf, kp, spp):
     """The oracle's apply (sequential C, one core) on the same matrices, bounded sample."""
     import numpy as np
     from oracle.schur_oracle import Inner, approx_schur_apply
-    Fh, Dh, Gh = F.to_scipy(), D.to_scipy(), G.to_scipy()
+    Fh, Dh, Gh = pc.F.to_scipy(), pc.D.to_scipy(), pc.G.to_scipy()
     GtGh, GtFGh = pc.GtG.to_scipy(), pc.GtFG.to_scipy()
     iF = Inner(kf, sf, pc.inner_F.lmin or 0.0, pc.inner_F.lmax or 0.0)
     iP = Inner(kp, spp, pc.inner_P.lmin or 0.0, pc.inner_P.lmax or 0.0)

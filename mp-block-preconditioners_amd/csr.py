@@ -123,6 +123,19 @@ class DeviceCSR:
         check(lib().mpbp_gershgorin(ctypes.byref(self.cstruct()), ptr(diag), ctypes.byref(out), stream_handle()))
         return out.value
 
+    def extract(self, rows: torch.Tensor, colmap: torch.Tensor, ncols_local: int) -> "DeviceCSR":
+        """Rows `rows` (global ids, device int32) with columns renumbered by `colmap` (device int32,
+        global col -> local col or -1).  Entry order within a row is kept, so local row sums equal
+        the global ones bit for bit.  Raises if a kept entry's column is unmapped."""
+        nloc = rows.numel()
+        row_nnz = torch.empty(max(nloc, 1), dtype=torch.int32, device=self.device)[:nloc]
+        check(lib().mpbp_csr_extract_count(ctypes.byref(self.cstruct()), ptr(rows), nloc, ptr(row_nnz),
+                                           stream_handle()))
+        rp, ci, va = csr_from_row_nnz(row_nnz, (nloc, ncols_local), self.device)
+        check(lib().mpbp_csr_extract_fill(ctypes.byref(self.cstruct()), ptr(rows), nloc, ptr(colmap), ptr(rp),
+                                          ptr(ci), ptr(va), stream_handle()))
+        return DeviceCSR(rp, ci, va, (nloc, ncols_local))
+
     def to_sell(self, ranges=None):
         """SELL-64 copy of the rows in `ranges` (list of [a, b) row ranges; default all rows)."""
         return DeviceSELL.from_csr(self, ranges)

@@ -1,0 +1,289 @@
+"""Row partition of the MAC grid over ranks (one process per GPU) with halo exchange over RCCL.
+
+Every field (u_n, v_n, u_s, v_s, p) is an n x n grid stored row-major; rank k owns grid rows
+[r0, r1) of every field.  A rank's vector is laid out "owned first, then ghosts":
+
+    owned:  field-major, f * L*n + (gr - r0)*n + c                  (L = r1 - r0)
+    ghosts: per field f, h rows above (r0-h .. r0-1) then h rows below (r1 .. r1+h-1), periodic
+
+Matrices keep their global row order inside a rank and have their columns renumbered into that
+layout (``DeviceCSR.extract``), so every local row sum is the global one, bit for bit.  Before a
+sweep reads a vector, ``HaloExchanger.begin`` packs the rank's top/bottom h owned rows of every
+field and posts one all-gather; rows that touch no ghost (the interior) are computed meanwhile;
+``end`` waits for the collective, copies the neighbours' strips into the ghost slots, and the
+boundary rows run.  The halo depth h of each vector kind is measured from the matrices that read
+it (F, D read velocity: h = 1; G, Gt_G, Gt_F_G read pressure: h = 2 for Gt_F_G).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr, stream_handle
+from .csr import DeviceCSR
+from .solve import PlanProfiling
+
+N_VEL_FIELDS = 4
+N_P_FIELDS = 1
+
+
+@dataclass
+class RowPartition:
+    n: int
+    world: int
+    rank: int
+
+    def __post_init__(self):
+        base, rem = divmod(self.n, self.world)
+        self.r0 = self.rank * base + min(self.rank, rem)
+        self.L = base + (1 if self.rank < rem else 0)
+        self.r1 = self.r0 + self.L
+        self.min_rows = base
+
+    @property
+    def N(self):
+        return self.n * self.n
+
+    def n_owned(self, nfields):
+        return nfields * self.L * self.n
+
+    def n_ext(self, nfields, h):
+        return self.n_owned(nfields) + (nfields * 2 * h * self.n if self.world > 1 else 0)
+
+    def owned_rows(self, nfields) -> np.ndarray:
+        """Global ids (in a field-major vector of nfields fields) of the owned unknowns, local order."""
+        n, N = self.n, self.N
+        return np.concatenate([f * N + np.arange(self.r0 * n, self.r1 * n, dtype=np.int64) for f in range(nfields)])
+
+    def colmap(self, nfields, h) -> np.ndarray:
+        """Global column -> local ext index (-1 where the rank holds no copy)."""
+        n, N, L = self.n, self.N, self.L
+        cm = np.full(nfields * N, -1, dtype=np.int32)
+        own = self.n_owned(nfields)
+        if self.world > 1:
+            if self.min_rows < h:
+                raise ValueError(f"halo depth {h} exceeds the {self.min_rows} grid rows of the smallest rank")
+            cols = np.arange(n, dtype=np.int64)
+            for f in range(nfields):
+                g0 = own + f * 2 * h * n
+                for j in range(h):
+                    top = (self.r0 - h + j) % n
+                    bot = (self.r1 + j) % n
+                    cm[f * N + top * n + cols] = g0 + j * n + cols
+                    cm[f * N + bot * n + cols] = g0 + h * n + j * n + cols
+        for f in range(nfields):
+            cm[f * N + self.r0 * n: f * N + self.r1 * n] = f * L * n + np.arange(L * n, dtype=np.int32)
+        return cm
+
+
+def halo_reach(row_ptr: torch.Tensor, col_idx: torch.Tensor, row_gid: torch.Tensor, n: int) -> int:
+    """Largest periodic grid-row distance between a row and the columns it reads."""
+    N = n * n
+    counts = (row_ptr[1:] - row_ptr[:-1]).to(torch.int64)
+    if col_idx.numel() == 0:
+        return 0
+    rgr = torch.repeat_interleave((row_gid.to(torch.int64) % N) // n, counts)
+    cgr = (col_idx.to(torch.int64) % N) // n
+    d = torch.remainder(cgr - rgr, n)
+    return int(torch.minimum(d, n - d).max().item())
+
+
+def boundary_ranges(row_ptr: torch.Tensor, col_idx: torch.Tensor, n_owned_cols: int):
+    """(interior, boundary) lists of [a, b) row ranges: a boundary row reads a ghost column."""
+    nrows = row_ptr.numel() - 1
+    counts = (row_ptr[1:] - row_ptr[:-1]).to(torch.int64)
+    rows = torch.repeat_interleave(torch.arange(nrows, device=col_idx.device), counts)
+    flag = torch.zeros(nrows, dtype=torch.bool, device=col_idx.device)
+    flag[rows[col_idx.to(torch.int64) >= n_owned_cols]] = True
+    f = flag.cpu().numpy().astype(np.int8)
+    edges = np.flatnonzero(np.diff(np.concatenate([[-1], f, [-1]])) != 0)
+    inner, bnd = [], []
+    for a, b in zip(edges[:-1], edges[1:]):
+        (bnd if f[a] else inner).append((int(a), int(b)))
+    return inner, bnd
+
+
+class HaloExchanger:
+    """All-gather of every rank's top/bottom h owned rows per field; ghosts filled from neighbours."""
+
+    def __init__(self, part: RowPartition, nfields: int, h: int, device, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.part, self.nf, self.h, self.group = part, nfields, h, group
+        self.hn = h * part.n
+        self.device = torch.device(device)
+        backend = dist.get_backend(group)
+        self.stage_cpu = backend != "nccl" and self.device.type != "cpu"
+        bdev = torch.device("cpu") if self.stage_cpu else self.device
+        self.send = torch.empty(nfields * 2 * self.hn, dtype=torch.float64, device=bdev)
+        self.recv = torch.empty(part.world * nfields * 2 * self.hn, dtype=torch.float64, device=bdev)
+        self.use_base = backend == "nccl"
+        self.work = None
+
+    def _pack(self, x_ext):
+        own = x_ext[: self.part.n_owned(self.nf)].view(self.nf, self.part.L * self.part.n)
+        s = (torch.empty(self.nf, 2, self.hn, dtype=torch.float64, device=x_ext.device)
+             if self.stage_cpu else self.send.view(self.nf, 2, self.hn))
+        s[:, 0] = own[:, : self.hn]
+        s[:, 1] = own[:, own.shape[1] - self.hn:]
+        if self.stage_cpu:
+            self.send.copy_(s.reshape(-1))
+
+    def begin(self, x_ext: torch.Tensor):
+        self._pack(x_ext)
+        if self.use_base:
+            self.work = self.dist.all_gather_into_tensor(self.recv, self.send, group=self.group, async_op=True)
+        else:
+            chunks = list(self.recv.view(self.part.world, -1).unbind(0))
+            self.work = self.dist.all_gather(chunks, self.send, group=self.group, async_op=True)
+
+    def end(self, x_ext: torch.Tensor):
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+        k, W = self.part.rank, self.part.world
+        R = self.recv.view(W, self.nf, 2, self.hn)
+        g = x_ext[self.part.n_owned(self.nf): self.part.n_ext(self.nf, self.h)].view(self.nf, 2, self.hn)
+        g[:, 0] = R[(k - 1) % W, :, 1].to(g.device, non_blocking=True)
+        g[:, 1] = R[(k + 1) % W, :, 0].to(g.device, non_blocking=True)
+
+    def exchange(self, x_ext):
+        self.begin(x_ext)
+        self.end(x_ext)
+
+
+class DistributedSchurPreconditioner(PlanProfiling):
+    """The approximate-commutator apply over a row partition of the grid (one rank per GPU).
+
+    Every rank assembles the global operators in its own HBM (setup only), keeps its rows with
+    columns renumbered into the owned+ghost layout, and runs ``mpbp_schur_apply`` with halo
+    callbacks; v and the result hold the rank's owned unknowns [u_n, v_n, u_s, v_s, p] rows r0..r1.
+    """
+
+    def __init__(self, n, xi, eta_n, eta_s, c=1.0, d_u=-1.0, inner_F=None, inner_P=None, group=None,
+                 device=None, layout="sell"):
+        import torch.distributed as dist
+        from .preconditioner import MultiphaseBlockPreconditioner
+        from .solve import InnerSolver
+        dev = torch.device(device or "cuda")
+        self.device = dev
+        world = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        self.part = part = RowPartition(n, world, rank)
+        bp = MultiphaseBlockPreconditioner(n, xi, eta_n, eta_s, device=dev)
+        _, _, F, D, G = bp.get_big_A_matrix(c=c, d_u=d_u)
+        GtG, GtFG = bp.commutator_products(F, D, G)
+        # inner-solver bounds from the global operators: identical on every rank
+        self.inner_F = (inner_F or InnerSolver()).resolve(F, F.diagonal())
+        self.inner_P = (inner_P or InnerSolver()).resolve(GtG, GtG.diagonal())
+        rows_u = torch.from_numpy(part.owned_rows(N_VEL_FIELDS).astype(np.int32)).to(dev)
+        rows_p = torch.from_numpy(part.owned_rows(N_P_FIELDS).astype(np.int32)).to(dev)
+
+        def reach(M, rows):
+            sub = M.extract(rows, torch.arange(M.shape[1], dtype=torch.int32, device=dev), M.shape[1])
+            return halo_reach(sub.row_ptr, sub.col_idx, rows, n)
+
+        self.h_u = max(1, reach(F, rows_u), reach(D, rows_p))
+        self.h_p = max(1, reach(G, rows_u), reach(GtG, rows_p), reach(GtFG, rows_p))
+        nu, np_ = part.n_owned(N_VEL_FIELDS), part.n_owned(N_P_FIELDS)
+        nu_ext, np_ext = part.n_ext(N_VEL_FIELDS, self.h_u), part.n_ext(N_P_FIELDS, self.h_p)
+        cm_u = torch.from_numpy(part.colmap(N_VEL_FIELDS, self.h_u)).to(dev)
+        cm_p = torch.from_numpy(part.colmap(N_P_FIELDS, self.h_p)).to(dev)
+        self.F = F.extract(rows_u, cm_u, nu_ext)
+        self.D = D.extract(rows_p, cm_u, nu_ext)
+        self.G = G.extract(rows_u, cm_p, np_ext)
+        self.GtG = GtG.extract(rows_p, cm_p, np_ext)
+        self.GtFG = GtFG.extract(rows_p, cm_p, np_ext)
+        del F, D, G, GtG, GtFG, bp
+        torch.cuda.empty_cache()
+        self.nu, self.np, self.nu_ext, self.np_ext = nu, np_, nu_ext, np_ext
+        self.shape = (nu + np_, nu + np_)
+        self.diag_F = self.F.diagonal()
+        self.diag_P = self.GtG.diagonal()
+
+        mats = {"F": (self.F, nu), "D": (self.D, nu), "G": (self.G, np_), "P": (self.GtG, np_),
+                "Q": (self.GtFG, np_)}
+        self._pieces = {}
+        self.layout = layout
+        for key, (M, n_own_cols) in mats.items():
+            inner, bnd = boundary_ranges(M.row_ptr, M.col_idx, n_own_cols) if world > 1 else \
+                ([(0, M.shape[0])], [])
+            if layout == "sell":
+                S = M.to_sell(inner + bnd)
+                n_in = sum((b - a + 63) // 64 for a, b in inner)
+                self._pieces[key] = (S, S.sub(0, n_in), S.sub(n_in, S.nslices - n_in))
+            else:
+                self._pieces[key] = (M.plan_blocks(rows=inner) if inner else None,
+                                     M.plan_blocks(rows=bnd) if bnd else None)
+        f64 = dict(dtype=torch.float64, device=dev)
+        self._wu = [torch.zeros(nu_ext, **f64) for _ in range(4)]
+        self._wu_owned = torch.zeros(nu, **f64)
+        self._wp = [torch.zeros(np_ext, **f64) for _ in range(7)]
+        self._tensors = {t.data_ptr(): t for t in self._wu + self._wp}
+        self._ex = {_lib.VEC_VELOCITY: HaloExchanger(part, N_VEL_FIELDS, self.h_u, dev, group),
+                    _lib.VEC_PRESSURE: HaloExchanger(part, N_P_FIELDS, self.h_p, dev, group)}
+        self._cb = _lib.HALO_FN(self._halo)
+        self._prof = None
+        self._plan = self._make_plan(world)
+
+    def _halo(self, ctx, kind, x_ptr, phase, stream):
+        x = self._tensors[int(x_ptr)]
+        ex = self._ex[int(kind)]
+        if phase == _lib.HALO_BEGIN:
+            ex.begin(x)
+        else:
+            ex.end(x)
+
+    def _make_plan(self, world):
+        p = _lib.SchurPlan()
+        p.nu, p.np, p.nu_ext, p.np_ext = self.nu, self.np, self.nu_ext, self.np_ext
+        p.F, p.D, p.G = self.F.cstruct(), self.D.cstruct(), self.G.cstruct()
+        p.GtG, p.GtFG = self.GtG.cstruct(), self.GtFG.cstruct()
+        empty_b = _lib.RowBlocks(None, 0)
+        empty_s = _lib.Sell(0, 0, 0, 0, None, None, None, None)
+        p.use_sell = 1 if self.layout == "sell" else 0
+        for key in "FDGPQ":
+            piece = self._pieces[key]
+            if self.layout == "sell":
+                setattr(p, key + "s_int", piece[1].cstruct())
+                setattr(p, key + "s_bnd", piece[2].cstruct())
+                setattr(p, key + "_int", empty_b)
+                setattr(p, key + "_bnd", empty_b)
+            else:
+                setattr(p, key + "_int", piece[0].cstruct() if piece[0] else empty_b)
+                setattr(p, key + "_bnd", piece[1].cstruct() if piece[1] else empty_b)
+                setattr(p, key + "s_int", empty_s)
+                setattr(p, key + "s_bnd", empty_s)
+        p.diag_F, p.diag_P = self.diag_F.data_ptr(), self.diag_P.data_ptr()
+        p.inner_F, p.inner_P = self.inner_F.cstruct(), self.inner_P.cstruct()
+        for i, t in enumerate(self._wu):
+            p.wu[i] = t.data_ptr()
+        p.wu_owned = self._wu_owned.data_ptr()
+        for i, t in enumerate(self._wp):
+            p.wp[i] = t.data_ptr()
+        p.halo = self._cb if world > 1 else _lib.HALO_FN()
+        p.halo_ctx = None
+        p.prof_events = None
+        p.prof_capacity = 0
+        p.prof_count = ctypes.POINTER(ctypes.c_int32)()
+        return p
+
+    def sell_of(self, key):
+        """The SELL-64 copy (interior + boundary slices) of F / D / G / P / Q, or None (CSR layout)."""
+        return self._pieces[key][0] if self.layout == "sell" else None
+
+    def apply(self, v: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        assert v.is_cuda and v.dtype == torch.float64 and v.numel() == self.nu + self.np
+        if out is None:
+            out = torch.empty_like(v)
+        check(lib().mpbp_schur_apply(ctypes.byref(self._plan), ptr(v), ptr(out), stream_handle()))
+        return out
+
+    def local_to_global_rows(self):
+        """Global ids (in the [u_n, v_n, u_s, v_s, p] numbering) of this rank's v / out entries."""
+        return np.concatenate([self.part.owned_rows(N_VEL_FIELDS),
+                               4 * self.part.N + self.part.owned_rows(N_P_FIELDS)])

@@ -59,7 +59,49 @@ def _device_csr(M, device):
     return M if isinstance(M, DeviceCSR) else DeviceCSR.from_scipy(M, device)
 
 
-class ApproxSchurPreconditioner(spla.LinearOperator):
+class PlanProfiling:
+    """hipEvent pairs recorded by mpbp_schur_apply around every inner-F SpMV sweep (bench.py)."""
+
+    def enable_profiling(self, capacity: int):
+        evs = (ctypes.c_void_p * (2 * capacity))()
+        for i in range(2 * capacity):
+            e = ctypes.c_void_p()
+            check(lib().mpbp_event_create(ctypes.byref(e)))
+            evs[i] = e
+        cnt = ctypes.c_int32(0)
+        self._prof = (evs, cnt, capacity)
+        self._plan.prof_events = ctypes.cast(evs, ctypes.c_void_p)
+        self._plan.prof_capacity = capacity
+        self._plan.prof_count = ctypes.pointer(cnt)
+
+    def reset_profiling(self):
+        if self._prof:
+            self._prof[1].value = 0
+
+    def profiled_ms(self):
+        """Durations (ms) of the recorded inner-F sweeps (call after synchronising)."""
+        if not self._prof:
+            return []
+        evs, cnt, _ = self._prof
+        out = []
+        for i in range(cnt.value):
+            ms = ctypes.c_float(0.0)
+            check(lib().mpbp_event_elapsed_ms(evs[2 * i], evs[2 * i + 1], ctypes.byref(ms)))
+            out.append(ms.value)
+        return out
+
+    def disable_profiling(self):
+        if self._prof:
+            evs, _, cap = self._prof
+            for i in range(2 * cap):
+                lib().mpbp_event_destroy(evs[i])
+        self._prof = None
+        self._plan.prof_events = None
+        self._plan.prof_capacity = 0
+        self._plan.prof_count = ctypes.POINTER(ctypes.c_int32)()
+
+
+class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
     """M^-1 of the block upper-triangular approximate-commutator preconditioner (solve.py:257-277).
 
     ``apply(v, out)`` works on CUDA tensors and is graph-capturable; ``matvec`` (the scipy
@@ -126,44 +168,9 @@ class ApproxSchurPreconditioner(spla.LinearOperator):
         p.prof_count = ctypes.POINTER(ctypes.c_int32)()
         return p
 
-    # -- profiling hook: hipEvent pairs around every inner-F SpMV sweep ------------------------------
-    def enable_profiling(self, capacity: int):
-        evs = (ctypes.c_void_p * (2 * capacity))()
-        for i in range(2 * capacity):
-            e = ctypes.c_void_p()
-            check(lib().mpbp_event_create(ctypes.byref(e)))
-            evs[i] = e
-        cnt = ctypes.c_int32(0)
-        self._prof = (evs, cnt, capacity)
-        self._plan.prof_events = ctypes.cast(evs, ctypes.c_void_p)
-        self._plan.prof_capacity = capacity
-        self._plan.prof_count = ctypes.pointer(cnt)
-
-    def reset_profiling(self):
-        if self._prof:
-            self._prof[1].value = 0
-
-    def profiled_ms(self):
-        """Durations (ms) of the recorded inner-F sweeps (call after synchronising)."""
-        if not self._prof:
-            return []
-        evs, cnt, _ = self._prof
-        out = []
-        for i in range(cnt.value):
-            ms = ctypes.c_float(0.0)
-            check(lib().mpbp_event_elapsed_ms(evs[2 * i], evs[2 * i + 1], ctypes.byref(ms)))
-            out.append(ms.value)
-        return out
-
-    def disable_profiling(self):
-        if self._prof:
-            evs, _, cap = self._prof
-            for i in range(2 * cap):
-                lib().mpbp_event_destroy(evs[i])
-        self._prof = None
-        self._plan.prof_events = None
-        self._plan.prof_capacity = 0
-        self._plan.prof_count = ctypes.POINTER(ctypes.c_int32)()
+    def sell_of(self, key):
+        """The SELL-64 copy of F / D / G / P (Gt_G) / Q (Gt_F_G), or None in the CSR layout."""
+        return self._sell["FDGPQ".index(key)] if self._sell else None
 
     # -- the apply ---------------------------------------------------------------------------------
     def apply(self, v: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
