@@ -50,7 +50,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--grid", "--grid-n", dest="n", type=int, default=1024, help="grid size n (n x n cells)")
     ap.add_argument("--strong", action="store_true", help="keep the global grid at n for every N")
     ap.add_argument("--xi", type=float, default=1.0)
     ap.add_argument("--eta-n", type=float, default=100.0)
@@ -69,9 +69,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # MPBP_BENCH_BACKEND=gloo rehearses the N > 1 path with several ranks on one GPU (ghosts staged
+    # through host memory); the measured configuration is RCCL ("nccl"), one GPU per rank.
+    backend = os.environ.get("MPBP_BENCH_BACKEND", "nccl")
+    dev_index = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(backend)
 
     import mp_block_preconditioners_amd as mp
 

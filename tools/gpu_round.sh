@@ -1,5 +1,6 @@
 #!/bin/bash
-# One GPU session: parity tests, smoke, bench (both layouts), rocprofv3 kernel stats.
+# One GPU session: parity tests, smoke, bench (both layouts), rocprofv3 kernel stats, and a
+# 2-rank rehearsal of the row-partitioned bench on the single GPU (gloo).
 # usage (on the GPU box, from the repo root): bash tools/gpu_round.sh TAG
 set -o pipefail
 TAG=${1:-run}
@@ -7,9 +8,10 @@ cd "$GRAFT_REPO_ROOT" || exit 9
 export TMPDIR=/tmp
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
-timeout -k 10 600 python -u -m pytest tests/ -x -v --timeout 300 --timeout-method thread -m gpu > "$OUT/pytest.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests/ -x -v --timeout 300 --timeout-method thread -m gpu > "$OUT/pytest.log" 2>&1
 echo "pytest exit $?" >> "$OUT/pytest.log"
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || exit 1
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --cpu-seconds 10 > "$OUT/bench_sell.log" 2>&1 || exit 2
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --layout csr --no-cpu-baseline > "$OUT/bench_csr.log" 2>&1 || exit 3
+MPBP_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --grid 512 > "$OUT/bench_rows2_gloo.log" 2>&1 || exit 5
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- python "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline > "$GRAFT_REPO_ROOT/$OUT/prof.log" 2>&1 || exit 4
