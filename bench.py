@@ -38,6 +38,9 @@ def sweep_bytes(pc, layout):
     (x_in, b, diag, d read + d write, x_out) and the slice / row-block descriptors."""
     F = pc.F
     nF, nnzF = F.shape[0], F.nnz
+    if getattr(pc, "f_stencil", None) is not None:
+        # matrix-free: x, b, d (r/w), x_out per row + the three thn tables read once (3 x 8 B per cell)
+        return nF * 8 * 5 + 3 * 8 * (nF // 4), "k_f_stencil<EpiCheb> (F Chebyshev sweep, matrix-free)"
     if layout == "sell":
         nsl = pc.sell_of("F").nslices
         return nnzF * 12 + nF * 1 + nF * 8 * 6 + nsl * 16, "k_sell_rows<EpiCheb> (F Chebyshev sweep, SELL-64)"
@@ -58,6 +61,8 @@ def main():
     ap.add_argument("--inner-f", default="chebyshev:4")
     ap.add_argument("--inner-p", default="chebyshev:4")
     ap.add_argument("--layout", default="sell", choices=["sell", "csr"])
+    ap.add_argument("--f-mode", default="auto", choices=["auto", "stencil", "assembled"],
+                    help="F sweeps: recompute F from thn (stencil) or stream the assembled F")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-spmv", action="store_true")
@@ -90,7 +95,8 @@ def main():
     if world == 1:
         bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
         A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
-        pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, layout=args.layout)
+        pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, layout=args.layout,
+                                          f_mode=args.f_mode)
         del F, D, G
     else:
         from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
@@ -167,7 +173,8 @@ def main():
                                    "(BASELINE configs[2]" + (")" if world == 1 else ", row-partitioned)"),
                        "n": n, "unknowns": 5 * n * n, "xi": args.xi, "eta_n": args.eta_n,
                        "eta_s": args.eta_s, "inner_F": f"{kf}:{sf}", "inner_P": f"{kp}:{spp}",
-                       "parallelism": f"rows{world}" if world > 1 else "single", "layout": args.layout},
+                       "parallelism": f"rows{world}" if world > 1 else "single", "layout": args.layout,
+                       "f_sweeps": "matrix-free" if getattr(pc, "f_stencil", None) is not None else "assembled"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
                          "bytes_per_launch": sbytes, "avg_launch_us": avg_sweep_s * 1e6,

@@ -137,6 +137,11 @@ typedef struct mpbp_schur_plan {
     int32_t* prof_count;             /* host int: pairs recorded so far (caller resets) */
     int32_t use_sell;                /* 1: run the SELL-64 copies below instead of CSR row blocks */
     mpbp_sell Fs_int, Fs_bnd, Ds_int, Ds_bnd, Gs_int, Gs_bnd, Ps_int, Ps_bnd, Qs_int, Qs_bnd;
+    int32_t f_stencil;               /* 1: F sweeps recompute F's rows from thn (one GPU, n >= 3) */
+    mpbp_stokes_params f_prm;        /* the parameters F was assembled with */
+    const double* f_cell;            /* device thn tables (n*n each) */
+    const double* f_uface;
+    const double* f_vface;
 } mpbp_schur_plan;
 
 const char* mpbp_version(void);
@@ -223,6 +228,18 @@ int mpbp_sell_jacobi_step(const mpbp_sell* S, const double* x_in, const double* 
                           const double* sub, double* x_out, void* stream);
 int mpbp_sell_cheb_step(const mpbp_sell* S, const double* x_in, const double* b, const double* diag,
                         double c1, double c2, double* d, const double* sub, double* x_out, void* stream);
+
+/* ---- matrix-free F (the reference's F, recomputed per row from the thn tables) -------------- */
+/* Same results as the assembled-F kernels bit for bit (same formulas, same summation order). */
+int mpbp_f_stencil_spmv(const mpbp_stokes_params* prm, const double* cell, const double* uface,
+                        const double* vface, int32_t mode, const double* x, const double* z, double* y,
+                        void* stream);
+int mpbp_f_stencil_jacobi_step(const mpbp_stokes_params* prm, const double* cell, const double* uface,
+                               const double* vface, const double* x_in, const double* b,
+                               const double* sub, double* x_out, void* stream);
+int mpbp_f_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell, const double* uface,
+                             const double* vface, const double* x_in, const double* b, double c1,
+                             double c2, double* d, const double* sub, double* x_out, void* stream);
 
 /* gather: dst[i] = src[idx[i]] ; scatter: dst[idx[i]] = src[i]   (halo pack / unpack) */
 int mpbp_gather(int32_t count, const int32_t* idx, const double* src, double* dst, void* stream);

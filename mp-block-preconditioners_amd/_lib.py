@@ -61,7 +61,9 @@ class SchurPlan(Structure):
                 ("prof_events", c_void_p), ("prof_capacity", c_int32), ("prof_count", POINTER(c_int32)),
                 ("use_sell", c_int32),
                 ("Fs_int", Sell), ("Fs_bnd", Sell), ("Ds_int", Sell), ("Ds_bnd", Sell), ("Gs_int", Sell),
-                ("Gs_bnd", Sell), ("Ps_int", Sell), ("Ps_bnd", Sell), ("Qs_int", Sell), ("Qs_bnd", Sell)]
+                ("Gs_bnd", Sell), ("Ps_int", Sell), ("Ps_bnd", Sell), ("Qs_int", Sell), ("Qs_bnd", Sell),
+                ("f_stencil", c_int32), ("f_prm", StokesParams), ("f_cell", c_void_p), ("f_uface", c_void_p),
+                ("f_vface", c_void_p)]
 
 
 _P = c_void_p
@@ -94,6 +96,10 @@ _SIGNATURES = {
     "mpbp_sell_spmv": ([POINTER(Sell), c_int32, _P, _P, _P, _P], c_int),
     "mpbp_sell_jacobi_step": ([POINTER(Sell), _P, _P, _P, _P, _P, _P], c_int),
     "mpbp_sell_cheb_step": ([POINTER(Sell), _P, _P, _P, c_double, c_double, _P, _P, _P, _P], c_int),
+    "mpbp_f_stencil_spmv": ([POINTER(StokesParams), _P, _P, _P, c_int32, _P, _P, _P, _P], c_int),
+    "mpbp_f_stencil_jacobi_step": ([POINTER(StokesParams), _P, _P, _P, _P, _P, _P, _P, _P], c_int),
+    "mpbp_f_stencil_cheb_step": ([POINTER(StokesParams), _P, _P, _P, _P, _P, c_double, c_double, _P, _P, _P, _P],
+                                 c_int),
     "mpbp_gather": ([c_int32, _P, _P, _P, _P], c_int),
     "mpbp_scatter": ([c_int32, _P, _P, _P, _P], c_int),
     "mpbp_event_create": ([POINTER(c_void_p)], c_int),

@@ -505,10 +505,10 @@ struct EpiJacobi {   // x = (b - R x)/D in residual form (solve.py:158)
     const double* diag;
     const double* sub;
     double* xout;
-    struct P { double x, b, d, s; };
-    __device__ P pre(int32_t r) const { return {xin[r], b[r], diag[r], sub ? sub[r] : 0.0}; }
+    struct P { double x, b, dg, s; };
+    __device__ P pre(int32_t r) const { return {xin[r], b[r], diag ? diag[r] : 0.0, sub ? sub[r] : 0.0}; }
     __device__ void operator()(int32_t r, double acc, const P& p) const {
-        const double x = p.x + (p.b - acc) / p.d;
+        const double x = p.x + (p.b - acc) / p.dg;
         xout[r] = sub ? p.s - x : x;
     }
 };
@@ -521,7 +521,7 @@ struct EpiCheb {
     const double* sub;
     double* xout;
     struct P { double x, b, dg, d, s; };
-    __device__ P pre(int32_t r) const { return {xin[r], b[r], diag[r], d[r], sub ? sub[r] : 0.0}; }
+    __device__ P pre(int32_t r) const { return {xin[r], b[r], diag ? diag[r] : 0.0, d[r], sub ? sub[r] : 0.0}; }
     __device__ void operator()(int32_t r, double acc, const P& p) const {
         const double z = (p.b - acc) / p.dg;
         const double dn = c1 * p.d + c2 * z;
@@ -530,6 +530,18 @@ struct EpiCheb {
         xout[r] = sub ? p.s - x : x;
     }
 };
+
+// XI entry xi * a * (1 - a) as the assembly evaluates it (left to right).
+__device__ inline double xi_of(double xi, double a) { return xi * a * (1.0 - a); }
+
+template <class PT>
+__device__ inline void set_diag(PT& p, double d) { p.dg = d; }
+template <>
+__device__ inline void set_diag<EpiStore::P>(EpiStore::P&, double) {}
+template <>
+__device__ inline void set_diag<EpiAdd::P>(EpiAdd::P&, double) {}
+template <>
+__device__ inline void set_diag<EpiResid::P>(EpiResid::P&, double) {}
 
 // CSR SpMV over a list of row blocks.  Phase 1 streams the block's [row_ptr[r0], row_ptr[r1])
 // slice of col_idx / val with 16-byte loads (fully coalesced across the workgroup), gathers x
@@ -673,6 +685,145 @@ __global__ void __launch_bounds__(kBlock) k_sell_rows(Sell S, const double* __re
         }
     }
     if (live) epi(r, acc, pe);
+}
+
+// ------------------------------------------------------------- F stencil ----
+// Matrix-free rows of F = XI + d_u blockdiag(eta_n L_n, eta_s L_s): the ten entries of a row are
+// recomputed from the thn tables (L1/L2-resident) with exactly the assembly's arithmetic
+// (phase_L_row / F_row above), sorted by column with fixed sorting networks, and summed in that
+// order -- the same IEEE operations as a sweep over the assembled F, without streaming its
+// 12 bytes x 10 entries per row from HBM.  Needs n >= 3 (no coinciding periodic neighbours).
+struct Ent {
+    int32_t c;
+    double v, x;
+};
+
+__device__ inline void cx(Ent& a, Ent& b) {   // compare-exchange by column, field-wise selects
+    const bool s = a.c > b.c;
+    const int32_t c0 = s ? b.c : a.c, c1 = s ? a.c : b.c;
+    const double v0 = s ? b.v : a.v, v1 = s ? a.v : b.v;
+    const double x0 = s ? b.x : a.x, x1 = s ? a.x : b.x;
+    a.c = c0; a.v = v0; a.x = x0;
+    b.c = c1; b.v = v1; b.x = x1;
+}
+__device__ inline void sort4(Ent* e) {
+    cx(e[0], e[1]); cx(e[2], e[3]); cx(e[0], e[2]); cx(e[1], e[3]); cx(e[1], e[2]);
+}
+__device__ inline void sort5(Ent* e) {
+    cx(e[0], e[1]); cx(e[3], e[4]); cx(e[2], e[4]); cx(e[2], e[3]); cx(e[1], e[4]);
+    cx(e[0], e[3]); cx(e[0], e[2]); cx(e[1], e[3]); cx(e[1], e[2]);
+}
+
+struct FStencilDev {
+    int n;
+    double xi, eta_n, eta_s, c, d_u;
+    const double* cell;
+    const double* uface;
+    const double* vface;
+};
+
+template <int K>
+__device__ inline void sortk(Ent* e) {
+    if constexpr (K == 4) sort4(e);
+    else sort5(e);
+}
+
+// Scale the L entries into F entries, gather x, sort each block by column, sum in CSR order.
+template <int NLO, int NHI>
+__device__ inline double f_row_finish(Ent (&lo)[NLO], Ent (&hi)[NHI], int32_t dcol, double fd, double eta,
+                                      double d_u, double vcross, int32_t off, int32_t xcross_idx, int p,
+                                      const double* __restrict__ x) {
+#pragma unroll
+    for (int t = 0; t < NLO; ++t) lo[t].v = (lo[t].c == dcol) ? fd : d_u * (eta * lo[t].v);
+#pragma unroll
+    for (int t = 0; t < NHI; ++t) hi[t].v = (hi[t].c == dcol) ? fd : d_u * (eta * hi[t].v);
+    const double xcross = x[xcross_idx];
+#pragma unroll
+    for (int t = 0; t < NLO; ++t) lo[t].x = x[off + lo[t].c];
+#pragma unroll
+    for (int t = 0; t < NHI; ++t) hi[t].x = x[off + hi[t].c];
+    sortk<NLO>(lo);
+    sortk<NHI>(hi);
+    double acc = 0.0;
+    if (p == 1) acc += vcross * xcross;
+#pragma unroll
+    for (int t = 0; t < NLO; ++t) acc += lo[t].v * lo[t].x;
+#pragma unroll
+    for (int t = 0; t < NHI; ++t) acc += hi[t].v * hi[t].x;
+    if (p == 0) acc += vcross * xcross;
+    return acc;
+}
+
+// acc = (F x)_R in assembled-CSR order; *fdiag = F_RR.
+__device__ inline double f_stencil_row(const FStencilDev& P, int32_t R, const double* __restrict__ x,
+                                       double* fdiag) {
+    const int n = P.n;
+    const int32_t N = n * n;
+    const int p = R >= 2 * N;
+    const int32_t i = R - p * 2 * N;
+    const Phase g{n, P.cell, p};
+    const double dx = 1.0 / n, dy = 1.0 / n;
+    const double idx2 = 1.0 / (dx * dx), idy2 = 1.0 / (dy * dy), idxy = 1.0 / (dx * dy), idyx = 1.0 / (dy * dx);
+    const double eta = p ? P.eta_s : P.eta_n;
+    const int32_t off = p * 2 * N, other = (1 - p) * 2 * N;
+    if (i < N) {   // u row: preconditioner.py:100-179
+        const int r = i / n, cc = i % n;
+        const double tij = g.T(r, cc - 1), tip1j = g.T(r, cc);
+        const double tijp1 = g.T(r - 1, cc - 1), tip1jp1 = g.T(r - 1, cc);
+        const double tijm1 = g.T(r + 1, cc - 1), tip1jm1 = g.T(r + 1, cc);
+        const double iph_jph = 0.25 * (tij + tijp1 + tip1jp1 + tip1j);
+        const double iph_jmh = 0.25 * (tij + tip1j + tijm1 + tip1jm1);
+        const double iph_j = 0.5 * (tij + tip1j);
+        const double xi_ii = xi_of(P.xi, iph_j);
+        const double th = P.uface[i];
+        const double w = p ? P.c * (1.0 - th) : P.c * th;
+        const double Ldiag = idx2 * (-tip1j - tij) + idy2 * (-iph_jph - iph_jmh);
+        const double fd = (w - P.d_u * xi_ii) + P.d_u * (eta * Ldiag);
+        *fdiag = fd;
+        Ent lo[5] = {Ent{g.idx(r - 1, cc), idy2 * (iph_jph), 0.0}, Ent{g.idx(r, cc - 1), idx2 * (tij), 0.0},
+                     Ent{i, 0.0, 0.0}, Ent{g.idx(r, cc + 1), tip1j / (dx * dx), 0.0},
+                     Ent{g.idx(r + 1, cc), idy2 * (iph_jmh), 0.0}};
+        Ent hi[4] = {Ent{N + g.idx(r, cc - 1), idyx * (tij - iph_jph), 0.0},
+                     Ent{N + g.idx(r, cc), idxy * (-tip1j + iph_jph), 0.0},
+                     Ent{N + g.idx(r + 1, cc - 1), idyx * (iph_jmh - tij), 0.0},
+                     Ent{N + g.idx(r + 1, cc), idxy * (tip1j - iph_jmh), 0.0}};
+        return f_row_finish<5, 4>(lo, hi, i, fd, eta, P.d_u, P.d_u * xi_ii, off, other + i, p, x);
+    } else {       // v row: preconditioner.py:182-295
+        const int32_t k = i - N;
+        const int r = k / n, cc = k % n;
+        const double tij = g.T(r, cc), tip1j = g.T(r, cc + 1);
+        const double tijp1 = g.T(r - 1, cc), tip1jp1 = g.T(r - 1, cc + 1);
+        const double tim1j = g.T(r, cc - 1), tim1jp1 = g.T(r - 1, cc - 1);
+        const double ip1_jph = 0.5 * (tij + tijp1);
+        const double xi_ii = xi_of(P.xi, ip1_jph);
+        const double th = P.vface[k];
+        const double w = p ? P.c * (1.0 - th) : P.c * th;
+        const double imh_jph = 0.25 * (tim1j + tim1jp1 + tij + tijp1);
+        const double iph_jph = 0.25 * (tij + tip1j + tijp1 + tip1jp1);
+        const double Ldiag = -1.0 / (dy * dy) * (tijp1 + tij) - idx2 * (iph_jph + imh_jph);
+        const double fd = (w - P.d_u * xi_ii) + P.d_u * (eta * Ldiag);
+        *fdiag = fd;
+        Ent lo[4] = {Ent{k, idxy * (imh_jph - tij), 0.0}, Ent{g.idx(r, cc + 1), idyx * (tij - iph_jph), 0.0},
+                     Ent{g.idx(r - 1, cc), idyx * (tijp1 - imh_jph), 0.0},
+                     Ent{g.idx(r - 1, cc + 1), idyx * (iph_jph - tijp1), 0.0}};
+        Ent hi[5] = {Ent{N + g.idx(r - 1, cc), idy2 * tijp1, 0.0}, Ent{N + g.idx(r, cc - 1), idx2 * imh_jph, 0.0},
+                     Ent{i, 0.0, 0.0}, Ent{N + g.idx(r, cc + 1), idx2 * iph_jph, 0.0},
+                     Ent{N + g.idx(r + 1, cc), idy2 * tij, 0.0}};
+        return f_row_finish<4, 5>(lo, hi, i, fd, eta, P.d_u, P.d_u * xi_ii, off, other + i, p, x);
+    }
+}
+
+template <class Epi>
+__global__ void __launch_bounds__(kBlock) k_f_stencil(FStencilDev P, int32_t nrows, const double* __restrict__ x,
+                                                      Epi epi) {
+    const int b = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int32_t r = b * kBlock + threadIdx.x;
+    if (r >= nrows) return;
+    typename Epi::P pe = epi.pre(r);
+    double fd;
+    const double acc = f_stencil_row(P, r, x, &fd);
+    set_diag(pe, fd);
+    epi(r, acc, pe);
 }
 
 // One thread per (slice, lane): copy the CSR row into its column-major slots.
@@ -1147,6 +1298,66 @@ int mpbp_sell_cheb_step(const mpbp_sell* S, const double* x_in, const double* b,
     return launch_sell(S, x_in, EpiCheb{x_in, b, diag, d, c1, c2, sub, x_out}, as_stream(stream));
 }
 
+static int make_fstencil(const mpbp_stokes_params* prm, const double* cell, const double* uface,
+                         const double* vface, FStencilDev* P) {
+    if (!prm || prm->n < 3 || !cell || !uface || !vface)
+        return set_error(MPBP_ERR_ARG, "f_stencil: needs n >= 3 and the three thn tables");
+    if ((int64_t)prm->n * prm->n * 5 > INT32_MAX) return set_error(MPBP_ERR_OVERFLOW, "f_stencil: n too large");
+    *P = FStencilDev{prm->n, prm->xi, prm->eta_n, prm->eta_s, prm->c, prm->d_u, cell, uface, vface};
+    return MPBP_OK;
+}
+
+}  // extern "C"
+
+namespace {
+template <class Epi>
+int launch_fstencil(const FStencilDev& P, const double* x, Epi epi, hipStream_t st) {
+    const int32_t rows = 4 * P.n * P.n;
+    k_f_stencil<Epi><<<grid_for(rows), kBlock, 0, st>>>(P, rows, x, epi);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mpbp_f_stencil_spmv(const mpbp_stokes_params* prm, const double* cell, const double* uface,
+                        const double* vface, int32_t mode, const double* x, const double* z, double* y,
+                        void* stream) {
+    FStencilDev P;
+    int rc = make_fstencil(prm, cell, uface, vface, &P);
+    if (rc) return rc;
+    if (!x || !y || (mode != MPBP_SPMV_STORE && !z)) return set_error(MPBP_ERR_ARG, "f_stencil_spmv: bad vectors");
+    const hipStream_t st = as_stream(stream);
+    switch (mode) {
+    case MPBP_SPMV_STORE: return launch_fstencil(P, x, EpiStore{y}, st);
+    case MPBP_SPMV_ADD: return launch_fstencil(P, x, EpiAdd{z, y}, st);
+    case MPBP_SPMV_RESID: return launch_fstencil(P, x, EpiResid{z, y}, st);
+    default: return set_error(MPBP_ERR_ARG, "f_stencil_spmv: unknown mode %d", mode);
+    }
+}
+
+int mpbp_f_stencil_jacobi_step(const mpbp_stokes_params* prm, const double* cell, const double* uface,
+                               const double* vface, const double* x_in, const double* b, const double* sub,
+                               double* x_out, void* stream) {
+    FStencilDev P;
+    int rc = make_fstencil(prm, cell, uface, vface, &P);
+    if (rc) return rc;
+    if (!x_in || !b || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "f_stencil_jacobi_step: bad vectors");
+    return launch_fstencil(P, x_in, EpiJacobi{x_in, b, nullptr, sub, x_out}, as_stream(stream));
+}
+
+int mpbp_f_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell, const double* uface,
+                             const double* vface, const double* x_in, const double* b, double c1, double c2,
+                             double* d, const double* sub, double* x_out, void* stream) {
+    FStencilDev P;
+    int rc = make_fstencil(prm, cell, uface, vface, &P);
+    if (rc) return rc;
+    if (!x_in || !b || !d || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "f_stencil_cheb_step: bad vectors");
+    return launch_fstencil(P, x_in, EpiCheb{x_in, b, nullptr, d, c1, c2, sub, x_out}, as_stream(stream));
+}
+
 }  // extern "C"
 
 // ======================================================= Schur apply ====
@@ -1162,19 +1373,33 @@ struct OpRef {
     const mpbp_csr* csr;
     const mpbp_rowblocks* blk;
     const mpbp_sell* sell;
+    const mpbp_schur_plan* stencil;   // F rows recomputed from the plan's thn tables
+    bool empty;
 };
 
 int op_spmv(const OpRef& o, int32_t mode, const double* x, const double* z, double* y, hipStream_t st) {
+    if (o.empty) return MPBP_OK;
+    if (o.stencil)
+        return mpbp_f_stencil_spmv(&o.stencil->f_prm, o.stencil->f_cell, o.stencil->f_uface, o.stencil->f_vface,
+                                   mode, x, z, y, (void*)st);
     return o.sell ? mpbp_sell_spmv(o.sell, mode, x, z, y, (void*)st)
                   : mpbp_spmv(o.csr, o.blk, mode, x, z, y, (void*)st);
 }
 int op_jacobi(const OpRef& o, const double* xin, const double* b, const double* dg, const double* sub, double* xo,
               hipStream_t st) {
+    if (o.empty) return MPBP_OK;
+    if (o.stencil)
+        return mpbp_f_stencil_jacobi_step(&o.stencil->f_prm, o.stencil->f_cell, o.stencil->f_uface,
+                                          o.stencil->f_vface, xin, b, sub, xo, (void*)st);
     return o.sell ? mpbp_sell_jacobi_step(o.sell, xin, b, dg, sub, xo, (void*)st)
                   : mpbp_jacobi_step(o.csr, o.blk, xin, b, dg, sub, xo, (void*)st);
 }
 int op_cheb(const OpRef& o, const double* xin, const double* b, const double* dg, double c1, double c2, double* d,
             const double* sub, double* xo, hipStream_t st) {
+    if (o.empty) return MPBP_OK;
+    if (o.stencil)
+        return mpbp_f_stencil_cheb_step(&o.stencil->f_prm, o.stencil->f_cell, o.stencil->f_uface,
+                                        o.stencil->f_vface, xin, b, c1, c2, d, sub, xo, (void*)st);
     return o.sell ? mpbp_sell_cheb_step(o.sell, xin, b, dg, c1, c2, d, sub, xo, (void*)st)
                   : mpbp_cheb_step(o.csr, o.blk, xin, b, dg, c1, c2, d, sub, xo, (void*)st);
 }
@@ -1185,8 +1410,8 @@ struct OpPair {
 
 OpPair make_op(const mpbp_schur_plan* p, const mpbp_csr& A, const mpbp_rowblocks& bi, const mpbp_rowblocks& bb,
                const mpbp_sell& si, const mpbp_sell& sb) {
-    if (p->use_sell) return OpPair{OpRef{&A, nullptr, &si}, OpRef{&A, nullptr, &sb}};
-    return OpPair{OpRef{&A, &bi, nullptr}, OpRef{&A, &bb, nullptr}};
+    if (p->use_sell) return OpPair{OpRef{&A, nullptr, &si, nullptr, false}, OpRef{&A, nullptr, &sb, nullptr, false}};
+    return OpPair{OpRef{&A, &bi, nullptr, nullptr, false}, OpRef{&A, &bb, nullptr, nullptr, false}};
 }
 
 // Launch one sweep over interior rows, then (after the halo is complete) boundary rows.
@@ -1251,7 +1476,10 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
         if (!p->wp[i]) return set_error(MPBP_ERR_ARG, "schur_apply: missing pressure workspace");
     if (!p->wu_owned || !p->diag_F || !p->diag_P) return set_error(MPBP_ERR_ARG, "schur_apply: missing operands");
     const Ctx c{p, as_stream(stream)};
-    const OpPair F = make_op(p, p->F, p->F_int, p->F_bnd, p->Fs_int, p->Fs_bnd);
+    if (p->f_stencil && p->halo) return set_error(MPBP_ERR_ARG, "schur_apply: the F stencil is single-GPU only");
+    const OpPair F = p->f_stencil ? OpPair{OpRef{nullptr, nullptr, nullptr, p, false},
+                                           OpRef{nullptr, nullptr, nullptr, nullptr, true}}
+                                  : make_op(p, p->F, p->F_int, p->F_bnd, p->Fs_int, p->Fs_bnd);
     const OpPair D = make_op(p, p->D, p->D_int, p->D_bnd, p->Ds_int, p->Ds_bnd);
     const OpPair G = make_op(p, p->G, p->G_int, p->G_bnd, p->Gs_int, p->Gs_bnd);
     const OpPair P = make_op(p, p->GtG, p->P_int, p->P_bnd, p->Ps_int, p->Ps_bnd);

@@ -37,6 +37,21 @@ def ths(y, x):
     return 1.0 - thn(y, x)
 
 
+class FStencil:
+    """What the matrix-free F kernels need: the assembly parameters and the thn tables (HBM)."""
+
+    def __init__(self, prm: _lib.StokesParams, tables):
+        self.prm = prm
+        self.cell, self.uface, self.vface = tables
+
+    def matvec(self, x, out=None, mode=_lib.SPMV_STORE, z=None):
+        if out is None:
+            out = torch.empty(4 * self.prm.n * self.prm.n, dtype=torch.float64, device=x.device)
+        check(lib().mpbp_f_stencil_spmv(ctypes.byref(self.prm), ptr(self.cell), ptr(self.uface), ptr(self.vface),
+                                        mode, ptr(x), ptr(z), ptr(out), stream_handle()))
+        return out
+
+
 class MultiphaseBlockPreconditioner:
     def __init__(self, n, xi, eta_n=1.0, eta_s=1.0, device=None):
         if int(n) < 1:
@@ -102,6 +117,8 @@ class MultiphaseBlockPreconditioner:
         kw = dict(c=c, d_u=d_u, d_p=d_p, d_div=d_div)
         A = self.assemble(_lib.OP_A, **kw)
         F = self.assemble(_lib.OP_F, **kw)
+        if self.n >= 3:
+            F.stencil = FStencil(self._params(**kw), self.theta_tables())
         D = self.assemble(_lib.OP_D, **kw)
         G = self.assemble(_lib.OP_G, **kw)
         return A, None, F, D, G

@@ -109,7 +109,7 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
     """
 
     def __init__(self, F, D, G, GtG=None, GtFG=None, inner_F: InnerSolver | None = None,
-                 inner_P: InnerSolver | None = None, device=None, layout: str = "sell"):
+                 inner_P: InnerSolver | None = None, device=None, layout: str = "sell", f_mode: str = "auto"):
         dev = torch.device(device or (F.device if isinstance(F, DeviceCSR) else "cuda"))
         self.F, self.D, self.G = (_device_csr(M, dev) for M in (F, D, G))
         if GtG is None or GtFG is None:
@@ -134,6 +134,14 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
             raise ValueError("layout must be 'sell' or 'csr'")
         self.layout = layout
         self._sell = [M.to_sell() for M in (self.F, self.D, self.G, self.GtG, self.GtFG)] if layout == "sell" else None
+        # F sweeps: "stencil" recomputes F's rows from thn (bit-identical to the assembled F, ~4x fewer
+        # HBM bytes); "assembled" streams the stored F; "auto" = stencil whenever F carries one.
+        if f_mode not in ("auto", "stencil", "assembled"):
+            raise ValueError("f_mode must be 'auto', 'stencil' or 'assembled'")
+        st = getattr(self.F, "stencil", None)
+        if f_mode == "stencil" and st is None:
+            raise ValueError("f_mode='stencil' needs F from MultiphaseBlockPreconditioner.get_big_A_matrix (n >= 3)")
+        self.f_stencil = st if f_mode in ("auto", "stencil") else None
         self._plan = self._make_plan()
         super().__init__(dtype=np.float64, shape=(nu + np_, nu + np_))
 
@@ -161,6 +169,11 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
             for name, S in zip(("Fs", "Ds", "Gs", "Ps", "Qs"), self._sell):
                 setattr(p, name + "_int", S.cstruct())
                 setattr(p, name + "_bnd", esell)
+        p.f_stencil = 1 if self.f_stencil is not None else 0
+        if self.f_stencil is not None:
+            p.f_prm = self.f_stencil.prm
+            p.f_cell, p.f_uface, p.f_vface = (t.data_ptr() for t in (self.f_stencil.cell, self.f_stencil.uface,
+                                                                    self.f_stencil.vface))
         p.halo = _lib.HALO_FN()
         p.halo_ctx = None
         p.prof_events = None

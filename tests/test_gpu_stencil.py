@@ -1,0 +1,94 @@
+"""Matrix-free F (rows recomputed from the thn tables) against the assembled F and the oracle.
+
+The stencil kernels must reproduce the assembled-F sweeps bit for bit: same entry values (same
+formulas and evaluation order as the assembly), summed in the same (sorted-column) order."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import rel_inf
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu(oracle_built):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _bits(a, b):
+    a = a.cpu().numpy() if hasattr(a, "cpu") else np.asarray(a)
+    b = b.cpu().numpy() if hasattr(b, "cpu") else np.asarray(b)
+    return np.array_equal(a.view(np.uint64), b.view(np.uint64))
+
+
+PARAMS = [(1.0, 100.0, 1.0, 1.0, -1.0), (2.5, 1.0e4, 1.0, 0.5, -2.0), (1.0, 1.0, 1.0, 0.0, -1.0)]
+
+
+@pytest.mark.parametrize("n", [3, 4, 17, 64, 255])
+@pytest.mark.parametrize("prm", PARAMS, ids=["visc", "stiff", "c0"])
+def test_stencil_matvec_and_sweeps_bit_exact(n, prm):
+    import mp_block_preconditioners_amd as mp
+    from mp_block_preconditioners_amd._lib import check, lib, ptr, stream_handle
+    xi, eta_n, eta_s, c, d_u = prm
+    bp = mp.MultiphaseBlockPreconditioner(n, xi, eta_n, eta_s)
+    _, _, F, _, _ = bp.get_big_A_matrix(c=c, d_u=d_u)
+    st = F.stencil
+    assert st is not None
+    g = torch.Generator(device="cuda").manual_seed(n)
+    x, b, d0, sub = (torch.randn(F.shape[0], dtype=torch.float64, device="cuda", generator=g) for _ in range(4))
+    for mode in (0, 1, 2):
+        assert _bits(st.matvec(x, mode=mode, z=b), F.matvec(x, mode=mode, z=b))
+    diag = F.diagonal()
+    blk = F.blocks.cstruct()
+    y1, y2 = torch.empty_like(x), torch.empty_like(x)
+    stencil_tabs = (ptr(st.cell), ptr(st.uface), ptr(st.vface))
+    check(lib().mpbp_jacobi_step(ctypes.byref(F.cstruct()), ctypes.byref(blk), ptr(x), ptr(b), ptr(diag), ptr(sub),
+                                 ptr(y1), stream_handle()))
+    check(lib().mpbp_f_stencil_jacobi_step(ctypes.byref(st.prm), *stencil_tabs, ptr(x), ptr(b), ptr(sub), ptr(y2),
+                                           stream_handle()))
+    assert _bits(y1, y2)
+    d1, d2 = d0.clone(), d0.clone()
+    check(lib().mpbp_cheb_step(ctypes.byref(F.cstruct()), ctypes.byref(blk), ptr(x), ptr(b), ptr(diag), 0.7, 1.3,
+                               ptr(d1), None, ptr(y1), stream_handle()))
+    check(lib().mpbp_f_stencil_cheb_step(ctypes.byref(st.prm), *stencil_tabs, ptr(x), ptr(b), 0.7, 1.3, ptr(d2),
+                                         None, ptr(y2), stream_handle()))
+    assert _bits(y1, y2) and _bits(d1, d2)
+
+
+@pytest.mark.parametrize("n", [3, 32, 96])
+def test_stencil_apply_matches_assembled_and_oracle(n):
+    import mp_block_preconditioners_amd as mp
+    from oracle.schur_oracle import Inner, approx_schur_apply
+    from oracle.stokes_oracle import StokesSystem, theta_tables
+    tabs = theta_tables(n)
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    bp.set_theta_tables(*tabs)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    kw = dict(inner_F=mp.InnerSolver("chebyshev", 5), inner_P=mp.InnerSolver("jacobi", 3))
+    pc_st = mp.ApproxSchurPreconditioner(F, D, G, f_mode="stencil", **kw)
+    pc_as = mp.ApproxSchurPreconditioner(F, D, G, pc_st.GtG, pc_st.GtFG, f_mode="assembled", **kw)
+    assert pc_st.f_stencil is not None and pc_as.f_stencil is None
+    v = np.random.default_rng(n).standard_normal(pc_st.shape[0])
+    vt = torch.from_numpy(v).cuda()
+    got = pc_st.apply(vt)
+    assert torch.equal(got, pc_as.apply(vt))
+    s = StokesSystem(n, 1.0, 100.0, 1.0, 1.0, -1.0, tables=tabs)
+    ref = approx_schur_apply(s.F, s.D, s.G, s.GtG, s.GtFG, v, Inner("chebyshev", 5, pc_st.inner_F.lmin,
+                                                                    pc_st.inner_F.lmax), Inner("jacobi", 3))
+    assert _bits(got, ref), rel_inf(got.cpu().numpy(), ref)
+
+
+def test_stencil_rejected_where_undefined():
+    import mp_block_preconditioners_amd as mp
+    bp = mp.MultiphaseBlockPreconditioner(2, 1.0, 1.0, 1.0)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    assert F.stencil is None                       # n <= 2: periodic neighbours coincide
+    with pytest.raises(ValueError):
+        mp.ApproxSchurPreconditioner(F, D, G, f_mode="stencil")
+    pc = mp.ApproxSchurPreconditioner(F, D, G, f_mode="auto")
+    assert pc.f_stencil is None

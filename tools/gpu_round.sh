@@ -15,3 +15,10 @@ timeout -k 10 300 python bench.py --steps 20 --warmup 5 --cpu-seconds 10 > "$OUT
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --layout csr --no-cpu-baseline > "$OUT/bench_csr.log" 2>&1 || exit 3
 MPBP_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --grid 512 > "$OUT/bench_rows2_gloo.log" 2>&1 || exit 5
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- python "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline > "$GRAFT_REPO_ROOT/$OUT/prof.log" 2>&1 || exit 4
+cd "$GRAFT_REPO_ROOT"
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --f-mode assembled --no-cpu-baseline --no-spmv > "$OUT/bench_sell_assembledF.log" 2>&1 || exit 6
+for L in stencil sell; do
+  for C in FETCH_SIZE WRITE_SIZE; do
+    cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/pmc_${L}_$C" -o pmc -- python "$GRAFT_REPO_ROOT/tools/pmc_sweep.py" --layout $L > "$GRAFT_REPO_ROOT/$OUT/pmc_${L}_$C.log" 2>&1 || exit 7
+  done
+done

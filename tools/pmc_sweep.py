@@ -16,7 +16,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--grid", type=int, default=1024)
     ap.add_argument("--sweeps", type=int, default=10)
-    ap.add_argument("--layout", default="sell", choices=["sell", "csr"])
+    ap.add_argument("--layout", default="sell", choices=["sell", "csr", "stencil"])
     args = ap.parse_args()
     import torch
     import mp_block_preconditioners_amd as mp
@@ -31,7 +31,11 @@ def main():
     y = torch.empty_like(x)
     torch.cuda.synchronize()
     for _ in range(args.sweeps):
-        if args.layout == "sell":
+        if args.layout == "stencil":
+            st = F.stencil
+            check(lib().mpbp_f_stencil_cheb_step(ctypes.byref(st.prm), ptr(st.cell), ptr(st.uface), ptr(st.vface),
+                                                 ptr(x), ptr(b), 0.3, 1.1, ptr(d), None, ptr(y), stream_handle()))
+        elif args.layout == "sell":
             check(lib().mpbp_sell_cheb_step(ctypes.byref(S.cstruct()), ptr(x), ptr(b), ptr(diag), 0.3, 1.1, ptr(d),
                                             None, ptr(y), stream_handle()))
         else:
