@@ -95,6 +95,17 @@ typedef struct mpbp_sell {
     const int32_t* col;
 } mpbp_sell;
 
+/* Grid-row partition of the 4 velocity fields (multi-GPU F stencil): the rank owns grid rows
+ * [r0, r0 + rows) of every field, followed in its vectors by `halo` ghost rows above and `halo`
+ * below per field.  which: 0 all owned rows, 1 rows off the first/last owned grid row, 2 those
+ * rows.  NULL (or halo = 0) = one GPU, whole grid. */
+typedef struct mpbp_row_part {
+    int32_t r0;
+    int32_t rows;
+    int32_t halo;
+    int32_t which;
+} mpbp_row_part;
+
 typedef struct mpbp_stokes_params {
     int32_t n;     /* grid is n x n, N = n*n cells, dx = dy = 1/n */
     double xi;     /* drag coefficient */
@@ -142,6 +153,7 @@ typedef struct mpbp_schur_plan {
     const double* f_cell;            /* device thn tables (n*n each) */
     const double* f_uface;
     const double* f_vface;
+    mpbp_row_part f_part;            /* halo = 0 on one GPU */
 } mpbp_schur_plan;
 
 const char* mpbp_version(void);
@@ -232,14 +244,15 @@ int mpbp_sell_cheb_step(const mpbp_sell* S, const double* x_in, const double* b,
 /* ---- matrix-free F (the reference's F, recomputed per row from the thn tables) -------------- */
 /* Same results as the assembled-F kernels bit for bit (same formulas, same summation order). */
 int mpbp_f_stencil_spmv(const mpbp_stokes_params* prm, const double* cell, const double* uface,
-                        const double* vface, int32_t mode, const double* x, const double* z, double* y,
-                        void* stream);
+                        const double* vface, const mpbp_row_part* part, int32_t mode, const double* x,
+                        const double* z, double* y, void* stream);
 int mpbp_f_stencil_jacobi_step(const mpbp_stokes_params* prm, const double* cell, const double* uface,
-                               const double* vface, const double* x_in, const double* b,
-                               const double* sub, double* x_out, void* stream);
+                               const double* vface, const mpbp_row_part* part, const double* x_in,
+                               const double* b, const double* sub, double* x_out, void* stream);
 int mpbp_f_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell, const double* uface,
-                             const double* vface, const double* x_in, const double* b, double c1,
-                             double c2, double* d, const double* sub, double* x_out, void* stream);
+                             const double* vface, const mpbp_row_part* part, const double* x_in,
+                             const double* b, double c1, double c2, double* d, const double* sub,
+                             double* x_out, void* stream);
 
 /* gather: dst[i] = src[idx[i]] ; scatter: dst[idx[i]] = src[i]   (halo pack / unpack) */
 int mpbp_gather(int32_t count, const int32_t* idx, const double* src, double* dst, void* stream);

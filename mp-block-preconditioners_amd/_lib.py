@@ -36,6 +36,10 @@ class Sell(Structure):
                 ("slices", c_void_p), ("row_len", c_void_p), ("val", c_void_p), ("col", c_void_p)]
 
 
+class RowPart(Structure):
+    _fields_ = [("r0", c_int32), ("rows", c_int32), ("halo", c_int32), ("which", c_int32)]
+
+
 class StokesParams(Structure):
     _fields_ = [("n", c_int32), ("xi", c_double), ("eta_n", c_double), ("eta_s", c_double),
                 ("c", c_double), ("d_u", c_double), ("d_p", c_double), ("d_div", c_double)]
@@ -63,7 +67,7 @@ class SchurPlan(Structure):
                 ("Fs_int", Sell), ("Fs_bnd", Sell), ("Ds_int", Sell), ("Ds_bnd", Sell), ("Gs_int", Sell),
                 ("Gs_bnd", Sell), ("Ps_int", Sell), ("Ps_bnd", Sell), ("Qs_int", Sell), ("Qs_bnd", Sell),
                 ("f_stencil", c_int32), ("f_prm", StokesParams), ("f_cell", c_void_p), ("f_uface", c_void_p),
-                ("f_vface", c_void_p)]
+                ("f_vface", c_void_p), ("f_part", RowPart)]
 
 
 _P = c_void_p
@@ -96,10 +100,11 @@ _SIGNATURES = {
     "mpbp_sell_spmv": ([POINTER(Sell), c_int32, _P, _P, _P, _P], c_int),
     "mpbp_sell_jacobi_step": ([POINTER(Sell), _P, _P, _P, _P, _P, _P], c_int),
     "mpbp_sell_cheb_step": ([POINTER(Sell), _P, _P, _P, c_double, c_double, _P, _P, _P, _P], c_int),
-    "mpbp_f_stencil_spmv": ([POINTER(StokesParams), _P, _P, _P, c_int32, _P, _P, _P, _P], c_int),
-    "mpbp_f_stencil_jacobi_step": ([POINTER(StokesParams), _P, _P, _P, _P, _P, _P, _P, _P], c_int),
-    "mpbp_f_stencil_cheb_step": ([POINTER(StokesParams), _P, _P, _P, _P, _P, c_double, c_double, _P, _P, _P, _P],
-                                 c_int),
+    "mpbp_f_stencil_spmv": ([POINTER(StokesParams), _P, _P, _P, POINTER(RowPart), c_int32, _P, _P, _P, _P], c_int),
+    "mpbp_f_stencil_jacobi_step": ([POINTER(StokesParams), _P, _P, _P, POINTER(RowPart), _P, _P, _P, _P, _P],
+                                   c_int),
+    "mpbp_f_stencil_cheb_step": ([POINTER(StokesParams), _P, _P, _P, POINTER(RowPart), _P, _P, c_double, c_double,
+                                  _P, _P, _P, _P], c_int),
     "mpbp_gather": ([c_int32, _P, _P, _P, _P], c_int),
     "mpbp_scatter": ([c_int32, _P, _P, _P, _P], c_int),
     "mpbp_event_create": ([POINTER(c_void_p)], c_int),
@@ -151,5 +156,5 @@ def stream_handle(stream=None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
-__all__ = ["lib", "check", "ptr", "stream_handle", "MpbpError", "Csr", "RowBlocks", "Sell", "StokesParams",
+__all__ = ["lib", "check", "ptr", "stream_handle", "MpbpError", "Csr", "RowBlocks", "Sell", "RowPart", "StokesParams",
            "InnerSolverC", "SchurPlan", "HALO_FN", "byref"]

@@ -92,7 +92,8 @@ struct Phase {
     int n;
     const double* cell;
     int s;
-    __device__ int wrap(int a) const { a %= n; return a < 0 ? a + n : a; }
+    // Periodic index for a in [-1, n]: every stencil offset is +-1 (no integer division).
+    __device__ int wrap(int a) const { return a < 0 ? a + n : (a >= n ? a - n : a); }
     __device__ int32_t idx(int r, int c) const { return wrap(r) * n + wrap(c); }
     __device__ double T(int r, int c) const { const double v = cell[idx(r, c)]; return s ? 1.0 - v : v; }
 };
@@ -694,17 +695,18 @@ __global__ void __launch_bounds__(kBlock) k_sell_rows(Sell S, const double* __re
 // order -- the same IEEE operations as a sweep over the assembled F, without streaming its
 // 12 bytes x 10 entries per row from HBM.  Needs n >= 3 (no coinciding periodic neighbours).
 struct Ent {
-    int32_t c;
+    int32_t c;   // phase-local global column: the sort key (CSR order of the assembled row)
+    int32_t g;   // index into x: global on one GPU, owned-then-ghost ("ext") under a row partition
     double v, x;
 };
 
 __device__ inline void cx(Ent& a, Ent& b) {   // compare-exchange by column, field-wise selects
     const bool s = a.c > b.c;
     const int32_t c0 = s ? b.c : a.c, c1 = s ? a.c : b.c;
+    const int32_t g0 = s ? b.g : a.g, g1 = s ? a.g : b.g;
     const double v0 = s ? b.v : a.v, v1 = s ? a.v : b.v;
-    const double x0 = s ? b.x : a.x, x1 = s ? a.x : b.x;
-    a.c = c0; a.v = v0; a.x = x0;
-    b.c = c1; b.v = v1; b.x = x1;
+    a.c = c0; a.g = g0; a.v = v0;
+    b.c = c1; b.g = g1; b.v = v1;
 }
 __device__ inline void sort4(Ent* e) {
     cx(e[0], e[1]); cx(e[2], e[3]); cx(e[0], e[2]); cx(e[1], e[3]); cx(e[1], e[2]);
@@ -713,6 +715,11 @@ __device__ inline void sort5(Ent* e) {
     cx(e[0], e[1]); cx(e[3], e[4]); cx(e[2], e[4]); cx(e[2], e[3]); cx(e[1], e[4]);
     cx(e[0], e[3]); cx(e[0], e[2]); cx(e[1], e[3]); cx(e[1], e[2]);
 }
+template <int K>
+__device__ inline void sortk(Ent* e) {
+    if constexpr (K == 4) sort4(e);
+    else sort5(e);
+}
 
 struct FStencilDev {
     int n;
@@ -720,30 +727,57 @@ struct FStencilDev {
     const double* cell;
     const double* uface;
     const double* vface;
+    // grid constants, evaluated once on the host exactly as the assembly evaluates them on the device
+    double dxdx;   // dx * dx
+    double idx2;   // 1.0 / (dx * dx)   (== 1.0 / (dy * dy), 1.0 / (dx * dy): dx == dy)
+    double midy2;  // -1.0 / (dy * dy)
+    // row partition: this rank owns grid rows [r0, r0 + L) of each of the 4 velocity fields; ghosts
+    // (h rows above, h below, per field) follow the 4*L*n owned entries.  One GPU: r0 = 0, L = n, h = 0.
+    int r0, L, h, which;
 };
 
-template <int K>
-__device__ inline void sortk(Ent* e) {
-    if constexpr (K == 4) sort4(e);
-    else sort5(e);
-}
+// Indices of grid point (field f, grid row gr, column gc) for gr in [r0-1, r0+L], gc in [-1, n].
+template <bool EDGE>
+struct Grid2 {
+    const FStencilDev& P;
+    int s;   // phase: ths = 1 - thn
+    __device__ int wrap(int a) const { return a < 0 ? a + P.n : (a >= P.n ? a - P.n : a); }
+    __device__ int32_t key(int gr, int gc) const {          // global cell index (sort key, tables)
+        return EDGE ? wrap(gr) * P.n + wrap(gc) : gr * P.n + gc;
+    }
+    __device__ int32_t xg(int f, int gr, int gc) const {    // where x holds that unknown
+        const int lr = gr - P.r0;
+        if (!EDGE) return (f * P.L + lr) * P.n + gc;
+        const int c = wrap(gc);
+        if (P.h == 0) return (f * P.L + wrap(gr)) * P.n + c;               // one GPU: global index
+        if (lr >= 0 && lr < P.L) return (f * P.L + lr) * P.n + c;
+        const int own = 4 * P.L * P.n;
+        return own + f * 2 * P.h * P.n + (lr < 0 ? (P.h - 1) : P.h) * P.n + c;   // row r0-1 / r0+L
+    }
+    __device__ double T(int gr, int gc) const { const double v = P.cell[key(gr, gc)]; return s ? 1.0 - v : v; }
+    __device__ Ent e(int f, int gr, int gc, int32_t base, double v) const {
+        return Ent{base + key(gr, gc), xg(f, gr, gc), v, 0.0};
+    }
+};
 
 // Scale the L entries into F entries, gather x, sort each block by column, sum in CSR order.
-template <int NLO, int NHI>
+template <int NLO, int NHI, bool EDGE>
 __device__ inline double f_row_finish(Ent (&lo)[NLO], Ent (&hi)[NHI], int32_t dcol, double fd, double eta,
-                                      double d_u, double vcross, int32_t off, int32_t xcross_idx, int p,
+                                      double d_u, double vcross, int32_t xcross_idx, int p,
                                       const double* __restrict__ x) {
 #pragma unroll
     for (int t = 0; t < NLO; ++t) lo[t].v = (lo[t].c == dcol) ? fd : d_u * (eta * lo[t].v);
 #pragma unroll
     for (int t = 0; t < NHI; ++t) hi[t].v = (hi[t].c == dcol) ? fd : d_u * (eta * hi[t].v);
+    if (EDGE) {   // wrapped neighbours can reorder the columns; interior rows are built sorted
+        sortk<NLO>(lo);
+        sortk<NHI>(hi);
+    }
     const double xcross = x[xcross_idx];
 #pragma unroll
-    for (int t = 0; t < NLO; ++t) lo[t].x = x[off + lo[t].c];
+    for (int t = 0; t < NLO; ++t) lo[t].x = x[lo[t].g];
 #pragma unroll
-    for (int t = 0; t < NHI; ++t) hi[t].x = x[off + hi[t].c];
-    sortk<NLO>(lo);
-    sortk<NHI>(hi);
+    for (int t = 0; t < NHI; ++t) hi[t].x = x[hi[t].g];
     double acc = 0.0;
     if (p == 1) acc += vcross * xcross;
 #pragma unroll
@@ -754,74 +788,111 @@ __device__ inline double f_row_finish(Ent (&lo)[NLO], Ent (&hi)[NHI], int32_t dc
     return acc;
 }
 
-// acc = (F x)_R in assembled-CSR order; *fdiag = F_RR.
-__device__ inline double f_stencil_row(const FStencilDev& P, int32_t R, const double* __restrict__ x,
+// acc = (F x)_R in assembled-CSR order; *fdiag = F_RR.  Same operations as phase_L_row / F_row.
+// Row = field f (p = f / 2 phase, f % 2: u / v), grid point (gr, gc).
+template <bool EDGE>
+__device__ inline double f_stencil_row(const FStencilDev& P, int f, int gr, int gc, const double* __restrict__ x,
                                        double* fdiag) {
     const int n = P.n;
     const int32_t N = n * n;
-    const int p = R >= 2 * N;
-    const int32_t i = R - p * 2 * N;
-    const Phase g{n, P.cell, p};
-    const double dx = 1.0 / n, dy = 1.0 / n;
-    const double idx2 = 1.0 / (dx * dx), idy2 = 1.0 / (dy * dy), idxy = 1.0 / (dx * dy), idyx = 1.0 / (dy * dx);
+    const int p = f >> 1;
+    const Grid2<EDGE> g{P, p};
+    const double idx2 = P.idx2;
     const double eta = p ? P.eta_s : P.eta_n;
-    const int32_t off = p * 2 * N, other = (1 - p) * 2 * N;
-    if (i < N) {   // u row: preconditioner.py:100-179
-        const int r = i / n, cc = i % n;
-        const double tij = g.T(r, cc - 1), tip1j = g.T(r, cc);
-        const double tijp1 = g.T(r - 1, cc - 1), tip1jp1 = g.T(r - 1, cc);
-        const double tijm1 = g.T(r + 1, cc - 1), tip1jm1 = g.T(r + 1, cc);
+    const int fu = 2 * p, fv = 2 * p + 1;                    // this phase's u / v fields
+    const int32_t kc = gr * n + gc;                          // the row's cell
+    const int32_t xcross = ((f ^ 2) * P.L + (gr - P.r0)) * n + gc;   // same point, other phase
+    if ((f & 1) == 0) {   // u row: preconditioner.py:100-179
+        const double tij = g.T(gr, gc - 1), tip1j = g.T(gr, gc);
+        const double tijp1 = g.T(gr - 1, gc - 1), tip1jp1 = g.T(gr - 1, gc);
+        const double tijm1 = g.T(gr + 1, gc - 1), tip1jm1 = g.T(gr + 1, gc);
         const double iph_jph = 0.25 * (tij + tijp1 + tip1jp1 + tip1j);
         const double iph_jmh = 0.25 * (tij + tip1j + tijm1 + tip1jm1);
         const double iph_j = 0.5 * (tij + tip1j);
         const double xi_ii = xi_of(P.xi, iph_j);
-        const double th = P.uface[i];
+        const double th = P.uface[kc];
         const double w = p ? P.c * (1.0 - th) : P.c * th;
-        const double Ldiag = idx2 * (-tip1j - tij) + idy2 * (-iph_jph - iph_jmh);
+        const double Ldiag = idx2 * (-tip1j - tij) + idx2 * (-iph_jph - iph_jmh);
         const double fd = (w - P.d_u * xi_ii) + P.d_u * (eta * Ldiag);
         *fdiag = fd;
-        Ent lo[5] = {Ent{g.idx(r - 1, cc), idy2 * (iph_jph), 0.0}, Ent{g.idx(r, cc - 1), idx2 * (tij), 0.0},
-                     Ent{i, 0.0, 0.0}, Ent{g.idx(r, cc + 1), tip1j / (dx * dx), 0.0},
-                     Ent{g.idx(r + 1, cc), idy2 * (iph_jmh), 0.0}};
-        Ent hi[4] = {Ent{N + g.idx(r, cc - 1), idyx * (tij - iph_jph), 0.0},
-                     Ent{N + g.idx(r, cc), idxy * (-tip1j + iph_jph), 0.0},
-                     Ent{N + g.idx(r + 1, cc - 1), idyx * (iph_jmh - tij), 0.0},
-                     Ent{N + g.idx(r + 1, cc), idxy * (tip1j - iph_jmh), 0.0}};
-        return f_row_finish<5, 4>(lo, hi, i, fd, eta, P.d_u, P.d_u * xi_ii, off, other + i, p, x);
-    } else {       // v row: preconditioner.py:182-295
-        const int32_t k = i - N;
-        const int r = k / n, cc = k % n;
-        const double tij = g.T(r, cc), tip1j = g.T(r, cc + 1);
-        const double tijp1 = g.T(r - 1, cc), tip1jp1 = g.T(r - 1, cc + 1);
-        const double tim1j = g.T(r, cc - 1), tim1jp1 = g.T(r - 1, cc - 1);
+        Ent lo[5] = {g.e(fu, gr - 1, gc, 0, idx2 * (iph_jph)), g.e(fu, gr, gc - 1, 0, idx2 * (tij)),
+                     g.e(fu, gr, gc, 0, 0.0), g.e(fu, gr, gc + 1, 0, tip1j / P.dxdx),
+                     g.e(fu, gr + 1, gc, 0, idx2 * (iph_jmh))};
+        Ent hi[4] = {g.e(fv, gr, gc - 1, N, idx2 * (tij - iph_jph)), g.e(fv, gr, gc, N, idx2 * (-tip1j + iph_jph)),
+                     g.e(fv, gr + 1, gc - 1, N, idx2 * (iph_jmh - tij)),
+                     g.e(fv, gr + 1, gc, N, idx2 * (tip1j - iph_jmh))};
+        return f_row_finish<5, 4, EDGE>(lo, hi, kc, fd, eta, P.d_u, P.d_u * xi_ii, xcross, p, x);
+    } else {              // v row: preconditioner.py:182-295
+        const double tij = g.T(gr, gc), tip1j = g.T(gr, gc + 1);
+        const double tijp1 = g.T(gr - 1, gc), tip1jp1 = g.T(gr - 1, gc + 1);
+        const double tim1j = g.T(gr, gc - 1), tim1jp1 = g.T(gr - 1, gc - 1);
         const double ip1_jph = 0.5 * (tij + tijp1);
         const double xi_ii = xi_of(P.xi, ip1_jph);
-        const double th = P.vface[k];
+        const double th = P.vface[kc];
         const double w = p ? P.c * (1.0 - th) : P.c * th;
         const double imh_jph = 0.25 * (tim1j + tim1jp1 + tij + tijp1);
         const double iph_jph = 0.25 * (tij + tip1j + tijp1 + tip1jp1);
-        const double Ldiag = -1.0 / (dy * dy) * (tijp1 + tij) - idx2 * (iph_jph + imh_jph);
+        const double Ldiag = P.midy2 * (tijp1 + tij) - idx2 * (iph_jph + imh_jph);
         const double fd = (w - P.d_u * xi_ii) + P.d_u * (eta * Ldiag);
         *fdiag = fd;
-        Ent lo[4] = {Ent{k, idxy * (imh_jph - tij), 0.0}, Ent{g.idx(r, cc + 1), idyx * (tij - iph_jph), 0.0},
-                     Ent{g.idx(r - 1, cc), idyx * (tijp1 - imh_jph), 0.0},
-                     Ent{g.idx(r - 1, cc + 1), idyx * (iph_jph - tijp1), 0.0}};
-        Ent hi[5] = {Ent{N + g.idx(r - 1, cc), idy2 * tijp1, 0.0}, Ent{N + g.idx(r, cc - 1), idx2 * imh_jph, 0.0},
-                     Ent{i, 0.0, 0.0}, Ent{N + g.idx(r, cc + 1), idx2 * iph_jph, 0.0},
-                     Ent{N + g.idx(r + 1, cc), idy2 * tij, 0.0}};
-        return f_row_finish<4, 5>(lo, hi, i, fd, eta, P.d_u, P.d_u * xi_ii, off, other + i, p, x);
+        Ent lo[4] = {g.e(fu, gr - 1, gc, 0, idx2 * (tijp1 - imh_jph)),
+                     g.e(fu, gr - 1, gc + 1, 0, idx2 * (iph_jph - tijp1)),
+                     g.e(fu, gr, gc, 0, idx2 * (imh_jph - tij)), g.e(fu, gr, gc + 1, 0, idx2 * (tij - iph_jph))};
+        Ent hi[5] = {g.e(fv, gr - 1, gc, N, idx2 * tijp1), g.e(fv, gr, gc - 1, N, idx2 * imh_jph),
+                     g.e(fv, gr, gc, N, 0.0), g.e(fv, gr, gc + 1, N, idx2 * iph_jph),
+                     g.e(fv, gr + 1, gc, N, idx2 * tij)};
+        return f_row_finish<4, 5, EDGE>(lo, hi, N + kc, fd, eta, P.d_u, P.d_u * xi_ii, xcross, p, x);
     }
 }
 
+// Thread t -> owned local row: which = 0 all rows, 1 rows not on the first / last owned grid row
+// of a field (they read no ghost), 2 rows on those grid rows.
+__device__ inline bool f_stencil_rowof(const FStencilDev& P, int64_t t, int32_t* r) {
+    const int n = P.n, L = P.L;
+    int f, lr, gc;
+    if (P.which == 0) {
+        if (t >= (int64_t)4 * L * n) return false;
+        const int32_t q = (int32_t)t;
+        f = q / (L * n);
+        const int32_t rem = q - f * L * n;
+        lr = rem / n;
+        gc = rem - lr * n;
+    } else if (P.which == 1) {
+        const int Li = L - 2;
+        if (Li <= 0 || t >= (int64_t)4 * Li * n) return false;
+        const int32_t q = (int32_t)t;
+        f = q / (Li * n);
+        const int32_t rem = q - f * Li * n;
+        lr = 1 + rem / n;
+        gc = rem - (lr - 1) * n;
+    } else {
+        const int nb = L >= 2 ? 2 : 1;
+        if (t >= (int64_t)4 * nb * n) return false;
+        const int32_t q = (int32_t)t;
+        f = q / (nb * n);
+        const int32_t rem = q - f * nb * n;
+        const int side = rem / n;
+        gc = rem - side * n;
+        lr = side ? L - 1 : 0;
+    }
+    *r = (f * L + lr) * n + gc;
+    return true;
+}
+
 template <class Epi>
-__global__ void __launch_bounds__(kBlock) k_f_stencil(FStencilDev P, int32_t nrows, const double* __restrict__ x,
-                                                      Epi epi) {
+__global__ void __launch_bounds__(kBlock) k_f_stencil(FStencilDev P, const double* __restrict__ x, Epi epi) {
     const int b = xcd_swizzle(blockIdx.x, gridDim.x);
-    const int32_t r = b * kBlock + threadIdx.x;
-    if (r >= nrows) return;
+    int32_t r;
+    if (!f_stencil_rowof(P, (int64_t)b * kBlock + threadIdx.x, &r)) return;
     typename Epi::P pe = epi.pre(r);
+    const int n = P.n;
+    const int f = r / (P.L * n);
+    const int32_t rem = r - f * P.L * n;
+    const int lr = rem / n, gc = rem - lr * n;
     double fd;
-    const double acc = f_stencil_row(P, r, x, &fd);
+    const bool edge = lr == 0 || lr == P.L - 1 || gc == 0 || gc == n - 1;
+    const double acc = edge ? f_stencil_row<true>(P, f, P.r0 + lr, gc, x, &fd)
+                            : f_stencil_row<false>(P, f, P.r0 + lr, gc, x, &fd);
     set_diag(pe, fd);
     epi(r, acc, pe);
 }
@@ -1299,11 +1370,19 @@ int mpbp_sell_cheb_step(const mpbp_sell* S, const double* x_in, const double* b,
 }
 
 static int make_fstencil(const mpbp_stokes_params* prm, const double* cell, const double* uface,
-                         const double* vface, FStencilDev* P) {
+                         const double* vface, const mpbp_row_part* part, FStencilDev* P) {
     if (!prm || prm->n < 3 || !cell || !uface || !vface)
         return set_error(MPBP_ERR_ARG, "f_stencil: needs n >= 3 and the three thn tables");
     if ((int64_t)prm->n * prm->n * 5 > INT32_MAX) return set_error(MPBP_ERR_OVERFLOW, "f_stencil: n too large");
-    *P = FStencilDev{prm->n, prm->xi, prm->eta_n, prm->eta_s, prm->c, prm->d_u, cell, uface, vface};
+    const double dx = 1.0 / prm->n;
+    int r0 = 0, L = prm->n, h = 0, which = 0;
+    if (part && part->halo > 0) {
+        r0 = part->r0; L = part->rows; h = part->halo; which = part->which;
+        if (L < 1 || r0 < 0 || r0 + L > prm->n || which < 0 || which > 2)
+            return set_error(MPBP_ERR_ARG, "f_stencil: bad row partition");
+    }
+    *P = FStencilDev{prm->n, prm->xi, prm->eta_n, prm->eta_s, prm->c, prm->d_u, cell, uface, vface,
+                     dx * dx, 1.0 / (dx * dx), -1.0 / (dx * dx), r0, L, h, which};
     return MPBP_OK;
 }
 
@@ -1312,8 +1391,11 @@ static int make_fstencil(const mpbp_stokes_params* prm, const double* cell, cons
 namespace {
 template <class Epi>
 int launch_fstencil(const FStencilDev& P, const double* x, Epi epi, hipStream_t st) {
-    const int32_t rows = 4 * P.n * P.n;
-    k_f_stencil<Epi><<<grid_for(rows), kBlock, 0, st>>>(P, rows, x, epi);
+    const int64_t rows = P.which == 0 ? (int64_t)4 * P.L * P.n
+                       : P.which == 1 ? (int64_t)4 * (P.L > 2 ? P.L - 2 : 0) * P.n
+                                      : (int64_t)4 * (P.L >= 2 ? 2 : 1) * P.n;
+    if (rows == 0) return MPBP_OK;
+    k_f_stencil<Epi><<<grid_for(rows), kBlock, 0, st>>>(P, x, epi);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
@@ -1323,10 +1405,10 @@ int launch_fstencil(const FStencilDev& P, const double* x, Epi epi, hipStream_t 
 extern "C" {
 
 int mpbp_f_stencil_spmv(const mpbp_stokes_params* prm, const double* cell, const double* uface,
-                        const double* vface, int32_t mode, const double* x, const double* z, double* y,
-                        void* stream) {
+                        const double* vface, const mpbp_row_part* part, int32_t mode, const double* x,
+                        const double* z, double* y, void* stream) {
     FStencilDev P;
-    int rc = make_fstencil(prm, cell, uface, vface, &P);
+    int rc = make_fstencil(prm, cell, uface, vface, part, &P);
     if (rc) return rc;
     if (!x || !y || (mode != MPBP_SPMV_STORE && !z)) return set_error(MPBP_ERR_ARG, "f_stencil_spmv: bad vectors");
     const hipStream_t st = as_stream(stream);
@@ -1339,20 +1421,21 @@ int mpbp_f_stencil_spmv(const mpbp_stokes_params* prm, const double* cell, const
 }
 
 int mpbp_f_stencil_jacobi_step(const mpbp_stokes_params* prm, const double* cell, const double* uface,
-                               const double* vface, const double* x_in, const double* b, const double* sub,
-                               double* x_out, void* stream) {
+                               const double* vface, const mpbp_row_part* part, const double* x_in,
+                               const double* b, const double* sub, double* x_out, void* stream) {
     FStencilDev P;
-    int rc = make_fstencil(prm, cell, uface, vface, &P);
+    int rc = make_fstencil(prm, cell, uface, vface, part, &P);
     if (rc) return rc;
     if (!x_in || !b || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "f_stencil_jacobi_step: bad vectors");
     return launch_fstencil(P, x_in, EpiJacobi{x_in, b, nullptr, sub, x_out}, as_stream(stream));
 }
 
 int mpbp_f_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell, const double* uface,
-                             const double* vface, const double* x_in, const double* b, double c1, double c2,
-                             double* d, const double* sub, double* x_out, void* stream) {
+                             const double* vface, const mpbp_row_part* part, const double* x_in,
+                             const double* b, double c1, double c2, double* d, const double* sub,
+                             double* x_out, void* stream) {
     FStencilDev P;
-    int rc = make_fstencil(prm, cell, uface, vface, &P);
+    int rc = make_fstencil(prm, cell, uface, vface, part, &P);
     if (rc) return rc;
     if (!x_in || !b || !d || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "f_stencil_cheb_step: bad vectors");
     return launch_fstencil(P, x_in, EpiCheb{x_in, b, nullptr, d, c1, c2, sub, x_out}, as_stream(stream));
@@ -1375,13 +1458,23 @@ struct OpRef {
     const mpbp_sell* sell;
     const mpbp_schur_plan* stencil;   // F rows recomputed from the plan's thn tables
     bool empty;
+    int32_t which;                    // stencil rows: 0 all, 1 interior, 2 boundary
 };
+
+inline mpbp_row_part stencil_part(const OpRef& o) {
+    mpbp_row_part q = o.stencil->f_part;
+    q.which = q.halo > 0 ? o.which : 0;
+    return q;
+}
 
 int op_spmv(const OpRef& o, int32_t mode, const double* x, const double* z, double* y, hipStream_t st) {
     if (o.empty) return MPBP_OK;
     if (o.stencil)
+    {
+        const mpbp_row_part q = stencil_part(o);
         return mpbp_f_stencil_spmv(&o.stencil->f_prm, o.stencil->f_cell, o.stencil->f_uface, o.stencil->f_vface,
-                                   mode, x, z, y, (void*)st);
+                                   &q, mode, x, z, y, (void*)st);
+    }
     return o.sell ? mpbp_sell_spmv(o.sell, mode, x, z, y, (void*)st)
                   : mpbp_spmv(o.csr, o.blk, mode, x, z, y, (void*)st);
 }
@@ -1389,8 +1482,11 @@ int op_jacobi(const OpRef& o, const double* xin, const double* b, const double* 
               hipStream_t st) {
     if (o.empty) return MPBP_OK;
     if (o.stencil)
+    {
+        const mpbp_row_part q = stencil_part(o);
         return mpbp_f_stencil_jacobi_step(&o.stencil->f_prm, o.stencil->f_cell, o.stencil->f_uface,
-                                          o.stencil->f_vface, xin, b, sub, xo, (void*)st);
+                                          o.stencil->f_vface, &q, xin, b, sub, xo, (void*)st);
+    }
     return o.sell ? mpbp_sell_jacobi_step(o.sell, xin, b, dg, sub, xo, (void*)st)
                   : mpbp_jacobi_step(o.csr, o.blk, xin, b, dg, sub, xo, (void*)st);
 }
@@ -1398,8 +1494,11 @@ int op_cheb(const OpRef& o, const double* xin, const double* b, const double* dg
             const double* sub, double* xo, hipStream_t st) {
     if (o.empty) return MPBP_OK;
     if (o.stencil)
+    {
+        const mpbp_row_part q = stencil_part(o);
         return mpbp_f_stencil_cheb_step(&o.stencil->f_prm, o.stencil->f_cell, o.stencil->f_uface,
-                                        o.stencil->f_vface, xin, b, c1, c2, d, sub, xo, (void*)st);
+                                        o.stencil->f_vface, &q, xin, b, c1, c2, d, sub, xo, (void*)st);
+    }
     return o.sell ? mpbp_sell_cheb_step(o.sell, xin, b, dg, c1, c2, d, sub, xo, (void*)st)
                   : mpbp_cheb_step(o.csr, o.blk, xin, b, dg, c1, c2, d, sub, xo, (void*)st);
 }
@@ -1410,8 +1509,9 @@ struct OpPair {
 
 OpPair make_op(const mpbp_schur_plan* p, const mpbp_csr& A, const mpbp_rowblocks& bi, const mpbp_rowblocks& bb,
                const mpbp_sell& si, const mpbp_sell& sb) {
-    if (p->use_sell) return OpPair{OpRef{&A, nullptr, &si, nullptr, false}, OpRef{&A, nullptr, &sb, nullptr, false}};
-    return OpPair{OpRef{&A, &bi, nullptr, nullptr, false}, OpRef{&A, &bb, nullptr, nullptr, false}};
+    if (p->use_sell)
+        return OpPair{OpRef{&A, nullptr, &si, nullptr, false, 0}, OpRef{&A, nullptr, &sb, nullptr, false, 0}};
+    return OpPair{OpRef{&A, &bi, nullptr, nullptr, false, 0}, OpRef{&A, &bb, nullptr, nullptr, false, 0}};
 }
 
 // Launch one sweep over interior rows, then (after the halo is complete) boundary rows.
@@ -1476,10 +1576,14 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
         if (!p->wp[i]) return set_error(MPBP_ERR_ARG, "schur_apply: missing pressure workspace");
     if (!p->wu_owned || !p->diag_F || !p->diag_P) return set_error(MPBP_ERR_ARG, "schur_apply: missing operands");
     const Ctx c{p, as_stream(stream)};
-    if (p->f_stencil && p->halo) return set_error(MPBP_ERR_ARG, "schur_apply: the F stencil is single-GPU only");
-    const OpPair F = p->f_stencil ? OpPair{OpRef{nullptr, nullptr, nullptr, p, false},
-                                           OpRef{nullptr, nullptr, nullptr, nullptr, true}}
-                                  : make_op(p, p->F, p->F_int, p->F_bnd, p->Fs_int, p->Fs_bnd);
+    if (p->f_stencil && p->halo && p->f_part.halo < 1)
+        return set_error(MPBP_ERR_ARG, "schur_apply: a partitioned F stencil needs f_part");
+    const bool part = p->f_stencil && p->f_part.halo > 0;
+    const OpPair F = !p->f_stencil ? make_op(p, p->F, p->F_int, p->F_bnd, p->Fs_int, p->Fs_bnd)
+                     : part ? OpPair{OpRef{nullptr, nullptr, nullptr, p, false, 1},
+                                     OpRef{nullptr, nullptr, nullptr, p, false, 2}}
+                            : OpPair{OpRef{nullptr, nullptr, nullptr, p, false, 0},
+                                     OpRef{nullptr, nullptr, nullptr, nullptr, true, 0}};
     const OpPair D = make_op(p, p->D, p->D_int, p->D_bnd, p->Ds_int, p->Ds_bnd);
     const OpPair G = make_op(p, p->G, p->G_int, p->G_bnd, p->Gs_int, p->Gs_bnd);
     const OpPair P = make_op(p, p->GtG, p->P_int, p->P_bnd, p->Ps_int, p->Ps_bnd);

@@ -165,7 +165,7 @@ class DistributedSchurPreconditioner(PlanProfiling):
     """
 
     def __init__(self, n, xi, eta_n, eta_s, c=1.0, d_u=-1.0, inner_F=None, inner_P=None, group=None,
-                 device=None, layout="sell"):
+                 device=None, layout="sell", f_mode="auto"):
         import torch.distributed as dist
         from .preconditioner import MultiphaseBlockPreconditioner
         from .solve import InnerSolver
@@ -177,6 +177,11 @@ class DistributedSchurPreconditioner(PlanProfiling):
         bp = MultiphaseBlockPreconditioner(n, xi, eta_n, eta_s, device=dev)
         _, _, F, D, G = bp.get_big_A_matrix(c=c, d_u=d_u)
         GtG, GtFG = bp.commutator_products(F, D, G)
+        if f_mode not in ("auto", "stencil", "assembled"):
+            raise ValueError("f_mode must be 'auto', 'stencil' or 'assembled'")
+        if f_mode == "stencil" and F.stencil is None:
+            raise ValueError("f_mode='stencil' needs n >= 3")
+        self.f_stencil = F.stencil if f_mode in ("auto", "stencil") else None
         # inner-solver bounds from the global operators: identical on every rank
         self.inner_F = (inner_F or InnerSolver()).resolve(F, F.diagonal())
         self.inner_P = (inner_P or InnerSolver()).resolve(GtG, GtG.diagonal())
@@ -265,6 +270,12 @@ class DistributedSchurPreconditioner(PlanProfiling):
         p.wu_owned = self._wu_owned.data_ptr()
         for i, t in enumerate(self._wp):
             p.wp[i] = t.data_ptr()
+        p.f_stencil = 1 if self.f_stencil is not None else 0
+        if self.f_stencil is not None:
+            st = self.f_stencil
+            p.f_prm = st.prm
+            p.f_cell, p.f_uface, p.f_vface = st.cell.data_ptr(), st.uface.data_ptr(), st.vface.data_ptr()
+            p.f_part = _lib.RowPart(self.part.r0, self.part.L, self.h_u if world > 1 else 0, 0)
         p.halo = self._cb if world > 1 else _lib.HALO_FN()
         p.halo_ctx = None
         p.prof_events = None

@@ -48,7 +48,7 @@ class FStencil:
         if out is None:
             out = torch.empty(4 * self.prm.n * self.prm.n, dtype=torch.float64, device=x.device)
         check(lib().mpbp_f_stencil_spmv(ctypes.byref(self.prm), ptr(self.cell), ptr(self.uface), ptr(self.vface),
-                                        mode, ptr(x), ptr(z), ptr(out), stream_handle()))
+                                        None, mode, ptr(x), ptr(z), ptr(out), stream_handle()))
         return out
 
 

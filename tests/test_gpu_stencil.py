@@ -49,13 +49,13 @@ def test_stencil_matvec_and_sweeps_bit_exact(n, prm):
     stencil_tabs = (ptr(st.cell), ptr(st.uface), ptr(st.vface))
     check(lib().mpbp_jacobi_step(ctypes.byref(F.cstruct()), ctypes.byref(blk), ptr(x), ptr(b), ptr(diag), ptr(sub),
                                  ptr(y1), stream_handle()))
-    check(lib().mpbp_f_stencil_jacobi_step(ctypes.byref(st.prm), *stencil_tabs, ptr(x), ptr(b), ptr(sub), ptr(y2),
+    check(lib().mpbp_f_stencil_jacobi_step(ctypes.byref(st.prm), *stencil_tabs, None, ptr(x), ptr(b), ptr(sub), ptr(y2),
                                            stream_handle()))
     assert _bits(y1, y2)
     d1, d2 = d0.clone(), d0.clone()
     check(lib().mpbp_cheb_step(ctypes.byref(F.cstruct()), ctypes.byref(blk), ptr(x), ptr(b), ptr(diag), 0.7, 1.3,
                                ptr(d1), None, ptr(y1), stream_handle()))
-    check(lib().mpbp_f_stencil_cheb_step(ctypes.byref(st.prm), *stencil_tabs, ptr(x), ptr(b), 0.7, 1.3, ptr(d2),
+    check(lib().mpbp_f_stencil_cheb_step(ctypes.byref(st.prm), *stencil_tabs, None, ptr(x), ptr(b), 0.7, 1.3, ptr(d2),
                                          None, ptr(y2), stream_handle()))
     assert _bits(y1, y2) and _bits(d1, d2)
 

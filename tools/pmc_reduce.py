@@ -1,0 +1,51 @@
+"""Reduce rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of tools/pmc_sweep.py to HBM bytes per F sweep.
+
+    python tools/pmc_reduce.py gpurun_out/<tag> [--write profiles/pmc_traffic.json]
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE
+reads exactly half of a wide (16 B/lane) coalesced stream, so the read side is doubled here
+("corrected"); WRITE_SIZE is exact for 16 B/lane streaming stores (ours are 8 B/lane -- uncalibrated,
+reported as read).  Both raw and corrected numbers are kept.
+"""
+import argparse
+import csv
+import json
+import os
+
+
+def mean_counter(path, counter, kernel_substr, grid):
+    vals = []
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter and kernel_substr in r["Kernel_Name"] and int(r["Grid_Size"]) == grid:
+            vals.append(float(r["Counter_Value"]))
+    return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("run_dir")
+    ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--write")
+    args = ap.parse_args()
+    grid = 4 * args.n * args.n
+    kernels = {"stencil": "k_f_stencil<(anonymous namespace)::EpiCheb>", "sell": "k_sell_rows<(anonymous namespace)::EpiCheb>"}
+    out = {"n": args.n, "source": args.run_dir}
+    for lay, kname in kernels.items():
+        res = {}
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            f = os.path.join(args.run_dir, f"pmc_{lay}_{c}", "pmc_counter_collection.csv")
+            if os.path.exists(f):
+                res[c] = mean_counter(f, c, kname, grid)
+        if "FETCH_SIZE" in res and res["FETCH_SIZE"][0] is not None and "WRITE_SIZE" in res:
+            fetch = res["FETCH_SIZE"][0] * 1024
+            write = res["WRITE_SIZE"][0] * 1024
+            out[lay] = {"fetch_bytes_raw": fetch, "write_bytes": write, "dispatches": res["FETCH_SIZE"][1],
+                        "traffic_bytes_corrected": 2 * fetch + write, "traffic_bytes_raw": fetch + write}
+    print(json.dumps(out, indent=1))
+    if args.write:
+        with open(args.write, "w") as fh:
+            json.dump(out, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()

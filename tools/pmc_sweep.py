@@ -34,7 +34,7 @@ def main():
         if args.layout == "stencil":
             st = F.stencil
             check(lib().mpbp_f_stencil_cheb_step(ctypes.byref(st.prm), ptr(st.cell), ptr(st.uface), ptr(st.vface),
-                                                 ptr(x), ptr(b), 0.3, 1.1, ptr(d), None, ptr(y), stream_handle()))
+                                                 None, ptr(x), ptr(b), 0.3, 1.1, ptr(d), None, ptr(y), stream_handle()))
         elif args.layout == "sell":
             check(lib().mpbp_sell_cheb_step(ctypes.byref(S.cstruct()), ptr(x), ptr(b), ptr(diag), 0.3, 1.1, ptr(d),
                                             None, ptr(y), stream_handle()))
