@@ -40,7 +40,7 @@ def sweep_bytes(pc, layout):
     nF, nnzF = F.shape[0], F.nnz
     if getattr(pc, "f_stencil", None) is not None:
         # matrix-free: x, b, d (r/w), x_out per row + the three thn tables read once (3 x 8 B per cell)
-        return nF * 8 * 5 + 3 * 8 * (nF // 4), "k_f_stencil<EpiCheb> (F Chebyshev sweep, matrix-free)"
+        return nF * 8 * 5 + 3 * 8 * (nF // 4), "k_f_cells / k_f_stencil <EpiCheb> (F Chebyshev sweep, matrix-free)"
     if layout == "sell":
         nsl = pc.sell_of("F").nslices
         return nnzF * 12 + nF * 1 + nF * 8 * 6 + nsl * 16, "k_sell_rows<EpiCheb> (F Chebyshev sweep, SELL-64)"
@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--layout", default="sell", choices=["sell", "csr"])
     ap.add_argument("--f-mode", default="auto", choices=["auto", "stencil", "assembled"],
                     help="F sweeps: recompute F from thn (stencil) or stream the assembled F")
+    ap.add_argument("--stencil-kind", default="cells", choices=["cells", "rows"],
+                    help="matrix-free F kernel: LDS-tiled cells or one row per thread")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-spmv", action="store_true")
@@ -86,6 +88,8 @@ def main():
             dist.init_process_group(backend)
 
     import mp_block_preconditioners_amd as mp
+    from mp_block_preconditioners_amd._lib import check as _check, lib as _lib
+    _check(_lib().mpbp_set_stencil_kind(0 if args.stencil_kind == "cells" else 1))
 
     n = args.n if (world == 1 or args.strong) else int(round(args.n * math.sqrt(world)))
     kf, sf = parse_inner(args.inner_f)
@@ -174,7 +178,8 @@ def main():
                        "n": n, "unknowns": 5 * n * n, "xi": args.xi, "eta_n": args.eta_n,
                        "eta_s": args.eta_s, "inner_F": f"{kf}:{sf}", "inner_P": f"{kp}:{spp}",
                        "parallelism": f"rows{world}" if world > 1 else "single", "layout": args.layout,
-                       "f_sweeps": "matrix-free" if getattr(pc, "f_stencil", None) is not None else "assembled"},
+                       "f_sweeps": ("matrix-free-" + args.stencil_kind) if getattr(pc, "f_stencil", None) is not None
+                       else "assembled"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
                          "bytes_per_launch": sbytes, "avg_launch_us": avg_sweep_s * 1e6,

@@ -254,6 +254,9 @@ int mpbp_f_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell, 
                              const double* b, double c1, double c2, double* d, const double* sub,
                              double* x_out, void* stream);
 
+/* F stencil kernel choice (process-wide): 0 = LDS-tiled cells (default), 1 = one row per thread. */
+int mpbp_set_stencil_kind(int32_t kind);
+
 /* gather: dst[i] = src[idx[i]] ; scatter: dst[idx[i]] = src[i]   (halo pack / unpack) */
 int mpbp_gather(int32_t count, const int32_t* idx, const double* src, double* dst, void* stream);
 int mpbp_scatter(int32_t count, const int32_t* idx, const double* src, double* dst, void* stream);

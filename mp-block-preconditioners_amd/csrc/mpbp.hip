@@ -18,6 +18,7 @@
 namespace {
 
 thread_local char g_err[1024] = "";
+int g_stencil_kind = 0;   // F stencil kernel: 0 LDS-tiled cells, 1 row per thread (mpbp_set_stencil_kind)
 
 int set_error(int code, const char* fmt, ...) {
     va_list ap;
@@ -484,6 +485,7 @@ struct EpiStore {
     double* y;
     struct P {};
     __device__ P pre(int32_t) const { return {}; }
+    __device__ P pre_lite(int32_t) const { return {}; }
     __device__ void operator()(int32_t r, double acc, const P&) const { y[r] = acc; }
 };
 struct EpiAdd {   // rhs = D Finv_v + v_p   (solve.py:259)
@@ -491,6 +493,7 @@ struct EpiAdd {   // rhs = D Finv_v + v_p   (solve.py:259)
     double* y;
     struct P { double z; };
     __device__ P pre(int32_t r) const { return {z[r]}; }
+    __device__ P pre_lite(int32_t r) const { return {z[r]}; }
     __device__ void operator()(int32_t r, double acc, const P& p) const { y[r] = acc + p.z; }
 };
 struct EpiResid {
@@ -498,6 +501,7 @@ struct EpiResid {
     double* y;
     struct P { double z; };
     __device__ P pre(int32_t r) const { return {z[r]}; }
+    __device__ P pre_lite(int32_t r) const { return {z[r]}; }
     __device__ void operator()(int32_t r, double acc, const P& p) const { y[r] = p.z - acc; }
 };
 struct EpiJacobi {   // x = (b - R x)/D in residual form (solve.py:158)
@@ -508,6 +512,8 @@ struct EpiJacobi {   // x = (b - R x)/D in residual form (solve.py:158)
     double* xout;
     struct P { double x, b, dg, s; };
     __device__ P pre(int32_t r) const { return {xin[r], b[r], diag ? diag[r] : 0.0, sub ? sub[r] : 0.0}; }
+    // x_in and diag supplied by the caller (set_x / set_diag)
+    __device__ P pre_lite(int32_t r) const { return {0.0, b[r], 0.0, sub ? sub[r] : 0.0}; }
     __device__ void operator()(int32_t r, double acc, const P& p) const {
         const double x = p.x + (p.b - acc) / p.dg;
         xout[r] = sub ? p.s - x : x;
@@ -523,6 +529,7 @@ struct EpiCheb {
     double* xout;
     struct P { double x, b, dg, d, s; };
     __device__ P pre(int32_t r) const { return {xin[r], b[r], diag ? diag[r] : 0.0, d[r], sub ? sub[r] : 0.0}; }
+    __device__ P pre_lite(int32_t r) const { return {0.0, b[r], 0.0, d[r], sub ? sub[r] : 0.0}; }
     __device__ void operator()(int32_t r, double acc, const P& p) const {
         const double z = (p.b - acc) / p.dg;
         const double dn = c1 * p.d + c2 * z;
@@ -537,6 +544,14 @@ __device__ inline double xi_of(double xi, double a) { return xi * a * (1.0 - a);
 
 template <class PT>
 __device__ inline void set_diag(PT& p, double d) { p.dg = d; }
+template <class PT>
+__device__ inline void set_x(PT& p, double x) { p.x = x; }
+template <>
+__device__ inline void set_x<EpiStore::P>(EpiStore::P&, double) {}
+template <>
+__device__ inline void set_x<EpiAdd::P>(EpiAdd::P&, double) {}
+template <>
+__device__ inline void set_x<EpiResid::P>(EpiResid::P&, double) {}
 template <>
 __device__ inline void set_diag<EpiStore::P>(EpiStore::P&, double) {}
 template <>
@@ -696,17 +711,16 @@ __global__ void __launch_bounds__(kBlock) k_sell_rows(Sell S, const double* __re
 // 12 bytes x 10 entries per row from HBM.  Needs n >= 3 (no coinciding periodic neighbours).
 struct Ent {
     int32_t c;   // phase-local global column: the sort key (CSR order of the assembled row)
-    int32_t g;   // index into x: global on one GPU, owned-then-ghost ("ext") under a row partition
     double v, x;
 };
 
 __device__ inline void cx(Ent& a, Ent& b) {   // compare-exchange by column, field-wise selects
     const bool s = a.c > b.c;
     const int32_t c0 = s ? b.c : a.c, c1 = s ? a.c : b.c;
-    const int32_t g0 = s ? b.g : a.g, g1 = s ? a.g : b.g;
     const double v0 = s ? b.v : a.v, v1 = s ? a.v : b.v;
-    a.c = c0; a.g = g0; a.v = v0;
-    b.c = c1; b.g = g1; b.v = v1;
+    const double x0 = s ? b.x : a.x, x1 = s ? a.x : b.x;
+    a.c = c0; a.v = v0; a.x = x0;
+    b.c = c1; b.v = v1; b.x = x1;
 }
 __device__ inline void sort4(Ent* e) {
     cx(e[0], e[1]); cx(e[2], e[3]); cx(e[0], e[2]); cx(e[1], e[3]); cx(e[1], e[2]);
@@ -734,78 +748,40 @@ struct FStencilDev {
     // row partition: this rank owns grid rows [r0, r0 + L) of each of the 4 velocity fields; ghosts
     // (h rows above, h below, per field) follow the 4*L*n owned entries.  One GPU: r0 = 0, L = n, h = 0.
     int r0, L, h, which;
-};
+    int pow2;      // n is a power of two: dx * dx is a power of two and v / (dx * dx) == v * idx2 exactly
 
-// Indices of grid point (field f, grid row gr, column gc) for gr in [r0-1, r0+L], gc in [-1, n].
-template <bool EDGE>
-struct Grid2 {
-    const FStencilDev& P;
-    int s;   // phase: ths = 1 - thn
-    __device__ int wrap(int a) const { return a < 0 ? a + P.n : (a >= P.n ? a - P.n : a); }
-    __device__ int32_t key(int gr, int gc) const {          // global cell index (sort key, tables)
-        return EDGE ? wrap(gr) * P.n + wrap(gc) : gr * P.n + gc;
-    }
-    __device__ int32_t xg(int f, int gr, int gc) const {    // where x holds that unknown
-        const int lr = gr - P.r0;
-        if (!EDGE) return (f * P.L + lr) * P.n + gc;
-        const int c = wrap(gc);
-        if (P.h == 0) return (f * P.L + wrap(gr)) * P.n + c;               // one GPU: global index
-        if (lr >= 0 && lr < P.L) return (f * P.L + lr) * P.n + c;
-        const int own = 4 * P.L * P.n;
-        return own + f * 2 * P.h * P.n + (lr < 0 ? (P.h - 1) : P.h) * P.n + c;   // row r0-1 / r0+L
-    }
-    __device__ double T(int gr, int gc) const { const double v = P.cell[key(gr, gc)]; return s ? 1.0 - v : v; }
-    __device__ Ent e(int f, int gr, int gc, int32_t base, double v) const {
-        return Ent{base + key(gr, gc), xg(f, gr, gc), v, 0.0};
+    __device__ int wrap(int a) const { return a < 0 ? a + n : (a >= n ? a - n : a); }
+    // index in x of (field f, grid row gr, column 0) for gr in [r0 - 1, r0 + L]
+    __device__ int32_t xrow(int f, int gr) const {
+        if (h == 0) return (f * n + wrap(gr)) * n;
+        const int lr = gr - r0;
+        if (lr >= 0 && lr < L) return (f * L + lr) * n;
+        return 4 * L * n + f * 2 * h * n + (lr < 0 ? (h - 1) : h) * n;    // ghost row r0-1 / r0+L
     }
 };
 
-// Scale the L entries into F entries, gather x, sort each block by column, sum in CSR order.
-template <int NLO, int NHI, bool EDGE>
-__device__ inline double f_row_finish(Ent (&lo)[NLO], Ent (&hi)[NHI], int32_t dcol, double fd, double eta,
-                                      double d_u, double vcross, int32_t xcross_idx, int p,
-                                      const double* __restrict__ x) {
-#pragma unroll
-    for (int t = 0; t < NLO; ++t) lo[t].v = (lo[t].c == dcol) ? fd : d_u * (eta * lo[t].v);
-#pragma unroll
-    for (int t = 0; t < NHI; ++t) hi[t].v = (hi[t].c == dcol) ? fd : d_u * (eta * hi[t].v);
-    if (EDGE) {   // wrapped neighbours can reorder the columns; interior rows are built sorted
-        sortk<NLO>(lo);
-        sortk<NHI>(hi);
-    }
-    const double xcross = x[xcross_idx];
-#pragma unroll
-    for (int t = 0; t < NLO; ++t) lo[t].x = x[lo[t].g];
-#pragma unroll
-    for (int t = 0; t < NHI; ++t) hi[t].x = x[hi[t].g];
-    double acc = 0.0;
-    if (p == 1) acc += vcross * xcross;
-#pragma unroll
-    for (int t = 0; t < NLO; ++t) acc += lo[t].v * lo[t].x;
-#pragma unroll
-    for (int t = 0; t < NHI; ++t) acc += hi[t].v * hi[t].x;
-    if (p == 0) acc += vcross * xcross;
-    return acc;
-}
-
-// acc = (F x)_R in assembled-CSR order; *fdiag = F_RR.  Same operations as phase_L_row / F_row.
-// Row = field f (p = f / 2 phase, f % 2: u / v), grid point (gr, gc).
-template <bool EDGE>
-__device__ inline double f_stencil_row(const FStencilDev& P, int f, int gr, int gc, const double* __restrict__ x,
-                                       double* fdiag) {
+// The ten entries of one F row, built in the assembled row's column order for interior points and
+// sorted (with fixed networks) where periodic wrap-around reorders them.  TA::T(s, gr, gc) is thn of
+// phase s at a cell, XA::X(f, gr, gc) the x entry of field f at a grid point (gr in [-1, n], gc in
+// [-1, n]; the accessors wrap).  Same operations as phase_L_row / F_row, same summation order.
+template <bool EDGE, class TA, class XA>
+__device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, const TA& ta, const XA& xa,
+                               double* fdiag) {
     const int n = P.n;
     const int32_t N = n * n;
     const int p = f >> 1;
-    const Grid2<EDGE> g{P, p};
     const double idx2 = P.idx2;
     const double eta = p ? P.eta_s : P.eta_n;
-    const int fu = 2 * p, fv = 2 * p + 1;                    // this phase's u / v fields
-    const int32_t kc = gr * n + gc;                          // the row's cell
-    const int32_t xcross = ((f ^ 2) * P.L + (gr - P.r0)) * n + gc;   // same point, other phase
+    const int fu = 2 * p, fv = 2 * p + 1;
+    const int32_t kc = gr * n + gc;
+    auto key = [&](int r, int c) -> int32_t { return EDGE ? P.wrap(r) * n + P.wrap(c) : r * n + c; };
+    auto T = [&](int r, int c) -> double { return ta.T(p, r, c); };
+    double acc = 0.0;
+    const double xcross = xa.X(f ^ 2, gr, gc);
     if ((f & 1) == 0) {   // u row: preconditioner.py:100-179
-        const double tij = g.T(gr, gc - 1), tip1j = g.T(gr, gc);
-        const double tijp1 = g.T(gr - 1, gc - 1), tip1jp1 = g.T(gr - 1, gc);
-        const double tijm1 = g.T(gr + 1, gc - 1), tip1jm1 = g.T(gr + 1, gc);
+        const double tij = T(gr, gc - 1), tip1j = T(gr, gc);
+        const double tijp1 = T(gr - 1, gc - 1), tip1jp1 = T(gr - 1, gc);
+        const double tijm1 = T(gr + 1, gc - 1), tip1jm1 = T(gr + 1, gc);
         const double iph_jph = 0.25 * (tij + tijp1 + tip1jp1 + tip1j);
         const double iph_jmh = 0.25 * (tij + tip1j + tijm1 + tip1jm1);
         const double iph_j = 0.5 * (tij + tip1j);
@@ -815,17 +791,28 @@ __device__ inline double f_stencil_row(const FStencilDev& P, int f, int gr, int 
         const double Ldiag = idx2 * (-tip1j - tij) + idx2 * (-iph_jph - iph_jmh);
         const double fd = (w - P.d_u * xi_ii) + P.d_u * (eta * Ldiag);
         *fdiag = fd;
-        Ent lo[5] = {g.e(fu, gr - 1, gc, 0, idx2 * (iph_jph)), g.e(fu, gr, gc - 1, 0, idx2 * (tij)),
-                     g.e(fu, gr, gc, 0, 0.0), g.e(fu, gr, gc + 1, 0, tip1j / P.dxdx),
-                     g.e(fu, gr + 1, gc, 0, idx2 * (iph_jmh))};
-        Ent hi[4] = {g.e(fv, gr, gc - 1, N, idx2 * (tij - iph_jph)), g.e(fv, gr, gc, N, idx2 * (-tip1j + iph_jph)),
-                     g.e(fv, gr + 1, gc - 1, N, idx2 * (iph_jmh - tij)),
-                     g.e(fv, gr + 1, gc, N, idx2 * (tip1j - iph_jmh))};
-        return f_row_finish<5, 4, EDGE>(lo, hi, kc, fd, eta, P.d_u, P.d_u * xi_ii, xcross, p, x);
+        const double du = P.d_u;
+        Ent lo[5] = {Ent{key(gr - 1, gc), du * (eta * (idx2 * (iph_jph))), xa.X(fu, gr - 1, gc)},
+                     Ent{key(gr, gc - 1), du * (eta * (idx2 * (tij))), xa.X(fu, gr, gc - 1)},
+                     Ent{key(gr, gc), fd, xa.X(fu, gr, gc)},
+                     Ent{key(gr, gc + 1), du * (eta * (P.pow2 ? tip1j * idx2 : tip1j / P.dxdx)), xa.X(fu, gr, gc + 1)},
+                     Ent{key(gr + 1, gc), du * (eta * (idx2 * (iph_jmh))), xa.X(fu, gr + 1, gc)}};
+        Ent hi[4] = {Ent{key(gr, gc - 1), du * (eta * (idx2 * (tij - iph_jph))), xa.X(fv, gr, gc - 1)},
+                     Ent{key(gr, gc), du * (eta * (idx2 * (-tip1j + iph_jph))), xa.X(fv, gr, gc)},
+                     Ent{key(gr + 1, gc - 1), du * (eta * (idx2 * (iph_jmh - tij))), xa.X(fv, gr + 1, gc - 1)},
+                     Ent{key(gr + 1, gc), du * (eta * (idx2 * (tip1j - iph_jmh))), xa.X(fv, gr + 1, gc)}};
+        if (EDGE) { sort5(lo); sort4(hi); }
+        const double vcross = du * xi_ii;
+        if (p == 1) acc += vcross * xcross;
+#pragma unroll
+        for (int t = 0; t < 5; ++t) acc += lo[t].v * lo[t].x;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc += hi[t].v * hi[t].x;
+        if (p == 0) acc += vcross * xcross;
     } else {              // v row: preconditioner.py:182-295
-        const double tij = g.T(gr, gc), tip1j = g.T(gr, gc + 1);
-        const double tijp1 = g.T(gr - 1, gc), tip1jp1 = g.T(gr - 1, gc + 1);
-        const double tim1j = g.T(gr, gc - 1), tim1jp1 = g.T(gr - 1, gc - 1);
+        const double tij = T(gr, gc), tip1j = T(gr, gc + 1);
+        const double tijp1 = T(gr - 1, gc), tip1jp1 = T(gr - 1, gc + 1);
+        const double tim1j = T(gr, gc - 1), tim1jp1 = T(gr - 1, gc - 1);
         const double ip1_jph = 0.5 * (tij + tijp1);
         const double xi_ii = xi_of(P.xi, ip1_jph);
         const double th = P.vface[kc];
@@ -835,18 +822,44 @@ __device__ inline double f_stencil_row(const FStencilDev& P, int f, int gr, int 
         const double Ldiag = P.midy2 * (tijp1 + tij) - idx2 * (iph_jph + imh_jph);
         const double fd = (w - P.d_u * xi_ii) + P.d_u * (eta * Ldiag);
         *fdiag = fd;
-        Ent lo[4] = {g.e(fu, gr - 1, gc, 0, idx2 * (tijp1 - imh_jph)),
-                     g.e(fu, gr - 1, gc + 1, 0, idx2 * (iph_jph - tijp1)),
-                     g.e(fu, gr, gc, 0, idx2 * (imh_jph - tij)), g.e(fu, gr, gc + 1, 0, idx2 * (tij - iph_jph))};
-        Ent hi[5] = {g.e(fv, gr - 1, gc, N, idx2 * tijp1), g.e(fv, gr, gc - 1, N, idx2 * imh_jph),
-                     g.e(fv, gr, gc, N, 0.0), g.e(fv, gr, gc + 1, N, idx2 * iph_jph),
-                     g.e(fv, gr + 1, gc, N, idx2 * tij)};
-        return f_row_finish<4, 5, EDGE>(lo, hi, N + kc, fd, eta, P.d_u, P.d_u * xi_ii, xcross, p, x);
+        const double du = P.d_u;
+        Ent lo[4] = {Ent{key(gr - 1, gc), du * (eta * (idx2 * (tijp1 - imh_jph))), xa.X(fu, gr - 1, gc)},
+                     Ent{key(gr - 1, gc + 1), du * (eta * (idx2 * (iph_jph - tijp1))), xa.X(fu, gr - 1, gc + 1)},
+                     Ent{key(gr, gc), du * (eta * (idx2 * (imh_jph - tij))), xa.X(fu, gr, gc)},
+                     Ent{key(gr, gc + 1), du * (eta * (idx2 * (tij - iph_jph))), xa.X(fu, gr, gc + 1)}};
+        Ent hi[5] = {Ent{key(gr - 1, gc), du * (eta * (idx2 * tijp1)), xa.X(fv, gr - 1, gc)},
+                     Ent{key(gr, gc - 1), du * (eta * (idx2 * imh_jph)), xa.X(fv, gr, gc - 1)},
+                     Ent{key(gr, gc), fd, xa.X(fv, gr, gc)},
+                     Ent{key(gr, gc + 1), du * (eta * (idx2 * iph_jph)), xa.X(fv, gr, gc + 1)},
+                     Ent{key(gr + 1, gc), du * (eta * (idx2 * tij)), xa.X(fv, gr + 1, gc)}};
+        if (EDGE) { sort4(lo); sort5(hi); }
+        const double vcross = du * xi_ii;
+        if (p == 1) acc += vcross * xcross;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc += lo[t].v * lo[t].x;
+#pragma unroll
+        for (int t = 0; t < 5; ++t) acc += hi[t].v * hi[t].x;
+        if (p == 0) acc += vcross * xcross;
     }
+    return acc;
 }
 
-// Thread t -> owned local row: which = 0 all rows, 1 rows not on the first / last owned grid row
-// of a field (they read no ghost), 2 rows on those grid rows.
+// Accessors reading global memory directly (k_f_stencil: one row per thread).
+struct TGlobal {
+    const FStencilDev& P;
+    __device__ double T(int s, int gr, int gc) const {
+        const double v = P.cell[P.wrap(gr) * P.n + P.wrap(gc)];
+        return s ? 1.0 - v : v;
+    }
+};
+struct XGlobal {
+    const FStencilDev& P;
+    const double* __restrict__ x;
+    __device__ double X(int f, int gr, int gc) const { return x[P.xrow(f, gr) + P.wrap(gc)]; }
+};
+
+// Thread t -> owned local row: which = 0 all rows, 1 rows off the first / last owned grid row of a
+// field (they read no ghost), 2 rows on those grid rows.
 __device__ inline bool f_stencil_rowof(const FStencilDev& P, int64_t t, int32_t* r) {
     const int n = P.n, L = P.L;
     int f, lr, gc;
@@ -879,6 +892,7 @@ __device__ inline bool f_stencil_rowof(const FStencilDev& P, int64_t t, int32_t*
     return true;
 }
 
+// One row per thread, every operand from global memory (reference form of the F stencil).
 template <class Epi>
 __global__ void __launch_bounds__(kBlock) k_f_stencil(FStencilDev P, const double* __restrict__ x, Epi epi) {
     const int b = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -888,13 +902,81 @@ __global__ void __launch_bounds__(kBlock) k_f_stencil(FStencilDev P, const doubl
     const int n = P.n;
     const int f = r / (P.L * n);
     const int32_t rem = r - f * P.L * n;
-    const int lr = rem / n, gc = rem - lr * n;
+    const int lr = rem / n, gc = rem - lr * n, gr = P.r0 + lr;
     double fd;
-    const bool edge = lr == 0 || lr == P.L - 1 || gc == 0 || gc == n - 1;
-    const double acc = edge ? f_stencil_row<true>(P, f, P.r0 + lr, gc, x, &fd)
-                            : f_stencil_row<false>(P, f, P.r0 + lr, gc, x, &fd);
+    const TGlobal ta{P};
+    const XGlobal xa{P, x};
+    const bool edge = gr == 0 || gr == n - 1 || gc == 0 || gc == n - 1;
+    const double acc = edge ? f_row<true>(P, f, gr, gc, ta, xa, &fd) : f_row<false>(P, f, gr, gc, ta, xa, &fd);
     set_diag(pe, fd);
     epi(r, acc, pe);
+}
+
+// ---- LDS-tiled cell kernel: one workgroup = 256 consecutive cells of one owned grid row, one thread
+// per cell computing that cell's 4 rows (u_n, v_n, u_s, v_s).  The workgroup first stages, with
+// coalesced loads, the rows gr-1, gr, gr+1 of x for all four fields and of the thn table (columns
+// c0-1 .. c0+256, wrapped) in LDS; every neighbour is then an LDS read.  Each x / thn value crosses
+// L2 -> CU once per workgroup instead of ~10 times per row.
+constexpr int kTileW = kBlock + 2;
+
+struct TLds {
+    const double* t;   // [3][kTileW]
+    int gr0, c0;       // grid row and first column of the tile
+    __device__ double T(int s, int gr, int gc) const {
+        const double v = t[(gr - gr0 + 1) * kTileW + (gc - c0 + 1)];
+        return s ? 1.0 - v : v;
+    }
+};
+struct XLds {
+    const double* x;   // [4][3][kTileW]
+    int gr0, c0;
+    __device__ double X(int f, int gr, int gc) const { return x[(f * 3 + (gr - gr0 + 1)) * kTileW + (gc - c0 + 1)]; }
+};
+
+template <class Epi>
+__global__ void __launch_bounds__(kBlock) k_f_cells(FStencilDev P, const double* __restrict__ x, Epi epi) {
+    __shared__ double sx[4 * 3 * kTileW];
+    __shared__ double st[3 * kTileW];
+    const int n = P.n, L = P.L;
+    const int strips = (n + kBlock - 1) / kBlock;
+    const int b = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int strip = b % strips, rsel = b / strips;
+    const int lr = P.which == 0 ? rsel : P.which == 1 ? 1 + rsel : (rsel == 0 ? 0 : L - 1);
+    const int gr = P.r0 + lr;
+    const int c0 = strip * kBlock;
+    const int tid = threadIdx.x;
+    // stage x (4 fields x 3 rows) and thn (3 rows), columns c0-1 .. c0+256
+    for (int q = tid; q < 15 * kTileW; q += kBlock) {
+        const int row = q / kTileW, col = q - row * kTileW;
+        const int gc = P.wrap(c0 - 1 + col);
+        if (row < 12) {
+            const int f = row / 3, dr = row - f * 3 - 1;
+            sx[q] = (c0 - 1 + col <= n) ? x[P.xrow(f, gr + dr) + gc] : 0.0;
+        } else {
+            const int dr = row - 12 - 1;
+            st[q - 12 * kTileW] = (c0 - 1 + col <= n) ? P.cell[P.wrap(gr + dr) * n + gc] : 0.0;
+        }
+    }
+    const int gc = c0 + tid;
+    const bool live = gc < n;
+    typename Epi::P pe[4];
+    if (live) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) pe[f] = epi.pre_lite((f * L + lr) * n + gc);
+    }
+    __syncthreads();
+    if (!live) return;
+    const TLds ta{st, gr, c0};
+    const XLds xa{sx, gr, c0};
+    const bool edge = gr == 0 || gr == n - 1 || gc == 0 || gc == n - 1;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+        double fd;
+        const double acc = edge ? f_row<true>(P, f, gr, gc, ta, xa, &fd) : f_row<false>(P, f, gr, gc, ta, xa, &fd);
+        set_x(pe[f], xa.X(f, gr, gc));
+        set_diag(pe[f], fd);
+        epi((f * L + lr) * n + gc, acc, pe[f]);
+    }
 }
 
 // One thread per (slice, lane): copy the CSR row into its column-major slots.
@@ -985,6 +1067,12 @@ void cheb_coeffs(double lmin, double lmax, int sweeps, double* c1, double* c2) {
 extern "C" {
 
 const char* mpbp_version(void) { return "libmpbp 0.1 (gfx950)"; }
+
+int mpbp_set_stencil_kind(int32_t kind) {
+    if (kind < 0 || kind > 1) return set_error(MPBP_ERR_ARG, "stencil kind must be 0 (cells) or 1 (rows)");
+    g_stencil_kind = kind;
+    return MPBP_OK;
+}
 const char* mpbp_last_error(void) { return g_err; }
 
 int mpbp_stokes_theta(int32_t n, double* cell, double* uface, double* vface, void* stream) {
@@ -1382,7 +1470,8 @@ static int make_fstencil(const mpbp_stokes_params* prm, const double* cell, cons
             return set_error(MPBP_ERR_ARG, "f_stencil: bad row partition");
     }
     *P = FStencilDev{prm->n, prm->xi, prm->eta_n, prm->eta_s, prm->c, prm->d_u, cell, uface, vface,
-                     dx * dx, 1.0 / (dx * dx), -1.0 / (dx * dx), r0, L, h, which};
+                     dx * dx, 1.0 / (dx * dx), -1.0 / (dx * dx), r0, L, h, which,
+                     (prm->n & (prm->n - 1)) == 0 ? 1 : 0};
     return MPBP_OK;
 }
 
@@ -1391,11 +1480,14 @@ static int make_fstencil(const mpbp_stokes_params* prm, const double* cell, cons
 namespace {
 template <class Epi>
 int launch_fstencil(const FStencilDev& P, const double* x, Epi epi, hipStream_t st) {
-    const int64_t rows = P.which == 0 ? (int64_t)4 * P.L * P.n
-                       : P.which == 1 ? (int64_t)4 * (P.L > 2 ? P.L - 2 : 0) * P.n
-                                      : (int64_t)4 * (P.L >= 2 ? 2 : 1) * P.n;
-    if (rows == 0) return MPBP_OK;
-    k_f_stencil<Epi><<<grid_for(rows), kBlock, 0, st>>>(P, x, epi);
+    const int64_t grows = P.which == 0 ? P.L : P.which == 1 ? (P.L > 2 ? P.L - 2 : 0) : (P.L >= 2 ? 2 : 1);
+    if (grows == 0) return MPBP_OK;
+    if (g_stencil_kind == 0) {   // LDS-tiled cells (default)
+        const int64_t blocks = grows * ((P.n + kBlock - 1) / kBlock);
+        k_f_cells<Epi><<<(unsigned)blocks, kBlock, 0, st>>>(P, x, epi);
+    } else {                     // one row per thread, global operands
+        k_f_stencil<Epi><<<grid_for(4 * grows * P.n), kBlock, 0, st>>>(P, x, epi);
+    }
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }

@@ -29,9 +29,17 @@ def _bits(a, b):
 PARAMS = [(1.0, 100.0, 1.0, 1.0, -1.0), (2.5, 1.0e4, 1.0, 0.5, -2.0), (1.0, 1.0, 1.0, 0.0, -1.0)]
 
 
-@pytest.mark.parametrize("n", [3, 4, 17, 64, 255])
+@pytest.fixture(params=[0, 1], ids=["cells-lds", "rows"])
+def stencil_kind(request):
+    from mp_block_preconditioners_amd._lib import check, lib
+    check(lib().mpbp_set_stencil_kind(request.param))
+    yield request.param
+    check(lib().mpbp_set_stencil_kind(0))
+
+
+@pytest.mark.parametrize("n", [3, 4, 17, 64, 255, 300])
 @pytest.mark.parametrize("prm", PARAMS, ids=["visc", "stiff", "c0"])
-def test_stencil_matvec_and_sweeps_bit_exact(n, prm):
+def test_stencil_matvec_and_sweeps_bit_exact(n, prm, stencil_kind):
     import mp_block_preconditioners_amd as mp
     from mp_block_preconditioners_amd._lib import check, lib, ptr, stream_handle
     xi, eta_n, eta_s, c, d_u = prm
@@ -61,7 +69,7 @@ def test_stencil_matvec_and_sweeps_bit_exact(n, prm):
 
 
 @pytest.mark.parametrize("n", [3, 32, 96])
-def test_stencil_apply_matches_assembled_and_oracle(n):
+def test_stencil_apply_matches_assembled_and_oracle(n, stencil_kind):
     import mp_block_preconditioners_amd as mp
     from oracle.schur_oracle import Inner, approx_schur_apply
     from oracle.stokes_oracle import StokesSystem, theta_tables
