@@ -945,17 +945,27 @@ __global__ void __launch_bounds__(kBlock) k_f_cells(FStencilDev P, const double*
     const int gr = P.r0 + lr;
     const int c0 = strip * kBlock;
     const int tid = threadIdx.x;
-    // stage x (4 fields x 3 rows) and thn (3 rows), columns c0-1 .. c0+256
-    for (int q = tid; q < 15 * kTileW; q += kBlock) {
-        const int row = q / kTileW, col = q - row * kTileW;
-        const int gc = P.wrap(c0 - 1 + col);
-        if (row < 12) {
-            const int f = row / 3, dr = row - f * 3 - 1;
-            sx[q] = (c0 - 1 + col <= n) ? x[P.xrow(f, gr + dr) + gc] : 0.0;
-        } else {
-            const int dr = row - 12 - 1;
-            st[q - 12 * kTileW] = (c0 - 1 + col <= n) ? P.cell[P.wrap(gr + dr) * n + gc] : 0.0;
-        }
+    // stage x (4 fields x 3 rows) and thn (3 rows), columns c0-1 .. c0+256: per tile row one
+    // wave-uniform base (scalar unit) and one coalesced load per thread (+2 halo columns)
+    const int colA = c0 - 1 + tid;                         // tile column tid
+    const bool okA = colA <= n;
+    const int gcA = P.wrap(colA);
+    const bool extra = tid < 2;                            // tile columns 256, 257
+    const int colB = c0 + kBlock - 1 + tid;
+    const bool okB = extra && colB <= n;
+    const int gcB = P.wrap(colB < n ? colB : (colB == n ? n : 0));
+#pragma unroll
+    for (int row = 0; row < 12; ++row) {
+        const int f = row / 3, dr = row - f * 3 - 1;
+        const int32_t base = P.xrow(f, gr + dr);
+        sx[row * kTileW + tid] = okA ? x[base + gcA] : 0.0;
+        if (extra) sx[row * kTileW + kBlock + tid] = okB ? x[base + gcB] : 0.0;
+    }
+#pragma unroll
+    for (int row = 0; row < 3; ++row) {
+        const int32_t base = P.wrap(gr + row - 1) * n;
+        st[row * kTileW + tid] = okA ? P.cell[base + gcA] : 0.0;
+        if (extra) st[row * kTileW + kBlock + tid] = okB ? P.cell[base + gcB] : 0.0;
     }
     const int gc = c0 + tid;
     const bool live = gc < n;
@@ -1543,6 +1553,14 @@ struct Ctx {
     hipStream_t st;
 };
 
+// Profiling events are recorded only on eager (uncaptured) launches: a capturing stream skips them.
+hipError_t record_event(hipEvent_t ev, hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    hipError_t e = hipStreamIsCapturing(st, &cs);
+    if (e != hipSuccess) return e;
+    return cs == hipStreamCaptureStatusNone ? hipEventRecord(ev, st) : hipSuccess;
+}
+
 // One operator of the apply, restricted to interior or boundary rows, in CSR or SELL form.
 struct OpRef {
     const mpbp_csr* csr;
@@ -1642,15 +1660,17 @@ int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag
         double* nxt = last ? dst : (cur == ping ? pong : ping);
         const double* sb = last ? sub : nullptr;
         const mpbp_schur_plan* p = c.p;
-        const bool rec = profile && p->prof_events && p->prof_count && *p->prof_count < p->prof_capacity;
-        if (rec) MPBP_HIP(hipEventRecord((hipEvent_t)p->prof_events[2 * *p->prof_count], c.st));
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        const bool rec = profile && p->prof_events && p->prof_count && *p->prof_count < p->prof_capacity &&
+                         hipStreamIsCapturing(c.st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone;
+        if (rec) MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count], c.st));
         rc = two_phase(c, kind, cur, op, [&](const OpRef& o) {
             return cheb ? op_cheb(o, cur, b, diag, c1[s], c2[s], dir, sb, nxt, c.st)
                         : op_jacobi(o, cur, b, diag, sb, nxt, c.st);
         });
         if (rc) return rc;
         if (rec) {
-            MPBP_HIP(hipEventRecord((hipEvent_t)p->prof_events[2 * *p->prof_count + 1], c.st));
+            MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count + 1], c.st));
             ++*p->prof_count;
         }
         cur = nxt;

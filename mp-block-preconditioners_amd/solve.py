@@ -193,6 +193,25 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
         check(lib().mpbp_schur_apply(ctypes.byref(self._plan), ptr(v), ptr(out), stream_handle()))
         return out
 
+    def capture(self, v: torch.Tensor, out: torch.Tensor):
+        """Capture one apply(v, out) into a hipGraph (torch.cuda.CUDAGraph); replay() re-runs it on the
+        same buffers.  mpbp_schur_apply allocates and synchronises nothing, so the whole apply becomes
+        one graph launch (profiling events are recorded by eager applies only)."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        saved = (self._plan.prof_events, self._plan.prof_capacity)
+        self._plan.prof_events, self._plan.prof_capacity = None, 0
+        try:
+            with torch.cuda.stream(s):
+                self.apply(v, out)                  # warm-up on a side stream, as torch requires
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.apply(v, out)
+        finally:
+            self._plan.prof_events, self._plan.prof_capacity = saved
+        return g
+
     def _matvec(self, x):
         v = torch.from_numpy(np.ascontiguousarray(np.ravel(x), dtype=np.float64)).to(self.device)
         return self.apply(v).cpu().numpy()

@@ -100,3 +100,29 @@ def test_stencil_rejected_where_undefined():
         mp.ApproxSchurPreconditioner(F, D, G, f_mode="stencil")
     pc = mp.ApproxSchurPreconditioner(F, D, G, f_mode="auto")
     assert pc.f_stencil is None
+
+
+def test_graph_replay_matches_eager():
+    """The apply captured into a hipGraph (bench.py's launch mode) replays to the eager result."""
+    import mp_block_preconditioners_amd as mp
+    bp = mp.MultiphaseBlockPreconditioner(48, 1.0, 100.0, 1.0)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    pc = mp.ApproxSchurPreconditioner(F, D, G)
+    v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda")
+    ref = pc.apply(v).clone()
+    out = torch.zeros_like(v)
+    pc.enable_profiling(8)
+    g = pc.capture(v, out)
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert pc.profiled_ms() == []              # no events are recorded under capture
+    pc.apply(v)
+    torch.cuda.synchronize()
+    ms = pc.profiled_ms()
+    pc.disable_profiling()
+    assert len(ms) == 6 and all(t > 0 for t in ms)
+    v.copy_(torch.randn_like(v))             # replay reads the captured buffers' new contents
+    g.replay()
+    assert torch.equal(out, pc.apply(v))
