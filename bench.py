@@ -15,6 +15,7 @@ system scaled to 1024^2-cell equivalents (n_N^2 / 1024^2 per apply; exactly appl
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import math
 import os
@@ -158,15 +159,18 @@ def main():
     if A is not None and not args.no_spmv:
         spmv = spmv_bench(A, gen)
 
+    # HBM bytes per F sweep from the committed rocprofv3 PMC passes (tools/pmc_sweep.py +
+    # tools/pmc_reduce.py: FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction + WRITE_SIZE)
     traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path):
+    pmc_files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic_r*.json")))
+    if pmc_files and world == 1:
         try:
-            with open(pmc_path) as f:
+            with open(pmc_files[-1]) as f:
                 pm = json.load(f)
-            if int(pm.get("n", -1)) == n and pm.get("layout") == args.layout:
-                traffic = pm.get("cheb_F_sweep_bytes")
-        except (OSError, ValueError):
+            key = "stencil" if getattr(pc, "f_stencil", None) is not None else args.layout
+            if int(pm.get("n", -1)) == n and key in pm:
+                traffic = pm[key]["traffic_bytes_corrected"]
+        except (OSError, ValueError, KeyError):
             traffic = None
 
     cpu = None

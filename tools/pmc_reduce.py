@@ -28,14 +28,16 @@ def main():
     ap.add_argument("--write")
     args = ap.parse_args()
     grid = 4 * args.n * args.n
-    kernels = {"stencil": "k_f_stencil<(anonymous namespace)::EpiCheb>", "sell": "k_sell_rows<(anonymous namespace)::EpiCheb>"}
+    # F sweep kernels and their launch grids (threads): the cell kernel runs one thread per cell
+    kernels = {"stencil": ("k_f_cells<(anonymous namespace)::EpiCheb>", grid // 4),
+               "sell": ("k_sell_rows<(anonymous namespace)::EpiCheb>", grid)}
     out = {"n": args.n, "source": args.run_dir}
-    for lay, kname in kernels.items():
+    for lay, (kname, kgrid) in kernels.items():
         res = {}
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
             f = os.path.join(args.run_dir, f"pmc_{lay}_{c}", "pmc_counter_collection.csv")
             if os.path.exists(f):
-                res[c] = mean_counter(f, c, kname, grid)
+                res[c] = mean_counter(f, c, kname, kgrid)
         if "FETCH_SIZE" in res and res["FETCH_SIZE"][0] is not None and "WRITE_SIZE" in res:
             fetch = res["FETCH_SIZE"][0] * 1024
             write = res["WRITE_SIZE"][0] * 1024
