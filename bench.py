@@ -64,8 +64,9 @@ def main():
     ap.add_argument("--layout", default="sell", choices=["sell", "csr"])
     ap.add_argument("--f-mode", default="auto", choices=["auto", "stencil", "assembled"],
                     help="F sweeps: recompute F from thn (stencil) or stream the assembled F")
-    ap.add_argument("--stencil-kind", default="cells", choices=["cells", "rows"],
-                    help="matrix-free F kernel: LDS-tiled cells or one row per thread")
+    ap.add_argument("--stencil-kind", default="march4",
+                    help="matrix-free F kernel: cells (LDS tile per grid row), rows (row per thread), "
+                         "marchR (LDS ring marching R grid rows per workgroup)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-spmv", action="store_true")
@@ -91,7 +92,8 @@ def main():
 
     import mp_block_preconditioners_amd as mp
     from mp_block_preconditioners_amd._lib import check as _check, lib as _lib
-    _check(_lib().mpbp_set_stencil_kind(0 if args.stencil_kind == "cells" else 1))
+    sk = args.stencil_kind
+    _check(_lib().mpbp_set_stencil_kind(0 if sk == "cells" else 1 if sk == "rows" else 2 + int(sk[5:] or 4)))
 
     n = args.n if (world == 1 or args.strong) else int(round(args.n * math.sqrt(world)))
     kf, sf = parse_inner(args.inner_f)

@@ -254,7 +254,8 @@ int mpbp_f_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell, 
                              const double* b, double c1, double c2, double* d, const double* sub,
                              double* x_out, void* stream);
 
-/* F stencil kernel choice (process-wide): 0 = LDS-tiled cells (default), 1 = one row per thread. */
+/* F stencil kernel choice (process-wide): 0 = LDS-tiled cells, 1 = one row per thread,
+ * 2 = marching cells, 4 grid rows per workgroup (default), 2 + R = marching cells, R rows per workgroup. */
 int mpbp_set_stencil_kind(int32_t kind);
 
 /* gather: dst[i] = src[idx[i]] ; scatter: dst[idx[i]] = src[i]   (halo pack / unpack) */

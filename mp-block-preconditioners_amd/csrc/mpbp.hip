@@ -18,7 +18,8 @@
 namespace {
 
 thread_local char g_err[1024] = "";
-int g_stencil_kind = 0;   // F stencil kernel: 0 LDS-tiled cells, 1 row per thread (mpbp_set_stencil_kind)
+int g_stencil_kind = 2;   // F stencil kernel: 0 LDS-tiled cells, 1 row per thread, 2 marching cells (default)
+int g_march_rows = 4;     // grid rows per workgroup of the marching kernel (4 is fastest at 1024^2)
 
 int set_error(int code, const char* fmt, ...) {
     va_list ap;
@@ -989,6 +990,113 @@ __global__ void __launch_bounds__(kBlock) k_f_cells(FStencilDev P, const double*
     }
 }
 
+// ---- marching variant: a workgroup owns a 256-column strip of `rows` consecutive grid rows and walks
+// down it with a 3-row LDS ring per field (+ thn).  Each step stages ONE new grid row (its loads are
+// issued before the current row is computed, so their latency hides under the arithmetic) instead of
+// three, and the epilogue operands of the next row are requested a step ahead as well.
+struct XRing {
+    const double* x;   // [4][3][kTileW]
+    int s[3];          // ring slot of rows gr-1, gr, gr+1
+    int gr, c0;
+    __device__ double X(int f, int r, int c) const { return x[(f * 3 + s[r - gr + 1]) * kTileW + (c - c0 + 1)]; }
+};
+struct TRing {
+    const double* t;   // [3][kTileW]
+    int s[3];
+    int gr, c0;
+    __device__ double T(int sph, int r, int c) const {
+        const double v = t[s[r - gr + 1] * kTileW + (c - c0 + 1)];
+        return sph ? 1.0 - v : v;
+    }
+};
+
+// Row of tile values held in registers between its global load and its LDS store.
+struct TileRow {
+    double xa[4], ta, xb[4], tb;
+};
+
+__device__ inline void load_tile_row(const FStencilDev& P, const double* __restrict__ x, int gr, int gcA, bool okA,
+                                     int gcB, bool okB, TileRow& tr) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+        const int32_t base = P.xrow(f, gr);
+        tr.xa[f] = okA ? x[base + gcA] : 0.0;
+        tr.xb[f] = okB ? x[base + gcB] : 0.0;
+    }
+    const int32_t tb = P.wrap(gr) * P.n;
+    tr.ta = okA ? P.cell[tb + gcA] : 0.0;
+    tr.tb = okB ? P.cell[tb + gcB] : 0.0;
+}
+
+__device__ inline void store_tile_row(double* sx, double* st, int slot, int tid, bool extra, const TileRow& tr) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+        sx[(f * 3 + slot) * kTileW + tid] = tr.xa[f];
+        if (extra) sx[(f * 3 + slot) * kTileW + kBlock + tid] = tr.xb[f];
+    }
+    st[slot * kTileW + tid] = tr.ta;
+    if (extra) st[slot * kTileW + kBlock + tid] = tr.tb;
+}
+
+template <class Epi>
+__global__ void __launch_bounds__(kBlock) k_f_march(FStencilDev P, const double* __restrict__ x, int rows_per_block,
+                                                    Epi epi) {
+    __shared__ double sx[4 * 3 * kTileW];
+    __shared__ double st[3 * kTileW];
+    const int n = P.n, L = P.L;
+    const int strips = (n + kBlock - 1) / kBlock;
+    const int b = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int strip = b % strips, chunk = b / strips;
+    const int lo = P.which == 1 ? 1 : 0, hi = P.which == 1 ? L - 1 : L;   // owned grid rows to compute
+    const int la = lo + chunk * rows_per_block;
+    const int lb = min(la + rows_per_block, hi);
+    if (la >= lb) return;
+    const int c0 = strip * kBlock, tid = threadIdx.x;
+    const int colA = c0 - 1 + tid;
+    const bool okA = colA <= n;
+    const int gcA = P.wrap(colA);
+    const bool extra = tid < 2;
+    const int colB = c0 + kBlock - 1 + tid;
+    const bool okB = extra && colB <= n;
+    const int gcB = P.wrap(colB < n ? colB : (colB == n ? n : 0));
+    const int gc = c0 + tid;
+    const bool live = gc < n;
+    // prologue: rows la-1 -> slot 0, la -> slot 1; row la+1 in registers
+    TileRow tr;
+    load_tile_row(P, x, P.r0 + la - 1, gcA, okA, gcB, okB, tr);
+    store_tile_row(sx, st, 0, tid, extra, tr);
+    load_tile_row(P, x, P.r0 + la, gcA, okA, gcB, okB, tr);
+    store_tile_row(sx, st, 1, tid, extra, tr);
+    load_tile_row(P, x, P.r0 + la + 1, gcA, okA, gcB, okB, tr);
+    for (int lr = la; lr < lb; ++lr) {
+        const int k = lr - la;
+        const int sm = k % 3, s0 = (k + 1) % 3, sp = (k + 2) % 3;
+        typename Epi::P pe[4];
+        if (live) {                                          // epilogue operands of row lr, in flight
+#pragma unroll
+            for (int f = 0; f < 4; ++f) pe[f] = epi.pre_lite((f * L + lr) * n + gc);
+        }
+        store_tile_row(sx, st, sp, tid, extra, tr);          // row lr+1
+        __syncthreads();
+        if (lr + 1 < lb) load_tile_row(P, x, P.r0 + lr + 2, gcA, okA, gcB, okB, tr);   // in flight
+        if (live) {
+            const int gr = P.r0 + lr;
+            const XRing xa{sx, {sm, s0, sp}, gr, c0};
+            const TRing ta{st, {sm, s0, sp}, gr, c0};
+            const bool edge = gr == 0 || gr == n - 1 || gc == 0 || gc == n - 1;
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                double fd;
+                const double acc = edge ? f_row<true>(P, f, gr, gc, ta, xa, &fd) : f_row<false>(P, f, gr, gc, ta, xa, &fd);
+                set_diag(pe[f], fd);
+                set_x(pe[f], xa.X(f, gr, gc));
+                epi((f * L + lr) * n + gc, acc, pe[f]);
+            }
+        }
+        __syncthreads();                                     // slot sm is rewritten next step
+    }
+}
+
 // One thread per (slice, lane): copy the CSR row into its column-major slots.
 __global__ void k_sell_fill(Csr A, const int4* slices, int nslices, uint8_t* rlen, double* val, int32_t* col) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1079,8 +1187,11 @@ extern "C" {
 const char* mpbp_version(void) { return "libmpbp 0.1 (gfx950)"; }
 
 int mpbp_set_stencil_kind(int32_t kind) {
-    if (kind < 0 || kind > 1) return set_error(MPBP_ERR_ARG, "stencil kind must be 0 (cells) or 1 (rows)");
-    g_stencil_kind = kind;
+    // kind: 0 cells, 1 rows, 2 + R (R >= 1): marching cells, R grid rows per workgroup (2 -> R = 8)
+    if (kind < 0) return set_error(MPBP_ERR_ARG, "stencil kind must be 0 (cells), 1 (rows) or 2+R (march)");
+    g_stencil_kind = kind > 2 ? 2 : kind;
+    if (kind > 2) g_march_rows = kind - 2;
+    else if (kind == 2) g_march_rows = 4;
     return MPBP_OK;
 }
 const char* mpbp_last_error(void) { return g_err; }
@@ -1492,7 +1603,11 @@ template <class Epi>
 int launch_fstencil(const FStencilDev& P, const double* x, Epi epi, hipStream_t st) {
     const int64_t grows = P.which == 0 ? P.L : P.which == 1 ? (P.L > 2 ? P.L - 2 : 0) : (P.L >= 2 ? 2 : 1);
     if (grows == 0) return MPBP_OK;
-    if (g_stencil_kind == 0) {   // LDS-tiled cells (default)
+    if (g_stencil_kind == 2 && P.which != 2) {   // marching LDS ring
+        const int64_t chunks = (grows + g_march_rows - 1) / g_march_rows;
+        const int64_t blocks = chunks * ((P.n + kBlock - 1) / kBlock);
+        k_f_march<Epi><<<(unsigned)blocks, kBlock, 0, st>>>(P, x, g_march_rows, epi);
+    } else if (g_stencil_kind != 1) {   // LDS-tiled cells (default)
         const int64_t blocks = grows * ((P.n + kBlock - 1) / kBlock);
         k_f_cells<Epi><<<(unsigned)blocks, kBlock, 0, st>>>(P, x, epi);
     } else {                     // one row per thread, global operands

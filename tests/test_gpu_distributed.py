@@ -20,13 +20,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, layout, f_mode, errfile):
+def _worker(rank, world, port, n, layout, f_mode, kind, errfile):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         import mp_block_preconditioners_amd as mpb
         from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
+        mpb.lib().mpbp_set_stencil_kind(kind)
         iF, iP = mpb.InnerSolver("chebyshev", 4), mpb.InnerSolver("chebyshev", 3)
         dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, layout=layout,
                                              f_mode=f_mode)
@@ -49,15 +50,16 @@ def _worker(rank, world, port, n, layout, f_mode, errfile):
         raise
 
 
-@pytest.mark.parametrize("world,n,layout,f_mode", [(2, 64, "sell", "stencil"), (2, 64, "sell", "assembled"),
-                                                   (2, 64, "csr", "assembled"), (3, 50, "sell", "stencil"),
-                                                   (4, 9, "csr", "stencil")])
-def test_distributed_apply_matches_single_gpu(world, n, layout, f_mode, tmp_path):
+@pytest.mark.parametrize("world,n,layout,f_mode,kind", [(2, 64, "sell", "stencil", 2), (2, 64, "sell", "assembled", 2),
+                                                        (2, 64, "csr", "assembled", 0), (3, 50, "sell", "stencil", 0),
+                                                        (4, 9, "csr", "stencil", 0), (2, 64, "sell", "stencil", 1),
+                                                        (3, 50, "sell", "stencil", 2 + 4), (4, 9, "sell", "stencil", 2 + 3)])
+def test_distributed_apply_matches_single_gpu(world, n, layout, f_mode, kind, tmp_path):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     errfile = str(tmp_path / "err.txt")
     try:
-        mp.spawn(_worker, args=(world, _free_port(), n, layout, f_mode, errfile), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), n, layout, f_mode, kind, errfile), nprocs=world, join=True)
     except Exception:
         msg = open(errfile).read() if os.path.exists(errfile) else ""
         pytest.fail(f"distributed worker failed:\n{msg}")

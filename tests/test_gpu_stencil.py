@@ -29,12 +29,12 @@ def _bits(a, b):
 PARAMS = [(1.0, 100.0, 1.0, 1.0, -1.0), (2.5, 1.0e4, 1.0, 0.5, -2.0), (1.0, 1.0, 1.0, 0.0, -1.0)]
 
 
-@pytest.fixture(params=[0, 1], ids=["cells-lds", "rows"])
+@pytest.fixture(params=[0, 1, 2 + 3, 2 + 8], ids=["cells-lds", "rows", "march3", "march8"])
 def stencil_kind(request):
     from mp_block_preconditioners_amd._lib import check, lib
     check(lib().mpbp_set_stencil_kind(request.param))
     yield request.param
-    check(lib().mpbp_set_stencil_kind(0))
+    check(lib().mpbp_set_stencil_kind(2))
 
 
 @pytest.mark.parametrize("n", [3, 4, 17, 64, 255, 300])
