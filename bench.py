@@ -41,7 +41,7 @@ def sweep_bytes(pc, layout):
     nF, nnzF = F.shape[0], F.nnz
     if getattr(pc, "f_stencil", None) is not None:
         # matrix-free: x, b, d (r/w), x_out per row + the three thn tables read once (3 x 8 B per cell)
-        return nF * 8 * 5 + 3 * 8 * (nF // 4), "k_f_cells / k_f_stencil <EpiCheb> (F Chebyshev sweep, matrix-free)"
+        return nF * 8 * 5 + 3 * 8 * (nF // 4), "k_march<FStencilDev, XPlain, EpiCheb> (F Chebyshev sweep, matrix-free)"
     if layout == "sell":
         nsl = pc.sell_of("F").nslices
         return nnzF * 12 + nF * 1 + nF * 8 * 6 + nsl * 16, "k_sell_rows<EpiCheb> (F Chebyshev sweep, SELL-64)"
@@ -64,6 +64,8 @@ def main():
     ap.add_argument("--layout", default="sell", choices=["sell", "csr"])
     ap.add_argument("--f-mode", default="auto", choices=["auto", "stencil", "assembled"],
                     help="F sweeps: recompute F from thn (stencil) or stream the assembled F")
+    ap.add_argument("--pg-mode", default="auto", choices=["auto", "stencil", "assembled"],
+                    help="D, G, Gt_G: recompute from thn (stencil) or stream the stored operators")
     ap.add_argument("--stencil-kind", default="march4",
                     help="matrix-free F kernel: cells (LDS tile per grid row), rows (row per thread), "
                          "marchR (LDS ring marching R grid rows per workgroup)")
@@ -104,12 +106,12 @@ def main():
         bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
         A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
         pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, layout=args.layout,
-                                          f_mode=args.f_mode)
+                                          f_mode=args.f_mode, pg_mode=args.pg_mode)
         del F, D, G
     else:
         from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
         pc = DistributedSchurPreconditioner(n, args.xi, args.eta_n, args.eta_s, inner_F=iF, inner_P=iP,
-                                            layout=args.layout)
+                                            layout=args.layout, f_mode=args.f_mode, pg_mode=args.pg_mode)
     gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
     v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda", generator=gen)
     out = torch.empty_like(v)
@@ -201,7 +203,9 @@ def main():
                        "eta_s": args.eta_s, "inner_F": f"{kf}:{sf}", "inner_P": f"{kp}:{spp}",
                        "parallelism": f"rows{world}" if world > 1 else "single", "layout": args.layout,
                        "f_sweeps": ("matrix-free-" + args.stencil_kind) if getattr(pc, "f_stencil", None) is not None
-                       else "assembled", "launch": "hipgraph" if graph is not None else "eager",
+                       else "assembled",
+                       "d_g_gtg": "matrix-free" if getattr(pc, "pg_stencil", None) is not None else "assembled",
+                       "launch": "hipgraph" if graph is not None else "eager",
                        **({"note": graph_note} if graph_note else {})},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,

@@ -153,7 +153,10 @@ typedef struct mpbp_schur_plan {
     const double* f_cell;            /* device thn tables (n*n each) */
     const double* f_uface;
     const double* f_vface;
-    mpbp_row_part f_part;            /* halo = 0 on one GPU */
+    mpbp_row_part f_part;            /* velocity partition (F, D stencils); halo = 0 on one GPU */
+    int32_t pg_stencil;              /* 1: D, G and Gt_G recomputed from the cell thn table (n >= 3);
+                                        f_prm / f_cell are set whenever f_stencil or pg_stencil is */
+    mpbp_row_part p_part;            /* pressure partition (G, Gt_G stencils); halo = 0 on one GPU */
 } mpbp_schur_plan;
 
 const char* mpbp_version(void);
@@ -253,6 +256,22 @@ int mpbp_f_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell, 
                              const double* vface, const mpbp_row_part* part, const double* x_in,
                              const double* b, double c1, double c2, double* d, const double* sub,
                              double* x_out, void* stream);
+
+/* ---- matrix-free pressure side: D, G and Gt_G = -(D G) recomputed from the cell thn table ------- */
+/* Same results as the assembled D (MPBP_OP_D), G (MPBP_OP_G, d_p from prm) and Gt_G (mpbp_spgemm of D
+ * and G, alpha = -1) bit for bit.  part: the INPUT vector's partition (velocity for D, pressure for
+ * G and Gt_G); NULL or halo = 0 = one GPU.  solve.py:246 (Gt_G), :259 (D), :273 (G). */
+#define MPBP_PG_D 0     /* y = D x    : N pressure rows from the 4 velocity fields */
+#define MPBP_PG_G 1     /* y = G x    : 4N velocity rows from pressure */
+#define MPBP_PG_GTG 2   /* y = Gt_G x : N pressure rows from pressure */
+int mpbp_pg_stencil_spmv(const mpbp_stokes_params* prm, const double* cell, const mpbp_row_part* part, int32_t op,
+                         int32_t mode, const double* x, const double* z, double* y, void* stream);
+int mpbp_gtg_stencil_jacobi_step(const mpbp_stokes_params* prm, const double* cell, const mpbp_row_part* part,
+                                 const double* x_in, const double* b, const double* sub, double* x_out,
+                                 void* stream);
+int mpbp_gtg_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell, const mpbp_row_part* part,
+                               const double* x_in, const double* b, double c1, double c2, double* d,
+                               const double* sub, double* x_out, void* stream);
 
 /* F stencil kernel choice (process-wide): 0 = LDS-tiled cells, 1 = one row per thread,
  * 2 = marching cells, 4 grid rows per workgroup (default), 2 + R = marching cells, R rows per workgroup. */

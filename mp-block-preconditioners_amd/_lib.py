@@ -15,6 +15,7 @@ SPMV_STORE, SPMV_ADD, SPMV_RESID = 0, 1, 2
 INNER_JACOBI, INNER_CHEBYSHEV = 0, 1
 HALO_BEGIN, HALO_END = 0, 1
 VEC_VELOCITY, VEC_PRESSURE = 0, 1
+PG_D, PG_G, PG_GTG = 0, 1, 2
 BLOCK_ROWS, BLOCK_NNZ = 256, 4095
 
 
@@ -67,7 +68,7 @@ class SchurPlan(Structure):
                 ("Fs_int", Sell), ("Fs_bnd", Sell), ("Ds_int", Sell), ("Ds_bnd", Sell), ("Gs_int", Sell),
                 ("Gs_bnd", Sell), ("Ps_int", Sell), ("Ps_bnd", Sell), ("Qs_int", Sell), ("Qs_bnd", Sell),
                 ("f_stencil", c_int32), ("f_prm", StokesParams), ("f_cell", c_void_p), ("f_uface", c_void_p),
-                ("f_vface", c_void_p), ("f_part", RowPart)]
+                ("f_vface", c_void_p), ("f_part", RowPart), ("pg_stencil", c_int32), ("p_part", RowPart)]
 
 
 _P = c_void_p
@@ -105,6 +106,10 @@ _SIGNATURES = {
                                    c_int),
     "mpbp_f_stencil_cheb_step": ([POINTER(StokesParams), _P, _P, _P, POINTER(RowPart), _P, _P, c_double, c_double,
                                   _P, _P, _P, _P], c_int),
+    "mpbp_pg_stencil_spmv": ([POINTER(StokesParams), _P, POINTER(RowPart), c_int32, c_int32, _P, _P, _P, _P], c_int),
+    "mpbp_gtg_stencil_jacobi_step": ([POINTER(StokesParams), _P, POINTER(RowPart), _P, _P, _P, _P, _P], c_int),
+    "mpbp_gtg_stencil_cheb_step": ([POINTER(StokesParams), _P, POINTER(RowPart), _P, _P, c_double, c_double, _P, _P,
+                                    _P, _P], c_int),
     "mpbp_set_stencil_kind": ([c_int32], c_int),
     "mpbp_gather": ([c_int32, _P, _P, _P, _P], c_int),
     "mpbp_scatter": ([c_int32, _P, _P, _P, _P], c_int),

@@ -29,7 +29,7 @@ class DeviceCSR:
         self._rp_host = row_ptr_host
         self._blocks = None
         self._cs = None
-        self.stencil = None     # FStencil when this is the Stokes F and can be recomputed on the fly
+        self.stencil = None     # FStencil / PGStencil when the operator can be recomputed on the fly
 
     # -- construction -------------------------------------------------------------------------
     @classmethod

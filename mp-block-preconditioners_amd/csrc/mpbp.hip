@@ -539,6 +539,25 @@ struct EpiCheb {
         xout[r] = sub ? p.s - x : x;
     }
 };
+// EpiCheb for the first sweep after x0 = d0 = c2[0] b / diag: the previous direction is the staged x0
+// itself (x and diag supplied by the stencil via set_x / set_diag), so d is written but not read.
+struct EpiChebFirst {
+    const double* b;
+    double* d;
+    double c1, c2;
+    const double* sub;
+    double* xout;
+    struct P { double x, b, dg, s; };
+    __device__ P pre(int32_t r) const { return {0.0, b[r], 0.0, sub ? sub[r] : 0.0}; }
+    __device__ P pre_lite(int32_t r) const { return {0.0, b[r], 0.0, sub ? sub[r] : 0.0}; }
+    __device__ void operator()(int32_t r, double acc, const P& p) const {
+        const double z = (p.b - acc) / p.dg;
+        const double dn = c1 * p.x + c2 * z;
+        d[r] = dn;
+        const double x = p.x + dn;
+        xout[r] = sub ? p.s - x : x;
+    }
+};
 
 // XI entry xi * a * (1 - a) as the assembly evaluates it (left to right).
 __device__ inline double xi_of(double xi, double a) { return xi * a * (1.0 - a); }
@@ -759,6 +778,11 @@ struct FStencilDev {
         if (lr >= 0 && lr < L) return (f * L + lr) * n;
         return 4 * L * n + f * 2 * h * n + (lr < 0 ? (h - 1) : h) * n;    // ghost row r0-1 / r0+L
     }
+    // k_march policy: the 4 velocity fields staged, the cell's 4 rows out
+    static constexpr int NF = 4, NOUT = 4;
+    __device__ int32_t out_row(int f, int lr, int gc) const { return (f * L + lr) * n + gc; }
+    template <bool EDGE, class TA, class XA>
+    __device__ double row(int f, int gr, int gc, const TA& ta, const XA& xa, double* fd) const;
 };
 
 // The ten entries of one F row, built in the assembled row's column order for interior points and
@@ -769,7 +793,6 @@ template <bool EDGE, class TA, class XA>
 __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, const TA& ta, const XA& xa,
                                double* fdiag) {
     const int n = P.n;
-    const int32_t N = n * n;
     const int p = f >> 1;
     const double idx2 = P.idx2;
     const double eta = p ? P.eta_s : P.eta_n;
@@ -990,12 +1013,18 @@ __global__ void __launch_bounds__(kBlock) k_f_cells(FStencilDev P, const double*
     }
 }
 
-// ---- marching variant: a workgroup owns a 256-column strip of `rows` consecutive grid rows and walks
-// down it with a 3-row LDS ring per field (+ thn).  Each step stages ONE new grid row (its loads are
-// issued before the current row is computed, so their latency hides under the arithmetic) instead of
-// three, and the epilogue operands of the next row are requested a step ahead as well.
+// ---- marching kernels: a workgroup owns a 256-column strip of `rows` consecutive grid rows and walks
+// down it with a 3-row LDS ring per staged field (+ thn).  Each step stages ONE new grid row (its loads
+// are issued before the current row is computed, so their latency hides under the arithmetic) instead
+// of three, and the epilogue operands of the row are requested before the barrier.  The kernel is
+// generic over the stencil S (F, D, G, Gt_G below):
+//   S::NF staged input fields, S::NOUT output rows per cell, S::xrow(f, gr) the input layout,
+//   S::out_row(o, lr, gc) the output layout, S::row<EDGE>(o, ...) output row o's sum and diagonal
+//   (EDGE: the cell is on the grid's border, where periodic wrap reorders the row's columns);
+// and over the source XS of the staged input: the vector itself, or (first inner sweep) the inner
+// solver's x0 = c2 * (b / diag) recomputed from b and diag, so that sweep needs no init pass.
 struct XRing {
-    const double* x;   // [4][3][kTileW]
+    const double* x;   // [NF][3][kTileW]
     int s[3];          // ring slot of rows gr-1, gr, gr+1
     int gr, c0;
     __device__ double X(int f, int r, int c) const { return x[(f * 3 + s[r - gr + 1]) * kTileW + (c - c0 + 1)]; }
@@ -1010,27 +1039,41 @@ struct TRing {
     }
 };
 
-// Row of tile values held in registers between its global load and its LDS store.
-struct TileRow {
-    double xa[4], ta, xb[4], tb;
+struct XPlain {        // staged value = x[i]
+    const double* __restrict__ x;
+    __device__ double operator()(int32_t i) const { return x[i]; }
+};
+struct XInit {         // staged value = the first inner iterate: c2 * (b[i] / diag[i]) (c2 = 1: Jacobi)
+    const double* __restrict__ b;
+    const double* __restrict__ dg;
+    double c2;
+    __device__ double operator()(int32_t i) const { return c2 * (b[i] / dg[i]); }
 };
 
-__device__ inline void load_tile_row(const FStencilDev& P, const double* __restrict__ x, int gr, int gcA, bool okA,
-                                     int gcB, bool okB, TileRow& tr) {
+// Row of tile values held in registers between its global load and its LDS store.
+template <int NF>
+struct TileRow {
+    double xa[NF], ta, xb[NF], tb;
+};
+
+template <class S, class XS>
+__device__ inline void load_tile_row(const S& P, const XS& xs, int gr, int gcA, bool okA, int gcB, bool okB,
+                                     TileRow<S::NF>& tr) {
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
+    for (int f = 0; f < S::NF; ++f) {
         const int32_t base = P.xrow(f, gr);
-        tr.xa[f] = okA ? x[base + gcA] : 0.0;
-        tr.xb[f] = okB ? x[base + gcB] : 0.0;
+        tr.xa[f] = okA ? xs(base + gcA) : 0.0;
+        tr.xb[f] = okB ? xs(base + gcB) : 0.0;
     }
     const int32_t tb = P.wrap(gr) * P.n;
     tr.ta = okA ? P.cell[tb + gcA] : 0.0;
     tr.tb = okB ? P.cell[tb + gcB] : 0.0;
 }
 
-__device__ inline void store_tile_row(double* sx, double* st, int slot, int tid, bool extra, const TileRow& tr) {
+template <int NF>
+__device__ inline void store_tile_row(double* sx, double* st, int slot, int tid, bool extra, const TileRow<NF>& tr) {
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
+    for (int f = 0; f < NF; ++f) {
         sx[(f * 3 + slot) * kTileW + tid] = tr.xa[f];
         if (extra) sx[(f * 3 + slot) * kTileW + kBlock + tid] = tr.xb[f];
     }
@@ -1038,19 +1081,31 @@ __device__ inline void store_tile_row(double* sx, double* st, int slot, int tid,
     if (extra) st[slot * kTileW + kBlock + tid] = tr.tb;
 }
 
-template <class Epi>
-__global__ void __launch_bounds__(kBlock) k_f_march(FStencilDev P, const double* __restrict__ x, int rows_per_block,
-                                                    Epi epi) {
-    __shared__ double sx[4 * 3 * kTileW];
+// Owned grid rows [la, lb) of workgroup chunk `chunk`: which = 0 all rows, 1 rows 1 .. L-2 (no ghost
+// read), 2 rows 0 and L-1 (one chunk each).
+__device__ inline bool march_rows(int which, int L, int chunk, int rows_per_block, int* la, int* lb) {
+    if (which == 2) {
+        *la = chunk == 0 ? 0 : L - 1;
+        *lb = *la + 1;
+        return chunk < (L >= 2 ? 2 : 1);
+    }
+    const int lo = which == 1 ? 1 : 0, hi = which == 1 ? L - 1 : L;
+    *la = lo + chunk * rows_per_block;
+    *lb = min(*la + rows_per_block, hi);
+    return *la < *lb;
+}
+
+template <class S, class XS, class Epi>
+__global__ void __launch_bounds__(kBlock) k_march(S P, XS xs, int rows_per_block, Epi epi) {
+    constexpr int NF = S::NF, NO = S::NOUT;
+    __shared__ double sx[NF * 3 * kTileW];
     __shared__ double st[3 * kTileW];
-    const int n = P.n, L = P.L;
+    const int n = P.n;
     const int strips = (n + kBlock - 1) / kBlock;
     const int b = xcd_swizzle(blockIdx.x, gridDim.x);
     const int strip = b % strips, chunk = b / strips;
-    const int lo = P.which == 1 ? 1 : 0, hi = P.which == 1 ? L - 1 : L;   // owned grid rows to compute
-    const int la = lo + chunk * rows_per_block;
-    const int lb = min(la + rows_per_block, hi);
-    if (la >= lb) return;
+    int la, lb;
+    if (!march_rows(P.which, P.L, chunk, rows_per_block, &la, &lb)) return;
     const int c0 = strip * kBlock, tid = threadIdx.x;
     const int colA = c0 - 1 + tid;
     const bool okA = colA <= n;
@@ -1062,40 +1117,191 @@ __global__ void __launch_bounds__(kBlock) k_f_march(FStencilDev P, const double*
     const int gc = c0 + tid;
     const bool live = gc < n;
     // prologue: rows la-1 -> slot 0, la -> slot 1; row la+1 in registers
-    TileRow tr;
-    load_tile_row(P, x, P.r0 + la - 1, gcA, okA, gcB, okB, tr);
+    TileRow<NF> tr;
+    load_tile_row(P, xs, P.r0 + la - 1, gcA, okA, gcB, okB, tr);
     store_tile_row(sx, st, 0, tid, extra, tr);
-    load_tile_row(P, x, P.r0 + la, gcA, okA, gcB, okB, tr);
+    load_tile_row(P, xs, P.r0 + la, gcA, okA, gcB, okB, tr);
     store_tile_row(sx, st, 1, tid, extra, tr);
-    load_tile_row(P, x, P.r0 + la + 1, gcA, okA, gcB, okB, tr);
+    load_tile_row(P, xs, P.r0 + la + 1, gcA, okA, gcB, okB, tr);
     for (int lr = la; lr < lb; ++lr) {
         const int k = lr - la;
         const int sm = k % 3, s0 = (k + 1) % 3, sp = (k + 2) % 3;
-        typename Epi::P pe[4];
+        typename Epi::P pe[NO];
         if (live) {                                          // epilogue operands of row lr, in flight
 #pragma unroll
-            for (int f = 0; f < 4; ++f) pe[f] = epi.pre_lite((f * L + lr) * n + gc);
+            for (int o = 0; o < NO; ++o) pe[o] = epi.pre_lite(P.out_row(o, lr, gc));
         }
         store_tile_row(sx, st, sp, tid, extra, tr);          // row lr+1
         __syncthreads();
-        if (lr + 1 < lb) load_tile_row(P, x, P.r0 + lr + 2, gcA, okA, gcB, okB, tr);   // in flight
+        if (lr + 1 < lb) load_tile_row(P, xs, P.r0 + lr + 2, gcA, okA, gcB, okB, tr);   // in flight
         if (live) {
             const int gr = P.r0 + lr;
             const XRing xa{sx, {sm, s0, sp}, gr, c0};
             const TRing ta{st, {sm, s0, sp}, gr, c0};
             const bool edge = gr == 0 || gr == n - 1 || gc == 0 || gc == n - 1;
 #pragma unroll
-            for (int f = 0; f < 4; ++f) {
-                double fd;
-                const double acc = edge ? f_row<true>(P, f, gr, gc, ta, xa, &fd) : f_row<false>(P, f, gr, gc, ta, xa, &fd);
-                set_diag(pe[f], fd);
-                set_x(pe[f], xa.X(f, gr, gc));
-                epi((f * L + lr) * n + gc, acc, pe[f]);
+            for (int o = 0; o < NO; ++o) {
+                double dg;
+                const double acc = edge ? P.template row<true>(o, gr, gc, ta, xa, &dg)
+                                        : P.template row<false>(o, gr, gc, ta, xa, &dg);
+                set_diag(pe[o], dg);
+                set_x(pe[o], xa.X(S::NF == 1 ? 0 : o, gr, gc));
+                epi(P.out_row(o, lr, gc), acc, pe[o]);
             }
         }
         __syncthreads();                                     // slot sm is rewritten next step
     }
 }
+
+// Launch k_march over the partition rows P.which selects.
+template <class S, class XS, class Epi>
+int launch_march(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStream_t st) {
+    const int64_t grows = P.which == 0 ? P.L : P.which == 1 ? (P.L > 2 ? P.L - 2 : 0) : (P.L >= 2 ? 2 : 1);
+    if (grows == 0) return MPBP_OK;
+    const int64_t chunks = P.which == 2 ? grows : (grows + rows_per_block - 1) / rows_per_block;
+    const int64_t blocks = chunks * ((P.n + kBlock - 1) / kBlock);
+    k_march<S, XS, Epi><<<(unsigned)blocks, kBlock, 0, st>>>(P, xs, rows_per_block, epi);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+// F row of field f at a cell (k_march policy).
+template <bool EDGE, class TA, class XA>
+__device__ inline double FStencilDev::row(int f, int gr, int gc, const TA& ta, const XA& xa, double* fd) const {
+    return f_row<EDGE>(*this, f, gr, gc, ta, xa, fd);
+}
+
+// ------------------------------------------------------- matrix-free D, G, Gt_G ----
+// The pressure-side operators rebuilt per row from the cell thn table: D (pressure rows, reading the 4
+// velocity fields), G (velocity rows, reading pressure) and Gt_G = -(D G) (pressure rows), with the
+// arithmetic of phase_D_row / phase_G_row (x d_p) / k_spgemm_fill (products accumulated in D's column
+// order, then scaled by alpha = -1) and summed in CSR column order -- the assembled operators' results
+// bit for bit.  Needs n >= 3 (distinct periodic neighbours).
+struct PGDev {
+    int n;
+    const double* cell;
+    double d_p, inv, minv;   // d_p, 1.0 / dx, -1.0 / dx  (dx == dy; evaluated as the assembly does)
+    // partition of the INPUT vector's grid rows, as FStencilDev (one GPU: r0 = 0, L = n, h = 0)
+    int r0, L, h, which;
+    __device__ int wrap(int a) const { return a < 0 ? a + n : (a >= n ? a - n : a); }
+    template <int NFI>
+    __device__ int32_t xrow_of(int f, int gr) const {
+        if (h == 0) return (f * n + wrap(gr)) * n;
+        const int lr = gr - r0;
+        if (lr >= 0 && lr < L) return (f * L + lr) * n;
+        return NFI * L * n + f * 2 * h * n + (lr < 0 ? (h - 1) : h) * n;
+    }
+};
+
+// y = D x: pressure row (gr, gc) = sum over phases of the 4 velocity entries in column order.
+struct DStencilDev : PGDev {
+    static constexpr int NF = 4, NOUT = 1;
+    __device__ int32_t xrow(int f, int gr) const { return xrow_of<4>(f, gr); }
+    __device__ int32_t out_row(int, int lr, int gc) const { return lr * n + gc; }
+    template <bool EDGE, class TA, class XA>
+    __device__ double row(int, int gr, int gc, const TA& ta, const XA& xa, double* dg) const {
+        const bool lastc = EDGE && gc == n - 1, lastr = EDGE && gr == n - 1;   // wrapped neighbour sorts first
+        double acc = 0.0;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const double t0 = ta.T(p, gr, gc), tE = ta.T(p, gr, gc + 1), tW = ta.T(p, gr, gc - 1);
+            const double tN = ta.T(p, gr - 1, gc), tS = ta.T(p, gr + 1, gc);
+            const double uE = (inv * (0.5 * (t0 + tE))) * xa.X(2 * p, gr, gc + 1);
+            const double uC = (minv * (0.5 * (t0 + tW))) * xa.X(2 * p, gr, gc);
+            const double vC = (inv * (0.5 * (t0 + tN))) * xa.X(2 * p + 1, gr, gc);
+            const double vS = (minv * (0.5 * (t0 + tS))) * xa.X(2 * p + 1, gr + 1, gc);
+            acc += lastc ? uE : uC;
+            acc += lastc ? uC : uE;
+            acc += lastr ? vS : vC;
+            acc += lastr ? vC : vS;
+        }
+        *dg = 0.0;
+        return acc;
+    }
+};
+
+// y = G x: velocity row o (u_n, v_n, u_s, v_s) at (gr, gc), two pressure entries in column order.
+struct GStencilDev : PGDev {
+    static constexpr int NF = 1, NOUT = 4;
+    __device__ int32_t xrow(int f, int gr) const { return xrow_of<1>(f, gr); }
+    __device__ int32_t out_row(int f, int lr, int gc) const { return (f * L + lr) * n + gc; }
+    template <bool EDGE, class TA, class XA>
+    __device__ double row(int o, int gr, int gc, const TA& ta, const XA& xa, double* dg) const {
+        const int p = o >> 1;
+        const double t0 = ta.T(p, gr, gc), xC = xa.X(0, gr, gc);
+        double acc = 0.0;
+        *dg = 0.0;
+        if ((o & 1) == 0) {   // u row: entries p(gr, gc-1), p(gr, gc); the wrapped one sorts last
+            const double gu = 0.5 * (t0 + ta.T(p, gr, gc - 1));
+            const double uC = (d_p * (inv * gu)) * xC, uW = (d_p * (minv * gu)) * xa.X(0, gr, gc - 1);
+            const bool wrapw = EDGE && gc == 0;
+            acc += wrapw ? uC : uW;
+            acc += wrapw ? uW : uC;
+        } else {              // v row: entries p(gr-1, gc), p(gr, gc)
+            const double gv = 0.5 * (t0 + ta.T(p, gr - 1, gc));
+            const double vC = (d_p * (minv * gv)) * xC, vN = (d_p * (inv * gv)) * xa.X(0, gr - 1, gc);
+            const bool wrapn = EDGE && gr == 0;
+            acc += wrapn ? vC : vN;
+            acc += wrapn ? vN : vC;
+        }
+        return acc;
+    }
+};
+
+// Gt_G = -(D G): row (gr, gc) has the five entries N, W, C, E, S (grid neighbours).  Each off-diagonal
+// gets one product per phase; the diagonal gets four per phase, accumulated in D's column order.
+struct GtGStencilDev : PGDev {
+    static constexpr int NF = 1, NOUT = 1;
+    __device__ int32_t xrow(int f, int gr) const { return xrow_of<1>(f, gr); }
+    __device__ int32_t out_row(int, int lr, int gc) const { return lr * n + gc; }
+    template <class TA>
+    __device__ void entries(int gr, int gc, const TA& ta, double* e) const {   // e = {N, W, C, E, S}
+        const bool lastc = gc == n - 1, lastr = gr == n - 1;
+        double cN = 0.0, cW = 0.0, cC = 0.0, cE = 0.0, cS = 0.0;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const double t0 = ta.T(p, gr, gc), tE = ta.T(p, gr, gc + 1), tW = ta.T(p, gr, gc - 1);
+            const double tN = ta.T(p, gr - 1, gc), tS = ta.T(p, gr + 1, gc);
+            // D row entries (phase_D_row)
+            const double DuE = inv * (0.5 * (t0 + tE)), DuC = minv * (0.5 * (t0 + tW));
+            const double DvC = inv * (0.5 * (t0 + tN)), DvS = minv * (0.5 * (t0 + tS));
+            // G rows of the velocity unknowns u(gr,gc), u(gr,gc+1), v(gr,gc), v(gr+1,gc) (phase_G_row x d_p)
+            const double gC = 0.5 * (t0 + tW), gE = 0.5 * (tE + t0);
+            const double gN = 0.5 * (t0 + tN), gS = 0.5 * (tS + t0);
+            const double uC_C = DuC * (d_p * (inv * gC)), uC_W = DuC * (d_p * (minv * gC));
+            const double uE_E = DuE * (d_p * (inv * gE)), uE_C = DuE * (d_p * (minv * gE));
+            const double vC_C = DvC * (d_p * (minv * gN)), vC_N = DvC * (d_p * (inv * gN));
+            const double vS_S = DvS * (d_p * (minv * gS)), vS_C = DvS * (d_p * (inv * gS));
+            const double u1 = lastc ? uE_C : uC_C, u2 = lastc ? uC_C : uE_C;
+            const double v1 = lastr ? vS_C : vC_C, v2 = lastr ? vC_C : vS_C;
+            if (p == 0) {   // first touch stores the product itself (k_spgemm_fill)
+                cC = u1; cW = uC_W; cE = uE_E; cN = vC_N; cS = vS_S;
+            } else {
+                cC += u1; cW += uC_W; cE += uE_E; cN += vC_N; cS += vS_S;
+            }
+            cC += u2;
+            cC += v1;
+            cC += v2;
+        }
+        e[0] = -1.0 * cN; e[1] = -1.0 * cW; e[2] = -1.0 * cC; e[3] = -1.0 * cE; e[4] = -1.0 * cS;
+    }
+    template <bool EDGE, class TA, class XA>
+    __device__ double row(int, int gr, int gc, const TA& ta, const XA& xa, double* dg) const {
+        double e[5];
+        entries(gr, gc, ta, e);
+        *dg = e[2];
+        Ent s[5] = {Ent{EDGE ? wrap(gr - 1) * n + gc : (gr - 1) * n + gc, e[0], xa.X(0, gr - 1, gc)},
+                    Ent{EDGE ? gr * n + wrap(gc - 1) : gr * n + gc - 1, e[1], xa.X(0, gr, gc - 1)},
+                    Ent{gr * n + gc, e[2], xa.X(0, gr, gc)},
+                    Ent{EDGE ? gr * n + wrap(gc + 1) : gr * n + gc + 1, e[3], xa.X(0, gr, gc + 1)},
+                    Ent{EDGE ? wrap(gr + 1) * n + gc : (gr + 1) * n + gc, e[4], xa.X(0, gr + 1, gc)}};
+        if (EDGE) sort5(s);
+        double acc = 0.0;
+#pragma unroll
+        for (int t = 0; t < 5; ++t) acc += s[t].v * s[t].x;
+        return acc;
+    }
+};
 
 // One thread per (slice, lane): copy the CSR row into its column-major slots.
 __global__ void k_sell_fill(Csr A, const int4* slices, int nslices, uint8_t* rlen, double* val, int32_t* col) {
@@ -1187,7 +1393,7 @@ extern "C" {
 const char* mpbp_version(void) { return "libmpbp 0.1 (gfx950)"; }
 
 int mpbp_set_stencil_kind(int32_t kind) {
-    // kind: 0 cells, 1 rows, 2 + R (R >= 1): marching cells, R grid rows per workgroup (2 -> R = 8)
+    // kind: 0 cells, 1 rows, 2 + R (R >= 1): marching cells, R grid rows per workgroup (2 -> R = 4)
     if (kind < 0) return set_error(MPBP_ERR_ARG, "stencil kind must be 0 (cells), 1 (rows) or 2+R (march)");
     g_stencil_kind = kind > 2 ? 2 : kind;
     if (kind > 2) g_march_rows = kind - 2;
@@ -1601,13 +1807,10 @@ static int make_fstencil(const mpbp_stokes_params* prm, const double* cell, cons
 namespace {
 template <class Epi>
 int launch_fstencil(const FStencilDev& P, const double* x, Epi epi, hipStream_t st) {
+    if (g_stencil_kind == 2) return launch_march(P, XPlain{x}, epi, g_march_rows, st);   // marching LDS ring
     const int64_t grows = P.which == 0 ? P.L : P.which == 1 ? (P.L > 2 ? P.L - 2 : 0) : (P.L >= 2 ? 2 : 1);
     if (grows == 0) return MPBP_OK;
-    if (g_stencil_kind == 2 && P.which != 2) {   // marching LDS ring
-        const int64_t chunks = (grows + g_march_rows - 1) / g_march_rows;
-        const int64_t blocks = chunks * ((P.n + kBlock - 1) / kBlock);
-        k_f_march<Epi><<<(unsigned)blocks, kBlock, 0, st>>>(P, x, g_march_rows, epi);
-    } else if (g_stencil_kind != 1) {   // LDS-tiled cells (default)
+    if (g_stencil_kind != 1) {   // LDS-tiled cells
         const int64_t blocks = grows * ((P.n + kBlock - 1) / kBlock);
         k_f_cells<Epi><<<(unsigned)blocks, kBlock, 0, st>>>(P, x, epi);
     } else {                     // one row per thread, global operands
@@ -1658,6 +1861,73 @@ int mpbp_f_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell, 
     return launch_fstencil(P, x_in, EpiCheb{x_in, b, nullptr, d, c1, c2, sub, x_out}, as_stream(stream));
 }
 
+static int make_pgstencil(const mpbp_stokes_params* prm, const double* cell, const mpbp_row_part* part, PGDev* P) {
+    if (!prm || prm->n < 3 || !cell) return set_error(MPBP_ERR_ARG, "pg_stencil: needs n >= 3 and the cell thn table");
+    if ((int64_t)prm->n * prm->n * 5 > INT32_MAX) return set_error(MPBP_ERR_OVERFLOW, "pg_stencil: n too large");
+    const double dx = 1.0 / prm->n;   // as phase_D_row / phase_G_row evaluate 1.0 / dx, -1.0 / dx
+    int r0 = 0, L = prm->n, h = 0, which = 0;
+    if (part && part->halo > 0) {
+        r0 = part->r0; L = part->rows; h = part->halo; which = part->which;
+        if (L < 1 || r0 < 0 || r0 + L > prm->n || which < 0 || which > 2)
+            return set_error(MPBP_ERR_ARG, "pg_stencil: bad row partition");
+    }
+    *P = PGDev{prm->n, cell, prm->d_p, 1.0 / dx, -1.0 / dx, r0, L, h, which};
+    return MPBP_OK;
+}
+
+}  // extern "C"
+
+namespace {
+template <class S>
+int pg_spmv(const S& P, int32_t mode, const double* x, const double* z, double* y, hipStream_t st) {
+    switch (mode) {
+    case MPBP_SPMV_STORE: return launch_march(P, XPlain{x}, EpiStore{y}, g_march_rows, st);
+    case MPBP_SPMV_ADD: return launch_march(P, XPlain{x}, EpiAdd{z, y}, g_march_rows, st);
+    case MPBP_SPMV_RESID: return launch_march(P, XPlain{x}, EpiResid{z, y}, g_march_rows, st);
+    default: return set_error(MPBP_ERR_ARG, "pg_stencil_spmv: unknown mode %d", mode);
+    }
+}
+}  // namespace
+
+extern "C" {
+
+int mpbp_pg_stencil_spmv(const mpbp_stokes_params* prm, const double* cell, const mpbp_row_part* part, int32_t op,
+                         int32_t mode, const double* x, const double* z, double* y, void* stream) {
+    PGDev P;
+    int rc = make_pgstencil(prm, cell, part, &P);
+    if (rc) return rc;
+    if (!x || !y || x == y || (mode != MPBP_SPMV_STORE && !z)) return set_error(MPBP_ERR_ARG, "pg_stencil_spmv: bad vectors");
+    const hipStream_t st = as_stream(stream);
+    switch (op) {
+    case MPBP_PG_D: return pg_spmv(DStencilDev{P}, mode, x, z, y, st);
+    case MPBP_PG_G: return pg_spmv(GStencilDev{P}, mode, x, z, y, st);
+    case MPBP_PG_GTG: return pg_spmv(GtGStencilDev{P}, mode, x, z, y, st);
+    default: return set_error(MPBP_ERR_ARG, "pg_stencil_spmv: unknown operator %d", op);
+    }
+}
+
+int mpbp_gtg_stencil_jacobi_step(const mpbp_stokes_params* prm, const double* cell, const mpbp_row_part* part,
+                                 const double* x_in, const double* b, const double* sub, double* x_out,
+                                 void* stream) {
+    PGDev P;
+    int rc = make_pgstencil(prm, cell, part, &P);
+    if (rc) return rc;
+    if (!x_in || !b || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "gtg_stencil_jacobi_step: bad vectors");
+    return launch_march(GtGStencilDev{P}, XPlain{x_in}, EpiJacobi{x_in, b, nullptr, sub, x_out}, g_march_rows,
+                        as_stream(stream));
+}
+
+int mpbp_gtg_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell, const mpbp_row_part* part,
+                               const double* x_in, const double* b, double c1, double c2, double* d,
+                               const double* sub, double* x_out, void* stream) {
+    PGDev P;
+    int rc = make_pgstencil(prm, cell, part, &P);
+    if (rc) return rc;
+    if (!x_in || !b || !d || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "gtg_stencil_cheb_step: bad vectors");
+    return launch_march(GtGStencilDev{P}, XPlain{x_in}, EpiCheb{x_in, b, nullptr, d, c1, c2, sub, x_out},
+                        g_march_rows, as_stream(stream));
+}
+
 }  // extern "C"
 
 // ======================================================= Schur apply ====
@@ -1677,28 +1947,34 @@ hipError_t record_event(hipEvent_t ev, hipStream_t st) {
 }
 
 // One operator of the apply, restricted to interior or boundary rows, in CSR or SELL form.
+enum StencilOp { SOP_NONE = 0, SOP_F, SOP_D, SOP_G, SOP_GTG };
+
 struct OpRef {
     const mpbp_csr* csr;
     const mpbp_rowblocks* blk;
     const mpbp_sell* sell;
-    const mpbp_schur_plan* stencil;   // F rows recomputed from the plan's thn tables
+    const mpbp_schur_plan* stencil;   // rows recomputed from the plan's thn tables (sop says which operator)
     bool empty;
     int32_t which;                    // stencil rows: 0 all, 1 interior, 2 boundary
+    int32_t sop;
 };
 
+// F and D read velocity vectors (f_part), G and Gt_G pressure vectors (p_part).
 inline mpbp_row_part stencil_part(const OpRef& o) {
-    mpbp_row_part q = o.stencil->f_part;
+    mpbp_row_part q = (o.sop == SOP_F || o.sop == SOP_D) ? o.stencil->f_part : o.stencil->p_part;
     q.which = q.halo > 0 ? o.which : 0;
     return q;
 }
 
 int op_spmv(const OpRef& o, int32_t mode, const double* x, const double* z, double* y, hipStream_t st) {
     if (o.empty) return MPBP_OK;
-    if (o.stencil)
-    {
+    if (o.stencil) {
+        const mpbp_schur_plan* p = o.stencil;
         const mpbp_row_part q = stencil_part(o);
-        return mpbp_f_stencil_spmv(&o.stencil->f_prm, o.stencil->f_cell, o.stencil->f_uface, o.stencil->f_vface,
-                                   &q, mode, x, z, y, (void*)st);
+        if (o.sop == SOP_F)
+            return mpbp_f_stencil_spmv(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, mode, x, z, y, (void*)st);
+        const int32_t op = o.sop == SOP_D ? MPBP_PG_D : o.sop == SOP_G ? MPBP_PG_G : MPBP_PG_GTG;
+        return mpbp_pg_stencil_spmv(&p->f_prm, p->f_cell, &q, op, mode, x, z, y, (void*)st);
     }
     return o.sell ? mpbp_sell_spmv(o.sell, mode, x, z, y, (void*)st)
                   : mpbp_spmv(o.csr, o.blk, mode, x, z, y, (void*)st);
@@ -1706,11 +1982,13 @@ int op_spmv(const OpRef& o, int32_t mode, const double* x, const double* z, doub
 int op_jacobi(const OpRef& o, const double* xin, const double* b, const double* dg, const double* sub, double* xo,
               hipStream_t st) {
     if (o.empty) return MPBP_OK;
-    if (o.stencil)
-    {
+    if (o.stencil) {
+        const mpbp_schur_plan* p = o.stencil;
         const mpbp_row_part q = stencil_part(o);
-        return mpbp_f_stencil_jacobi_step(&o.stencil->f_prm, o.stencil->f_cell, o.stencil->f_uface,
-                                          o.stencil->f_vface, &q, xin, b, sub, xo, (void*)st);
+        if (o.sop == SOP_F)
+            return mpbp_f_stencil_jacobi_step(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, xin, b, sub, xo,
+                                              (void*)st);
+        return mpbp_gtg_stencil_jacobi_step(&p->f_prm, p->f_cell, &q, xin, b, sub, xo, (void*)st);
     }
     return o.sell ? mpbp_sell_jacobi_step(o.sell, xin, b, dg, sub, xo, (void*)st)
                   : mpbp_jacobi_step(o.csr, o.blk, xin, b, dg, sub, xo, (void*)st);
@@ -1718,11 +1996,13 @@ int op_jacobi(const OpRef& o, const double* xin, const double* b, const double* 
 int op_cheb(const OpRef& o, const double* xin, const double* b, const double* dg, double c1, double c2, double* d,
             const double* sub, double* xo, hipStream_t st) {
     if (o.empty) return MPBP_OK;
-    if (o.stencil)
-    {
+    if (o.stencil) {
+        const mpbp_schur_plan* p = o.stencil;
         const mpbp_row_part q = stencil_part(o);
-        return mpbp_f_stencil_cheb_step(&o.stencil->f_prm, o.stencil->f_cell, o.stencil->f_uface,
-                                        o.stencil->f_vface, &q, xin, b, c1, c2, d, sub, xo, (void*)st);
+        if (o.sop == SOP_F)
+            return mpbp_f_stencil_cheb_step(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, xin, b, c1, c2, d, sub,
+                                            xo, (void*)st);
+        return mpbp_gtg_stencil_cheb_step(&p->f_prm, p->f_cell, &q, xin, b, c1, c2, d, sub, xo, (void*)st);
     }
     return o.sell ? mpbp_sell_cheb_step(o.sell, xin, b, dg, c1, c2, d, sub, xo, (void*)st)
                   : mpbp_cheb_step(o.csr, o.blk, xin, b, dg, c1, c2, d, sub, xo, (void*)st);
@@ -1732,11 +2012,46 @@ struct OpPair {
     OpRef in, bd;
 };
 
+// The first sweep of an inner solve can fold in the init pass (x0 = d0 = c2[0] b / diag, recomputed
+// from b and diag wherever the sweep stages x) when the operator is a whole-grid marching stencil.
+bool can_fuse_init(const OpPair& op) {
+    const OpRef& o = op.in;
+    return o.stencil && !o.empty && op.bd.empty && o.which == 0 &&
+           (o.sop == SOP_GTG || (o.sop == SOP_F && g_stencil_kind == 2));
+}
+
+int op_first_sweep(const OpRef& o, bool cheb, const double* b, const double* diag, double c2_0, double c1, double c2,
+                   double* d, const double* sub, double* xo, hipStream_t st) {
+    const mpbp_schur_plan* p = o.stencil;
+    const XInit xs{b, diag, cheb ? c2_0 : 1.0};
+    if (o.sop == SOP_F) {
+        FStencilDev P;
+        const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &P);
+        if (rc) return rc;
+        return cheb ? launch_march(P, xs, EpiChebFirst{b, d, c1, c2, sub, xo}, g_march_rows, st)
+                    : launch_march(P, xs, EpiJacobi{nullptr, b, nullptr, sub, xo}, g_march_rows, st);
+    }
+    PGDev P;
+    const int rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &P);
+    if (rc) return rc;
+    const GtGStencilDev S{P};
+    return cheb ? launch_march(S, xs, EpiChebFirst{b, d, c1, c2, sub, xo}, g_march_rows, st)
+                : launch_march(S, xs, EpiJacobi{nullptr, b, nullptr, sub, xo}, g_march_rows, st);
+}
+
 OpPair make_op(const mpbp_schur_plan* p, const mpbp_csr& A, const mpbp_rowblocks& bi, const mpbp_rowblocks& bb,
                const mpbp_sell& si, const mpbp_sell& sb) {
     if (p->use_sell)
-        return OpPair{OpRef{&A, nullptr, &si, nullptr, false, 0}, OpRef{&A, nullptr, &sb, nullptr, false, 0}};
-    return OpPair{OpRef{&A, &bi, nullptr, nullptr, false, 0}, OpRef{&A, &bb, nullptr, nullptr, false, 0}};
+        return OpPair{OpRef{&A, nullptr, &si, nullptr, false, 0, SOP_NONE},
+                      OpRef{&A, nullptr, &sb, nullptr, false, 0, SOP_NONE}};
+    return OpPair{OpRef{&A, &bi, nullptr, nullptr, false, 0, SOP_NONE}, OpRef{&A, &bb, nullptr, nullptr, false, 0, SOP_NONE}};
+}
+
+// Stencil operator: interior + boundary rows under a row partition, else all rows in one launch.
+OpPair make_stencil_op(const mpbp_schur_plan* p, int32_t sop, bool partitioned) {
+    if (partitioned)
+        return OpPair{OpRef{nullptr, nullptr, nullptr, p, false, 1, sop}, OpRef{nullptr, nullptr, nullptr, p, false, 2, sop}};
+    return OpPair{OpRef{nullptr, nullptr, nullptr, p, false, 0, sop}, OpRef{nullptr, nullptr, nullptr, nullptr, true, 0, SOP_NONE}};
 }
 
 // Launch one sweep over interior rows, then (after the halo is complete) boundary rows.
@@ -1766,11 +2081,20 @@ int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag
         return set_error(MPBP_ERR_ARG, "unknown inner solver %d", in.kind);
     }
     double* cur = (K == 1) ? dst : ping;
-    const double* s0 = (K == 1) ? sub : nullptr;
-    int rc = cheb ? mpbp_cheb_init(nrows, b, diag, c2[0], dir, s0, cur, (void*)c.st)
+    int s = 1, rc;
+    if (K >= 2 && can_fuse_init(op)) {   // sweep 1 recomputes x0 = d0 from b and diag: no init pass
+        double* nxt = K == 2 ? dst : pong;
+        rc = op_first_sweep(op.in, cheb, b, diag, c2[0], c1[1], c2[1], dir, K == 2 ? sub : nullptr, nxt, c.st);
+        if (rc) return rc;
+        cur = nxt;
+        s = 2;
+    } else {
+        const double* s0 = (K == 1) ? sub : nullptr;
+        rc = cheb ? mpbp_cheb_init(nrows, b, diag, c2[0], dir, s0, cur, (void*)c.st)
                   : mpbp_jacobi_init(nrows, b, diag, s0, cur, (void*)c.st);
-    if (rc) return rc;
-    for (int s = 1; s < K; ++s) {
+        if (rc) return rc;
+    }
+    for (; s < K; ++s) {
         const bool last = s == K - 1;
         double* nxt = last ? dst : (cur == ping ? pong : ping);
         const double* sb = last ? sub : nullptr;
@@ -1805,15 +2129,19 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
     const Ctx c{p, as_stream(stream)};
     if (p->f_stencil && p->halo && p->f_part.halo < 1)
         return set_error(MPBP_ERR_ARG, "schur_apply: a partitioned F stencil needs f_part");
-    const bool part = p->f_stencil && p->f_part.halo > 0;
-    const OpPair F = !p->f_stencil ? make_op(p, p->F, p->F_int, p->F_bnd, p->Fs_int, p->Fs_bnd)
-                     : part ? OpPair{OpRef{nullptr, nullptr, nullptr, p, false, 1},
-                                     OpRef{nullptr, nullptr, nullptr, p, false, 2}}
-                            : OpPair{OpRef{nullptr, nullptr, nullptr, p, false, 0},
-                                     OpRef{nullptr, nullptr, nullptr, nullptr, true, 0}};
-    const OpPair D = make_op(p, p->D, p->D_int, p->D_bnd, p->Ds_int, p->Ds_bnd);
-    const OpPair G = make_op(p, p->G, p->G_int, p->G_bnd, p->Gs_int, p->Gs_bnd);
-    const OpPair P = make_op(p, p->GtG, p->P_int, p->P_bnd, p->Ps_int, p->Ps_bnd);
+    if (p->pg_stencil && p->halo && (p->p_part.halo < 1 || p->f_part.halo < 1))
+        return set_error(MPBP_ERR_ARG, "schur_apply: partitioned D / G / Gt_G stencils need f_part and p_part");
+    if ((p->f_stencil || p->pg_stencil) && !p->f_cell)
+        return set_error(MPBP_ERR_ARG, "schur_apply: stencil operators need the thn tables");
+    const bool part = p->halo != nullptr;
+    const OpPair F = p->f_stencil ? make_stencil_op(p, SOP_F, part)
+                                  : make_op(p, p->F, p->F_int, p->F_bnd, p->Fs_int, p->Fs_bnd);
+    const OpPair D = p->pg_stencil ? make_stencil_op(p, SOP_D, part)
+                                   : make_op(p, p->D, p->D_int, p->D_bnd, p->Ds_int, p->Ds_bnd);
+    const OpPair G = p->pg_stencil ? make_stencil_op(p, SOP_G, part)
+                                   : make_op(p, p->G, p->G_int, p->G_bnd, p->Gs_int, p->Gs_bnd);
+    const OpPair P = p->pg_stencil ? make_stencil_op(p, SOP_GTG, part)
+                                   : make_op(p, p->GtG, p->P_int, p->P_bnd, p->Ps_int, p->Ps_bnd);
     const OpPair Q = make_op(p, p->GtFG, p->Q_int, p->Q_bnd, p->Qs_int, p->Qs_bnd);
     const double* v_u = v;
     const double* v_p = v + p->nu;

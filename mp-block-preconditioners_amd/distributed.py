@@ -25,7 +25,7 @@ import torch
 from . import _lib
 from ._lib import check, lib, ptr, stream_handle
 from .csr import DeviceCSR
-from .solve import PlanProfiling
+from .solve import PlanProfiling, _pg_stencil
 
 N_VEL_FIELDS = 4
 N_P_FIELDS = 1
@@ -165,7 +165,7 @@ class DistributedSchurPreconditioner(PlanProfiling):
     """
 
     def __init__(self, n, xi, eta_n, eta_s, c=1.0, d_u=-1.0, inner_F=None, inner_P=None, group=None,
-                 device=None, layout="sell", f_mode="auto"):
+                 device=None, layout="sell", f_mode="auto", pg_mode="auto"):
         import torch.distributed as dist
         from .preconditioner import MultiphaseBlockPreconditioner
         from .solve import InnerSolver
@@ -182,6 +182,7 @@ class DistributedSchurPreconditioner(PlanProfiling):
         if f_mode == "stencil" and F.stencil is None:
             raise ValueError("f_mode='stencil' needs n >= 3")
         self.f_stencil = F.stencil if f_mode in ("auto", "stencil") else None
+        self.pg_stencil = _pg_stencil(D, G, GtG, self.f_stencil, pg_mode)
         # inner-solver bounds from the global operators: identical on every rank
         self.inner_F = (inner_F or InnerSolver()).resolve(F, F.diagonal())
         self.inner_P = (inner_P or InnerSolver()).resolve(GtG, GtG.diagonal())
@@ -271,11 +272,16 @@ class DistributedSchurPreconditioner(PlanProfiling):
         for i, t in enumerate(self._wp):
             p.wp[i] = t.data_ptr()
         p.f_stencil = 1 if self.f_stencil is not None else 0
+        p.pg_stencil = 1 if self.pg_stencil is not None else 0
         if self.f_stencil is not None:
             st = self.f_stencil
             p.f_prm = st.prm
             p.f_cell, p.f_uface, p.f_vface = st.cell.data_ptr(), st.uface.data_ptr(), st.vface.data_ptr()
-            p.f_part = _lib.RowPart(self.part.r0, self.part.L, self.h_u if world > 1 else 0, 0)
+        elif self.pg_stencil is not None:
+            p.f_prm, p.f_cell = self.pg_stencil.prm, self.pg_stencil.cell.data_ptr()
+        # velocity (F, D) and pressure (G, Gt_G) input partitions of the stencil operators
+        p.f_part = _lib.RowPart(self.part.r0, self.part.L, self.h_u if world > 1 else 0, 0)
+        p.p_part = _lib.RowPart(self.part.r0, self.part.L, self.h_p if world > 1 else 0, 0)
         p.halo = self._cb if world > 1 else _lib.HALO_FN()
         p.halo_ctx = None
         p.prof_events = None

@@ -52,6 +52,31 @@ class FStencil:
         return out
 
 
+class PGStencil:
+    """Matrix-free D, G or Gt_G = -(D G) (op = _lib.PG_D / PG_G / PG_GTG), recomputed per row from the cell
+    thn table -- bit-identical to the assembled operator (and, for Gt_G, to the sparse product)."""
+
+    def __init__(self, prm: _lib.StokesParams, cell: torch.Tensor, op: int):
+        self.prm, self.cell, self.op = prm, cell, int(op)
+
+    @property
+    def shape(self):
+        N = self.prm.n * self.prm.n
+        return {_lib.PG_D: (N, 4 * N), _lib.PG_G: (4 * N, N), _lib.PG_GTG: (N, N)}[self.op]
+
+    def same_grid(self, other) -> bool:
+        """True when `other` was built from the same tables and parameters (one get_big_A_matrix call)."""
+        return isinstance(other, (PGStencil, FStencil)) and other.cell.data_ptr() == self.cell.data_ptr() and \
+            bytes(other.prm) == bytes(self.prm)
+
+    def matvec(self, x, out=None, mode=_lib.SPMV_STORE, z=None):
+        if out is None:
+            out = torch.empty(self.shape[0], dtype=torch.float64, device=x.device)
+        check(lib().mpbp_pg_stencil_spmv(ctypes.byref(self.prm), ptr(self.cell), None, self.op, mode, ptr(x), ptr(z),
+                                         ptr(out), stream_handle()))
+        return out
+
+
 class MultiphaseBlockPreconditioner:
     def __init__(self, n, xi, eta_n=1.0, eta_s=1.0, device=None):
         if int(n) < 1:
@@ -117,10 +142,13 @@ class MultiphaseBlockPreconditioner:
         kw = dict(c=c, d_u=d_u, d_p=d_p, d_div=d_div)
         A = self.assemble(_lib.OP_A, **kw)
         F = self.assemble(_lib.OP_F, **kw)
-        if self.n >= 3:
-            F.stencil = FStencil(self._params(**kw), self.theta_tables())
         D = self.assemble(_lib.OP_D, **kw)
         G = self.assemble(_lib.OP_G, **kw)
+        if self.n >= 3:   # the matrix-free forms (periodic neighbours are distinct from n = 3 on)
+            prm, tabs = self._params(**kw), self.theta_tables()
+            F.stencil = FStencil(prm, tabs)
+            D.stencil = PGStencil(prm, tabs[0], _lib.PG_D)
+            G.stencil = PGStencil(prm, tabs[0], _lib.PG_G)
         return A, None, F, D, G
 
     @staticmethod
@@ -130,4 +158,8 @@ class MultiphaseBlockPreconditioner:
         GtF = spgemm(D, F, alpha=-1.0)
         GtFG = spgemm(GtF, G, alpha=1.0)
         del GtF
+        sd, sg = getattr(D, "stencil", None), getattr(G, "stencil", None)
+        if isinstance(sd, PGStencil) and sd.op == _lib.PG_D and isinstance(sg, PGStencil) and sg.op == _lib.PG_G \
+                and sd.same_grid(sg):
+            GtG.stencil = PGStencil(sd.prm, sd.cell, _lib.PG_GTG)
         return GtG, GtFG

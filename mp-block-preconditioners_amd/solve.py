@@ -23,7 +23,7 @@ import torch
 from . import _lib
 from ._lib import check, lib, ptr, stream_handle
 from .csr import DeviceCSR
-from .preconditioner import MultiphaseBlockPreconditioner
+from .preconditioner import MultiphaseBlockPreconditioner, PGStencil
 
 
 @dataclass
@@ -101,6 +101,22 @@ class PlanProfiling:
         self._plan.prof_count = ctypes.POINTER(ctypes.c_int32)()
 
 
+def _pg_stencil(D, G, GtG, f_stencil, pg_mode):
+    """The PGStencil of Gt_G when D, G and Gt_G can run matrix-free (pg_mode 'auto' / 'stencil'), else None."""
+    if pg_mode not in ("auto", "stencil", "assembled"):
+        raise ValueError("pg_mode must be 'auto', 'stencil' or 'assembled'")
+    if pg_mode == "assembled":
+        return None
+    sd, sg, sp = (getattr(M, "stencil", None) for M in (D, G, GtG))
+    ok = all(isinstance(s, PGStencil) for s in (sd, sg, sp)) and \
+        (sd.op, sg.op, sp.op) == (_lib.PG_D, _lib.PG_G, _lib.PG_GTG) and sd.same_grid(sg) and sd.same_grid(sp) and \
+        (f_stencil is None or sd.same_grid(f_stencil))
+    if not ok and pg_mode == "stencil":
+        raise ValueError("pg_mode='stencil' needs D, G from one get_big_A_matrix call (n >= 3) and Gt_G from "
+                         "commutator_products")
+    return sp if ok else None
+
+
 class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
     """M^-1 of the block upper-triangular approximate-commutator preconditioner (solve.py:257-277).
 
@@ -109,7 +125,8 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
     """
 
     def __init__(self, F, D, G, GtG=None, GtFG=None, inner_F: InnerSolver | None = None,
-                 inner_P: InnerSolver | None = None, device=None, layout: str = "sell", f_mode: str = "auto"):
+                 inner_P: InnerSolver | None = None, device=None, layout: str = "sell", f_mode: str = "auto",
+                 pg_mode: str = "auto"):
         dev = torch.device(device or (F.device if isinstance(F, DeviceCSR) else "cuda"))
         self.F, self.D, self.G = (_device_csr(M, dev) for M in (F, D, G))
         if GtG is None or GtFG is None:
@@ -142,6 +159,9 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
         if f_mode == "stencil" and st is None:
             raise ValueError("f_mode='stencil' needs F from MultiphaseBlockPreconditioner.get_big_A_matrix (n >= 3)")
         self.f_stencil = st if f_mode in ("auto", "stencil") else None
+        # D, G, Gt_G likewise ("pg"): recomputed from the cell thn table when all three carry stencils of
+        # one grid (get_big_A_matrix + commutator_products), else streamed from their stored copies.
+        self.pg_stencil = _pg_stencil(self.D, self.G, self.GtG, self.f_stencil, pg_mode)
         self._plan = self._make_plan()
         super().__init__(dtype=np.float64, shape=(nu + np_, nu + np_))
 
@@ -174,6 +194,9 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
             p.f_prm = self.f_stencil.prm
             p.f_cell, p.f_uface, p.f_vface = (t.data_ptr() for t in (self.f_stencil.cell, self.f_stencil.uface,
                                                                     self.f_stencil.vface))
+        p.pg_stencil = 1 if self.pg_stencil is not None else 0
+        if self.pg_stencil is not None and self.f_stencil is None:
+            p.f_prm, p.f_cell = self.pg_stencil.prm, self.pg_stencil.cell.data_ptr()
         p.halo = _lib.HALO_FN()
         p.halo_ctx = None
         p.prof_events = None

@@ -122,7 +122,7 @@ def test_graph_replay_matches_eager():
     torch.cuda.synchronize()
     ms = pc.profiled_ms()
     pc.disable_profiling()
-    assert len(ms) == 6 and all(t > 0 for t in ms)
+    assert len(ms) == 4 and all(t > 0 for t in ms)   # 2 solves x 2 plain sweeps (the first is fused with init)
     v.copy_(torch.randn_like(v))             # replay reads the captured buffers' new contents
     g.replay()
     assert torch.equal(out, pc.apply(v))

@@ -16,7 +16,8 @@ import os
 def mean_counter(path, counter, kernel_substr, grid):
     vals = []
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] == counter and kernel_substr in r["Kernel_Name"] and int(r["Grid_Size"]) == grid:
+        if r["Counter_Name"] == counter and kernel_substr in r["Kernel_Name"] and \
+                (grid is None or int(r["Grid_Size"]) == grid):
             vals.append(float(r["Counter_Value"]))
     return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
 
@@ -28,8 +29,10 @@ def main():
     ap.add_argument("--write")
     args = ap.parse_args()
     grid = 4 * args.n * args.n
-    # F sweep kernels and their launch grids (threads): the cell kernel runs one thread per cell
-    kernels = {"stencil": ("k_f_cells<(anonymous namespace)::EpiCheb>", grid // 4),
+    # F sweep kernels and their launch grids (threads)
+    # (the marching kernel's grid depends on its rows per workgroup: matched by name only)
+    kernels = {"stencil": ("k_march<(anonymous namespace)::FStencilDev, (anonymous namespace)::XPlain, "
+                           "(anonymous namespace)::EpiCheb>", None),
                "sell": ("k_sell_rows<(anonymous namespace)::EpiCheb>", grid)}
     out = {"n": args.n, "source": args.run_dir}
     for lay, (kname, kgrid) in kernels.items():
