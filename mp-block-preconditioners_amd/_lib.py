@@ -7,7 +7,8 @@ from ctypes import (CFUNCTYPE, POINTER, Structure, byref, c_char_p, c_double, c_
                     c_int64, c_void_p)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libmpbp.so")
+# MPBP_LIB selects an experiment build of the same library (tools/build_variants.py); default: the product
+LIB_PATH = os.environ.get("MPBP_LIB") or os.path.join(HERE, "lib", "libmpbp.so")
 
 OP_A, OP_F, OP_D, OP_G = 0, 1, 2, 3
 OP_L_N, OP_L_S, OP_D_N, OP_D_S, OP_G_N, OP_G_S, OP_XI_N, OP_XI_S = range(4, 12)

@@ -44,6 +44,52 @@ constexpr int kPairs = kCap / (2 * kBlock);    // 16-byte (2 x f64) loads per th
 
 inline int grid_for(int64_t n, int block = kBlock) { return (int)((n + block - 1) / block); }
 
+// Cache policy of the once-touched streams.  The SELL kernel reads its matrix (touched once per SpMV)
+// and writes its result with nontemporal hints (MPBP_SELL_NT, default on: +2-4 % on the 1024^2 A SpMV);
+// the stencil kernels keep default-policy loads and stores (their x / b / d vectors are re-read by the
+// next sweep from the cache; nontemporal costs them 3-7 %).  MPBP_NT_LOAD / MPBP_NT_STORE force the hint
+// on every epilogue load / store (experiment builds, tools/build_variants.py).
+#ifndef MPBP_SELL_NT
+#define MPBP_SELL_NT 1
+#endif
+#ifndef MPBP_NT_LOAD
+#define MPBP_NT_LOAD 0
+#endif
+#ifndef MPBP_NT_STORE
+#define MPBP_NT_STORE 0
+#endif
+template <class T>
+__device__ inline T ld_stream(const T* p) {
+#if MPBP_NT_LOAD
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+template <bool NT = false, class T>
+__device__ inline void st_stream(T* p, T v) {
+    if constexpr (NT || MPBP_NT_STORE) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+__device__ inline double2 ld_matrix(const double2* p) {
+#if MPBP_SELL_NT
+    const f64x2 v = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(p));
+    return make_double2(v.x, v.y);
+#else
+    return *p;
+#endif
+}
+__device__ inline int2 ld_matrix(const int2* p) {
+#if MPBP_SELL_NT
+    const i32x2 v = __builtin_nontemporal_load(reinterpret_cast<const i32x2*>(p));
+    return make_int2(v.x, v.y);
+#else
+    return *p;
+#endif
+}
+
 // ================================================================== theta ====
 // thn(y, x) = 0.25 sin(2 pi x) sin(2 pi y) + 0.5 -- preconditioner.py:9-11
 __device__ inline double thn_fn(double y, double x) {
@@ -487,23 +533,29 @@ struct EpiStore {
     struct P {};
     __device__ P pre(int32_t) const { return {}; }
     __device__ P pre_lite(int32_t) const { return {}; }
-    __device__ void operator()(int32_t r, double acc, const P&) const { y[r] = acc; }
+    template <bool NT = false>
+    __device__ void apply(int32_t r, double acc, const P&) const { st_stream<NT>(y + r, acc); }
+    __device__ void operator()(int32_t r, double acc, const P& p) const { apply<false>(r, acc, p); }
 };
 struct EpiAdd {   // rhs = D Finv_v + v_p   (solve.py:259)
     const double* z;
     double* y;
     struct P { double z; };
-    __device__ P pre(int32_t r) const { return {z[r]}; }
-    __device__ P pre_lite(int32_t r) const { return {z[r]}; }
-    __device__ void operator()(int32_t r, double acc, const P& p) const { y[r] = acc + p.z; }
+    __device__ P pre(int32_t r) const { return {ld_stream(z + r)}; }
+    __device__ P pre_lite(int32_t r) const { return {ld_stream(z + r)}; }
+    template <bool NT = false>
+    __device__ void apply(int32_t r, double acc, const P& p) const { st_stream<NT>(y + r, acc + p.z); }
+    __device__ void operator()(int32_t r, double acc, const P& p) const { apply<false>(r, acc, p); }
 };
 struct EpiResid {
     const double* z;
     double* y;
     struct P { double z; };
-    __device__ P pre(int32_t r) const { return {z[r]}; }
-    __device__ P pre_lite(int32_t r) const { return {z[r]}; }
-    __device__ void operator()(int32_t r, double acc, const P& p) const { y[r] = p.z - acc; }
+    __device__ P pre(int32_t r) const { return {ld_stream(z + r)}; }
+    __device__ P pre_lite(int32_t r) const { return {ld_stream(z + r)}; }
+    template <bool NT = false>
+    __device__ void apply(int32_t r, double acc, const P& p) const { st_stream<NT>(y + r, p.z - acc); }
+    __device__ void operator()(int32_t r, double acc, const P& p) const { apply<false>(r, acc, p); }
 };
 struct EpiJacobi {   // x = (b - R x)/D in residual form (solve.py:158)
     const double* xin;
@@ -512,13 +564,15 @@ struct EpiJacobi {   // x = (b - R x)/D in residual form (solve.py:158)
     const double* sub;
     double* xout;
     struct P { double x, b, dg, s; };
-    __device__ P pre(int32_t r) const { return {xin[r], b[r], diag ? diag[r] : 0.0, sub ? sub[r] : 0.0}; }
+    __device__ P pre(int32_t r) const { return {xin[r], ld_stream(b + r), diag ? diag[r] : 0.0, sub ? ld_stream(sub + r) : 0.0}; }
     // x_in and diag supplied by the caller (set_x / set_diag)
-    __device__ P pre_lite(int32_t r) const { return {0.0, b[r], 0.0, sub ? sub[r] : 0.0}; }
-    __device__ void operator()(int32_t r, double acc, const P& p) const {
+    __device__ P pre_lite(int32_t r) const { return {0.0, ld_stream(b + r), 0.0, sub ? ld_stream(sub + r) : 0.0}; }
+    template <bool NT = false>
+    __device__ void apply(int32_t r, double acc, const P& p) const {
         const double x = p.x + (p.b - acc) / p.dg;
-        xout[r] = sub ? p.s - x : x;
+        st_stream<NT>(xout + r, sub ? p.s - x : x);
     }
+    __device__ void operator()(int32_t r, double acc, const P& p) const { apply<false>(r, acc, p); }
 };
 struct EpiCheb {
     const double* xin;
@@ -529,15 +583,17 @@ struct EpiCheb {
     const double* sub;
     double* xout;
     struct P { double x, b, dg, d, s; };
-    __device__ P pre(int32_t r) const { return {xin[r], b[r], diag ? diag[r] : 0.0, d[r], sub ? sub[r] : 0.0}; }
-    __device__ P pre_lite(int32_t r) const { return {0.0, b[r], 0.0, d[r], sub ? sub[r] : 0.0}; }
-    __device__ void operator()(int32_t r, double acc, const P& p) const {
+    __device__ P pre(int32_t r) const { return {xin[r], ld_stream(b + r), diag ? diag[r] : 0.0, ld_stream(d + r), sub ? ld_stream(sub + r) : 0.0}; }
+    __device__ P pre_lite(int32_t r) const { return {0.0, ld_stream(b + r), 0.0, ld_stream(d + r), sub ? ld_stream(sub + r) : 0.0}; }
+    template <bool NT = false>
+    __device__ void apply(int32_t r, double acc, const P& p) const {
         const double z = (p.b - acc) / p.dg;
         const double dn = c1 * p.d + c2 * z;
-        d[r] = dn;
+        st_stream<NT>(d + r, dn);
         const double x = p.x + dn;
-        xout[r] = sub ? p.s - x : x;
+        st_stream<NT>(xout + r, sub ? p.s - x : x);
     }
+    __device__ void operator()(int32_t r, double acc, const P& p) const { apply<false>(r, acc, p); }
 };
 // EpiCheb for the first sweep after x0 = d0 = c2[0] b / diag: the previous direction is the staged x0
 // itself (x and diag supplied by the stencil via set_x / set_diag), so d is written but not read.
@@ -548,15 +604,17 @@ struct EpiChebFirst {
     const double* sub;
     double* xout;
     struct P { double x, b, dg, s; };
-    __device__ P pre(int32_t r) const { return {0.0, b[r], 0.0, sub ? sub[r] : 0.0}; }
-    __device__ P pre_lite(int32_t r) const { return {0.0, b[r], 0.0, sub ? sub[r] : 0.0}; }
-    __device__ void operator()(int32_t r, double acc, const P& p) const {
+    __device__ P pre(int32_t r) const { return {0.0, ld_stream(b + r), 0.0, sub ? ld_stream(sub + r) : 0.0}; }
+    __device__ P pre_lite(int32_t r) const { return {0.0, ld_stream(b + r), 0.0, sub ? ld_stream(sub + r) : 0.0}; }
+    template <bool NT = false>
+    __device__ void apply(int32_t r, double acc, const P& p) const {
         const double z = (p.b - acc) / p.dg;
         const double dn = c1 * p.x + c2 * z;
-        d[r] = dn;
+        st_stream<NT>(d + r, dn);
         const double x = p.x + dn;
-        xout[r] = sub ? p.s - x : x;
+        st_stream<NT>(xout + r, sub ? p.s - x : x);
     }
+    __device__ void operator()(int32_t r, double acc, const P& p) const { apply<false>(r, acc, p); }
 };
 
 // XI entry xi * a * (1 - a) as the assembly evaluates it (left to right).
@@ -694,8 +752,8 @@ __global__ void __launch_bounds__(kBlock) k_sell_rows(Sell S, const double* __re
 #pragma unroll
         for (int j = 0; j < kSellPairs; ++j) {
             if (j < np) {
-                v[j] = vp[(size_t)j * 64];
-                c[j] = cp[(size_t)j * 64];
+                v[j] = ld_matrix(vp + (size_t)j * 64);
+                c[j] = ld_matrix(cp + (size_t)j * 64);
             } else {
                 v[j] = make_double2(0.0, 0.0);
                 c[j] = make_int2(0, 0);
@@ -720,7 +778,7 @@ __global__ void __launch_bounds__(kBlock) k_sell_rows(Sell S, const double* __re
             if (2 * j + 1 < len) acc += vv.y * x[cc.y];
         }
     }
-    if (live) epi(r, acc, pe);
+    if (live) epi.template apply<MPBP_SELL_NT != 0>(r, acc, pe);
 }
 
 // ------------------------------------------------------------- F stencil ----
@@ -1023,18 +1081,23 @@ __global__ void __launch_bounds__(kBlock) k_f_cells(FStencilDev P, const double*
 //   (EDGE: the cell is on the grid's border, where periodic wrap reorders the row's columns);
 // and over the source XS of the staged input: the vector itself, or (first inner sweep) the inner
 // solver's x0 = c2 * (b / diag) recomputed from b and diag, so that sweep needs no init pass.
+#ifndef MPBP_MARCH_BLOCK
+#define MPBP_MARCH_BLOCK 256
+#endif
+constexpr int kMB = MPBP_MARCH_BLOCK;   // columns (threads) per marching workgroup
+constexpr int kMTileW = kMB + 2;       // + one halo column each side
 struct XRing {
-    const double* x;   // [NF][3][kTileW]
+    const double* x;   // [NF][3][kMTileW]
     int s[3];          // ring slot of rows gr-1, gr, gr+1
     int gr, c0;
-    __device__ double X(int f, int r, int c) const { return x[(f * 3 + s[r - gr + 1]) * kTileW + (c - c0 + 1)]; }
+    __device__ double X(int f, int r, int c) const { return x[(f * 3 + s[r - gr + 1]) * kMTileW + (c - c0 + 1)]; }
 };
 struct TRing {
-    const double* t;   // [3][kTileW]
+    const double* t;   // [3][kMTileW]
     int s[3];
     int gr, c0;
     __device__ double T(int sph, int r, int c) const {
-        const double v = t[s[r - gr + 1] * kTileW + (c - c0 + 1)];
+        const double v = t[s[r - gr + 1] * kMTileW + (c - c0 + 1)];
         return sph ? 1.0 - v : v;
     }
 };
@@ -1074,11 +1137,11 @@ template <int NF>
 __device__ inline void store_tile_row(double* sx, double* st, int slot, int tid, bool extra, const TileRow<NF>& tr) {
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
-        sx[(f * 3 + slot) * kTileW + tid] = tr.xa[f];
-        if (extra) sx[(f * 3 + slot) * kTileW + kBlock + tid] = tr.xb[f];
+        sx[(f * 3 + slot) * kMTileW + tid] = tr.xa[f];
+        if (extra) sx[(f * 3 + slot) * kMTileW + kMB + tid] = tr.xb[f];
     }
-    st[slot * kTileW + tid] = tr.ta;
-    if (extra) st[slot * kTileW + kBlock + tid] = tr.tb;
+    st[slot * kMTileW + tid] = tr.ta;
+    if (extra) st[slot * kMTileW + kMB + tid] = tr.tb;
 }
 
 // Owned grid rows [la, lb) of workgroup chunk `chunk`: which = 0 all rows, 1 rows 1 .. L-2 (no ghost
@@ -1096,22 +1159,22 @@ __device__ inline bool march_rows(int which, int L, int chunk, int rows_per_bloc
 }
 
 template <class S, class XS, class Epi>
-__global__ void __launch_bounds__(kBlock) k_march(S P, XS xs, int rows_per_block, Epi epi) {
+__global__ void __launch_bounds__(kMB) k_march(S P, XS xs, int rows_per_block, Epi epi) {
     constexpr int NF = S::NF, NO = S::NOUT;
-    __shared__ double sx[NF * 3 * kTileW];
-    __shared__ double st[3 * kTileW];
+    __shared__ double sx[NF * 3 * kMTileW];
+    __shared__ double st[3 * kMTileW];
     const int n = P.n;
-    const int strips = (n + kBlock - 1) / kBlock;
+    const int strips = (n + kMB - 1) / kMB;
     const int b = xcd_swizzle(blockIdx.x, gridDim.x);
     const int strip = b % strips, chunk = b / strips;
     int la, lb;
     if (!march_rows(P.which, P.L, chunk, rows_per_block, &la, &lb)) return;
-    const int c0 = strip * kBlock, tid = threadIdx.x;
+    const int c0 = strip * kMB, tid = threadIdx.x;
     const int colA = c0 - 1 + tid;
     const bool okA = colA <= n;
     const int gcA = P.wrap(colA);
     const bool extra = tid < 2;
-    const int colB = c0 + kBlock - 1 + tid;
+    const int colB = c0 + kMB - 1 + tid;
     const bool okB = extra && colB <= n;
     const int gcB = P.wrap(colB < n ? colB : (colB == n ? n : 0));
     const int gc = c0 + tid;
@@ -1159,8 +1222,8 @@ int launch_march(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStrea
     const int64_t grows = P.which == 0 ? P.L : P.which == 1 ? (P.L > 2 ? P.L - 2 : 0) : (P.L >= 2 ? 2 : 1);
     if (grows == 0) return MPBP_OK;
     const int64_t chunks = P.which == 2 ? grows : (grows + rows_per_block - 1) / rows_per_block;
-    const int64_t blocks = chunks * ((P.n + kBlock - 1) / kBlock);
-    k_march<S, XS, Epi><<<(unsigned)blocks, kBlock, 0, st>>>(P, xs, rows_per_block, epi);
+    const int64_t blocks = chunks * ((P.n + kMB - 1) / kMB);
+    k_march<S, XS, Epi><<<(unsigned)blocks, kMB, 0, st>>>(P, xs, rows_per_block, epi);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }

@@ -1,6 +1,7 @@
 """Summarise a rocprofv3 --kernel-trace CSV per (kernel, grid size): calls, mean/min/max duration.
 
     python tools/prof_summary.py gpurun_out/<tag>/prof/run_kernel_trace.csv [--out profiles/x.md]
+    python tools/prof_summary.py gpurun_out/<tag>/prof/run_results.db        (rocprofv3's default SQLite output)
 
 The per-grid split separates launches of one template over different matrices (e.g. the
 Chebyshev sweep over F, 4N rows, from the one over Gt_G, N rows), which rocprofv3 --stats lumps
@@ -24,9 +25,15 @@ def main():
     ap.add_argument("--out")
     args = ap.parse_args()
     agg = collections.defaultdict(list)
-    for r in csv.DictReader(open(args.trace)):
-        d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-        agg[(short(r["Kernel_Name"]), int(r["Grid_Size_X"]), int(r["Workgroup_Size_X"]))].append(d)
+    if args.trace.endswith(".db"):
+        import sqlite3
+        db = sqlite3.connect(args.trace)
+        for name, start, end, gx, wx in db.execute("select name, start, end, grid_x, workgroup_x from kernels"):
+            agg[(short(name), int(gx), int(wx))].append(int(end) - int(start))
+    else:
+        for r in csv.DictReader(open(args.trace)):
+            d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            agg[(short(r["Kernel_Name"]), int(r["Grid_Size_X"]), int(r["Workgroup_Size_X"]))].append(d)
     total = sum(sum(v) for v in agg.values())
     lines = ["| kernel | grid (threads) | block | calls | mean us | min us | max us | % time |",
              "|---|---|---|---|---|---|---|---|"]
