@@ -582,6 +582,7 @@ struct EpiCheb {
     double c1, c2;
     const double* sub;
     double* xout;
+    int store_d = 1;   // 0: the inner solve's last sweep (its direction is never read again)
     struct P { double x, b, dg, d, s; };
     __device__ P pre(int32_t r) const { return {xin[r], ld_stream(b + r), diag ? diag[r] : 0.0, ld_stream(d + r), sub ? ld_stream(sub + r) : 0.0}; }
     __device__ P pre_lite(int32_t r) const { return {0.0, ld_stream(b + r), 0.0, ld_stream(d + r), sub ? ld_stream(sub + r) : 0.0}; }
@@ -589,7 +590,7 @@ struct EpiCheb {
     __device__ void apply(int32_t r, double acc, const P& p) const {
         const double z = (p.b - acc) / p.dg;
         const double dn = c1 * p.d + c2 * z;
-        st_stream<NT>(d + r, dn);
+        if (store_d) st_stream<NT>(d + r, dn);
         const double x = p.x + dn;
         st_stream<NT>(xout + r, sub ? p.s - x : x);
     }
@@ -603,6 +604,7 @@ struct EpiChebFirst {
     double c1, c2;
     const double* sub;
     double* xout;
+    int store_d = 1;
     struct P { double x, b, dg, s; };
     __device__ P pre(int32_t r) const { return {0.0, ld_stream(b + r), 0.0, sub ? ld_stream(sub + r) : 0.0}; }
     __device__ P pre_lite(int32_t r) const { return {0.0, ld_stream(b + r), 0.0, sub ? ld_stream(sub + r) : 0.0}; }
@@ -610,7 +612,7 @@ struct EpiChebFirst {
     __device__ void apply(int32_t r, double acc, const P& p) const {
         const double z = (p.b - acc) / p.dg;
         const double dn = c1 * p.x + c2 * z;
-        st_stream<NT>(d + r, dn);
+        if (store_d) st_stream<NT>(d + r, dn);
         const double x = p.x + dn;
         st_stream<NT>(xout + r, sub ? p.s - x : x);
     }
@@ -1179,13 +1181,13 @@ __global__ void __launch_bounds__(kMB) k_march(S P, XS xs, int rows_per_block, E
     const int gcB = P.wrap(colB < n ? colB : (colB == n ? n : 0));
     const int gc = c0 + tid;
     const bool live = gc < n;
-    // prologue: rows la-1 -> slot 0, la -> slot 1; row la+1 in registers
-    TileRow<NF> tr;
-    load_tile_row(P, xs, P.r0 + la - 1, gcA, okA, gcB, okB, tr);
-    store_tile_row(sx, st, 0, tid, extra, tr);
-    load_tile_row(P, xs, P.r0 + la, gcA, okA, gcB, okB, tr);
-    store_tile_row(sx, st, 1, tid, extra, tr);
+    // prologue: rows la-1 -> slot 0, la -> slot 1; row la+1 in registers -- all three requested at once
+    TileRow<NF> tr, tp0, tp1;
+    load_tile_row(P, xs, P.r0 + la - 1, gcA, okA, gcB, okB, tp0);
+    load_tile_row(P, xs, P.r0 + la, gcA, okA, gcB, okB, tp1);
     load_tile_row(P, xs, P.r0 + la + 1, gcA, okA, gcB, okB, tr);
+    store_tile_row(sx, st, 0, tid, extra, tp0);
+    store_tile_row(sx, st, 1, tid, extra, tp1);
     for (int lr = la; lr < lb; ++lr) {
         const int k = lr - la;
         const int sm = k % 3, s0 = (k + 1) % 3, sp = (k + 2) % 3;
@@ -1718,13 +1720,19 @@ int mpbp_cheb_init(int32_t nrows, const double* b, const double* diag, double c2
     return MPBP_OK;
 }
 
-int mpbp_cheb_step(const mpbp_csr* A, const mpbp_rowblocks* blocks, const double* x_in,
-                   const double* b, const double* diag, double c1, double c2, double* d,
-                   const double* sub, double* x_out, void* stream) {
+static int cheb_step_impl(const mpbp_csr* A, const mpbp_rowblocks* blocks, const double* x_in,
+                          const double* b, const double* diag, double c1, double c2, double* d,
+                          const double* sub, double* x_out, void* stream, int store_d) {
     int rc = check_csr(A);
     if (rc) return rc;
     if (!x_in || !b || !diag || !d || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "cheb_step: bad vectors");
-    return launch_rows(A, blocks, x_in, EpiCheb{x_in, b, diag, d, c1, c2, sub, x_out}, as_stream(stream));
+    return launch_rows(A, blocks, x_in, EpiCheb{x_in, b, diag, d, c1, c2, sub, x_out, store_d}, as_stream(stream));
+}
+
+int mpbp_cheb_step(const mpbp_csr* A, const mpbp_rowblocks* blocks, const double* x_in,
+                   const double* b, const double* diag, double c1, double c2, double* d,
+                   const double* sub, double* x_out, void* stream) {
+    return cheb_step_impl(A, blocks, x_in, b, diag, c1, c2, d, sub, x_out, stream, 1);
 }
 
 int mpbp_cheb_coeffs(double lmin, double lmax, int32_t sweeps, double* c1, double* c2) {
@@ -1839,12 +1847,17 @@ int mpbp_sell_jacobi_step(const mpbp_sell* S, const double* x_in, const double* 
     return launch_sell(S, x_in, EpiJacobi{x_in, b, diag, sub, x_out}, as_stream(stream));
 }
 
-int mpbp_sell_cheb_step(const mpbp_sell* S, const double* x_in, const double* b, const double* diag, double c1,
-                        double c2, double* d, const double* sub, double* x_out, void* stream) {
+static int sell_cheb_impl(const mpbp_sell* S, const double* x_in, const double* b, const double* diag, double c1,
+                          double c2, double* d, const double* sub, double* x_out, void* stream, int store_d) {
     int rc = check_sell(S);
     if (rc) return rc;
     if (!x_in || !b || !diag || !d || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "sell_cheb_step: bad vectors");
-    return launch_sell(S, x_in, EpiCheb{x_in, b, diag, d, c1, c2, sub, x_out}, as_stream(stream));
+    return launch_sell(S, x_in, EpiCheb{x_in, b, diag, d, c1, c2, sub, x_out, store_d}, as_stream(stream));
+}
+
+int mpbp_sell_cheb_step(const mpbp_sell* S, const double* x_in, const double* b, const double* diag, double c1,
+                        double c2, double* d, const double* sub, double* x_out, void* stream) {
+    return sell_cheb_impl(S, x_in, b, diag, c1, c2, d, sub, x_out, stream, 1);
 }
 
 static int make_fstencil(const mpbp_stokes_params* prm, const double* cell, const double* uface,
@@ -1913,15 +1926,22 @@ int mpbp_f_stencil_jacobi_step(const mpbp_stokes_params* prm, const double* cell
     return launch_fstencil(P, x_in, EpiJacobi{x_in, b, nullptr, sub, x_out}, as_stream(stream));
 }
 
-int mpbp_f_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell, const double* uface,
-                             const double* vface, const mpbp_row_part* part, const double* x_in,
-                             const double* b, double c1, double c2, double* d, const double* sub,
-                             double* x_out, void* stream) {
+static int f_stencil_cheb_impl(const mpbp_stokes_params* prm, const double* cell, const double* uface,
+                               const double* vface, const mpbp_row_part* part, const double* x_in,
+                               const double* b, double c1, double c2, double* d, const double* sub,
+                               double* x_out, void* stream, int store_d) {
     FStencilDev P;
     int rc = make_fstencil(prm, cell, uface, vface, part, &P);
     if (rc) return rc;
     if (!x_in || !b || !d || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "f_stencil_cheb_step: bad vectors");
-    return launch_fstencil(P, x_in, EpiCheb{x_in, b, nullptr, d, c1, c2, sub, x_out}, as_stream(stream));
+    return launch_fstencil(P, x_in, EpiCheb{x_in, b, nullptr, d, c1, c2, sub, x_out, store_d}, as_stream(stream));
+}
+
+int mpbp_f_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell, const double* uface,
+                             const double* vface, const mpbp_row_part* part, const double* x_in,
+                             const double* b, double c1, double c2, double* d, const double* sub,
+                             double* x_out, void* stream) {
+    return f_stencil_cheb_impl(prm, cell, uface, vface, part, x_in, b, c1, c2, d, sub, x_out, stream, 1);
 }
 
 static int make_pgstencil(const mpbp_stokes_params* prm, const double* cell, const mpbp_row_part* part, PGDev* P) {
@@ -1980,15 +2000,21 @@ int mpbp_gtg_stencil_jacobi_step(const mpbp_stokes_params* prm, const double* ce
                         as_stream(stream));
 }
 
-int mpbp_gtg_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell, const mpbp_row_part* part,
-                               const double* x_in, const double* b, double c1, double c2, double* d,
-                               const double* sub, double* x_out, void* stream) {
+static int gtg_stencil_cheb_impl(const mpbp_stokes_params* prm, const double* cell, const mpbp_row_part* part,
+                                 const double* x_in, const double* b, double c1, double c2, double* d,
+                                 const double* sub, double* x_out, void* stream, int store_d) {
     PGDev P;
     int rc = make_pgstencil(prm, cell, part, &P);
     if (rc) return rc;
     if (!x_in || !b || !d || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "gtg_stencil_cheb_step: bad vectors");
-    return launch_march(GtGStencilDev{P}, XPlain{x_in}, EpiCheb{x_in, b, nullptr, d, c1, c2, sub, x_out},
+    return launch_march(GtGStencilDev{P}, XPlain{x_in}, EpiCheb{x_in, b, nullptr, d, c1, c2, sub, x_out, store_d},
                         g_march_rows, as_stream(stream));
+}
+
+int mpbp_gtg_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell, const mpbp_row_part* part,
+                               const double* x_in, const double* b, double c1, double c2, double* d,
+                               const double* sub, double* x_out, void* stream) {
+    return gtg_stencil_cheb_impl(prm, cell, part, x_in, b, c1, c2, d, sub, x_out, stream, 1);
 }
 
 }  // extern "C"
@@ -2057,18 +2083,18 @@ int op_jacobi(const OpRef& o, const double* xin, const double* b, const double* 
                   : mpbp_jacobi_step(o.csr, o.blk, xin, b, dg, sub, xo, (void*)st);
 }
 int op_cheb(const OpRef& o, const double* xin, const double* b, const double* dg, double c1, double c2, double* d,
-            const double* sub, double* xo, hipStream_t st) {
+            const double* sub, double* xo, hipStream_t st, int store_d) {
     if (o.empty) return MPBP_OK;
     if (o.stencil) {
         const mpbp_schur_plan* p = o.stencil;
         const mpbp_row_part q = stencil_part(o);
         if (o.sop == SOP_F)
-            return mpbp_f_stencil_cheb_step(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, xin, b, c1, c2, d, sub,
-                                            xo, (void*)st);
-        return mpbp_gtg_stencil_cheb_step(&p->f_prm, p->f_cell, &q, xin, b, c1, c2, d, sub, xo, (void*)st);
+            return f_stencil_cheb_impl(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, xin, b, c1, c2, d, sub,
+                                       xo, (void*)st, store_d);
+        return gtg_stencil_cheb_impl(&p->f_prm, p->f_cell, &q, xin, b, c1, c2, d, sub, xo, (void*)st, store_d);
     }
-    return o.sell ? mpbp_sell_cheb_step(o.sell, xin, b, dg, c1, c2, d, sub, xo, (void*)st)
-                  : mpbp_cheb_step(o.csr, o.blk, xin, b, dg, c1, c2, d, sub, xo, (void*)st);
+    return o.sell ? sell_cheb_impl(o.sell, xin, b, dg, c1, c2, d, sub, xo, (void*)st, store_d)
+                  : cheb_step_impl(o.csr, o.blk, xin, b, dg, c1, c2, d, sub, xo, (void*)st, store_d);
 }
 
 struct OpPair {
@@ -2084,21 +2110,21 @@ bool can_fuse_init(const OpPair& op) {
 }
 
 int op_first_sweep(const OpRef& o, bool cheb, const double* b, const double* diag, double c2_0, double c1, double c2,
-                   double* d, const double* sub, double* xo, hipStream_t st) {
+                   double* d, const double* sub, double* xo, hipStream_t st, int store_d) {
     const mpbp_schur_plan* p = o.stencil;
     const XInit xs{b, diag, cheb ? c2_0 : 1.0};
     if (o.sop == SOP_F) {
         FStencilDev P;
         const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &P);
         if (rc) return rc;
-        return cheb ? launch_march(P, xs, EpiChebFirst{b, d, c1, c2, sub, xo}, g_march_rows, st)
+        return cheb ? launch_march(P, xs, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, g_march_rows, st)
                     : launch_march(P, xs, EpiJacobi{nullptr, b, nullptr, sub, xo}, g_march_rows, st);
     }
     PGDev P;
     const int rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &P);
     if (rc) return rc;
     const GtGStencilDev S{P};
-    return cheb ? launch_march(S, xs, EpiChebFirst{b, d, c1, c2, sub, xo}, g_march_rows, st)
+    return cheb ? launch_march(S, xs, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, g_march_rows, st)
                 : launch_march(S, xs, EpiJacobi{nullptr, b, nullptr, sub, xo}, g_march_rows, st);
 }
 
@@ -2147,7 +2173,8 @@ int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag
     int s = 1, rc;
     if (K >= 2 && can_fuse_init(op)) {   // sweep 1 recomputes x0 = d0 from b and diag: no init pass
         double* nxt = K == 2 ? dst : pong;
-        rc = op_first_sweep(op.in, cheb, b, diag, c2[0], c1[1], c2[1], dir, K == 2 ? sub : nullptr, nxt, c.st);
+        rc = op_first_sweep(op.in, cheb, b, diag, c2[0], c1[1], c2[1], dir, K == 2 ? sub : nullptr, nxt, c.st,
+                            K == 2 ? 0 : 1);
         if (rc) return rc;
         cur = nxt;
         s = 2;
@@ -2167,7 +2194,7 @@ int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag
                          hipStreamIsCapturing(c.st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone;
         if (rec) MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count], c.st));
         rc = two_phase(c, kind, cur, op, [&](const OpRef& o) {
-            return cheb ? op_cheb(o, cur, b, diag, c1[s], c2[s], dir, sb, nxt, c.st)
+            return cheb ? op_cheb(o, cur, b, diag, c1[s], c2[s], dir, sb, nxt, c.st, last ? 0 : 1)
                         : op_jacobi(o, cur, b, diag, sb, nxt, c.st);
         });
         if (rc) return rc;

@@ -22,3 +22,7 @@ for L in stencil sell; do
     cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/pmc_${L}_$C" -o pmc -- python "$GRAFT_REPO_ROOT/tools/pmc_sweep.py" --layout $L > "$GRAFT_REPO_ROOT/$OUT/pmc_${L}_$C.log" 2>&1 || exit 7
   done
 done
+cd "$GRAFT_REPO_ROOT"
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --pg-mode assembled --no-cpu-baseline --no-spmv > "$OUT/bench_pg_assembled.log" 2>&1 || exit 8
+cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/sq_stencil" -o pmc -- python "$GRAFT_REPO_ROOT/tools/pmc_sweep.py" --layout stencil > "$GRAFT_REPO_ROOT/$OUT/sq_stencil.log" 2>&1 || exit 9
+cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_VMEM_RD SQ_LDS_BANK_CONFLICT --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/sq2_stencil" -o pmc -- python "$GRAFT_REPO_ROOT/tools/pmc_sweep.py" --layout stencil > "$GRAFT_REPO_ROOT/$OUT/sq2_stencil.log" 2>&1 || exit 10
