@@ -276,6 +276,10 @@ int mpbp_gtg_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell
 /* F stencil kernel choice (process-wide): 0 = LDS-tiled cells, 1 = one row per thread,
  * 2 = marching cells, 4 grid rows per workgroup (default), 2 + R = marching cells, R rows per workgroup. */
 int mpbp_set_stencil_kind(int32_t kind);
+/* Two-sweep fusion of mpbp_schur_apply's F inner solves (process-wide): the init pass and sweeps 1-2 of
+ * each solve run as one kernel marching `rows` grid rows per workgroup (default 8); 0 = one kernel per
+ * sweep.  Used on one GPU with the marching F stencil; results are bit-identical either way. */
+int mpbp_set_sweep_fusion(int32_t rows);
 
 /* gather: dst[i] = src[idx[i]] ; scatter: dst[idx[i]] = src[i]   (halo pack / unpack) */
 int mpbp_gather(int32_t count, const int32_t* idx, const double* src, double* dst, void* stream);

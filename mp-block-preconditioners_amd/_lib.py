@@ -112,6 +112,7 @@ _SIGNATURES = {
     "mpbp_gtg_stencil_cheb_step": ([POINTER(StokesParams), _P, POINTER(RowPart), _P, _P, c_double, c_double, _P, _P,
                                     _P, _P], c_int),
     "mpbp_set_stencil_kind": ([c_int32], c_int),
+    "mpbp_set_sweep_fusion": ([c_int32], c_int),
     "mpbp_gather": ([c_int32, _P, _P, _P, _P], c_int),
     "mpbp_scatter": ([c_int32, _P, _P, _P, _P], c_int),
     "mpbp_event_create": ([POINTER(c_void_p)], c_int),

@@ -20,6 +20,7 @@ namespace {
 thread_local char g_err[1024] = "";
 int g_stencil_kind = 2;   // F stencil kernel: 0 LDS-tiled cells, 1 row per thread, 2 marching cells (default)
 int g_march_rows = 4;     // grid rows per workgroup of the marching kernel (4 is fastest at 1024^2)
+int g_sweep2_rows = 8;    // grid rows per workgroup of the two-sweep kernel; 0 = no two-sweep fusion
 
 int set_error(int code, const char* fmt, ...) {
     va_list ap;
@@ -849,7 +850,7 @@ struct FStencilDev {
 // sorted (with fixed networks) where periodic wrap-around reorders them.  TA::T(s, gr, gc) is thn of
 // phase s at a cell, XA::X(f, gr, gc) the x entry of field f at a grid point (gr in [-1, n], gc in
 // [-1, n]; the accessors wrap).  Same operations as phase_L_row / F_row, same summation order.
-template <bool EDGE, class TA, class XA>
+template <bool EDGE, class TA, class XA, bool VIRT = false>
 __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, const TA& ta, const XA& xa,
                                double* fdiag) {
     const int n = P.n;
@@ -857,7 +858,7 @@ __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, cons
     const double idx2 = P.idx2;
     const double eta = p ? P.eta_s : P.eta_n;
     const int fu = 2 * p, fv = 2 * p + 1;
-    const int32_t kc = gr * n + gc;
+    const int32_t kc = VIRT ? P.wrap(gr) * n + P.wrap(gc) : gr * n + gc;   // VIRT: (gr, gc) may lie one cell outside
     auto key = [&](int r, int c) -> int32_t { return EDGE ? P.wrap(r) * n + P.wrap(c) : r * n + c; };
     auto T = [&](int r, int c) -> double { return ta.T(p, r, c); };
     double acc = 0.0;
@@ -1368,6 +1369,165 @@ struct GtGStencilDev : PGDev {
     }
 };
 
+// ---- two sweeps in one pass (temporal blocking): the first two sweeps of an F inner solve ----------
+// Level 0 is the solve's x0 = d0 = c2_0 (b / diag) recomputed from b and diag (no init pass); level 1
+// (sweep 1) is computed one grid row ahead of level 2 (sweep 2) and kept in an LDS ring, so x1 and d1
+// never touch HBM: the two sweeps read b, diag and thn and write x2 (+ d2) -- 24-32 B per row instead
+// of ~72.  A workgroup marches down a 256-column strip; level 1 covers one halo column each side
+// (wave 0 computes those two cells in a second pass) and one halo row above and below the chunk,
+// level 0 two.  Each cell is computed with exactly the single-sweep arithmetic (f_row, EpiChebFirst /
+// EpiCheb / EpiJacobi formulas): the results are bit-identical to init + sweep 1 + sweep 2.
+// One GPU (whole grid), n >= 3.  Rings: level 0 and level 1 four rows, thn five, so a workgroup
+// needs only two barriers per row (a fast wave may stage the next row while others finish this one).
+constexpr int kW0 = kMB + 4;   // level 0 / thn tile: virtual columns c0-2 .. c0+257
+constexpr int kW1 = kMB + 2;   // level 1 tile: virtual columns c0-1 .. c0+256
+
+template <int W, int OFF>
+struct XRing4 {                // rows in slot (row + 8) & 3; column c at c - c0 + OFF
+    const double* x;
+    int gr, c0;
+    __device__ double X(int f, int r, int c) const { return x[(f * 4 + ((r + 8) & 3)) * W + (c - c0 + OFF)]; }
+};
+struct TRing5 {                // thn rows in slot (row + 10) % 5
+    const double* t;
+    int gr, c0;
+    __device__ double T(int sph, int r, int c) const {
+        const double v = t[((r + 10) % 5) * kW0 + (c - c0 + 2)];
+        return sph ? 1.0 - v : v;
+    }
+};
+
+struct Sweep2Args {
+    const double* b;
+    const double* diag;   // the inner solve's diag (x0 = c2_0 * (b / diag))
+    double c2_0;          // 1.0 for Jacobi
+    double c1a, c2a;      // sweep 1 (Chebyshev)
+    double c1b, c2b;      // sweep 2 (Chebyshev)
+    double* d_out;        // sweep 2 direction (Chebyshev, when store_d)
+    int store_d;
+    const double* sub;    // sweep 2 result: x_out = sub - x (the solve's last sweep)
+    double* x_out;
+};
+
+// The four F rows at (gr, gc) swept once: xn = x + d with d = c1 dprev + c2 (b - F x) / diag(F)
+// (Chebyshev; dprev = the staged x itself when FIRST) or xn = x + (b - F x) / diag(F) (Jacobi).
+template <bool CHEB, bool FIRST, class TA, class XA>
+__device__ inline void f_sweep_cell(const FStencilDev& P, int gr, int gc, const TA& ta, const XA& xa,
+                                    const double* bb, const double* dprev, double c1, double c2, double* xn,
+                                    double* dn) {
+    const int n = P.n;
+    const bool edge = gr <= 0 || gr >= n - 1 || gc <= 0 || gc >= n - 1;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+        double fd;
+        const double acc = edge ? f_row<true, TA, XA, true>(P, f, gr, gc, ta, xa, &fd)
+                                : f_row<false>(P, f, gr, gc, ta, xa, &fd);
+        const double xc = xa.X(f, gr, gc);
+        if constexpr (CHEB) {
+            const double z = (bb[f] - acc) / fd;
+            const double d = c1 * (FIRST ? xc : dprev[f]) + c2 * z;
+            dn[f] = d;
+            xn[f] = xc + d;
+        } else {
+            xn[f] = xc + (bb[f] - acc) / fd;
+        }
+    }
+}
+
+template <bool CHEB>
+__global__ void __launch_bounds__(kMB) k_f_sweep2(FStencilDev P, Sweep2Args a, int rows_per_block) {
+    __shared__ double s0[4 * 4 * kW0];   // level 0: [field][slot][col]
+    __shared__ double s1[4 * 4 * kW1];   // level 1
+    __shared__ double st[5 * kW0];       // thn
+    const int n = P.n;
+    const int strips = (n + kMB - 1) / kMB;
+    const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int strip = bid % strips, chunk = bid / strips;
+    const int la = chunk * rows_per_block, lb = min(la + rows_per_block, n);
+    if (la >= lb) return;
+    const int c0 = strip * kMB, tid = threadIdx.x;
+    const XInit xs{a.b, a.diag, a.c2_0};
+    // staging: tile column tid <-> virtual column c0-2+tid; threads 0..3 also c0+254+tid
+    const int colA = c0 - 2 + tid, colB = c0 + kMB - 2 + tid;
+    const bool okA = colA <= n + 1, extra = tid < 4, okB = extra && colB <= n + 1;
+    const int gcA = okA ? P.wrap(colA) : 0, gcB = okB ? P.wrap(colB) : 0;
+    auto stage = [&](int r, const TileRow<4>& tr) {
+        const int sx = (r + 8) & 3, sth = (r + 10) % 5;
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            s0[(f * 4 + sx) * kW0 + tid] = tr.xa[f];
+            if (extra) s0[(f * 4 + sx) * kW0 + kMB + tid] = tr.xb[f];
+        }
+        st[sth * kW0 + tid] = tr.ta;
+        if (extra) st[sth * kW0 + kMB + tid] = tr.tb;
+    };
+    // level-1 cells of this thread: column c0+tid (needed up to column n, the right halo of n-1), and
+    // for threads 0 / 1 the halo columns c0-1 / c0+256
+    const int c1m = c0 + tid;
+    const bool need1 = c1m <= n;
+    const int c1h = tid == 0 ? c0 - 1 : c0 + kMB;
+    const bool needh = (tid == 0) || (tid == 1 && c0 + kMB <= n);
+    const int c2c = c0 + tid;
+    const bool live2 = c2c < n;
+    auto vidx = [&](int f, int r, int c) -> int32_t { return (f * n + P.wrap(r)) * n + P.wrap(c); };
+    // prologue: level-0 / thn rows la-2, la-1 staged, row la in registers
+    TileRow<4> tr, tp0, tp1;
+    load_tile_row(P, xs, la - 2, gcA, okA, gcB, okB, tp0);
+    load_tile_row(P, xs, la - 1, gcA, okA, gcB, okB, tp1);
+    load_tile_row(P, xs, la, gcA, okA, gcB, okB, tr);
+    stage(la - 2, tp0);
+    stage(la - 1, tp1);
+    double d1prev[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int k = la - 1; k <= lb; ++k) {
+        // operands of this step, requested before the barrier: b at level-1 row k, b (+ sub) at level-2 row k-1
+        double b1[4], b2[4], s2[4];
+        const bool lev2 = k - 1 >= la && live2;
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            b1[f] = need1 ? a.b[vidx(f, k, c1m)] : 0.0;
+            b2[f] = lev2 ? a.b[(f * n + k - 1) * n + c2c] : 0.0;
+            s2[f] = (lev2 && a.sub) ? a.sub[(f * n + k - 1) * n + c2c] : 0.0;
+        }
+        stage(k + 1, tr);
+        __syncthreads();
+        if (k + 2 <= lb + 1) load_tile_row(P, xs, k + 2, gcA, okA, gcB, okB, tr);   // in flight
+        const XRing4<kW0, 2> x0a{s0, k, c0};
+        const TRing5 tha{st, k, c0};
+        double xn[4], dn[4];
+        if (need1) {   // level 1 (sweep 1) at row k
+            f_sweep_cell<CHEB, true>(P, k, c1m, tha, x0a, b1, nullptr, a.c1a, a.c2a, xn, dn);
+#pragma unroll
+            for (int f = 0; f < 4; ++f) s1[(f * 4 + ((k + 8) & 3)) * kW1 + (c1m - c0 + 1)] = xn[f];
+        }
+        if (tid < 2 && needh) {   // its halo cells (wave 0, second pass)
+            double bh[4];
+#pragma unroll
+            for (int f = 0; f < 4; ++f) bh[f] = a.b[vidx(f, k, c1h)];
+            double xh[4], dh[4];
+            f_sweep_cell<CHEB, true>(P, k, c1h, tha, x0a, bh, nullptr, a.c1a, a.c2a, xh, dh);
+#pragma unroll
+            for (int f = 0; f < 4; ++f) s1[(f * 4 + ((k + 8) & 3)) * kW1 + (c1h - c0 + 1)] = xh[f];
+        }
+        __syncthreads();
+        if (lev2) {   // level 2 (sweep 2) at row k-1
+            const XRing4<kW1, 1> x1a{s1, k - 1, c0};
+            const TRing5 thb{st, k - 1, c0};
+            double xo[4], dout[4];
+            f_sweep_cell<CHEB, false>(P, k - 1, c2c, thb, x1a, b2, d1prev, a.c1b, a.c2b, xo, dout);
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                const int32_t r = (f * n + k - 1) * n + c2c;
+                if (CHEB && a.store_d) st_stream(a.d_out + r, dout[f]);
+                st_stream(a.x_out + r, a.sub ? s2[f] - xo[f] : xo[f]);
+            }
+        }
+        if (CHEB) {
+#pragma unroll
+            for (int f = 0; f < 4; ++f) d1prev[f] = dn[f];
+        }
+    }
+}
+
 // One thread per (slice, lane): copy the CSR row into its column-major slots.
 __global__ void k_sell_fill(Csr A, const int4* slices, int nslices, uint8_t* rlen, double* val, int32_t* col) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1463,6 +1623,11 @@ int mpbp_set_stencil_kind(int32_t kind) {
     g_stencil_kind = kind > 2 ? 2 : kind;
     if (kind > 2) g_march_rows = kind - 2;
     else if (kind == 2) g_march_rows = 4;
+    return MPBP_OK;
+}
+int mpbp_set_sweep_fusion(int32_t rows) {
+    if (rows < 0 || rows > 4096) return set_error(MPBP_ERR_ARG, "sweep fusion rows must be in [0, 4096]");
+    g_sweep2_rows = rows;
     return MPBP_OK;
 }
 const char* mpbp_last_error(void) { return g_err; }
@@ -2128,6 +2293,22 @@ int op_first_sweep(const OpRef& o, bool cheb, const double* b, const double* dia
                 : launch_march(S, xs, EpiJacobi{nullptr, b, nullptr, sub, xo}, g_march_rows, st);
 }
 
+// Sweeps 1 and 2 of an F inner solve from x0 = d0 = c2_0 b / diag in one pass (k_f_sweep2).
+int op_first_two_sweeps(const OpRef& o, bool cheb, const double* b, const double* diag, const double* c1,
+                        const double* c2, double* d, const double* sub, double* xo, hipStream_t st, int store_d) {
+    const mpbp_schur_plan* p = o.stencil;
+    FStencilDev P;
+    const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &P);
+    if (rc) return rc;
+    const Sweep2Args a{b, diag, cheb ? c2[0] : 1.0, c1[1], c2[1], c1[2], c2[2], d, store_d, sub, xo};
+    const int R = g_sweep2_rows;
+    const unsigned blocks = (unsigned)(((P.n + kMB - 1) / kMB) * ((P.n + R - 1) / R));
+    if (cheb) k_f_sweep2<true><<<blocks, kMB, 0, st>>>(P, a, R);
+    else k_f_sweep2<false><<<blocks, kMB, 0, st>>>(P, a, R);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
 OpPair make_op(const mpbp_schur_plan* p, const mpbp_csr& A, const mpbp_rowblocks& bi, const mpbp_rowblocks& bb,
                const mpbp_sell& si, const mpbp_sell& sb) {
     if (p->use_sell)
@@ -2171,7 +2352,13 @@ int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag
     }
     double* cur = (K == 1) ? dst : ping;
     int s = 1, rc;
-    if (K >= 2 && can_fuse_init(op)) {   // sweep 1 recomputes x0 = d0 from b and diag: no init pass
+    if (K >= 3 && can_fuse_init(op) && op.in.sop == SOP_F && g_sweep2_rows > 0) {   // init + sweeps 1, 2: one pass
+        double* nxt = K == 3 ? dst : pong;
+        rc = op_first_two_sweeps(op.in, cheb, b, diag, c1, c2, dir, K == 3 ? sub : nullptr, nxt, c.st, K == 3 ? 0 : 1);
+        if (rc) return rc;
+        cur = nxt;
+        s = 3;
+    } else if (K >= 2 && can_fuse_init(op)) {   // sweep 1 recomputes x0 = d0 from b and diag: no init pass
         double* nxt = K == 2 ? dst : pong;
         rc = op_first_sweep(op.in, cheb, b, diag, c2[0], c1[1], c2[1], dir, K == 2 ? sub : nullptr, nxt, c.st,
                             K == 2 ? 0 : 1);

@@ -126,3 +126,26 @@ def test_graph_replay_matches_eager():
     v.copy_(torch.randn_like(v))             # replay reads the captured buffers' new contents
     g.replay()
     assert torch.equal(out, pc.apply(v))
+
+
+@pytest.mark.parametrize("n", [3, 4, 5, 17, 256, 257, 300, 520])
+@pytest.mark.parametrize("rows", [1, 3, 8])
+def test_two_sweep_fusion_bit_exact(n, rows):
+    """k_f_sweep2 (init + sweeps 1-2 of each F solve in one pass, level 1 kept in LDS) against one kernel
+    per sweep, for Chebyshev and Jacobi inner solves of 3, 4 and 5 sweeps (3: the pass is the solve's last
+    sweep, with sub and no direction store)."""
+    import mp_block_preconditioners_amd as mp
+    from mp_block_preconditioners_amd._lib import check, lib
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.3, 50.0, 2.0)
+    _, _, F, D, G = bp.get_big_A_matrix(c=0.7, d_u=-1.5)
+    v = torch.from_numpy(np.random.default_rng(n + rows).standard_normal(5 * n * n)).cuda()
+    try:
+        for kind, k in (("chebyshev", 4), ("chebyshev", 3), ("jacobi", 3), ("chebyshev", 5), ("jacobi", 4)):
+            pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver(kind, k), inner_P=mp.InnerSolver("jacobi", 2))
+            check(lib().mpbp_set_sweep_fusion(0))
+            ref = pc.apply(v).clone()
+            check(lib().mpbp_set_sweep_fusion(rows))
+            got = pc.apply(v)
+            assert _bits(got, ref), (kind, k, float((got - ref).abs().max()))
+    finally:
+        check(lib().mpbp_set_sweep_fusion(8))
