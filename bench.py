@@ -69,6 +69,8 @@ def main():
     ap.add_argument("--stencil-kind", default="march4",
                     help="matrix-free F kernel: cells (LDS tile per grid row), rows (row per thread), "
                          "marchR (LDS ring marching R grid rows per workgroup)")
+    ap.add_argument("--sweep-fusion", type=int, default=0,
+                    help="grid rows per workgroup of the fused init + two-sweep F kernel; 0 = one kernel per sweep")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-spmv", action="store_true")
@@ -96,6 +98,7 @@ def main():
     from mp_block_preconditioners_amd._lib import check as _check, lib as _lib
     sk = args.stencil_kind
     _check(_lib().mpbp_set_stencil_kind(0 if sk == "cells" else 1 if sk == "rows" else 2 + int(sk[5:] or 4)))
+    _check(_lib().mpbp_set_sweep_fusion(args.sweep_fusion))
 
     n = args.n if (world == 1 or args.strong) else int(round(args.n * math.sqrt(world)))
     kf, sf = parse_inner(args.inner_f)
@@ -205,6 +208,7 @@ def main():
                        "f_sweeps": ("matrix-free-" + args.stencil_kind) if getattr(pc, "f_stencil", None) is not None
                        else "assembled",
                        "d_g_gtg": "matrix-free" if getattr(pc, "pg_stencil", None) is not None else "assembled",
+                       "sweep_fusion_rows": args.sweep_fusion,
                        "launch": "hipgraph" if graph is not None else "eager",
                        **({"note": graph_note} if graph_note else {})},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -277,8 +277,8 @@ int mpbp_gtg_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell
  * 2 = marching cells, 4 grid rows per workgroup (default), 2 + R = marching cells, R rows per workgroup. */
 int mpbp_set_stencil_kind(int32_t kind);
 /* Two-sweep fusion of mpbp_schur_apply's F inner solves (process-wide): the init pass and sweeps 1-2 of
- * each solve run as one kernel marching `rows` grid rows per workgroup (default 8); 0 = one kernel per
- * sweep.  Used on one GPU with the marching F stencil; results are bit-identical either way. */
+ * each solve run as one kernel marching `rows` grid rows per workgroup; 0 (default) = one kernel per
+ * sweep, which is faster on MI355X.  One GPU, marching F stencil; results bit-identical. */
 int mpbp_set_sweep_fusion(int32_t rows);
 
 /* gather: dst[i] = src[idx[i]] ; scatter: dst[idx[i]] = src[i]   (halo pack / unpack) */

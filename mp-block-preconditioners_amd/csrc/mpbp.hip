@@ -20,7 +20,7 @@ namespace {
 thread_local char g_err[1024] = "";
 int g_stencil_kind = 2;   // F stencil kernel: 0 LDS-tiled cells, 1 row per thread, 2 marching cells (default)
 int g_march_rows = 4;     // grid rows per workgroup of the marching kernel (4 is fastest at 1024^2)
-int g_sweep2_rows = 8;    // grid rows per workgroup of the two-sweep kernel; 0 = no two-sweep fusion
+int g_sweep2_rows = 0;    // grid rows per workgroup of the two-sweep kernel; 0 (default) = no two-sweep fusion
 
 int set_error(int code, const char* fmt, ...) {
     va_list ap;
@@ -1379,6 +1379,9 @@ struct GtGStencilDev : PGDev {
 // EpiCheb / EpiJacobi formulas): the results are bit-identical to init + sweep 1 + sweep 2.
 // One GPU (whole grid), n >= 3.  Rings: level 0 and level 1 four rows, thn five, so a workgroup
 // needs only two barriers per row (a fast wave may stage the next row while others finish this one).
+// Measured on MI355X at 1024^2 (R = 8): 163 us against 61 + 46 us for the fused-init sweep and the plain
+// sweep it replaces -- 205 VGPRs and 77 KiB of LDS leave 2 waves per SIMD, and wave 0's halo pass
+// doubles its level-1 work -- so it is off by default (mpbp_set_sweep_fusion).
 constexpr int kW0 = kMB + 4;   // level 0 / thn tile: virtual columns c0-2 .. c0+257
 constexpr int kW1 = kMB + 2;   // level 1 tile: virtual columns c0-1 .. c0+256
 

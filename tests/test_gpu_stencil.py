@@ -148,4 +148,4 @@ def test_two_sweep_fusion_bit_exact(n, rows):
             got = pc.apply(v)
             assert _bits(got, ref), (kind, k, float((got - ref).abs().max()))
     finally:
-        check(lib().mpbp_set_sweep_fusion(8))
+        check(lib().mpbp_set_sweep_fusion(0))
