@@ -33,20 +33,35 @@ def parse_inner(s):
     return kind, int(k or 4)
 
 
-def sweep_bytes(pc, layout):
-    """Algorithmic bytes of one F Chebyshev sweep on this rank: every entry's value (8 B) and column
-    (4 B), the per-row index data (SELL: 1 B length; CSR: 4 B row_ptr), the six row vectors
-    (x_in, b, diag, d read + d write, x_out) and the slice / row-block descriptors."""
+def sweep_bytes(pc, layout, kind, sweeps, fused_init):
+    """Algorithmic HBM bytes of the F inner-solve sweeps bench.py times, averaged per launch.
+
+    mpbp_schur_apply records events around sweeps s = 1 .. K-1 of both F solves (s = 2 .. K-1 when the
+    init pass is fused into sweep 1).  A sweep moves per F row: x_in, b, x_out (8 B each), the direction
+    d read (Chebyshev) and written (Chebyshev, not on the last sweep), the solve's `sub` on the second
+    solve's last sweep, and diag (assembled layouts); plus the matrix (assembled: 12 B per entry + index
+    data) or the thn tables (matrix-free: cell, u-face, v-face = 3 x 8 B per cell = 6 B per row)."""
     F = pc.F
     nF, nnzF = F.shape[0], F.nnz
-    if getattr(pc, "f_stencil", None) is not None:
-        # matrix-free: x, b, d (r/w), x_out per row + the three thn tables read once (3 x 8 B per cell)
-        return nF * 8 * 5 + 3 * 8 * (nF // 4), "k_march<FStencilDev, XPlain, EpiCheb> (F Chebyshev sweep, matrix-free)"
-    if layout == "sell":
-        nsl = pc.sell_of("F").nslices
-        return nnzF * 12 + nF * 1 + nF * 8 * 6 + nsl * 16, "k_sell_rows<EpiCheb> (F Chebyshev sweep, SELL-64)"
-    return (nnzF * 12 + (nF + 1) * 4 + nF * 8 * 6 + F.blocks.count * 8,
-            "k_csr_rows<EpiCheb> (F Chebyshev sweep, CSR)")
+    cheb = kind == "chebyshev"
+    stencil = getattr(pc, "f_stencil", None) is not None
+    if stencil:
+        fixed, kname = 3 * 8 * (nF // 4), "k_march<FStencilDev, XPlain, EpiCheb> (F sweep, matrix-free)"
+    elif layout == "sell":
+        fixed = nnzF * 12 + nF * 1 + pc.sell_of("F").nslices * 16
+        kname = "k_sell_rows<EpiCheb> (F sweep, SELL-64)"
+    else:
+        fixed, kname = nnzF * 12 + (nF + 1) * 4 + F.blocks.count * 8, "k_csr_rows<EpiCheb> (F sweep, CSR)"
+    total, launches = 0, 0
+    for solve in (1, 2):
+        for s in range(2 if fused_init else 1, sweeps):
+            last = s == sweeps - 1
+            streams = 3 + (0 if stencil else 1)                     # x_in, b, x_out (+ diag)
+            streams += (1 + (0 if last else 1)) if cheb else 0      # d read (+ write)
+            streams += 1 if (last and solve == 2) else 0            # sub
+            total += fixed + nF * 8 * streams
+            launches += 1
+    return (total / launches if launches else float("nan")), kname
 
 
 def main():
@@ -158,7 +173,8 @@ def main():
     pc.disable_profiling()
 
     # dominant kernel: the fused Chebyshev-Jacobi sweep over F
-    sbytes, kname = sweep_bytes(pc, args.layout)
+    fused_init = world == 1 and getattr(pc, "f_stencil", None) is not None and sk.startswith("march")
+    sbytes, kname = sweep_bytes(pc, args.layout, kf, sf, fused_init)
     avg_sweep_s = (sum(sweep_ms) / len(sweep_ms) / 1e3) if sweep_ms else float("nan")
     achieved = sbytes / avg_sweep_s / 1e9
 

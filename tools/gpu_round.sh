@@ -17,9 +17,11 @@ MPBP_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnod
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- python "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline > "$GRAFT_REPO_ROOT/$OUT/prof.log" 2>&1 || exit 4
 cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --f-mode assembled --no-cpu-baseline --no-spmv > "$OUT/bench_sell_assembledF.log" 2>&1 || exit 6
+# HBM bytes of the F sweeps inside the apply itself (eager launches; the sweeps bench.py times)
 for L in stencil sell; do
+  FM=auto; [ $L = sell ] && FM=assembled
   for C in FETCH_SIZE WRITE_SIZE; do
-    cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/pmc_${L}_$C" -o pmc -- python "$GRAFT_REPO_ROOT/tools/pmc_sweep.py" --layout $L > "$GRAFT_REPO_ROOT/$OUT/pmc_${L}_$C.log" 2>&1 || exit 7
+    cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $C --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/pmc_${L}_$C" -o pmc -- python "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-spmv --no-graph --f-mode $FM > "$GRAFT_REPO_ROOT/$OUT/pmc_${L}_$C.log" 2>&1 || exit 7
   done
 done
 cd "$GRAFT_REPO_ROOT"

@@ -1,4 +1,5 @@
-"""Reduce rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of tools/pmc_sweep.py to HBM bytes per F sweep.
+"""Reduce rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (over bench.py's apply, tools/gpu_round.sh) to HBM
+bytes per F sweep launch -- the same launches bench.py's HIP events time.
 
     python tools/pmc_reduce.py gpurun_out/<tag> [--write profiles/pmc_traffic.json]
 
@@ -33,7 +34,7 @@ def main():
     # (the marching kernel's grid depends on its rows per workgroup: matched by name only)
     kernels = {"stencil": ("k_march<(anonymous namespace)::FStencilDev, (anonymous namespace)::XPlain, "
                            "(anonymous namespace)::EpiCheb>", None),
-               "sell": ("k_sell_rows<(anonymous namespace)::EpiCheb>", grid)}
+               "sell": ("k_sell_rows<(anonymous namespace)::EpiCheb>", grid)}   # grid 4N: F rows, not Gt_G
     out = {"n": args.n, "source": args.run_dir}
     for lay, (kname, kgrid) in kernels.items():
         res = {}
@@ -46,6 +47,19 @@ def main():
             write = res["WRITE_SIZE"][0] * 1024
             out[lay] = {"fetch_bytes_raw": fetch, "write_bytes": write, "dispatches": res["FETCH_SIZE"][1],
                         "traffic_bytes_corrected": 2 * fetch + write, "traffic_bytes_raw": fetch + write}
+    # calibration on a known byte count in the same runs: k_cheb_init over F's 4N rows reads b, diag and
+    # writes d, x with 8-B lanes -- exactly 2 x 8 x 4N bytes each way (f_mode=assembled pass only)
+    cal = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        f = os.path.join(args.run_dir, f"pmc_sell_{c}", "pmc_counter_collection.csv")
+        if os.path.exists(f):
+            cal[c] = mean_counter(f, c, "k_cheb_init", grid)
+    if cal.get("FETCH_SIZE", (None,))[0] is not None and cal.get("WRITE_SIZE", (None,))[0] is not None:
+        want = 2 * 8 * grid
+        out["calibration_k_cheb_init"] = {
+            "expected_read_bytes": want, "expected_write_bytes": want,
+            "fetch_bytes_raw": cal["FETCH_SIZE"][0] * 1024, "fetch_x2_over_expected": 2 * cal["FETCH_SIZE"][0] * 1024 / want,
+            "write_bytes": cal["WRITE_SIZE"][0] * 1024, "write_over_expected": cal["WRITE_SIZE"][0] * 1024 / want}
     print(json.dumps(out, indent=1))
     if args.write:
         with open(args.write, "w") as fh:
