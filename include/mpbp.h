@@ -15,6 +15,9 @@
  *                         A @ xk in the FGMRES residual callback              solve.py:166
  *   mpbp_jacobi_*         Jacobi(A, b, N, x)                                  solve.py:149-159
  *   mpbp_cheb_*           inner Chebyshev sweeps (BASELINE.json configs[3])
+ *   mpbp_f_stencil_*      the F products / sweeps above with F's rows recomputed from thn
+ *   mpbp_pg_stencil_spmv  D @ Finv_v (solve.py:259), G @ x_p (solve.py:273), Gt_G products
+ *   mpbp_gtg_stencil_*    sweeps over Gt_G = np.matmul(mD, G) (solve.py:246, 265, 271)
  *   mpbp_schur_apply      approx_schur_op(v) -- the LinearOperator matvec    solve.py:257-277
  */
 #ifndef MPBP_H
