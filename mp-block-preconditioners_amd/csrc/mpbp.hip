@@ -20,6 +20,10 @@ namespace {
 thread_local char g_err[1024] = "";
 int g_stencil_kind = 2;   // F stencil kernel: 0 LDS-tiled cells, 1 row per thread, 2 marching cells (default)
 int g_march_rows = 4;     // grid rows per workgroup of the marching kernel (4 is fastest at 1024^2)
+#ifndef MPBP_PG_ROWS
+#define MPBP_PG_ROWS 0    // rows per workgroup of the D / G / Gt_G marching kernels (0: as F)
+#endif
+inline int pg_rows() { return MPBP_PG_ROWS > 0 ? MPBP_PG_ROWS : g_march_rows; }
 int g_sweep2_rows = 0;    // grid rows per workgroup of the two-sweep kernel; 0 (default) = no two-sweep fusion
 
 int set_error(int code, const char* fmt, ...) {
@@ -74,21 +78,26 @@ __device__ inline void st_stream(T* p, T v) {
 }
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef int i32x2 __attribute__((ext_vector_type(2)));
+#ifndef MPBP_CSR_NT
+#define MPBP_CSR_NT 1
+#endif
+template <bool NT>
 __device__ inline double2 ld_matrix(const double2* p) {
-#if MPBP_SELL_NT
-    const f64x2 v = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(p));
-    return make_double2(v.x, v.y);
-#else
-    return *p;
-#endif
+    if constexpr (NT) {
+        const f64x2 v = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(p));
+        return make_double2(v.x, v.y);
+    } else {
+        return *p;
+    }
 }
+template <bool NT>
 __device__ inline int2 ld_matrix(const int2* p) {
-#if MPBP_SELL_NT
-    const i32x2 v = __builtin_nontemporal_load(reinterpret_cast<const i32x2*>(p));
-    return make_int2(v.x, v.y);
-#else
-    return *p;
-#endif
+    if constexpr (NT) {
+        const i32x2 v = __builtin_nontemporal_load(reinterpret_cast<const i32x2*>(p));
+        return make_int2(v.x, v.y);
+    } else {
+        return *p;
+    }
 }
 
 // ================================================================== theta ====
@@ -672,8 +681,8 @@ __global__ void __launch_bounds__(kBlock) k_csr_rows(Csr A, const double* __rest
         for (int j = 0; j < kPairs; ++j) {
             const int32_t k = base + 2 * (tid + j * kBlock);
             if (k + 1 < e) {
-                v[j] = *reinterpret_cast<const double2*>(A.va + k);
-                cc[j] = *reinterpret_cast<const int2*>(A.ci + k);
+                v[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const double2*>(A.va + k));
+                cc[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const int2*>(A.ci + k));
             } else if (k < e) {
                 v[j] = make_double2(A.va[k], 0.0);
                 cc[j] = make_int2(A.ci[k], 0);
@@ -699,7 +708,7 @@ __global__ void __launch_bounds__(kBlock) k_csr_rows(Csr A, const double* __rest
         if (live) {
             double acc = 0.0;
             for (int32_t k = ks; k < ke; ++k) acc += prod[k];
-            epi(r, acc, pe);
+            epi.template apply<MPBP_CSR_NT != 0>(r, acc, pe);
         }
     } else {
         // A single row longer than the LDS stage (the planner never groups such a row).
@@ -755,8 +764,8 @@ __global__ void __launch_bounds__(kBlock) k_sell_rows(Sell S, const double* __re
 #pragma unroll
         for (int j = 0; j < kSellPairs; ++j) {
             if (j < np) {
-                v[j] = ld_matrix(vp + (size_t)j * 64);
-                c[j] = ld_matrix(cp + (size_t)j * 64);
+                v[j] = ld_matrix<MPBP_SELL_NT != 0>(vp + (size_t)j * 64);
+                c[j] = ld_matrix<MPBP_SELL_NT != 0>(cp + (size_t)j * 64);
             } else {
                 v[j] = make_double2(0.0, 0.0);
                 c[j] = make_int2(0, 0);
@@ -1204,7 +1213,9 @@ __global__ void __launch_bounds__(kMB) k_march(S P, XS xs, int rows_per_block, E
             const int gr = P.r0 + lr;
             const XRing xa{sx, {sm, s0, sp}, gr, c0};
             const TRing ta{st, {sm, s0, sp}, gr, c0};
-            const bool edge = gr == 0 || gr == n - 1 || gc == 0 || gc == n - 1;
+            // the wrap-aware (sorting) form is exact for interior cells too: take it for the whole wave when
+            // any of its cells is on the periodic edge, so a wave never runs both forms
+            const bool edge = __builtin_amdgcn_readfirstlane(__any(gr == 0 || gr == n - 1 || gc == 0 || gc == n - 1)) != 0;
 #pragma unroll
             for (int o = 0; o < NO; ++o) {
                 double dg;
@@ -1419,7 +1430,7 @@ __device__ inline void f_sweep_cell(const FStencilDev& P, int gr, int gc, const 
                                     const double* bb, const double* dprev, double c1, double c2, double* xn,
                                     double* dn) {
     const int n = P.n;
-    const bool edge = gr <= 0 || gr >= n - 1 || gc <= 0 || gc >= n - 1;
+    const bool edge = __builtin_amdgcn_readfirstlane(__any(gr <= 0 || gr >= n - 1 || gc <= 0 || gc >= n - 1)) != 0;
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
         double fd;
@@ -2132,9 +2143,9 @@ namespace {
 template <class S>
 int pg_spmv(const S& P, int32_t mode, const double* x, const double* z, double* y, hipStream_t st) {
     switch (mode) {
-    case MPBP_SPMV_STORE: return launch_march(P, XPlain{x}, EpiStore{y}, g_march_rows, st);
-    case MPBP_SPMV_ADD: return launch_march(P, XPlain{x}, EpiAdd{z, y}, g_march_rows, st);
-    case MPBP_SPMV_RESID: return launch_march(P, XPlain{x}, EpiResid{z, y}, g_march_rows, st);
+    case MPBP_SPMV_STORE: return launch_march(P, XPlain{x}, EpiStore{y}, pg_rows(), st);
+    case MPBP_SPMV_ADD: return launch_march(P, XPlain{x}, EpiAdd{z, y}, pg_rows(), st);
+    case MPBP_SPMV_RESID: return launch_march(P, XPlain{x}, EpiResid{z, y}, pg_rows(), st);
     default: return set_error(MPBP_ERR_ARG, "pg_stencil_spmv: unknown mode %d", mode);
     }
 }
@@ -2164,7 +2175,7 @@ int mpbp_gtg_stencil_jacobi_step(const mpbp_stokes_params* prm, const double* ce
     int rc = make_pgstencil(prm, cell, part, &P);
     if (rc) return rc;
     if (!x_in || !b || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "gtg_stencil_jacobi_step: bad vectors");
-    return launch_march(GtGStencilDev{P}, XPlain{x_in}, EpiJacobi{x_in, b, nullptr, sub, x_out}, g_march_rows,
+    return launch_march(GtGStencilDev{P}, XPlain{x_in}, EpiJacobi{x_in, b, nullptr, sub, x_out}, pg_rows(),
                         as_stream(stream));
 }
 
@@ -2176,7 +2187,7 @@ static int gtg_stencil_cheb_impl(const mpbp_stokes_params* prm, const double* ce
     if (rc) return rc;
     if (!x_in || !b || !d || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "gtg_stencil_cheb_step: bad vectors");
     return launch_march(GtGStencilDev{P}, XPlain{x_in}, EpiCheb{x_in, b, nullptr, d, c1, c2, sub, x_out, store_d},
-                        g_march_rows, as_stream(stream));
+                        pg_rows(), as_stream(stream));
 }
 
 int mpbp_gtg_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell, const mpbp_row_part* part,
@@ -2292,8 +2303,8 @@ int op_first_sweep(const OpRef& o, bool cheb, const double* b, const double* dia
     const int rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &P);
     if (rc) return rc;
     const GtGStencilDev S{P};
-    return cheb ? launch_march(S, xs, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, g_march_rows, st)
-                : launch_march(S, xs, EpiJacobi{nullptr, b, nullptr, sub, xo}, g_march_rows, st);
+    return cheb ? launch_march(S, xs, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, pg_rows(), st)
+                : launch_march(S, xs, EpiJacobi{nullptr, b, nullptr, sub, xo}, pg_rows(), st);
 }
 
 // Sweeps 1 and 2 of an F inner solve from x0 = d0 = c2_0 b / diag in one pass (k_f_sweep2).
