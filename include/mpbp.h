@@ -284,6 +284,22 @@ int mpbp_set_stencil_kind(int32_t kind);
  * sweep, which is faster on MI355X.  One GPU, marching F stencil; results bit-identical. */
 int mpbp_set_sweep_fusion(int32_t rows);
 
+/* ---- ghost rows over RCCL point-to-point (multi-GPU row partition) ------------------------------ */
+/* One RCCL group of neighbour sends / receives straight from the owned boundary rows into the ghost
+ * rows of the ext layout (csrc/halo.cpp).  RCCL is dlopen'ed from rccl_path (NULL: "librccl.so").
+ * Setup: mpbp_rccl_unique_id on one rank (128 bytes), shared by the caller, then mpbp_halo_create on
+ * every rank (collective).  mpbp_halo_exchange is an mpbp_halo_fn: plan.halo = mpbp_halo_exchange,
+ * plan.halo_ctx = the handle; it cannot return an error, so callers check mpbp_halo_status after an
+ * apply.  world = 1 exchanges with itself (the periodic wrap) -- the single-GPU test of this path. */
+typedef struct mpbp_halo mpbp_halo;
+int mpbp_rccl_unique_id(const char* rccl_path, uint8_t* id_out);
+int mpbp_halo_create(const char* rccl_path, const uint8_t* id, int32_t world, int32_t rank, int32_t n,
+                     int32_t r0, int32_t rows, int32_t h_u, int32_t h_p, mpbp_halo** out);
+void mpbp_halo_destroy(mpbp_halo* halo);
+void mpbp_halo_exchange(void* halo, int32_t vec_kind, double* x_ext, int32_t phase, void* stream);
+int mpbp_halo_status(const mpbp_halo* halo);
+const char* mpbp_halo_last_error(const mpbp_halo* halo);
+
 /* gather: dst[i] = src[idx[i]] ; scatter: dst[idx[i]] = src[i]   (halo pack / unpack) */
 int mpbp_gather(int32_t count, const int32_t* idx, const double* src, double* dst, void* stream);
 int mpbp_scatter(int32_t count, const int32_t* idx, const double* src, double* dst, void* stream);

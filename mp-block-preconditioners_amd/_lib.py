@@ -111,6 +111,13 @@ _SIGNATURES = {
     "mpbp_gtg_stencil_jacobi_step": ([POINTER(StokesParams), _P, POINTER(RowPart), _P, _P, _P, _P, _P], c_int),
     "mpbp_gtg_stencil_cheb_step": ([POINTER(StokesParams), _P, POINTER(RowPart), _P, _P, c_double, c_double, _P, _P,
                                     _P, _P], c_int),
+    "mpbp_rccl_unique_id": ([ctypes.c_char_p, _P], c_int),
+    "mpbp_halo_create": ([ctypes.c_char_p, _P, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
+                          POINTER(c_void_p)], c_int),
+    "mpbp_halo_destroy": ([_P], None),
+    "mpbp_halo_exchange": ([_P, c_int32, _P, c_int32, _P], None),
+    "mpbp_halo_status": ([_P], c_int),
+    "mpbp_halo_last_error": ([_P], c_char_p),
     "mpbp_set_stencil_kind": ([c_int32], c_int),
     "mpbp_set_sweep_fusion": ([c_int32], c_int),
     "mpbp_gather": ([c_int32, _P, _P, _P, _P], c_int),

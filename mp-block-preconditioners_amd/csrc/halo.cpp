@@ -1,0 +1,213 @@
+// libmpbp -- ghost-row exchange of the row-partitioned apply over RCCL point-to-point (xGMI).
+//
+// Rank k owns grid rows [r0, r0 + L) of every field; its vectors hold the owned rows field-major and
+// then, per field, h ghost rows above and h below (distributed.py's "ext" layout).  A halo exchange is
+// one RCCL group of neighbour sends / receives issued straight from and into those rows -- no pack or
+// unpack kernels, no collective over all ranks, no Python in the loop:
+//   send own rows [r0, r0+h)        -> up   (= rank k-1, periodic): they are its bottom ghost rows
+//   send own rows [r0+L-h, r0+L)    -> down (= rank k+1, periodic): they are its top ghost rows
+//   recv bottom ghost rows          <- down,   recv top ghost rows <- up
+// Per peer pair the operations are matched in issue order, so every rank issues them in the same
+// order (fields ascending; send up, send down, recv down, recv up), which also covers world = 2 (up ==
+// down) and world = 1 (the periodic wrap onto itself).
+//
+// mpbp_halo_exchange has the mpbp_halo_fn signature: mpbp_schur_apply calls it with phase BEGIN before
+// a sweep's interior launch (the group runs on the halo's own stream, after an event recorded on the
+// apply stream) and END before its boundary launch (the apply stream waits for the group) -- the
+// interior rows overlap the transfer, and the fork/join is graph-capturable.
+//
+// RCCL is resolved at run time (dlopen of the library the caller names -- the one torch loaded, so the
+// process holds one RCCL), which keeps libmpbp free of a link-time RCCL dependency.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+
+#include "mpbp.h"
+
+namespace {
+
+struct Rccl {
+    void* lib = nullptr;
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+char g_halo_err[512] = "";
+
+int halo_error(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(g_halo_err, sizeof(g_halo_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int load_rccl(const char* path, Rccl* r) {
+    r->lib = dlopen(path && *path ? path : "librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!r->lib) return halo_error(MPBP_ERR_ARG, "dlopen RCCL: %s", dlerror());
+#define MPBP_SYM(field, name)                                                                  \
+    do {                                                                                       \
+        *reinterpret_cast<void**>(&r->field) = dlsym(r->lib, name);                           \
+        if (!r->field) return halo_error(MPBP_ERR_ARG, "RCCL symbol %s missing", name);        \
+    } while (0)
+    MPBP_SYM(get_unique_id, "ncclGetUniqueId");
+    MPBP_SYM(comm_init_rank, "ncclCommInitRank");
+    MPBP_SYM(comm_destroy, "ncclCommDestroy");
+    MPBP_SYM(send, "ncclSend");
+    MPBP_SYM(recv, "ncclRecv");
+    MPBP_SYM(group_start, "ncclGroupStart");
+    MPBP_SYM(group_end, "ncclGroupEnd");
+    MPBP_SYM(error_string, "ncclGetErrorString");
+#undef MPBP_SYM
+    return MPBP_OK;
+}
+
+}  // namespace
+
+struct mpbp_halo {
+    Rccl rccl;
+    ncclComm_t comm = nullptr;
+    int world = 0, rank = 0, up = 0, down = 0;
+    int n = 0, r0 = 0, rows = 0;
+    int h[2] = {0, 0};     // ghost depth of velocity (4 fields) and pressure (1 field) vectors
+    int nf[2] = {4, 1};
+    hipStream_t stream = nullptr;
+    hipEvent_t ready[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
+    int status = MPBP_OK;  // first error seen by mpbp_halo_exchange (its signature returns nothing)
+    char err[512] = "";
+};
+
+namespace {
+
+void fail(mpbp_halo* H, int code, const char* what, const char* detail) {
+    if (H->status == MPBP_OK) {
+        H->status = code;
+        std::snprintf(H->err, sizeof(H->err), "halo exchange: %s: %s", what, detail);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int mpbp_rccl_unique_id(const char* rccl_path, uint8_t* id_out) {
+    if (!id_out) return halo_error(MPBP_ERR_ARG, "rccl_unique_id: null output");
+    Rccl r;
+    int rc = load_rccl(rccl_path, &r);
+    if (rc) return rc;
+    ncclUniqueId id;
+    const ncclResult_t e = r.get_unique_id(&id);
+    if (e != ncclSuccess) return halo_error(MPBP_ERR_HIP, "ncclGetUniqueId: %s", r.error_string(e));
+    std::memcpy(id_out, &id, sizeof(id));
+    return MPBP_OK;
+}
+
+int mpbp_halo_create(const char* rccl_path, const uint8_t* id, int32_t world, int32_t rank, int32_t n,
+                     int32_t r0, int32_t rows, int32_t h_u, int32_t h_p, mpbp_halo** out) {
+    if (!id || !out || world < 1 || rank < 0 || rank >= world || n < 1 || rows < 1 || r0 < 0 || r0 + rows > n ||
+        h_u < 1 || h_p < 1 || h_u > rows || h_p > rows)
+        return halo_error(MPBP_ERR_ARG, "halo_create: bad partition (world %d rank %d n %d r0 %d rows %d h %d/%d)",
+                          world, rank, n, r0, rows, h_u, h_p);
+    mpbp_halo* H = new (std::nothrow) mpbp_halo();
+    if (!H) return halo_error(MPBP_ERR_ARG, "halo_create: out of host memory");
+    int rc = load_rccl(rccl_path, &H->rccl);
+    if (rc) {
+        delete H;
+        return rc;
+    }
+    H->world = world;
+    H->rank = rank;
+    H->up = (rank + world - 1) % world;
+    H->down = (rank + 1) % world;
+    H->n = n;
+    H->r0 = r0;
+    H->rows = rows;
+    H->h[0] = h_u;
+    H->h[1] = h_p;
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    const ncclResult_t e = H->rccl.comm_init_rank(&H->comm, world, uid, rank);
+    if (e != ncclSuccess) {
+        halo_error(MPBP_ERR_HIP, "ncclCommInitRank: %s", H->rccl.error_string(e));
+        delete H;
+        return MPBP_ERR_HIP;
+    }
+    bool ok = hipStreamCreateWithFlags(&H->stream, hipStreamNonBlocking) == hipSuccess;
+    for (int k = 0; k < 2 && ok; ++k)
+        ok = hipEventCreateWithFlags(&H->ready[k], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&H->done[k], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        mpbp_halo_destroy(H);
+        return halo_error(MPBP_ERR_HIP, "halo_create: stream / event creation failed");
+    }
+    *out = H;
+    return MPBP_OK;
+}
+
+void mpbp_halo_destroy(mpbp_halo* H) {
+    if (!H) return;
+    if (H->stream) (void)hipStreamSynchronize(H->stream);
+    for (int k = 0; k < 2; ++k) {
+        if (H->ready[k]) (void)hipEventDestroy(H->ready[k]);
+        if (H->done[k]) (void)hipEventDestroy(H->done[k]);
+    }
+    if (H->stream) (void)hipStreamDestroy(H->stream);
+    if (H->comm) H->rccl.comm_destroy(H->comm);
+    // the RCCL library stays loaded: torch (or another communicator) may still use it
+    delete H;
+}
+
+void mpbp_halo_exchange(void* ctx, int32_t vec_kind, double* x_ext, int32_t phase, void* stream) {
+    mpbp_halo* H = static_cast<mpbp_halo*>(ctx);
+    if (!H || H->status != MPBP_OK) return;
+    if (vec_kind != MPBP_VEC_VELOCITY && vec_kind != MPBP_VEC_PRESSURE) {
+        fail(H, MPBP_ERR_ARG, "vector kind", "unknown");
+        return;
+    }
+    const int k = vec_kind == MPBP_VEC_VELOCITY ? 0 : 1;
+    const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (phase == MPBP_HALO_END) {
+        if (hipStreamWaitEvent(st, H->done[k], 0) != hipSuccess) fail(H, MPBP_ERR_HIP, "join", "hipStreamWaitEvent");
+        return;
+    }
+    if (hipEventRecord(H->ready[k], st) != hipSuccess || hipStreamWaitEvent(H->stream, H->ready[k], 0) != hipSuccess) {
+        fail(H, MPBP_ERR_HIP, "fork", "hipEventRecord / hipStreamWaitEvent");
+        return;
+    }
+    const int nf = H->nf[k], h = H->h[k], n = H->n, L = H->rows;
+    const size_t cnt = (size_t)h * n;
+    const Rccl& R = H->rccl;
+    ncclResult_t e = R.group_start();
+    for (int f = 0; f < nf && e == ncclSuccess; ++f) {
+        double* own = x_ext + (size_t)f * L * n;
+        double* ghost = x_ext + (size_t)nf * L * n + (size_t)f * 2 * h * n;   // [h rows above | h rows below]
+        e = R.send(own, cnt, ncclFloat64, H->up, H->comm, H->stream);
+        if (e == ncclSuccess) e = R.send(own + (size_t)(L - h) * n, cnt, ncclFloat64, H->down, H->comm, H->stream);
+        if (e == ncclSuccess) e = R.recv(ghost + cnt, cnt, ncclFloat64, H->down, H->comm, H->stream);
+        if (e == ncclSuccess) e = R.recv(ghost, cnt, ncclFloat64, H->up, H->comm, H->stream);
+    }
+    const ncclResult_t eg = R.group_end();
+    if (e == ncclSuccess) e = eg;
+    if (e != ncclSuccess) {
+        fail(H, MPBP_ERR_HIP, "RCCL group", R.error_string(e));
+        return;
+    }
+    if (hipEventRecord(H->done[k], H->stream) != hipSuccess) fail(H, MPBP_ERR_HIP, "fork", "hipEventRecord");
+}
+
+int mpbp_halo_status(const mpbp_halo* H) { return H ? H->status : MPBP_ERR_ARG; }
+
+const char* mpbp_halo_last_error(const mpbp_halo* H) { return (H && H->status != MPBP_OK) ? H->err : g_halo_err; }
+
+}  // extern "C"

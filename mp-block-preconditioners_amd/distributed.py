@@ -8,15 +8,23 @@ Every field (u_n, v_n, u_s, v_s, p) is an n x n grid stored row-major; rank k ow
 
 Matrices keep their global row order inside a rank and have their columns renumbered into that
 layout (``DeviceCSR.extract``), so every local row sum is the global one, bit for bit.  Before a
-sweep reads a vector, ``HaloExchanger.begin`` packs the rank's top/bottom h owned rows of every
-field and posts one all-gather; rows that touch no ghost (the interior) are computed meanwhile;
-``end`` waits for the collective, copies the neighbours' strips into the ghost slots, and the
-boundary rows run.  The halo depth h of each vector kind is measured from the matrices that read
-it (F, D read velocity: h = 1; G, Gt_G, Gt_F_G read pressure: h = 2 for Gt_F_G).
+sweep reads a vector its ghost rows are refreshed while the rows that touch no ghost (the interior)
+are computed; the boundary rows run after.  Two exchange implementations:
+
+* ``RcclHalo`` (default with the nccl = RCCL backend): libmpbp's own RCCL communicator; one group of
+  neighbour ncclSend / ncclRecv per sweep straight from the owned boundary rows into the ghost rows,
+  issued from C inside ``mpbp_schur_apply`` on a side stream (fork / join by events) -- no pack
+  kernels, no Python between the kernels, graph-capturable.
+* ``HaloExchanger`` (gloo, CPU-staged; the tests' backend): packs the top/bottom h owned rows of every
+  field, all-gathers them, copies the neighbours' strips into the ghost slots.
+
+The halo depth h of each vector kind is measured from the matrices that read it (F, D read
+velocity: h = 1; G, Gt_G, Gt_F_G read pressure: h = 2 for Gt_F_G).
 """
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -25,7 +33,7 @@ import torch
 from . import _lib
 from ._lib import check, lib, ptr, stream_handle
 from .csr import DeviceCSR
-from .solve import PlanProfiling, _pg_stencil
+from .solve import PlanProfiling, _capture, _pg_stencil
 
 N_VEL_FIELDS = 4
 N_P_FIELDS = 1
@@ -36,8 +44,10 @@ class RowPartition:
     n: int
     world: int
     rank: int
+    ghosts: bool = False   # ghost slots even at world = 1 (the periodic self-exchange; tests the halo path)
 
     def __post_init__(self):
+        self.ghosts = self.ghosts or self.world > 1
         base, rem = divmod(self.n, self.world)
         self.r0 = self.rank * base + min(self.rank, rem)
         self.L = base + (1 if self.rank < rem else 0)
@@ -52,7 +62,7 @@ class RowPartition:
         return nfields * self.L * self.n
 
     def n_ext(self, nfields, h):
-        return self.n_owned(nfields) + (nfields * 2 * h * self.n if self.world > 1 else 0)
+        return self.n_owned(nfields) + (nfields * 2 * h * self.n if self.ghosts else 0)
 
     def owned_rows(self, nfields) -> np.ndarray:
         """Global ids (in a field-major vector of nfields fields) of the owned unknowns, local order."""
@@ -156,6 +166,53 @@ class HaloExchanger:
         self.end(x_ext)
 
 
+def rccl_library_path() -> str:
+    """The RCCL torch itself loaded (one RCCL per process), else ROCm's."""
+    p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    return p if os.path.exists(p) else "/opt/rocm/lib/librccl.so"
+
+
+class RcclHalo:
+    """Ghost-row exchange in libmpbp (csrc/halo.cpp): one RCCL group of neighbour sends / receives per
+    sweep, issued from C inside mpbp_schur_apply -- no pack kernels, no Python callback, no all-gather.
+    The communicator is libmpbp's own (its unique id travels over `group`); world = 1 exchanges with
+    itself (the periodic wrap)."""
+
+    def __init__(self, part: RowPartition, h_u: int, h_p: int, group=None):
+        path = rccl_library_path().encode()
+        uid = (ctypes.c_uint8 * 128)()
+        if part.world == 1:
+            check(lib().mpbp_rccl_unique_id(path, uid))
+        else:
+            import torch.distributed as dist
+            box = [None]
+            if part.rank == 0:
+                check(lib().mpbp_rccl_unique_id(path, uid))
+                box = [bytes(uid)]
+            dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                       group=group)
+            ctypes.memmove(uid, box[0], 128)
+        self.handle = ctypes.c_void_p()
+        check(lib().mpbp_halo_create(path, uid, part.world, part.rank, part.n, part.r0, part.L, h_u, h_p,
+                                     ctypes.byref(self.handle)))
+        self.fn = _lib.HALO_FN(ctypes.cast(lib().mpbp_halo_exchange, ctypes.c_void_p).value)
+
+    def check(self):
+        if lib().mpbp_halo_status(self.handle) != 0:
+            raise _lib.MpbpError(lib().mpbp_halo_last_error(self.handle).decode())
+
+    def close(self):
+        if self.handle:
+            lib().mpbp_halo_destroy(self.handle)
+            self.handle = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class DistributedSchurPreconditioner(PlanProfiling):
     """The approximate-commutator apply over a row partition of the grid (one rank per GPU).
 
@@ -165,7 +222,7 @@ class DistributedSchurPreconditioner(PlanProfiling):
     """
 
     def __init__(self, n, xi, eta_n, eta_s, c=1.0, d_u=-1.0, inner_F=None, inner_P=None, group=None,
-                 device=None, layout="sell", f_mode="auto", pg_mode="auto"):
+                 device=None, layout="sell", f_mode="auto", pg_mode="auto", halo="auto", self_halo=False):
         import torch.distributed as dist
         from .preconditioner import MultiphaseBlockPreconditioner
         from .solve import InnerSolver
@@ -173,7 +230,14 @@ class DistributedSchurPreconditioner(PlanProfiling):
         self.device = dev
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
-        self.part = part = RowPartition(n, world, rank)
+        # self_halo: a single rank still runs the partitioned apply, its ghost rows filled by the periodic
+        # self-exchange (exercises the interior / boundary launches and the halo path on one GPU)
+        self.part = part = RowPartition(n, world, rank, ghosts=bool(self_halo))
+        self.partitioned = part.ghosts
+        if halo not in ("auto", "rccl", "torch"):
+            raise ValueError("halo must be 'auto', 'rccl' or 'torch'")
+        backend = dist.get_backend(group)
+        self.halo_impl = halo if halo != "auto" else ("rccl" if backend == "nccl" else "torch")
         bp = MultiphaseBlockPreconditioner(n, xi, eta_n, eta_s, device=dev)
         _, _, F, D, G = bp.get_big_A_matrix(c=c, d_u=d_u)
         GtG, GtFG = bp.commutator_products(F, D, G)
@@ -230,9 +294,16 @@ class DistributedSchurPreconditioner(PlanProfiling):
         self._wu_owned = torch.zeros(nu, **f64)
         self._wp = [torch.zeros(np_ext, **f64) for _ in range(7)]
         self._tensors = {t.data_ptr(): t for t in self._wu + self._wp}
-        self._ex = {_lib.VEC_VELOCITY: HaloExchanger(part, N_VEL_FIELDS, self.h_u, dev, group),
-                    _lib.VEC_PRESSURE: HaloExchanger(part, N_P_FIELDS, self.h_p, dev, group)}
-        self._cb = _lib.HALO_FN(self._halo)
+        self._rccl = None
+        if not self.partitioned:
+            self._cb = _lib.HALO_FN()
+        elif self.halo_impl == "rccl":
+            self._rccl = RcclHalo(part, self.h_u, self.h_p, group)
+            self._cb = self._rccl.fn
+        else:
+            self._ex = {_lib.VEC_VELOCITY: HaloExchanger(part, N_VEL_FIELDS, self.h_u, dev, group),
+                        _lib.VEC_PRESSURE: HaloExchanger(part, N_P_FIELDS, self.h_p, dev, group)}
+            self._cb = _lib.HALO_FN(self._halo)
         self._prof = None
         self._plan = self._make_plan(world)
 
@@ -280,10 +351,11 @@ class DistributedSchurPreconditioner(PlanProfiling):
         elif self.pg_stencil is not None:
             p.f_prm, p.f_cell = self.pg_stencil.prm, self.pg_stencil.cell.data_ptr()
         # velocity (F, D) and pressure (G, Gt_G) input partitions of the stencil operators
-        p.f_part = _lib.RowPart(self.part.r0, self.part.L, self.h_u if world > 1 else 0, 0)
-        p.p_part = _lib.RowPart(self.part.r0, self.part.L, self.h_p if world > 1 else 0, 0)
-        p.halo = self._cb if world > 1 else _lib.HALO_FN()
-        p.halo_ctx = None
+        ghost = self.partitioned
+        p.f_part = _lib.RowPart(self.part.r0, self.part.L, self.h_u if ghost else 0, 0)
+        p.p_part = _lib.RowPart(self.part.r0, self.part.L, self.h_p if ghost else 0, 0)
+        p.halo = self._cb
+        p.halo_ctx = self._rccl.handle if self._rccl is not None else None
         p.prof_events = None
         p.prof_capacity = 0
         p.prof_count = ctypes.POINTER(ctypes.c_int32)()
@@ -298,7 +370,22 @@ class DistributedSchurPreconditioner(PlanProfiling):
         if out is None:
             out = torch.empty_like(v)
         check(lib().mpbp_schur_apply(ctypes.byref(self._plan), ptr(v), ptr(out), stream_handle()))
+        if self._rccl is not None:
+            self._rccl.check()
         return out
+
+    def capture(self, v: torch.Tensor, out: torch.Tensor):
+        """Capture one apply(v, out) into a hipGraph -- unpartitioned (single-rank) applies only: capturing
+        the RCCL point-to-point group of the halo exchange crashes this RCCL build (2.26.6, SIGSEGV
+        during capture), and the torch halo runs host-staged collectives between the kernels."""
+        if self.partitioned:
+            raise NotImplementedError("graph capture of the partitioned apply (halo exchange) is not supported")
+        return _capture(self, v, out)
+
+    def close(self):
+        if self._rccl is not None:
+            self._rccl.close()
+            self._rccl = None
 
     def local_to_global_rows(self):
         """Global ids (in the [u_n, v_n, u_s, v_s, p] numbering) of this rank's v / out entries."""

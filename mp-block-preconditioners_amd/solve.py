@@ -117,6 +117,24 @@ def _pg_stencil(D, G, GtG, f_stencil, pg_mode):
     return sp if ok else None
 
 
+def _capture(pc, v: torch.Tensor, out: torch.Tensor):
+    """One pc.apply(v, out) captured into a torch.cuda.CUDAGraph (warm-up on a side stream first)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    saved = (pc._plan.prof_events, pc._plan.prof_capacity)
+    pc._plan.prof_events, pc._plan.prof_capacity = None, 0
+    try:
+        with torch.cuda.stream(s):
+            pc.apply(v, out)                    # warm-up on a side stream, as torch requires
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            pc.apply(v, out)
+    finally:
+        pc._plan.prof_events, pc._plan.prof_capacity = saved
+    return g
+
+
 class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
     """M^-1 of the block upper-triangular approximate-commutator preconditioner (solve.py:257-277).
 
@@ -220,20 +238,7 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
         """Capture one apply(v, out) into a hipGraph (torch.cuda.CUDAGraph); replay() re-runs it on the
         same buffers.  mpbp_schur_apply allocates and synchronises nothing, so the whole apply becomes
         one graph launch (profiling events are recorded by eager applies only)."""
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        saved = (self._plan.prof_events, self._plan.prof_capacity)
-        self._plan.prof_events, self._plan.prof_capacity = None, 0
-        try:
-            with torch.cuda.stream(s):
-                self.apply(v, out)                  # warm-up on a side stream, as torch requires
-            torch.cuda.current_stream().wait_stream(s)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self.apply(v, out)
-        finally:
-            self._plan.prof_events, self._plan.prof_capacity = saved
-        return g
+        return _capture(self, v, out)
 
     def _matvec(self, x):
         v = torch.from_numpy(np.ascontiguousarray(np.ravel(x), dtype=np.float64)).to(self.device)

@@ -21,7 +21,7 @@ def build(spec):
     os.makedirs(out_dir, exist_ok=True)
     out = os.path.join(out_dir, f"libmpbp_{name}.so")
     cmd = [ge.HIPCC, *ge.HIP_FLAGS, *[f for f in flags.split(",") if f], "-I", os.path.join(ROOT, "include"),
-           os.path.join(ge.PKG, "csrc", "mpbp.hip"), "-o", out]
+           *ge.SOURCES, "-o", out, *ge.LIBS]
     subprocess.check_call(cmd)
     return out
 
