@@ -86,6 +86,11 @@ def main():
                          "marchR (LDS ring marching R grid rows per workgroup)")
     ap.add_argument("--sweep-fusion", type=int, default=0,
                     help="grid rows per workgroup of the fused init + two-sweep F kernel; 0 = one kernel per sweep")
+    ap.add_argument("--self-halo", action="store_true",
+                    help="N = 1 only: run the row-partitioned apply with the ghost rows refreshed by the periodic "
+                         "self-exchange over RCCL (measures the multi-GPU code path's overhead on one GPU)")
+    ap.add_argument("--halo-overlap", action="store_true",
+                    help="RCCL halo group on a side stream overlapping the interior rows (default: in order)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-spmv", action="store_true")
@@ -108,6 +113,10 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
         else:
             dist.init_process_group(backend)
+    elif args.self_halo:
+        dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{29400 + os.getpid() % 1000}", rank=0,
+                                world_size=1, **({"device_id": torch.device("cuda", dev_index)} if backend == "nccl" else {}))
+    partitioned = world > 1 or args.self_halo
 
     import mp_block_preconditioners_amd as mp
     from mp_block_preconditioners_amd._lib import check as _check, lib as _lib
@@ -120,7 +129,7 @@ def main():
     kp, spp = parse_inner(args.inner_p)
     iF, iP = mp.InnerSolver(kf, sf), mp.InnerSolver(kp, spp)
     A = None
-    if world == 1:
+    if not partitioned:
         bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
         A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
         pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, layout=args.layout,
@@ -129,7 +138,8 @@ def main():
     else:
         from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
         pc = DistributedSchurPreconditioner(n, args.xi, args.eta_n, args.eta_s, inner_F=iF, inner_P=iP,
-                                            layout=args.layout, f_mode=args.f_mode, pg_mode=args.pg_mode)
+                                            layout=args.layout, f_mode=args.f_mode, pg_mode=args.pg_mode,
+                                            self_halo=args.self_halo, halo_overlap=args.halo_overlap)
     gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
     v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda", generator=gen)
     out = torch.empty_like(v)
@@ -142,7 +152,7 @@ def main():
     # the events inside the timed loop itself.
     sweeps_per_apply = 2 * max(sf - 1, 0)
     graph, graph_note = None, None
-    if world == 1 and not args.no_graph:
+    if not partitioned and not args.no_graph:
         try:
             graph = pc.capture(v, out)
         except Exception as e:   # fall back to eager launches, and say so in the JSON line
@@ -173,7 +183,7 @@ def main():
     pc.disable_profiling()
 
     # dominant kernel: the fused Chebyshev-Jacobi sweep over F
-    fused_init = world == 1 and getattr(pc, "f_stencil", None) is not None and sk.startswith("march")
+    fused_init = not partitioned and getattr(pc, "f_stencil", None) is not None and sk.startswith("march")
     sbytes, kname = sweep_bytes(pc, args.layout, kf, sf, fused_init)
     avg_sweep_s = (sum(sweep_ms) / len(sweep_ms) / 1e3) if sweep_ms else float("nan")
     achieved = sbytes / avg_sweep_s / 1e9
@@ -186,7 +196,7 @@ def main():
     # tools/pmc_reduce.py: FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction + WRITE_SIZE)
     traffic = None
     pmc_files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic_r*.json")))
-    if pmc_files and world == 1:
+    if pmc_files and not partitioned:
         try:
             with open(pmc_files[-1]) as f:
                 pm = json.load(f)
@@ -197,7 +207,7 @@ def main():
             traffic = None
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not partitioned and not args.no_cpu_baseline:
         cpu = cpu_baseline(pc, v, args.cpu_seconds, kf, sf, kp, spp)
 
     if rank == 0:
@@ -226,6 +236,8 @@ def main():
                        "d_g_gtg": "matrix-free" if getattr(pc, "pg_stencil", None) is not None else "assembled",
                        "sweep_fusion_rows": args.sweep_fusion,
                        "launch": "hipgraph" if graph is not None else "eager",
+                       **({"halo": f"{pc.halo_impl} ({'self-exchange' if world == 1 else 'neighbour'})"}
+                          if partitioned else {}),
                        **({"note": graph_note} if graph_note else {})},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
@@ -238,7 +250,8 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if partitioned:
+        pc.close()
         dist.destroy_process_group()
 
 

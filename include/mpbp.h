@@ -99,8 +99,8 @@ typedef struct mpbp_sell {
 } mpbp_sell;
 
 /* Grid-row partition of the 4 velocity fields (multi-GPU F stencil): the rank owns grid rows
- * [r0, r0 + rows) of every field, followed in its vectors by `halo` ghost rows above and `halo`
- * below per field.  which: 0 all owned rows, 1 rows off the first/last owned grid row, 2 those
+ * [r0, r0 + rows) of every field, followed in its vectors by the ghost rows: `halo` rows above of
+ * every field (field-major), then `halo` rows below of every field.  which: 0 all owned rows, 1 rows off the first/last owned grid row, 2 those
  * rows.  NULL (or halo = 0) = one GPU, whole grid. */
 typedef struct mpbp_row_part {
     int32_t r0;
@@ -160,6 +160,9 @@ typedef struct mpbp_schur_plan {
     int32_t pg_stencil;              /* 1: D, G and Gt_G recomputed from the cell thn table (n >= 3);
                                         f_prm / f_cell are set whenever f_stencil or pg_stencil is */
     mpbp_row_part p_part;            /* pressure partition (G, Gt_G stencils); halo = 0 on one GPU */
+    int32_t halo_first;              /* 1: each exchange completes (BEGIN, END) before the sweep, whose
+                                        stencil rows then run as one launch; 0: interior rows launch
+                                        between BEGIN and END, boundary rows after */
 } mpbp_schur_plan;
 
 const char* mpbp_version(void);
@@ -285,8 +288,9 @@ int mpbp_set_stencil_kind(int32_t kind);
 int mpbp_set_sweep_fusion(int32_t rows);
 
 /* ---- ghost rows over RCCL point-to-point (multi-GPU row partition) ------------------------------ */
-/* One RCCL group of neighbour sends / receives straight from the owned boundary rows into the ghost
- * rows of the ext layout (csrc/halo.cpp).  RCCL is dlopen'ed from rccl_path (NULL: "librccl.so").
+/* One RCCL group of neighbour sends / receives: the owned boundary rows (packed into one buffer per
+ * direction when a vector has several fields) straight into the ghost rows of the ext layout
+ * (csrc/halo.cpp).  RCCL is dlopen'ed from rccl_path (NULL: "librccl.so").
  * Setup: mpbp_rccl_unique_id on one rank (128 bytes), shared by the caller, then mpbp_halo_create on
  * every rank (collective).  mpbp_halo_exchange is an mpbp_halo_fn: plan.halo = mpbp_halo_exchange,
  * plan.halo_ctx = the handle; it cannot return an error, so callers check mpbp_halo_status after an
@@ -298,6 +302,9 @@ int mpbp_halo_create(const char* rccl_path, const uint8_t* id, int32_t world, in
 void mpbp_halo_destroy(mpbp_halo* halo);
 void mpbp_halo_exchange(void* halo, int32_t vec_kind, double* x_ext, int32_t phase, void* stream);
 int mpbp_halo_status(const mpbp_halo* halo);
+#define MPBP_HALO_IN_ORDER 0   /* group issued on the apply stream between interior and boundary (default) */
+#define MPBP_HALO_OVERLAP 1    /* group on a side stream, forked / joined by events around the interior */
+int mpbp_halo_set_mode(mpbp_halo* halo, int32_t mode);
 const char* mpbp_halo_last_error(const mpbp_halo* halo);
 
 /* gather: dst[i] = src[idx[i]] ; scatter: dst[idx[i]] = src[i]   (halo pack / unpack) */

@@ -17,6 +17,7 @@ INNER_JACOBI, INNER_CHEBYSHEV = 0, 1
 HALO_BEGIN, HALO_END = 0, 1
 VEC_VELOCITY, VEC_PRESSURE = 0, 1
 PG_D, PG_G, PG_GTG = 0, 1, 2
+HALO_IN_ORDER, HALO_OVERLAP = 0, 1
 BLOCK_ROWS, BLOCK_NNZ = 256, 4095
 
 
@@ -69,7 +70,8 @@ class SchurPlan(Structure):
                 ("Fs_int", Sell), ("Fs_bnd", Sell), ("Ds_int", Sell), ("Ds_bnd", Sell), ("Gs_int", Sell),
                 ("Gs_bnd", Sell), ("Ps_int", Sell), ("Ps_bnd", Sell), ("Qs_int", Sell), ("Qs_bnd", Sell),
                 ("f_stencil", c_int32), ("f_prm", StokesParams), ("f_cell", c_void_p), ("f_uface", c_void_p),
-                ("f_vface", c_void_p), ("f_part", RowPart), ("pg_stencil", c_int32), ("p_part", RowPart)]
+                ("f_vface", c_void_p), ("f_part", RowPart), ("pg_stencil", c_int32), ("p_part", RowPart),
+                ("halo_first", c_int32)]
 
 
 _P = c_void_p
@@ -117,6 +119,7 @@ _SIGNATURES = {
     "mpbp_halo_destroy": ([_P], None),
     "mpbp_halo_exchange": ([_P, c_int32, _P, c_int32, _P], None),
     "mpbp_halo_status": ([_P], c_int),
+    "mpbp_halo_set_mode": ([_P, c_int32], c_int),
     "mpbp_halo_last_error": ([_P], c_char_p),
     "mpbp_set_stencil_kind": ([c_int32], c_int),
     "mpbp_set_sweep_fusion": ([c_int32], c_int),

@@ -1,20 +1,24 @@
 // libmpbp -- ghost-row exchange of the row-partitioned apply over RCCL point-to-point (xGMI).
 //
 // Rank k owns grid rows [r0, r0 + L) of every field; its vectors hold the owned rows field-major and
-// then, per field, h ghost rows above and h below (distributed.py's "ext" layout).  A halo exchange is
-// one RCCL group of neighbour sends / receives issued straight from and into those rows -- no pack or
-// unpack kernels, no collective over all ranks, no Python in the loop:
-//   send own rows [r0, r0+h)        -> up   (= rank k-1, periodic): they are its bottom ghost rows
-//   send own rows [r0+L-h, r0+L)    -> down (= rank k+1, periodic): they are its top ghost rows
-//   recv bottom ghost rows          <- down,   recv top ghost rows <- up
-// Per peer pair the operations are matched in issue order, so every rank issues them in the same
-// order (fields ascending; send up, send down, recv down, recv up), which also covers world = 2 (up ==
-// down) and world = 1 (the periodic wrap onto itself).
+// then the ghosts: h rows above of every field, then h rows below of every field (distributed.py's
+// "ext" layout), so each direction's ghosts are one contiguous block.  A halo exchange is one RCCL group
+// of four neighbour operations -- no collective over all ranks, no Python in the loop:
+//   send own rows [r0, r0+h) of every field      -> up   (= rank k-1, periodic): its rows below
+//   send own rows [r0+L-h, r0+L) of every field  -> down (= rank k+1, periodic): its rows above
+//   recv the rows below <- down,  recv the rows above <- up
+// A one-field vector sends its rows in place; a four-field one first gathers them (mpbp_gather, one
+// kernel) into [top rows of every field | bottom rows of every field].  Per peer pair the operations
+// are matched in issue order, so every rank issues them in the same order (send up, send down, recv
+// down, recv up), which also covers world = 2 (up == down) and world = 1 (the wrap onto itself).
 //
 // mpbp_halo_exchange has the mpbp_halo_fn signature: mpbp_schur_apply calls it with phase BEGIN before
-// a sweep's interior launch (the group runs on the halo's own stream, after an event recorded on the
-// apply stream) and END before its boundary launch (the apply stream waits for the group) -- the
-// interior rows overlap the transfer, and the fork/join is graph-capturable.
+// a sweep's interior launch and END before its boundary launch.  Two schedules (mpbp_halo_set_mode):
+//   IN_ORDER (default): the group is issued at END on the apply stream itself, after the interior.
+//   OVERLAP: the group runs on the halo's own highest-priority stream, forked at BEGIN and joined at
+//     END by events, so the transfer can overlap the interior rows.
+// Measured on one MI355X (self-exchange, 1024^2): OVERLAP gains nothing -- the group's kernel waits for
+// CUs behind the interior sweep, and each event packet adds ~15 us of queue latency -- so IN_ORDER.
 //
 // RCCL is resolved at run time (dlopen of the library the caller names -- the one torch loaded, so the
 // process holds one RCCL), which keeps libmpbp free of a link-time RCCL dependency.
@@ -24,6 +28,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
@@ -84,6 +89,9 @@ struct mpbp_halo {
     int nf[2] = {4, 1};
     hipStream_t stream = nullptr;
     hipEvent_t ready[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
+    int32_t* pack_idx[2] = {nullptr, nullptr};   // device: owned indices of [top rows | bottom rows] (nf > 1)
+    double* pack_buf[2] = {nullptr, nullptr};    // device: 2 nf h n staged values
+    int mode = MPBP_HALO_IN_ORDER;
     int status = MPBP_OK;  // first error seen by mpbp_halo_exchange (its signature returns nothing)
     char err[512] = "";
 };
@@ -143,13 +151,33 @@ int mpbp_halo_create(const char* rccl_path, const uint8_t* id, int32_t world, in
         delete H;
         return MPBP_ERR_HIP;
     }
-    bool ok = hipStreamCreateWithFlags(&H->stream, hipStreamNonBlocking) == hipSuccess;
+    // The group's kernel is launched next to the interior sweep, which fills every CU: on a
+    // highest-priority stream it is dispatched first instead of waiting for the sweep to drain.
+    int least = 0, greatest = 0;
+    bool ok = hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
+              hipStreamCreateWithPriority(&H->stream, hipStreamNonBlocking, greatest) == hipSuccess;
     for (int k = 0; k < 2 && ok; ++k)
         ok = hipEventCreateWithFlags(&H->ready[k], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&H->done[k], hipEventDisableTiming) == hipSuccess;
+    for (int k = 0; k < 2 && ok; ++k) {
+        if (H->nf[k] == 1) continue;
+        const int nf = H->nf[k], h = H->h[k];
+        const size_t cnt = (size_t)2 * nf * h * n;
+        int32_t* idx = static_cast<int32_t*>(std::malloc(cnt * sizeof(int32_t)));
+        ok = idx != nullptr;
+        for (int f = 0; ok && f < nf; ++f)
+            for (int j = 0; j < h * n; ++j) {
+                idx[(size_t)f * h * n + j] = f * rows * n + j;                                  // top rows
+                idx[(size_t)(nf + f) * h * n + j] = f * rows * n + (rows - h) * n + j;          // bottom rows
+            }
+        ok = ok && hipMalloc(&H->pack_idx[k], cnt * sizeof(int32_t)) == hipSuccess &&
+             hipMalloc(&H->pack_buf[k], cnt * sizeof(double)) == hipSuccess &&
+             hipMemcpy(H->pack_idx[k], idx, cnt * sizeof(int32_t), hipMemcpyHostToDevice) == hipSuccess;
+        std::free(idx);
+    }
     if (!ok) {
         mpbp_halo_destroy(H);
-        return halo_error(MPBP_ERR_HIP, "halo_create: stream / event creation failed");
+        return halo_error(MPBP_ERR_HIP, "halo_create: stream / event / buffer creation failed");
     }
     *out = H;
     return MPBP_OK;
@@ -163,10 +191,43 @@ void mpbp_halo_destroy(mpbp_halo* H) {
         if (H->done[k]) (void)hipEventDestroy(H->done[k]);
     }
     if (H->stream) (void)hipStreamDestroy(H->stream);
+    for (int k = 0; k < 2; ++k) {
+        if (H->pack_idx[k]) (void)hipFree(H->pack_idx[k]);
+        if (H->pack_buf[k]) (void)hipFree(H->pack_buf[k]);
+    }
     if (H->comm) H->rccl.comm_destroy(H->comm);
     // the RCCL library stays loaded: torch (or another communicator) may still use it
     delete H;
 }
+
+namespace {
+
+// One RCCL group on stream `on`: own top rows -> up, own bottom rows -> down, rows below <- down,
+// rows above <- up (a multi-field vector's rows gathered into pack_buf first, on the same stream).
+ncclResult_t halo_group(mpbp_halo* H, int k, double* x_ext, hipStream_t on) {
+    const int nf = H->nf[k], h = H->h[k], n = H->n, L = H->rows;
+    const size_t cnt = (size_t)nf * h * n;                   // values per direction
+    const double* top = x_ext;                               // nf == 1: the rows in place
+    const double* bot = x_ext + (size_t)(L - h) * n;
+    if (nf > 1) {
+        if (mpbp_gather((int32_t)(2 * cnt), H->pack_idx[k], x_ext, H->pack_buf[k], (void*)on) != MPBP_OK)
+            return ncclUnhandledCudaError;
+        top = H->pack_buf[k];
+        bot = H->pack_buf[k] + cnt;
+    }
+    double* above = x_ext + (size_t)nf * L * n;
+    double* below = above + cnt;
+    const Rccl& R = H->rccl;
+    ncclResult_t e = R.group_start();
+    if (e == ncclSuccess) e = R.send(top, cnt, ncclFloat64, H->up, H->comm, on);
+    if (e == ncclSuccess) e = R.send(bot, cnt, ncclFloat64, H->down, H->comm, on);
+    if (e == ncclSuccess) e = R.recv(below, cnt, ncclFloat64, H->down, H->comm, on);
+    if (e == ncclSuccess) e = R.recv(above, cnt, ncclFloat64, H->up, H->comm, on);
+    const ncclResult_t eg = R.group_end();
+    return e == ncclSuccess ? eg : e;
+}
+
+}  // namespace
 
 void mpbp_halo_exchange(void* ctx, int32_t vec_kind, double* x_ext, int32_t phase, void* stream) {
     mpbp_halo* H = static_cast<mpbp_halo*>(ctx);
@@ -177,6 +238,15 @@ void mpbp_halo_exchange(void* ctx, int32_t vec_kind, double* x_ext, int32_t phas
     }
     const int k = vec_kind == MPBP_VEC_VELOCITY ? 0 : 1;
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (H->mode == MPBP_HALO_IN_ORDER) {
+        // the group goes on the apply stream between the interior and the boundary launches: no event
+        // packets (each costs ~15 us of queue latency here), and its host-side enqueue overlaps the interior
+        if (phase == MPBP_HALO_END) {
+            const ncclResult_t e = halo_group(H, k, x_ext, st);
+            if (e != ncclSuccess) fail(H, MPBP_ERR_HIP, "RCCL group", H->rccl.error_string(e));
+        }
+        return;
+    }
     if (phase == MPBP_HALO_END) {
         if (hipStreamWaitEvent(st, H->done[k], 0) != hipSuccess) fail(H, MPBP_ERR_HIP, "join", "hipStreamWaitEvent");
         return;
@@ -185,25 +255,19 @@ void mpbp_halo_exchange(void* ctx, int32_t vec_kind, double* x_ext, int32_t phas
         fail(H, MPBP_ERR_HIP, "fork", "hipEventRecord / hipStreamWaitEvent");
         return;
     }
-    const int nf = H->nf[k], h = H->h[k], n = H->n, L = H->rows;
-    const size_t cnt = (size_t)h * n;
-    const Rccl& R = H->rccl;
-    ncclResult_t e = R.group_start();
-    for (int f = 0; f < nf && e == ncclSuccess; ++f) {
-        double* own = x_ext + (size_t)f * L * n;
-        double* ghost = x_ext + (size_t)nf * L * n + (size_t)f * 2 * h * n;   // [h rows above | h rows below]
-        e = R.send(own, cnt, ncclFloat64, H->up, H->comm, H->stream);
-        if (e == ncclSuccess) e = R.send(own + (size_t)(L - h) * n, cnt, ncclFloat64, H->down, H->comm, H->stream);
-        if (e == ncclSuccess) e = R.recv(ghost + cnt, cnt, ncclFloat64, H->down, H->comm, H->stream);
-        if (e == ncclSuccess) e = R.recv(ghost, cnt, ncclFloat64, H->up, H->comm, H->stream);
-    }
-    const ncclResult_t eg = R.group_end();
-    if (e == ncclSuccess) e = eg;
+    const ncclResult_t e = halo_group(H, k, x_ext, H->stream);
     if (e != ncclSuccess) {
-        fail(H, MPBP_ERR_HIP, "RCCL group", R.error_string(e));
+        fail(H, MPBP_ERR_HIP, "RCCL group", H->rccl.error_string(e));
         return;
     }
     if (hipEventRecord(H->done[k], H->stream) != hipSuccess) fail(H, MPBP_ERR_HIP, "fork", "hipEventRecord");
+}
+
+int mpbp_halo_set_mode(mpbp_halo* H, int32_t mode) {
+    if (!H || (mode != MPBP_HALO_OVERLAP && mode != MPBP_HALO_IN_ORDER))
+        return halo_error(MPBP_ERR_ARG, "halo_set_mode: mode must be MPBP_HALO_OVERLAP or MPBP_HALO_IN_ORDER");
+    H->mode = mode;
+    return MPBP_OK;
 }
 
 int mpbp_halo_status(const mpbp_halo* H) { return H ? H->status : MPBP_ERR_ARG; }

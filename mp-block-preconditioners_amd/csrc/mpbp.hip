@@ -835,8 +835,9 @@ struct FStencilDev {
     double dxdx;   // dx * dx
     double idx2;   // 1.0 / (dx * dx)   (== 1.0 / (dy * dy), 1.0 / (dx * dy): dx == dy)
     double midy2;  // -1.0 / (dy * dy)
-    // row partition: this rank owns grid rows [r0, r0 + L) of each of the 4 velocity fields; ghosts
-    // (h rows above, h below, per field) follow the 4*L*n owned entries.  One GPU: r0 = 0, L = n, h = 0.
+    // row partition: this rank owns grid rows [r0, r0 + L) of each of the 4 velocity fields; the ghosts
+    // follow the 4*L*n owned entries: h rows above of every field, then h rows below of every field.
+    // One GPU: r0 = 0, L = n, h = 0.
     int r0, L, h, which;
     int pow2;      // n is a power of two: dx * dx is a power of two and v / (dx * dx) == v * idx2 exactly
 
@@ -846,7 +847,7 @@ struct FStencilDev {
         if (h == 0) return (f * n + wrap(gr)) * n;
         const int lr = gr - r0;
         if (lr >= 0 && lr < L) return (f * L + lr) * n;
-        return 4 * L * n + f * 2 * h * n + (lr < 0 ? (h - 1) : h) * n;    // ghost row r0-1 / r0+L
+        return 4 * L * n + (lr < 0 ? f * h + h - 1 : 4 * h + f * h) * n;   // ghost row r0-1 / r0+L
     }
     // k_march policy: the 4 velocity fields staged, the cell's 4 rows out
     static constexpr int NF = 4, NOUT = 4;
@@ -1266,7 +1267,7 @@ struct PGDev {
         if (h == 0) return (f * n + wrap(gr)) * n;
         const int lr = gr - r0;
         if (lr >= 0 && lr < L) return (f * L + lr) * n;
-        return NFI * L * n + f * 2 * h * n + (lr < 0 ? (h - 1) : h) * n;
+        return NFI * L * n + (lr < 0 ? f * h + h - 1 : NFI * h + f * h) * n;
     }
 };
 
@@ -2284,7 +2285,7 @@ struct OpPair {
 // from b and diag wherever the sweep stages x) when the operator is a whole-grid marching stencil.
 bool can_fuse_init(const OpPair& op) {
     const OpRef& o = op.in;
-    return o.stencil && !o.empty && op.bd.empty && o.which == 0 &&
+    return o.stencil && !o.stencil->halo && !o.empty && op.bd.empty && o.which == 0 &&
            (o.sop == SOP_GTG || (o.sop == SOP_F && g_stencil_kind == 2));
 }
 
@@ -2342,6 +2343,12 @@ OpPair make_stencil_op(const mpbp_schur_plan* p, int32_t sop, bool partitioned) 
 template <class Fn>
 int two_phase(const Ctx& c, int32_t kind, const double* x_ext, const OpPair& op, Fn&& launch) {
     const mpbp_schur_plan* p = c.p;
+    if (p->halo && p->halo_first) {   // exchange first, then every row (stencils: one whole-partition launch)
+        p->halo(p->halo_ctx, kind, const_cast<double*>(x_ext), MPBP_HALO_BEGIN, (void*)c.st);
+        p->halo(p->halo_ctx, kind, const_cast<double*>(x_ext), MPBP_HALO_END, (void*)c.st);
+        const int rc = launch(op.in);
+        return rc ? rc : launch(op.bd);
+    }
     if (p->halo) p->halo(p->halo_ctx, kind, const_cast<double*>(x_ext), MPBP_HALO_BEGIN, (void*)c.st);
     int rc = launch(op.in);
     if (rc) return rc;
@@ -2424,7 +2431,7 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
         return set_error(MPBP_ERR_ARG, "schur_apply: partitioned D / G / Gt_G stencils need f_part and p_part");
     if ((p->f_stencil || p->pg_stencil) && !p->f_cell)
         return set_error(MPBP_ERR_ARG, "schur_apply: stencil operators need the thn tables");
-    const bool part = p->halo != nullptr;
+    const bool part = p->halo != nullptr && !p->halo_first;   // stencils split interior / boundary rows
     const OpPair F = p->f_stencil ? make_stencil_op(p, SOP_F, part)
                                   : make_op(p, p->F, p->F_int, p->F_bnd, p->Fs_int, p->Fs_bnd);
     const OpPair D = p->pg_stencil ? make_stencil_op(p, SOP_D, part)

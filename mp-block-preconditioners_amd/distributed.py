@@ -4,7 +4,8 @@ Every field (u_n, v_n, u_s, v_s, p) is an n x n grid stored row-major; rank k ow
 [r0, r1) of every field.  A rank's vector is laid out "owned first, then ghosts":
 
     owned:  field-major, f * L*n + (gr - r0)*n + c                  (L = r1 - r0)
-    ghosts: per field f, h rows above (r0-h .. r0-1) then h rows below (r1 .. r1+h-1), periodic
+    ghosts: h rows above (r0-h .. r0-1) of every field, then h rows below (r1 .. r1+h-1) of every
+            field (periodic): above row j of field f at (f*h + j)*n, below at (nf*h + f*h + j)*n
 
 Matrices keep their global row order inside a rank and have their columns renumbered into that
 layout (``DeviceCSR.extract``), so every local row sum is the global one, bit for bit.  Before a
@@ -79,12 +80,11 @@ class RowPartition:
                 raise ValueError(f"halo depth {h} exceeds the {self.min_rows} grid rows of the smallest rank")
             cols = np.arange(n, dtype=np.int64)
             for f in range(nfields):
-                g0 = own + f * 2 * h * n
                 for j in range(h):
                     top = (self.r0 - h + j) % n
                     bot = (self.r1 + j) % n
-                    cm[f * N + top * n + cols] = g0 + j * n + cols
-                    cm[f * N + bot * n + cols] = g0 + h * n + j * n + cols
+                    cm[f * N + top * n + cols] = own + (f * h + j) * n + cols
+                    cm[f * N + bot * n + cols] = own + (nfields * h + f * h + j) * n + cols
         for f in range(nfields):
             cm[f * N + self.r0 * n: f * N + self.r1 * n] = f * L * n + np.arange(L * n, dtype=np.int32)
         return cm
@@ -157,9 +157,9 @@ class HaloExchanger:
             self.work = None
         k, W = self.part.rank, self.part.world
         R = self.recv.view(W, self.nf, 2, self.hn)
-        g = x_ext[self.part.n_owned(self.nf): self.part.n_ext(self.nf, self.h)].view(self.nf, 2, self.hn)
-        g[:, 0] = R[(k - 1) % W, :, 1].to(g.device, non_blocking=True)
-        g[:, 1] = R[(k + 1) % W, :, 0].to(g.device, non_blocking=True)
+        g = x_ext[self.part.n_owned(self.nf): self.part.n_ext(self.nf, self.h)].view(2, self.nf, self.hn)
+        g[0] = R[(k - 1) % W, :, 1].to(g.device, non_blocking=True)     # rows above: up's bottom rows
+        g[1] = R[(k + 1) % W, :, 0].to(g.device, non_blocking=True)     # rows below: down's top rows
 
     def exchange(self, x_ext):
         self.begin(x_ext)
@@ -178,7 +178,7 @@ class RcclHalo:
     The communicator is libmpbp's own (its unique id travels over `group`); world = 1 exchanges with
     itself (the periodic wrap)."""
 
-    def __init__(self, part: RowPartition, h_u: int, h_p: int, group=None):
+    def __init__(self, part: RowPartition, h_u: int, h_p: int, group=None, overlap: bool = False):
         path = rccl_library_path().encode()
         uid = (ctypes.c_uint8 * 128)()
         if part.world == 1:
@@ -195,6 +195,8 @@ class RcclHalo:
         self.handle = ctypes.c_void_p()
         check(lib().mpbp_halo_create(path, uid, part.world, part.rank, part.n, part.r0, part.L, h_u, h_p,
                                      ctypes.byref(self.handle)))
+        check(lib().mpbp_halo_set_mode(self.handle, _lib.HALO_OVERLAP if overlap else _lib.HALO_IN_ORDER))
+        self.overlap = overlap
         self.fn = _lib.HALO_FN(ctypes.cast(lib().mpbp_halo_exchange, ctypes.c_void_p).value)
 
     def check(self):
@@ -222,7 +224,8 @@ class DistributedSchurPreconditioner(PlanProfiling):
     """
 
     def __init__(self, n, xi, eta_n, eta_s, c=1.0, d_u=-1.0, inner_F=None, inner_P=None, group=None,
-                 device=None, layout="sell", f_mode="auto", pg_mode="auto", halo="auto", self_halo=False):
+                 device=None, layout="sell", f_mode="auto", pg_mode="auto", halo="auto", self_halo=False,
+                 halo_overlap=False):
         import torch.distributed as dist
         from .preconditioner import MultiphaseBlockPreconditioner
         from .solve import InnerSolver
@@ -298,7 +301,7 @@ class DistributedSchurPreconditioner(PlanProfiling):
         if not self.partitioned:
             self._cb = _lib.HALO_FN()
         elif self.halo_impl == "rccl":
-            self._rccl = RcclHalo(part, self.h_u, self.h_p, group)
+            self._rccl = RcclHalo(part, self.h_u, self.h_p, group, overlap=halo_overlap)
             self._cb = self._rccl.fn
         else:
             self._ex = {_lib.VEC_VELOCITY: HaloExchanger(part, N_VEL_FIELDS, self.h_u, dev, group),
@@ -356,6 +359,9 @@ class DistributedSchurPreconditioner(PlanProfiling):
         p.p_part = _lib.RowPart(self.part.r0, self.part.L, self.h_p if ghost else 0, 0)
         p.halo = self._cb
         p.halo_ctx = self._rccl.handle if self._rccl is not None else None
+        # the in-order RCCL schedule gains nothing from splitting rows around the exchange: exchange first,
+        # then one launch per sweep
+        p.halo_first = 1 if (self._rccl is not None and not self._rccl.overlap) else 0
         p.prof_events = None
         p.prof_capacity = 0
         p.prof_count = ctypes.POINTER(ctypes.c_int32)()

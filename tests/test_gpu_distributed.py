@@ -65,7 +65,7 @@ def test_distributed_apply_matches_single_gpu(world, n, layout, f_mode, kind, tm
         pytest.fail(f"distributed worker failed:\n{msg}")
 
 
-def _self_halo_worker(_index, port, n, halo, f_mode, pg_mode, kind, graph, errfile):
+def _self_halo_worker(_index, port, n, halo, f_mode, pg_mode, kind, graph, errfile, overlap=False):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         torch.cuda.set_device(0)
@@ -75,7 +75,7 @@ def _self_halo_worker(_index, port, n, halo, f_mode, pg_mode, kind, graph, errfi
         mpb.lib().mpbp_set_stencil_kind(kind)
         iF, iP = mpb.InnerSolver("chebyshev", 4), mpb.InnerSolver("chebyshev", 3)
         dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, f_mode=f_mode,
-                                             pg_mode=pg_mode, halo=halo, self_halo=True)
+                                             pg_mode=pg_mode, halo=halo, self_halo=True, halo_overlap=overlap)
         assert dpc.partitioned and dpc.nu_ext > dpc.nu
         bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
         _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
@@ -99,11 +99,12 @@ def _self_halo_worker(_index, port, n, halo, f_mode, pg_mode, kind, graph, errfi
         raise
 
 
-@pytest.mark.parametrize("n,halo,f_mode,pg_mode,kind,graph", [
-    (64, "rccl", "stencil", "stencil", 2, False), (50, "rccl", "assembled", "assembled", 2, False),
-    (33, "rccl", "stencil", "assembled", 0, False), (64, "torch", "stencil", "stencil", 2, False),
-    (64, "rccl", "stencil", "stencil", 2, True)])
-def test_self_halo_partitioned_apply(n, halo, f_mode, pg_mode, kind, graph, tmp_path):
+@pytest.mark.parametrize("n,halo,f_mode,pg_mode,kind,graph,overlap", [
+    (64, "rccl", "stencil", "stencil", 2, False, False), (50, "rccl", "assembled", "assembled", 2, False, False),
+    (33, "rccl", "stencil", "assembled", 0, False, False), (64, "torch", "stencil", "stencil", 2, False, False),
+    (64, "rccl", "stencil", "stencil", 2, True, False), (64, "rccl", "stencil", "stencil", 2, False, True),
+    (40, "rccl", "assembled", "stencil", 2, False, True)])
+def test_self_halo_partitioned_apply(n, halo, f_mode, pg_mode, kind, graph, overlap, tmp_path):
     """One rank runs the partitioned apply with ghost rows filled by the periodic self-exchange -- the
     RCCL point-to-point halo (libmpbp's own communicator) and the torch one -- bit for bit against the
     single-GPU apply."""
@@ -111,8 +112,8 @@ def test_self_halo_partitioned_apply(n, halo, f_mode, pg_mode, kind, graph, tmp_
         pytest.skip("no GPU")
     errfile = str(tmp_path / "err.txt")
     try:
-        mp.spawn(_self_halo_worker, args=(_free_port(), n, halo, f_mode, pg_mode, kind, graph, errfile), nprocs=1,
-                 join=True)
+        mp.spawn(_self_halo_worker, args=(_free_port(), n, halo, f_mode, pg_mode, kind, graph, errfile, overlap),
+                 nprocs=1, join=True)
     except Exception:
         msg = open(errfile).read() if os.path.exists(errfile) else ""
         pytest.fail(f"self-halo worker failed:\n{msg}")
