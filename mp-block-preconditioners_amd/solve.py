@@ -374,3 +374,19 @@ def solve_with_approx_schur_pc(n, xi, etan, etas, c, d, b_vec, u_vec, inner_F=No
         print("\nPrinting error norms for solving Ax=b using fGMRES with approx schur complement as preconditioner:")
         print_norms(u_approx, u_vec, 1 / n, 1 / n, n)
     return u_approx, info, hist
+
+
+def solve_without_pc(n, A, b_vec, u_vec, tol=1e-8, maxiter=100, verbose=True):
+    """solve.py:202-208: FGMRES on A without a preconditioner (x0 = 0), then the error norms.
+
+    A is the DeviceCSR from get_big_A_matrix; returns (u_approx, info, residual history)."""
+    from .utils import print_norms
+    b = torch.from_numpy(np.ascontiguousarray(b_vec, dtype=np.float64)).to(A.device)
+    hist = []
+    x, info = fgmres(A, b, x0=torch.zeros_like(b), M=None, tol=tol, maxiter=maxiter,
+                     callback=print_true_res_norm(A, b) if verbose else None, residuals=hist)
+    u_approx = x.cpu().numpy()
+    if verbose:
+        print("\nPrinting error norms for solving Ax=b using fGMRES without preconditioner:")
+        print_norms(u_approx, u_vec, 1 / n, 1 / n, n)
+    return u_approx, info, hist

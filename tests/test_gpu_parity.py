@@ -288,3 +288,27 @@ def test_fgmres_converges_with_gpu_preconditioner():
     assert info == 0 and hist[-1] <= 1e-8 * hist[0] * 1.0001
     # discretisation error of the converged solution (velocity components), O(h^2)
     assert np.max(np.abs(x[: 4 * n * n] - u[: 4 * n * n])) < 5e-2
+
+
+def test_fgmres_without_preconditioner_and_constant_theta():
+    """configs[0]'s plumbing case on the GPU path: constant thn (theta_n = theta_s = 1/2), FGMRES without a
+    preconditioner (solve.py:202-208) -- and the preconditioned solve cuts the iteration count."""
+    mp = _mp()
+    n = 16
+    N = n * n
+    half = np.full(N, 0.5)
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 1.0, 1.0)
+    bp.set_theta_tables(half, half, half)
+    A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    rng = np.random.default_rng(0)
+    u = rng.standard_normal(5 * N)
+    b = A.matvec(torch.from_numpy(u).cuda()).cpu().numpy()
+    x, info, hist = mp.solve_without_pc(n, A, b, u, tol=1e-10, maxiter=2000, verbose=False)
+    assert info == 0 and hist[-1] <= 1e-10 * hist[0] * 1.0001
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("chebyshev", 8),
+                                      inner_P=mp.InnerSolver("chebyshev", 8))
+    hist_pc = []
+    xp, info_pc = mp.fgmres(A, torch.from_numpy(b).cuda(), M=pc, tol=1e-10, maxiter=2000, residuals=hist_pc)
+    assert info_pc == 0 and len(hist_pc) < len(hist)
+    # the pressure is determined up to a constant on the periodic grid: compare velocities
+    assert np.max(np.abs(x[: 4 * N] - u[: 4 * N])) < 1e-6 and np.max(np.abs(xp.cpu().numpy()[: 4 * N] - u[: 4 * N])) < 1e-6
