@@ -849,11 +849,14 @@ struct FStencilDev {
         if (lr >= 0 && lr < L) return (f * L + lr) * n;
         return 4 * L * n + (lr < 0 ? f * h + h - 1 : 4 * h + f * h) * n;   // ghost row r0-1 / r0+L
     }
-    // k_march policy: the 4 velocity fields staged, the cell's 4 rows out
+    // k_march policy: the 4 velocity fields staged, the cell's 4 rows out; per cell, the u- and v-face
+    // thn values are requested with the epilogue operands (before the barrier), not inside the rows
     static constexpr int NF = 4, NOUT = 4;
+    struct Cell { double face[2]; };
+    __device__ Cell cell_pre(int gr, int gc) const { return {{uface[gr * n + gc], vface[gr * n + gc]}}; }
     __device__ int32_t out_row(int f, int lr, int gc) const { return (f * L + lr) * n + gc; }
     template <bool EDGE, class TA, class XA>
-    __device__ double row(int f, int gr, int gc, const TA& ta, const XA& xa, double* fd) const;
+    __device__ double row(int f, int gr, int gc, const TA& ta, const XA& xa, double* fd, const Cell& cl) const;
 };
 
 // The ten entries of one F row, built in the assembled row's column order for interior points and
@@ -862,7 +865,7 @@ struct FStencilDev {
 // [-1, n]; the accessors wrap).  Same operations as phase_L_row / F_row, same summation order.
 template <bool EDGE, class TA, class XA, bool VIRT = false>
 __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, const TA& ta, const XA& xa,
-                               double* fdiag) {
+                               double* fdiag, const double* face = nullptr) {
     const int n = P.n;
     const int p = f >> 1;
     const double idx2 = P.idx2;
@@ -881,7 +884,7 @@ __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, cons
         const double iph_jmh = 0.25 * (tij + tip1j + tijm1 + tip1jm1);
         const double iph_j = 0.5 * (tij + tip1j);
         const double xi_ii = xi_of(P.xi, iph_j);
-        const double th = P.uface[kc];
+        const double th = face ? face[0] : P.uface[kc];   // face: thn at the u / v face, loaded ahead
         const double w = p ? P.c * (1.0 - th) : P.c * th;
         const double Ldiag = idx2 * (-tip1j - tij) + idx2 * (-iph_jph - iph_jmh);
         const double fd = (w - P.d_u * xi_ii) + P.d_u * (eta * Ldiag);
@@ -910,7 +913,7 @@ __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, cons
         const double tim1j = T(gr, gc - 1), tim1jp1 = T(gr - 1, gc - 1);
         const double ip1_jph = 0.5 * (tij + tijp1);
         const double xi_ii = xi_of(P.xi, ip1_jph);
-        const double th = P.vface[kc];
+        const double th = face ? face[1] : P.vface[kc];
         const double w = p ? P.c * (1.0 - th) : P.c * th;
         const double imh_jph = 0.25 * (tim1j + tim1jp1 + tij + tijp1);
         const double iph_jph = 0.25 * (tij + tip1j + tijp1 + tip1jp1);
@@ -1135,14 +1138,20 @@ struct TileRow {
 template <class S, class XS>
 __device__ inline void load_tile_row(const S& P, const XS& xs, int gr, int gcA, bool okA, int gcB, bool okB,
                                      TileRow<S::NF>& tr) {
+    // the main column's loads unconditional from a clamped column, then a select (no branch: the waits
+    // stay counted, so the row's loads remain in flight through the next compute); the 2 halo lanes' ones
+    // under their predicate
+    const int ca = okA ? gcA : 0;
 #pragma unroll
     for (int f = 0; f < S::NF; ++f) {
         const int32_t base = P.xrow(f, gr);
-        tr.xa[f] = okA ? xs(base + gcA) : 0.0;
+        const double va = xs(base + ca);
+        tr.xa[f] = okA ? va : 0.0;
         tr.xb[f] = okB ? xs(base + gcB) : 0.0;
     }
     const int32_t tb = P.wrap(gr) * P.n;
-    tr.ta = okA ? P.cell[tb + gcA] : 0.0;
+    const double ta = P.cell[tb + ca];
+    tr.ta = okA ? ta : 0.0;
     tr.tb = okB ? P.cell[tb + gcB] : 0.0;
 }
 
@@ -1172,7 +1181,9 @@ __device__ inline bool march_rows(int which, int L, int chunk, int rows_per_bloc
 }
 
 template <class S, class XS, class Epi>
-__global__ void __launch_bounds__(kMB) k_march(S P, XS xs, int rows_per_block, Epi epi) {
+// (4 waves per SIMD asked for explicitly: the F Chebyshev instance would otherwise take 130 VGPRs -> 3)
+__global__ void __launch_bounds__(kMB) __attribute__((amdgpu_waves_per_eu(4, 8)))
+k_march(S P, XS xs, int rows_per_block, Epi epi) {
     constexpr int NF = S::NF, NO = S::NOUT;
     __shared__ double sx[NF * 3 * kMTileW];
     __shared__ double st[3 * kMTileW];
@@ -1202,12 +1213,14 @@ __global__ void __launch_bounds__(kMB) k_march(S P, XS xs, int rows_per_block, E
     for (int lr = la; lr < lb; ++lr) {
         const int k = lr - la;
         const int sm = k % 3, s0 = (k + 1) % 3, sp = (k + 2) % 3;
-        typename Epi::P pe[NO];
-        if (live) {                                          // epilogue operands of row lr, in flight
-#pragma unroll
-            for (int o = 0; o < NO; ++o) pe[o] = epi.pre_lite(P.out_row(o, lr, gc));
-        }
         store_tile_row(sx, st, sp, tid, extra, tr);          // row lr+1
+        // operands of this row's epilogues and cells, requested unconditionally (lanes past the grid edge
+        // read row 0 and discard it) so the wait counts stay exact and later loads stay in flight
+        const int gcl = live ? gc : 0;
+        typename Epi::P pe[NO];
+#pragma unroll
+        for (int o = 0; o < NO; ++o) pe[o] = epi.pre_lite(P.out_row(o, lr, gcl));
+        const typename S::Cell cl = P.cell_pre(P.r0 + lr, gcl);
         __syncthreads();
         if (lr + 1 < lb) load_tile_row(P, xs, P.r0 + lr + 2, gcA, okA, gcB, okB, tr);   // in flight
         if (live) {
@@ -1220,8 +1233,8 @@ __global__ void __launch_bounds__(kMB) k_march(S P, XS xs, int rows_per_block, E
 #pragma unroll
             for (int o = 0; o < NO; ++o) {
                 double dg;
-                const double acc = edge ? P.template row<true>(o, gr, gc, ta, xa, &dg)
-                                        : P.template row<false>(o, gr, gc, ta, xa, &dg);
+                const double acc = edge ? P.template row<true>(o, gr, gc, ta, xa, &dg, cl)
+                                        : P.template row<false>(o, gr, gc, ta, xa, &dg, cl);
                 set_diag(pe[o], dg);
                 set_x(pe[o], xa.X(S::NF == 1 ? 0 : o, gr, gc));
                 epi(P.out_row(o, lr, gc), acc, pe[o]);
@@ -1245,8 +1258,9 @@ int launch_march(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStrea
 
 // F row of field f at a cell (k_march policy).
 template <bool EDGE, class TA, class XA>
-__device__ inline double FStencilDev::row(int f, int gr, int gc, const TA& ta, const XA& xa, double* fd) const {
-    return f_row<EDGE>(*this, f, gr, gc, ta, xa, fd);
+__device__ inline double FStencilDev::row(int f, int gr, int gc, const TA& ta, const XA& xa, double* fd,
+                                          const Cell& cl) const {
+    return f_row<EDGE>(*this, f, gr, gc, ta, xa, fd, cl.face);
 }
 
 // ------------------------------------------------------- matrix-free D, G, Gt_G ----
@@ -1273,11 +1287,13 @@ struct PGDev {
 
 // y = D x: pressure row (gr, gc) = sum over phases of the 4 velocity entries in column order.
 struct DStencilDev : PGDev {
+    struct Cell {};
+    __device__ Cell cell_pre(int, int) const { return {}; }
     static constexpr int NF = 4, NOUT = 1;
     __device__ int32_t xrow(int f, int gr) const { return xrow_of<4>(f, gr); }
     __device__ int32_t out_row(int, int lr, int gc) const { return lr * n + gc; }
     template <bool EDGE, class TA, class XA>
-    __device__ double row(int, int gr, int gc, const TA& ta, const XA& xa, double* dg) const {
+    __device__ double row(int, int gr, int gc, const TA& ta, const XA& xa, double* dg, const Cell&) const {
         const bool lastc = EDGE && gc == n - 1, lastr = EDGE && gr == n - 1;   // wrapped neighbour sorts first
         double acc = 0.0;
 #pragma unroll
@@ -1300,11 +1316,13 @@ struct DStencilDev : PGDev {
 
 // y = G x: velocity row o (u_n, v_n, u_s, v_s) at (gr, gc), two pressure entries in column order.
 struct GStencilDev : PGDev {
+    struct Cell {};
+    __device__ Cell cell_pre(int, int) const { return {}; }
     static constexpr int NF = 1, NOUT = 4;
     __device__ int32_t xrow(int f, int gr) const { return xrow_of<1>(f, gr); }
     __device__ int32_t out_row(int f, int lr, int gc) const { return (f * L + lr) * n + gc; }
     template <bool EDGE, class TA, class XA>
-    __device__ double row(int o, int gr, int gc, const TA& ta, const XA& xa, double* dg) const {
+    __device__ double row(int o, int gr, int gc, const TA& ta, const XA& xa, double* dg, const Cell&) const {
         const int p = o >> 1;
         const double t0 = ta.T(p, gr, gc), xC = xa.X(0, gr, gc);
         double acc = 0.0;
@@ -1329,6 +1347,8 @@ struct GStencilDev : PGDev {
 // Gt_G = -(D G): row (gr, gc) has the five entries N, W, C, E, S (grid neighbours).  Each off-diagonal
 // gets one product per phase; the diagonal gets four per phase, accumulated in D's column order.
 struct GtGStencilDev : PGDev {
+    struct Cell {};
+    __device__ Cell cell_pre(int, int) const { return {}; }
     static constexpr int NF = 1, NOUT = 1;
     __device__ int32_t xrow(int f, int gr) const { return xrow_of<1>(f, gr); }
     __device__ int32_t out_row(int, int lr, int gc) const { return lr * n + gc; }
@@ -1364,7 +1384,7 @@ struct GtGStencilDev : PGDev {
         e[0] = -1.0 * cN; e[1] = -1.0 * cW; e[2] = -1.0 * cC; e[3] = -1.0 * cE; e[4] = -1.0 * cS;
     }
     template <bool EDGE, class TA, class XA>
-    __device__ double row(int, int gr, int gc, const TA& ta, const XA& xa, double* dg) const {
+    __device__ double row(int, int gr, int gc, const TA& ta, const XA& xa, double* dg, const Cell&) const {
         double e[5];
         entries(gr, gc, ta, e);
         *dg = e[2];
