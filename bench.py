@@ -86,6 +86,8 @@ def main():
                          "marchR (LDS ring marching R grid rows per workgroup)")
     ap.add_argument("--sweep-fusion", type=int, default=0,
                     help="grid rows per workgroup of the fused init + two-sweep F kernel; 0 = one kernel per sweep")
+    ap.add_argument("--p-fusion", type=int, default=0,
+                    help="grid rows per workgroup of the one-pass Gt_G inner solve; 0 = one kernel per sweep")
     ap.add_argument("--self-halo", action="store_true",
                     help="N = 1 only: run the row-partitioned apply with the ghost rows refreshed by the periodic "
                          "self-exchange over RCCL (measures the multi-GPU code path's overhead on one GPU)")
@@ -123,6 +125,7 @@ def main():
     sk = args.stencil_kind
     _check(_lib().mpbp_set_stencil_kind(0 if sk == "cells" else 1 if sk == "rows" else 2 + int(sk[5:] or 4)))
     _check(_lib().mpbp_set_sweep_fusion(args.sweep_fusion))
+    _check(_lib().mpbp_set_pressure_solve_fusion(args.p_fusion))
 
     n = args.n if (world == 1 or args.strong) else int(round(args.n * math.sqrt(world)))
     kf, sf = parse_inner(args.inner_f)
@@ -234,7 +237,7 @@ def main():
                        "f_sweeps": ("matrix-free-" + args.stencil_kind) if getattr(pc, "f_stencil", None) is not None
                        else "assembled",
                        "d_g_gtg": "matrix-free" if getattr(pc, "pg_stencil", None) is not None else "assembled",
-                       "sweep_fusion_rows": args.sweep_fusion,
+                       "sweep_fusion_rows": args.sweep_fusion, "pressure_solve_fusion_rows": args.p_fusion,
                        "launch": "hipgraph" if graph is not None else "eager",
                        **({"halo": f"{pc.halo_impl} ({'self-exchange' if world == 1 else 'neighbour'})"}
                           if partitioned else {}),

@@ -286,6 +286,10 @@ int mpbp_set_stencil_kind(int32_t kind);
  * each solve run as one kernel marching `rows` grid rows per workgroup; 0 (default) = one kernel per
  * sweep, which is faster on MI355X.  One GPU, marching F stencil; results bit-identical. */
 int mpbp_set_sweep_fusion(int32_t rows);
+/* One-pass Gt_G inner solves (process-wide): with the matrix-free Gt_G on one GPU and 3 <= sweeps <= 5,
+ * the init and every sweep of the solve run as one kernel (levels kept in LDS), `rows` grid rows per
+ * workgroup; 0 (default) = one kernel per sweep, faster on MI355X.  Bit-identical either way. */
+int mpbp_set_pressure_solve_fusion(int32_t rows);
 
 /* ---- ghost rows over RCCL point-to-point (multi-GPU row partition) ------------------------------ */
 /* One RCCL group of neighbour sends / receives: the owned boundary rows (packed into one buffer per

@@ -25,6 +25,7 @@ int g_march_rows = 4;     // grid rows per workgroup of the marching kernel (4 i
 #endif
 inline int pg_rows() { return MPBP_PG_ROWS > 0 ? MPBP_PG_ROWS : g_march_rows; }
 int g_sweep2_rows = 0;    // grid rows per workgroup of the two-sweep kernel; 0 (default) = no two-sweep fusion
+int g_gtg_solve_rows = 0; // grid rows per workgroup of the one-pass Gt_G solve (k_gtg_solve); 0 (default) = off
 
 int set_error(int code, const char* fmt, ...) {
     va_list ap;
@@ -1352,14 +1353,16 @@ struct GtGStencilDev : PGDev {
     static constexpr int NF = 1, NOUT = 1;
     __device__ int32_t xrow(int f, int gr) const { return xrow_of<1>(f, gr); }
     __device__ int32_t out_row(int, int lr, int gc) const { return lr * n + gc; }
+    // e = {N, W, C, E, S}.  (vr, vc): the cell in the accessor's coordinates (it may lie up to a few cells
+    // outside the grid in the fused solve); (gr, gc): the same cell wrapped onto the grid.
     template <class TA>
-    __device__ void entries(int gr, int gc, const TA& ta, double* e) const {   // e = {N, W, C, E, S}
+    __device__ void entries(int vr, int vc, int gr, int gc, const TA& ta, double* e) const {
         const bool lastc = gc == n - 1, lastr = gr == n - 1;
         double cN = 0.0, cW = 0.0, cC = 0.0, cE = 0.0, cS = 0.0;
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
-            const double t0 = ta.T(p, gr, gc), tE = ta.T(p, gr, gc + 1), tW = ta.T(p, gr, gc - 1);
-            const double tN = ta.T(p, gr - 1, gc), tS = ta.T(p, gr + 1, gc);
+            const double t0 = ta.T(p, vr, vc), tE = ta.T(p, vr, vc + 1), tW = ta.T(p, vr, vc - 1);
+            const double tN = ta.T(p, vr - 1, vc), tS = ta.T(p, vr + 1, vc);
             // D row entries (phase_D_row)
             const double DuE = inv * (0.5 * (t0 + tE)), DuC = minv * (0.5 * (t0 + tW));
             const double DvC = inv * (0.5 * (t0 + tN)), DvS = minv * (0.5 * (t0 + tS));
@@ -1383,23 +1386,194 @@ struct GtGStencilDev : PGDev {
         }
         e[0] = -1.0 * cN; e[1] = -1.0 * cW; e[2] = -1.0 * cC; e[3] = -1.0 * cE; e[4] = -1.0 * cS;
     }
+    // Gt_G x at a cell: the five entries summed in CSR column order (EDGE: sorted by wrapped column)
     template <bool EDGE, class TA, class XA>
-    __device__ double row(int, int gr, int gc, const TA& ta, const XA& xa, double* dg, const Cell&) const {
+    __device__ double apply_v(int vr, int vc, int gr, int gc, const TA& ta, const XA& xa, double* dg) const {
         double e[5];
-        entries(gr, gc, ta, e);
+        entries(vr, vc, gr, gc, ta, e);
         *dg = e[2];
-        Ent s[5] = {Ent{EDGE ? wrap(gr - 1) * n + gc : (gr - 1) * n + gc, e[0], xa.X(0, gr - 1, gc)},
-                    Ent{EDGE ? gr * n + wrap(gc - 1) : gr * n + gc - 1, e[1], xa.X(0, gr, gc - 1)},
-                    Ent{gr * n + gc, e[2], xa.X(0, gr, gc)},
-                    Ent{EDGE ? gr * n + wrap(gc + 1) : gr * n + gc + 1, e[3], xa.X(0, gr, gc + 1)},
-                    Ent{EDGE ? wrap(gr + 1) * n + gc : (gr + 1) * n + gc, e[4], xa.X(0, gr + 1, gc)}};
+        Ent s[5] = {Ent{EDGE ? wrap(gr - 1) * n + gc : (gr - 1) * n + gc, e[0], xa.X(0, vr - 1, vc)},
+                    Ent{EDGE ? gr * n + wrap(gc - 1) : gr * n + gc - 1, e[1], xa.X(0, vr, vc - 1)},
+                    Ent{gr * n + gc, e[2], xa.X(0, vr, vc)},
+                    Ent{EDGE ? gr * n + wrap(gc + 1) : gr * n + gc + 1, e[3], xa.X(0, vr, vc + 1)},
+                    Ent{EDGE ? wrap(gr + 1) * n + gc : (gr + 1) * n + gc, e[4], xa.X(0, vr + 1, vc)}};
         if (EDGE) sort5(s);
         double acc = 0.0;
 #pragma unroll
         for (int t = 0; t < 5; ++t) acc += s[t].v * s[t].x;
         return acc;
     }
+    template <bool EDGE, class TA, class XA>
+    __device__ double row(int, int gr, int gc, const TA& ta, const XA& xa, double* dg, const Cell&) const {
+        return apply_v<EDGE>(gr, gc, gr, gc, ta, xa, dg);
+    }
 };
+
+// ---- a whole Gt_G inner solve in one pass (temporal blocking) ----------------------------------------
+// Sweeps 1 .. S of a Chebyshev / Jacobi solve from x0 = c2_0 (b / diag) (recomputed from b and diag, no
+// init pass): level s (sweep s) is computed one grid row behind level s-1, levels 0 .. S-1 live in 4-row
+// LDS rings and never touch HBM, so the solve reads b, diag and thn and writes x_S -- ~32 B per pressure
+// row instead of ~136 for the init pass and S single sweeps.  A workgroup marches down a 256-column strip;
+// level s covers S-s halo columns each side (lanes 0 .. 2(S-1)-1 compute those cells in a second pass and
+// keep each halo column's direction in registers) and S-s halo rows above and below the chunk.  Every
+// cell is computed with the single-sweep arithmetic (apply_v, EpiChebFirst / EpiCheb / EpiJacobi
+// formulas): results are bit-identical to the unfused solve.  One GPU, S <= n.
+// Measured on MI355X at 1024^2 (4-sweep Chebyshev, S = 3): 68 us per solve at 8 rows per workgroup (the
+// unfused init-fused sweep + 2 sweeps: 17.5 + 2 x 13.5 = 44.5 us); 4 / 2 / 16 rows are slower too -- the
+// three barriers per row step and the doubled level-1 rows leave it latency-bound -- so it is off by
+// default (mpbp_set_pressure_solve_fusion).
+struct GtgSolveArgs {
+    const double* b;
+    const double* diag;
+    double c2_0;            // x0 = c2_0 * (b / diag)   (1.0: Jacobi)
+    double c1[8], c2[8];    // sweep s uses c1[s], c2[s] (Chebyshev)
+    const double* sub;      // x_out = sub - x_S when set
+    double* x_out;
+};
+
+template <int W, int OFF>
+struct PRing4 {             // one field, rows in slot (row + 8) & 3, virtual column c at c - c0 + OFF
+    const double* x;
+    int c0;
+    __device__ double X(int, int r, int c) const { return x[((r + 8) & 3) * W + (c - c0 + OFF)]; }
+};
+template <int W, int OFF, int TS>
+struct PThetaRing {         // thn rows in slot (row + 2 TS) % TS
+    const double* t;
+    int c0;
+    __device__ double T(int sph, int r, int c) const {
+        const double v = t[((r + 2 * TS) % TS) * W + (c - c0 + OFF)];
+        return sph ? 1.0 - v : v;
+    }
+};
+
+template <int S, bool CHEB>
+__global__ void __launch_bounds__(kMB) k_gtg_solve(GtGStencilDev P, GtgSolveArgs a, int rows_per_block) {
+    constexpr int W = kMB + 2 * S;   // virtual columns c0-S .. c0+256+S-1
+    constexpr int TS = S + 3;        // thn ring slots (rows k-S .. k+1 live, one of slack)
+    __shared__ double lv[S * 4 * W];   // levels 0 .. S-1
+    __shared__ double th[TS * W];
+    const int n = P.n;
+    const int strips = (n + kMB - 1) / kMB;
+    const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int strip = bid % strips, chunk = bid / strips;
+    const int la = chunk * rows_per_block, lb = min(la + rows_per_block, n);
+    if (la >= lb) return;
+    const int c0 = strip * kMB, tid = threadIdx.x;
+    auto vw = [&](int v) { return v < 0 ? v + n : (v >= n ? v - n : v); };   // |offset| <= S <= n
+    // staging of level 0 (x0 from b, diag) and thn: tile column tid <-> virtual column c0-S+tid, threads
+    // 0 .. 2S-1 also c0+256-S+tid; virtual columns beyond n-1+S are never read by a needed cell
+    const int colA = c0 - S + tid, colB = c0 + kMB - S + tid;
+    const bool okA = colA <= n - 1 + S, okB = tid < 2 * S && colB <= n - 1 + S;
+    const int gcA = okA ? vw(colA) : 0, gcB = okB ? vw(colB) : 0;
+    double x0A = 0.0, x0B = 0.0, tA = 0.0, tB = 0.0;   // the row in flight
+    auto load_row = [&](int r) {
+        const int32_t base = vw(r) * n;
+        const double bA = a.b[base + gcA], dA = a.diag[base + gcA], thA = P.cell[base + gcA];
+        x0A = okA ? a.c2_0 * (bA / dA) : 0.0;
+        tA = okA ? thA : 0.0;
+        if (okB) {
+            x0B = a.c2_0 * (a.b[base + gcB] / a.diag[base + gcB]);
+            tB = P.cell[base + gcB];
+        }
+    };
+    auto stage_row = [&](int r) {
+        lv[((r + 8) & 3) * W + tid] = x0A;
+        th[((r + 2 * TS) % TS) * W + tid] = tA;
+        if (okB) {
+            lv[((r + 8) & 3) * W + kMB + tid] = x0B;
+            th[((r + 2 * TS) % TS) * W + kMB + tid] = tB;
+        }
+    };
+    // cells of this thread: main column c0+tid at every level; halo columns (lanes 0 .. 2(S-1)-1):
+    // lane j-1 -> c0-j, lane S-2+j -> c0+255+j (j = 1 .. S-1), computed at levels s <= S-j
+    const int cm = c0 + tid;
+    const int hj = tid < S - 1 ? tid + 1 : (tid < 2 * (S - 1) ? tid - (S - 1) + 1 : 0);
+    const int ch = tid < S - 1 ? c0 - hj : c0 + kMB - 1 + hj;
+    double dm_old[S + 1], dh_old[S + 1];   // direction of level s at its previous row (main / halo column)
+#pragma unroll
+    for (int s = 0; s <= S; ++s) { dm_old[s] = 0.0; dh_old[s] = 0.0; }
+    const int k0 = la - (S - 1), k1 = lb - 1 + (S - 1);
+    {   // prologue: rows k0-1, k0 staged, k0+1 in flight
+        load_row(k0 - 1);
+        stage_row(k0 - 1);
+        load_row(k0);
+        stage_row(k0);
+        load_row(k0 + 1);
+    }
+    for (int k = k0; k <= k1; ++k) {
+        // b of every level's cells this step (row k - (s-1)); L2-resident after the first level reads it
+        double bm[S + 1], bh[S + 1];
+#pragma unroll
+        for (int s = 1; s <= S; ++s) {
+            const int r = k - (s - 1);
+            const bool rowok = r >= la - (S - s) && r <= lb - 1 + (S - s);   // then |r wrap offset| <= S <= n
+            bm[s] = rowok ? a.b[vw(r) * n + (cm <= n - 1 + (S - s) ? vw(cm) : 0)] : 0.0;
+            bh[s] = (rowok && hj > 0 && hj <= S - s) ? a.b[vw(r) * n + vw(ch)] : 0.0;
+        }
+        const double subv = a.sub ? a.sub[(k - (S - 1) >= 0 && k - (S - 1) < n ? k - (S - 1) : 0) * n +
+                                          (cm < n ? cm : 0)] : 0.0;
+        stage_row(k + 1);
+        __syncthreads();
+        if (k + 2 <= k1 + 1) load_row(k + 2);   // in flight
+        double dm_new[S + 1], dh_new[S + 1];
+#pragma unroll
+        for (int s = 1; s <= S; ++s) {
+            const int r = k - (s - 1);                   // this level's row
+            const bool rowok = r >= la - (S - s) && r <= lb - 1 + (S - s);
+            const PRing4<W, S> xa{lv + (s - 1) * 4 * W, c0};
+            const PThetaRing<W, S, TS> ta{th, c0};
+            // main column
+            const bool needm = rowok && cm <= n - 1 + (S - s);
+            const int gr = vw(r);
+            double xn = 0.0, dn = 0.0;
+            if (needm) {
+                const int gc = vw(cm);
+                const bool edge = __builtin_amdgcn_readfirstlane(
+                    __any(gr == 0 || gr == n - 1 || gc == 0 || gc == n - 1)) != 0;
+                double dg;
+                const double acc = edge ? P.template apply_v<true>(r, cm, gr, gc, ta, xa, &dg)
+                                        : P.template apply_v<false>(r, cm, gr, gc, ta, xa, &dg);
+                const double xc = xa.X(0, r, cm);
+                if constexpr (CHEB) {
+                    const double z = (bm[s] - acc) / dg;
+                    dn = a.c1[s] * (s == 1 ? xc : dm_old[s - 1]) + a.c2[s] * z;
+                    xn = xc + dn;
+                } else {
+                    xn = xc + (bm[s] - acc) / dg;
+                }
+            }
+            // halo column (second pass of the first lanes)
+            double xhn = 0.0, dhn = 0.0;
+            const bool needh = rowok && hj > 0 && hj <= S - s && !(tid >= S - 1 && ch > n - 1 + (S - s));
+            if (needh) {
+                const int gc = vw(ch);
+                double dg;
+                const double acc = P.template apply_v<true>(r, ch, gr, gc, ta, xa, &dg);
+                const double xc = xa.X(0, r, ch);
+                if constexpr (CHEB) {
+                    const double z = (bh[s] - acc) / dg;
+                    dhn = a.c1[s] * (s == 1 ? xc : dh_old[s - 1]) + a.c2[s] * z;
+                    xhn = xc + dhn;
+                } else {
+                    xhn = xc + (bh[s] - acc) / dg;
+                }
+            }
+            dm_new[s] = dn;
+            dh_new[s] = dhn;
+            if (s < S) {
+                if (needm) lv[(s * 4 + ((r + 8) & 3)) * W + (cm - c0 + S)] = xn;
+                if (needh) lv[(s * 4 + ((r + 8) & 3)) * W + (ch - c0 + S)] = xhn;
+                __syncthreads();
+            } else if (needm && r >= la && r < lb && cm < n) {
+                st_stream(a.x_out + r * n + cm, a.sub ? subv - xn : xn);
+            }
+        }
+#pragma unroll
+        for (int s = 1; s <= S; ++s) { dm_old[s] = dm_new[s]; dh_old[s] = dh_new[s]; }
+    }
+}
+
 
 // ---- two sweeps in one pass (temporal blocking): the first two sweeps of an F inner solve ----------
 // Level 0 is the solve's x0 = d0 = c2_0 (b / diag) recomputed from b and diag (no init pass); level 1
@@ -1658,6 +1832,11 @@ int mpbp_set_stencil_kind(int32_t kind) {
     g_stencil_kind = kind > 2 ? 2 : kind;
     if (kind > 2) g_march_rows = kind - 2;
     else if (kind == 2) g_march_rows = 4;
+    return MPBP_OK;
+}
+int mpbp_set_pressure_solve_fusion(int32_t rows) {
+    if (rows < 0 || rows > 4096) return set_error(MPBP_ERR_ARG, "pressure solve fusion rows must be in [0, 4096]");
+    g_gtg_solve_rows = rows;
     return MPBP_OK;
 }
 int mpbp_set_sweep_fusion(int32_t rows) {
@@ -2344,6 +2523,40 @@ int op_first_two_sweeps(const OpRef& o, bool cheb, const double* b, const double
     return MPBP_OK;
 }
 
+// A whole Gt_G inner solve (sweeps 1 .. K-1 from the fused init) in one k_gtg_solve pass, when the
+// operator is the single-GPU Gt_G stencil and 2 <= K-1 <= 4 <= n.  Returns 1 if it launched.
+int try_gtg_solve(const OpPair& op, bool cheb, int K, const double* b, const double* diag, const double* c1,
+                  const double* c2, const double* sub, double* xo, hipStream_t st, int* rc) {
+    const OpRef& o = op.in;
+    const int S = K - 1;
+    if (g_gtg_solve_rows <= 0 || !can_fuse_init(op) || o.sop != SOP_GTG || S < 2 || S > 4) return 0;
+    const mpbp_schur_plan* p = o.stencil;
+    PGDev P;
+    *rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &P);
+    if (*rc) return 1;
+    if (S > P.n) return 0;
+    GtgSolveArgs a{b, diag, cheb ? c2[0] : 1.0, {}, {}, sub, xo};
+    for (int s = 0; cheb && s <= S; ++s) {
+        a.c1[s] = c1[s];
+        a.c2[s] = c2[s];
+    }
+    const int R = g_gtg_solve_rows;
+    const unsigned blocks = (unsigned)(((P.n + kMB - 1) / kMB) * ((P.n + R - 1) / R));
+    const GtGStencilDev G{P};
+#define MPBP_GTG_SOLVE(SS)                                                                              \
+    (cheb ? (k_gtg_solve<SS, true><<<blocks, kMB, 0, st>>>(G, a, R), 0)                                 \
+          : (k_gtg_solve<SS, false><<<blocks, kMB, 0, st>>>(G, a, R), 0))
+    switch (S) {
+    case 2: MPBP_GTG_SOLVE(2); break;
+    case 3: MPBP_GTG_SOLVE(3); break;
+    default: MPBP_GTG_SOLVE(4); break;
+    }
+#undef MPBP_GTG_SOLVE
+    const hipError_t e = hipGetLastError();
+    *rc = e == hipSuccess ? MPBP_OK : set_error(MPBP_ERR_HIP, "k_gtg_solve: %s", hipGetErrorString(e));
+    return 1;
+}
+
 OpPair make_op(const mpbp_schur_plan* p, const mpbp_csr& A, const mpbp_rowblocks& bi, const mpbp_rowblocks& bb,
                const mpbp_sell& si, const mpbp_sell& sb) {
     if (p->use_sell)
@@ -2392,7 +2605,8 @@ int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag
         return set_error(MPBP_ERR_ARG, "unknown inner solver %d", in.kind);
     }
     double* cur = (K == 1) ? dst : ping;
-    int s = 1, rc;
+    int s = 1, rc = MPBP_OK;
+    if (try_gtg_solve(op, cheb, K, b, diag, c1, c2, sub, dst, c.st, &rc)) return rc;   // the whole solve
     if (K >= 3 && can_fuse_init(op) && op.in.sop == SOP_F && g_sweep2_rows > 0) {   // init + sweeps 1, 2: one pass
         double* nxt = K == 3 ? dst : pong;
         rc = op_first_two_sweeps(op.in, cheb, b, diag, c1, c2, dir, K == 3 ? sub : nullptr, nxt, c.st, K == 3 ? 0 : 1);
