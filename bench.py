@@ -266,9 +266,13 @@ def spmv_bench(A, gen, reps=20):
     y = torch.empty(A.shape[0], dtype=torch.float64, device="cuda")
     res = {"nnz": A.nnz}
     AS = A.to_sell()
-    for name, M, nbytes in (
-            ("csr", A, A.nnz * 12 + (A.shape[0] + 1) * 4 + (A.shape[0] + A.shape[1]) * 8 + A.blocks.count * 8),
-            ("sell", AS, A.nnz * 12 + A.shape[0] + (A.shape[0] + A.shape[1]) * 8 + AS.nslices * 16)):
+    from mp_block_preconditioners_amd._lib import lib
+    csr_bytes = A.nnz * 12 + (A.shape[0] + 1) * 4 + (A.shape[0] + A.shape[1]) * 8 + A.blocks.count * 8
+    for name, M, nbytes, kind in (
+            ("csr", A, csr_bytes, 1),           # per-wave chunked kernel (default)
+            ("csr_block", A, csr_bytes, 0),     # one LDS stage per 256-row block
+            ("sell", AS, A.nnz * 12 + A.shape[0] + (A.shape[0] + A.shape[1]) * 8 + AS.nslices * 16, 1)):
+        lib().mpbp_set_csr_kernel(kind)
         for _ in range(3):
             M.matvec(x, out=y)
         ev[0].record()
@@ -278,6 +282,7 @@ def spmv_bench(A, gen, reps=20):
         torch.cuda.synchronize()
         s = ev[0].elapsed_time(ev[1]) / 1e3 / reps
         res.update({f"{name}_gbs": nbytes / s / 1e9, f"{name}_us": s * 1e6, f"{name}_bytes": nbytes})
+    lib().mpbp_set_csr_kernel(1)
     return res
 
 

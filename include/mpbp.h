@@ -290,6 +290,9 @@ int mpbp_set_sweep_fusion(int32_t rows);
  * the init and every sweep of the solve run as one kernel (levels kept in LDS), `rows` grid rows per
  * workgroup; 0 (default) = one kernel per sweep, faster on MI355X.  Bit-identical either way. */
 int mpbp_set_pressure_solve_fusion(int32_t rows);
+/* CSR SpMV kernel over row blocks (process-wide): 1 = one wavefront per 64 rows, chunked LDS stage, no
+ * workgroup barrier (default); 0 = one LDS stage per 256-row block.  Bit-identical either way. */
+int mpbp_set_csr_kernel(int32_t kind);
 
 /* ---- ghost rows over RCCL point-to-point (multi-GPU row partition) ------------------------------ */
 /* One RCCL group of neighbour sends / receives: the owned boundary rows (packed into one buffer per

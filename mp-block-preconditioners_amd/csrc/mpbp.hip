@@ -26,6 +26,7 @@ int g_march_rows = 4;     // grid rows per workgroup of the marching kernel (4 i
 inline int pg_rows() { return MPBP_PG_ROWS > 0 ? MPBP_PG_ROWS : g_march_rows; }
 int g_sweep2_rows = 0;    // grid rows per workgroup of the two-sweep kernel; 0 (default) = no two-sweep fusion
 int g_gtg_solve_rows = 0; // grid rows per workgroup of the one-pass Gt_G solve (k_gtg_solve); 0 (default) = off
+int g_csr_kind = 1;       // CSR SpMV kernel: 0 workgroup-staged row blocks (k_csr_rows), 1 per-wave chunks (k_csr_wave)
 
 int set_error(int code, const char* fmt, ...) {
     va_list ap;
@@ -724,6 +725,90 @@ __global__ void __launch_bounds__(kBlock) k_csr_rows(Csr A, const double* __rest
         }
         if (tid == 0) epi(r0, prod[0], epi.pre(r0));
     }
+}
+
+// CSR SpMV over the same row blocks, one wavefront per 64-row quarter of a block and no block-wide
+// barrier: each wave streams its rows' [row_ptr[ra], row_ptr[rb]) entries in chunks of kWaveCap with
+// 16-byte loads (1 KiB of values per wave-instruction), stages the chunk's products in its own 6 KiB
+// of LDS as double2 pairs, and each lane then adds the part of its row that lies in the chunk, left to
+// right, chunk after chunk -- the oracle's sequential order, so bit-exact.  A 1024^2 A row block
+// (12 entries per velocity row) is one chunk per wave.  Waves never wait for each other, 24 KiB of LDS
+// per workgroup keeps 6 workgroups on a CU, and the b128 LDS reads are 2-way conflicted at most for
+// 12-entry rows.
+constexpr int kWaveCap = 768;                  // products per wave chunk (64 rows x 12 entries)
+constexpr int kWavePairs = kWaveCap / 128;     // 16-byte loads per lane per chunk
+
+// Lanes of one wave exchange data through LDS: order the LDS writes before the reads (compiler
+// and wave scope; a wave's LDS operations complete in order).
+__device__ inline void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <class Epi>
+__global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __restrict__ x,
+                                                     const int2* __restrict__ blocks, int nblocks,
+                                                     Epi epi) {
+    __shared__ double2 stage[kBlock / 64][kWaveCap / 2];
+    const int b = xcd_swizzle(blockIdx.x, nblocks);
+    const int2 blk = blocks[b];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int32_t ra = blk.x + 64 * w;
+    if (ra >= blk.y) return;   // waves are independent: no workgroup barrier below
+    const int32_t rb = min(ra + 64, blk.y);
+    const int32_t r = ra + lane;
+    const bool live = r < rb;
+    const int32_t s = A.rp[ra], e = A.rp[rb];
+    int32_t ks = 0, ke = 0;
+    typename Epi::P pe{};
+    if (live) {
+        ks = A.rp[r];
+        ke = A.rp[r + 1];
+        pe = epi.pre(r);
+    }
+    double2* st = stage[w];
+    const double* sp = reinterpret_cast<const double*>(st);
+    double acc = 0.0;
+    for (int32_t cb = s & ~1; cb < e; cb += kWaveCap) {
+        double2 v[kWavePairs];
+        int2 cc[kWavePairs];
+#pragma unroll
+        for (int j = 0; j < kWavePairs; ++j) {
+            const int32_t k = cb + 2 * (lane + 64 * j);
+            if (k + 1 < e) {
+                v[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const double2*>(A.va + k));
+                cc[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const int2*>(A.ci + k));
+            } else if (k < e) {
+                v[j] = make_double2(A.va[k], 0.0);
+                cc[j] = make_int2(A.ci[k], 0);
+            } else {
+                v[j] = make_double2(0.0, 0.0);
+                cc[j] = make_int2(0, 0);
+            }
+        }
+        double x0[kWavePairs], x1[kWavePairs];
+#pragma unroll
+        for (int j = 0; j < kWavePairs; ++j) {
+            const int32_t k = cb + 2 * (lane + 64 * j);
+            x0[j] = (k >= s && k < e) ? x[cc[j].x] : 0.0;
+            x1[j] = (k + 1 >= s && k + 1 < e) ? x[cc[j].y] : 0.0;
+        }
+        if (cb != (s & ~1)) wave_lds_sync();   // the previous chunk's reads are done
+#pragma unroll
+        for (int j = 0; j < kWavePairs; ++j) st[lane + 64 * j] = make_double2(v[j].x * x0[j], v[j].y * x1[j]);
+        wave_lds_sync();
+        int32_t k = max(ks, cb) - cb;
+        const int32_t kend = min(ke, cb + kWaveCap) - cb;
+        if ((k & 1) && k < kend) acc += sp[k++];
+        for (; k + 1 < kend; k += 2) {
+            const double2 q = st[k >> 1];
+            acc += q.x;
+            acc += q.y;
+        }
+        if (k < kend) acc += sp[k];
+    }
+    if (live) epi.template apply<MPBP_CSR_NT != 0>(r, acc, pe);
 }
 
 // ------------------------------------------------------------------ SELL-64 ----
@@ -1777,9 +1862,12 @@ inline Csr to_csr(const mpbp_csr* A) { return Csr{A->row_ptr, A->col_idx, A->val
 template <class Epi>
 int launch_rows(const mpbp_csr* A, const mpbp_rowblocks* blk, const double* x, Epi epi, hipStream_t st) {
     if (!blk || blk->count <= 0) return MPBP_OK;
-    k_csr_rows<Epi><<<blk->count, kBlock, 0, st>>>(to_csr(A), x,
-                                                    reinterpret_cast<const int2*>(blk->pairs),
-                                                    blk->count, epi);
+    if (g_csr_kind == 1)
+        k_csr_wave<Epi><<<blk->count, kBlock, 0, st>>>(to_csr(A), x, reinterpret_cast<const int2*>(blk->pairs),
+                                                        blk->count, epi);
+    else
+        k_csr_rows<Epi><<<blk->count, kBlock, 0, st>>>(to_csr(A), x, reinterpret_cast<const int2*>(blk->pairs),
+                                                        blk->count, epi);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
@@ -1837,6 +1925,11 @@ int mpbp_set_stencil_kind(int32_t kind) {
 int mpbp_set_pressure_solve_fusion(int32_t rows) {
     if (rows < 0 || rows > 4096) return set_error(MPBP_ERR_ARG, "pressure solve fusion rows must be in [0, 4096]");
     g_gtg_solve_rows = rows;
+    return MPBP_OK;
+}
+int mpbp_set_csr_kernel(int32_t kind) {
+    if (kind < 0 || kind > 1) return set_error(MPBP_ERR_ARG, "csr kernel must be 0 (workgroup-staged) or 1 (per-wave)");
+    g_csr_kind = kind;
     return MPBP_OK;
 }
 int mpbp_set_sweep_fusion(int32_t rows) {

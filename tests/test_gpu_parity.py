@@ -116,8 +116,17 @@ def test_spgemm_bit_exact(n):
     _same_csr(mp.spgemm(F, G, alpha=2.5), co.spgemm(osys.F, osys.G, alpha=2.5))
 
 
+@pytest.fixture(params=[1, 0], ids=["csr_wave", "csr_block"])
+def csr_kernel(request):
+    """Both CSR SpMV kernels (mpbp_set_csr_kernel): per-wave chunks (default) and 256-row LDS stages."""
+    from mp_block_preconditioners_amd._lib import check, lib
+    check(lib().mpbp_set_csr_kernel(request.param))
+    yield request.param
+    check(lib().mpbp_set_csr_kernel(1))
+
+
 @pytest.mark.parametrize("n", [2, 16, 100])
-def test_spmv_bit_exact(n):
+def test_spmv_bit_exact(n, csr_kernel):
     mp = _mp()
     from oracle import csr_oracle as co
     osys = _oracle_system(n, products=False, **PARAMS)
@@ -157,9 +166,11 @@ def test_sell_ragged_rows_and_partial_slices():
     assert _bits_equal(got[sel], ref[sel]) and np.all(got[np.r_[0:3, 100:500]] == 7.0)
 
 
-def test_spmv_long_rows_and_empty_rows():
-    """Rows longer than the LDS stage (single-row blocks, tree reduction) and empty rows."""
+def test_spmv_long_rows_and_empty_rows(csr_kernel):
+    """Rows longer than a row block's LDS stage (single-row blocks) and empty rows.  The per-wave kernel
+    sums a long row chunk after chunk in order (bit-exact); the 256-row-stage kernel tree-reduces it."""
     mp = _mp()
+    from oracle import csr_oracle as co
     rng = np.random.default_rng(7)
     lengths = rng.integers(0, 30, size=2000)
     lengths[[5, 777, 1999]] = [9000, 4096, 20000]
@@ -173,10 +184,32 @@ def test_spmv_long_rows_and_empty_rows():
     ref = M @ x
     assert rel_inf(y, ref) <= 1e-13
     assert y[0] == 0.0 and y[10] == 0.0
+    if csr_kernel == 1:
+        assert _bits_equal(y, co.spmv(M, x))
+
+
+@pytest.mark.parametrize("maxlen", [13, 40, 200])
+def test_csr_wave_chunks_ragged_bit_exact(maxlen, csr_kernel):
+    """Ragged rows whose 64-row wave ranges exceed one 768-entry chunk (rows straddle chunk edges,
+    odd starts), partial last wave, empty rows, all three epilogue modes; bit-exact vs the oracle."""
+    mp = _mp()
+    from oracle import csr_oracle as co
+    rng = np.random.default_rng(maxlen)
+    lengths = rng.integers(0, maxlen + 1, size=3001)
+    lengths[:70] = 0
+    lengths[100:164] = maxlen
+    rows = np.repeat(np.arange(lengths.size), lengths)
+    M = sp.csr_matrix((rng.standard_normal(rows.size), (rows, rng.integers(0, 4000, size=rows.size))),
+                      shape=(lengths.size, 4000))
+    M.sum_duplicates()
+    x, z = rng.standard_normal(4000), rng.standard_normal(lengths.size)
+    dM = mp.DeviceCSR.from_scipy(M)
+    for mode in (0, 1, 2):
+        assert _bits_equal(dM.matvec(_cuda(x), mode=mode, z=_cuda(z)), co.spmv(M, x, z, mode=mode)), mode
 
 
 @pytest.mark.parametrize("n", [4, 32])
-def test_inner_steps_bit_exact(n):
+def test_inner_steps_bit_exact(n, csr_kernel):
     mp = _mp()
     from mp_block_preconditioners_amd import _lib
     from mp_block_preconditioners_amd._lib import check, lib, ptr, stream_handle
