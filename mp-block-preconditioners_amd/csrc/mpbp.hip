@@ -728,15 +728,26 @@ __global__ void __launch_bounds__(kBlock) k_csr_rows(Csr A, const double* __rest
 }
 
 // CSR SpMV over the same row blocks, one wavefront per 64-row quarter of a block and no block-wide
-// barrier: each wave streams its rows' [row_ptr[ra], row_ptr[rb]) entries in chunks of kWaveCap with
-// 16-byte loads (1 KiB of values per wave-instruction), stages the chunk's products in its own 6 KiB
-// of LDS as double2 pairs, and each lane then adds the part of its row that lies in the chunk, left to
-// right, chunk after chunk -- the oracle's sequential order, so bit-exact.  A 1024^2 A row block
-// (12 entries per velocity row) is one chunk per wave.  Waves never wait for each other, 24 KiB of LDS
-// per workgroup keeps 6 workgroups on a CU, and the b128 LDS reads are 2-way conflicted at most for
-// 12-entry rows.
-constexpr int kWaveCap = 768;                  // products per wave chunk (64 rows x 12 entries)
+// barrier.  Each wave streams its rows' [row_ptr[ra], row_ptr[rb]) entries in chunks of kWaveCap with
+// 16-byte loads (1 KiB of values per wave-instruction) and transposes the chunk through its own LDS
+// (values and columns as pairs, 9 KiB); each lane then walks the part of its own row that lies in the
+// chunk, gathers x for it and adds the products left to right, chunk after chunk -- the oracle's
+// sequential order, so bit-exact.  Gathering per row (lane = row, as in SELL) makes one
+// wave-instruction's x addresses the same stencil neighbour of 64 consecutive rows instead of all
+// neighbours of ~10 rows: fewer cache lines per instruction (153 vs 172 us for the 1024^2 A).  A 1024^2
+// A row block (12 entries per velocity row) is one chunk per wave.
+// MPBP_CSR_TGATHER=0 selects the earlier order: gather in entry order, stage the products (6 KiB).
+// Measured dead end: no staging at all, each lane loading its own row (16-byte loads 96 B apart across
+// the wave) -- 567 us, the texture addresser then touches ~48 cache lines per wave-instruction.
+#ifndef MPBP_CSR_WAVECAP
+#define MPBP_CSR_WAVECAP 768
+#endif
+#ifndef MPBP_CSR_TGATHER
+#define MPBP_CSR_TGATHER 1
+#endif
+constexpr int kWaveCap = MPBP_CSR_WAVECAP;     // entries per wave chunk (64 rows x 12 entries)
 constexpr int kWavePairs = kWaveCap / 128;     // 16-byte loads per lane per chunk
+constexpr int kRowBatch = 8;                   // pairs of a row gathered at once (16 entries)
 
 // Lanes of one wave exchange data through LDS: order the LDS writes before the reads (compiler
 // and wave scope; a wave's LDS operations complete in order).
@@ -750,7 +761,10 @@ template <class Epi>
 __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __restrict__ x,
                                                      const int2* __restrict__ blocks, int nblocks,
                                                      Epi epi) {
-    __shared__ double2 stage[kBlock / 64][kWaveCap / 2];
+    __shared__ double2 vstage[kBlock / 64][kWaveCap / 2];
+#if MPBP_CSR_TGATHER
+    __shared__ int2 cstage[kBlock / 64][kWaveCap / 2];
+#endif
     const int b = xcd_swizzle(blockIdx.x, nblocks);
     const int2 blk = blocks[b];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -767,9 +781,9 @@ __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __rest
         ke = A.rp[r + 1];
         pe = epi.pre(r);
     }
-    double2* st = stage[w];
-    const double* sp = reinterpret_cast<const double*>(st);
     double acc = 0.0;
+    double2* vs = vstage[w];
+    const double* vs1 = reinterpret_cast<const double*>(vs);
     for (int32_t cb = s & ~1; cb < e; cb += kWaveCap) {
         double2 v[kWavePairs];
         int2 cc[kWavePairs];
@@ -787,6 +801,43 @@ __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __rest
                 cc[j] = make_int2(0, 0);
             }
         }
+        int32_t t = max(ks, cb) - cb;                       // this lane's row within the chunk
+        const int32_t tend = min(ke, cb + kWaveCap) - cb;
+#if MPBP_CSR_TGATHER
+        if (cb != (s & ~1)) wave_lds_sync();   // the previous chunk's reads are done
+        int2* cs = cstage[w];
+        const int32_t* cs1 = reinterpret_cast<const int32_t*>(cs);
+#pragma unroll
+        for (int j = 0; j < kWavePairs; ++j) {
+            vs[lane + 64 * j] = v[j];
+            cs[lane + 64 * j] = cc[j];
+        }
+        wave_lds_sync();
+        if ((t & 1) && t < tend) {   // odd start: one entry, then whole pairs
+            acc += vs1[t] * x[cs1[t]];
+            ++t;
+        }
+        for (; t < tend; t += 2 * kRowBatch) {
+            const int32_t p0 = t >> 1;
+            int2 c[kRowBatch];
+            double x0[kRowBatch], x1[kRowBatch];
+#pragma unroll
+            for (int i = 0; i < kRowBatch; ++i) c[i] = (t + 2 * i < tend) ? cs[p0 + i] : make_int2(0, 0);
+#pragma unroll
+            for (int i = 0; i < kRowBatch; ++i) {
+                x0[i] = (t + 2 * i < tend) ? x[c[i].x] : 0.0;
+                x1[i] = (t + 2 * i + 1 < tend) ? x[c[i].y] : 0.0;
+            }
+#pragma unroll
+            for (int i = 0; i < kRowBatch; ++i) {
+                if (t + 2 * i < tend) {
+                    const double2 q = vs[p0 + i];
+                    acc += q.x * x0[i];
+                    if (t + 2 * i + 1 < tend) acc += q.y * x1[i];
+                }
+            }
+        }
+#else
         double x0[kWavePairs], x1[kWavePairs];
 #pragma unroll
         for (int j = 0; j < kWavePairs; ++j) {
@@ -796,17 +847,16 @@ __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __rest
         }
         if (cb != (s & ~1)) wave_lds_sync();   // the previous chunk's reads are done
 #pragma unroll
-        for (int j = 0; j < kWavePairs; ++j) st[lane + 64 * j] = make_double2(v[j].x * x0[j], v[j].y * x1[j]);
+        for (int j = 0; j < kWavePairs; ++j) vs[lane + 64 * j] = make_double2(v[j].x * x0[j], v[j].y * x1[j]);
         wave_lds_sync();
-        int32_t k = max(ks, cb) - cb;
-        const int32_t kend = min(ke, cb + kWaveCap) - cb;
-        if ((k & 1) && k < kend) acc += sp[k++];
-        for (; k + 1 < kend; k += 2) {
-            const double2 q = st[k >> 1];
+        if ((t & 1) && t < tend) acc += vs1[t++];
+        for (; t + 1 < tend; t += 2) {
+            const double2 q = vs[t >> 1];
             acc += q.x;
             acc += q.y;
         }
-        if (k < kend) acc += sp[k];
+        if (t < tend) acc += vs1[t];
+#endif
     }
     if (live) epi.template apply<MPBP_CSR_NT != 0>(r, acc, pe);
 }
