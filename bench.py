@@ -198,6 +198,7 @@ def main():
     # HBM bytes per F sweep from the committed rocprofv3 PMC passes (tools/pmc_sweep.py +
     # tools/pmc_reduce.py: FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction + WRITE_SIZE)
     traffic = None
+    spmv_traffic = None
     pmc_files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic_r*.json")))
     if pmc_files and not partitioned:
         try:
@@ -206,6 +207,8 @@ def main():
             key = "stencil" if getattr(pc, "f_stencil", None) is not None else args.layout
             if int(pm.get("n", -1)) == n and key in pm:
                 traffic = pm[key]["traffic_bytes_corrected"]
+            if spmv is not None and int(pm.get("n", -1)) == n and "csr_spmv_A" in pm:
+                spmv_traffic = pm["csr_spmv_A"]["traffic_bytes_corrected"]
         except (OSError, ValueError, KeyError):
             traffic = None
 
@@ -250,6 +253,13 @@ def main():
                                    + (", eager pass of the same K applies after the graph-timed loop"
                                       if graph is not None else ", inside the timed loop")},
             "spmv_A": spmv,
+            # north_star's CSR SpMV target: the plain A u product (apply.py:72) on the scipy CSR arrays
+            "roofline_csr_spmv": None if spmv is None else {
+                "bound": "hbm", "achieved": spmv["csr_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": spmv["csr_gbs"] / HBM_PEAK_GBS, "traffic": spmv_traffic,
+                "kernel": "k_csr_wave<EpiStore> (A u, 5N rows, CSR)", "bytes_per_launch": spmv["csr_bytes"],
+                "avg_launch_us": spmv["csr_us"],
+                "timing": "HIP events around 20 back-to-back launches (one kernel per matvec)"},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -24,6 +24,10 @@ for L in stencil sell; do
     cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $C --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/pmc_${L}_$C" -o pmc -- python "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-spmv --no-graph --f-mode $FM > "$GRAFT_REPO_ROOT/$OUT/pmc_${L}_$C.log" 2>&1 || exit 7
   done
 done
+# HBM bytes of the plain A SpMV kernels (tools/spmv_ab.py: CSR per-wave, CSR block, SELL)
+for C in FETCH_SIZE WRITE_SIZE; do
+  cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/pmc_spmv_$C" -o pmc -- python "$GRAFT_REPO_ROOT/tools/spmv_ab.py" --reps 10 > "$GRAFT_REPO_ROOT/$OUT/pmc_spmv_$C.log" 2>&1 || exit 11
+done
 cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --pg-mode assembled --no-cpu-baseline --no-spmv > "$OUT/bench_pg_assembled.log" 2>&1 || exit 8
 cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/sq_stencil" -o pmc -- python "$GRAFT_REPO_ROOT/tools/pmc_sweep.py" --layout stencil > "$GRAFT_REPO_ROOT/$OUT/sq_stencil.log" 2>&1 || exit 9

@@ -47,6 +47,20 @@ def main():
             write = res["WRITE_SIZE"][0] * 1024
             out[lay] = {"fetch_bytes_raw": fetch, "write_bytes": write, "dispatches": res["FETCH_SIZE"][1],
                         "traffic_bytes_corrected": 2 * fetch + write, "traffic_bytes_raw": fetch + write}
+    # the plain A SpMV (apply.py:72) of tools/spmv_ab.py, both layouts' product kernels
+    spmv_k = {"csr_spmv_A": "k_csr_wave<(anonymous namespace)::EpiStore>",
+              "sell_spmv_A": "k_sell_rows<(anonymous namespace)::EpiStore>"}
+    for key, kname in spmv_k.items():
+        res = {}
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            f = os.path.join(args.run_dir, f"pmc_spmv_{c}", "pmc_counter_collection.csv")
+            if os.path.exists(f):
+                res[c] = mean_counter(f, c, kname, None)
+        if res.get("FETCH_SIZE", (None,))[0] is not None and res.get("WRITE_SIZE", (None,))[0] is not None:
+            fetch = res["FETCH_SIZE"][0] * 1024
+            write = res["WRITE_SIZE"][0] * 1024
+            out[key] = {"fetch_bytes_raw": fetch, "write_bytes": write, "dispatches": res["FETCH_SIZE"][1],
+                        "traffic_bytes_corrected": 2 * fetch + write, "traffic_bytes_raw": fetch + write}
     # calibration on a known byte count in the same runs: k_cheb_init over F's 4N rows reads b, diag and
     # writes d, x with 8-B lanes -- exactly 2 x 8 x 4N bytes each way (f_mode=assembled pass only)
     cal = {}
