@@ -144,6 +144,7 @@ class MultiphaseBlockPreconditioner:
         F = self.assemble(_lib.OP_F, **kw)
         D = self.assemble(_lib.OP_D, **kw)
         G = self.assemble(_lib.OP_G, **kw)
+        A.row_groups, F.row_groups, G.row_groups = 5, 4, 4   # [u_n|v_n|u_s|v_s|p] rows over the same cells
         if self.n >= 3:   # the matrix-free forms (periodic neighbours are distinct from n = 3 on)
             prm, tabs = self._params(**kw), self.theta_tables()
             F.stencil = FStencil(prm, tabs)

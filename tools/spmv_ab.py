@@ -32,14 +32,17 @@ def main():
     ref = AS.matvec(x).clone()
     nbytes = A.nnz * 12 + (A.shape[0] + 1) * 4 + (A.shape[0] + A.shape[1]) * 8 + A.blocks.count * 8
     res = {"n": args.n, "nnz": A.nnz, "lib": os.environ.get("MPBP_LIB", "default")}
-    for name, M, kind in (("csr_wave", A, 1), ("csr_block", A, 0), ("sell", AS, 1)):
+    flat = A.plan_blocks(groups=1)   # blocks in plain row order (no per-field interleave)
+    for name, M, kind, blk in (("csr_wave", A, 1, None), ("csr_wave_roworder", A, 1, flat), ("csr_block", A, 0, None),
+                               ("sell", AS, 1, None)):
         check(lib().mpbp_set_csr_kernel(kind))
+        kw = {"blocks": blk} if blk is not None else {}
         for _ in range(5):
-            M.matvec(x, out=y)
+            M.matvec(x, out=y, **kw)
         torch.cuda.synchronize()
         ev[0].record()
         for _ in range(args.reps):
-            M.matvec(x, out=y)
+            M.matvec(x, out=y, **kw)
         ev[1].record()
         torch.cuda.synchronize()
         us = ev[0].elapsed_time(ev[1]) * 1e3 / args.reps
