@@ -364,42 +364,85 @@ __global__ void k_stokes_fill(StokesDev P, int op, int64_t nrows, const int32_t*
 }
 
 // One 1024-thread workgroup scans the whole array in 1024-element chunks (setup only).
-__global__ void __launch_bounds__(1024) k_exclusive_scan(const int32_t* in, int32_t* out, int64_t n,
-                                                         long long* total) {
-    __shared__ long long wsum[16];
-    __shared__ long long carry;
+// Exclusive scan of row counts into row_ptr (int64 running sums, so an int32 overflow is detected).
+// Three passes over tiles of kScanTile counts: tile sums; one workgroup scans the tile sums (and writes
+// row_ptr[n] = total); every tile then scans its counts from LDS and adds its offset.
+constexpr int kScanTile = 4096;   // 256 threads x 16 counts
+
+// Inclusive scan of one value per thread over a 256-thread workgroup; *sum = the workgroup's total.
+__device__ inline long long block_scan256(long long x, long long* wsum, long long* sum) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (threadIdx.x == 0) carry = 0;
+    for (int d = 1; d < 64; d <<= 1) {
+        const long long y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
     __syncthreads();
-    for (int64_t base = 0; base < n; base += 1024) {
+    long long off = 0;
+    for (int w = 0; w < wid; ++w) off += wsum[w];
+    *sum = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+    return x + off;
+}
+
+// Tile t's counts into LDS (coalesced; zeros past n).
+__device__ inline void scan_load_tile(const int32_t* in, int64_t n, int32_t* tile) {
+    const int64_t base = (int64_t)blockIdx.x * kScanTile;
+    for (int i = threadIdx.x; i < kScanTile; i += 256) tile[i] = base + i < n ? in[base + i] : 0;
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_scan_tiles(const int32_t* in, int64_t n, long long* tile_sum) {
+    __shared__ int32_t tile[kScanTile];
+    __shared__ long long wsum[4];
+    scan_load_tile(in, n, tile);
+    long long s = 0;
+    for (int i = 0; i < 16; ++i) s += tile[threadIdx.x * 16 + i];
+    long long tot;
+    block_scan256(s, wsum, &tot);
+    if (threadIdx.x == 0) tile_sum[blockIdx.x] = tot;
+}
+
+// In place: tile_sum[t] -> exclusive prefix of the tile sums; out[n] = total = *total.
+__global__ void __launch_bounds__(256) k_scan_offsets(long long* tile_sum, int64_t ntiles, int32_t* out, int64_t n,
+                                                      long long* total) {
+    __shared__ long long wsum[4];
+    long long carry = 0;
+    for (int64_t base = 0; base < ntiles; base += 256) {
         const int64_t i = base + threadIdx.x;
-        const long long v = i < n ? (long long)in[i] : 0;
-        long long x = v;
-        for (int d = 1; d < 64; d <<= 1) {
-            const long long y = __shfl_up(x, d, 64);
-            if (lane >= d) x += y;
-        }
-        if (lane == 63) wsum[wid] = x;
-        __syncthreads();
-        if (wid == 0) {
-            long long s = lane < 16 ? wsum[lane] : 0;
-            for (int d = 1; d < 16; d <<= 1) {
-                const long long y = __shfl_up(s, d, 64);
-                if (lane >= d) s += y;
-            }
-            if (lane < 16) wsum[lane] = s;
-        }
-        __syncthreads();
-        const long long excl = carry + (wid ? wsum[wid - 1] : 0) + x - v;
-        if (i < n) out[i] = (int32_t)excl;
-        __syncthreads();
-        if (threadIdx.x == 1023) carry = excl + v;
-        __syncthreads();
+        const long long v = i < ntiles ? tile_sum[i] : 0;
+        long long sum;
+        const long long inc = block_scan256(v, wsum, &sum);
+        if (i < ntiles) tile_sum[i] = carry + inc - v;
+        carry += sum;
     }
     if (threadIdx.x == 0) {
         out[n] = (int32_t)carry;
         *total = carry;
     }
+}
+
+__global__ void __launch_bounds__(256) k_scan_apply(const int32_t* in, int64_t n, const long long* tile_off,
+                                                    int32_t* out) {
+    __shared__ int32_t tile[kScanTile];
+    __shared__ long long wsum[4];
+    scan_load_tile(in, n, tile);
+    int32_t c[16];
+    long long s = 0;
+    for (int i = 0; i < 16; ++i) {
+        c[i] = tile[threadIdx.x * 16 + i];
+        s += c[i];
+    }
+    long long tot;
+    long long run = tile_off[blockIdx.x] + block_scan256(s, wsum, &tot) - s;
+    for (int i = 0; i < 16; ++i) {   // exclusive values back into the tile (this thread's own slots)
+        tile[threadIdx.x * 16 + i] = (int32_t)run;
+        run += c[i];
+    }
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * kScanTile;
+    for (int i = threadIdx.x; i < kScanTile; i += 256)
+        if (base + i < n) out[base + i] = tile[i];
 }
 
 // ================================================================ SpGEMM ====
@@ -2059,9 +2102,13 @@ int mpbp_stokes_fill(const mpbp_stokes_params* prm, int32_t op, const double* ce
 int mpbp_exclusive_scan(const int32_t* row_nnz, int32_t* row_ptr, int64_t n, int64_t* total,
                         void* stream) {
     if (n < 0 || !row_ptr || (n > 0 && !row_nnz)) return set_error(MPBP_ERR_ARG, "scan: bad args");
-    long long* d_total = nullptr;
-    MPBP_HIP(hipMalloc(&d_total, sizeof(long long)));
-    k_exclusive_scan<<<1, 1024, 0, as_stream(stream)>>>(row_nnz, row_ptr, n, d_total);
+    const int64_t ntiles = (n + kScanTile - 1) / kScanTile;
+    long long* d_total = nullptr;   // [total, tile sums...]
+    MPBP_HIP(hipMalloc(&d_total, sizeof(long long) * (size_t)(1 + ntiles)));
+    hipStream_t st = as_stream(stream);
+    if (ntiles > 0) k_scan_tiles<<<(unsigned)ntiles, 256, 0, st>>>(row_nnz, n, d_total + 1);
+    k_scan_offsets<<<1, 256, 0, st>>>(d_total + 1, ntiles, row_ptr, n, d_total);
+    if (ntiles > 0) k_scan_apply<<<(unsigned)ntiles, 256, 0, st>>>(row_nnz, n, d_total + 1, row_ptr);
     hipError_t e = hipGetLastError();
     long long h = 0;
     if (e == hipSuccess) e = hipMemcpyAsync(&h, d_total, sizeof(h), hipMemcpyDeviceToHost, as_stream(stream));

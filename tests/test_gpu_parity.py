@@ -345,3 +345,28 @@ def test_fgmres_without_preconditioner_and_constant_theta():
     assert info_pc == 0 and len(hist_pc) < len(hist)
     # the pressure is determined up to a constant on the periodic grid: compare velocities
     assert np.max(np.abs(x[: 4 * N] - u[: 4 * N])) < 1e-6 and np.max(np.abs(xp.cpu().numpy()[: 4 * N] - u[: 4 * N])) < 1e-6
+
+
+@pytest.mark.parametrize("n", [0, 1, 255, 4095, 4096, 4097, 1_000_003])
+def test_exclusive_scan(n):
+    """Tiled row_ptr scan (assembly / SpGEMM / extraction setup): exact against numpy, row_ptr[n] = total."""
+    import ctypes
+    from mp_block_preconditioners_amd._lib import check, lib, ptr, stream_handle
+    rng = np.random.default_rng(n)
+    cnt = torch.from_numpy(rng.integers(0, 40, size=max(n, 1)).astype(np.int32)).cuda()
+    out = torch.full((n + 1,), -7, dtype=torch.int32, device="cuda")
+    total = ctypes.c_int64(-1)
+    check(lib().mpbp_exclusive_scan(ptr(cnt), ptr(out), n, ctypes.byref(total), stream_handle()))
+    ref = np.concatenate([[0], np.cumsum(cnt.cpu().numpy()[:n], dtype=np.int64)])
+    assert total.value == ref[-1]
+    assert np.array_equal(out.cpu().numpy(), ref.astype(np.int32))
+
+
+def test_exclusive_scan_overflow():
+    import ctypes
+    from mp_block_preconditioners_amd._lib import lib, ptr, stream_handle
+    cnt = torch.full((5000,), 1 << 20, dtype=torch.int32, device="cuda")   # total 5.2e9 > INT32_MAX
+    out = torch.empty(5001, dtype=torch.int32, device="cuda")
+    total = ctypes.c_int64(0)
+    rc = lib().mpbp_exclusive_scan(ptr(cnt), ptr(out), 5000, ctypes.byref(total), stream_handle())
+    assert rc == -3 and b"exceed int32" in lib().mpbp_last_error()
