@@ -88,6 +88,8 @@ def main():
                     help="grid rows per workgroup of the fused init + two-sweep F kernel; 0 = one kernel per sweep")
     ap.add_argument("--p-fusion", type=int, default=0,
                     help="grid rows per workgroup of the one-pass Gt_G inner solve; 0 = one kernel per sweep")
+    ap.add_argument("--no-ca", action="store_true",
+                    help="row partition: exchange before every sweep instead of the communication-avoiding schedule")
     ap.add_argument("--self-halo", action="store_true",
                     help="N = 1 only: run the row-partitioned apply with the ghost rows refreshed by the periodic "
                          "self-exchange over RCCL (measures the multi-GPU code path's overhead on one GPU)")
@@ -142,7 +144,8 @@ def main():
         from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
         pc = DistributedSchurPreconditioner(n, args.xi, args.eta_n, args.eta_s, inner_F=iF, inner_P=iP,
                                             layout=args.layout, f_mode=args.f_mode, pg_mode=args.pg_mode,
-                                            self_halo=args.self_halo, halo_overlap=args.halo_overlap)
+                                            self_halo=args.self_halo, halo_overlap=args.halo_overlap,
+                                            ca=False if args.no_ca else "auto")
     gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
     v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda", generator=gen)
     out = torch.empty_like(v)
@@ -242,7 +245,10 @@ def main():
                        "d_g_gtg": "matrix-free" if getattr(pc, "pg_stencil", None) is not None else "assembled",
                        "sweep_fusion_rows": args.sweep_fusion, "pressure_solve_fusion_rows": args.p_fusion,
                        "launch": "hipgraph" if graph is not None else "eager",
-                       **({"halo": f"{pc.halo_impl} ({'self-exchange' if world == 1 else 'neighbour'})"}
+                       **({"halo": f"{pc.halo_impl} ({'self-exchange' if world == 1 else 'neighbour'})",
+                           "halo_schedule": (f"communication-avoiding: 2 exchanges per apply, ghost depth "
+                                             f"{pc.h_u} (velocity) / {pc.h_p} (pressure)") if pc.ca
+                           else "one exchange per sweep"}
                           if partitioned else {}),
                        **({"note": graph_note} if graph_note else {})},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -106,7 +106,10 @@ typedef struct mpbp_row_part {
     int32_t r0;
     int32_t rows;
     int32_t halo;
-    int32_t which;
+    int32_t which;  /* 3: rows [-ext, rows + ext) -- the owned rows and `ext` ghost rows each side */
+    int32_t ext;    /* which = 3 only: ghost rows computed redundantly on each side (<= the halo depths) */
+    int32_t oh;     /* ghost depth of the OUTPUT vector's layout when it differs from `halo` (D: pressure
+                       out of velocity, G: velocity out of pressure); 0 = same as halo */
 } mpbp_row_part;
 
 typedef struct mpbp_stokes_params {
@@ -163,6 +166,16 @@ typedef struct mpbp_schur_plan {
     int32_t halo_first;              /* 1: each exchange completes (BEGIN, END) before the sweep, whose
                                         stencil rows then run as one launch; 0: interior rows launch
                                         between BEGIN and END, boundary rows after */
+    /* Communication-avoiding schedule (row partition, every operator but Gt_F_G matrix-free): v's halo
+     * and x_b's halo are exchanged once each, deep enough that every other operator runs on its owned
+     * rows plus the ghost rows its successors still need (computed redundantly): 2 exchanges per apply
+     * instead of one per sweep.  Depths (S_F, S_P = inner sweeps - 1, q = ca_reach_q):
+     *   f_part.halo >= q + S_P + 1 + S_F,  p_part.halo >= max(q + S_P, S_F + 1 + S_P). */
+    int32_t ca;                      /* 1: use it (ignored on one GPU) */
+    int32_t ca_reach_q;              /* grid-row reach of Gt_F_G's columns (its input's ghost depth) */
+    double* wu_ext;                  /* device, nu_ext: v's velocity part with its halo, later G x_p */
+    const double* diag_F_ext;        /* device, nu_ext: diag(F) on owned + ghost rows */
+    const double* diag_P_ext;        /* device, np_ext: diag(Gt_G) on owned + ghost rows */
 } mpbp_schur_plan;
 
 const char* mpbp_version(void);

@@ -40,7 +40,8 @@ class Sell(Structure):
 
 
 class RowPart(Structure):
-    _fields_ = [("r0", c_int32), ("rows", c_int32), ("halo", c_int32), ("which", c_int32)]
+    _fields_ = [("r0", c_int32), ("rows", c_int32), ("halo", c_int32), ("which", c_int32), ("ext", c_int32),
+                ("oh", c_int32)]
 
 
 class StokesParams(Structure):
@@ -71,7 +72,8 @@ class SchurPlan(Structure):
                 ("Gs_bnd", Sell), ("Ps_int", Sell), ("Ps_bnd", Sell), ("Qs_int", Sell), ("Qs_bnd", Sell),
                 ("f_stencil", c_int32), ("f_prm", StokesParams), ("f_cell", c_void_p), ("f_uface", c_void_p),
                 ("f_vface", c_void_p), ("f_part", RowPart), ("pg_stencil", c_int32), ("p_part", RowPart),
-                ("halo_first", c_int32)]
+                ("halo_first", c_int32), ("ca", c_int32), ("ca_reach_q", c_int32), ("wu_ext", c_void_p),
+                ("diag_F_ext", c_void_p), ("diag_P_ext", c_void_p)]
 
 
 _P = c_void_p

@@ -1004,6 +1004,14 @@ __device__ inline void sortk(Ent* e) {
     else sort5(e);
 }
 
+// Offset of local grid row lr (-h <= lr < L + h) of field f in an nf-field vector of the row-partition
+// layout: the owned rows field-major, then h ghost rows above of every field (increasing row order), then
+// h ghost rows below of every field.
+__device__ inline int32_t ext_row(int nf, int f, int lr, int L, int h, int n) {
+    if (lr >= 0 && lr < L) return (f * L + lr) * n;
+    return nf * L * n + (lr < 0 ? f * h + h + lr : nf * h + f * h + lr - L) * n;
+}
+
 struct FStencilDev {
     int n;
     double xi, eta_n, eta_s, c, d_u;
@@ -1019,21 +1027,23 @@ struct FStencilDev {
     // One GPU: r0 = 0, L = n, h = 0.
     int r0, L, h, which;
     int pow2;      // n is a power of two: dx * dx is a power of two and v / (dx * dx) == v * idx2 exactly
+    int ext = 0;   // which = 3: ghost rows computed on each side
+    int oh = 0;    // ghost depth of the output's layout (== h)
 
     __device__ int wrap(int a) const { return a < 0 ? a + n : (a >= n ? a - n : a); }
-    // index in x of (field f, grid row gr, column 0) for gr in [r0 - 1, r0 + L]
+    // index in x of (field f, grid row gr, column 0) for gr in [r0 - h, r0 + L + h)
     __device__ int32_t xrow(int f, int gr) const {
         if (h == 0) return (f * n + wrap(gr)) * n;
-        const int lr = gr - r0;
-        if (lr >= 0 && lr < L) return (f * L + lr) * n;
-        return 4 * L * n + (lr < 0 ? f * h + h - 1 : 4 * h + f * h) * n;   // ghost row r0-1 / r0+L
+        return ext_row(4, f, gr - r0, L, h, n);
     }
     // k_march policy: the 4 velocity fields staged, the cell's 4 rows out; per cell, the u- and v-face
     // thn values are requested with the epilogue operands (before the barrier), not inside the rows
     static constexpr int NF = 4, NOUT = 4;
     struct Cell { double face[2]; };
     __device__ Cell cell_pre(int gr, int gc) const { return {{uface[gr * n + gc], vface[gr * n + gc]}}; }
-    __device__ int32_t out_row(int f, int lr, int gc) const { return (f * L + lr) * n + gc; }
+    __device__ int32_t out_row(int f, int lr, int gc) const {
+        return (lr >= 0 && lr < L ? (f * L + lr) * n : ext_row(4, f, lr, L, oh, n)) + gc;
+    }
     template <bool EDGE, class TA, class XA>
     __device__ double row(int f, int gr, int gc, const TA& ta, const XA& xa, double* fd, const Cell& cl) const;
 };
@@ -1347,7 +1357,12 @@ __device__ inline void store_tile_row(double* sx, double* st, int slot, int tid,
 
 // Owned grid rows [la, lb) of workgroup chunk `chunk`: which = 0 all rows, 1 rows 1 .. L-2 (no ghost
 // read), 2 rows 0 and L-1 (one chunk each).
-__device__ inline bool march_rows(int which, int L, int chunk, int rows_per_block, int* la, int* lb) {
+__device__ inline bool march_rows(int which, int L, int ext, int chunk, int rows_per_block, int* la, int* lb) {
+    if (which == 3) {   // owned rows and `ext` ghost rows each side
+        *la = -ext + chunk * rows_per_block;
+        *lb = min(*la + rows_per_block, L + ext);
+        return *la < *lb;
+    }
     if (which == 2) {
         *la = chunk == 0 ? 0 : L - 1;
         *lb = *la + 1;
@@ -1371,7 +1386,7 @@ k_march(S P, XS xs, int rows_per_block, Epi epi) {
     const int b = xcd_swizzle(blockIdx.x, gridDim.x);
     const int strip = b % strips, chunk = b / strips;
     int la, lb;
-    if (!march_rows(P.which, P.L, chunk, rows_per_block, &la, &lb)) return;
+    if (!march_rows(P.which, P.L, P.ext, chunk, rows_per_block, &la, &lb)) return;
     const int c0 = strip * kMB, tid = threadIdx.x;
     const int colA = c0 - 1 + tid;
     const bool okA = colA <= n;
@@ -1399,11 +1414,11 @@ k_march(S P, XS xs, int rows_per_block, Epi epi) {
         typename Epi::P pe[NO];
 #pragma unroll
         for (int o = 0; o < NO; ++o) pe[o] = epi.pre_lite(P.out_row(o, lr, gcl));
-        const typename S::Cell cl = P.cell_pre(P.r0 + lr, gcl);
+        const typename S::Cell cl = P.cell_pre(P.wrap(P.r0 + lr), gcl);   // ghost rows wrap periodically
         __syncthreads();
         if (lr + 1 < lb) load_tile_row(P, xs, P.r0 + lr + 2, gcA, okA, gcB, okB, tr);   // in flight
         if (live) {
-            const int gr = P.r0 + lr;
+            const int gr = P.wrap(P.r0 + lr);
             const XRing xa{sx, {sm, s0, sp}, gr, c0};
             const TRing ta{st, {sm, s0, sp}, gr, c0};
             // the wrap-aware (sorting) form is exact for interior cells too: take it for the whole wave when
@@ -1426,7 +1441,8 @@ k_march(S P, XS xs, int rows_per_block, Epi epi) {
 // Launch k_march over the partition rows P.which selects.
 template <class S, class XS, class Epi>
 int launch_march(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStream_t st) {
-    const int64_t grows = P.which == 0 ? P.L : P.which == 1 ? (P.L > 2 ? P.L - 2 : 0) : (P.L >= 2 ? 2 : 1);
+    const int64_t grows = P.which == 0 ? P.L : P.which == 1 ? (P.L > 2 ? P.L - 2 : 0)
+                          : P.which == 3 ? P.L + 2 * P.ext : (P.L >= 2 ? 2 : 1);
     if (grows == 0) return MPBP_OK;
     const int64_t chunks = P.which == 2 ? grows : (grows + rows_per_block - 1) / rows_per_block;
     const int64_t blocks = chunks * ((P.n + kMB - 1) / kMB);
@@ -1454,13 +1470,17 @@ struct PGDev {
     double d_p, inv, minv;   // d_p, 1.0 / dx, -1.0 / dx  (dx == dy; evaluated as the assembly does)
     // partition of the INPUT vector's grid rows, as FStencilDev (one GPU: r0 = 0, L = n, h = 0)
     int r0, L, h, which;
+    int ext = 0;   // which = 3: ghost rows computed on each side
+    int oh = 0;    // ghost depth of the output's layout (D: pressure, G: velocity, Gt_G: == h)
     __device__ int wrap(int a) const { return a < 0 ? a + n : (a >= n ? a - n : a); }
     template <int NFI>
     __device__ int32_t xrow_of(int f, int gr) const {
         if (h == 0) return (f * n + wrap(gr)) * n;
-        const int lr = gr - r0;
-        if (lr >= 0 && lr < L) return (f * L + lr) * n;
-        return NFI * L * n + (lr < 0 ? f * h + h - 1 : NFI * h + f * h) * n;
+        return ext_row(NFI, f, gr - r0, L, h, n);
+    }
+    template <int NFO>
+    __device__ int32_t out_of(int f, int lr, int gc) const {
+        return (lr >= 0 && lr < L ? (f * L + lr) * n : ext_row(NFO, f, lr, L, oh, n)) + gc;
     }
 };
 
@@ -1470,7 +1490,7 @@ struct DStencilDev : PGDev {
     __device__ Cell cell_pre(int, int) const { return {}; }
     static constexpr int NF = 4, NOUT = 1;
     __device__ int32_t xrow(int f, int gr) const { return xrow_of<4>(f, gr); }
-    __device__ int32_t out_row(int, int lr, int gc) const { return lr * n + gc; }
+    __device__ int32_t out_row(int, int lr, int gc) const { return out_of<1>(0, lr, gc); }
     template <bool EDGE, class TA, class XA>
     __device__ double row(int, int gr, int gc, const TA& ta, const XA& xa, double* dg, const Cell&) const {
         const bool lastc = EDGE && gc == n - 1, lastr = EDGE && gr == n - 1;   // wrapped neighbour sorts first
@@ -1499,7 +1519,7 @@ struct GStencilDev : PGDev {
     __device__ Cell cell_pre(int, int) const { return {}; }
     static constexpr int NF = 1, NOUT = 4;
     __device__ int32_t xrow(int f, int gr) const { return xrow_of<1>(f, gr); }
-    __device__ int32_t out_row(int f, int lr, int gc) const { return (f * L + lr) * n + gc; }
+    __device__ int32_t out_row(int f, int lr, int gc) const { return out_of<4>(f, lr, gc); }
     template <bool EDGE, class TA, class XA>
     __device__ double row(int o, int gr, int gc, const TA& ta, const XA& xa, double* dg, const Cell&) const {
         const int p = o >> 1;
@@ -1530,7 +1550,7 @@ struct GtGStencilDev : PGDev {
     __device__ Cell cell_pre(int, int) const { return {}; }
     static constexpr int NF = 1, NOUT = 1;
     __device__ int32_t xrow(int f, int gr) const { return xrow_of<1>(f, gr); }
-    __device__ int32_t out_row(int, int lr, int gc) const { return lr * n + gc; }
+    __device__ int32_t out_row(int, int lr, int gc) const { return out_of<1>(0, lr, gc); }
     // e = {N, W, C, E, S}.  (vr, vc): the cell in the accessor's coordinates (it may lie up to a few cells
     // outside the grid in the fused solve); (gr, gc): the same cell wrapped onto the grid.
     template <class TA>
@@ -2435,15 +2455,18 @@ static int make_fstencil(const mpbp_stokes_params* prm, const double* cell, cons
         return set_error(MPBP_ERR_ARG, "f_stencil: needs n >= 3 and the three thn tables");
     if ((int64_t)prm->n * prm->n * 5 > INT32_MAX) return set_error(MPBP_ERR_OVERFLOW, "f_stencil: n too large");
     const double dx = 1.0 / prm->n;
-    int r0 = 0, L = prm->n, h = 0, which = 0;
+    int r0 = 0, L = prm->n, h = 0, which = 0, ext = 0, oh = 0;
     if (part && part->halo > 0) {
         r0 = part->r0; L = part->rows; h = part->halo; which = part->which;
-        if (L < 1 || r0 < 0 || r0 + L > prm->n || which < 0 || which > 2)
+        ext = which == 3 ? part->ext : 0;
+        oh = part->oh > 0 ? part->oh : h;
+        if (L < 1 || r0 < 0 || r0 + L > prm->n || which < 0 || which > 3 || ext < 0 || ext + 1 > h || ext > oh ||
+            h > L || oh > L)
             return set_error(MPBP_ERR_ARG, "f_stencil: bad row partition");
     }
     *P = FStencilDev{prm->n, prm->xi, prm->eta_n, prm->eta_s, prm->c, prm->d_u, cell, uface, vface,
                      dx * dx, 1.0 / (dx * dx), -1.0 / (dx * dx), r0, L, h, which,
-                     (prm->n & (prm->n - 1)) == 0 ? 1 : 0};
+                     (prm->n & (prm->n - 1)) == 0 ? 1 : 0, ext, oh};
     return MPBP_OK;
 }
 
@@ -2453,6 +2476,7 @@ namespace {
 template <class Epi>
 int launch_fstencil(const FStencilDev& P, const double* x, Epi epi, hipStream_t st) {
     if (g_stencil_kind == 2) return launch_march(P, XPlain{x}, epi, g_march_rows, st);   // marching LDS ring
+    if (P.which == 3) return set_error(MPBP_ERR_ARG, "f_stencil: ghost-row (which = 3) launches need the marching kernel");
     const int64_t grows = P.which == 0 ? P.L : P.which == 1 ? (P.L > 2 ? P.L - 2 : 0) : (P.L >= 2 ? 2 : 1);
     if (grows == 0) return MPBP_OK;
     if (g_stencil_kind != 1) {   // LDS-tiled cells
@@ -2517,13 +2541,16 @@ static int make_pgstencil(const mpbp_stokes_params* prm, const double* cell, con
     if (!prm || prm->n < 3 || !cell) return set_error(MPBP_ERR_ARG, "pg_stencil: needs n >= 3 and the cell thn table");
     if ((int64_t)prm->n * prm->n * 5 > INT32_MAX) return set_error(MPBP_ERR_OVERFLOW, "pg_stencil: n too large");
     const double dx = 1.0 / prm->n;   // as phase_D_row / phase_G_row evaluate 1.0 / dx, -1.0 / dx
-    int r0 = 0, L = prm->n, h = 0, which = 0;
+    int r0 = 0, L = prm->n, h = 0, which = 0, ext = 0, oh = 0;
     if (part && part->halo > 0) {
         r0 = part->r0; L = part->rows; h = part->halo; which = part->which;
-        if (L < 1 || r0 < 0 || r0 + L > prm->n || which < 0 || which > 2)
+        ext = which == 3 ? part->ext : 0;
+        oh = part->oh > 0 ? part->oh : h;
+        if (L < 1 || r0 < 0 || r0 + L > prm->n || which < 0 || which > 3 || ext < 0 || ext + 1 > h || ext > oh ||
+            h > L || oh > L)
             return set_error(MPBP_ERR_ARG, "pg_stencil: bad row partition");
     }
-    *P = PGDev{prm->n, cell, prm->d_p, 1.0 / dx, -1.0 / dx, r0, L, h, which};
+    *P = PGDev{prm->n, cell, prm->d_p, 1.0 / dx, -1.0 / dx, r0, L, h, which, ext, oh};
     return MPBP_OK;
 }
 
@@ -2613,14 +2640,19 @@ struct OpRef {
     const mpbp_sell* sell;
     const mpbp_schur_plan* stencil;   // rows recomputed from the plan's thn tables (sop says which operator)
     bool empty;
-    int32_t which;                    // stencil rows: 0 all, 1 interior, 2 boundary
+    int32_t which;                    // stencil rows: 0 all, 1 interior, 2 boundary, 3 owned + ext ghost rows
     int32_t sop;
+    int32_t ext = 0;                  // which = 3
 };
 
-// F and D read velocity vectors (f_part), G and Gt_G pressure vectors (p_part).
+// F and D read velocity vectors (f_part), G and Gt_G pressure vectors (p_part); D writes a pressure vector
+// and G a velocity one (output ghost depth oh).
 inline mpbp_row_part stencil_part(const OpRef& o) {
-    mpbp_row_part q = (o.sop == SOP_F || o.sop == SOP_D) ? o.stencil->f_part : o.stencil->p_part;
+    const mpbp_schur_plan* p = o.stencil;
+    mpbp_row_part q = (o.sop == SOP_F || o.sop == SOP_D) ? p->f_part : p->p_part;
     q.which = q.halo > 0 ? o.which : 0;
+    q.ext = q.which == 3 ? o.ext : 0;
+    q.oh = o.sop == SOP_D ? p->p_part.halo : o.sop == SOP_G ? p->f_part.halo : 0;
     return q;
 }
 
@@ -2682,15 +2714,16 @@ int op_first_sweep(const OpRef& o, bool cheb, const double* b, const double* dia
                    double* d, const double* sub, double* xo, hipStream_t st, int store_d) {
     const mpbp_schur_plan* p = o.stencil;
     const XInit xs{b, diag, cheb ? c2_0 : 1.0};
+    const mpbp_row_part q = stencil_part(o);   // one GPU: no partition; CA schedule: owned + ext ghost rows
     if (o.sop == SOP_F) {
         FStencilDev P;
-        const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &P);
+        const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, &P);
         if (rc) return rc;
         return cheb ? launch_march(P, xs, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, g_march_rows, st)
                     : launch_march(P, xs, EpiJacobi{nullptr, b, nullptr, sub, xo}, g_march_rows, st);
     }
     PGDev P;
-    const int rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &P);
+    const int rc = make_pgstencil(&p->f_prm, p->f_cell, &q, &P);
     if (rc) return rc;
     const GtGStencilDev S{P};
     return cheb ? launch_march(S, xs, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, pg_rows(), st)
@@ -2839,6 +2872,114 @@ int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag
     return MPBP_OK;
 }
 
+// ---- communication-avoiding schedule (row partition) ----
+// A stencil operator over the owned rows and `ext` ghost rows each side.
+OpRef ext_op(const mpbp_schur_plan* p, int32_t sop, int ext) {
+    OpRef o{nullptr, nullptr, nullptr, p, false, 3, sop};
+    o.ext = ext;
+    return o;
+}
+
+// Inner solve whose result is needed on the owned rows and d_out ghost rows each side: no exchange --
+// sweep s (of S = K - 1) runs on d_out + S - s ghost rows, the fused first sweep stages x0 from b and the
+// ghost-row diagonal d_out + S rows deep.  Same IEEE operations per row as the one-GPU solve.
+int ca_inner_solve(const Ctx& c, int32_t sop, const double* b, const double* diag_ext, const mpbp_inner_solver& in,
+                   int32_t n_init, double* dst, const double* sub, double* ping, double* pong, double* dir, int d_out,
+                   bool profile) {
+    const mpbp_schur_plan* p = c.p;
+    const int K = in.sweeps;
+    double c1[64], c2[64];
+    if (K < 1 || K > 64) return set_error(MPBP_ERR_ARG, "inner sweeps must be in [1, 64]");
+    const bool cheb = in.kind == MPBP_INNER_CHEBYSHEV;
+    if (cheb) {
+        if (!(in.lmax > in.lmin) || !(in.lmin >= 0.0)) return set_error(MPBP_ERR_ARG, "bad Chebyshev interval");
+        cheb_coeffs(in.lmin, in.lmax, K, c1, c2);
+    } else if (in.kind != MPBP_INNER_JACOBI) {
+        return set_error(MPBP_ERR_ARG, "unknown inner solver %d", in.kind);
+    }
+    if (K == 1) {   // x = x0 elementwise on every row the caller needs (n_init: owned, or the whole ext vector)
+        if (n_init <= 0) return MPBP_OK;
+        if (cheb) k_cheb_init<<<grid_for(n_init), kBlock, 0, c.st>>>(n_init, b, diag_ext, c2[0], dir, sub, dst);
+        else k_jacobi_init<<<grid_for(n_init), kBlock, 0, c.st>>>(n_init, b, diag_ext, sub, dst);
+        MPBP_HIP(hipGetLastError());
+        return MPBP_OK;
+    }
+    double* cur = K == 2 ? dst : pong;
+    int rc = op_first_sweep(ext_op(p, sop, d_out + K - 2), cheb, b, diag_ext, c2[0], c1[1], c2[1], dir,
+                            K == 2 ? sub : nullptr, cur, c.st, K == 2 ? 0 : 1);
+    if (rc) return rc;
+    for (int s = 2; s < K; ++s) {
+        const bool last = s == K - 1;
+        double* nxt = last ? dst : (cur == ping ? pong : ping);
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        const bool rec = profile && p->prof_events && p->prof_count && *p->prof_count < p->prof_capacity &&
+                         hipStreamIsCapturing(c.st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone;
+        if (rec) MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count], c.st));
+        const OpRef o = ext_op(p, sop, d_out + K - 1 - s);
+        rc = cheb ? op_cheb(o, cur, b, nullptr, c1[s], c2[s], dir, last ? sub : nullptr, nxt, c.st, last ? 0 : 1)
+                  : op_jacobi(o, cur, b, nullptr, last ? sub : nullptr, nxt, c.st);
+        if (rc) return rc;
+        if (rec) {
+            MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count + 1], c.st));
+            ++*p->prof_count;
+        }
+        cur = nxt;
+    }
+    return MPBP_OK;
+}
+
+// The exchange of one vector, complete before the next launch.
+void ca_exchange(const Ctx& c, int32_t kind, double* x_ext) {
+    c.p->halo(c.p->halo_ctx, kind, x_ext, MPBP_HALO_BEGIN, (void*)c.st);
+    c.p->halo(c.p->halo_ctx, kind, x_ext, MPBP_HALO_END, (void*)c.st);
+}
+
+// solve.py:257-277 with 2 halo exchanges: v (velocity and pressure parts) before the first F solve, x_b
+// before the second Gt_G solve; every other operator runs on the ghost rows its successors read.
+int schur_apply_ca(const Ctx& c, const double* v, double* out) {
+    const mpbp_schur_plan* p = c.p;
+    const int SF = p->inner_F.sweeps - 1, SP = p->inner_P.sweeps - 1, q = p->ca_reach_q;
+    const int d_xa = q, d_rhs = d_xa + SP, d_Y = d_rhs + 1, d_W = SF, d_xp = d_W + 1, d_xb = d_xp + SP;
+    if (SF < 0 || SP < 0 || q < 1 || p->f_part.halo < d_Y + SF || p->p_part.halo < d_rhs || p->p_part.halo < d_xb ||
+        p->p_part.halo < q || !p->wu_ext || !p->diag_F_ext || !p->diag_P_ext)
+        return set_error(MPBP_ERR_ARG, "schur_apply (CA): halo depths %d/%d below the schedule's %d/%d, or ext "
+                         "buffers missing", p->f_part.halo, p->p_part.halo, d_Y + SF, d_rhs > d_xb ? d_rhs : d_xb);
+    double *Y = p->wu[0], *U0 = p->wu[1], *U1 = p->wu[2], *Ud = p->wu[3], *Vu = p->wu_ext;
+    double *Prhs = p->wp[0], *Pxa = p->wp[1], *Pxb = p->wp[2], *Pxp = p->wp[3];
+    double *P0 = p->wp[4], *P1 = p->wp[5], *Pd = p->wp[6];
+    double* Vp = Pxb;   // v's pressure part lives in x_b's buffer until Gt_F_G overwrites it
+    int rc;
+    // v with its halo: velocity d_Y + S_F rows deep, pressure d_rhs rows deep (one exchange each)
+    MPBP_HIP(hipMemcpyAsync(Vu, v, sizeof(double) * (size_t)p->nu, hipMemcpyDeviceToDevice, c.st));
+    MPBP_HIP(hipMemcpyAsync(Vp, v + p->nu, sizeof(double) * (size_t)p->np, hipMemcpyDeviceToDevice, c.st));
+    ca_exchange(c, MPBP_VEC_VELOCITY, Vu);
+    ca_exchange(c, MPBP_VEC_PRESSURE, Vp);
+    // 1. Finv_v on owned + d_Y ghost rows                                    solve.py:258
+    rc = ca_inner_solve(c, SOP_F, Vu, p->diag_F_ext, p->inner_F, p->nu_ext, Y, nullptr, U0, U1, Ud, d_Y, true);
+    if (rc) return rc;
+    // 2. rhs = D Finv_v + v_p on owned + d_rhs ghost rows                      solve.py:259
+    rc = op_spmv(ext_op(p, SOP_D, d_rhs), MPBP_SPMV_ADD, Y, Vp, Prhs, c.st);
+    if (rc) return rc;
+    // 3. x_a = Gt_G^-1 rhs on owned + q ghost rows                            solve.py:265
+    rc = ca_inner_solve(c, SOP_GTG, Prhs, p->diag_P_ext, p->inner_P, p->np_ext, Pxa, nullptr, P0, P1, Pd, d_xa, false);
+    if (rc) return rc;
+    // 4. x_b = Gt_F_G x_a on the owned rows (its columns reach q ghost rows)  solve.py:267
+    const OpPair Q = make_op(p, p->GtFG, p->Q_int, p->Q_bnd, p->Qs_int, p->Qs_bnd);
+    rc = op_spmv(Q.in, MPBP_SPMV_STORE, Pxa, nullptr, Pxb, c.st);
+    if (!rc) rc = op_spmv(Q.bd, MPBP_SPMV_STORE, Pxa, nullptr, Pxb, c.st);
+    if (rc) return rc;
+    ca_exchange(c, MPBP_VEC_PRESSURE, Pxb);
+    // 5. x_p = Gt_G^-1 x_b on owned + d_xp ghost rows                         solve.py:271
+    rc = ca_inner_solve(c, SOP_GTG, Pxb, p->diag_P_ext, p->inner_P, p->np_ext, Pxp, nullptr, P0, P1, Pd, d_xp, false);
+    if (rc) return rc;
+    MPBP_HIP(hipMemcpyAsync(out + p->nu, Pxp, sizeof(double) * (size_t)p->np, hipMemcpyDeviceToDevice, c.st));
+    // 6. G x_p on owned + d_W ghost rows (into v's velocity buffer)          solve.py:273
+    rc = op_spmv(ext_op(p, SOP_G, d_W), MPBP_SPMV_STORE, Pxp, nullptr, Vu, c.st);
+    if (rc) return rc;
+    // 7. u = Finv_v - F^-1 (G x_p) on the owned rows                          solve.py:274-276
+    return ca_inner_solve(c, SOP_F, Vu, p->diag_F_ext, p->inner_F, p->nu, out, Y, U0, U1, Ud, 0, true);
+}
+
 }  // namespace
 
 extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, double* out, void* stream) {
@@ -2849,6 +2990,9 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
         if (!p->wp[i]) return set_error(MPBP_ERR_ARG, "schur_apply: missing pressure workspace");
     if (!p->wu_owned || !p->diag_F || !p->diag_P) return set_error(MPBP_ERR_ARG, "schur_apply: missing operands");
     const Ctx c{p, as_stream(stream)};
+    // the CA schedule needs every operator but Gt_F_G matrix-free on the marching kernel; otherwise the
+    // per-sweep exchanges below (its deeper halos serve them as well)
+    if (p->ca && p->halo && p->f_stencil && p->pg_stencil && g_stencil_kind == 2) return schur_apply_ca(c, v, out);
     if (p->f_stencil && p->halo && p->f_part.halo < 1)
         return set_error(MPBP_ERR_ARG, "schur_apply: a partitioned F stencil needs f_part");
     if (p->pg_stencil && p->halo && (p->p_part.halo < 1 || p->f_part.halo < 1))

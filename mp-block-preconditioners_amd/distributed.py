@@ -70,6 +70,16 @@ class RowPartition:
         n, N = self.n, self.N
         return np.concatenate([f * N + np.arange(self.r0 * n, self.r1 * n, dtype=np.int64) for f in range(nfields)])
 
+    def ext_rows(self, nfields, h) -> np.ndarray:
+        """Global id of every slot of the owned + ghost ("ext") layout: owned rows field-major, then h rows
+        above of every field (increasing row order), then h rows below of every field (periodic)."""
+        n, N = self.n, self.N
+        cols = np.arange(n, dtype=np.int64)
+        above = [f * N + ((self.r0 - h + j) % n) * n + cols for f in range(nfields) for j in range(h)]
+        below = [f * N + ((self.r1 + j) % n) * n + cols for f in range(nfields) for j in range(h)]
+        parts = [self.owned_rows(nfields)] + (above + below if self.ghosts else [])
+        return np.concatenate(parts)
+
     def colmap(self, nfields, h) -> np.ndarray:
         """Global column -> local ext index (-1 where the rank holds no copy)."""
         n, N, L = self.n, self.N, self.L
@@ -225,7 +235,7 @@ class DistributedSchurPreconditioner(PlanProfiling):
 
     def __init__(self, n, xi, eta_n, eta_s, c=1.0, d_u=-1.0, inner_F=None, inner_P=None, group=None,
                  device=None, layout="sell", f_mode="auto", pg_mode="auto", halo="auto", self_halo=False,
-                 halo_overlap=False):
+                 halo_overlap=False, ca="auto"):
         import torch.distributed as dist
         from .preconditioner import MultiphaseBlockPreconditioner
         from .solve import InnerSolver
@@ -260,12 +270,30 @@ class DistributedSchurPreconditioner(PlanProfiling):
             sub = M.extract(rows, torch.arange(M.shape[1], dtype=torch.int32, device=dev), M.shape[1])
             return halo_reach(sub.row_ptr, sub.col_idx, rows, n)
 
+        q = reach(GtFG, rows_p)
         self.h_u = max(1, reach(F, rows_u), reach(D, rows_p))
-        self.h_p = max(1, reach(G, rows_u), reach(GtG, rows_p), reach(GtFG, rows_p))
+        self.h_p = max(1, reach(G, rows_u), reach(GtG, rows_p), q)
+        # communication-avoiding schedule (mpbp_schur_plan.ca): v's halo and x_b's halo only, deep enough for
+        # every matrix-free operator to also compute the ghost rows its successors read
+        if ca not in ("auto", True, False):
+            raise ValueError("ca must be 'auto', True or False")
+        self.ca, self.ca_q = False, q
+        if ca and part.ghosts and self.f_stencil is not None and self.pg_stencil is not None:
+            sf, sp = self.inner_F.sweeps - 1, self.inner_P.sweeps - 1
+            hu, hp = q + sp + 1 + sf, max(q + sp, sf + 1 + sp, q)
+            if max(hu, hp) <= part.min_rows:
+                self.ca = True
+                self.h_u, self.h_p = max(self.h_u, hu), max(self.h_p, hp)
+            elif ca is True:
+                raise ValueError(f"ca=True needs {max(hu, hp)} grid rows per rank, the smallest has {part.min_rows}")
+        elif ca is True:
+            raise ValueError("ca=True needs a row partition and the matrix-free F, D, G, Gt_G")
         nu, np_ = part.n_owned(N_VEL_FIELDS), part.n_owned(N_P_FIELDS)
         nu_ext, np_ext = part.n_ext(N_VEL_FIELDS, self.h_u), part.n_ext(N_P_FIELDS, self.h_p)
         cm_u = torch.from_numpy(part.colmap(N_VEL_FIELDS, self.h_u)).to(dev)
         cm_p = torch.from_numpy(part.colmap(N_P_FIELDS, self.h_p)).to(dev)
+        if self.ca:
+            diag_F_glob, diag_P_glob = F.diagonal(), GtG.diagonal()
         self.F = F.extract(rows_u, cm_u, nu_ext)
         self.D = D.extract(rows_p, cm_u, nu_ext)
         self.G = G.extract(rows_u, cm_p, np_ext)
@@ -277,6 +305,12 @@ class DistributedSchurPreconditioner(PlanProfiling):
         self.shape = (nu + np_, nu + np_)
         self.diag_F = self.F.diagonal()
         self.diag_P = self.GtG.diagonal()
+        if self.ca:   # diagonals on owned + ghost rows (the CA schedule's ghost-row sweeps stage x0 = b / diag)
+            gu = torch.from_numpy(part.ext_rows(N_VEL_FIELDS, self.h_u)).to(dev)
+            gp = torch.from_numpy(part.ext_rows(N_P_FIELDS, self.h_p)).to(dev)
+            self.diag_F_ext = diag_F_glob[gu].contiguous()
+            self.diag_P_ext = diag_P_glob[gp].contiguous()
+            del diag_F_glob, diag_P_glob
 
         mats = {"F": (self.F, nu), "D": (self.D, nu), "G": (self.G, np_), "P": (self.GtG, np_),
                 "Q": (self.GtFG, np_)}
@@ -296,7 +330,8 @@ class DistributedSchurPreconditioner(PlanProfiling):
         self._wu = [torch.zeros(nu_ext, **f64) for _ in range(4)]
         self._wu_owned = torch.zeros(nu, **f64)
         self._wp = [torch.zeros(np_ext, **f64) for _ in range(7)]
-        self._tensors = {t.data_ptr(): t for t in self._wu + self._wp}
+        self._wu_ext = torch.zeros(nu_ext if self.ca else 0, **f64)
+        self._tensors = {t.data_ptr(): t for t in self._wu + self._wp + ([self._wu_ext] if self.ca else [])}
         self._rccl = None
         if not self.partitioned:
             self._cb = _lib.HALO_FN()
@@ -362,6 +397,10 @@ class DistributedSchurPreconditioner(PlanProfiling):
         # the in-order RCCL schedule gains nothing from splitting rows around the exchange: exchange first,
         # then one launch per sweep
         p.halo_first = 1 if (self._rccl is not None and not self._rccl.overlap) else 0
+        p.ca, p.ca_reach_q = (1 if self.ca else 0), self.ca_q
+        if self.ca:
+            p.wu_ext = self._wu_ext.data_ptr()
+            p.diag_F_ext, p.diag_P_ext = self.diag_F_ext.data_ptr(), self.diag_P_ext.data_ptr()
         p.prof_events = None
         p.prof_capacity = 0
         p.prof_count = ctypes.POINTER(ctypes.c_int32)()

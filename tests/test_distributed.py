@@ -108,3 +108,22 @@ def test_row_partition_maps():
                     assert np.all(row == -1)
     with pytest.raises(ValueError):
         RowPartition(8, 4, 0).colmap(1, 3)
+
+
+@pytest.mark.parametrize("n,world,h", [(12, 3, 2), (20, 2, 9), (9, 1, 3), (17, 4, 4)])
+def test_ext_rows_inverts_colmap(n, world, h):
+    """The ext layout's global ids (ext_rows: the CA schedule's ghost-row diagonals) are the inverse of
+    colmap (the extracted operators' column renumbering), ghosts included, for every rank."""
+    from mp_block_preconditioners_amd.distributed import RowPartition
+    for rank in range(world):
+        part = RowPartition(n, world, rank, ghosts=True)
+        for nf in (1, 4):
+            gid = part.ext_rows(nf, h)
+            assert gid.size == part.n_ext(nf, h)
+            cm = part.colmap(nf, h)
+            own = part.n_owned(nf)
+            assert np.array_equal(cm[gid[:own]], np.arange(own))
+            if world > 1:   # a ghost row may sit in two slots (2 h > a neighbour's rows): same global id
+                assert np.all(cm[gid] >= 0) and np.array_equal(gid[cm[gid]], gid)
+            else:           # one rank: the periodic ghosts duplicate owned rows
+                assert np.array_equal(np.sort(np.unique(gid)), np.arange(nf * n * n))

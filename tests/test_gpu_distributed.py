@@ -20,7 +20,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, layout, f_mode, kind, errfile):
+def _worker(rank, world, port, n, layout, f_mode, kind, errfile, ca="auto"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         torch.cuda.set_device(0)
@@ -30,8 +30,10 @@ def _worker(rank, world, port, n, layout, f_mode, kind, errfile):
         mpb.lib().mpbp_set_stencil_kind(kind)
         iF, iP = mpb.InnerSolver("chebyshev", 4), mpb.InnerSolver("chebyshev", 3)
         dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, layout=layout,
-                                             f_mode=f_mode)
+                                             f_mode=f_mode, ca=ca)
         assert (dpc.f_stencil is not None) == (f_mode != "assembled")
+        if ca is True:
+            assert dpc.ca and dpc.h_u == dpc.ca_q + 2 + 1 + 3, (dpc.h_u, dpc.ca_q)
         bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
         _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
         pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, layout=layout, f_mode="assembled")
@@ -65,7 +67,22 @@ def test_distributed_apply_matches_single_gpu(world, n, layout, f_mode, kind, tm
         pytest.fail(f"distributed worker failed:\n{msg}")
 
 
-def _self_halo_worker(_index, port, n, halo, f_mode, pg_mode, kind, graph, errfile, overlap=False):
+@pytest.mark.parametrize("world,n,layout,ca", [(2, 64, "sell", True), (2, 64, "sell", False), (3, 50, "csr", True),
+                                              (4, 40, "sell", True)])
+def test_distributed_apply_ca_schedule(world, n, layout, ca, tmp_path):
+    """The communication-avoiding schedule (2 exchanges per apply, ghost rows recomputed) and the per-sweep
+    one, 2-4 gloo ranks on one GPU, bit for bit against the single-GPU apply."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    errfile = str(tmp_path / "err.txt")
+    try:
+        mp.spawn(_worker, args=(world, _free_port(), n, layout, "stencil", 2, errfile, ca), nprocs=world, join=True)
+    except Exception:
+        msg = open(errfile).read() if os.path.exists(errfile) else ""
+        pytest.fail(f"distributed worker failed:\n{msg}")
+
+
+def _self_halo_worker(_index, port, n, halo, f_mode, pg_mode, kind, graph, errfile, overlap=False, ca="auto"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         torch.cuda.set_device(0)
@@ -75,7 +92,8 @@ def _self_halo_worker(_index, port, n, halo, f_mode, pg_mode, kind, graph, errfi
         mpb.lib().mpbp_set_stencil_kind(kind)
         iF, iP = mpb.InnerSolver("chebyshev", 4), mpb.InnerSolver("chebyshev", 3)
         dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, f_mode=f_mode,
-                                             pg_mode=pg_mode, halo=halo, self_halo=True, halo_overlap=overlap)
+                                             pg_mode=pg_mode, halo=halo, self_halo=True, halo_overlap=overlap,
+                                             ca=ca)
         assert dpc.partitioned and dpc.nu_ext > dpc.nu
         bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
         _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
@@ -104,7 +122,7 @@ def _self_halo_worker(_index, port, n, halo, f_mode, pg_mode, kind, graph, errfi
     (33, "rccl", "stencil", "assembled", 0, False, False), (64, "torch", "stencil", "stencil", 2, False, False),
     (64, "rccl", "stencil", "stencil", 2, True, False), (64, "rccl", "stencil", "stencil", 2, False, True),
     (40, "rccl", "assembled", "stencil", 2, False, True)])
-def test_self_halo_partitioned_apply(n, halo, f_mode, pg_mode, kind, graph, overlap, tmp_path):
+def test_self_halo_partitioned_apply(n, halo, f_mode, pg_mode, kind, graph, overlap, tmp_path, ca="auto"):
     """One rank runs the partitioned apply with ghost rows filled by the periodic self-exchange -- the
     RCCL point-to-point halo (libmpbp's own communicator) and the torch one -- bit for bit against the
     single-GPU apply."""
@@ -112,8 +130,14 @@ def test_self_halo_partitioned_apply(n, halo, f_mode, pg_mode, kind, graph, over
         pytest.skip("no GPU")
     errfile = str(tmp_path / "err.txt")
     try:
-        mp.spawn(_self_halo_worker, args=(_free_port(), n, halo, f_mode, pg_mode, kind, graph, errfile, overlap),
+        mp.spawn(_self_halo_worker, args=(_free_port(), n, halo, f_mode, pg_mode, kind, graph, errfile, overlap, ca),
                  nprocs=1, join=True)
     except Exception:
         msg = open(errfile).read() if os.path.exists(errfile) else ""
         pytest.fail(f"self-halo worker failed:\n{msg}")
+
+
+@pytest.mark.parametrize("halo,ca", [("rccl", False), ("rccl", True), ("torch", True)])
+def test_self_halo_ca_schedule(halo, ca, tmp_path):
+    """RCCL / torch self-exchange with and without the communication-avoiding schedule."""
+    test_self_halo_partitioned_apply(48, halo, "stencil", "stencil", 2, False, False, tmp_path, ca=ca)
