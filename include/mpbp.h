@@ -131,6 +131,8 @@ typedef struct mpbp_inner_solver {
 } mpbp_inner_solver;
 
 typedef void (*mpbp_halo_fn)(void* ctx, int32_t vec_kind, double* x_ext, int32_t phase, void* stream);
+/* A velocity and a pressure vector's halos in one exchange, complete on `stream` when it returns. */
+typedef void (*mpbp_halo_pair_fn)(void* ctx, double* xu_ext, double* xp_ext, void* stream);
 
 /* The apply's operands.  On one GPU every matrix's columns index the full vector and the
  * *_bnd row blocks are empty.  Under a row partition the columns index the "ext" layout of the
@@ -176,6 +178,8 @@ typedef struct mpbp_schur_plan {
     double* wu_ext;                  /* device, nu_ext: v's velocity part with its halo, later G x_p */
     const double* diag_F_ext;        /* device, nu_ext: diag(F) on owned + ghost rows */
     const double* diag_P_ext;        /* device, np_ext: diag(Gt_G) on owned + ghost rows */
+    mpbp_halo_pair_fn halo_pair;     /* optional (CA schedule): both halves of v in one exchange
+                                        (mpbp_halo_exchange_pair); NULL: two halo calls */
 } mpbp_schur_plan;
 
 const char* mpbp_version(void);
@@ -324,6 +328,9 @@ void mpbp_halo_exchange(void* halo, int32_t vec_kind, double* x_ext, int32_t pha
 int mpbp_halo_status(const mpbp_halo* halo);
 #define MPBP_HALO_IN_ORDER 0   /* group issued on the apply stream between interior and boundary (default) */
 #define MPBP_HALO_OVERLAP 1    /* group on a side stream, forked / joined by events around the interior */
+/* mpbp_halo_pair_fn over RCCL: one group with both vectors' neighbour sends / receives (IN_ORDER on
+ * `stream`; the velocity rows gathered first). */
+void mpbp_halo_exchange_pair(void* ctx, double* xu_ext, double* xp_ext, void* stream);
 int mpbp_halo_set_mode(mpbp_halo* halo, int32_t mode);
 const char* mpbp_halo_last_error(const mpbp_halo* halo);
 

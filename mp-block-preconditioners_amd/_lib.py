@@ -54,6 +54,7 @@ class InnerSolverC(Structure):
 
 
 HALO_FN = CFUNCTYPE(None, c_void_p, c_int32, c_void_p, c_int32, c_void_p)
+HALO_PAIR_FN = CFUNCTYPE(None, c_void_p, c_void_p, c_void_p, c_void_p)
 
 
 class SchurPlan(Structure):
@@ -73,7 +74,7 @@ class SchurPlan(Structure):
                 ("f_stencil", c_int32), ("f_prm", StokesParams), ("f_cell", c_void_p), ("f_uface", c_void_p),
                 ("f_vface", c_void_p), ("f_part", RowPart), ("pg_stencil", c_int32), ("p_part", RowPart),
                 ("halo_first", c_int32), ("ca", c_int32), ("ca_reach_q", c_int32), ("wu_ext", c_void_p),
-                ("diag_F_ext", c_void_p), ("diag_P_ext", c_void_p)]
+                ("diag_F_ext", c_void_p), ("diag_P_ext", c_void_p), ("halo_pair", HALO_PAIR_FN)]
 
 
 _P = c_void_p
@@ -120,6 +121,7 @@ _SIGNATURES = {
                           POINTER(c_void_p)], c_int),
     "mpbp_halo_destroy": ([_P], None),
     "mpbp_halo_exchange": ([_P, c_int32, _P, c_int32, _P], None),
+    "mpbp_halo_exchange_pair": ([_P, _P, _P, _P], None),
     "mpbp_halo_status": ([_P], c_int),
     "mpbp_halo_set_mode": ([_P, c_int32], c_int),
     "mpbp_halo_last_error": ([_P], c_char_p),

@@ -204,7 +204,17 @@ namespace {
 
 // One RCCL group on stream `on`: own top rows -> up, own bottom rows -> down, rows below <- down,
 // rows above <- up (a multi-field vector's rows gathered into pack_buf first, on the same stream).
+// The sends / receives of vector kind k (inside an open group).
+ncclResult_t halo_ops(mpbp_halo* H, int k, double* x_ext, hipStream_t on);
+
 ncclResult_t halo_group(mpbp_halo* H, int k, double* x_ext, hipStream_t on) {
+    const ncclResult_t e = H->rccl.group_start();
+    const ncclResult_t e2 = e == ncclSuccess ? halo_ops(H, k, x_ext, on) : e;
+    const ncclResult_t eg = H->rccl.group_end();
+    return e2 == ncclSuccess ? eg : e2;
+}
+
+ncclResult_t halo_ops(mpbp_halo* H, int k, double* x_ext, hipStream_t on) {
     const int nf = H->nf[k], h = H->h[k], n = H->n, L = H->rows;
     const size_t cnt = (size_t)nf * h * n;                   // values per direction
     const double* top = x_ext;                               // nf == 1: the rows in place
@@ -218,13 +228,11 @@ ncclResult_t halo_group(mpbp_halo* H, int k, double* x_ext, hipStream_t on) {
     double* above = x_ext + (size_t)nf * L * n;
     double* below = above + cnt;
     const Rccl& R = H->rccl;
-    ncclResult_t e = R.group_start();
-    if (e == ncclSuccess) e = R.send(top, cnt, ncclFloat64, H->up, H->comm, on);
+    ncclResult_t e = R.send(top, cnt, ncclFloat64, H->up, H->comm, on);
     if (e == ncclSuccess) e = R.send(bot, cnt, ncclFloat64, H->down, H->comm, on);
     if (e == ncclSuccess) e = R.recv(below, cnt, ncclFloat64, H->down, H->comm, on);
     if (e == ncclSuccess) e = R.recv(above, cnt, ncclFloat64, H->up, H->comm, on);
-    const ncclResult_t eg = R.group_end();
-    return e == ncclSuccess ? eg : e;
+    return e;
 }
 
 }  // namespace
@@ -261,6 +269,19 @@ void mpbp_halo_exchange(void* ctx, int32_t vec_kind, double* x_ext, int32_t phas
         return;
     }
     if (hipEventRecord(H->done[k], H->stream) != hipSuccess) fail(H, MPBP_ERR_HIP, "fork", "hipEventRecord");
+}
+
+void mpbp_halo_exchange_pair(void* ctx, double* xu_ext, double* xp_ext, void* stream) {
+    mpbp_halo* H = static_cast<mpbp_halo*>(ctx);
+    if (!H || H->status != MPBP_OK) return;
+    const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    // both vectors' operations in one group: the gather of the velocity rows runs before the group opens
+    const ncclResult_t e0 = H->rccl.group_start();
+    ncclResult_t e = e0 == ncclSuccess ? halo_ops(H, 0, xu_ext, st) : e0;
+    if (e == ncclSuccess) e = halo_ops(H, 1, xp_ext, st);
+    const ncclResult_t eg = H->rccl.group_end();
+    if (e == ncclSuccess) e = eg;
+    if (e != ncclSuccess) fail(H, MPBP_ERR_HIP, "RCCL pair group", H->rccl.error_string(e));
 }
 
 int mpbp_halo_set_mode(mpbp_halo* H, int32_t mode) {

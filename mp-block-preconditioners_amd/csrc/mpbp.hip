@@ -2952,8 +2952,12 @@ int schur_apply_ca(const Ctx& c, const double* v, double* out) {
     // v with its halo: velocity d_Y + S_F rows deep, pressure d_rhs rows deep (one exchange each)
     MPBP_HIP(hipMemcpyAsync(Vu, v, sizeof(double) * (size_t)p->nu, hipMemcpyDeviceToDevice, c.st));
     MPBP_HIP(hipMemcpyAsync(Vp, v + p->nu, sizeof(double) * (size_t)p->np, hipMemcpyDeviceToDevice, c.st));
-    ca_exchange(c, MPBP_VEC_VELOCITY, Vu);
-    ca_exchange(c, MPBP_VEC_PRESSURE, Vp);
+    if (p->halo_pair) {
+        p->halo_pair(p->halo_ctx, Vu, Vp, (void*)c.st);
+    } else {
+        ca_exchange(c, MPBP_VEC_VELOCITY, Vu);
+        ca_exchange(c, MPBP_VEC_PRESSURE, Vp);
+    }
     // 1. Finv_v on owned + d_Y ghost rows                                    solve.py:258
     rc = ca_inner_solve(c, SOP_F, Vu, p->diag_F_ext, p->inner_F, p->nu_ext, Y, nullptr, U0, U1, Ud, d_Y, true);
     if (rc) return rc;

@@ -208,6 +208,7 @@ class RcclHalo:
         check(lib().mpbp_halo_set_mode(self.handle, _lib.HALO_OVERLAP if overlap else _lib.HALO_IN_ORDER))
         self.overlap = overlap
         self.fn = _lib.HALO_FN(ctypes.cast(lib().mpbp_halo_exchange, ctypes.c_void_p).value)
+        self.pair_fn = _lib.HALO_PAIR_FN(ctypes.cast(lib().mpbp_halo_exchange_pair, ctypes.c_void_p).value)
 
     def check(self):
         if lib().mpbp_halo_status(self.handle) != 0:
@@ -399,6 +400,8 @@ class DistributedSchurPreconditioner(PlanProfiling):
         p.halo_first = 1 if (self._rccl is not None and not self._rccl.overlap) else 0
         p.ca, p.ca_reach_q = (1 if self.ca else 0), self.ca_q
         if self.ca:
+            if self._rccl is not None and not self._rccl.overlap:   # v's two halves in one RCCL group
+                p.halo_pair = self._rccl.pair_fn
             p.wu_ext = self._wu_ext.data_ptr()
             p.diag_F_ext, p.diag_P_ext = self.diag_F_ext.data_ptr(), self.diag_P_ext.data_ptr()
         p.prof_events = None
