@@ -1355,29 +1355,28 @@ __device__ inline void store_tile_row(double* sx, double* st, int slot, int tid,
     if (extra) st[slot * kMTileW + kMB + tid] = tr.tb;
 }
 
-// Owned grid rows [la, lb) of workgroup chunk `chunk`: which = 0 all rows, 1 rows 1 .. L-2 (no ghost
-// read), 2 rows 0 and L-1 (one chunk each).
-__device__ inline bool march_rows(int which, int L, int ext, int chunk, int rows_per_block, int* la, int* lb) {
-    if (which == 3) {   // owned rows and `ext` ghost rows each side
-        *la = -ext + chunk * rows_per_block;
-        *lb = min(*la + rows_per_block, L + ext);
-        return *la < *lb;
-    }
+// Grid rows [la, lb) of workgroup chunk `chunk` of `nchunks`: which = 0 all owned rows, 1 rows 1 .. L-2 (no
+// ghost read), 2 rows 0 and L-1 (one chunk each), 3 the owned rows and `ext` ghost rows each side.  The
+// rows are split evenly (chunk sizes differ by at most one), so a launch can be sized to one round of
+// workgroups (launch_march).
+__device__ inline bool march_rows(int which, int L, int ext, int chunk, int nchunks, int* la, int* lb) {
     if (which == 2) {
         *la = chunk == 0 ? 0 : L - 1;
         *lb = *la + 1;
         return chunk < (L >= 2 ? 2 : 1);
     }
-    const int lo = which == 1 ? 1 : 0, hi = which == 1 ? L - 1 : L;
-    *la = lo + chunk * rows_per_block;
-    *lb = min(*la + rows_per_block, hi);
+    const int lo = which == 1 ? 1 : which == 3 ? -ext : 0;
+    const int hi = which == 1 ? L - 1 : which == 3 ? L + ext : L;
+    const int rows = hi - lo;
+    *la = lo + (int)((int64_t)chunk * rows / nchunks);
+    *lb = lo + (int)((int64_t)(chunk + 1) * rows / nchunks);
     return *la < *lb;
 }
 
 template <class S, class XS, class Epi>
 // (4 waves per SIMD asked for explicitly: the F Chebyshev instance would otherwise take 130 VGPRs -> 3)
 __global__ void __launch_bounds__(kMB) __attribute__((amdgpu_waves_per_eu(4, 8)))
-k_march(S P, XS xs, int rows_per_block, Epi epi) {
+k_march(S P, XS xs, int nchunks, Epi epi) {
     constexpr int NF = S::NF, NO = S::NOUT;
     __shared__ double sx[NF * 3 * kMTileW];
     __shared__ double st[3 * kMTileW];
@@ -1386,7 +1385,7 @@ k_march(S P, XS xs, int rows_per_block, Epi epi) {
     const int b = xcd_swizzle(blockIdx.x, gridDim.x);
     const int strip = b % strips, chunk = b / strips;
     int la, lb;
-    if (!march_rows(P.which, P.L, P.ext, chunk, rows_per_block, &la, &lb)) return;
+    if (!march_rows(P.which, P.L, P.ext, chunk, nchunks, &la, &lb)) return;
     const int c0 = strip * kMB, tid = threadIdx.x;
     const int colA = c0 - 1 + tid;
     const bool okA = colA <= n;
@@ -1438,15 +1437,37 @@ k_march(S P, XS xs, int rows_per_block, Epi epi) {
     }
 }
 
-// Launch k_march over the partition rows P.which selects.
+// Workgroups of one k_march instance the device holds at once (occupancy x CUs), queried once.
+template <class S, class XS, class Epi>
+int64_t march_capacity() {
+    static int64_t cap = -1;
+    if (cap < 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_march<S, XS, Epi>, kMB, 0) != hipSuccess)
+            cus = per_cu = 0;
+        cap = (int64_t)cus * per_cu;
+    }
+    return cap;
+}
+
+// Launch k_march over the partition rows P.which selects, rows_per_block rows per workgroup -- except that
+// a launch up to 25 % over one round of workgroups is rebalanced into exactly one round (chunks of
+// rows_per_block or rows_per_block + 1 rows): a second round of a few workgroups would cost almost a whole
+// sweep's latency (ghost-row launches of the CA schedule, multi-GPU row partitions).
 template <class S, class XS, class Epi>
 int launch_march(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStream_t st) {
     const int64_t grows = P.which == 0 ? P.L : P.which == 1 ? (P.L > 2 ? P.L - 2 : 0)
                           : P.which == 3 ? P.L + 2 * P.ext : (P.L >= 2 ? 2 : 1);
     if (grows == 0) return MPBP_OK;
-    const int64_t chunks = P.which == 2 ? grows : (grows + rows_per_block - 1) / rows_per_block;
-    const int64_t blocks = chunks * ((P.n + kMB - 1) / kMB);
-    k_march<S, XS, Epi><<<(unsigned)blocks, kMB, 0, st>>>(P, xs, rows_per_block, epi);
+    const int64_t strips = (P.n + kMB - 1) / kMB;
+    int64_t chunks = P.which == 2 ? grows : (grows + rows_per_block - 1) / rows_per_block;
+    if (P.which != 2) {
+        const int64_t one_round = march_capacity<S, XS, Epi>() / strips;
+        if (one_round > 0 && chunks > one_round && chunks * 4 <= one_round * 5) chunks = one_round;
+    }
+    k_march<S, XS, Epi><<<(unsigned)(chunks * strips), kMB, 0, st>>>(P, xs, (int)chunks, epi);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
