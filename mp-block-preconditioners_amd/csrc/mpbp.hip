@@ -1052,13 +1052,19 @@ struct FStencilDev {
 // sorted (with fixed networks) where periodic wrap-around reorders them.  TA::T(s, gr, gc) is thn of
 // phase s at a cell, XA::X(f, gr, gc) the x entry of field f at a grid point (gr in [-1, n], gc in
 // [-1, n]; the accessors wrap).  Same operations as phase_L_row / F_row, same summation order.
-template <bool EDGE, class TA, class XA, bool VIRT = false>
+// M (exact parameter identities, compile time): bit 0 d_u == -1 (d_u * y is an exact negation, folded into
+// the products as a sign), bit 1 eta_n == 1, bit 2 eta_s == 1 (eta * y == y exactly).  Every entry keeps
+// the assembly's rounding; only multiplications whose result is exactly known are skipped.
+template <bool EDGE, class TA, class XA, bool VIRT = false, int M = 0>
 __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, const TA& ta, const XA& xa,
                                double* fdiag, const double* face = nullptr) {
     const int n = P.n;
     const int p = f >> 1;
     const double idx2 = P.idx2;
     const double eta = p ? P.eta_s : P.eta_n;
+    const bool eta1 = p ? (M & 4) != 0 : (M & 2) != 0;
+    auto dmul = [&](double y) -> double { return (M & 1) ? -y : P.d_u * y; };   // d_u * y
+    auto emul = [&](double y) -> double { return eta1 ? y : eta * y; };          // eta * y
     const int fu = 2 * p, fv = 2 * p + 1;
     const int32_t kc = VIRT ? P.wrap(gr) * n + P.wrap(gc) : gr * n + gc;   // VIRT: (gr, gc) may lie one cell outside
     auto key = [&](int r, int c) -> int32_t { return EDGE ? P.wrap(r) * n + P.wrap(c) : r * n + c; };
@@ -1076,20 +1082,19 @@ __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, cons
         const double th = face ? face[0] : P.uface[kc];   // face: thn at the u / v face, loaded ahead
         const double w = p ? P.c * (1.0 - th) : P.c * th;
         const double Ldiag = idx2 * (-tip1j - tij) + idx2 * (-iph_jph - iph_jmh);
-        const double fd = (w - P.d_u * xi_ii) + P.d_u * (eta * Ldiag);
+        const double fd = (w - dmul(xi_ii)) + dmul(emul(Ldiag));
         *fdiag = fd;
-        const double du = P.d_u;
-        Ent lo[5] = {Ent{key(gr - 1, gc), du * (eta * (idx2 * (iph_jph))), xa.X(fu, gr - 1, gc)},
-                     Ent{key(gr, gc - 1), du * (eta * (idx2 * (tij))), xa.X(fu, gr, gc - 1)},
+        Ent lo[5] = {Ent{key(gr - 1, gc), dmul(emul(idx2 * (iph_jph))), xa.X(fu, gr - 1, gc)},
+                     Ent{key(gr, gc - 1), dmul(emul(idx2 * (tij))), xa.X(fu, gr, gc - 1)},
                      Ent{key(gr, gc), fd, xa.X(fu, gr, gc)},
-                     Ent{key(gr, gc + 1), du * (eta * (P.pow2 ? tip1j * idx2 : tip1j / P.dxdx)), xa.X(fu, gr, gc + 1)},
-                     Ent{key(gr + 1, gc), du * (eta * (idx2 * (iph_jmh))), xa.X(fu, gr + 1, gc)}};
-        Ent hi[4] = {Ent{key(gr, gc - 1), du * (eta * (idx2 * (tij - iph_jph))), xa.X(fv, gr, gc - 1)},
-                     Ent{key(gr, gc), du * (eta * (idx2 * (-tip1j + iph_jph))), xa.X(fv, gr, gc)},
-                     Ent{key(gr + 1, gc - 1), du * (eta * (idx2 * (iph_jmh - tij))), xa.X(fv, gr + 1, gc - 1)},
-                     Ent{key(gr + 1, gc), du * (eta * (idx2 * (tip1j - iph_jmh))), xa.X(fv, gr + 1, gc)}};
+                     Ent{key(gr, gc + 1), dmul(emul(P.pow2 ? tip1j * idx2 : tip1j / P.dxdx)), xa.X(fu, gr, gc + 1)},
+                     Ent{key(gr + 1, gc), dmul(emul(idx2 * (iph_jmh))), xa.X(fu, gr + 1, gc)}};
+        Ent hi[4] = {Ent{key(gr, gc - 1), dmul(emul(idx2 * (tij - iph_jph))), xa.X(fv, gr, gc - 1)},
+                     Ent{key(gr, gc), dmul(emul(idx2 * (-tip1j + iph_jph))), xa.X(fv, gr, gc)},
+                     Ent{key(gr + 1, gc - 1), dmul(emul(idx2 * (iph_jmh - tij))), xa.X(fv, gr + 1, gc - 1)},
+                     Ent{key(gr + 1, gc), dmul(emul(idx2 * (tip1j - iph_jmh))), xa.X(fv, gr + 1, gc)}};
         if (EDGE) { sort5(lo); sort4(hi); }
-        const double vcross = du * xi_ii;
+        const double vcross = dmul(xi_ii);
         if (p == 1) acc += vcross * xcross;
 #pragma unroll
         for (int t = 0; t < 5; ++t) acc += lo[t].v * lo[t].x;
@@ -1107,20 +1112,19 @@ __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, cons
         const double imh_jph = 0.25 * (tim1j + tim1jp1 + tij + tijp1);
         const double iph_jph = 0.25 * (tij + tip1j + tijp1 + tip1jp1);
         const double Ldiag = P.midy2 * (tijp1 + tij) - idx2 * (iph_jph + imh_jph);
-        const double fd = (w - P.d_u * xi_ii) + P.d_u * (eta * Ldiag);
+        const double fd = (w - dmul(xi_ii)) + dmul(emul(Ldiag));
         *fdiag = fd;
-        const double du = P.d_u;
-        Ent lo[4] = {Ent{key(gr - 1, gc), du * (eta * (idx2 * (tijp1 - imh_jph))), xa.X(fu, gr - 1, gc)},
-                     Ent{key(gr - 1, gc + 1), du * (eta * (idx2 * (iph_jph - tijp1))), xa.X(fu, gr - 1, gc + 1)},
-                     Ent{key(gr, gc), du * (eta * (idx2 * (imh_jph - tij))), xa.X(fu, gr, gc)},
-                     Ent{key(gr, gc + 1), du * (eta * (idx2 * (tij - iph_jph))), xa.X(fu, gr, gc + 1)}};
-        Ent hi[5] = {Ent{key(gr - 1, gc), du * (eta * (idx2 * tijp1)), xa.X(fv, gr - 1, gc)},
-                     Ent{key(gr, gc - 1), du * (eta * (idx2 * imh_jph)), xa.X(fv, gr, gc - 1)},
+        Ent lo[4] = {Ent{key(gr - 1, gc), dmul(emul(idx2 * (tijp1 - imh_jph))), xa.X(fu, gr - 1, gc)},
+                     Ent{key(gr - 1, gc + 1), dmul(emul(idx2 * (iph_jph - tijp1))), xa.X(fu, gr - 1, gc + 1)},
+                     Ent{key(gr, gc), dmul(emul(idx2 * (imh_jph - tij))), xa.X(fu, gr, gc)},
+                     Ent{key(gr, gc + 1), dmul(emul(idx2 * (tij - iph_jph))), xa.X(fu, gr, gc + 1)}};
+        Ent hi[5] = {Ent{key(gr - 1, gc), dmul(emul(idx2 * tijp1)), xa.X(fv, gr - 1, gc)},
+                     Ent{key(gr, gc - 1), dmul(emul(idx2 * imh_jph)), xa.X(fv, gr, gc - 1)},
                      Ent{key(gr, gc), fd, xa.X(fv, gr, gc)},
-                     Ent{key(gr, gc + 1), du * (eta * (idx2 * iph_jph)), xa.X(fv, gr, gc + 1)},
-                     Ent{key(gr + 1, gc), du * (eta * (idx2 * tij)), xa.X(fv, gr + 1, gc)}};
+                     Ent{key(gr, gc + 1), dmul(emul(idx2 * iph_jph)), xa.X(fv, gr, gc + 1)},
+                     Ent{key(gr + 1, gc), dmul(emul(idx2 * tij)), xa.X(fv, gr + 1, gc)}};
         if (EDGE) { sort4(lo); sort5(hi); }
-        const double vcross = du * xi_ii;
+        const double vcross = dmul(xi_ii);
         if (p == 1) acc += vcross * xcross;
 #pragma unroll
         for (int t = 0; t < 4; ++t) acc += lo[t].v * lo[t].x;
@@ -1477,6 +1481,23 @@ template <bool EDGE, class TA, class XA>
 __device__ inline double FStencilDev::row(int f, int gr, int gc, const TA& ta, const XA& xa, double* fd,
                                           const Cell& cl) const {
     return f_row<EDGE>(*this, f, gr, gc, ta, xa, fd, cl.face);
+}
+
+// The F policy with the parameter identities of f_row's M compiled in (the reference's own parameters,
+// d_u = -1 and eta_s = 1, solve.py:292-297 / apply.py:33-35): fewer fp64 multiplies per row, same bits.
+template <int M>
+struct FStencilDevM : FStencilDev {
+    template <bool EDGE, class TA, class XA>
+    __device__ double row(int f, int gr, int gc, const TA& ta, const XA& xa, double* fd, const Cell& cl) const {
+        return f_row<EDGE, TA, XA, false, M>(*this, f, gr, gc, ta, xa, fd, cl.face);
+    }
+};
+
+// Calls fn with the F policy specialised for P's parameters (M = 0: none apply).
+template <class Fn>
+int with_f_identities(const FStencilDev& P, Fn&& fn) {
+    if (P.d_u == -1.0 && P.eta_s == 1.0) return P.eta_n == 1.0 ? fn(FStencilDevM<7>{P}) : fn(FStencilDevM<5>{P});
+    return fn(P);
 }
 
 // ------------------------------------------------------- matrix-free D, G, Gt_G ----
@@ -2496,7 +2517,8 @@ static int make_fstencil(const mpbp_stokes_params* prm, const double* cell, cons
 namespace {
 template <class Epi>
 int launch_fstencil(const FStencilDev& P, const double* x, Epi epi, hipStream_t st) {
-    if (g_stencil_kind == 2) return launch_march(P, XPlain{x}, epi, g_march_rows, st);   // marching LDS ring
+    if (g_stencil_kind == 2)   // marching LDS ring
+        return with_f_identities(P, [&](const auto& Q) { return launch_march(Q, XPlain{x}, epi, g_march_rows, st); });
     if (P.which == 3) return set_error(MPBP_ERR_ARG, "f_stencil: ghost-row (which = 3) launches need the marching kernel");
     const int64_t grows = P.which == 0 ? P.L : P.which == 1 ? (P.L > 2 ? P.L - 2 : 0) : (P.L >= 2 ? 2 : 1);
     if (grows == 0) return MPBP_OK;
@@ -2740,8 +2762,10 @@ int op_first_sweep(const OpRef& o, bool cheb, const double* b, const double* dia
         FStencilDev P;
         const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, &P);
         if (rc) return rc;
-        return cheb ? launch_march(P, xs, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, g_march_rows, st)
-                    : launch_march(P, xs, EpiJacobi{nullptr, b, nullptr, sub, xo}, g_march_rows, st);
+        return with_f_identities(P, [&](const auto& Q) {
+            return cheb ? launch_march(Q, xs, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, g_march_rows, st)
+                        : launch_march(Q, xs, EpiJacobi{nullptr, b, nullptr, sub, xo}, g_march_rows, st);
+        });
     }
     PGDev P;
     const int rc = make_pgstencil(&p->f_prm, p->f_cell, &q, &P);
