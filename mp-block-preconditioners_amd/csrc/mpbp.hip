@@ -3081,9 +3081,12 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
                    [&](const OpRef& o) { return op_spmv(o, MPBP_SPMV_STORE, Pxa, nullptr, Pxb, c.st); });
     if (rc) return rc;
     // 5. x_p = Gt_G_factorization @ x_b                                    solve.py:271
+    //    (one GPU: straight into the output, which G then reads; a partition needs x_p's ghost rows)
+    if (!p->halo) Pxp = out_p;
     rc = inner_solve(c, MPBP_VEC_PRESSURE, P, p->diag_P, p->inner_P, p->np, Pxb, Pxp, nullptr, P0, P1, Pd, false);
     if (rc) return rc;
-    MPBP_HIP(hipMemcpyAsync(out_p, Pxp, sizeof(double) * (size_t)p->np, hipMemcpyDeviceToDevice, c.st));
+    if (Pxp != out_p)
+        MPBP_HIP(hipMemcpyAsync(out_p, Pxp, sizeof(double) * (size_t)p->np, hipMemcpyDeviceToDevice, c.st));
     // 6. G_xp = G @ x_p                                                     solve.py:273
     rc = two_phase(c, MPBP_VEC_PRESSURE, Pxp, G,
                    [&](const OpRef& o) { return op_spmv(o, MPBP_SPMV_STORE, Pxp, nullptr, W, c.st); });
