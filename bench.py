@@ -46,12 +46,15 @@ def sweep_bytes(pc, layout, kind, sweeps, fused_init):
     cheb = kind == "chebyshev"
     stencil = getattr(pc, "f_stencil", None) is not None
     if stencil:
-        fixed, kname = 3 * 8 * (nF // 4), "k_march<FStencilDev, XPlain, EpiCheb> (F sweep, matrix-free)"
+        prm = pc.f_stencil.prm   # the parameter identities compiled into the F policy (csrc: with_f_identities)
+        pol = ("FStencilDevM<7>" if prm.eta_n == 1.0 else "FStencilDevM<5>") \
+            if (prm.d_u == -1.0 and prm.eta_s == 1.0) else "FStencilDev"
+        fixed, kname = 3 * 8 * (nF // 4), f"k_march<{pol}, XPlain, EpiCheb> (F sweep, matrix-free)"
     elif layout == "sell":
         fixed = nnzF * 12 + nF * 1 + pc.sell_of("F").nslices * 16
         kname = "k_sell_rows<EpiCheb> (F sweep, SELL-64)"
     else:
-        fixed, kname = nnzF * 12 + (nF + 1) * 4 + F.blocks.count * 8, "k_csr_rows<EpiCheb> (F sweep, CSR)"
+        fixed, kname = nnzF * 12 + (nF + 1) * 4 + F.blocks.count * 8, "k_csr_wave<EpiCheb> (F sweep, CSR)"
     total, launches = 0, 0
     for solve in (1, 2):
         for s in range(2 if fused_init else 1, sweeps):

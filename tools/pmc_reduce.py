@@ -17,7 +17,8 @@ import os
 def mean_counter(path, counter, kernel_substr, grid):
     vals = []
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] == counter and kernel_substr in r["Kernel_Name"] and \
+        parts = kernel_substr if isinstance(kernel_substr, tuple) else (kernel_substr,)
+        if r["Counter_Name"] == counter and all(k in r["Kernel_Name"] for k in parts) and \
                 (grid is None or int(r["Grid_Size"]) == grid):
             vals.append(float(r["Counter_Value"]))
     return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
@@ -32,8 +33,9 @@ def main():
     grid = 4 * args.n * args.n
     # F sweep kernels and their launch grids (threads)
     # (the marching kernel's grid depends on its rows per workgroup: matched by name only)
-    kernels = {"stencil": ("k_march<(anonymous namespace)::FStencilDev, (anonymous namespace)::XPlain, "
-                           "(anonymous namespace)::EpiCheb>", None),
+    # (the F policy may carry the parameter identities: FStencilDev or FStencilDevM<M>)
+    kernels = {"stencil": (("k_march<(anonymous namespace)::FStencilDev", "(anonymous namespace)::XPlain, "
+                            "(anonymous namespace)::EpiCheb>"), None),
                "sell": ("k_sell_rows<(anonymous namespace)::EpiCheb>", grid)}   # grid 4N: F rows, not Gt_G
     out = {"n": args.n, "source": args.run_dir}
     for lay, (kname, kgrid) in kernels.items():
