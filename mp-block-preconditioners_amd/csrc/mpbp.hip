@@ -2863,7 +2863,7 @@ int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag
                 int32_t nrows, const double* b, double* dst, const double* sub, double* ping, double* pong,
                 double* dir, bool profile) {
     const int K = in.sweeps;
-    double c1[64], c2[64];
+    double c1[64] = {}, c2[64] = {};   // zeros for Jacobi (never read uninitialised)
     if (K < 1 || K > 64) return set_error(MPBP_ERR_ARG, "inner sweeps must be in [1, 64]");
     const bool cheb = in.kind == MPBP_INNER_CHEBYSHEV;
     if (cheb) {
@@ -2933,7 +2933,7 @@ int ca_inner_solve(const Ctx& c, int32_t sop, const double* b, const double* dia
                    bool profile) {
     const mpbp_schur_plan* p = c.p;
     const int K = in.sweeps;
-    double c1[64], c2[64];
+    double c1[64] = {}, c2[64] = {};   // zeros for Jacobi (never read uninitialised)
     if (K < 1 || K > 64) return set_error(MPBP_ERR_ARG, "inner sweeps must be in [1, 64]");
     const bool cheb = in.kind == MPBP_INNER_CHEBYSHEV;
     if (cheb) {

@@ -82,7 +82,8 @@ def test_distributed_apply_ca_schedule(world, n, layout, ca, tmp_path):
         pytest.fail(f"distributed worker failed:\n{msg}")
 
 
-def _self_halo_worker(_index, port, n, halo, f_mode, pg_mode, kind, graph, errfile, overlap=False, ca="auto"):
+def _self_halo_worker(_index, port, n, halo, f_mode, pg_mode, kind, graph, errfile, overlap=False, ca="auto",
+                      inner=(("chebyshev", 4), ("chebyshev", 3))):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         torch.cuda.set_device(0)
@@ -90,10 +91,12 @@ def _self_halo_worker(_index, port, n, halo, f_mode, pg_mode, kind, graph, errfi
         import mp_block_preconditioners_amd as mpb
         from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
         mpb.lib().mpbp_set_stencil_kind(kind)
-        iF, iP = mpb.InnerSolver("chebyshev", 4), mpb.InnerSolver("chebyshev", 3)
+        iF, iP = mpb.InnerSolver(*inner[0]), mpb.InnerSolver(*inner[1])
         dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, f_mode=f_mode,
                                              pg_mode=pg_mode, halo=halo, self_halo=True, halo_overlap=overlap,
                                              ca=ca)
+        if ca is True:
+            assert dpc.ca
         assert dpc.partitioned and dpc.nu_ext > dpc.nu
         bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
         _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
@@ -122,7 +125,8 @@ def _self_halo_worker(_index, port, n, halo, f_mode, pg_mode, kind, graph, errfi
     (33, "rccl", "stencil", "assembled", 0, False, False), (64, "torch", "stencil", "stencil", 2, False, False),
     (64, "rccl", "stencil", "stencil", 2, True, False), (64, "rccl", "stencil", "stencil", 2, False, True),
     (40, "rccl", "assembled", "stencil", 2, False, True)])
-def test_self_halo_partitioned_apply(n, halo, f_mode, pg_mode, kind, graph, overlap, tmp_path, ca="auto"):
+def test_self_halo_partitioned_apply(n, halo, f_mode, pg_mode, kind, graph, overlap, tmp_path, ca="auto",
+                                     inner=(("chebyshev", 4), ("chebyshev", 3))):
     """One rank runs the partitioned apply with ghost rows filled by the periodic self-exchange -- the
     RCCL point-to-point halo (libmpbp's own communicator) and the torch one -- bit for bit against the
     single-GPU apply."""
@@ -130,7 +134,8 @@ def test_self_halo_partitioned_apply(n, halo, f_mode, pg_mode, kind, graph, over
         pytest.skip("no GPU")
     errfile = str(tmp_path / "err.txt")
     try:
-        mp.spawn(_self_halo_worker, args=(_free_port(), n, halo, f_mode, pg_mode, kind, graph, errfile, overlap, ca),
+        mp.spawn(_self_halo_worker, args=(_free_port(), n, halo, f_mode, pg_mode, kind, graph, errfile, overlap, ca,
+                                          inner),
                  nprocs=1, join=True)
     except Exception:
         msg = open(errfile).read() if os.path.exists(errfile) else ""
@@ -141,3 +146,13 @@ def test_self_halo_partitioned_apply(n, halo, f_mode, pg_mode, kind, graph, over
 def test_self_halo_ca_schedule(halo, ca, tmp_path):
     """RCCL / torch self-exchange with and without the communication-avoiding schedule."""
     test_self_halo_partitioned_apply(48, halo, "stencil", "stencil", 2, False, False, tmp_path, ca=ca)
+
+
+@pytest.mark.parametrize("inner", [(("jacobi", 1), ("jacobi", 1)), (("jacobi", 2), ("chebyshev", 2)),
+                                   (("chebyshev", 6), ("jacobi", 3)), (("chebyshev", 3), ("chebyshev", 5))],
+                         ids=["jac1-jac1", "jac2-cheb2", "cheb6-jac3", "cheb3-cheb5"])
+def test_self_halo_ca_inner_solvers(inner, tmp_path):
+    """The CA schedule's ghost-row depths for other inner solvers: one-sweep (init only) solves, Jacobi,
+    deeper Chebyshev -- bit for bit against the single-GPU apply (RCCL self-exchange)."""
+    test_self_halo_partitioned_apply(40, "rccl", "stencil", "stencil", 2, False, False, tmp_path, ca=True,
+                                     inner=inner)

@@ -149,3 +149,55 @@ def test_two_sweep_fusion_bit_exact(n, rows):
             assert _bits(got, ref), (kind, k, float((got - ref).abs().max()))
     finally:
         check(lib().mpbp_set_sweep_fusion(0))
+
+
+def _ext_local_rows(n, L, h, nf):
+    """Local grid row (-h .. L+h-1) of every slot of the owned + ghost layout (RowPartition.ext_rows order)."""
+    own = np.repeat(np.tile(np.arange(L), nf), n)
+    above = np.repeat(np.tile(np.arange(-h, 0), nf), n)
+    below = np.repeat(np.tile(np.arange(L, L + h), nf), n)
+    return np.concatenate([own, above, below])
+
+
+@pytest.mark.parametrize("kind", ["jacobi", "chebyshev", "spmv"])
+def test_f_stencil_ghost_rows_bit_exact(kind):
+    """The marching F stencil on owned + ext ghost rows (mpbp_row_part.which = 3, the CA schedule's launches):
+    every computed slot equals the one-GPU result at that slot's global row, ghost rows at the periodic grid
+    edge included."""
+    import mp_block_preconditioners_amd as mp
+    from mp_block_preconditioners_amd._lib import RowPart, check, lib, ptr, stream_handle
+    from mp_block_preconditioners_amd.distributed import RowPartition
+    n, h, e = 24, 4, 3
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    _, _, F, _, _ = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    st = F.stencil
+    tabs = (ptr(st.cell), ptr(st.uface), ptr(st.vface))
+    part = RowPartition(n, 1, 0, ghosts=True)
+    gid = torch.from_numpy(part.ext_rows(4, h)).cuda()
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x, b, d = (torch.randn(F.shape[0], dtype=torch.float64, device="cuda", generator=g) for _ in range(3))
+    y = torch.empty_like(x)
+    ye = torch.full((gid.numel(),), float("nan"), dtype=torch.float64, device="cuda")
+    xe, be, de = x[gid].contiguous(), b[gid].contiguous(), d[gid].contiguous()
+    rp = RowPart(0, n, h, 3, e, 0)
+    if kind == "jacobi":
+        check(lib().mpbp_f_stencil_jacobi_step(ctypes.byref(st.prm), *tabs, None, ptr(x), ptr(b), None, ptr(y),
+                                               stream_handle()))
+        check(lib().mpbp_f_stencil_jacobi_step(ctypes.byref(st.prm), *tabs, ctypes.byref(rp), ptr(xe), ptr(be), None,
+                                               ptr(ye), stream_handle()))
+    elif kind == "chebyshev":
+        check(lib().mpbp_f_stencil_cheb_step(ctypes.byref(st.prm), *tabs, None, ptr(x), ptr(b), 0.7, 1.3, ptr(d),
+                                             None, ptr(y), stream_handle()))
+        check(lib().mpbp_f_stencil_cheb_step(ctypes.byref(st.prm), *tabs, ctypes.byref(rp), ptr(xe), ptr(be), 0.7,
+                                             1.3, ptr(de), None, ptr(ye), stream_handle()))
+    else:
+        check(lib().mpbp_f_stencil_spmv(ctypes.byref(st.prm), *tabs, None, 1, ptr(x), ptr(b), ptr(y),
+                                        stream_handle()))
+        check(lib().mpbp_f_stencil_spmv(ctypes.byref(st.prm), *tabs, ctypes.byref(rp), 1, ptr(xe), ptr(be), ptr(ye),
+                                        stream_handle()))
+    lr = torch.from_numpy(_ext_local_rows(n, n, h, 4)).cuda()
+    sel = (lr >= -e) & (lr < n + e)
+    assert _bits(ye[sel], y[gid][sel])
+    if kind == "chebyshev":
+        assert _bits(de[sel], d[gid][sel])
+    assert torch.isnan(ye[~sel]).all()     # rows beyond the ext depth are not written
