@@ -326,9 +326,24 @@ def cpu_baseline(pc, v, seconds, kf, sf, kp, spp):
     # the GPU apply of the same vector must be bit-identical to the timed oracle output
     gpu = pc.apply(v).cpu().numpy()
     same = bool(np.array_equal(gpu.view(np.uint64), ref.view(np.uint64)))
+    # the reference's own CPU form of the same apply: scipy.sparse `@` products + numpy vectors
+    from oracle.schur_oracle import approx_schur_apply_scipy
+    sdone = 0
+    t0 = time.perf_counter()
+    while True:
+        sref = approx_schur_apply_scipy(Fh, Dh, Gh, GtGh, GtFGh, vh, iF, iP, dF, dP)
+        sdone += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    sel = time.perf_counter() - t0
+    srel = float(np.max(np.abs(sref - gpu)) / np.max(np.abs(gpu)))
     return {"value": done / el, "unit": "applies/s", "cores": 1, "kind": "port",
             "sample": f"{done} full applies of the same {pc.shape[0]}-unknown system in {el:.1f} s "
-                      f"(oracle/csr_oracle.c, 1 thread)", "bit_exact_vs_gpu": same}
+                      f"(oracle/csr_oracle.c, 1 thread)", "bit_exact_vs_gpu": same,
+            "scipy": {"value": sdone / sel, "unit": "applies/s", "cores": 1,
+                      "sample": f"{sdone} applies composed from scipy.sparse CSR products (the reference's "
+                                f"CPU form, solve.py:257-277) in {sel:.1f} s, 1 thread",
+                      "rel_inf_vs_gpu": srel}}
 
 
 if __name__ == "__main__":

@@ -308,7 +308,9 @@ int mpbp_set_sweep_fusion(int32_t rows);
  * workgroup; 0 (default) = one kernel per sweep, faster on MI355X.  Bit-identical either way. */
 int mpbp_set_pressure_solve_fusion(int32_t rows);
 /* CSR SpMV kernel over row blocks (process-wide): 1 = one wavefront per 64 rows, chunked LDS stage, no
- * workgroup barrier (default); 0 = one LDS stage per 256-row block.  Bit-identical either way. */
+ * workgroup barrier (default); 2 = as 1 over several consecutive row blocks per workgroup, each wave
+ * prefetching its next block's chunk during the current block's gathers; 0 = one LDS stage per 256-row
+ * block.  Bit-identical in every case. */
 int mpbp_set_csr_kernel(int32_t kind);
 
 /* ---- ghost rows over RCCL point-to-point (multi-GPU row partition) ------------------------------ */

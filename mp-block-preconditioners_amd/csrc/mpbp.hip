@@ -26,7 +26,12 @@ int g_march_rows = 4;     // grid rows per workgroup of the marching kernel (4 i
 inline int pg_rows() { return MPBP_PG_ROWS > 0 ? MPBP_PG_ROWS : g_march_rows; }
 int g_sweep2_rows = 0;    // grid rows per workgroup of the two-sweep kernel; 0 (default) = no two-sweep fusion
 int g_gtg_solve_rows = 0; // grid rows per workgroup of the one-pass Gt_G solve (k_gtg_solve); 0 (default) = off
-int g_csr_kind = 1;       // CSR SpMV kernel: 0 workgroup-staged row blocks (k_csr_rows), 1 per-wave chunks (k_csr_wave)
+#ifndef MPBP_CSR_KIND
+#define MPBP_CSR_KIND 1
+#endif
+// CSR SpMV kernel: 0 workgroup-staged row blocks (k_csr_rows), 1 per-wave chunks (k_csr_wave), 2 per-wave
+// chunks over several row blocks per workgroup with the next block's chunk prefetched (k_csr_wave_pf)
+int g_csr_kind = MPBP_CSR_KIND;
 
 int set_error(int code, const char* fmt, ...) {
     va_list ap;
@@ -902,6 +907,130 @@ __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __rest
 #endif
     }
     if (live) epi.template apply<MPBP_CSR_NT != 0>(r, acc, pe);
+}
+
+// k_csr_wave with SEGS consecutive row blocks per workgroup and the next block's matrix chunk
+// prefetched: as soon as a wave has moved its chunk into LDS, its (now free) chunk registers receive the
+// loads of its quarter of the next row block, so that stream is in flight during this block's x gathers
+// and sums instead of after them (a wave's life was load -> wait -> gather -> wait -> store, with LDS
+// capping occupancy at 4 waves per SIMD).  Same per-row order of additions as k_csr_wave: bit-exact.
+#ifndef MPBP_CSR_SEGS
+#define MPBP_CSR_SEGS 4
+#endif
+constexpr int kRowBatchPf = 6;   // pairs of a row gathered at once (a 12-entry velocity row: one batch)
+template <class Epi, int SEGS>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) k_csr_wave_pf(Csr A, const double* __restrict__ x,
+                                                        const int2* __restrict__ blocks, int nblocks,
+                                                        Epi epi) {
+    __shared__ double2 vstage[kBlock / 64][kWaveCap / 2];
+    __shared__ int2 cstage[kBlock / 64][kWaveCap / 2];
+    const int nwg = (nblocks + SEGS - 1) / SEGS;
+    const int g = xcd_swizzle(blockIdx.x, nwg);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double2* vs = vstage[w];
+    int2* cs = cstage[w];
+    const double* vs1 = reinterpret_cast<const double*>(vs);
+    const int32_t* cs1 = reinterpret_cast<const int32_t*>(cs);
+    const int b_end = min(g * SEGS + SEGS, nblocks);
+    // this wave's rows of block b: [ra, rb), or false when the block has no rows for it
+    auto seg = [&](int b, int32_t& ra, int32_t& rb) -> bool {
+        const int2 blk = blocks[b];
+        ra = blk.x + 64 * w;
+        rb = min(ra + 64, blk.y);
+        return ra < blk.y;
+    };
+    double2 v[kWavePairs];
+    int2 cc[kWavePairs];
+    auto load_chunk = [&](int32_t cb, int32_t e) {
+#pragma unroll
+        for (int j = 0; j < kWavePairs; ++j) {
+            const int32_t k = cb + 2 * (lane + 64 * j);
+            if (k + 1 < e) {
+                v[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const double2*>(A.va + k));
+                cc[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const int2*>(A.ci + k));
+            } else if (k < e) {
+                v[j] = make_double2(A.va[k], 0.0);
+                cc[j] = make_int2(A.ci[k], 0);
+            } else {
+                v[j] = make_double2(0.0, 0.0);
+                cc[j] = make_int2(0, 0);
+            }
+        }
+    };
+    int b = g * SEGS;
+    int32_t ra = 0, rb = 0;
+    while (b < b_end && !seg(b, ra, rb)) ++b;
+    if (b >= b_end) return;   // waves are independent: no workgroup barrier below
+    int32_t s = A.rp[ra], e = A.rp[rb];
+    load_chunk(s & ~1, e);
+    bool staged = false;      // LDS holds an earlier chunk whose reads must finish before the next store
+    for (;;) {
+        const int32_t r = ra + lane;
+        const bool live = r < rb;
+        int32_t ks = 0, ke = 0;
+        typename Epi::P pe{};
+        if (live) {
+            ks = A.rp[r];
+            ke = A.rp[r + 1];
+            pe = epi.pre(r);
+        }
+        int nb = b + 1;
+        int32_t nra = 0, nrb = 0;
+        while (nb < b_end && !seg(nb, nra, nrb)) ++nb;
+        const bool more = nb < b_end;
+        int32_t ns = 0, ne = 0;
+        if (more) {
+            ns = A.rp[nra];
+            ne = A.rp[nrb];
+        }
+        double acc = 0.0;
+        if (s >= e && more) load_chunk(ns & ~1, ne);   // rows all empty: no chunk, prefetch right away
+        for (int32_t cb = s & ~1; cb < e; cb += kWaveCap) {
+            if (cb != (s & ~1)) load_chunk(cb, e);   // further chunks of long rows: loaded in place
+            if (staged) wave_lds_sync();
+            staged = true;
+#pragma unroll
+            for (int j = 0; j < kWavePairs; ++j) {
+                vs[lane + 64 * j] = v[j];
+                cs[lane + 64 * j] = cc[j];
+            }
+            wave_lds_sync();
+            if (more && cb + kWaveCap >= e) load_chunk(ns & ~1, ne);   // prefetch the next block's chunk
+            int32_t t = max(ks, cb) - cb;
+            const int32_t tend = min(ke, cb + kWaveCap) - cb;
+            if ((t & 1) && t < tend) {
+                acc += vs1[t] * x[cs1[t]];
+                ++t;
+            }
+            for (; t < tend; t += 2 * kRowBatchPf) {
+                const int32_t p0 = t >> 1;
+                int2 c[kRowBatchPf];
+                double x0[kRowBatchPf], x1[kRowBatchPf];
+#pragma unroll
+                for (int i = 0; i < kRowBatchPf; ++i) c[i] = (t + 2 * i < tend) ? cs[p0 + i] : make_int2(0, 0);
+#pragma unroll
+                for (int i = 0; i < kRowBatchPf; ++i) {
+                    x0[i] = (t + 2 * i < tend) ? x[c[i].x] : 0.0;
+                    x1[i] = (t + 2 * i + 1 < tend) ? x[c[i].y] : 0.0;
+                }
+#pragma unroll
+                for (int i = 0; i < kRowBatchPf; ++i) {
+                    if (t + 2 * i < tend) {
+                        const double2 q = vs[p0 + i];
+                        acc += q.x * x0[i];
+                        if (t + 2 * i + 1 < tend) acc += q.y * x1[i];
+                    }
+                }
+            }
+        }
+        if (live) epi.template apply<MPBP_CSR_NT != 0>(r, acc, pe);
+        if (!more) break;
+        b = nb;
+        ra = nra;
+        rb = nrb;
+        s = ns;
+        e = ne;
+    }
 }
 
 // ------------------------------------------------------------------ SELL-64 ----
@@ -2017,7 +2146,10 @@ inline Csr to_csr(const mpbp_csr* A) { return Csr{A->row_ptr, A->col_idx, A->val
 template <class Epi>
 int launch_rows(const mpbp_csr* A, const mpbp_rowblocks* blk, const double* x, Epi epi, hipStream_t st) {
     if (!blk || blk->count <= 0) return MPBP_OK;
-    if (g_csr_kind == 1)
+    if (g_csr_kind == 2)
+        k_csr_wave_pf<Epi, MPBP_CSR_SEGS><<<(blk->count + MPBP_CSR_SEGS - 1) / MPBP_CSR_SEGS, kBlock, 0, st>>>(
+            to_csr(A), x, reinterpret_cast<const int2*>(blk->pairs), blk->count, epi);
+    else if (g_csr_kind == 1)
         k_csr_wave<Epi><<<blk->count, kBlock, 0, st>>>(to_csr(A), x, reinterpret_cast<const int2*>(blk->pairs),
                                                         blk->count, epi);
     else
@@ -2083,7 +2215,9 @@ int mpbp_set_pressure_solve_fusion(int32_t rows) {
     return MPBP_OK;
 }
 int mpbp_set_csr_kernel(int32_t kind) {
-    if (kind < 0 || kind > 1) return set_error(MPBP_ERR_ARG, "csr kernel must be 0 (workgroup-staged) or 1 (per-wave)");
+    if (kind < 0 || kind > 2)
+        return set_error(MPBP_ERR_ARG, "csr kernel must be 0 (workgroup-staged), 1 (per-wave) or 2 (per-wave, "
+                                       "prefetching, several row blocks per workgroup)");
     g_csr_kind = kind;
     return MPBP_OK;
 }

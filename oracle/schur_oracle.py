@@ -101,3 +101,37 @@ def approx_schur_apply(F, D, G, GtG, GtFG, v, inner_F: Inner, inner_P: Inner,
     G_xp = co.spmv(G, x_p)
     u = inner_solve(F, diag_F, inner_F, G_xp, sub=Finv_v, dense_inv=F_inv)
     return np.concatenate([u, x_p])
+
+
+def _inner_solve_scipy(M, diag, inner: Inner, b, sub=None):
+    """inner_solve with scipy.sparse products and numpy vector updates (the reference's own CPU form:
+    solve.py:149-159 Jacobi, `A @ x` on scipy CSR); same recurrences and coefficients as inner_solve."""
+    K = inner.sweeps
+    if inner.kind == "jacobi":
+        x = b / diag
+        for _ in range(1, K):
+            x = x + (b - M @ x) / diag
+    elif inner.kind == "chebyshev":
+        c1, c2 = cheb_coeffs(inner.lmin, inner.lmax, K)
+        d = c2[0] * (b / diag)
+        x = d
+        for s in range(1, K):
+            d = c1[s] * d + c2[s] * ((b - M @ x) / diag)
+            x = x + d
+    else:
+        raise ValueError(inner.kind)
+    return x if sub is None else sub - x
+
+
+def approx_schur_apply_scipy(F, D, G, GtG, GtFG, v, inner_F: Inner, inner_P: Inner, diag_F, diag_P):
+    """approx_schur_op (solve.py:257-277) composed from scipy.sparse `@` products, as the reference runs
+    it on the CPU.  Used only as bench.py's reported CPU baseline (scipy's summation may contract
+    differently from the C restatement: compared within 1e-12, not bit for bit)."""
+    nu = F.shape[0]
+    Finv_v = _inner_solve_scipy(F, diag_F, inner_F, v[:nu])
+    rhs = D @ Finv_v + v[nu:]
+    x_a = _inner_solve_scipy(GtG, diag_P, inner_P, rhs)
+    x_b = GtFG @ x_a
+    x_p = _inner_solve_scipy(GtG, diag_P, inner_P, x_b)
+    u = _inner_solve_scipy(F, diag_F, inner_F, G @ x_p, sub=Finv_v)
+    return np.concatenate([u, x_p])

@@ -116,9 +116,10 @@ def test_spgemm_bit_exact(n):
     _same_csr(mp.spgemm(F, G, alpha=2.5), co.spgemm(osys.F, osys.G, alpha=2.5))
 
 
-@pytest.fixture(params=[1, 0], ids=["csr_wave", "csr_block"])
+@pytest.fixture(params=[1, 2, 0], ids=["csr_wave", "csr_wave_pf", "csr_block"])
 def csr_kernel(request):
-    """Both CSR SpMV kernels (mpbp_set_csr_kernel): per-wave chunks (default) and 256-row LDS stages."""
+    """Every CSR SpMV kernel (mpbp_set_csr_kernel): per-wave chunks (default), per-wave chunks over several
+    row blocks with prefetch, and 256-row LDS stages."""
     from mp_block_preconditioners_amd._lib import check, lib
     check(lib().mpbp_set_csr_kernel(request.param))
     yield request.param
@@ -184,7 +185,7 @@ def test_spmv_long_rows_and_empty_rows(csr_kernel):
     ref = M @ x
     assert rel_inf(y, ref) <= 1e-13
     assert y[0] == 0.0 and y[10] == 0.0
-    if csr_kernel == 1:
+    if csr_kernel in (1, 2):
         assert _bits_equal(y, co.spmv(M, x))
 
 

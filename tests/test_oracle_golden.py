@@ -105,3 +105,22 @@ def test_schur_apply_exact_inverses(case, oracle_built):
     out = approx_schur_apply(s.F, s.D, s.G, s.GtG, s.GtFG, g["v"], Inner("exact"), Inner("exact"),
                              F_inv=lambda r: np.linalg.solve(Fd, r), GtG_inv=lambda r: Pinv @ r)
     assert rel_inf(out, g["schur_exact"]) <= 1e-8
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if "n32" not in c])
+def test_scipy_form_matches_oracle(case, oracle_built):
+    """bench.py's scipy-form CPU baseline (scipy.sparse products) computes the oracle's apply, and the
+    Jacobi case matches the reference's own composition fixture."""
+    from oracle.schur_oracle import Inner, approx_schur_apply, approx_schur_apply_scipy, diagonal, gershgorin
+    g = load_golden(os.path.join(os.path.dirname(__file__), "golden", case))
+    s = _system(g)
+    dF, dP = diagonal(s.F), diagonal(s.GtG)
+    lf, lp = gershgorin(s.F, dF), gershgorin(s.GtG, dP)
+    for iF, iP in ((Inner("jacobi", 3), Inner("jacobi", 2)),
+                   (Inner("chebyshev", 4, lf / 30, lf), Inner("chebyshev", 4, lp / 30, lp))):
+        ref = approx_schur_apply(s.F, s.D, s.G, s.GtG, s.GtFG, g["v"], iF, iP)
+        out = approx_schur_apply_scipy(s.F, s.D, s.G, s.GtG, s.GtFG, g["v"], iF, iP, dF, dP)
+        assert rel_inf(out, ref) <= 1e-12, iF.kind
+    out = approx_schur_apply_scipy(s.F, s.D, s.G, s.GtG, s.GtFG, g["v"], Inner("jacobi", 3), Inner("jacobi", 2),
+                                   dF, dP)
+    assert rel_inf(out, g["schur_jacobi_3_2"]) <= 1e-11

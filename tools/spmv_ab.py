@@ -33,7 +33,8 @@ def main():
     nbytes = A.nnz * 12 + (A.shape[0] + 1) * 4 + (A.shape[0] + A.shape[1]) * 8 + A.blocks.count * 8
     res = {"n": args.n, "nnz": A.nnz, "lib": os.environ.get("MPBP_LIB", "default")}
     flat = A.plan_blocks(groups=1)   # blocks in plain row order (no per-field interleave)
-    for name, M, kind, blk in (("csr_wave", A, 1, None), ("csr_wave_roworder", A, 1, flat), ("csr_block", A, 0, None),
+    for name, M, kind, blk in (("csr_wave", A, 1, None), ("csr_wave_pf", A, 2, None), ("csr_wave_roworder", A, 1, flat),
+                               ("csr_block", A, 0, None),
                                ("sell", AS, 1, None)):
         check(lib().mpbp_set_csr_kernel(kind))
         kw = {"blocks": blk} if blk is not None else {}
