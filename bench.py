@@ -218,6 +218,22 @@ def main():
         except (OSError, ValueError, KeyError):
             traffic = None
 
+    # the LinearOperator boundary with host buffers (solve.py:281: pyamg on the host hands M a numpy
+    # vector): H2D of v + apply + D2H of the result per call.  Reported beside `value`, never as it.
+    host_io = None
+    if rank == 0 and not partitioned:
+        vh = v.cpu().numpy()
+        pc.matvec(vh)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        reps = 10
+        for _ in range(reps):
+            pc.matvec(vh)
+        el = time.perf_counter() - t0
+        host_io = {"value": reps / el, "unit": "applies/s",
+                   "note": f"ApproxSchurPreconditioner.matvec on a host ndarray ({vh.nbytes / 1e6:.0f} MB in and "
+                           "out over PCIe per call, pageable memory), eager apply; wall clock over 10 calls"}
+
     cpu = None
     if rank == 0 and not partitioned and not args.no_cpu_baseline:
         cpu = cpu_baseline(pc, v, args.cpu_seconds, kf, sf, kp, spp)
@@ -269,6 +285,7 @@ def main():
                 "kernel": "k_csr_wave<EpiStore> (A u, 5N rows, CSR)", "bytes_per_launch": spmv["csr_bytes"],
                 "avg_launch_us": spmv["csr_us"],
                 "timing": "HIP events around 20 back-to-back launches (one kernel per matvec)"},
+            "host_buffer_matvec": host_io,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -455,6 +455,7 @@ struct Csr {
     const int32_t* rp;
     const int32_t* ci;
     const double* va;
+    int32_t ncols = 0;   // set by to_csr (the uniform CSR path's x buffer descriptor); 0 = unknown
 };
 
 constexpr int kSpgemmMaxW = 64;
@@ -805,6 +806,65 @@ __device__ inline void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// A wave whose 64 rows all hold LEN entries (stencil operators: A's velocity rows 12, pressure rows 8,
+// F's rows 10) from an even start: its entries are exactly one chunk, lane l's row is pairs
+// [l*LEN/2, (l+1)*LEN/2) of it, so the loads, LDS transposition, gathers and sums unroll with no
+// per-entry bounds tests.  Same additions in the same order as the general loop (bit-exact).
+#ifndef MPBP_CSR_UNIFORM
+#define MPBP_CSR_UNIFORM 1
+#endif
+#ifndef MPBP_CSR_XBUF
+#define MPBP_CSR_XBUF 1
+#endif
+// XB: x gathered with buffer loads (one descriptor for x, a 32-bit byte offset per entry: no 64-bit
+// address arithmetic per gather); needs ncols * 8 < 2^31.
+template <int LEN, bool XB>
+__device__ inline double csr_wave_uniform(const Csr& A, const double* __restrict__ x, int32_t s, int lane,
+                                          double2* vs, int2* cs) {
+    constexpr int P = LEN / 2;   // pairs per row == 16-byte loads per lane
+    double2 v[P];
+    int2 cc[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const int32_t k = s + 2 * (lane + 64 * j);
+        v[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const double2*>(A.va + k));
+        cc[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const int2*>(A.ci + k));
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        vs[lane + 64 * j] = v[j];
+        cs[lane + 64 * j] = cc[j];
+    }
+    wave_lds_sync();
+    const int p0 = lane * P;
+    int2 c[P];
+#pragma unroll
+    for (int i = 0; i < P; ++i) c[i] = cs[p0 + i];
+    double x0[P], x1[P];
+    if constexpr (XB) {
+        const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(x), (short)0, A.ncols * 8, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+            x0[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, c[i].x * 8, 0, 0));
+            x1[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, c[i].y * 8, 0, 0));
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+            x0[i] = x[c[i].x];
+            x1[i] = x[c[i].y];
+        }
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+        const double2 q = vs[p0 + i];
+        acc += q.x * x0[i];
+        acc += q.y * x1[i];
+    }
+    return acc;
+}
+
 template <class Epi>
 __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __restrict__ x,
                                                      const int2* __restrict__ blocks, int nblocks,
@@ -832,6 +892,25 @@ __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __rest
     double acc = 0.0;
     double2* vs = vstage[w];
     const double* vs1 = reinterpret_cast<const double*>(vs);
+#if MPBP_CSR_TGATHER && MPBP_CSR_UNIFORM
+    {
+        const int32_t len = (e - s) >> 6;   // wave-uniform
+        if (rb - ra == 64 && ((e - s) & 63) == 0 && (s & 1) == 0 && (len == 8 || len == 10 || len == 12) &&
+            __all(ke - ks == len)) {
+            constexpr bool XB = MPBP_CSR_XBUF != 0;
+            if (XB && A.ncols > 0 && A.ncols < (1 << 28))
+                acc = len == 12 ? csr_wave_uniform<12, XB>(A, x, s, lane, vs, cstage[w])
+                                : (len == 10 ? csr_wave_uniform<10, XB>(A, x, s, lane, vs, cstage[w])
+                                             : csr_wave_uniform<8, XB>(A, x, s, lane, vs, cstage[w]));
+            else
+                acc = len == 12 ? csr_wave_uniform<12, false>(A, x, s, lane, vs, cstage[w])
+                                : (len == 10 ? csr_wave_uniform<10, false>(A, x, s, lane, vs, cstage[w])
+                                             : csr_wave_uniform<8, false>(A, x, s, lane, vs, cstage[w]));
+            epi.template apply<MPBP_CSR_NT != 0>(r, acc, pe);   // every lane holds a row here
+            return;
+        }
+    }
+#endif
     for (int32_t cb = s & ~1; cb < e; cb += kWaveCap) {
         double2 v[kWavePairs];
         int2 cc[kWavePairs];
@@ -2141,7 +2220,7 @@ __global__ void k_cheb_init(int32_t n, const double* b, const double* diag, doub
     xout[r] = sub ? sub[r] - dn : dn;
 }
 
-inline Csr to_csr(const mpbp_csr* A) { return Csr{A->row_ptr, A->col_idx, A->val}; }
+inline Csr to_csr(const mpbp_csr* A) { return Csr{A->row_ptr, A->col_idx, A->val, A->ncols}; }
 
 template <class Epi>
 int launch_rows(const mpbp_csr* A, const mpbp_rowblocks* blk, const double* x, Epi epi, hipStream_t st) {

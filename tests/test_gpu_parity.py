@@ -371,3 +371,24 @@ def test_exclusive_scan_overflow():
     total = ctypes.c_int64(0)
     rc = lib().mpbp_exclusive_scan(ptr(cnt), ptr(out), 5000, ctypes.byref(total), stream_handle())
     assert rc == -3 and b"exceed int32" in lib().mpbp_last_error()
+
+
+@pytest.mark.parametrize("start_odd", [False, True])
+def test_csr_wave_uniform_waves_bit_exact(start_odd):
+    """k_csr_wave's uniform-wave path (64 rows of 8, 10 or 12 entries from an even start: unrolled,
+    buffer-load gathers) next to waves it must not take (length 14, mixed lengths, a partial wave, an odd
+    start); every epilogue mode bit-exact vs the oracle."""
+    mp = _mp()
+    from oracle import csr_oracle as co
+    rng = np.random.default_rng(5 + start_odd)
+    segs = [np.full(64, 12), np.full(64, 10), np.full(64, 8), np.full(64, 14),
+            rng.integers(6, 13, size=64), np.full(64, 12), np.full(30, 12)]
+    lengths = np.concatenate(([1] if start_odd else []) + segs).astype(np.int64)
+    rows = np.repeat(np.arange(lengths.size), lengths)
+    cols = np.concatenate([np.sort(rng.choice(5000, size=k, replace=False)) for k in lengths])
+    M = sp.csr_matrix((rng.standard_normal(rows.size), cols, np.r_[0, np.cumsum(lengths)]),
+                      shape=(lengths.size, 5000))
+    x, z = rng.standard_normal(5000), rng.standard_normal(lengths.size)
+    dM = mp.DeviceCSR.from_scipy(M)
+    for mode in (0, 1, 2):
+        assert _bits_equal(dM.matvec(_cuda(x), mode=mode, z=_cuda(z)), co.spmv(M, x, z, mode=mode)), mode
