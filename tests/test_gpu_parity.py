@@ -383,7 +383,7 @@ def test_csr_wave_uniform_waves_bit_exact(start_odd):
     rng = np.random.default_rng(5 + start_odd)
     segs = [np.full(64, 12), np.full(64, 10), np.full(64, 8), np.full(64, 14),
             rng.integers(6, 13, size=64), np.full(64, 12), np.full(30, 12)]
-    lengths = np.concatenate(([1] if start_odd else []) + segs).astype(np.int64)
+    lengths = np.concatenate(([np.array([1])] if start_odd else []) + segs).astype(np.int64)
     rows = np.repeat(np.arange(lengths.size), lengths)
     cols = np.concatenate([np.sort(rng.choice(5000, size=k, replace=False)) for k in lengths])
     M = sp.csr_matrix((rng.standard_normal(rows.size), cols, np.r_[0, np.cumsum(lengths)]),
