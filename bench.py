@@ -232,7 +232,7 @@ def main():
         el = time.perf_counter() - t0
         host_io = {"value": reps / el, "unit": "applies/s",
                    "note": f"ApproxSchurPreconditioner.matvec on a host ndarray ({vh.nbytes / 1e6:.0f} MB in and "
-                           "out over PCIe per call, pageable memory), eager apply; wall clock over 10 calls"}
+                           "out over PCIe per call through page-locked staging buffers), eager apply; wall clock over 10 calls"}
 
     cpu = None
     if rank == 0 and not partitioned and not args.no_cpu_baseline:

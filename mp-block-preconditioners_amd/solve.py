@@ -241,8 +241,22 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
         return _capture(self, v, out)
 
     def _matvec(self, x):
-        v = torch.from_numpy(np.ascontiguousarray(np.ravel(x), dtype=np.float64)).to(self.device)
-        return self.apply(v).cpu().numpy()
+        """Host vector in, host vector out (the LinearOperator surface pyamg drives, solve.py:281): staged
+        through page-locked buffers allocated on first use, so both PCIe copies run at DMA speed."""
+        x = np.ravel(x)
+        n = self.nu + self.np
+        if getattr(self, "_pinned", None) is None:
+            self._pinned = (torch.empty(n, dtype=torch.float64, pin_memory=True),
+                            torch.empty(n, dtype=torch.float64, pin_memory=True),
+                            torch.empty(n, dtype=torch.float64, device=self.device),
+                            torch.empty(n, dtype=torch.float64, device=self.device))
+        h_in, h_out, d_in, d_out = self._pinned
+        h_in.numpy()[:] = x
+        d_in.copy_(h_in, non_blocking=True)
+        self.apply(d_in, d_out)
+        h_out.copy_(d_out, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        return h_out.numpy().copy()
 
     # reference naming (solve.py:257)
     def approx_schur_op(self, v):

@@ -263,7 +263,10 @@ def test_schur_apply_bit_exact(n, inner, layout):
     got = pc.apply(_cuda(v))
     ref = approx_schur_apply(osys.F, osys.D, osys.G, osys.GtG, osys.GtFG, v, iF, iP)
     assert _bits_equal(got, ref), rel_inf(got.cpu().numpy(), ref)
-    assert np.array_equal(pc.matvec(v), got.cpu().numpy())           # LinearOperator surface
+    m1 = pc.matvec(v)
+    assert np.array_equal(m1, got.cpu().numpy())                      # LinearOperator surface
+    m2 = pc.matvec(list(2.0 * v))                                      # staging buffers reused, results not aliased
+    assert np.array_equal(m1, got.cpu().numpy()) and np.array_equal(m2, pc.apply(_cuda(2.0 * v)).cpu().numpy())
 
 
 @pytest.mark.parametrize("path", [p for p in golden_files() if "n32" not in p], ids=os.path.basename)
