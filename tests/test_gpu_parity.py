@@ -143,6 +143,9 @@ def test_spmv_bit_exact(n, csr_kernel):
             assert _bits_equal(y, ref), (M.shape, mode)
             y = dS.matvec(_cuda(x), mode=mode, z=_cuda(z))
             assert _bits_equal(y, ref), ("sell", M.shape, mode)
+        h1 = dM @ x                                   # host vector in / out (page-locked staging)
+        h2 = dM @ (2.0 * x)
+        assert np.array_equal(h1, co.spmv(M, x)) and np.array_equal(h2, co.spmv(M, 2.0 * x))
 
 
 def test_sell_ragged_rows_and_partial_slices():
