@@ -1,16 +1,17 @@
-"""Benchmark: preconditioner applies per second on the 1024^2 multiphase-Stokes system (BASELINE.json
-configs[2]) on MI355X, with the roofline of the dominant kernel and the CPU oracle timed beside it.
+"""Benchmark: preconditioner applies per second on the multiphase-Stokes system on MI355X, with the roofline
+of the dominant kernel and the CPU oracle timed beside it.
 
 One step = one application of the approximate-commutator block preconditioner (solve.py:257-277,
 ``mpbp_schur_apply``) to a resident random vector of 5 n^2 doubles.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 1024] [--strong] ...
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--grid n] [--weak] ...
 
-N > 1 is launched by torch.distributed.run (one rank per GPU, RCCL).  The grid is row-partitioned
-over the ranks with halo all-gathers between sweeps.  Default is weak scaling: the global grid is
-n_N = round(n * sqrt(N)) so every GPU holds ~n^2 cells, and `value` counts applies of the global
-system scaled to 1024^2-cell equivalents (n_N^2 / 1024^2 per apply; exactly applies/s at N = 1).
---strong keeps the global grid at n.  Rank 0 prints ONE JSON line.
+N = 1: BASELINE configs[2], the 1024^2 grid on one GPU.  N > 1: BASELINE configs[4], the 2048^2 grid row-
+partitioned over N ranks (one per GPU, RCCL point-to-point halos).  `python bench.py --gpus N` launches the N
+ranks itself (a torch.distributed.run child process started before anything touches the GPU); under an
+external launcher (WORLD_SIZE set) --gpus must equal WORLD_SIZE.  `value` counts applies of the global system
+in 1024^2-cell equivalents (applies/s x n^2 / 1024^2: exactly applies/s at N = 1), so the N = 1 and N > 1
+lines share a unit.  --weak instead grows the grid as n = round(1024 sqrt(N)).  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -69,11 +70,15 @@ def sweep_bytes(pc, layout, kind, sweeps, fused_init):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default WORLD_SIZE or 1.  Without WORLD_SIZE, N > 1 launches N ranks")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--grid", "--grid-n", dest="n", type=int, default=1024, help="grid size n (n x n cells)")
-    ap.add_argument("--strong", action="store_true", help="keep the global grid at n for every N")
+    ap.add_argument("--grid", "--grid-n", dest="n", type=int, default=None,
+                    help="global grid size n (n x n cells); default 1024 at N = 1 (configs[2]), 2048 at N > 1 "
+                         "(configs[4])")
+    ap.add_argument("--weak", action="store_true", help="weak scaling: global grid round(1024 sqrt(N))")
+    ap.add_argument("--strong", action="store_true", help="(kept for old command lines) same as the default")
     ap.add_argument("--xi", type=float, default=1.0)
     ap.add_argument("--eta-n", type=float, default=100.0)
     ap.add_argument("--eta-s", type=float, default=1.0)
@@ -102,7 +107,16 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-spmv", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch the apply eagerly instead of a hipGraph")
+    ap.add_argument("--no-check", action="store_true", help="N > 1: skip the bit-exact check against one GPU")
     args = ap.parse_args()
+
+    # --gpus N > 1 without a launcher: start the N ranks as a child process BEFORE anything touches the GPU
+    # (torch is not even imported yet) and exit with its status; never re-exec this process
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        return launch_ranks(args.gpus)
+    if env_world is not None and args.gpus is not None and int(env_world) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={env_world} set by the launcher")
 
     import torch
     import torch.distributed as dist
@@ -113,7 +127,11 @@ def main():
     # MPBP_BENCH_BACKEND=gloo rehearses the N > 1 path with several ranks on one GPU (ghosts staged
     # through host memory); the measured configuration is RCCL ("nccl"), one GPU per rank.
     backend = os.environ.get("MPBP_BENCH_BACKEND", "nccl")
-    dev_index = local % max(1, torch.cuda.device_count())
+    ndev = torch.cuda.device_count()
+    if world > 1 and backend == "nccl" and ndev < world:
+        raise SystemExit(f"bench.py: {world} RCCL ranks need {world} GPUs, this node shows {ndev} "
+                         "(MPBP_BENCH_BACKEND=gloo rehearses several ranks on one GPU)")
+    dev_index = local % max(1, ndev)
     torch.cuda.set_device(dev_index)
     if world > 1:
         if backend == "nccl":
@@ -132,7 +150,10 @@ def main():
     _check(_lib().mpbp_set_sweep_fusion(args.sweep_fusion))
     _check(_lib().mpbp_set_pressure_solve_fusion(args.p_fusion))
 
-    n = args.n if (world == 1 or args.strong) else int(round(args.n * math.sqrt(world)))
+    if args.weak:
+        n = int(round((args.n or 1024) * math.sqrt(world)))
+    else:
+        n = args.n or (1024 if world == 1 else 2048)
     kf, sf = parse_inner(args.inner_f)
     kp, spp = parse_inner(args.inner_p)
     iF, iP = mp.InnerSolver(kf, sf), mp.InnerSolver(kp, spp)
@@ -154,11 +175,11 @@ def main():
     out = torch.empty_like(v)
     torch.cuda.synchronize()
 
-    # One GPU: the apply is captured once into a hipGraph and replayed (22 launches -> 1).  The
-    # F-sweep durations for the roofline come from HIP events recorded around every F sweep by
-    # mpbp_schur_apply on the same stream during an eager pass of the same K applies right after the
-    # timed loop (events are not recorded inside a graph).  N > 1 runs eagerly (halo callbacks), with
-    # the events inside the timed loop itself.
+    # One GPU: the apply is captured once into a hipGraph and replayed (22 launches -> 1).  N > 1 launches
+    # eagerly (the halo exchanges are RCCL groups issued from inside mpbp_schur_apply).  The timed loop
+    # records no events; the F-sweep durations for the roofline come from HIP events that
+    # mpbp_schur_apply records around every F sweep on the apply stream, in an eager pass of the same K
+    # applies right after the timed loop.
     sweeps_per_apply = 2 * max(sf - 1, 0)
     graph, graph_note = None, None
     if not partitioned and not args.no_graph:
@@ -168,8 +189,6 @@ def main():
             graph, graph_note = None, f"graph capture failed: {e}"
     for _ in range(args.warmup):
         graph.replay() if graph is not None else pc.apply(v, out)
-    pc.enable_profiling(max(1, args.steps * sweeps_per_apply))
-    pc.reset_profiling()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -184,12 +203,20 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    if graph is not None:
-        for _ in range(args.steps):
-            pc.apply(v, out)
-        torch.cuda.synchronize()
+    pc.enable_profiling(max(1, args.steps * sweeps_per_apply))
+    pc.reset_profiling()
+    for _ in range(args.steps):
+        pc.apply(v, out)
+    torch.cuda.synchronize()
     sweep_ms = pc.profiled_ms()
     pc.disable_profiling()
+
+    # N > 1: every rank compares its rows of the partitioned apply with the one-GPU apply of the global
+    # system (built on its own GPU from the same operators), bit for bit; plus an order-free checksum of
+    # the global output (sum of the results' bit patterns mod 2^64) that the gloo rehearsal can match
+    single = None
+    if world > 1 and not args.no_check:
+        single = single_gpu_check(pc, n, args, iF, iP, rank, dist, torch)
 
     # dominant kernel: the fused Chebyshev-Jacobi sweep over F
     fused_init = not partitioned and getattr(pc, "f_stencil", None) is not None and sk.startswith("march")
@@ -240,22 +267,24 @@ def main():
 
     if rank == 0:
         scale = n * n / float(1024 * 1024)
-        value = args.steps / dt * (1.0 if args.strong else scale)
+        value = args.steps / dt * scale
+        cfg = "configs[2]" if (world == 1 and n == 1024) else "configs[4]" if n == 2048 else "custom grid"
         line = {
             "metric": "precond-applies/sec",
             "value": value,
-            "unit": "applies/s" if (world == 1 or args.strong) else "applies/s (1024^2-cell equivalents)",
+            "unit": "applies/s (1024^2-cell equivalents)",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
+            "scaling": "weak" if args.weak else "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: reference operator (thn = 0.25 sin sin + 0.5), random input vector",
-            "config": {"workload": f"{n}x{n} MAC grid, approx-commutator Schur preconditioner apply "
-                                   "(BASELINE configs[2]" + (")" if world == 1 else ", row-partitioned)"),
+            "config": {"workload": f"{n}x{n} MAC grid, approx-commutator Schur preconditioner apply (BASELINE "
+                                   f"{cfg}" + (")" if world == 1 else f", rows partitioned over {world} ranks)"),
+                       "applies_per_s_of_this_grid": args.steps / dt,
                        "n": n, "unknowns": 5 * n * n, "xi": args.xi, "eta_n": args.eta_n,
                        "eta_s": args.eta_s, "inner_F": f"{kf}:{sf}", "inner_P": f"{kp}:{spp}",
                        "parallelism": f"rows{world}" if world > 1 else "single", "layout": args.layout,
@@ -269,14 +298,15 @@ def main():
                                              f"{pc.h_u} (velocity) / {pc.h_p} (pressure)") if pc.ca
                            else "one exchange per sweep"}
                           if partitioned else {}),
+                       **({"backend": backend} if world > 1 else {}),
                        **({"note": graph_note} if graph_note else {})},
+            **({"bit_exact_vs_single_gpu": single["bit_exact"], "single_gpu_check": single} if single else {}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
                          "bytes_per_launch": sbytes, "avg_launch_us": avg_sweep_s * 1e6,
                          "launches_timed": len(sweep_ms),
                          "timing": "HIP events around each F sweep on the apply stream"
-                                   + (", eager pass of the same K applies after the graph-timed loop"
-                                      if graph is not None else ", inside the timed loop")},
+                                   + ", eager pass of the same K applies after the timed loop"},
             "spmv_A": spmv,
             # north_star's CSR SpMV target: the plain A u product (apply.py:72) on the scipy CSR arrays
             "roofline_csr_spmv": None if spmv is None else {
@@ -292,6 +322,46 @@ def main():
     if partitioned:
         pc.close()
         dist.destroy_process_group()
+
+
+def launch_ranks(n_ranks):
+    """Run this command line as n_ranks torch.distributed.run ranks (127.0.0.1 rendezvous) in a child process
+    and return its exit status.  Called before torch is imported: the parent never touches the GPU."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n_ranks}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd)
+
+
+def single_gpu_check(dpc, n, args, iF, iP, rank, dist, torch):
+    """The partitioned apply of a global random vector against the one-GPU apply (every rank, its rows)."""
+    import numpy as np
+    import mp_block_preconditioners_amd as mp
+    t0 = time.perf_counter()
+    bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, layout=args.layout, f_mode=args.f_mode,
+                                      pg_mode=args.pg_mode)
+    del F, D, G
+    vg = torch.from_numpy(np.random.default_rng(2048).standard_normal(pc.shape[0])).cuda()
+    gids = torch.from_numpy(dpc.local_to_global_rows()).cuda()
+    ref = pc.apply(vg)[gids]
+    got = dpc.apply(vg[gids].contiguous())
+    torch.cuda.synchronize()
+    same = torch.tensor([1 if torch.equal(got, ref) else 0], dtype=torch.int64, device="cuda")
+    csum = got.view(torch.int64).sum().reshape(1)
+    dist.all_reduce(same, op=dist.ReduceOp.MIN)
+    dist.all_reduce(csum, op=dist.ReduceOp.SUM)
+    ok = bool(same.item())
+    del pc
+    torch.cuda.empty_cache()
+    return {"bit_exact": ok, "output_bits_sum_mod_2^64": int(csum.item()) & (2 ** 64 - 1),
+            "note": "every rank's rows of the partitioned apply vs the single-GPU apply of the same global "
+                    f"vector (numpy seed 2048), built on each rank's GPU; {time.perf_counter() - t0:.1f} s"}
 
 
 def spmv_bench(A, gen, reps=20):
@@ -364,4 +434,4 @@ def cpu_baseline(pc, v, seconds, kf, sf, kp, spp):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

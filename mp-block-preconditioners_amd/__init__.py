@@ -7,12 +7,12 @@ from .csr import DeviceCSR, DeviceSELL, spgemm
 from .preconditioner import MultiphaseBlockPreconditioner, thn, ths
 from .solve import (ApproxSchurPreconditioner, InnerSolver, fgmres, print_true_res_norm,
                     solve_with_approx_schur_pc, solve_without_pc)
-from .utils import (fill_sol_and_RHS_vecs, manufactured_problem, max_norm, print_norms, weighted_L1,
+from .utils import (fill_sol_and_RHS_vecs, manufactured_problem, manufactured_problem_constant, max_norm, print_norms, weighted_L1,
                     weighted_L2)
 
 __all__ = [
     "MpbpError", "lib", "DeviceCSR", "DeviceSELL", "spgemm", "MultiphaseBlockPreconditioner", "thn", "ths",
     "ApproxSchurPreconditioner", "InnerSolver", "fgmres", "print_true_res_norm",
-    "solve_with_approx_schur_pc", "solve_without_pc", "fill_sol_and_RHS_vecs", "manufactured_problem", "max_norm",
+    "solve_with_approx_schur_pc", "solve_without_pc", "fill_sol_and_RHS_vecs", "manufactured_problem", "manufactured_problem_constant", "max_norm",
     "print_norms", "weighted_L1", "weighted_L2",
 ]

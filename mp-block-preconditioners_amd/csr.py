@@ -127,20 +127,15 @@ class DeviceCSR:
 
     def _host_matvec(self, x: np.ndarray) -> np.ndarray:
         """A @ x for a host vector (apply.py:72 on host data; a host-side Krylov loop's operator): staged
-        through page-locked buffers allocated on first use, so both PCIe copies run at DMA speed."""
-        if getattr(self, "_pinned", None) is None:
-            m, k = self.shape
-            self._pinned = (torch.empty(k, dtype=torch.float64, pin_memory=True),
-                            torch.empty(m, dtype=torch.float64, pin_memory=True),
-                            torch.empty(k, dtype=torch.float64, device=self.device),
-                            torch.empty(m, dtype=torch.float64, device=self.device))
-        h_in, h_out, d_in, d_out = self._pinned
-        h_in.numpy()[:] = x
-        d_in.copy_(h_in, non_blocking=True)
-        self.matvec(d_in, out=d_out)
-        h_out.copy_(d_out, non_blocking=True)
-        torch.cuda.current_stream(self.device).synchronize()
-        return h_out.numpy().copy()
+        through page-locked buffers allocated on first use, so both PCIe copies run at DMA speed.  x must
+        have exactly ncols entries (scipy's dimension check); one call at a time (a lock serialises threads)."""
+        from .solve import _staged_host_call
+        return _staged_host_call(self, x, self.shape[1], self.shape[0], self.device,
+                                 lambda d_in, d_out: self.matvec(d_in, out=d_out))
+
+    def release_staging(self):
+        """Free the host-vector matvec's staging buffers (re-created on demand)."""
+        self._pinned = None
 
     def diagonal(self, col_offset=0) -> torch.Tensor:
         d = torch.empty(self.shape[0], dtype=torch.float64, device=self.device)

@@ -8,7 +8,7 @@
 //   send own rows [r0+L-h, r0+L) of every field  -> down (= rank k+1, periodic): its rows above
 //   recv the rows below <- down,  recv the rows above <- up
 // A one-field vector sends its rows in place; a four-field one first gathers them (mpbp_gather, one
-// kernel) into [top rows of every field | bottom rows of every field].  Per peer pair the operations
+// kernel, launched before the group opens) into [top rows of every field | bottom rows of every field].  Per peer pair the operations
 // are matched in issue order, so every rank issues them in the same order (send up, send down, recv
 // down, recv up), which also covers world = 2 (up == down) and world = 1 (the wrap onto itself).
 //
@@ -202,37 +202,51 @@ void mpbp_halo_destroy(mpbp_halo* H) {
 
 namespace {
 
-// One RCCL group on stream `on`: own top rows -> up, own bottom rows -> down, rows below <- down,
-// rows above <- up (a multi-field vector's rows gathered into pack_buf first, on the same stream).
-// The sends / receives of vector kind k (inside an open group).
-ncclResult_t halo_ops(mpbp_halo* H, int k, double* x_ext, hipStream_t on);
+// One exchange of vector kind k on stream `on`: a multi-field vector's boundary rows are first gathered
+// into pack_buf by one kernel launched BEFORE the RCCL group opens (a kernel launch never sits between
+// ncclGroupStart and ncclGroupEnd, which graph capture of the group requires to be plain RCCL calls); then
+// one group: own top rows -> up, own bottom rows -> down, rows below <- down, rows above <- up.
+struct HaloBufs {
+    const double* top;
+    const double* bot;
+    double* above;
+    double* below;
+    size_t cnt;   // values per direction
+};
 
-ncclResult_t halo_group(mpbp_halo* H, int k, double* x_ext, hipStream_t on) {
-    const ncclResult_t e = H->rccl.group_start();
-    const ncclResult_t e2 = e == ncclSuccess ? halo_ops(H, k, x_ext, on) : e;
-    const ncclResult_t eg = H->rccl.group_end();
-    return e2 == ncclSuccess ? eg : e2;
+int halo_pack(mpbp_halo* H, int k, double* x_ext, hipStream_t on, HaloBufs* b) {
+    const int nf = H->nf[k], h = H->h[k], n = H->n, L = H->rows;
+    b->cnt = (size_t)nf * h * n;
+    b->top = x_ext;                               // nf == 1: the rows in place
+    b->bot = x_ext + (size_t)(L - h) * n;
+    if (nf > 1) {
+        const int rc = mpbp_gather((int32_t)(2 * b->cnt), H->pack_idx[k], x_ext, H->pack_buf[k], (void*)on);
+        if (rc != MPBP_OK) return rc;
+        b->top = H->pack_buf[k];
+        b->bot = H->pack_buf[k] + b->cnt;
+    }
+    b->above = x_ext + (size_t)nf * L * n;
+    b->below = b->above + b->cnt;
+    return MPBP_OK;
 }
 
-ncclResult_t halo_ops(mpbp_halo* H, int k, double* x_ext, hipStream_t on) {
-    const int nf = H->nf[k], h = H->h[k], n = H->n, L = H->rows;
-    const size_t cnt = (size_t)nf * h * n;                   // values per direction
-    const double* top = x_ext;                               // nf == 1: the rows in place
-    const double* bot = x_ext + (size_t)(L - h) * n;
-    if (nf > 1) {
-        if (mpbp_gather((int32_t)(2 * cnt), H->pack_idx[k], x_ext, H->pack_buf[k], (void*)on) != MPBP_OK)
-            return ncclUnhandledCudaError;
-        top = H->pack_buf[k];
-        bot = H->pack_buf[k] + cnt;
-    }
-    double* above = x_ext + (size_t)nf * L * n;
-    double* below = above + cnt;
+// The sends / receives of one vector (inside an open group).
+ncclResult_t halo_ops(mpbp_halo* H, const HaloBufs& b, hipStream_t on) {
     const Rccl& R = H->rccl;
-    ncclResult_t e = R.send(top, cnt, ncclFloat64, H->up, H->comm, on);
-    if (e == ncclSuccess) e = R.send(bot, cnt, ncclFloat64, H->down, H->comm, on);
-    if (e == ncclSuccess) e = R.recv(below, cnt, ncclFloat64, H->down, H->comm, on);
-    if (e == ncclSuccess) e = R.recv(above, cnt, ncclFloat64, H->up, H->comm, on);
+    ncclResult_t e = R.send(b.top, b.cnt, ncclFloat64, H->up, H->comm, on);
+    if (e == ncclSuccess) e = R.send(b.bot, b.cnt, ncclFloat64, H->down, H->comm, on);
+    if (e == ncclSuccess) e = R.recv(b.below, b.cnt, ncclFloat64, H->down, H->comm, on);
+    if (e == ncclSuccess) e = R.recv(b.above, b.cnt, ncclFloat64, H->up, H->comm, on);
     return e;
+}
+
+ncclResult_t halo_group(mpbp_halo* H, int k, double* x_ext, hipStream_t on) {
+    HaloBufs b;
+    if (halo_pack(H, k, x_ext, on, &b) != MPBP_OK) return ncclUnhandledCudaError;
+    const ncclResult_t e = H->rccl.group_start();
+    const ncclResult_t e2 = e == ncclSuccess ? halo_ops(H, b, on) : e;
+    const ncclResult_t eg = H->rccl.group_end();
+    return e2 == ncclSuccess ? eg : e2;
 }
 
 }  // namespace
@@ -275,10 +289,15 @@ void mpbp_halo_exchange_pair(void* ctx, double* xu_ext, double* xp_ext, void* st
     mpbp_halo* H = static_cast<mpbp_halo*>(ctx);
     if (!H || H->status != MPBP_OK) return;
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    // both vectors' operations in one group: the gather of the velocity rows runs before the group opens
+    // both vectors' operations in one group; the velocity rows are gathered before the group opens
+    HaloBufs bu, bp;
+    if (halo_pack(H, 0, xu_ext, st, &bu) != MPBP_OK || halo_pack(H, 1, xp_ext, st, &bp) != MPBP_OK) {
+        fail(H, MPBP_ERR_HIP, "pack", "mpbp_gather");
+        return;
+    }
     const ncclResult_t e0 = H->rccl.group_start();
-    ncclResult_t e = e0 == ncclSuccess ? halo_ops(H, 0, xu_ext, st) : e0;
-    if (e == ncclSuccess) e = halo_ops(H, 1, xp_ext, st);
+    ncclResult_t e = e0 == ncclSuccess ? halo_ops(H, bu, st) : e0;
+    if (e == ncclSuccess) e = halo_ops(H, bp, st);
     const ncclResult_t eg = H->rccl.group_end();
     if (e == ncclSuccess) e = eg;
     if (e != ncclSuccess) fail(H, MPBP_ERR_HIP, "RCCL pair group", H->rccl.error_string(e));

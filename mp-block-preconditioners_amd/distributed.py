@@ -12,10 +12,12 @@ layout (``DeviceCSR.extract``), so every local row sum is the global one, bit fo
 sweep reads a vector its ghost rows are refreshed while the rows that touch no ghost (the interior)
 are computed; the boundary rows run after.  Two exchange implementations:
 
-* ``RcclHalo`` (default with the nccl = RCCL backend): libmpbp's own RCCL communicator; one group of
-  neighbour ncclSend / ncclRecv per sweep straight from the owned boundary rows into the ghost rows,
-  issued from C inside ``mpbp_schur_apply`` on a side stream (fork / join by events) -- no pack
-  kernels, no Python between the kernels, graph-capturable.
+* ``RcclHalo`` (default with the nccl = RCCL backend): libmpbp's own RCCL communicator; the exchange is
+  issued from C inside ``mpbp_schur_apply`` (no Python between the kernels): a four-field vector's
+  boundary rows are packed by one gather kernel, then one RCCL group of neighbour ncclSend / ncclRecv
+  writes straight into the ghost rows, in order on the apply stream (``MPBP_HALO_IN_ORDER``, default; a
+  side-stream variant forked / joined by events is ``halo_overlap=True``).  With the communication-
+  avoiding schedule (``ca``) an apply makes two such exchanges.
 * ``HaloExchanger`` (gloo, CPU-staged; the tests' backend): packs the top/bottom h owned rows of every
   field, all-gathers them, copies the neighbours' strips into the ghost slots.
 
@@ -423,12 +425,14 @@ class DistributedSchurPreconditioner(PlanProfiling):
         return out
 
     def capture(self, v: torch.Tensor, out: torch.Tensor):
-        """Capture one apply(v, out) into a hipGraph -- unpartitioned (single-rank) applies only: capturing
-        the RCCL point-to-point group of the halo exchange crashes this RCCL build (2.26.6, SIGSEGV
-        during capture), and the torch halo runs host-staged collectives between the kernels."""
-        if self.partitioned:
-            raise NotImplementedError("graph capture of the partitioned apply (halo exchange) is not supported")
-        return _capture(self, v, out)
+        """Capture one apply(v, out) into a hipGraph.  Partitioned applies need the RCCL halo in order on the
+        apply stream (the exchange is then a gather kernel plus one RCCL group of point-to-point calls, which
+        RCCL records into the graph); the capture runs in thread-local error mode so that RCCL's proxy thread
+        may keep calling HIP.  The torch halo (host-staged gloo collectives between kernels) cannot be
+        captured."""
+        if self.partitioned and (self._rccl is None or self._rccl.overlap):
+            raise NotImplementedError("graph capture of a partitioned apply needs the in-order RCCL halo")
+        return _capture(self, v, out, capture_error_mode="thread_local" if self.partitioned else "global")
 
     def close(self):
         if self._rccl is not None:

@@ -101,10 +101,13 @@ class MultiphaseBlockPreconditioner:
         return self._theta
 
     def set_theta_tables(self, cell, uface, vface):
-        """Use caller-provided thn tables (any volume-fraction field; host arrays or tensors)."""
+        """Use caller-provided thn tables (any volume-fraction field; host arrays or tensors of n*n values, or
+        scalars for a constant thn such as BASELINE configs[0]'s / solve.py:60-68's 0.75)."""
         N = self.n * self.n
         tabs = []
         for a in (cell, uface, vface):
+            if np.ndim(a) == 0 and not isinstance(a, torch.Tensor):
+                a = np.full(N, float(a))
             a = torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64) if isinstance(a, np.ndarray) else a)
             a = a.to(device=self.device, dtype=torch.float64).contiguous()
             if a.numel() != N:

@@ -117,8 +117,10 @@ def _pg_stencil(D, G, GtG, f_stencil, pg_mode):
     return sp if ok else None
 
 
-def _capture(pc, v: torch.Tensor, out: torch.Tensor):
-    """One pc.apply(v, out) captured into a torch.cuda.CUDAGraph (warm-up on a side stream first)."""
+def _capture(pc, v: torch.Tensor, out: torch.Tensor, capture_error_mode: str = "global"):
+    """One pc.apply(v, out) captured into a torch.cuda.CUDAGraph (warm-up on a side stream first).
+    capture_error_mode "thread_local" lets other threads (RCCL's proxy thread) keep making HIP calls that
+    are illegal during a global-mode capture."""
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     saved = (pc._plan.prof_events, pc._plan.prof_capacity)
@@ -128,7 +130,7 @@ def _capture(pc, v: torch.Tensor, out: torch.Tensor):
             pc.apply(v, out)                    # warm-up on a side stream, as torch requires
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode=capture_error_mode):
             pc.apply(v, out)
     finally:
         pc._plan.prof_events, pc._plan.prof_capacity = saved
@@ -242,25 +244,44 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
 
     def _matvec(self, x):
         """Host vector in, host vector out (the LinearOperator surface pyamg drives, solve.py:281): staged
-        through page-locked buffers allocated on first use, so both PCIe copies run at DMA speed."""
-        x = np.ravel(x)
-        n = self.nu + self.np
-        if getattr(self, "_pinned", None) is None:
-            self._pinned = (torch.empty(n, dtype=torch.float64, pin_memory=True),
-                            torch.empty(n, dtype=torch.float64, pin_memory=True),
-                            torch.empty(n, dtype=torch.float64, device=self.device),
-                            torch.empty(n, dtype=torch.float64, device=self.device))
-        h_in, h_out, d_in, d_out = self._pinned
-        h_in.numpy()[:] = x
-        d_in.copy_(h_in, non_blocking=True)
-        self.apply(d_in, d_out)
-        h_out.copy_(d_out, non_blocking=True)
-        torch.cuda.current_stream(self.device).synchronize()
-        return h_out.numpy().copy()
+        through page-locked buffers allocated on first use, so both PCIe copies run at DMA speed.  One call
+        at a time per preconditioner (the staging buffers are shared; a lock serialises threads)."""
+        return _staged_host_call(self, x, self.nu + self.np, self.nu + self.np, self.device, self.apply)
+
+    def release_staging(self):
+        """Free the page-locked / device staging buffers of the host-vector matvec (re-created on demand)."""
+        self._pinned = None
 
     # reference naming (solve.py:257)
     def approx_schur_op(self, v):
         return self._matvec(v)
+
+
+def _staged_host_call(obj, x, n_in, n_out, device, fn):
+    """y = fn(x_dev, y_dev) for a host vector x of n_in entries through obj's page-locked staging buffers.
+    Raises like scipy on a wrong length (no broadcasting); the stream is synchronised even when fn raises,
+    so the next call never overwrites a buffer a DMA is still reading."""
+    import threading
+    x = np.ravel(np.asarray(x))
+    if x.shape != (n_in,):
+        raise ValueError(f"dimension mismatch: operand has {x.shape[0]} entries, the operator takes {n_in}")
+    lock = obj.__dict__.setdefault("_stage_lock", threading.Lock())
+    with lock:
+        if getattr(obj, "_pinned", None) is None:
+            obj._pinned = (torch.empty(n_in, dtype=torch.float64, pin_memory=True),
+                           torch.empty(n_out, dtype=torch.float64, pin_memory=True),
+                           torch.empty(n_in, dtype=torch.float64, device=device),
+                           torch.empty(n_out, dtype=torch.float64, device=device))
+        h_in, h_out, d_in, d_out = obj._pinned
+        stream = torch.cuda.current_stream(device)
+        try:
+            h_in.numpy()[:] = x
+            d_in.copy_(h_in, non_blocking=True)
+            fn(d_in, d_out)
+            h_out.copy_(d_out, non_blocking=True)
+        finally:
+            stream.synchronize()
+        return h_out.numpy().copy()
 
 
 def _as_operator(A):

@@ -4,6 +4,8 @@
     fill_sol_and_RHS_vecs                             utils.py:159-210 (vectorised over the grid)
     manufactured_problem                              the variable-thn manufactured solution of
                                                       solve.py:52-80 / apply.py:40-66
+    manufactured_problem_constant                     the constant-thn one (solve.py:60-68: thn = 0.75;
+                                                      any constant theta here, BASELINE configs[0])
 """
 from __future__ import annotations
 
@@ -76,3 +78,27 @@ def manufactured_problem(n, c=1.0, d=-1.0, xi=1.0, etan=1.0, etas=1.0):
         lambda y, x: C2(y) * S2(x) * core(y, x, -1.0, etas) / (8 * nu),
         lambda y, x: C2(x) * S2(y) * core(y, x, -1.0, etas) / (8 * nu),
         lambda y, x: -PI * np.sin(4 * PI * x) * np.sin(4 * PI * y))
+
+
+def manufactured_problem_constant(n, c=1.0, d=-1.0, xi=1.0, etan=1.0, etas=1.0, theta=0.75):
+    """(u_vec, b_vec) for a constant volume fraction thn = theta (ths = 1 - theta), same solution as the
+    variable case (solve.py:52-58).  With constant theta the rows of A reduce to
+        b_n = (c theta - 2 d xi theta (1 - theta) - 8 pi^2 d eta_n theta) u_n          (u_s = -u_n)
+        b_s = (-c (1 - theta) + 2 d xi theta (1 - theta) + 8 pi^2 d eta_s (1 - theta)) u_n
+        b_p = -(2 theta - 1) 4 pi cos(2 pi x) cos(2 pi y)                                 (d_div = -1)
+    which at theta = 0.75 are the reference's expressions at solve.py:62-68.  Use with
+    MultiphaseBlockPreconditioner.set_theta_tables(theta, theta, theta) (constant tables)."""
+    nu = 1.0
+    th = float(theta)
+    S2 = lambda a: np.sin(2 * PI * a)
+    C2 = lambda a: np.cos(2 * PI * a)
+    kn = (c * nu * th - 2 * d * xi * th * (1 - th) - 8 * PI * PI * d * etan * nu * th) / nu
+    ks = (-c * nu * (1 - th) + 2 * d * xi * th * (1 - th) + 8 * PI * PI * d * etas * nu * (1 - th)) / nu
+    return fill_sol_and_RHS_vecs(
+        n,
+        lambda y, x: S2(x) * C2(y), lambda y, x: C2(x) * S2(y),
+        lambda y, x: -S2(x) * C2(y), lambda y, x: -C2(x) * S2(y),
+        lambda y, x: 0.0,
+        lambda y, x: kn * S2(x) * C2(y), lambda y, x: kn * C2(x) * S2(y),
+        lambda y, x: ks * S2(x) * C2(y), lambda y, x: ks * C2(x) * S2(y),
+        lambda y, x: -(2 * th - 1) * 4 * PI * C2(x) * C2(y))

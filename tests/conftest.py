@@ -37,6 +37,16 @@ def golden_params(g):
                 d_u=float(d), d_p=float(d_p), d_div=float(d_div))
 
 
+def golden_tables(g):
+    """The thn tables a fixture was generated with: None (the reference's variable thn, preconditioner.py:9-11)
+    or constant tables for the constant-thn cases (BASELINE configs[0], solve.py:60-68)."""
+    if "theta_const" not in g:
+        return None
+    n = golden_params(g)["n"]
+    t = np.full(n * n, float(g["theta_const"]))
+    return t, t.copy(), t.copy()
+
+
 def rel_inf(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)

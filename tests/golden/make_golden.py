@@ -41,6 +41,10 @@ CASES = [
     ("stiff", 8, 2.5, 1.0e4, 1.0, 1.0, -1.0),      # BASELINE configs[3]: eta_n/eta_s = 1e4
 ]
 BIG = [("visc", 32, 1.0, 100.0, 1.0, 1.0, -1.0)]   # A, u_vec, b_vec, A @ u_vec only
+# BASELINE configs[0]: the reference's "Fixed Thn = 0.75" manufactured problem (solve.py:60-68): the
+# reference's own thn (preconditioner.py:9-11) replaced by the constant 0.75 in the executed module.
+CONST = [("const75", 8, 1.0, 1.0, 1.0, 1.0, -1.0, False), ("const75", 32, 1.0, 1.0, 1.0, 1.0, -1.0, True)]
+THETA_CONST = 0.75
 
 
 def load_reference(ref_dir):
@@ -85,6 +89,23 @@ def manufactured(n, c, d, xi, etan, etas, utils):
     return utils.fill_sol_and_RHS_vecs(n, u_n_x, u_n_y, u_s_x, u_s_y, p_f, b_n_x, b_n_y, b_s_x, b_s_y, b_p)
 
 
+def manufactured_const75(n, c, d, xi, etan, etas, utils):
+    """u_vec, b_vec of the constant-thn (0.75) manufactured problem: the RHS expressions the reference keeps
+    commented out at solve.py:62-68 (same solution components, solve.py:52-58)."""
+    nu = 1.0
+    u_n_x = lambda y, x: np.sin(2 * PI * x) * np.cos(2 * PI * y)
+    u_n_y = lambda y, x: np.cos(2 * PI * x) * np.sin(2 * PI * y)
+    u_s_x = lambda y, x: -np.sin(2 * PI * x) * np.cos(2 * PI * y)
+    u_s_y = lambda y, x: -np.cos(2 * PI * x) * np.sin(2 * PI * y)
+    p_f = lambda y, x: 0.0
+    b_n_x = lambda y, x: (3 * (2 * c * nu - d * (16 * etan * nu * PI * PI + xi)) * np.cos(2 * PI * y) * np.sin(2 * PI * x)) / (8 * nu)
+    b_n_y = lambda y, x: (3 * (2 * c * nu - d * (16 * etan * nu * PI * PI + xi)) * np.cos(2 * PI * x) * np.sin(2 * PI * y)) / (8 * nu)
+    b_s_x = lambda y, x: ((-2 * c * nu + 16 * d * etas * nu * PI * PI + 3 * d * xi) * np.cos(2 * PI * y) * np.sin(2 * PI * x)) / (8 * nu)
+    b_s_y = lambda y, x: ((-2 * c * nu + 16 * d * etas * nu * PI * PI + 3 * d * xi) * np.cos(2 * PI * x) * np.sin(2 * PI * y)) / (8 * nu)
+    b_p = lambda y, x: -2 * PI * np.cos(2 * PI * x) * np.cos(2 * PI * y)
+    return utils.fill_sol_and_RHS_vecs(n, u_n_x, u_n_y, u_s_x, u_s_y, p_f, b_n_x, b_n_y, b_s_x, b_s_y, b_p)
+
+
 def csr_fields(prefix, M):
     M = sp.csr_matrix(M)
     M.sort_indices()
@@ -109,7 +130,11 @@ def make_case(prec, utils, tag, n, xi, eta_n, eta_s, c, d, big=False):
     A, S, F, D, G = bp.get_big_A_matrix(c=c, d_u=d)
     out = {"params": np.array([n, xi, eta_n, eta_s, c, d, 1.0, -1.0])}
     out.update(csr_fields("A", A))
-    u_vec, b_vec = manufactured(n, c, d, xi, eta_n, eta_s, utils)
+    if tag == "const75":
+        out["theta_const"] = np.array(THETA_CONST)
+        u_vec, b_vec = manufactured_const75(n, c, d, xi, eta_n, eta_s, utils)
+    else:
+        u_vec, b_vec = manufactured(n, c, d, xi, eta_n, eta_s, utils)
     out["u_vec"], out["b_vec"] = u_vec, b_vec
     out["Au"] = np.matmul(A, u_vec)                                  # apply.py:72
     if not big:
@@ -155,6 +180,15 @@ def main():
         make_case(prec, utils, *case)
     for case in BIG:
         make_case(prec, utils, *case, big=True)
+    # the constant-thn cases run the reference's assembly with its module-level thn (which ths and
+    # get_thn_vals / get_big_A_matrix look up at call time) bound to the constant
+    variable_thn = prec.thn
+    prec.thn = lambda y, x: THETA_CONST
+    try:
+        for *case, big in CONST:
+            make_case(prec, utils, *case, big=big)
+    finally:
+        prec.thn = variable_thn
 
 
 if __name__ == "__main__":

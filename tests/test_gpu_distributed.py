@@ -106,12 +106,24 @@ def _self_halo_worker(_index, port, n, halo, f_mode, pg_mode, kind, graph, errfi
         for _ in range(2):
             got = dpc.apply(v.clone())
             assert torch.equal(got, ref), float((got - ref).abs().max())
-        if graph:   # not supported for partitioned applies (see DistributedSchurPreconditioner.capture)
-            try:
-                dpc.capture(v.clone(), torch.zeros_like(v))
-                raise AssertionError("capture of a partitioned apply should be refused")
-            except NotImplementedError:
-                pass
+        if graph:   # in-order RCCL halo: captured (thread-local error mode); other halos are refused
+            vin, out = v.clone(), torch.zeros_like(v)
+            if halo == "rccl" and not overlap:
+                g = dpc.capture(vin, out)
+                out.zero_()
+                g.replay()
+                torch.cuda.synchronize()
+                assert torch.equal(out, ref)
+                vin.copy_(2.0 * v)
+                g.replay()
+                assert torch.equal(out, pc.apply(2.0 * v))
+                del g
+            else:
+                try:
+                    dpc.capture(vin, out)
+                    raise AssertionError("capture of this partitioned apply should be refused")
+                except NotImplementedError:
+                    pass
         dpc.close()
         dist.destroy_process_group()
     except BaseException as e:
@@ -124,6 +136,7 @@ def _self_halo_worker(_index, port, n, halo, f_mode, pg_mode, kind, graph, errfi
     (64, "rccl", "stencil", "stencil", 2, False, False), (50, "rccl", "assembled", "assembled", 2, False, False),
     (33, "rccl", "stencil", "assembled", 0, False, False), (64, "torch", "stencil", "stencil", 2, False, False),
     (64, "rccl", "stencil", "stencil", 2, True, False), (64, "rccl", "stencil", "stencil", 2, False, True),
+    (64, "torch", "stencil", "stencil", 2, True, False),
     (40, "rccl", "assembled", "stencil", 2, False, True)])
 def test_self_halo_partitioned_apply(n, halo, f_mode, pg_mode, kind, graph, overlap, tmp_path, ca="auto",
                                      inner=(("chebyshev", 4), ("chebyshev", 3))):

@@ -1,0 +1,90 @@
+#!/bin/bash
+# The one GPU-box launcher: runs named steps in order, each under its own time limit, logs under
+# gpurun_out/TAG/, and stops at the first step that fails (a test failure, a GPU fault, a time limit).
+#
+#   gpurun --timeout 1200 -- bash tools/gpu.sh TAG tests smoke bench ...
+#
+# Steps:
+#   tests        pytest -m gpu (all GPU parity tests)          smoke     __graft_entry__.smoke()
+#   bench        bench.py, N = 1 (the driver's command)        bench_csr bench.py --layout csr
+#   rows2_gloo   bench.py --gpus 2 --grid 512 over gloo on one GPU (the N > 1 path; launcher inside bench.py)
+#   selfhalo     bench.py --self-halo (partitioned apply over the RCCL self-exchange)
+#   probe        tools/capture_probe.py 256 1024 (hipGraph capture of the partitioned apply)
+#   prof         rocprofv3 --kernel-trace --stats of bench.py
+#   pmc          FETCH_SIZE / WRITE_SIZE passes: the apply's F sweeps and the A SpMV
+#   sq           SQ counter passes over the F sweep (tools/pmc_sweep.py) and the CSR SpMV (tools/spmv_ab.py)
+#   py:FILE      python FILE (any experiment script), 300 s
+#   ab:V1,V2,..  A/B of experiment builds (tools/build_variants.py): bench.py and tools/spmv_ab.py per variant
+#                (variant "base" = the product library); extra bench args in $BENCH_ARGS
+set -o pipefail
+TAG=${1:-run}
+shift
+cd "$GRAFT_REPO_ROOT" || exit 99
+export TMPDIR=/tmp
+ROOTD=$GRAFT_REPO_ROOT
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+
+prof() {   # prof NAME TIMEOUT ARGS... : rocprofv3 run from /tmp with the program right after --
+  local name=$1 t=$2
+  shift 2
+  (cd /tmp && timeout -s KILL "$t" rocprofv3 "$@") > "$ROOTD/$OUT/$name.log" 2>&1
+}
+
+step() {
+  local s=$1
+  echo "== $s $(date +%T)"
+  case $s in
+    tests) timeout -k 10 1000 python -u -m pytest tests/ -x -v --timeout 240 --timeout-method thread -m gpu \
+             > "$OUT/pytest.log" 2>&1 ;;
+    smoke) timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
+    bench) timeout -k 10 300 python bench.py --steps 20 --warmup 5 > "$OUT/bench.log" 2>&1 ;;
+    bench_csr) timeout -k 10 300 python bench.py --steps 20 --warmup 5 --layout csr --no-cpu-baseline \
+                 > "$OUT/bench_csr.log" 2>&1 ;;
+    rows2_gloo) MPBP_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --steps 5 --warmup 2 --grid 512 \
+                  > "$OUT/rows2_gloo.log" 2>&1 ;;
+    selfhalo) timeout -k 10 300 python bench.py --self-halo --steps 20 --warmup 5 --no-cpu-baseline --no-spmv \
+                > "$OUT/selfhalo.log" 2>&1 ;;
+    probe) timeout -k 10 240 python -u tools/capture_probe.py 256 1024 > "$OUT/probe.log" 2>&1 ;;
+    prof) prof prof 300 --kernel-trace --stats --output-format csv -d "$ROOTD/$OUT/prof" -o run -- \
+            python "$ROOTD/bench.py" --steps 20 --warmup 5 --no-cpu-baseline ;;
+    pmc) for C in FETCH_SIZE WRITE_SIZE; do
+           prof "pmc_apply_$C" 150 --pmc $C --output-format csv -d "$ROOTD/$OUT/pmc_apply_$C" -o pmc -- \
+             python "$ROOTD/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-spmv --no-graph || return 1
+           prof "pmc_spmv_$C" 120 --pmc $C --output-format csv -d "$ROOTD/$OUT/pmc_spmv_$C" -o pmc -- \
+             python "$ROOTD/tools/spmv_ab.py" --reps 10 || return 1
+         done ;;
+    sq) for W in "pmc_sweep.py --layout stencil" "spmv_ab.py --reps 10"; do
+          local tag=${W%%.py*}
+          prof "sq1_$tag" 120 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+            SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU --output-format csv -d "$ROOTD/$OUT/sq1_$tag" \
+            -o pmc -- python "$ROOTD/tools/"$W || return 1
+          prof "sq2_$tag" 120 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS \
+            SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_VMEM_RD SQ_LDS_BANK_CONFLICT --output-format csv \
+            -d "$ROOTD/$OUT/sq2_$tag" -o pmc -- python "$ROOTD/tools/"$W || return 1
+        done ;;
+    ab:*) local V
+          for V in $(echo "${s#ab:}" | tr , ' '); do
+            local L=mp-block-preconditioners_amd/lib/variants/libmpbp_$V.so
+            [ "$V" = base ] && L=
+            MPBP_LIB=$L timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline $BENCH_ARGS \
+              >> "$OUT/ab_bench_$V.log" 2>&1 || return 1
+            MPBP_LIB=$L timeout -k 10 120 python tools/spmv_ab.py >> "$OUT/ab_spmv_$V.log" 2>&1 || return 1
+          done ;;
+    py:*) timeout -k 10 300 python -u "${s#py:}" > "$OUT/$(basename "${s#py:}" .py).log" 2>&1 ;;
+    *) echo "unknown step $s"; return 98 ;;
+  esac
+}
+
+i=0
+for s in "$@"; do
+  i=$((i + 1))
+  step "$s"
+  rc=$?
+  echo "== $s exit $rc"
+  if [ $rc -ne 0 ]; then
+    echo "step $s failed ($rc): stopping" | tee -a "$OUT/steps.log"
+    exit $i
+  fi
+  echo "$s ok" >> "$OUT/steps.log"
+done

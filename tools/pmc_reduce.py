@@ -1,4 +1,4 @@
-"""Reduce rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (over bench.py's apply, tools/gpu_round.sh) to HBM
+"""Reduce rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (over bench.py's apply, tools/gpu.sh (step pmc)) to HBM
 bytes per F sweep launch -- the same launches bench.py's HIP events time.
 
     python tools/pmc_reduce.py gpurun_out/<tag> [--write profiles/pmc_traffic.json]
