@@ -108,6 +108,8 @@ def main():
     ap.add_argument("--no-spmv", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch the apply eagerly instead of a hipGraph")
     ap.add_argument("--no-check", action="store_true", help="N > 1: skip the bit-exact check against one GPU")
+    ap.add_argument("--partitioned-graph", action="store_true",
+                    help="N > 1: capture the partitioned apply (RCCL halo groups included) into a hipGraph")
     args = ap.parse_args()
 
     # --gpus N > 1 without a launcher: start the N ranks as a child process BEFORE anything touches the GPU
@@ -182,7 +184,11 @@ def main():
     # applies right after the timed loop.
     sweeps_per_apply = 2 * max(sf - 1, 0)
     graph, graph_note = None, None
-    if not partitioned and not args.no_graph:
+    # partitioned applies are captured for the one-GPU self-exchange (measured, bit-exact) and, on request,
+    # for N > 1 (--partitioned-graph: cross-GPU RCCL point-to-point inside a graph is unmeasured here)
+    use_graph = not args.no_graph and (not partitioned or (world == 1 and not args.halo_overlap) or
+                                       (args.partitioned_graph and not args.halo_overlap and backend == "nccl"))
+    if use_graph:
         try:
             graph = pc.capture(v, out)
         except Exception as e:   # fall back to eager launches, and say so in the JSON line

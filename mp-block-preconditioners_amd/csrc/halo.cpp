@@ -41,6 +41,7 @@ struct Rccl {
     ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
     ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
     ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*group_start)() = nullptr;
@@ -69,6 +70,7 @@ int load_rccl(const char* path, Rccl* r) {
     MPBP_SYM(get_unique_id, "ncclGetUniqueId");
     MPBP_SYM(comm_init_rank, "ncclCommInitRank");
     MPBP_SYM(comm_destroy, "ncclCommDestroy");
+    MPBP_SYM(comm_abort, "ncclCommAbort");
     MPBP_SYM(send, "ncclSend");
     MPBP_SYM(recv, "ncclRecv");
     MPBP_SYM(group_start, "ncclGroupStart");
@@ -93,6 +95,7 @@ struct mpbp_halo {
     double* pack_buf[2] = {nullptr, nullptr};    // device: 2 nf h n staged values
     int mode = MPBP_HALO_IN_ORDER;
     int status = MPBP_OK;  // first error seen by mpbp_halo_exchange (its signature returns nothing)
+    bool captured = false; // an exchange was recorded into a hipGraph (stream capture) with this communicator
     char err[512] = "";
 };
 
@@ -195,7 +198,16 @@ void mpbp_halo_destroy(mpbp_halo* H) {
         if (H->pack_idx[k]) (void)hipFree(H->pack_idx[k]);
         if (H->pack_buf[k]) (void)hipFree(H->pack_buf[k]);
     }
-    if (H->comm) H->rccl.comm_destroy(H->comm);
+    // A communicator whose operations were captured into a hipGraph is not destroyed: with RCCL 2.26.6,
+    // ncclCommDestroy never returns once a graph holding this communicator's point-to-point kernels has
+    // been instantiated and destroyed (measured: tools/capture_probe.py).  It is
+    // released with the process instead (MPBP_HALO_CAPTURED_DESTROY=abort tries ncclCommAbort,
+    // =destroy the plain destroy).
+    if (H->comm) {
+        const char* pol = std::getenv("MPBP_HALO_CAPTURED_DESTROY");
+        if (!H->captured || (pol && std::strcmp(pol, "destroy") == 0)) H->rccl.comm_destroy(H->comm);
+        else if (pol && std::strcmp(pol, "abort") == 0) H->rccl.comm_abort(H->comm);
+    }
     // the RCCL library stays loaded: torch (or another communicator) may still use it
     delete H;
 }
@@ -240,7 +252,13 @@ ncclResult_t halo_ops(mpbp_halo* H, const HaloBufs& b, hipStream_t on) {
     return e;
 }
 
+void note_capture(mpbp_halo* H, hipStream_t on) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(on, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) H->captured = true;
+}
+
 ncclResult_t halo_group(mpbp_halo* H, int k, double* x_ext, hipStream_t on) {
+    note_capture(H, on);
     HaloBufs b;
     if (halo_pack(H, k, x_ext, on, &b) != MPBP_OK) return ncclUnhandledCudaError;
     const ncclResult_t e = H->rccl.group_start();
@@ -290,6 +308,7 @@ void mpbp_halo_exchange_pair(void* ctx, double* xu_ext, double* xp_ext, void* st
     if (!H || H->status != MPBP_OK) return;
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     // both vectors' operations in one group; the velocity rows are gathered before the group opens
+    note_capture(H, st);
     HaloBufs bu, bp;
     if (halo_pack(H, 0, xu_ext, st, &bu) != MPBP_OK || halo_pack(H, 1, xp_ext, st, &bp) != MPBP_OK) {
         fail(H, MPBP_ERR_HIP, "pack", "mpbp_gather");

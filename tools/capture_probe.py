@@ -5,6 +5,7 @@
 For every grid size: eager apply, capture (thread-local error mode), replay, bit-compare, and time
 eager vs replayed applies.  Prints one line per step so a hang names the step it happened in.
 """
+import gc
 import os
 import sys
 import time
@@ -24,7 +25,9 @@ def main():
     from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
     for n in sizes:
         iF, iP = mp.InnerSolver("chebyshev", 4), mp.InnerSolver("chebyshev", 4)
+        print(f"n={n} setup", flush=True)
         dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, self_halo=True)
+        print(f"n={n} setup done", flush=True)
         v = torch.randn(dpc.shape[0], dtype=torch.float64, device="cuda")
         ref = dpc.apply(v).clone()
         torch.cuda.synchronize()
@@ -47,8 +50,13 @@ def main():
             torch.cuda.synchronize()
             print(f"n={n} {name}: {20 / (time.perf_counter() - t0):.0f} applies/s", flush=True)
         del g
+        gc.collect()
+        torch.cuda.synchronize()
+        print(f"n={n} graph destroyed", flush=True)
         dpc.close()
+        print(f"n={n} halo communicator destroyed", flush=True)
     dist.destroy_process_group()
+    print("process group destroyed", flush=True)
 
 
 if __name__ == "__main__":

@@ -9,7 +9,7 @@
 #   bench        bench.py, N = 1 (the driver's command)        bench_csr bench.py --layout csr
 #   rows2_gloo   bench.py --gpus 2 --grid 512 over gloo on one GPU (the N > 1 path; launcher inside bench.py)
 #   selfhalo     bench.py --self-halo (partitioned apply over the RCCL self-exchange)
-#   probe        tools/capture_probe.py 256 1024 (hipGraph capture of the partitioned apply)
+#   probe        tools/capture_probe.py 256 1024 (hipGraph capture of the partitioned apply); probe:N1,N2 sizes
 #   prof         rocprofv3 --kernel-trace --stats of bench.py
 #   pmc          FETCH_SIZE / WRITE_SIZE passes: the apply's F sweeps and the A SpMV
 #   sq           SQ counter passes over the F sweep (tools/pmc_sweep.py) and the CSR SpMV (tools/spmv_ab.py)
@@ -45,7 +45,9 @@ step() {
                   > "$OUT/rows2_gloo.log" 2>&1 ;;
     selfhalo) timeout -k 10 300 python bench.py --self-halo --steps 20 --warmup 5 --no-cpu-baseline --no-spmv \
                 > "$OUT/selfhalo.log" 2>&1 ;;
-    probe) timeout -k 10 240 python -u tools/capture_probe.py 256 1024 > "$OUT/probe.log" 2>&1 ;;
+    probe) timeout -k 10 120 python -u tools/capture_probe.py 256 1024 > "$OUT/probe.log" 2>&1 ;;
+    probe:*) timeout -k 10 120 python -u tools/capture_probe.py $(echo "${s#probe:}" | tr , ' ') \
+               > "$OUT/probe_${s#probe:}_${MPBP_HALO_CAPTURED_DESTROY:-leak}.log" 2>&1 ;;
     prof) prof prof 300 --kernel-trace --stats --output-format csv -d "$ROOTD/$OUT/prof" -o run -- \
             python "$ROOTD/bench.py" --steps 20 --warmup 5 --no-cpu-baseline ;;
     pmc) for C in FETCH_SIZE WRITE_SIZE; do
