@@ -89,13 +89,8 @@ def main():
                     help="F sweeps: recompute F from thn (stencil) or stream the assembled F")
     ap.add_argument("--pg-mode", default="auto", choices=["auto", "stencil", "assembled"],
                     help="D, G, Gt_G: recompute from thn (stencil) or stream the stored operators")
-    ap.add_argument("--stencil-kind", default="march4",
-                    help="matrix-free F kernel: cells (LDS tile per grid row), rows (row per thread), "
-                         "marchR (LDS ring marching R grid rows per workgroup)")
-    ap.add_argument("--sweep-fusion", type=int, default=0,
-                    help="grid rows per workgroup of the fused init + two-sweep F kernel; 0 = one kernel per sweep")
-    ap.add_argument("--p-fusion", type=int, default=0,
-                    help="grid rows per workgroup of the one-pass Gt_G inner solve; 0 = one kernel per sweep")
+    ap.add_argument("--march-rows", type=int, default=4,
+                    help="grid rows per workgroup of the marching stencil kernels (matrix-free F, D, G, Gt_G)")
     ap.add_argument("--no-ca", action="store_true",
                     help="row partition: exchange before every sweep instead of the communication-avoiding schedule")
     ap.add_argument("--self-halo", action="store_true",
@@ -147,10 +142,7 @@ def main():
 
     import mp_block_preconditioners_amd as mp
     from mp_block_preconditioners_amd._lib import check as _check, lib as _lib
-    sk = args.stencil_kind
-    _check(_lib().mpbp_set_stencil_kind(0 if sk == "cells" else 1 if sk == "rows" else 2 + int(sk[5:] or 4)))
-    _check(_lib().mpbp_set_sweep_fusion(args.sweep_fusion))
-    _check(_lib().mpbp_set_pressure_solve_fusion(args.p_fusion))
+    _check(_lib().mpbp_set_march_rows(args.march_rows))
 
     if args.weak:
         n = int(round((args.n or 1024) * math.sqrt(world)))
@@ -225,7 +217,7 @@ def main():
         single = single_gpu_check(pc, n, args, iF, iP, rank, dist, torch)
 
     # dominant kernel: the fused Chebyshev-Jacobi sweep over F
-    fused_init = not partitioned and getattr(pc, "f_stencil", None) is not None and sk.startswith("march")
+    fused_init = getattr(pc, "f_stencil", None) is not None and (not partitioned or pc.ca)
     sbytes, kname = sweep_bytes(pc, args.layout, kf, sf, fused_init)
     avg_sweep_s = (sum(sweep_ms) / len(sweep_ms) / 1e3) if sweep_ms else float("nan")
     achieved = sbytes / avg_sweep_s / 1e9
@@ -294,10 +286,9 @@ def main():
                        "n": n, "unknowns": 5 * n * n, "xi": args.xi, "eta_n": args.eta_n,
                        "eta_s": args.eta_s, "inner_F": f"{kf}:{sf}", "inner_P": f"{kp}:{spp}",
                        "parallelism": f"rows{world}" if world > 1 else "single", "layout": args.layout,
-                       "f_sweeps": ("matrix-free-" + args.stencil_kind) if getattr(pc, "f_stencil", None) is not None
+                       "f_sweeps": f"matrix-free-march{args.march_rows}" if getattr(pc, "f_stencil", None) is not None
                        else "assembled",
                        "d_g_gtg": "matrix-free" if getattr(pc, "pg_stencil", None) is not None else "assembled",
-                       "sweep_fusion_rows": args.sweep_fusion, "pressure_solve_fusion_rows": args.p_fusion,
                        "launch": "hipgraph" if graph is not None else "eager",
                        **({"halo": f"{pc.halo_impl} ({'self-exchange' if world == 1 else 'neighbour'})",
                            "halo_schedule": (f"communication-avoiding: 2 exchanges per apply, ghost depth "
@@ -378,13 +369,10 @@ def spmv_bench(A, gen, reps=20):
     y = torch.empty(A.shape[0], dtype=torch.float64, device="cuda")
     res = {"nnz": A.nnz}
     AS = A.to_sell()
-    from mp_block_preconditioners_amd._lib import lib
     csr_bytes = A.nnz * 12 + (A.shape[0] + 1) * 4 + (A.shape[0] + A.shape[1]) * 8 + A.blocks.count * 8
-    for name, M, nbytes, kind in (
-            ("csr", A, csr_bytes, 1),           # per-wave chunked kernel (default)
-            ("csr_block", A, csr_bytes, 0),     # one LDS stage per 256-row block
-            ("sell", AS, A.nnz * 12 + A.shape[0] + (A.shape[0] + A.shape[1]) * 8 + AS.nslices * 16, 1)):
-        lib().mpbp_set_csr_kernel(kind)
+    for name, M, nbytes in (
+            ("csr", A, csr_bytes),              # per-wave chunked kernel (k_csr_wave)
+            ("sell", AS, A.nnz * 12 + A.shape[0] + (A.shape[0] + A.shape[1]) * 8 + AS.nslices * 16)):
         for _ in range(3):
             M.matvec(x, out=y)
         ev[0].record()
@@ -394,7 +382,6 @@ def spmv_bench(A, gen, reps=20):
         torch.cuda.synchronize()
         s = ev[0].elapsed_time(ev[1]) / 1e3 / reps
         res.update({f"{name}_gbs": nbytes / s / 1e9, f"{name}_us": s * 1e6, f"{name}_bytes": nbytes})
-    lib().mpbp_set_csr_kernel(1)
     return res
 
 

@@ -296,22 +296,9 @@ int mpbp_gtg_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell
                                const double* x_in, const double* b, double c1, double c2, double* d,
                                const double* sub, double* x_out, void* stream);
 
-/* F stencil kernel choice (process-wide): 0 = LDS-tiled cells, 1 = one row per thread,
- * 2 = marching cells, 4 grid rows per workgroup (default), 2 + R = marching cells, R rows per workgroup. */
-int mpbp_set_stencil_kind(int32_t kind);
-/* Two-sweep fusion of mpbp_schur_apply's F inner solves (process-wide): the init pass and sweeps 1-2 of
- * each solve run as one kernel marching `rows` grid rows per workgroup; 0 (default) = one kernel per
- * sweep, which is faster on MI355X.  One GPU, marching F stencil; results bit-identical. */
-int mpbp_set_sweep_fusion(int32_t rows);
-/* One-pass Gt_G inner solves (process-wide): with the matrix-free Gt_G on one GPU and 3 <= sweeps <= 5,
- * the init and every sweep of the solve run as one kernel (levels kept in LDS), `rows` grid rows per
- * workgroup; 0 (default) = one kernel per sweep, faster on MI355X.  Bit-identical either way. */
-int mpbp_set_pressure_solve_fusion(int32_t rows);
-/* CSR SpMV kernel over row blocks (process-wide): 1 = one wavefront per 64 rows, chunked LDS stage, no
- * workgroup barrier (default); 2 = as 1 over several consecutive row blocks per workgroup, each wave
- * prefetching its next block's chunk during the current block's gathers; 0 = one LDS stage per 256-row
- * block.  Bit-identical in every case. */
-int mpbp_set_csr_kernel(int32_t kind);
+/* Grid rows per workgroup of the marching stencil kernels (matrix-free F, D, G, Gt_G), process-wide; 4 (default)
+ * is fastest on MI355X at 1024^2 (one round of workgroups).  Results are bit-identical for every value. */
+int mpbp_set_march_rows(int32_t rows);
 
 /* ---- ghost rows over RCCL point-to-point (multi-GPU row partition) ------------------------------ */
 /* One RCCL group of neighbour sends / receives: the owned boundary rows (packed into one buffer per

@@ -125,10 +125,7 @@ _SIGNATURES = {
     "mpbp_halo_status": ([_P], c_int),
     "mpbp_halo_set_mode": ([_P, c_int32], c_int),
     "mpbp_halo_last_error": ([_P], c_char_p),
-    "mpbp_set_stencil_kind": ([c_int32], c_int),
-    "mpbp_set_sweep_fusion": ([c_int32], c_int),
-    "mpbp_set_pressure_solve_fusion": ([c_int32], c_int),
-    "mpbp_set_csr_kernel": ([c_int32], c_int),
+    "mpbp_set_march_rows": ([c_int32], c_int),
     "mpbp_gather": ([c_int32, _P, _P, _P, _P], c_int),
     "mpbp_scatter": ([c_int32, _P, _P, _P, _P], c_int),
     "mpbp_event_create": ([POINTER(c_void_p)], c_int),

@@ -11,6 +11,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <type_traits>
 #include <vector>
 
 #include "mpbp.h"
@@ -18,20 +19,11 @@
 namespace {
 
 thread_local char g_err[1024] = "";
-int g_stencil_kind = 2;   // F stencil kernel: 0 LDS-tiled cells, 1 row per thread, 2 marching cells (default)
-int g_march_rows = 4;     // grid rows per workgroup of the marching kernel (4 is fastest at 1024^2)
+int g_march_rows = 4;     // grid rows per workgroup of the marching kernels (4 is fastest at 1024^2)
 #ifndef MPBP_PG_ROWS
 #define MPBP_PG_ROWS 0    // rows per workgroup of the D / G / Gt_G marching kernels (0: as F)
 #endif
 inline int pg_rows() { return MPBP_PG_ROWS > 0 ? MPBP_PG_ROWS : g_march_rows; }
-int g_sweep2_rows = 0;    // grid rows per workgroup of the two-sweep kernel; 0 (default) = no two-sweep fusion
-int g_gtg_solve_rows = 0; // grid rows per workgroup of the one-pass Gt_G solve (k_gtg_solve); 0 (default) = off
-#ifndef MPBP_CSR_KIND
-#define MPBP_CSR_KIND 1
-#endif
-// CSR SpMV kernel: 0 workgroup-staged row blocks (k_csr_rows), 1 per-wave chunks (k_csr_wave), 2 per-wave
-// chunks over several row blocks per workgroup with the next block's chunk prefetched (k_csr_wave_pf)
-int g_csr_kind = MPBP_CSR_KIND;
 
 int set_error(int code, const char* fmt, ...) {
     va_list ap;
@@ -51,8 +43,6 @@ int set_error(int code, const char* fmt, ...) {
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 constexpr int kBlock = 256;                    // 4 wave64 per workgroup, one row per thread
-constexpr int kCap = MPBP_BLOCK_NNZ + 1;       // products staged in LDS per row block (32 KiB)
-constexpr int kPairs = kCap / (2 * kBlock);    // 16-byte (2 x f64) loads per thread
 
 inline int grid_for(int64_t n, int block = kBlock) { return (int)((n + block - 1) / block); }
 
@@ -618,24 +608,31 @@ struct EpiResid {
     __device__ void apply(int32_t r, double acc, const P& p) const { st_stream<NT>(y + r, p.z - acc); }
     __device__ void operator()(int32_t r, double acc, const P& p) const { apply<false>(r, acc, p); }
 };
-struct EpiJacobi {   // x = (b - R x)/D in residual form (solve.py:158)
+// The solver epilogues carry two run-time switches -- `sub` (the solve's last sweep returns sub - x) and
+// `store_d` (the direction is stored except on a solve's last sweep).  The marching kernels get them as
+// template flags instead (FIXED = true; launch_march picks the instance): no load or store then sits under
+// a branch (the compiler's wait counts stay exact) and the unused operand costs no registers.
+template <bool FIXED = false, bool SUB = true>
+struct EpiJacobiT {   // x = (b - R x)/D in residual form (solve.py:158)
     const double* xin;
     const double* b;
     const double* diag;
     const double* sub;
     double* xout;
     struct P { double x, b, dg, s; };
+    __device__ bool has_sub() const { return FIXED ? SUB : sub != nullptr; }
     __device__ P pre(int32_t r) const { return {xin[r], ld_stream(b + r), diag ? diag[r] : 0.0, sub ? ld_stream(sub + r) : 0.0}; }
     // x_in and diag supplied by the caller (set_x / set_diag)
-    __device__ P pre_lite(int32_t r) const { return {0.0, ld_stream(b + r), 0.0, sub ? ld_stream(sub + r) : 0.0}; }
+    __device__ P pre_lite(int32_t r) const { return {0.0, ld_stream(b + r), 0.0, has_sub() ? ld_stream(sub + r) : 0.0}; }
     template <bool NT = false>
     __device__ void apply(int32_t r, double acc, const P& p) const {
         const double x = p.x + (p.b - acc) / p.dg;
-        st_stream<NT>(xout + r, sub ? p.s - x : x);
+        st_stream<NT>(xout + r, has_sub() ? p.s - x : x);
     }
     __device__ void operator()(int32_t r, double acc, const P& p) const { apply<false>(r, acc, p); }
 };
-struct EpiCheb {
+template <bool FIXED = false, bool SUB = true, bool SD = true>
+struct EpiChebT {
     const double* xin;
     const double* b;
     const double* diag;
@@ -645,21 +642,24 @@ struct EpiCheb {
     double* xout;
     int store_d = 1;   // 0: the inner solve's last sweep (its direction is never read again)
     struct P { double x, b, dg, d, s; };
+    __device__ bool has_sub() const { return FIXED ? SUB : sub != nullptr; }
+    __device__ bool stores_d() const { return FIXED ? SD : store_d != 0; }
     __device__ P pre(int32_t r) const { return {xin[r], ld_stream(b + r), diag ? diag[r] : 0.0, ld_stream(d + r), sub ? ld_stream(sub + r) : 0.0}; }
-    __device__ P pre_lite(int32_t r) const { return {0.0, ld_stream(b + r), 0.0, ld_stream(d + r), sub ? ld_stream(sub + r) : 0.0}; }
+    __device__ P pre_lite(int32_t r) const { return {0.0, ld_stream(b + r), 0.0, ld_stream(d + r), has_sub() ? ld_stream(sub + r) : 0.0}; }
     template <bool NT = false>
     __device__ void apply(int32_t r, double acc, const P& p) const {
         const double z = (p.b - acc) / p.dg;
         const double dn = c1 * p.d + c2 * z;
-        if (store_d) st_stream<NT>(d + r, dn);
+        if (stores_d()) st_stream<NT>(d + r, dn);
         const double x = p.x + dn;
-        st_stream<NT>(xout + r, sub ? p.s - x : x);
+        st_stream<NT>(xout + r, has_sub() ? p.s - x : x);
     }
     __device__ void operator()(int32_t r, double acc, const P& p) const { apply<false>(r, acc, p); }
 };
 // EpiCheb for the first sweep after x0 = d0 = c2[0] b / diag: the previous direction is the staged x0
 // itself (x and diag supplied by the stencil via set_x / set_diag), so d is written but not read.
-struct EpiChebFirst {
+template <bool FIXED = false, bool SUB = true, bool SD = true>
+struct EpiChebFirstT {
     const double* b;
     double* d;
     double c1, c2;
@@ -667,18 +667,46 @@ struct EpiChebFirst {
     double* xout;
     int store_d = 1;
     struct P { double x, b, dg, s; };
+    __device__ bool has_sub() const { return FIXED ? SUB : sub != nullptr; }
+    __device__ bool stores_d() const { return FIXED ? SD : store_d != 0; }
     __device__ P pre(int32_t r) const { return {0.0, ld_stream(b + r), 0.0, sub ? ld_stream(sub + r) : 0.0}; }
-    __device__ P pre_lite(int32_t r) const { return {0.0, ld_stream(b + r), 0.0, sub ? ld_stream(sub + r) : 0.0}; }
+    __device__ P pre_lite(int32_t r) const { return {0.0, ld_stream(b + r), 0.0, has_sub() ? ld_stream(sub + r) : 0.0}; }
     template <bool NT = false>
     __device__ void apply(int32_t r, double acc, const P& p) const {
         const double z = (p.b - acc) / p.dg;
         const double dn = c1 * p.x + c2 * z;
-        if (store_d) st_stream<NT>(d + r, dn);
+        if (stores_d()) st_stream<NT>(d + r, dn);
         const double x = p.x + dn;
-        st_stream<NT>(xout + r, sub ? p.s - x : x);
+        st_stream<NT>(xout + r, has_sub() ? p.s - x : x);
     }
     __device__ void operator()(int32_t r, double acc, const P& p) const { apply<false>(r, acc, p); }
 };
+using EpiJacobi = EpiJacobiT<>;
+using EpiCheb = EpiChebT<>;
+using EpiChebFirst = EpiChebFirstT<>;
+
+// Run fn with the epilogue's run-time switches turned into template flags (other epilogues unchanged).
+template <class Epi, class Fn>
+__host__ inline int with_fixed_epi(const Epi& e, Fn&& fn) { return fn(e); }
+template <class Fn>
+__host__ inline int with_fixed_epi(const EpiJacobi& e, Fn&& fn) {
+    return e.sub ? fn(EpiJacobiT<true, true>{e.xin, e.b, e.diag, e.sub, e.xout})
+                 : fn(EpiJacobiT<true, false>{e.xin, e.b, e.diag, e.sub, e.xout});
+}
+template <class Fn>
+__host__ inline int with_fixed_epi(const EpiCheb& e, Fn&& fn) {
+#define MPBP_CHEB(SUB, SD) fn(EpiChebT<true, SUB, SD>{e.xin, e.b, e.diag, e.d, e.c1, e.c2, e.sub, e.xout, e.store_d})
+    return e.sub ? (e.store_d ? MPBP_CHEB(true, true) : MPBP_CHEB(true, false))
+                 : (e.store_d ? MPBP_CHEB(false, true) : MPBP_CHEB(false, false));
+#undef MPBP_CHEB
+}
+template <class Fn>
+__host__ inline int with_fixed_epi(const EpiChebFirst& e, Fn&& fn) {
+#define MPBP_CHEBF(SUB, SD) fn(EpiChebFirstT<true, SUB, SD>{e.b, e.d, e.c1, e.c2, e.sub, e.xout, e.store_d})
+    return e.sub ? (e.store_d ? MPBP_CHEBF(true, true) : MPBP_CHEBF(true, false))
+                 : (e.store_d ? MPBP_CHEBF(false, true) : MPBP_CHEBF(false, false));
+#undef MPBP_CHEBF
+}
 
 // XI entry xi * a * (1 - a) as the assembly evaluates it (left to right).
 __device__ inline double xi_of(double xi, double a) { return xi * a * (1.0 - a); }
@@ -699,82 +727,6 @@ template <>
 __device__ inline void set_diag<EpiAdd::P>(EpiAdd::P&, double) {}
 template <>
 __device__ inline void set_diag<EpiResid::P>(EpiResid::P&, double) {}
-
-// CSR SpMV over a list of row blocks.  Phase 1 streams the block's [row_ptr[r0], row_ptr[r1])
-// slice of col_idx / val with 16-byte loads (fully coalesced across the workgroup), gathers x
-// and stages the products in LDS; phase 2 gives each row to one lane, which sums its products
-// left to right (a segmented reduction with sequential order -> bit-exact with the oracle) and
-// runs the fused epilogue.
-template <class Epi>
-__global__ void __launch_bounds__(kBlock) k_csr_rows(Csr A, const double* __restrict__ x,
-                                                     const int2* __restrict__ blocks, int nblocks,
-                                                     Epi epi) {
-    __shared__ double prod[kCap];
-    const int b = xcd_swizzle(blockIdx.x, nblocks);
-    const int2 blk = blocks[b];
-    const int32_t r0 = blk.x, r1 = blk.y;
-    const int32_t s = A.rp[r0], e = A.rp[r1];
-    const int tid = threadIdx.x;
-    const int32_t base = s & ~1;
-    if (e - base <= kCap) {
-        const int32_t r = r0 + tid;
-        const bool live = r < r1;
-        int32_t ks = 0, ke = 0;
-        typename Epi::P pe{};
-        if (live) {
-            ks = A.rp[r] - s;
-            ke = A.rp[r + 1] - s;
-            pe = epi.pre(r);
-        }
-        double2 v[kPairs];
-        int2 cc[kPairs];
-#pragma unroll
-        for (int j = 0; j < kPairs; ++j) {
-            const int32_t k = base + 2 * (tid + j * kBlock);
-            if (k + 1 < e) {
-                v[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const double2*>(A.va + k));
-                cc[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const int2*>(A.ci + k));
-            } else if (k < e) {
-                v[j] = make_double2(A.va[k], 0.0);
-                cc[j] = make_int2(A.ci[k], 0);
-            } else {
-                v[j] = make_double2(0.0, 0.0);
-                cc[j] = make_int2(0, 0);
-            }
-        }
-        double x0[kPairs], x1[kPairs];
-#pragma unroll
-        for (int j = 0; j < kPairs; ++j) {
-            const int32_t k = base + 2 * (tid + j * kBlock);
-            x0[j] = (k >= s && k < e) ? x[cc[j].x] : 0.0;
-            x1[j] = (k + 1 >= s && k + 1 < e) ? x[cc[j].y] : 0.0;
-        }
-#pragma unroll
-        for (int j = 0; j < kPairs; ++j) {
-            const int32_t k = base + 2 * (tid + j * kBlock);
-            if (k >= s && k < e) prod[k - s] = v[j].x * x0[j];
-            if (k + 1 >= s && k + 1 < e) prod[k + 1 - s] = v[j].y * x1[j];
-        }
-        __syncthreads();
-        if (live) {
-            double acc = 0.0;
-            for (int32_t k = ks; k < ke; ++k) acc += prod[k];
-            epi.template apply<MPBP_CSR_NT != 0>(r, acc, pe);
-        }
-    } else {
-        // A single row longer than the LDS stage (the planner never groups such a row).
-        // Tree-reduced: not in sequential order.
-        double part = 0.0;
-        for (int32_t k = s + tid; k < e; k += kBlock) part += A.va[k] * x[A.ci[k]];
-        prod[tid] = part;
-        __syncthreads();
-        for (int w = kBlock / 2; w > 0; w >>= 1) {
-            if (tid < w) prod[tid] += prod[tid + w];
-            __syncthreads();
-        }
-        if (tid == 0) epi(r0, prod[0], epi.pre(r0));
-    }
-}
 
 // CSR SpMV over the same row blocks, one wavefront per 64-row quarter of a block and no block-wide
 // barrier.  Each wave streams its rows' [row_ptr[ra], row_ptr[rb]) entries in chunks of kWaveCap with
@@ -988,130 +940,6 @@ __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __rest
     if (live) epi.template apply<MPBP_CSR_NT != 0>(r, acc, pe);
 }
 
-// k_csr_wave with SEGS consecutive row blocks per workgroup and the next block's matrix chunk
-// prefetched: as soon as a wave has moved its chunk into LDS, its (now free) chunk registers receive the
-// loads of its quarter of the next row block, so that stream is in flight during this block's x gathers
-// and sums instead of after them (a wave's life was load -> wait -> gather -> wait -> store, with LDS
-// capping occupancy at 4 waves per SIMD).  Same per-row order of additions as k_csr_wave: bit-exact.
-#ifndef MPBP_CSR_SEGS
-#define MPBP_CSR_SEGS 4
-#endif
-constexpr int kRowBatchPf = 6;   // pairs of a row gathered at once (a 12-entry velocity row: one batch)
-template <class Epi, int SEGS>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) k_csr_wave_pf(Csr A, const double* __restrict__ x,
-                                                        const int2* __restrict__ blocks, int nblocks,
-                                                        Epi epi) {
-    __shared__ double2 vstage[kBlock / 64][kWaveCap / 2];
-    __shared__ int2 cstage[kBlock / 64][kWaveCap / 2];
-    const int nwg = (nblocks + SEGS - 1) / SEGS;
-    const int g = xcd_swizzle(blockIdx.x, nwg);
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    double2* vs = vstage[w];
-    int2* cs = cstage[w];
-    const double* vs1 = reinterpret_cast<const double*>(vs);
-    const int32_t* cs1 = reinterpret_cast<const int32_t*>(cs);
-    const int b_end = min(g * SEGS + SEGS, nblocks);
-    // this wave's rows of block b: [ra, rb), or false when the block has no rows for it
-    auto seg = [&](int b, int32_t& ra, int32_t& rb) -> bool {
-        const int2 blk = blocks[b];
-        ra = blk.x + 64 * w;
-        rb = min(ra + 64, blk.y);
-        return ra < blk.y;
-    };
-    double2 v[kWavePairs];
-    int2 cc[kWavePairs];
-    auto load_chunk = [&](int32_t cb, int32_t e) {
-#pragma unroll
-        for (int j = 0; j < kWavePairs; ++j) {
-            const int32_t k = cb + 2 * (lane + 64 * j);
-            if (k + 1 < e) {
-                v[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const double2*>(A.va + k));
-                cc[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const int2*>(A.ci + k));
-            } else if (k < e) {
-                v[j] = make_double2(A.va[k], 0.0);
-                cc[j] = make_int2(A.ci[k], 0);
-            } else {
-                v[j] = make_double2(0.0, 0.0);
-                cc[j] = make_int2(0, 0);
-            }
-        }
-    };
-    int b = g * SEGS;
-    int32_t ra = 0, rb = 0;
-    while (b < b_end && !seg(b, ra, rb)) ++b;
-    if (b >= b_end) return;   // waves are independent: no workgroup barrier below
-    int32_t s = A.rp[ra], e = A.rp[rb];
-    load_chunk(s & ~1, e);
-    bool staged = false;      // LDS holds an earlier chunk whose reads must finish before the next store
-    for (;;) {
-        const int32_t r = ra + lane;
-        const bool live = r < rb;
-        int32_t ks = 0, ke = 0;
-        typename Epi::P pe{};
-        if (live) {
-            ks = A.rp[r];
-            ke = A.rp[r + 1];
-            pe = epi.pre(r);
-        }
-        int nb = b + 1;
-        int32_t nra = 0, nrb = 0;
-        while (nb < b_end && !seg(nb, nra, nrb)) ++nb;
-        const bool more = nb < b_end;
-        int32_t ns = 0, ne = 0;
-        if (more) {
-            ns = A.rp[nra];
-            ne = A.rp[nrb];
-        }
-        double acc = 0.0;
-        if (s >= e && more) load_chunk(ns & ~1, ne);   // rows all empty: no chunk, prefetch right away
-        for (int32_t cb = s & ~1; cb < e; cb += kWaveCap) {
-            if (cb != (s & ~1)) load_chunk(cb, e);   // further chunks of long rows: loaded in place
-            if (staged) wave_lds_sync();
-            staged = true;
-#pragma unroll
-            for (int j = 0; j < kWavePairs; ++j) {
-                vs[lane + 64 * j] = v[j];
-                cs[lane + 64 * j] = cc[j];
-            }
-            wave_lds_sync();
-            if (more && cb + kWaveCap >= e) load_chunk(ns & ~1, ne);   // prefetch the next block's chunk
-            int32_t t = max(ks, cb) - cb;
-            const int32_t tend = min(ke, cb + kWaveCap) - cb;
-            if ((t & 1) && t < tend) {
-                acc += vs1[t] * x[cs1[t]];
-                ++t;
-            }
-            for (; t < tend; t += 2 * kRowBatchPf) {
-                const int32_t p0 = t >> 1;
-                int2 c[kRowBatchPf];
-                double x0[kRowBatchPf], x1[kRowBatchPf];
-#pragma unroll
-                for (int i = 0; i < kRowBatchPf; ++i) c[i] = (t + 2 * i < tend) ? cs[p0 + i] : make_int2(0, 0);
-#pragma unroll
-                for (int i = 0; i < kRowBatchPf; ++i) {
-                    x0[i] = (t + 2 * i < tend) ? x[c[i].x] : 0.0;
-                    x1[i] = (t + 2 * i + 1 < tend) ? x[c[i].y] : 0.0;
-                }
-#pragma unroll
-                for (int i = 0; i < kRowBatchPf; ++i) {
-                    if (t + 2 * i < tend) {
-                        const double2 q = vs[p0 + i];
-                        acc += q.x * x0[i];
-                        if (t + 2 * i + 1 < tend) acc += q.y * x1[i];
-                    }
-                }
-            }
-        }
-        if (live) epi.template apply<MPBP_CSR_NT != 0>(r, acc, pe);
-        if (!more) break;
-        b = nb;
-        ra = nra;
-        rb = nrb;
-        s = ns;
-        e = ne;
-    }
-}
-
 // ------------------------------------------------------------------ SELL-64 ----
 // Sliced ELLPACK with one wavefront per slice: a slice is <= 64 consecutive rows, its entries
 // stored column-major in pairs -- pair-row j of the slice holds entries (2j, 2j+1) of every row,
@@ -1183,33 +1011,58 @@ __global__ void __launch_bounds__(kBlock) k_sell_rows(Sell S, const double* __re
 // ------------------------------------------------------------- F stencil ----
 // Matrix-free rows of F = XI + d_u blockdiag(eta_n L_n, eta_s L_s): the ten entries of a row are
 // recomputed from the thn tables (L1/L2-resident) with exactly the assembly's arithmetic
-// (phase_L_row / F_row above), sorted by column with fixed sorting networks, and summed in that
-// order -- the same IEEE operations as a sweep over the assembled F, without streaming its
-// 12 bytes x 10 entries per row from HBM.  Needs n >= 3 (no coinciding periodic neighbours).
-struct Ent {
-    int32_t c;   // phase-local global column: the sort key (CSR order of the assembled row)
-    double v, x;
+// (phase_L_row / F_row above) and their products summed in the assembled row's column order -- the same
+// IEEE operations as a sweep over the assembled F, without streaming its 12 bytes x 10 entries per row
+// from HBM.  Needs n >= 3 (no coinciding periodic neighbours).
+//
+// Column order on the periodic edge.  A stencil's products are listed in the interior's sorted-column order;
+// on the grid's edge a wrapped neighbour moves (row -1 -> n-1 sorts last, row n -> 0 first, and likewise for
+// columns).  Instead of sorting, the edge form adds every product at each position it can occupy, with the
+// positions it does not occupy on this lane contributing -0.0 -- the exact identity of IEEE addition in
+// round-to-nearest (x + -0.0 == x for every x, signed zeros included) -- so the sum performs exactly the
+// sorted row's additions, with no sorting network and the same code on every lane.
+struct Wrap {
+    bool r0, rl, c0, cl;   // the cell's grid row is 0 / n-1, its column 0 / n-1
 };
-
-__device__ inline void cx(Ent& a, Ent& b) {   // compare-exchange by column, field-wise selects
-    const bool s = a.c > b.c;
-    const int32_t c0 = s ? b.c : a.c, c1 = s ? a.c : b.c;
-    const double v0 = s ? b.v : a.v, v1 = s ? a.v : b.v;
-    const double x0 = s ? b.x : a.x, x1 = s ? a.x : b.x;
-    a.c = c0; a.v = v0; a.x = x0;
-    b.c = c1; b.v = v1; b.x = x1;
+__device__ inline double opt(bool c, double p) { return c ? p : -0.0; }
+// Five-point products p = {N, W, C, E, S} (interior column order), added to acc in the row's column order.
+template <bool EDGE>
+__device__ inline double add5(double acc, const double* p, const Wrap& w) {
+    if constexpr (!EDGE) {
+#pragma unroll
+        for (int t = 0; t < 5; ++t) acc += p[t];
+        return acc;
+    }
+    acc += opt(w.rl, p[4]);    // S wrapped to row 0: first
+    acc += opt(!w.r0, p[0]);   // N
+    acc += opt(w.cl, p[3]);    // E wrapped to column 0: before W
+    acc += opt(!w.c0, p[1]);   // W
+    acc += p[2];               // C
+    acc += opt(!w.cl, p[3]);   // E
+    acc += opt(w.c0, p[1]);    // W wrapped to column n-1: after E
+    acc += opt(!w.rl, p[4]);   // S
+    acc += opt(w.r0, p[0]);    // N wrapped to row n-1: last
+    return acc;
 }
-__device__ inline void sort4(Ent* e) {
-    cx(e[0], e[1]); cx(e[2], e[3]); cx(e[0], e[2]); cx(e[1], e[3]); cx(e[1], e[2]);
-}
-__device__ inline void sort5(Ent* e) {
-    cx(e[0], e[1]); cx(e[3], e[4]); cx(e[2], e[4]); cx(e[2], e[3]); cx(e[1], e[4]);
-    cx(e[0], e[3]); cx(e[0], e[2]); cx(e[1], e[3]); cx(e[1], e[2]);
-}
-template <int K>
-__device__ inline void sortk(Ent* e) {
-    if constexpr (K == 4) sort4(e);
-    else sort5(e);
+// 2 x 2 block products p = {a_lo, a_hi, b_lo, b_hi} (rows a above b, columns lo left of hi): the lower row
+// comes first when it wraps (bwrap), the high column first when the pair wraps (cwrap).
+template <bool EDGE>
+__device__ inline double add4(double acc, const double* p, bool bwrap, bool cwrap) {
+    if constexpr (!EDGE) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc += p[t];
+        return acc;
+    }
+    acc += opt(bwrap && cwrap, p[3]);
+    acc += opt(bwrap, p[2]);
+    acc += opt(bwrap && !cwrap, p[3]);
+    acc += opt(cwrap, p[1]);
+    acc += p[0];
+    acc += opt(!cwrap, p[1]);
+    acc += opt(!bwrap && cwrap, p[3]);
+    acc += opt(!bwrap, p[2]);
+    acc += opt(!bwrap && !cwrap, p[3]);
+    return acc;
 }
 
 // Offset of local grid row lr (-h <= lr < L + h) of field f in an nf-field vector of the row-partition
@@ -1275,8 +1128,8 @@ __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, cons
     auto emul = [&](double y) -> double { return eta1 ? y : eta * y; };          // eta * y
     const int fu = 2 * p, fv = 2 * p + 1;
     const int32_t kc = VIRT ? P.wrap(gr) * n + P.wrap(gc) : gr * n + gc;   // VIRT: (gr, gc) may lie one cell outside
-    auto key = [&](int r, int c) -> int32_t { return EDGE ? P.wrap(r) * n + P.wrap(c) : r * n + c; };
     auto T = [&](int r, int c) -> double { return ta.T(p, r, c); };
+    const Wrap w{gr == 0, gr == n - 1, gc == 0, gc == n - 1};   // read by the EDGE form only
     double acc = 0.0;
     const double xcross = xa.X(f ^ 2, gr, gc);
     if ((f & 1) == 0) {   // u row: preconditioner.py:100-179
@@ -1288,26 +1141,25 @@ __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, cons
         const double iph_j = 0.5 * (tij + tip1j);
         const double xi_ii = xi_of(P.xi, iph_j);
         const double th = face ? face[0] : P.uface[kc];   // face: thn at the u / v face, loaded ahead
-        const double w = p ? P.c * (1.0 - th) : P.c * th;
+        const double wt = p ? P.c * (1.0 - th) : P.c * th;
         const double Ldiag = idx2 * (-tip1j - tij) + idx2 * (-iph_jph - iph_jmh);
-        const double fd = (w - dmul(xi_ii)) + dmul(emul(Ldiag));
+        const double fd = (wt - dmul(xi_ii)) + dmul(emul(Ldiag));
         *fdiag = fd;
-        Ent lo[5] = {Ent{key(gr - 1, gc), dmul(emul(idx2 * (iph_jph))), xa.X(fu, gr - 1, gc)},
-                     Ent{key(gr, gc - 1), dmul(emul(idx2 * (tij))), xa.X(fu, gr, gc - 1)},
-                     Ent{key(gr, gc), fd, xa.X(fu, gr, gc)},
-                     Ent{key(gr, gc + 1), dmul(emul(P.pow2 ? tip1j * idx2 : tip1j / P.dxdx)), xa.X(fu, gr, gc + 1)},
-                     Ent{key(gr + 1, gc), dmul(emul(idx2 * (iph_jmh))), xa.X(fu, gr + 1, gc)}};
-        Ent hi[4] = {Ent{key(gr, gc - 1), dmul(emul(idx2 * (tij - iph_jph))), xa.X(fv, gr, gc - 1)},
-                     Ent{key(gr, gc), dmul(emul(idx2 * (-tip1j + iph_jph))), xa.X(fv, gr, gc)},
-                     Ent{key(gr + 1, gc - 1), dmul(emul(idx2 * (iph_jmh - tij))), xa.X(fv, gr + 1, gc - 1)},
-                     Ent{key(gr + 1, gc), dmul(emul(idx2 * (tip1j - iph_jmh))), xa.X(fv, gr + 1, gc)}};
-        if (EDGE) { sort5(lo); sort4(hi); }
+        // same field: N, W, C, E, S; the other component (v of this phase): (gr, gc-1), (gr, gc), (gr+1, gc-1),
+        // (gr+1, gc)
+        const double lo[5] = {dmul(emul(idx2 * (iph_jph))) * xa.X(fu, gr - 1, gc),
+                              dmul(emul(idx2 * (tij))) * xa.X(fu, gr, gc - 1),
+                              fd * xa.X(fu, gr, gc),
+                              dmul(emul(P.pow2 ? tip1j * idx2 : tip1j / P.dxdx)) * xa.X(fu, gr, gc + 1),
+                              dmul(emul(idx2 * (iph_jmh))) * xa.X(fu, gr + 1, gc)};
+        const double hi[4] = {dmul(emul(idx2 * (tij - iph_jph))) * xa.X(fv, gr, gc - 1),
+                              dmul(emul(idx2 * (-tip1j + iph_jph))) * xa.X(fv, gr, gc),
+                              dmul(emul(idx2 * (iph_jmh - tij))) * xa.X(fv, gr + 1, gc - 1),
+                              dmul(emul(idx2 * (tip1j - iph_jmh))) * xa.X(fv, gr + 1, gc)};
         const double vcross = dmul(xi_ii);
         if (p == 1) acc += vcross * xcross;
-#pragma unroll
-        for (int t = 0; t < 5; ++t) acc += lo[t].v * lo[t].x;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc += hi[t].v * hi[t].x;
+        acc = add5<EDGE>(acc, lo, w);
+        acc = add4<EDGE>(acc, hi, w.rl, w.c0);
         if (p == 0) acc += vcross * xcross;
     } else {              // v row: preconditioner.py:182-295
         const double tij = T(gr, gc), tip1j = T(gr, gc + 1);
@@ -1316,176 +1168,30 @@ __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, cons
         const double ip1_jph = 0.5 * (tij + tijp1);
         const double xi_ii = xi_of(P.xi, ip1_jph);
         const double th = face ? face[1] : P.vface[kc];
-        const double w = p ? P.c * (1.0 - th) : P.c * th;
+        const double wt = p ? P.c * (1.0 - th) : P.c * th;
         const double imh_jph = 0.25 * (tim1j + tim1jp1 + tij + tijp1);
         const double iph_jph = 0.25 * (tij + tip1j + tijp1 + tip1jp1);
         const double Ldiag = P.midy2 * (tijp1 + tij) - idx2 * (iph_jph + imh_jph);
-        const double fd = (w - dmul(xi_ii)) + dmul(emul(Ldiag));
+        const double fd = (wt - dmul(xi_ii)) + dmul(emul(Ldiag));
         *fdiag = fd;
-        Ent lo[4] = {Ent{key(gr - 1, gc), dmul(emul(idx2 * (tijp1 - imh_jph))), xa.X(fu, gr - 1, gc)},
-                     Ent{key(gr - 1, gc + 1), dmul(emul(idx2 * (iph_jph - tijp1))), xa.X(fu, gr - 1, gc + 1)},
-                     Ent{key(gr, gc), dmul(emul(idx2 * (imh_jph - tij))), xa.X(fu, gr, gc)},
-                     Ent{key(gr, gc + 1), dmul(emul(idx2 * (tij - iph_jph))), xa.X(fu, gr, gc + 1)}};
-        Ent hi[5] = {Ent{key(gr - 1, gc), dmul(emul(idx2 * tijp1)), xa.X(fv, gr - 1, gc)},
-                     Ent{key(gr, gc - 1), dmul(emul(idx2 * imh_jph)), xa.X(fv, gr, gc - 1)},
-                     Ent{key(gr, gc), fd, xa.X(fv, gr, gc)},
-                     Ent{key(gr, gc + 1), dmul(emul(idx2 * iph_jph)), xa.X(fv, gr, gc + 1)},
-                     Ent{key(gr + 1, gc), dmul(emul(idx2 * tij)), xa.X(fv, gr + 1, gc)}};
-        if (EDGE) { sort4(lo); sort5(hi); }
+        // the other component (u of this phase): (gr-1, gc), (gr-1, gc+1), (gr, gc), (gr, gc+1); same field: N, W,
+        // C, E, S
+        const double lo[4] = {dmul(emul(idx2 * (tijp1 - imh_jph))) * xa.X(fu, gr - 1, gc),
+                              dmul(emul(idx2 * (iph_jph - tijp1))) * xa.X(fu, gr - 1, gc + 1),
+                              dmul(emul(idx2 * (imh_jph - tij))) * xa.X(fu, gr, gc),
+                              dmul(emul(idx2 * (tij - iph_jph))) * xa.X(fu, gr, gc + 1)};
+        const double hi[5] = {dmul(emul(idx2 * tijp1)) * xa.X(fv, gr - 1, gc),
+                              dmul(emul(idx2 * imh_jph)) * xa.X(fv, gr, gc - 1),
+                              fd * xa.X(fv, gr, gc),
+                              dmul(emul(idx2 * iph_jph)) * xa.X(fv, gr, gc + 1),
+                              dmul(emul(idx2 * tij)) * xa.X(fv, gr + 1, gc)};
         const double vcross = dmul(xi_ii);
         if (p == 1) acc += vcross * xcross;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc += lo[t].v * lo[t].x;
-#pragma unroll
-        for (int t = 0; t < 5; ++t) acc += hi[t].v * hi[t].x;
+        acc = add4<EDGE>(acc, lo, w.r0, w.cl);
+        acc = add5<EDGE>(acc, hi, w);
         if (p == 0) acc += vcross * xcross;
     }
     return acc;
-}
-
-// Accessors reading global memory directly (k_f_stencil: one row per thread).
-struct TGlobal {
-    const FStencilDev& P;
-    __device__ double T(int s, int gr, int gc) const {
-        const double v = P.cell[P.wrap(gr) * P.n + P.wrap(gc)];
-        return s ? 1.0 - v : v;
-    }
-};
-struct XGlobal {
-    const FStencilDev& P;
-    const double* __restrict__ x;
-    __device__ double X(int f, int gr, int gc) const { return x[P.xrow(f, gr) + P.wrap(gc)]; }
-};
-
-// Thread t -> owned local row: which = 0 all rows, 1 rows off the first / last owned grid row of a
-// field (they read no ghost), 2 rows on those grid rows.
-__device__ inline bool f_stencil_rowof(const FStencilDev& P, int64_t t, int32_t* r) {
-    const int n = P.n, L = P.L;
-    int f, lr, gc;
-    if (P.which == 0) {
-        if (t >= (int64_t)4 * L * n) return false;
-        const int32_t q = (int32_t)t;
-        f = q / (L * n);
-        const int32_t rem = q - f * L * n;
-        lr = rem / n;
-        gc = rem - lr * n;
-    } else if (P.which == 1) {
-        const int Li = L - 2;
-        if (Li <= 0 || t >= (int64_t)4 * Li * n) return false;
-        const int32_t q = (int32_t)t;
-        f = q / (Li * n);
-        const int32_t rem = q - f * Li * n;
-        lr = 1 + rem / n;
-        gc = rem - (lr - 1) * n;
-    } else {
-        const int nb = L >= 2 ? 2 : 1;
-        if (t >= (int64_t)4 * nb * n) return false;
-        const int32_t q = (int32_t)t;
-        f = q / (nb * n);
-        const int32_t rem = q - f * nb * n;
-        const int side = rem / n;
-        gc = rem - side * n;
-        lr = side ? L - 1 : 0;
-    }
-    *r = (f * L + lr) * n + gc;
-    return true;
-}
-
-// One row per thread, every operand from global memory (reference form of the F stencil).
-template <class Epi>
-__global__ void __launch_bounds__(kBlock) k_f_stencil(FStencilDev P, const double* __restrict__ x, Epi epi) {
-    const int b = xcd_swizzle(blockIdx.x, gridDim.x);
-    int32_t r;
-    if (!f_stencil_rowof(P, (int64_t)b * kBlock + threadIdx.x, &r)) return;
-    typename Epi::P pe = epi.pre(r);
-    const int n = P.n;
-    const int f = r / (P.L * n);
-    const int32_t rem = r - f * P.L * n;
-    const int lr = rem / n, gc = rem - lr * n, gr = P.r0 + lr;
-    double fd;
-    const TGlobal ta{P};
-    const XGlobal xa{P, x};
-    const bool edge = gr == 0 || gr == n - 1 || gc == 0 || gc == n - 1;
-    const double acc = edge ? f_row<true>(P, f, gr, gc, ta, xa, &fd) : f_row<false>(P, f, gr, gc, ta, xa, &fd);
-    set_diag(pe, fd);
-    epi(r, acc, pe);
-}
-
-// ---- LDS-tiled cell kernel: one workgroup = 256 consecutive cells of one owned grid row, one thread
-// per cell computing that cell's 4 rows (u_n, v_n, u_s, v_s).  The workgroup first stages, with
-// coalesced loads, the rows gr-1, gr, gr+1 of x for all four fields and of the thn table (columns
-// c0-1 .. c0+256, wrapped) in LDS; every neighbour is then an LDS read.  Each x / thn value crosses
-// L2 -> CU once per workgroup instead of ~10 times per row.
-constexpr int kTileW = kBlock + 2;
-
-struct TLds {
-    const double* t;   // [3][kTileW]
-    int gr0, c0;       // grid row and first column of the tile
-    __device__ double T(int s, int gr, int gc) const {
-        const double v = t[(gr - gr0 + 1) * kTileW + (gc - c0 + 1)];
-        return s ? 1.0 - v : v;
-    }
-};
-struct XLds {
-    const double* x;   // [4][3][kTileW]
-    int gr0, c0;
-    __device__ double X(int f, int gr, int gc) const { return x[(f * 3 + (gr - gr0 + 1)) * kTileW + (gc - c0 + 1)]; }
-};
-
-template <class Epi>
-__global__ void __launch_bounds__(kBlock) k_f_cells(FStencilDev P, const double* __restrict__ x, Epi epi) {
-    __shared__ double sx[4 * 3 * kTileW];
-    __shared__ double st[3 * kTileW];
-    const int n = P.n, L = P.L;
-    const int strips = (n + kBlock - 1) / kBlock;
-    const int b = xcd_swizzle(blockIdx.x, gridDim.x);
-    const int strip = b % strips, rsel = b / strips;
-    const int lr = P.which == 0 ? rsel : P.which == 1 ? 1 + rsel : (rsel == 0 ? 0 : L - 1);
-    const int gr = P.r0 + lr;
-    const int c0 = strip * kBlock;
-    const int tid = threadIdx.x;
-    // stage x (4 fields x 3 rows) and thn (3 rows), columns c0-1 .. c0+256: per tile row one
-    // wave-uniform base (scalar unit) and one coalesced load per thread (+2 halo columns)
-    const int colA = c0 - 1 + tid;                         // tile column tid
-    const bool okA = colA <= n;
-    const int gcA = P.wrap(colA);
-    const bool extra = tid < 2;                            // tile columns 256, 257
-    const int colB = c0 + kBlock - 1 + tid;
-    const bool okB = extra && colB <= n;
-    const int gcB = P.wrap(colB < n ? colB : (colB == n ? n : 0));
-#pragma unroll
-    for (int row = 0; row < 12; ++row) {
-        const int f = row / 3, dr = row - f * 3 - 1;
-        const int32_t base = P.xrow(f, gr + dr);
-        sx[row * kTileW + tid] = okA ? x[base + gcA] : 0.0;
-        if (extra) sx[row * kTileW + kBlock + tid] = okB ? x[base + gcB] : 0.0;
-    }
-#pragma unroll
-    for (int row = 0; row < 3; ++row) {
-        const int32_t base = P.wrap(gr + row - 1) * n;
-        st[row * kTileW + tid] = okA ? P.cell[base + gcA] : 0.0;
-        if (extra) st[row * kTileW + kBlock + tid] = okB ? P.cell[base + gcB] : 0.0;
-    }
-    const int gc = c0 + tid;
-    const bool live = gc < n;
-    typename Epi::P pe[4];
-    if (live) {
-#pragma unroll
-        for (int f = 0; f < 4; ++f) pe[f] = epi.pre_lite((f * L + lr) * n + gc);
-    }
-    __syncthreads();
-    if (!live) return;
-    const TLds ta{st, gr, c0};
-    const XLds xa{sx, gr, c0};
-    const bool edge = gr == 0 || gr == n - 1 || gc == 0 || gc == n - 1;
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-        double fd;
-        const double acc = edge ? f_row<true>(P, f, gr, gc, ta, xa, &fd) : f_row<false>(P, f, gr, gc, ta, xa, &fd);
-        set_x(pe[f], xa.X(f, gr, gc));
-        set_diag(pe[f], fd);
-        epi((f * L + lr) * n + gc, acc, pe[f]);
-    }
 }
 
 // ---- marching kernels: a workgroup owns a 256-column strip of `rows` consecutive grid rows and walks
@@ -1519,52 +1225,114 @@ struct TRing {
     }
 };
 
+// Staged sources: load(i) issues the loads of element i (raw registers, nothing consumes them yet), value(raw)
+// turns them into the staged value at LDS-store time -- so a tile row's loads stay in flight through the
+// previous row's compute even when the staged value needs arithmetic (XInit's division).  load_uniform(i) is the
+// same for a wave-uniform index: scalar loads (constant address space) into SGPRs, for the tile's two right-hand
+// halo columns, which every lane of a workgroup shares -- no VGPRs held for them between load and store.
+typedef __attribute__((address_space(4))) const double cdouble;
+__device__ inline double ld_uniform(const double* p, int32_t i) {
+    return ((cdouble*)p)[__builtin_amdgcn_readfirstlane(i)];
+}
 struct XPlain {        // staged value = x[i]
     const double* __restrict__ x;
+    typedef double Raw;
+    __device__ Raw load(int32_t i) const { return x[i]; }
+    __device__ Raw load_uniform(int32_t i) const { return ld_uniform(x, i); }
+    __device__ double value(const Raw& r) const { return r; }
     __device__ double operator()(int32_t i) const { return x[i]; }
+};
+struct XInitRaw {
+    double b, d;
 };
 struct XInit {         // staged value = the first inner iterate: c2 * (b[i] / diag[i]) (c2 = 1: Jacobi)
     const double* __restrict__ b;
     const double* __restrict__ dg;
     double c2;
+#ifdef MPBP_EXP_XINIT_EARLY   // experiment: divide at load time (the loads are then waited for at once)
+    typedef double Raw;
+    __device__ Raw load(int32_t i) const { return c2 * (b[i] / dg[i]); }
+    __device__ Raw load_uniform(int32_t i) const { return c2 * (ld_uniform(b, i) / ld_uniform(dg, i)); }
+    __device__ double value(const Raw& r) const { return r; }
+#else
+    typedef XInitRaw Raw;
+    __device__ Raw load(int32_t i) const { return {b[i], dg[i]}; }
+    __device__ Raw load_uniform(int32_t i) const { return {ld_uniform(b, i), ld_uniform(dg, i)}; }
+    __device__ double value(const Raw& r) const { return c2 * (r.b / r.d); }
+#endif
     __device__ double operator()(int32_t i) const { return c2 * (b[i] / dg[i]); }
 };
 
-// Row of tile values held in registers between its global load and its LDS store.
-template <int NF>
+// Row of tile values held between its loads and its LDS store: every lane's main column (xa, ta; tile columns
+// c0-1 .. c0+254) in VGPRs, the two halo columns c0+255 and c0+256 (h*, scalar) in SGPRs.
+#ifndef MPBP_HALO_SCALAR
+#define MPBP_HALO_SCALAR 0
+#endif
+template <int NF, class Raw>
 struct TileRow {
-    double xa[NF], ta, xb[NF], tb;
+    Raw xa[NF], h0[NF];
+#if MPBP_HALO_SCALAR
+    Raw h1[NF];
+    double ta, t0, t1;
+#else
+    double ta, t0;
+#endif
+};
+
+// Columns of the strip's right-hand halo (tile columns kMB, kMB + 1) and whether they exist.
+struct HaloCols {
+    int g0, g1;     // wrapped grid columns
+    bool ok0, ok1;  // inside the grid or its periodic right neighbour (column n -> 0)
+    int gl;         // this lane's halo column (lanes 0, 1: g0, g1; others re-read their main column, cached)
 };
 
 template <class S, class XS>
-__device__ inline void load_tile_row(const S& P, const XS& xs, int gr, int gcA, bool okA, int gcB, bool okB,
-                                     TileRow<S::NF>& tr) {
-    // the main column's loads unconditional from a clamped column, then a select (no branch: the waits
-    // stay counted, so the row's loads remain in flight through the next compute); the 2 halo lanes' ones
-    // under their predicate
+__device__ inline void load_tile_row(const S& P, const XS& xs, int gr, int gcA, bool okA, const HaloCols& hc,
+                                     TileRow<S::NF, typename XS::Raw>& tr) {
+    // Every load unconditional (lanes without a column of their own read a clamped one): no branch around a
+    // load, so the compiler's wait counts stay exact and the row's loads remain in flight through the next
+    // compute.  The selects happen at the LDS store (store_tile_row).
     const int ca = okA ? gcA : 0;
 #pragma unroll
     for (int f = 0; f < S::NF; ++f) {
         const int32_t base = P.xrow(f, gr);
-        const double va = xs(base + ca);
-        tr.xa[f] = okA ? va : 0.0;
-        tr.xb[f] = okB ? xs(base + gcB) : 0.0;
+        tr.xa[f] = xs.load(base + ca);
+#if MPBP_HALO_SCALAR
+        tr.h0[f] = xs.load_uniform(base + hc.g0);
+        tr.h1[f] = xs.load_uniform(base + hc.g1);
+#else
+        tr.h0[f] = xs.load(base + hc.gl);
+#endif
     }
     const int32_t tb = P.wrap(gr) * P.n;
-    const double ta = P.cell[tb + ca];
-    tr.ta = okA ? ta : 0.0;
-    tr.tb = okB ? P.cell[tb + gcB] : 0.0;
+    tr.ta = P.cell[tb + ca];
+#if MPBP_HALO_SCALAR
+    tr.t0 = ld_uniform(P.cell, tb + hc.g0);
+    tr.t1 = ld_uniform(P.cell, tb + hc.g1);
+#else
+    tr.t0 = P.cell[tb + hc.gl];
+#endif
 }
 
-template <int NF>
-__device__ inline void store_tile_row(double* sx, double* st, int slot, int tid, bool extra, const TileRow<NF>& tr) {
+template <class XS, int NF>
+__device__ inline void store_tile_row(const XS& xs, double* sx, double* st, int slot, int tid, bool okA,
+                                      const HaloCols& hc, const TileRow<NF, typename XS::Raw>& tr) {
 #pragma unroll
-    for (int f = 0; f < NF; ++f) {
-        sx[(f * 3 + slot) * kMTileW + tid] = tr.xa[f];
-        if (extra) sx[(f * 3 + slot) * kMTileW + kMB + tid] = tr.xb[f];
+    for (int f = 0; f < NF; ++f) sx[(f * 3 + slot) * kMTileW + tid] = okA ? xs.value(tr.xa[f]) : 0.0;
+    st[slot * kMTileW + tid] = okA ? tr.ta : 0.0;
+    if (tid < 2) {   // lanes 0 and 1 store the halo columns
+        const bool ok = tid == 0 ? hc.ok0 : hc.ok1;
+#if MPBP_HALO_SCALAR
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+            sx[(f * 3 + slot) * kMTileW + kMB + tid] = ok ? xs.value(tid == 0 ? tr.h0[f] : tr.h1[f]) : 0.0;
+        st[slot * kMTileW + kMB + tid] = ok ? (tid == 0 ? tr.t0 : tr.t1) : 0.0;
+#else
+#pragma unroll
+        for (int f = 0; f < NF; ++f) sx[(f * 3 + slot) * kMTileW + kMB + tid] = ok ? xs.value(tr.h0[f]) : 0.0;
+        st[slot * kMTileW + kMB + tid] = ok ? tr.t0 : 0.0;
+#endif
     }
-    st[slot * kMTileW + tid] = tr.ta;
-    if (extra) st[slot * kMTileW + kMB + tid] = tr.tb;
 }
 
 // Grid rows [la, lb) of workgroup chunk `chunk` of `nchunks`: which = 0 all owned rows, 1 rows 1 .. L-2 (no
@@ -1602,23 +1370,32 @@ k_march(S P, XS xs, int nchunks, Epi epi) {
     const int colA = c0 - 1 + tid;
     const bool okA = colA <= n;
     const int gcA = P.wrap(colA);
-    const bool extra = tid < 2;
-    const int colB = c0 + kMB - 1 + tid;
-    const bool okB = extra && colB <= n;
-    const int gcB = P.wrap(colB < n ? colB : (colB == n ? n : 0));
+    // the right-hand halo columns c0+255, c0+256 (the grid's last column's periodic neighbour is column 0)
+    HaloCols hc;
+    {
+        const int b0 = c0 + kMB - 1, b1 = c0 + kMB;
+        hc.ok0 = b0 <= n;
+        hc.ok1 = b1 <= n;
+        hc.g0 = b0 < n ? b0 : 0;
+        hc.g1 = b1 < n ? b1 : 0;
+        hc.gl = tid == 0 ? hc.g0 : tid == 1 ? hc.g1 : (okA ? gcA : 0);
+    }
     const int gc = c0 + tid;
     const bool live = gc < n;
     // prologue: rows la-1 -> slot 0, la -> slot 1; row la+1 in registers -- all three requested at once
-    TileRow<NF> tr, tp0, tp1;
-    load_tile_row(P, xs, P.r0 + la - 1, gcA, okA, gcB, okB, tp0);
-    load_tile_row(P, xs, P.r0 + la, gcA, okA, gcB, okB, tp1);
-    load_tile_row(P, xs, P.r0 + la + 1, gcA, okA, gcB, okB, tr);
-    store_tile_row(sx, st, 0, tid, extra, tp0);
-    store_tile_row(sx, st, 1, tid, extra, tp1);
-    for (int lr = la; lr < lb; ++lr) {
+    typedef TileRow<NF, typename XS::Raw> TR;
+    TR tr, tp0, tp1;
+    load_tile_row(P, xs, P.r0 + la - 1, gcA, okA, hc, tp0);
+    load_tile_row(P, xs, P.r0 + la, gcA, okA, hc, tp1);
+    load_tile_row(P, xs, P.r0 + la + 1, gcA, okA, hc, tr);
+    store_tile_row(xs, sx, st, 0, tid, okA, hc, tp0);
+    store_tile_row(xs, sx, st, 1, tid, okA, hc, tp1);
+    // One step: row lr+1 into the ring, the next row's loads issued (LOAD: every step but the last, which is
+    // peeled off so that no load sits under a branch), row lr computed from LDS.
+    auto step = [&](int lr, auto load_next) {
         const int k = lr - la;
         const int sm = k % 3, s0 = (k + 1) % 3, sp = (k + 2) % 3;
-        store_tile_row(sx, st, sp, tid, extra, tr);          // row lr+1
+        store_tile_row(xs, sx, st, sp, tid, okA, hc, tr);   // row lr+1
         // operands of this row's epilogues and cells, requested unconditionally (lanes past the grid edge
         // read row 0 and discard it) so the wait counts stay exact and later loads stay in flight
         const int gcl = live ? gc : 0;
@@ -1627,14 +1404,18 @@ k_march(S P, XS xs, int nchunks, Epi epi) {
         for (int o = 0; o < NO; ++o) pe[o] = epi.pre_lite(P.out_row(o, lr, gcl));
         const typename S::Cell cl = P.cell_pre(P.wrap(P.r0 + lr), gcl);   // ghost rows wrap periodically
         __syncthreads();
-        if (lr + 1 < lb) load_tile_row(P, xs, P.r0 + lr + 2, gcA, okA, gcB, okB, tr);   // in flight
+        if constexpr (decltype(load_next)::value) load_tile_row(P, xs, P.r0 + lr + 2, gcA, okA, hc, tr);
         if (live) {
             const int gr = P.wrap(P.r0 + lr);
             const XRing xa{sx, {sm, s0, sp}, gr, c0};
             const TRing ta{st, {sm, s0, sp}, gr, c0};
             // the wrap-aware (sorting) form is exact for interior cells too: take it for the whole wave when
             // any of its cells is on the periodic edge, so a wave never runs both forms
+#ifdef MPBP_EXP_NO_EDGE   // timing experiment only (wrong results on the periodic edge)
+            const bool edge = false;
+#else
             const bool edge = __builtin_amdgcn_readfirstlane(__any(gr == 0 || gr == n - 1 || gc == 0 || gc == n - 1)) != 0;
+#endif
 #pragma unroll
             for (int o = 0; o < NO; ++o) {
                 double dg;
@@ -1646,7 +1427,9 @@ k_march(S P, XS xs, int nchunks, Epi epi) {
             }
         }
         __syncthreads();                                     // slot sm is rewritten next step
-    }
+    };
+    for (int lr = la; lr < lb - 1; ++lr) step(lr, std::true_type{});
+    step(lb - 1, std::false_type{});
 }
 
 // Workgroups of one k_march instance the device holds at once (occupancy x CUs), queried once.
@@ -1669,7 +1452,7 @@ int64_t march_capacity() {
 // rows_per_block or rows_per_block + 1 rows): a second round of a few workgroups would cost almost a whole
 // sweep's latency (ghost-row launches of the CA schedule, multi-GPU row partitions).
 template <class S, class XS, class Epi>
-int launch_march(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStream_t st) {
+int launch_march_fixed(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStream_t st) {
     const int64_t grows = P.which == 0 ? P.L : P.which == 1 ? (P.L > 2 ? P.L - 2 : 0)
                           : P.which == 3 ? P.L + 2 * P.ext : (P.L >= 2 ? 2 : 1);
     if (grows == 0) return MPBP_OK;
@@ -1682,6 +1465,11 @@ int launch_march(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStrea
     k_march<S, XS, Epi><<<(unsigned)(chunks * strips), kMB, 0, st>>>(P, xs, (int)chunks, epi);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
+}
+
+template <class S, class XS, class Epi>
+int launch_march(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStream_t st) {
+    return with_fixed_epi(epi, [&](const auto& e) { return launch_march_fixed(P, xs, e, rows_per_block, st); });
 }
 
 // F row of field f at a cell (k_march policy).
@@ -1840,350 +1628,15 @@ struct GtGStencilDev : PGDev {
         double e[5];
         entries(vr, vc, gr, gc, ta, e);
         *dg = e[2];
-        Ent s[5] = {Ent{EDGE ? wrap(gr - 1) * n + gc : (gr - 1) * n + gc, e[0], xa.X(0, vr - 1, vc)},
-                    Ent{EDGE ? gr * n + wrap(gc - 1) : gr * n + gc - 1, e[1], xa.X(0, vr, vc - 1)},
-                    Ent{gr * n + gc, e[2], xa.X(0, vr, vc)},
-                    Ent{EDGE ? gr * n + wrap(gc + 1) : gr * n + gc + 1, e[3], xa.X(0, vr, vc + 1)},
-                    Ent{EDGE ? wrap(gr + 1) * n + gc : (gr + 1) * n + gc, e[4], xa.X(0, vr + 1, vc)}};
-        if (EDGE) sort5(s);
-        double acc = 0.0;
-#pragma unroll
-        for (int t = 0; t < 5; ++t) acc += s[t].v * s[t].x;
-        return acc;
+        const double p[5] = {e[0] * xa.X(0, vr - 1, vc), e[1] * xa.X(0, vr, vc - 1), e[2] * xa.X(0, vr, vc),
+                             e[3] * xa.X(0, vr, vc + 1), e[4] * xa.X(0, vr + 1, vc)};
+        return add5<EDGE>(0.0, p, Wrap{gr == 0, gr == n - 1, gc == 0, gc == n - 1});
     }
     template <bool EDGE, class TA, class XA>
     __device__ double row(int, int gr, int gc, const TA& ta, const XA& xa, double* dg, const Cell&) const {
         return apply_v<EDGE>(gr, gc, gr, gc, ta, xa, dg);
     }
 };
-
-// ---- a whole Gt_G inner solve in one pass (temporal blocking) ----------------------------------------
-// Sweeps 1 .. S of a Chebyshev / Jacobi solve from x0 = c2_0 (b / diag) (recomputed from b and diag, no
-// init pass): level s (sweep s) is computed one grid row behind level s-1, levels 0 .. S-1 live in 4-row
-// LDS rings and never touch HBM, so the solve reads b, diag and thn and writes x_S -- ~32 B per pressure
-// row instead of ~136 for the init pass and S single sweeps.  A workgroup marches down a 256-column strip;
-// level s covers S-s halo columns each side (lanes 0 .. 2(S-1)-1 compute those cells in a second pass and
-// keep each halo column's direction in registers) and S-s halo rows above and below the chunk.  Every
-// cell is computed with the single-sweep arithmetic (apply_v, EpiChebFirst / EpiCheb / EpiJacobi
-// formulas): results are bit-identical to the unfused solve.  One GPU, S <= n.
-// Measured on MI355X at 1024^2 (4-sweep Chebyshev, S = 3): 68 us per solve at 8 rows per workgroup (the
-// unfused init-fused sweep + 2 sweeps: 17.5 + 2 x 13.5 = 44.5 us); 4 / 2 / 16 rows are slower too -- the
-// three barriers per row step and the doubled level-1 rows leave it latency-bound -- so it is off by
-// default (mpbp_set_pressure_solve_fusion).
-struct GtgSolveArgs {
-    const double* b;
-    const double* diag;
-    double c2_0;            // x0 = c2_0 * (b / diag)   (1.0: Jacobi)
-    double c1[8], c2[8];    // sweep s uses c1[s], c2[s] (Chebyshev)
-    const double* sub;      // x_out = sub - x_S when set
-    double* x_out;
-};
-
-template <int W, int OFF>
-struct PRing4 {             // one field, rows in slot (row + 8) & 3, virtual column c at c - c0 + OFF
-    const double* x;
-    int c0;
-    __device__ double X(int, int r, int c) const { return x[((r + 8) & 3) * W + (c - c0 + OFF)]; }
-};
-template <int W, int OFF, int TS>
-struct PThetaRing {         // thn rows in slot (row + 2 TS) % TS
-    const double* t;
-    int c0;
-    __device__ double T(int sph, int r, int c) const {
-        const double v = t[((r + 2 * TS) % TS) * W + (c - c0 + OFF)];
-        return sph ? 1.0 - v : v;
-    }
-};
-
-template <int S, bool CHEB>
-__global__ void __launch_bounds__(kMB) k_gtg_solve(GtGStencilDev P, GtgSolveArgs a, int rows_per_block) {
-    constexpr int W = kMB + 2 * S;   // virtual columns c0-S .. c0+256+S-1
-    constexpr int TS = S + 3;        // thn ring slots (rows k-S .. k+1 live, one of slack)
-    __shared__ double lv[S * 4 * W];   // levels 0 .. S-1
-    __shared__ double th[TS * W];
-    const int n = P.n;
-    const int strips = (n + kMB - 1) / kMB;
-    const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
-    const int strip = bid % strips, chunk = bid / strips;
-    const int la = chunk * rows_per_block, lb = min(la + rows_per_block, n);
-    if (la >= lb) return;
-    const int c0 = strip * kMB, tid = threadIdx.x;
-    auto vw = [&](int v) { return v < 0 ? v + n : (v >= n ? v - n : v); };   // |offset| <= S <= n
-    // staging of level 0 (x0 from b, diag) and thn: tile column tid <-> virtual column c0-S+tid, threads
-    // 0 .. 2S-1 also c0+256-S+tid; virtual columns beyond n-1+S are never read by a needed cell
-    const int colA = c0 - S + tid, colB = c0 + kMB - S + tid;
-    const bool okA = colA <= n - 1 + S, okB = tid < 2 * S && colB <= n - 1 + S;
-    const int gcA = okA ? vw(colA) : 0, gcB = okB ? vw(colB) : 0;
-    double x0A = 0.0, x0B = 0.0, tA = 0.0, tB = 0.0;   // the row in flight
-    auto load_row = [&](int r) {
-        const int32_t base = vw(r) * n;
-        const double bA = a.b[base + gcA], dA = a.diag[base + gcA], thA = P.cell[base + gcA];
-        x0A = okA ? a.c2_0 * (bA / dA) : 0.0;
-        tA = okA ? thA : 0.0;
-        if (okB) {
-            x0B = a.c2_0 * (a.b[base + gcB] / a.diag[base + gcB]);
-            tB = P.cell[base + gcB];
-        }
-    };
-    auto stage_row = [&](int r) {
-        lv[((r + 8) & 3) * W + tid] = x0A;
-        th[((r + 2 * TS) % TS) * W + tid] = tA;
-        if (okB) {
-            lv[((r + 8) & 3) * W + kMB + tid] = x0B;
-            th[((r + 2 * TS) % TS) * W + kMB + tid] = tB;
-        }
-    };
-    // cells of this thread: main column c0+tid at every level; halo columns (lanes 0 .. 2(S-1)-1):
-    // lane j-1 -> c0-j, lane S-2+j -> c0+255+j (j = 1 .. S-1), computed at levels s <= S-j
-    const int cm = c0 + tid;
-    const int hj = tid < S - 1 ? tid + 1 : (tid < 2 * (S - 1) ? tid - (S - 1) + 1 : 0);
-    const int ch = tid < S - 1 ? c0 - hj : c0 + kMB - 1 + hj;
-    double dm_old[S + 1], dh_old[S + 1];   // direction of level s at its previous row (main / halo column)
-#pragma unroll
-    for (int s = 0; s <= S; ++s) { dm_old[s] = 0.0; dh_old[s] = 0.0; }
-    const int k0 = la - (S - 1), k1 = lb - 1 + (S - 1);
-    {   // prologue: rows k0-1, k0 staged, k0+1 in flight
-        load_row(k0 - 1);
-        stage_row(k0 - 1);
-        load_row(k0);
-        stage_row(k0);
-        load_row(k0 + 1);
-    }
-    for (int k = k0; k <= k1; ++k) {
-        // b of every level's cells this step (row k - (s-1)); L2-resident after the first level reads it
-        double bm[S + 1], bh[S + 1];
-#pragma unroll
-        for (int s = 1; s <= S; ++s) {
-            const int r = k - (s - 1);
-            const bool rowok = r >= la - (S - s) && r <= lb - 1 + (S - s);   // then |r wrap offset| <= S <= n
-            bm[s] = rowok ? a.b[vw(r) * n + (cm <= n - 1 + (S - s) ? vw(cm) : 0)] : 0.0;
-            bh[s] = (rowok && hj > 0 && hj <= S - s) ? a.b[vw(r) * n + vw(ch)] : 0.0;
-        }
-        const double subv = a.sub ? a.sub[(k - (S - 1) >= 0 && k - (S - 1) < n ? k - (S - 1) : 0) * n +
-                                          (cm < n ? cm : 0)] : 0.0;
-        stage_row(k + 1);
-        __syncthreads();
-        if (k + 2 <= k1 + 1) load_row(k + 2);   // in flight
-        double dm_new[S + 1], dh_new[S + 1];
-#pragma unroll
-        for (int s = 1; s <= S; ++s) {
-            const int r = k - (s - 1);                   // this level's row
-            const bool rowok = r >= la - (S - s) && r <= lb - 1 + (S - s);
-            const PRing4<W, S> xa{lv + (s - 1) * 4 * W, c0};
-            const PThetaRing<W, S, TS> ta{th, c0};
-            // main column
-            const bool needm = rowok && cm <= n - 1 + (S - s);
-            const int gr = vw(r);
-            double xn = 0.0, dn = 0.0;
-            if (needm) {
-                const int gc = vw(cm);
-                const bool edge = __builtin_amdgcn_readfirstlane(
-                    __any(gr == 0 || gr == n - 1 || gc == 0 || gc == n - 1)) != 0;
-                double dg;
-                const double acc = edge ? P.template apply_v<true>(r, cm, gr, gc, ta, xa, &dg)
-                                        : P.template apply_v<false>(r, cm, gr, gc, ta, xa, &dg);
-                const double xc = xa.X(0, r, cm);
-                if constexpr (CHEB) {
-                    const double z = (bm[s] - acc) / dg;
-                    dn = a.c1[s] * (s == 1 ? xc : dm_old[s - 1]) + a.c2[s] * z;
-                    xn = xc + dn;
-                } else {
-                    xn = xc + (bm[s] - acc) / dg;
-                }
-            }
-            // halo column (second pass of the first lanes)
-            double xhn = 0.0, dhn = 0.0;
-            const bool needh = rowok && hj > 0 && hj <= S - s && !(tid >= S - 1 && ch > n - 1 + (S - s));
-            if (needh) {
-                const int gc = vw(ch);
-                double dg;
-                const double acc = P.template apply_v<true>(r, ch, gr, gc, ta, xa, &dg);
-                const double xc = xa.X(0, r, ch);
-                if constexpr (CHEB) {
-                    const double z = (bh[s] - acc) / dg;
-                    dhn = a.c1[s] * (s == 1 ? xc : dh_old[s - 1]) + a.c2[s] * z;
-                    xhn = xc + dhn;
-                } else {
-                    xhn = xc + (bh[s] - acc) / dg;
-                }
-            }
-            dm_new[s] = dn;
-            dh_new[s] = dhn;
-            if (s < S) {
-                if (needm) lv[(s * 4 + ((r + 8) & 3)) * W + (cm - c0 + S)] = xn;
-                if (needh) lv[(s * 4 + ((r + 8) & 3)) * W + (ch - c0 + S)] = xhn;
-                __syncthreads();
-            } else if (needm && r >= la && r < lb && cm < n) {
-                st_stream(a.x_out + r * n + cm, a.sub ? subv - xn : xn);
-            }
-        }
-#pragma unroll
-        for (int s = 1; s <= S; ++s) { dm_old[s] = dm_new[s]; dh_old[s] = dh_new[s]; }
-    }
-}
-
-
-// ---- two sweeps in one pass (temporal blocking): the first two sweeps of an F inner solve ----------
-// Level 0 is the solve's x0 = d0 = c2_0 (b / diag) recomputed from b and diag (no init pass); level 1
-// (sweep 1) is computed one grid row ahead of level 2 (sweep 2) and kept in an LDS ring, so x1 and d1
-// never touch HBM: the two sweeps read b, diag and thn and write x2 (+ d2) -- 24-32 B per row instead
-// of ~72.  A workgroup marches down a 256-column strip; level 1 covers one halo column each side
-// (wave 0 computes those two cells in a second pass) and one halo row above and below the chunk,
-// level 0 two.  Each cell is computed with exactly the single-sweep arithmetic (f_row, EpiChebFirst /
-// EpiCheb / EpiJacobi formulas): the results are bit-identical to init + sweep 1 + sweep 2.
-// One GPU (whole grid), n >= 3.  Rings: level 0 and level 1 four rows, thn five, so a workgroup
-// needs only two barriers per row (a fast wave may stage the next row while others finish this one).
-// Measured on MI355X at 1024^2 (R = 8): 163 us against 61 + 46 us for the fused-init sweep and the plain
-// sweep it replaces -- 205 VGPRs and 77 KiB of LDS leave 2 waves per SIMD, and wave 0's halo pass
-// doubles its level-1 work -- so it is off by default (mpbp_set_sweep_fusion).
-constexpr int kW0 = kMB + 4;   // level 0 / thn tile: virtual columns c0-2 .. c0+257
-constexpr int kW1 = kMB + 2;   // level 1 tile: virtual columns c0-1 .. c0+256
-
-template <int W, int OFF>
-struct XRing4 {                // rows in slot (row + 8) & 3; column c at c - c0 + OFF
-    const double* x;
-    int gr, c0;
-    __device__ double X(int f, int r, int c) const { return x[(f * 4 + ((r + 8) & 3)) * W + (c - c0 + OFF)]; }
-};
-struct TRing5 {                // thn rows in slot (row + 10) % 5
-    const double* t;
-    int gr, c0;
-    __device__ double T(int sph, int r, int c) const {
-        const double v = t[((r + 10) % 5) * kW0 + (c - c0 + 2)];
-        return sph ? 1.0 - v : v;
-    }
-};
-
-struct Sweep2Args {
-    const double* b;
-    const double* diag;   // the inner solve's diag (x0 = c2_0 * (b / diag))
-    double c2_0;          // 1.0 for Jacobi
-    double c1a, c2a;      // sweep 1 (Chebyshev)
-    double c1b, c2b;      // sweep 2 (Chebyshev)
-    double* d_out;        // sweep 2 direction (Chebyshev, when store_d)
-    int store_d;
-    const double* sub;    // sweep 2 result: x_out = sub - x (the solve's last sweep)
-    double* x_out;
-};
-
-// The four F rows at (gr, gc) swept once: xn = x + d with d = c1 dprev + c2 (b - F x) / diag(F)
-// (Chebyshev; dprev = the staged x itself when FIRST) or xn = x + (b - F x) / diag(F) (Jacobi).
-template <bool CHEB, bool FIRST, class TA, class XA>
-__device__ inline void f_sweep_cell(const FStencilDev& P, int gr, int gc, const TA& ta, const XA& xa,
-                                    const double* bb, const double* dprev, double c1, double c2, double* xn,
-                                    double* dn) {
-    const int n = P.n;
-    const bool edge = __builtin_amdgcn_readfirstlane(__any(gr <= 0 || gr >= n - 1 || gc <= 0 || gc >= n - 1)) != 0;
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-        double fd;
-        const double acc = edge ? f_row<true, TA, XA, true>(P, f, gr, gc, ta, xa, &fd)
-                                : f_row<false>(P, f, gr, gc, ta, xa, &fd);
-        const double xc = xa.X(f, gr, gc);
-        if constexpr (CHEB) {
-            const double z = (bb[f] - acc) / fd;
-            const double d = c1 * (FIRST ? xc : dprev[f]) + c2 * z;
-            dn[f] = d;
-            xn[f] = xc + d;
-        } else {
-            xn[f] = xc + (bb[f] - acc) / fd;
-        }
-    }
-}
-
-template <bool CHEB>
-__global__ void __launch_bounds__(kMB) k_f_sweep2(FStencilDev P, Sweep2Args a, int rows_per_block) {
-    __shared__ double s0[4 * 4 * kW0];   // level 0: [field][slot][col]
-    __shared__ double s1[4 * 4 * kW1];   // level 1
-    __shared__ double st[5 * kW0];       // thn
-    const int n = P.n;
-    const int strips = (n + kMB - 1) / kMB;
-    const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
-    const int strip = bid % strips, chunk = bid / strips;
-    const int la = chunk * rows_per_block, lb = min(la + rows_per_block, n);
-    if (la >= lb) return;
-    const int c0 = strip * kMB, tid = threadIdx.x;
-    const XInit xs{a.b, a.diag, a.c2_0};
-    // staging: tile column tid <-> virtual column c0-2+tid; threads 0..3 also c0+254+tid
-    const int colA = c0 - 2 + tid, colB = c0 + kMB - 2 + tid;
-    const bool okA = colA <= n + 1, extra = tid < 4, okB = extra && colB <= n + 1;
-    const int gcA = okA ? P.wrap(colA) : 0, gcB = okB ? P.wrap(colB) : 0;
-    auto stage = [&](int r, const TileRow<4>& tr) {
-        const int sx = (r + 8) & 3, sth = (r + 10) % 5;
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-            s0[(f * 4 + sx) * kW0 + tid] = tr.xa[f];
-            if (extra) s0[(f * 4 + sx) * kW0 + kMB + tid] = tr.xb[f];
-        }
-        st[sth * kW0 + tid] = tr.ta;
-        if (extra) st[sth * kW0 + kMB + tid] = tr.tb;
-    };
-    // level-1 cells of this thread: column c0+tid (needed up to column n, the right halo of n-1), and
-    // for threads 0 / 1 the halo columns c0-1 / c0+256
-    const int c1m = c0 + tid;
-    const bool need1 = c1m <= n;
-    const int c1h = tid == 0 ? c0 - 1 : c0 + kMB;
-    const bool needh = (tid == 0) || (tid == 1 && c0 + kMB <= n);
-    const int c2c = c0 + tid;
-    const bool live2 = c2c < n;
-    auto vidx = [&](int f, int r, int c) -> int32_t { return (f * n + P.wrap(r)) * n + P.wrap(c); };
-    // prologue: level-0 / thn rows la-2, la-1 staged, row la in registers
-    TileRow<4> tr, tp0, tp1;
-    load_tile_row(P, xs, la - 2, gcA, okA, gcB, okB, tp0);
-    load_tile_row(P, xs, la - 1, gcA, okA, gcB, okB, tp1);
-    load_tile_row(P, xs, la, gcA, okA, gcB, okB, tr);
-    stage(la - 2, tp0);
-    stage(la - 1, tp1);
-    double d1prev[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int k = la - 1; k <= lb; ++k) {
-        // operands of this step, requested before the barrier: b at level-1 row k, b (+ sub) at level-2 row k-1
-        double b1[4], b2[4], s2[4];
-        const bool lev2 = k - 1 >= la && live2;
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-            b1[f] = need1 ? a.b[vidx(f, k, c1m)] : 0.0;
-            b2[f] = lev2 ? a.b[(f * n + k - 1) * n + c2c] : 0.0;
-            s2[f] = (lev2 && a.sub) ? a.sub[(f * n + k - 1) * n + c2c] : 0.0;
-        }
-        stage(k + 1, tr);
-        __syncthreads();
-        if (k + 2 <= lb + 1) load_tile_row(P, xs, k + 2, gcA, okA, gcB, okB, tr);   // in flight
-        const XRing4<kW0, 2> x0a{s0, k, c0};
-        const TRing5 tha{st, k, c0};
-        double xn[4], dn[4];
-        if (need1) {   // level 1 (sweep 1) at row k
-            f_sweep_cell<CHEB, true>(P, k, c1m, tha, x0a, b1, nullptr, a.c1a, a.c2a, xn, dn);
-#pragma unroll
-            for (int f = 0; f < 4; ++f) s1[(f * 4 + ((k + 8) & 3)) * kW1 + (c1m - c0 + 1)] = xn[f];
-        }
-        if (tid < 2 && needh) {   // its halo cells (wave 0, second pass)
-            double bh[4];
-#pragma unroll
-            for (int f = 0; f < 4; ++f) bh[f] = a.b[vidx(f, k, c1h)];
-            double xh[4], dh[4];
-            f_sweep_cell<CHEB, true>(P, k, c1h, tha, x0a, bh, nullptr, a.c1a, a.c2a, xh, dh);
-#pragma unroll
-            for (int f = 0; f < 4; ++f) s1[(f * 4 + ((k + 8) & 3)) * kW1 + (c1h - c0 + 1)] = xh[f];
-        }
-        __syncthreads();
-        if (lev2) {   // level 2 (sweep 2) at row k-1
-            const XRing4<kW1, 1> x1a{s1, k - 1, c0};
-            const TRing5 thb{st, k - 1, c0};
-            double xo[4], dout[4];
-            f_sweep_cell<CHEB, false>(P, k - 1, c2c, thb, x1a, b2, d1prev, a.c1b, a.c2b, xo, dout);
-#pragma unroll
-            for (int f = 0; f < 4; ++f) {
-                const int32_t r = (f * n + k - 1) * n + c2c;
-                if (CHEB && a.store_d) st_stream(a.d_out + r, dout[f]);
-                st_stream(a.x_out + r, a.sub ? s2[f] - xo[f] : xo[f]);
-            }
-        }
-        if (CHEB) {
-#pragma unroll
-            for (int f = 0; f < 4; ++f) d1prev[f] = dn[f];
-        }
-    }
-}
 
 // One thread per (slice, lane): copy the CSR row into its column-major slots.
 __global__ void k_sell_fill(Csr A, const int4* slices, int nslices, uint8_t* rlen, double* val, int32_t* col) {
@@ -2225,15 +1678,8 @@ inline Csr to_csr(const mpbp_csr* A) { return Csr{A->row_ptr, A->col_idx, A->val
 template <class Epi>
 int launch_rows(const mpbp_csr* A, const mpbp_rowblocks* blk, const double* x, Epi epi, hipStream_t st) {
     if (!blk || blk->count <= 0) return MPBP_OK;
-    if (g_csr_kind == 2)
-        k_csr_wave_pf<Epi, MPBP_CSR_SEGS><<<(blk->count + MPBP_CSR_SEGS - 1) / MPBP_CSR_SEGS, kBlock, 0, st>>>(
-            to_csr(A), x, reinterpret_cast<const int2*>(blk->pairs), blk->count, epi);
-    else if (g_csr_kind == 1)
-        k_csr_wave<Epi><<<blk->count, kBlock, 0, st>>>(to_csr(A), x, reinterpret_cast<const int2*>(blk->pairs),
-                                                        blk->count, epi);
-    else
-        k_csr_rows<Epi><<<blk->count, kBlock, 0, st>>>(to_csr(A), x, reinterpret_cast<const int2*>(blk->pairs),
-                                                        blk->count, epi);
+    k_csr_wave<Epi><<<blk->count, kBlock, 0, st>>>(to_csr(A), x, reinterpret_cast<const int2*>(blk->pairs),
+                                                    blk->count, epi);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
@@ -2280,29 +1726,9 @@ extern "C" {
 
 const char* mpbp_version(void) { return "libmpbp 0.1 (gfx950)"; }
 
-int mpbp_set_stencil_kind(int32_t kind) {
-    // kind: 0 cells, 1 rows, 2 + R (R >= 1): marching cells, R grid rows per workgroup (2 -> R = 4)
-    if (kind < 0) return set_error(MPBP_ERR_ARG, "stencil kind must be 0 (cells), 1 (rows) or 2+R (march)");
-    g_stencil_kind = kind > 2 ? 2 : kind;
-    if (kind > 2) g_march_rows = kind - 2;
-    else if (kind == 2) g_march_rows = 4;
-    return MPBP_OK;
-}
-int mpbp_set_pressure_solve_fusion(int32_t rows) {
-    if (rows < 0 || rows > 4096) return set_error(MPBP_ERR_ARG, "pressure solve fusion rows must be in [0, 4096]");
-    g_gtg_solve_rows = rows;
-    return MPBP_OK;
-}
-int mpbp_set_csr_kernel(int32_t kind) {
-    if (kind < 0 || kind > 2)
-        return set_error(MPBP_ERR_ARG, "csr kernel must be 0 (workgroup-staged), 1 (per-wave) or 2 (per-wave, "
-                                       "prefetching, several row blocks per workgroup)");
-    g_csr_kind = kind;
-    return MPBP_OK;
-}
-int mpbp_set_sweep_fusion(int32_t rows) {
-    if (rows < 0 || rows > 4096) return set_error(MPBP_ERR_ARG, "sweep fusion rows must be in [0, 4096]");
-    g_sweep2_rows = rows;
+int mpbp_set_march_rows(int32_t rows) {
+    if (rows < 1 || rows > 4096) return set_error(MPBP_ERR_ARG, "march rows must be in [1, 4096]");
+    g_march_rows = rows;
     return MPBP_OK;
 }
 const char* mpbp_last_error(void) { return g_err; }
@@ -2730,19 +2156,7 @@ static int make_fstencil(const mpbp_stokes_params* prm, const double* cell, cons
 namespace {
 template <class Epi>
 int launch_fstencil(const FStencilDev& P, const double* x, Epi epi, hipStream_t st) {
-    if (g_stencil_kind == 2)   // marching LDS ring
-        return with_f_identities(P, [&](const auto& Q) { return launch_march(Q, XPlain{x}, epi, g_march_rows, st); });
-    if (P.which == 3) return set_error(MPBP_ERR_ARG, "f_stencil: ghost-row (which = 3) launches need the marching kernel");
-    const int64_t grows = P.which == 0 ? P.L : P.which == 1 ? (P.L > 2 ? P.L - 2 : 0) : (P.L >= 2 ? 2 : 1);
-    if (grows == 0) return MPBP_OK;
-    if (g_stencil_kind != 1) {   // LDS-tiled cells
-        const int64_t blocks = grows * ((P.n + kBlock - 1) / kBlock);
-        k_f_cells<Epi><<<(unsigned)blocks, kBlock, 0, st>>>(P, x, epi);
-    } else {                     // one row per thread, global operands
-        k_f_stencil<Epi><<<grid_for(4 * grows * P.n), kBlock, 0, st>>>(P, x, epi);
-    }
-    MPBP_HIP(hipGetLastError());
-    return MPBP_OK;
+    return with_f_identities(P, [&](const auto& Q) { return launch_march(Q, XPlain{x}, epi, g_march_rows, st); });
 }
 
 }  // namespace
@@ -2963,7 +2377,7 @@ struct OpPair {
 bool can_fuse_init(const OpPair& op) {
     const OpRef& o = op.in;
     return o.stencil && !o.stencil->halo && !o.empty && op.bd.empty && o.which == 0 &&
-           (o.sop == SOP_GTG || (o.sop == SOP_F && g_stencil_kind == 2));
+           (o.sop == SOP_GTG || o.sop == SOP_F);
 }
 
 int op_first_sweep(const OpRef& o, bool cheb, const double* b, const double* diag, double c2_0, double c1, double c2,
@@ -2986,56 +2400,6 @@ int op_first_sweep(const OpRef& o, bool cheb, const double* b, const double* dia
     const GtGStencilDev S{P};
     return cheb ? launch_march(S, xs, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, pg_rows(), st)
                 : launch_march(S, xs, EpiJacobi{nullptr, b, nullptr, sub, xo}, pg_rows(), st);
-}
-
-// Sweeps 1 and 2 of an F inner solve from x0 = d0 = c2_0 b / diag in one pass (k_f_sweep2).
-int op_first_two_sweeps(const OpRef& o, bool cheb, const double* b, const double* diag, const double* c1,
-                        const double* c2, double* d, const double* sub, double* xo, hipStream_t st, int store_d) {
-    const mpbp_schur_plan* p = o.stencil;
-    FStencilDev P;
-    const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &P);
-    if (rc) return rc;
-    const Sweep2Args a{b, diag, cheb ? c2[0] : 1.0, c1[1], c2[1], c1[2], c2[2], d, store_d, sub, xo};
-    const int R = g_sweep2_rows;
-    const unsigned blocks = (unsigned)(((P.n + kMB - 1) / kMB) * ((P.n + R - 1) / R));
-    if (cheb) k_f_sweep2<true><<<blocks, kMB, 0, st>>>(P, a, R);
-    else k_f_sweep2<false><<<blocks, kMB, 0, st>>>(P, a, R);
-    MPBP_HIP(hipGetLastError());
-    return MPBP_OK;
-}
-
-// A whole Gt_G inner solve (sweeps 1 .. K-1 from the fused init) in one k_gtg_solve pass, when the
-// operator is the single-GPU Gt_G stencil and 2 <= K-1 <= 4 <= n.  Returns 1 if it launched.
-int try_gtg_solve(const OpPair& op, bool cheb, int K, const double* b, const double* diag, const double* c1,
-                  const double* c2, const double* sub, double* xo, hipStream_t st, int* rc) {
-    const OpRef& o = op.in;
-    const int S = K - 1;
-    if (g_gtg_solve_rows <= 0 || !can_fuse_init(op) || o.sop != SOP_GTG || S < 2 || S > 4) return 0;
-    const mpbp_schur_plan* p = o.stencil;
-    PGDev P;
-    *rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &P);
-    if (*rc) return 1;
-    if (S > P.n) return 0;
-    GtgSolveArgs a{b, diag, cheb ? c2[0] : 1.0, {}, {}, sub, xo};
-    for (int s = 0; cheb && s <= S; ++s) {
-        a.c1[s] = c1[s];
-        a.c2[s] = c2[s];
-    }
-    const int R = g_gtg_solve_rows;
-    const unsigned blocks = (unsigned)(((P.n + kMB - 1) / kMB) * ((P.n + R - 1) / R));
-    const GtGStencilDev G{P};
-#define MPBP_GTG_SOLVE(SS)                                                                              \
-    (cheb ? (k_gtg_solve<SS, true><<<blocks, kMB, 0, st>>>(G, a, R), 0)                                 \
-          : (k_gtg_solve<SS, false><<<blocks, kMB, 0, st>>>(G, a, R), 0))
-    switch (S) {
-    case 2: MPBP_GTG_SOLVE(2); break;
-    case 3: MPBP_GTG_SOLVE(3); break;
-    default: MPBP_GTG_SOLVE(4); break;
-    }
-#undef MPBP_GTG_SOLVE
-    const hipError_t e = hipGetLastError();
-    *rc = e == hipSuccess ? MPBP_OK : set_error(MPBP_ERR_HIP, "k_gtg_solve: %s", hipGetErrorString(e));
-    return 1;
 }
 
 OpPair make_op(const mpbp_schur_plan* p, const mpbp_csr& A, const mpbp_rowblocks& bi, const mpbp_rowblocks& bb,
@@ -3087,14 +2451,7 @@ int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag
     }
     double* cur = (K == 1) ? dst : ping;
     int s = 1, rc = MPBP_OK;
-    if (try_gtg_solve(op, cheb, K, b, diag, c1, c2, sub, dst, c.st, &rc)) return rc;   // the whole solve
-    if (K >= 3 && can_fuse_init(op) && op.in.sop == SOP_F && g_sweep2_rows > 0) {   // init + sweeps 1, 2: one pass
-        double* nxt = K == 3 ? dst : pong;
-        rc = op_first_two_sweeps(op.in, cheb, b, diag, c1, c2, dir, K == 3 ? sub : nullptr, nxt, c.st, K == 3 ? 0 : 1);
-        if (rc) return rc;
-        cur = nxt;
-        s = 3;
-    } else if (K >= 2 && can_fuse_init(op)) {   // sweep 1 recomputes x0 = d0 from b and diag: no init pass
+    if (K >= 2 && can_fuse_init(op)) {   // sweep 1 recomputes x0 = d0 from b and diag: no init pass
         double* nxt = K == 2 ? dst : pong;
         rc = op_first_sweep(op.in, cheb, b, diag, c2[0], c1[1], c2[1], dir, K == 2 ? sub : nullptr, nxt, c.st,
                             K == 2 ? 0 : 1);
@@ -3254,7 +2611,7 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
     const Ctx c{p, as_stream(stream)};
     // the CA schedule needs every operator but Gt_F_G matrix-free on the marching kernel; otherwise the
     // per-sweep exchanges below (its deeper halos serve them as well)
-    if (p->ca && p->halo && p->f_stencil && p->pg_stencil && g_stencil_kind == 2) return schur_apply_ca(c, v, out);
+    if (p->ca && p->halo && p->f_stencil && p->pg_stencil) return schur_apply_ca(c, v, out);
     if (p->f_stencil && p->halo && p->f_part.halo < 1)
         return set_error(MPBP_ERR_ARG, "schur_apply: a partitioned F stencil needs f_part");
     if (p->pg_stencil && p->halo && (p->p_part.halo < 1 || p->f_part.halo < 1))

@@ -27,7 +27,7 @@ def _worker(rank, world, port, n, layout, f_mode, kind, errfile, ca="auto"):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         import mp_block_preconditioners_amd as mpb
         from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
-        mpb.lib().mpbp_set_stencil_kind(kind)
+        mpb.lib().mpbp_set_march_rows(kind)
         iF, iP = mpb.InnerSolver("chebyshev", 4), mpb.InnerSolver("chebyshev", 3)
         dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, layout=layout,
                                              f_mode=f_mode, ca=ca)
@@ -52,10 +52,10 @@ def _worker(rank, world, port, n, layout, f_mode, kind, errfile, ca="auto"):
         raise
 
 
-@pytest.mark.parametrize("world,n,layout,f_mode,kind", [(2, 64, "sell", "stencil", 2), (2, 64, "sell", "assembled", 2),
-                                                        (2, 64, "csr", "assembled", 0), (3, 50, "sell", "stencil", 0),
-                                                        (4, 9, "csr", "stencil", 0), (2, 64, "sell", "stencil", 1),
-                                                        (3, 50, "sell", "stencil", 2 + 4), (4, 9, "sell", "stencil", 2 + 3)])
+@pytest.mark.parametrize("world,n,layout,f_mode,kind", [(2, 64, "sell", "stencil", 4), (2, 64, "sell", "assembled", 4),
+                                                        (2, 64, "csr", "assembled", 2), (3, 50, "sell", "stencil", 1),
+                                                        (4, 9, "csr", "stencil", 1), (2, 64, "sell", "stencil", 3),
+                                                        (3, 50, "sell", "stencil", 6), (4, 9, "sell", "stencil", 3)])
 def test_distributed_apply_matches_single_gpu(world, n, layout, f_mode, kind, tmp_path):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -76,7 +76,7 @@ def test_distributed_apply_ca_schedule(world, n, layout, ca, tmp_path):
         pytest.skip("no GPU")
     errfile = str(tmp_path / "err.txt")
     try:
-        mp.spawn(_worker, args=(world, _free_port(), n, layout, "stencil", 2, errfile, ca), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), n, layout, "stencil", 4, errfile, ca), nprocs=world, join=True)
     except Exception:
         msg = open(errfile).read() if os.path.exists(errfile) else ""
         pytest.fail(f"distributed worker failed:\n{msg}")
@@ -90,7 +90,7 @@ def _self_halo_worker(_index, port, n, halo, f_mode, pg_mode, kind, graph, errfi
         dist.init_process_group("gloo", rank=0, world_size=1)
         import mp_block_preconditioners_amd as mpb
         from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
-        mpb.lib().mpbp_set_stencil_kind(kind)
+        mpb.lib().mpbp_set_march_rows(kind)
         iF, iP = mpb.InnerSolver(*inner[0]), mpb.InnerSolver(*inner[1])
         dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, f_mode=f_mode,
                                              pg_mode=pg_mode, halo=halo, self_halo=True, halo_overlap=overlap,
@@ -133,11 +133,11 @@ def _self_halo_worker(_index, port, n, halo, f_mode, pg_mode, kind, graph, errfi
 
 
 @pytest.mark.parametrize("n,halo,f_mode,pg_mode,kind,graph,overlap", [
-    (64, "rccl", "stencil", "stencil", 2, False, False), (50, "rccl", "assembled", "assembled", 2, False, False),
-    (33, "rccl", "stencil", "assembled", 0, False, False), (64, "torch", "stencil", "stencil", 2, False, False),
-    (64, "rccl", "stencil", "stencil", 2, True, False), (64, "rccl", "stencil", "stencil", 2, False, True),
-    (64, "torch", "stencil", "stencil", 2, True, False),
-    (40, "rccl", "assembled", "stencil", 2, False, True)])
+    (64, "rccl", "stencil", "stencil", 4, False, False), (50, "rccl", "assembled", "assembled", 4, False, False),
+    (33, "rccl", "stencil", "assembled", 1, False, False), (64, "torch", "stencil", "stencil", 4, False, False),
+    (64, "rccl", "stencil", "stencil", 4, True, False), (64, "rccl", "stencil", "stencil", 4, False, True),
+    (64, "torch", "stencil", "stencil", 4, True, False),
+    (40, "rccl", "assembled", "stencil", 4, False, True)])
 def test_self_halo_partitioned_apply(n, halo, f_mode, pg_mode, kind, graph, overlap, tmp_path, ca="auto",
                                      inner=(("chebyshev", 4), ("chebyshev", 3))):
     """One rank runs the partitioned apply with ghost rows filled by the periodic self-exchange -- the
@@ -158,7 +158,7 @@ def test_self_halo_partitioned_apply(n, halo, f_mode, pg_mode, kind, graph, over
 @pytest.mark.parametrize("halo,ca", [("rccl", False), ("rccl", True), ("torch", True)])
 def test_self_halo_ca_schedule(halo, ca, tmp_path):
     """RCCL / torch self-exchange with and without the communication-avoiding schedule."""
-    test_self_halo_partitioned_apply(48, halo, "stencil", "stencil", 2, False, False, tmp_path, ca=ca)
+    test_self_halo_partitioned_apply(48, halo, "stencil", "stencil", 4, False, False, tmp_path, ca=ca)
 
 
 @pytest.mark.parametrize("inner", [(("jacobi", 1), ("jacobi", 1)), (("jacobi", 2), ("chebyshev", 2)),
@@ -167,5 +167,5 @@ def test_self_halo_ca_schedule(halo, ca, tmp_path):
 def test_self_halo_ca_inner_solvers(inner, tmp_path):
     """The CA schedule's ghost-row depths for other inner solvers: one-sweep (init only) solves, Jacobi,
     deeper Chebyshev -- bit for bit against the single-GPU apply (RCCL self-exchange)."""
-    test_self_halo_partitioned_apply(40, "rccl", "stencil", "stencil", 2, False, False, tmp_path, ca=True,
+    test_self_halo_partitioned_apply(40, "rccl", "stencil", "stencil", 4, False, False, tmp_path, ca=True,
                                      inner=inner)

@@ -118,18 +118,8 @@ def test_spgemm_bit_exact(n):
     _same_csr(mp.spgemm(F, G, alpha=2.5), co.spgemm(osys.F, osys.G, alpha=2.5))
 
 
-@pytest.fixture(params=[1, 2, 0], ids=["csr_wave", "csr_wave_pf", "csr_block"])
-def csr_kernel(request):
-    """Every CSR SpMV kernel (mpbp_set_csr_kernel): per-wave chunks (default), per-wave chunks over several
-    row blocks with prefetch, and 256-row LDS stages."""
-    from mp_block_preconditioners_amd._lib import check, lib
-    check(lib().mpbp_set_csr_kernel(request.param))
-    yield request.param
-    check(lib().mpbp_set_csr_kernel(1))
-
-
 @pytest.mark.parametrize("n", [2, 16, 100])
-def test_spmv_bit_exact(n, csr_kernel):
+def test_spmv_bit_exact(n):
     mp = _mp()
     from oracle import csr_oracle as co
     osys = _oracle_system(n, products=False, **PARAMS)
@@ -172,9 +162,9 @@ def test_sell_ragged_rows_and_partial_slices():
     assert _bits_equal(got[sel], ref[sel]) and np.all(got[np.r_[0:3, 100:500]] == 7.0)
 
 
-def test_spmv_long_rows_and_empty_rows(csr_kernel):
-    """Rows longer than a row block's LDS stage (single-row blocks) and empty rows.  The per-wave kernel
-    sums a long row chunk after chunk in order (bit-exact); the 256-row-stage kernel tree-reduces it."""
+def test_spmv_long_rows_and_empty_rows():
+    """Rows longer than a row block's LDS stage (single-row blocks) and empty rows: the per-wave kernel sums a
+    long row chunk after chunk in order (bit-exact)."""
     mp = _mp()
     from oracle import csr_oracle as co
     rng = np.random.default_rng(7)
@@ -190,12 +180,11 @@ def test_spmv_long_rows_and_empty_rows(csr_kernel):
     ref = M @ x
     assert rel_inf(y, ref) <= 1e-13
     assert y[0] == 0.0 and y[10] == 0.0
-    if csr_kernel in (1, 2):
-        assert _bits_equal(y, co.spmv(M, x))
+    assert _bits_equal(y, co.spmv(M, x))
 
 
 @pytest.mark.parametrize("maxlen", [13, 40, 200])
-def test_csr_wave_chunks_ragged_bit_exact(maxlen, csr_kernel):
+def test_csr_wave_chunks_ragged_bit_exact(maxlen):
     """Ragged rows whose 64-row wave ranges exceed one 768-entry chunk (rows straddle chunk edges,
     odd starts), partial last wave, empty rows, all three epilogue modes; bit-exact vs the oracle."""
     mp = _mp()
@@ -215,7 +204,7 @@ def test_csr_wave_chunks_ragged_bit_exact(maxlen, csr_kernel):
 
 
 @pytest.mark.parametrize("n", [4, 32])
-def test_inner_steps_bit_exact(n, csr_kernel):
+def test_inner_steps_bit_exact(n):
     mp = _mp()
     from mp_block_preconditioners_amd import _lib
     from mp_block_preconditioners_amd._lib import check, lib, ptr, stream_handle

@@ -29,12 +29,13 @@ def _bits(a, b):
 PARAMS = [(1.0, 100.0, 1.0, 1.0, -1.0), (2.5, 1.0e4, 1.0, 0.5, -2.0), (1.0, 1.0, 1.0, 0.0, -1.0)]
 
 
-@pytest.fixture(params=[0, 1, 2 + 3, 2 + 8], ids=["cells-lds", "rows", "march3", "march8"])
+@pytest.fixture(params=[4, 1, 3, 8], ids=["march4", "march1", "march3", "march8"])
 def stencil_kind(request):
+    """Rows per workgroup of the marching kernel (mpbp_set_march_rows): results must not depend on it."""
     from mp_block_preconditioners_amd._lib import check, lib
-    check(lib().mpbp_set_stencil_kind(request.param))
+    check(lib().mpbp_set_march_rows(request.param))
     yield request.param
-    check(lib().mpbp_set_stencil_kind(2))
+    check(lib().mpbp_set_march_rows(4))
 
 
 @pytest.mark.parametrize("n", [3, 4, 17, 64, 255, 300])
@@ -126,29 +127,6 @@ def test_graph_replay_matches_eager():
     v.copy_(torch.randn_like(v))             # replay reads the captured buffers' new contents
     g.replay()
     assert torch.equal(out, pc.apply(v))
-
-
-@pytest.mark.parametrize("n", [3, 4, 5, 17, 256, 257, 300, 520])
-@pytest.mark.parametrize("rows", [1, 3, 8])
-def test_two_sweep_fusion_bit_exact(n, rows):
-    """k_f_sweep2 (init + sweeps 1-2 of each F solve in one pass, level 1 kept in LDS) against one kernel
-    per sweep, for Chebyshev and Jacobi inner solves of 3, 4 and 5 sweeps (3: the pass is the solve's last
-    sweep, with sub and no direction store)."""
-    import mp_block_preconditioners_amd as mp
-    from mp_block_preconditioners_amd._lib import check, lib
-    bp = mp.MultiphaseBlockPreconditioner(n, 1.3, 50.0, 2.0)
-    _, _, F, D, G = bp.get_big_A_matrix(c=0.7, d_u=-1.5)
-    v = torch.from_numpy(np.random.default_rng(n + rows).standard_normal(5 * n * n)).cuda()
-    try:
-        for kind, k in (("chebyshev", 4), ("chebyshev", 3), ("jacobi", 3), ("chebyshev", 5), ("jacobi", 4)):
-            pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver(kind, k), inner_P=mp.InnerSolver("jacobi", 2))
-            check(lib().mpbp_set_sweep_fusion(0))
-            ref = pc.apply(v).clone()
-            check(lib().mpbp_set_sweep_fusion(rows))
-            got = pc.apply(v)
-            assert _bits(got, ref), (kind, k, float((got - ref).abs().max()))
-    finally:
-        check(lib().mpbp_set_sweep_fusion(0))
 
 
 def _ext_local_rows(n, L, h, nf):

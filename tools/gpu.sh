@@ -13,9 +13,11 @@
 #   prof         rocprofv3 --kernel-trace --stats of bench.py
 #   pmc          FETCH_SIZE / WRITE_SIZE passes: the apply's F sweeps and the A SpMV
 #   sq           SQ counter passes over the F sweep (tools/pmc_sweep.py) and the CSR SpMV (tools/spmv_ab.py)
+#   sqapply      SQ counter passes over bench.py's eager apply (every kernel of the apply; tools/pmc_table.py)
 #   py:FILE      python FILE (any experiment script), 300 s
-#   ab:V1,V2,..  A/B of experiment builds (tools/build_variants.py): bench.py and tools/spmv_ab.py per variant
-#                (variant "base" = the product library); extra bench args in $BENCH_ARGS
+#   ab:V1,V2,..  A/B of experiment builds (tools/build_variants.py): bench.py per variant (V or V@ARGS, '+' for
+#                spaces; variant "base" = the product library); extra bench args for all in $BENCH_ARGS
+#   spmv:V1,..   tools/spmv_ab.py (the A SpMV kernels) per variant
 set -o pipefail
 TAG=${1:-run}
 shift
@@ -65,14 +67,28 @@ step() {
             SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_VMEM_RD SQ_LDS_BANK_CONFLICT --output-format csv \
             -d "$ROOTD/$OUT/sq2_$tag" -o pmc -- python "$ROOTD/tools/"$W || return 1
         done ;;
-    ab:*) local V
+    ab:*) local V   # VARIANT[@ARGS] (ARGS with '+' for spaces), e.g. ab:base,mb128@--march-rows+8
           for V in $(echo "${s#ab:}" | tr , ' '); do
+            local N=${V%%@*} A=""
+            [ "$N" != "$V" ] && A=$(echo "${V#*@}" | tr + ' ')
+            local L=mp-block-preconditioners_amd/lib/variants/libmpbp_$N.so
+            [ "$N" = base ] && L=
+            MPBP_LIB=$L timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-spmv $A \
+              $BENCH_ARGS >> "$OUT/ab_bench_$N$(echo "$A" | tr -d ' -').log" 2>&1 || return 1
+          done ;;
+    spmv:*) local V
+          for V in $(echo "${s#spmv:}" | tr , ' '); do
             local L=mp-block-preconditioners_amd/lib/variants/libmpbp_$V.so
             [ "$V" = base ] && L=
-            MPBP_LIB=$L timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline $BENCH_ARGS \
-              >> "$OUT/ab_bench_$V.log" 2>&1 || return 1
-            MPBP_LIB=$L timeout -k 10 120 python tools/spmv_ab.py >> "$OUT/ab_spmv_$V.log" 2>&1 || return 1
+            MPBP_LIB=$L timeout -k 10 120 python tools/spmv_ab.py >> "$OUT/spmv_$V.log" 2>&1 || return 1
           done ;;
+    sqapply) local B="$ROOTD/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-spmv --no-graph"
+          prof sq1_apply 150 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+            SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU --output-format csv -d "$ROOTD/$OUT/sq1_apply" \
+            -o pmc -- python $B || return 1
+          prof sq2_apply 150 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS \
+            SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_VMEM_RD SQ_LDS_BANK_CONFLICT --output-format csv \
+            -d "$ROOTD/$OUT/sq2_apply" -o pmc -- python $B || return 1 ;;
     py:*) timeout -k 10 300 python -u "${s#py:}" > "$OUT/$(basename "${s#py:}" .py).log" 2>&1 ;;
     *) echo "unknown step $s"; return 98 ;;
   esac

@@ -33,7 +33,7 @@ def main():
         d = d.replace("(anonymous namespace)::", "")
         if keys and not any(k in d for k in keys):
             continue
-        print(f"{r.get('VGPRs', '?'):>4} vgpr {r.get('ScratchSize', '?'):>4} scratch occ {r.get('Occupancy', '?')}  {d[:150]}")
+        print(f"{r.get('VGPRs', '?'):>4} vgpr {r.get('SGPRs', '?'):>4} sgpr {r.get('ScratchSize', '?'):>4} scratch occ {r.get('Occupancy', '?')}  {d[:150]}")
 
 
 if __name__ == "__main__":

@@ -21,7 +21,6 @@ def main():
     args = ap.parse_args()
     import torch
     import mp_block_preconditioners_amd as mp
-    from mp_block_preconditioners_amd._lib import check, lib
     bp = mp.MultiphaseBlockPreconditioner(args.n, 1.0, 100.0, 1.0, device="cuda:0")
     A = bp.get_big_A_matrix(c=1.0, d_u=-1.0)[0]
     gen = torch.Generator(device="cuda").manual_seed(0)
@@ -33,10 +32,7 @@ def main():
     nbytes = A.nnz * 12 + (A.shape[0] + 1) * 4 + (A.shape[0] + A.shape[1]) * 8 + A.blocks.count * 8
     res = {"n": args.n, "nnz": A.nnz, "lib": os.environ.get("MPBP_LIB", "default")}
     flat = A.plan_blocks(groups=1)   # blocks in plain row order (no per-field interleave)
-    for name, M, kind, blk in (("csr_wave", A, 1, None), ("csr_wave_pf", A, 2, None), ("csr_wave_roworder", A, 1, flat),
-                               ("csr_block", A, 0, None),
-                               ("sell", AS, 1, None)):
-        check(lib().mpbp_set_csr_kernel(kind))
+    for name, M, blk in (("csr_wave", A, None), ("csr_wave_roworder", A, flat), ("sell", AS, None)):
         kw = {"blocks": blk} if blk is not None else {}
         for _ in range(5):
             M.matvec(x, out=y, **kw)
