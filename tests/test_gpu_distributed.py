@@ -169,3 +169,46 @@ def test_self_halo_ca_inner_solvers(inner, tmp_path):
     deeper Chebyshev -- bit for bit against the single-GPU apply (RCCL self-exchange)."""
     test_self_halo_partitioned_apply(40, "rccl", "stencil", "stencil", 4, False, False, tmp_path, ca=True,
                                      inner=inner)
+
+
+def _rccl_worker(rank, world, port, n, ca, errfile):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", rank))
+        import mp_block_preconditioners_amd as mpb
+        from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
+        iF, iP = mpb.InnerSolver("chebyshev", 4), mpb.InnerSolver("chebyshev", 4)
+        dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, halo="rccl", ca=ca,
+                                             device=f"cuda:{rank}")
+        bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0, device=f"cuda:{rank}")
+        _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+        pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP)
+        v = torch.from_numpy(np.random.default_rng(11).standard_normal(pc.shape[0])).to(f"cuda:{rank}")
+        gids = torch.from_numpy(dpc.local_to_global_rows()).to(f"cuda:{rank}")
+        ref = pc.apply(v)[gids]
+        for _ in range(2):
+            got = dpc.apply(v[gids].contiguous())
+            assert torch.equal(got, ref), float((got - ref).abs().max())
+        dist.barrier()
+        dpc.close()
+        dist.destroy_process_group()
+    except BaseException as e:
+        with open(errfile, "a") as f:
+            f.write(f"rank {rank}: {type(e).__name__}: {e}\n")
+        raise
+
+
+@pytest.mark.parametrize("world,n,ca", [(2, 256, True), (2, 256, False), (2, 130, True)])
+def test_rccl_two_gpus_matches_single_gpu(world, n, ca, tmp_path):
+    """The partitioned apply over RCCL point-to-point between two GPUs (one rank per GPU, libmpbp's own
+    communicator), bit for bit against the single-GPU apply of the global system.  Runs where the node has
+    two GPUs (the driver's multi-GPU box); skipped on a one-GPU box."""
+    if not torch.cuda.is_available() or torch.cuda.device_count() < world:
+        pytest.skip(f"needs {world} GPUs")
+    errfile = str(tmp_path / "err.txt")
+    try:
+        mp.spawn(_rccl_worker, args=(world, _free_port(), n, ca, errfile), nprocs=world, join=True)
+    except Exception:
+        msg = open(errfile).read() if os.path.exists(errfile) else ""
+        pytest.fail(f"RCCL worker failed:\n{msg}")
