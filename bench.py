@@ -89,6 +89,8 @@ def main():
                     help="F sweeps: recompute F from thn (stencil) or stream the assembled F")
     ap.add_argument("--pg-mode", default="auto", choices=["auto", "stencil", "assembled"],
                     help="D, G, Gt_G: recompute from thn (stencil) or stream the stored operators")
+    ap.add_argument("--q-mode", default="auto", choices=["auto", "diamond", "assembled"],
+                    help="Gt_F_G: values in the 13-point diamond layout (columns implicit) or the assembled copy")
     ap.add_argument("--march-rows", type=int, default=4,
                     help="grid rows per workgroup of the marching stencil kernels (matrix-free F, D, G, Gt_G)")
     ap.add_argument("--no-ca", action="store_true",
@@ -156,7 +158,7 @@ def main():
         bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
         A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
         pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, layout=args.layout,
-                                          f_mode=args.f_mode, pg_mode=args.pg_mode)
+                                          f_mode=args.f_mode, pg_mode=args.pg_mode, q_mode=args.q_mode)
         del F, D, G
     else:
         from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
@@ -289,6 +291,7 @@ def main():
                        "f_sweeps": f"matrix-free-march{args.march_rows}" if getattr(pc, "f_stencil", None) is not None
                        else "assembled",
                        "d_g_gtg": "matrix-free" if getattr(pc, "pg_stencil", None) is not None else "assembled",
+                       "gt_f_g": "diamond-13" if getattr(pc, "q13", None) is not None else args.layout,
                        "launch": "hipgraph" if graph is not None else "eager",
                        **({"halo": f"{pc.halo_impl} ({'self-exchange' if world == 1 else 'neighbour'})",
                            "halo_schedule": (f"communication-avoiding: 2 exchanges per apply, ghost depth "

@@ -180,6 +180,9 @@ typedef struct mpbp_schur_plan {
     const double* diag_P_ext;        /* device, np_ext: diag(Gt_G) on owned + ghost rows */
     mpbp_halo_pair_fn halo_pair;     /* optional (CA schedule): both halves of v in one exchange
                                         (mpbp_halo_exchange_pair); NULL: two halo calls */
+    const double* q13;               /* optional (one GPU): Gt_F_G in the 13-point diamond layout
+                                        (mpbp_q13_build), used instead of GtFG / Qs_* when set */
+    int32_t q13_n;                   /* its grid size n */
 } mpbp_schur_plan;
 
 const char* mpbp_version(void);
@@ -208,6 +211,16 @@ int mpbp_exclusive_scan(const int32_t* row_nnz, int32_t* row_ptr, int64_t n, int
 int mpbp_spgemm_count(const mpbp_csr* A, const mpbp_csr* B, int32_t* row_nnz, void* stream);
 int mpbp_spgemm_fill(const mpbp_csr* A, const mpbp_csr* B, double alpha, const int32_t* row_ptr,
                      int32_t* col_idx, double* val, void* stream);
+
+/* ---- Gt_F_G in the 13-point diamond layout ---------------------------------------------------- */
+/* Gt_F_G = ((-D) F) G (solve.py:246-249) couples each pressure cell with the 13 cells |dr| + |dc| <= 2 (n >= 5).
+ * mpbp_q13_build copies the CSR values into vals[13 * n^2] (slot-major, slots in (dr, dc) lexicographic order);
+ * MPBP_ERR_ARG if a row is not exactly that diamond.  Setup: synchronises the stream.
+ * mpbp_q13_spmv: y = Q x (modes as mpbp_spmv), the CSR SpMV's result bit for bit; replaces np.matmul(Gt_F_G, x_a)
+ * (solve.py:267) -- the columns are implicit in the grid, so the layout streams 104 B per row instead of 156. */
+int mpbp_q13_build(const mpbp_csr* Q, int32_t n, double* vals, void* stream);
+int mpbp_q13_spmv(int32_t n, const double* vals, int32_t mode, const double* x, const double* z, double* y,
+                  void* stream);
 
 /* ---- planning / helpers (setup) ------------------------------------------------------------ */
 /* Host-side greedy row blocking of rows [row_begin, row_end) of a HOST row_ptr; writes at most
@@ -299,6 +312,9 @@ int mpbp_gtg_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell
 /* Grid rows per workgroup of the marching stencil kernels (matrix-free F, D, G, Gt_G), process-wide; 4 (default)
  * is fastest on MI355X at 1024^2 (one round of workgroups).  Results are bit-identical for every value. */
 int mpbp_set_march_rows(int32_t rows);
+/* The first sweep of a matrix-free F inner solve stages x0 = c2 b / diag: mode 1 (default) rebuilds diag from the
+ * thn tables inside the sweep (no diag stream), mode 0 streams the stored diagonal.  Same bits either way. */
+int mpbp_set_init_diag(int32_t mode);
 
 /* ---- ghost rows over RCCL point-to-point (multi-GPU row partition) ------------------------------ */
 /* One RCCL group of neighbour sends / receives: the owned boundary rows (packed into one buffer per

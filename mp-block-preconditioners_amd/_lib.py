@@ -74,7 +74,8 @@ class SchurPlan(Structure):
                 ("f_stencil", c_int32), ("f_prm", StokesParams), ("f_cell", c_void_p), ("f_uface", c_void_p),
                 ("f_vface", c_void_p), ("f_part", RowPart), ("pg_stencil", c_int32), ("p_part", RowPart),
                 ("halo_first", c_int32), ("ca", c_int32), ("ca_reach_q", c_int32), ("wu_ext", c_void_p),
-                ("diag_F_ext", c_void_p), ("diag_P_ext", c_void_p), ("halo_pair", HALO_PAIR_FN)]
+                ("diag_F_ext", c_void_p), ("diag_P_ext", c_void_p), ("halo_pair", HALO_PAIR_FN),
+                ("q13", c_void_p), ("q13_n", c_int32)]
 
 
 _P = c_void_p
@@ -126,6 +127,9 @@ _SIGNATURES = {
     "mpbp_halo_set_mode": ([_P, c_int32], c_int),
     "mpbp_halo_last_error": ([_P], c_char_p),
     "mpbp_set_march_rows": ([c_int32], c_int),
+    "mpbp_set_init_diag": ([c_int32], c_int),
+    "mpbp_q13_build": ([POINTER(Csr), c_int32, c_void_p, c_void_p], c_int),
+    "mpbp_q13_spmv": ([c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "mpbp_gather": ([c_int32, _P, _P, _P, _P], c_int),
     "mpbp_scatter": ([c_int32, _P, _P, _P, _P], c_int),
     "mpbp_event_create": ([POINTER(c_void_p)], c_int),

@@ -20,6 +20,7 @@ namespace {
 
 thread_local char g_err[1024] = "";
 int g_march_rows = 4;     // grid rows per workgroup of the marching kernels (4 is fastest at 1024^2)
+int g_init_diag = 1;      // fused first F sweep: 1 rebuilds the staged diagonal from thn, 0 streams diag
 #ifndef MPBP_PG_ROWS
 #define MPBP_PG_ROWS 0    // rows per workgroup of the D / G / Gt_G marching kernels (0: as F)
 #endif
@@ -1107,7 +1108,75 @@ struct FStencilDev {
     }
     template <bool EDGE, class TA, class XA>
     __device__ double row(int f, int gr, int gc, const TA& ta, const XA& xa, double* fd, const Cell& cl) const;
+    // k_march_init: the face thn a staged point's diagonal needs, and that diagonal
+    struct Stage { double face[2]; };
+    __device__ Stage stage_pre(int gr, int gcw) const {
+        const int32_t k = wrap(gr) * n + gcw;
+        return {{uface[k], vface[k]}};
+    }
+    template <class TA>
+    __device__ double stage_diag(int f, int gr, int gc, const TA& ta, const Stage& s) const;
 };
+
+// The diagonal of an F row (phase_L_row's diagonal + XI + the c-weighted identity, F_row), with the
+// intermediate thn averages the row's off-diagonal entries reuse.  One definition serves the row itself
+// (f_row) and the first inner sweep's staged x0 = c2 b / diag (k_march_init), so both see the same bits.
+// M: f_row's compile-time parameter identities.
+template <int M>
+struct FDiagCommon {
+    __device__ static double dmul(const FStencilDev& P, double y) { return (M & 1) ? -y : P.d_u * y; }
+    __device__ static double emul(const FStencilDev& P, int p, double y) {
+        const bool eta1 = p ? (M & 4) != 0 : (M & 2) != 0;
+        return eta1 ? y : (p ? P.eta_s : P.eta_n) * y;
+    }
+};
+template <int M>
+struct FDiagU : FDiagCommon<M> {   // u row at (gr, gc): preconditioner.py:100-179
+    double iph_jph, iph_jmh, xi_ii, fd;
+    template <class TA>
+    __device__ FDiagU(const FStencilDev& P, int p, const TA& ta, int gr, int gc, double th) {
+        const double tij = ta.T(p, gr, gc - 1), tip1j = ta.T(p, gr, gc);
+        const double tijp1 = ta.T(p, gr - 1, gc - 1), tip1jp1 = ta.T(p, gr - 1, gc);
+        const double tijm1 = ta.T(p, gr + 1, gc - 1), tip1jm1 = ta.T(p, gr + 1, gc);
+        iph_jph = 0.25 * (tij + tijp1 + tip1jp1 + tip1j);
+        iph_jmh = 0.25 * (tij + tip1j + tijm1 + tip1jm1);
+        const double iph_j = 0.5 * (tij + tip1j);
+        xi_ii = xi_of(P.xi, iph_j);
+        const double wt = p ? P.c * (1.0 - th) : P.c * th;
+        const double Ldiag = P.idx2 * (-tip1j - tij) + P.idx2 * (-iph_jph - iph_jmh);
+        fd = (wt - this->dmul(P, xi_ii)) + this->dmul(P, this->emul(P, p, Ldiag));
+    }
+};
+template <int M>
+struct FDiagV : FDiagCommon<M> {   // v row at (gr, gc): preconditioner.py:182-295
+    double tij, tijp1, imh_jph, iph_jph, xi_ii, fd;
+    template <class TA>
+    __device__ FDiagV(const FStencilDev& P, int p, const TA& ta, int gr, int gc, double th) {
+        tij = ta.T(p, gr, gc);
+        const double tip1j = ta.T(p, gr, gc + 1);
+        tijp1 = ta.T(p, gr - 1, gc);
+        const double tip1jp1 = ta.T(p, gr - 1, gc + 1);
+        const double tim1j = ta.T(p, gr, gc - 1), tim1jp1 = ta.T(p, gr - 1, gc - 1);
+        const double ip1_jph = 0.5 * (tij + tijp1);
+        xi_ii = xi_of(P.xi, ip1_jph);
+        const double wt = p ? P.c * (1.0 - th) : P.c * th;
+        imh_jph = 0.25 * (tim1j + tim1jp1 + tij + tijp1);
+        iph_jph = 0.25 * (tij + tip1j + tijp1 + tip1jp1);
+        const double Ldiag = P.midy2 * (tijp1 + tij) - P.idx2 * (iph_jph + imh_jph);
+        fd = (wt - this->dmul(P, xi_ii)) + this->dmul(P, this->emul(P, p, Ldiag));
+    }
+};
+
+template <int M, class TA>
+__device__ inline double f_stage_diag(const FStencilDev& P, int f, int gr, int gc, const TA& ta,
+                                      const FStencilDev::Stage& s) {
+    const int p = f >> 1;
+    return (f & 1) == 0 ? FDiagU<M>(P, p, ta, gr, gc, s.face[0]).fd : FDiagV<M>(P, p, ta, gr, gc, s.face[1]).fd;
+}
+template <class TA>
+__device__ inline double FStencilDev::stage_diag(int f, int gr, int gc, const TA& ta, const Stage& s) const {
+    return f_stage_diag<0>(*this, f, gr, gc, ta, s);
+}
 
 // The ten entries of one F row, built in the assembled row's column order for interior points and
 // sorted (with fixed networks) where periodic wrap-around reorders them.  TA::T(s, gr, gc) is thn of
@@ -1134,16 +1203,10 @@ __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, cons
     const double xcross = xa.X(f ^ 2, gr, gc);
     if ((f & 1) == 0) {   // u row: preconditioner.py:100-179
         const double tij = T(gr, gc - 1), tip1j = T(gr, gc);
-        const double tijp1 = T(gr - 1, gc - 1), tip1jp1 = T(gr - 1, gc);
-        const double tijm1 = T(gr + 1, gc - 1), tip1jm1 = T(gr + 1, gc);
-        const double iph_jph = 0.25 * (tij + tijp1 + tip1jp1 + tip1j);
-        const double iph_jmh = 0.25 * (tij + tip1j + tijm1 + tip1jm1);
-        const double iph_j = 0.5 * (tij + tip1j);
-        const double xi_ii = xi_of(P.xi, iph_j);
         const double th = face ? face[0] : P.uface[kc];   // face: thn at the u / v face, loaded ahead
-        const double wt = p ? P.c * (1.0 - th) : P.c * th;
-        const double Ldiag = idx2 * (-tip1j - tij) + idx2 * (-iph_jph - iph_jmh);
-        const double fd = (wt - dmul(xi_ii)) + dmul(emul(Ldiag));
+        const FDiagU<M> dd(P, p, ta, gr, gc, th);
+        const double iph_jph = dd.iph_jph, iph_jmh = dd.iph_jmh, xi_ii = dd.xi_ii;
+        const double fd = dd.fd;
         *fdiag = fd;
         // same field: N, W, C, E, S; the other component (v of this phase): (gr, gc-1), (gr, gc), (gr+1, gc-1),
         // (gr+1, gc)
@@ -1162,17 +1225,11 @@ __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, cons
         acc = add4<EDGE>(acc, hi, w.rl, w.c0);
         if (p == 0) acc += vcross * xcross;
     } else {              // v row: preconditioner.py:182-295
-        const double tij = T(gr, gc), tip1j = T(gr, gc + 1);
-        const double tijp1 = T(gr - 1, gc), tip1jp1 = T(gr - 1, gc + 1);
-        const double tim1j = T(gr, gc - 1), tim1jp1 = T(gr - 1, gc - 1);
-        const double ip1_jph = 0.5 * (tij + tijp1);
-        const double xi_ii = xi_of(P.xi, ip1_jph);
         const double th = face ? face[1] : P.vface[kc];
-        const double wt = p ? P.c * (1.0 - th) : P.c * th;
-        const double imh_jph = 0.25 * (tim1j + tim1jp1 + tij + tijp1);
-        const double iph_jph = 0.25 * (tij + tip1j + tijp1 + tip1jp1);
-        const double Ldiag = P.midy2 * (tijp1 + tij) - idx2 * (iph_jph + imh_jph);
-        const double fd = (wt - dmul(xi_ii)) + dmul(emul(Ldiag));
+        const FDiagV<M> dd(P, p, ta, gr, gc, th);
+        const double tij = dd.tij, tijp1 = dd.tijp1;
+        const double imh_jph = dd.imh_jph, iph_jph = dd.iph_jph, xi_ii = dd.xi_ii;
+        const double fd = dd.fd;
         *fdiag = fd;
         // the other component (u of this phase): (gr-1, gc), (gr-1, gc+1), (gr, gc), (gr, gc+1); same field: N, W,
         // C, E, S
@@ -1215,15 +1272,17 @@ struct XRing {
     int gr, c0;
     __device__ double X(int f, int r, int c) const { return x[(f * 3 + s[r - gr + 1]) * kMTileW + (c - c0 + 1)]; }
 };
-struct TRing {
-    const double* t;   // [3][kMTileW]
+template <int W, int OFF>
+struct TRingT {
+    const double* t;   // [slots][W]: tile column 0 is grid column c0 - OFF
     int s[3];
     int gr, c0;
     __device__ double T(int sph, int r, int c) const {
-        const double v = t[s[r - gr + 1] * kMTileW + (c - c0 + 1)];
+        const double v = t[s[r - gr + 1] * W + (c - c0 + OFF)];
         return sph ? 1.0 - v : v;
     }
 };
+using TRing = TRingT<kMTileW, 1>;
 
 // Staged sources: load(i) issues the loads of element i (raw registers, nothing consumes them yet), value(raw)
 // turns them into the staged value at LDS-store time -- so a tile row's loads stay in flight through the
@@ -1432,15 +1491,171 @@ k_march(S P, XS xs, int nchunks, Epi epi) {
     step(lb - 1, std::false_type{});
 }
 
-// Workgroups of one k_march instance the device holds at once (occupancy x CUs), queried once.
-template <class S, class XS, class Epi>
+// ---- first inner sweep with the init pass folded in, diagonal recomputed (k_march_init) ----
+// The sweep stages x0 = c2 * (b / diag) (c2 = 1: Jacobi) wherever k_march would stage x, with diag -- the
+// operator's own diagonal at the staged point -- rebuilt from the thn tile by the stencil (S::stage_diag, the
+// same expression its rows use), so the sweep streams b alone: no diag vector, and one value in flight per
+// staged point.  Rebuilding the staged row's diagonal needs thn one row below it, so the thn ring runs a row
+// ahead of the x ring: 5 slots over columns c0-2 .. c0+257 (one more each side than the x tile, for the v
+// rows' and the halo columns' neighbours).  Invariant at the start of step k: thn rows k-1 .. k+2 and x0 rows
+// k-1, k in LDS, b row k+1 (+ its S::Stage operands) in registers.
+constexpr int kTW = kMTileW + 2;
+template <int NF, class Stage>
+struct InitRow {
+    double xa[NF], h0[NF];   // b at the lane's main column and (lanes 0, 1) its halo column
+    Stage sa, sh;            // the stencil's per-point operands for the diagonal (F: the u/v face thn)
+};
+struct ThnRow {
+    double ta, te;           // thn at the lane's main column; lanes 0..3 an extra column (c0+255, c0+256, c0-2, c0+257)
+};
+__device__ inline int thn_extra_col(int tid, int c0) {
+    return tid == 0 ? c0 + kMB - 1 : tid == 1 ? c0 + kMB : tid == 2 ? c0 - 2 : c0 + kMB + 1;
+}
+__device__ inline int thn_extra_slot(int tid) { return tid == 0 ? kMB + 1 : tid == 1 ? kMB + 2 : tid == 2 ? 0 : kMB + 3; }
+
+template <class S>
+__device__ inline void load_thn_row(const S& P, int gr, int colA, int tid, int c0, ThnRow& t) {
+    const int n = P.n;
+    const int32_t tb = P.wrap(gr) * n;
+    const int ce = thn_extra_col(tid, c0);
+    t.ta = P.cell[tb + (colA <= n + 1 ? P.wrap(colA) : 0)];
+    t.te = P.cell[tb + (ce <= n + 1 ? P.wrap(ce) : 0)];
+}
+__device__ inline void store_thn_row(double* st, int slot, int tid, const ThnRow& t) {
+    st[slot * kTW + tid + 1] = t.ta;
+    if (tid < 4) st[slot * kTW + thn_extra_slot(tid)] = t.te;
+}
+template <class S>
+__device__ inline void load_init_row(const S& P, const double* __restrict__ b, int gr, int gcA, bool okA,
+                                     const HaloCols& hc, InitRow<S::NF, typename S::Stage>& tr) {
+    const int ca = okA ? gcA : 0;
+#pragma unroll
+    for (int f = 0; f < S::NF; ++f) {
+        const int32_t base = P.xrow(f, gr);
+        tr.xa[f] = b[base + ca];
+        tr.h0[f] = b[base + hc.gl];
+    }
+    tr.sa = P.stage_pre(gr, ca);
+    tr.sh = P.stage_pre(gr, hc.gl);
+}
+// x0 of staged grid row gr (ring slot `slot`) from b and the diagonal rebuilt over thn rows gr-1 .. gr+1.
+template <class S>
+__device__ inline void store_init_row(const S& P, double c2, double* sx, const double* st, int slot, const int ts[3],
+                                      int gr, int c0, int tid, int colA, bool okA, const HaloCols& hc,
+                                      const InitRow<S::NF, typename S::Stage>& tr) {
+    const TRingT<kTW, 2> ta{st, {ts[0], ts[1], ts[2]}, gr, c0};
+#pragma unroll
+    for (int f = 0; f < S::NF; ++f) {
+        const double dg = P.stage_diag(f, gr, colA, ta, tr.sa);
+        sx[(f * 3 + slot) * kMTileW + tid] = okA ? c2 * (tr.xa[f] / dg) : 0.0;
+    }
+    if (tid < 2) {   // lanes 0 and 1: the halo columns c0+255, c0+256
+        const bool ok = tid == 0 ? hc.ok0 : hc.ok1;
+        const int col = c0 + kMB - 1 + tid;
+#pragma unroll
+        for (int f = 0; f < S::NF; ++f) {
+            const double dg = P.stage_diag(f, gr, col, ta, tr.sh);
+            sx[(f * 3 + slot) * kMTileW + kMB + tid] = ok ? c2 * (tr.h0[f] / dg) : 0.0;
+        }
+    }
+}
+
+template <class S, class Epi>
+__global__ void __launch_bounds__(kMB) __attribute__((amdgpu_waves_per_eu(4, 8)))
+k_march_init(S P, const double* __restrict__ b, double c2, int nchunks, Epi epi) {
+    constexpr int NF = S::NF, NO = S::NOUT;
+    __shared__ double sx[NF * 3 * kMTileW];
+    __shared__ double st[5 * kTW];
+    const int n = P.n;
+    const int strips = (n + kMB - 1) / kMB;
+    const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int strip = bk % strips, chunk = bk / strips;
+    int la, lb;
+    if (!march_rows(P.which, P.L, P.ext, chunk, nchunks, &la, &lb)) return;
+    const int c0 = strip * kMB, tid = threadIdx.x;
+    const int colA = c0 - 1 + tid;
+    const bool okA = colA <= n;
+    const int gcA = P.wrap(colA <= n + 1 ? colA : 0);
+    HaloCols hc;
+    {
+        const int b0 = c0 + kMB - 1, b1 = c0 + kMB;
+        hc.ok0 = b0 <= n;
+        hc.ok1 = b1 <= n;
+        hc.g0 = b0 < n ? b0 : 0;
+        hc.g1 = b1 < n ? b1 : 0;
+        hc.gl = tid == 0 ? hc.g0 : tid == 1 ? hc.g1 : (okA ? gcA : 0);
+    }
+    const int gc = c0 + tid;
+    const bool live = gc < n;
+    auto tslot = [&](int lr) { return (lr - la + 2) % 5; };   // thn ring slot of local row lr (lr >= la - 2)
+    auto xslot = [&](int lr) { return (lr - la + 1) % 3; };   // x ring slot (lr >= la - 1)
+    auto grow = [&](int lr) { return P.wrap(P.r0 + lr); };    // grid row (ghost rows wrap periodically)
+    typedef InitRow<NF, typename S::Stage> IR;
+    // prologue: thn rows la-2 .. la+2, x0 rows la-1 and la; b row la+1 into registers
+    {
+        ThnRow t[5];
+        IR r0, r1;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) load_thn_row(P, P.r0 + la - 2 + i, colA, tid, c0, t[i]);
+        load_init_row(P, b, P.r0 + la - 1, gcA, okA, hc, r0);
+        load_init_row(P, b, P.r0 + la, gcA, okA, hc, r1);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) store_thn_row(st, i, tid, t[i]);
+        __syncthreads();
+        const int s0[3] = {tslot(la - 2), tslot(la - 1), tslot(la)};
+        store_init_row(P, c2, sx, st, xslot(la - 1), s0, grow(la - 1), c0, tid, colA, okA, hc, r0);
+        const int s1[3] = {tslot(la - 1), tslot(la), tslot(la + 1)};
+        store_init_row(P, c2, sx, st, xslot(la), s1, grow(la), c0, tid, colA, okA, hc, r1);
+    }
+    IR tr;
+    ThnRow tn;
+    load_init_row(P, b, P.r0 + la + 1, gcA, okA, hc, tr);
+    auto step = [&](int lr, auto load_next) {
+        {   // x0 of row lr+1 (thn rows lr .. lr+2)
+            const int ts[3] = {tslot(lr), tslot(lr + 1), tslot(lr + 2)};
+            store_init_row(P, c2, sx, st, xslot(lr + 1), ts, grow(lr + 1), c0, tid, colA, okA, hc, tr);
+        }
+        const int gcl = live ? gc : 0;
+        typename Epi::P pe[NO];
+#pragma unroll
+        for (int o = 0; o < NO; ++o) pe[o] = epi.pre_lite(P.out_row(o, lr, gcl));
+        const typename S::Cell cl = P.cell_pre(grow(lr), gcl);
+        __syncthreads();
+        if constexpr (decltype(load_next)::value) {   // thn row lr+3 first: it is stored at the end of this step
+            load_thn_row(P, P.r0 + lr + 3, colA, tid, c0, tn);
+            load_init_row(P, b, P.r0 + lr + 2, gcA, okA, hc, tr);
+        }
+        if (live) {
+            const int gr = grow(lr);
+            const XRing xa{sx, {xslot(lr - 1), xslot(lr), xslot(lr + 1)}, gr, c0};
+            const TRingT<kTW, 2> ta{st, {tslot(lr - 1), tslot(lr), tslot(lr + 1)}, gr, c0};
+            const bool edge = __builtin_amdgcn_readfirstlane(__any(gr == 0 || gr == n - 1 || gc == 0 || gc == n - 1)) != 0;
+#pragma unroll
+            for (int o = 0; o < NO; ++o) {
+                double dg;
+                const double acc = edge ? P.template row<true>(o, gr, gc, ta, xa, &dg, cl)
+                                        : P.template row<false>(o, gr, gc, ta, xa, &dg, cl);
+                set_diag(pe[o], dg);
+                set_x(pe[o], xa.X(S::NF == 1 ? 0 : o, gr, gc));
+                epi(P.out_row(o, lr, gc), acc, pe[o]);
+            }
+        }
+        if constexpr (decltype(load_next)::value) store_thn_row(st, tslot(lr + 3), tid, tn);   // slot of row lr-2
+        __syncthreads();
+    };
+    for (int lr = la; lr < lb - 1; ++lr) step(lr, std::true_type{});
+    step(lb - 1, std::false_type{});
+}
+
+// Workgroups of one marching-kernel instance the device holds at once (occupancy x CUs), queried once.
+template <auto K>
 int64_t march_capacity() {
     static int64_t cap = -1;
     if (cap < 0) {
         int dev = 0, cus = 0, per_cu = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_march<S, XS, Epi>, kMB, 0) != hipSuccess)
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, K, kMB, 0) != hipSuccess)
             cus = per_cu = 0;
         cap = (int64_t)cus * per_cu;
     }
@@ -1451,20 +1666,43 @@ int64_t march_capacity() {
 // a launch up to 25 % over one round of workgroups is rebalanced into exactly one round (chunks of
 // rows_per_block or rows_per_block + 1 rows): a second round of a few workgroups would cost almost a whole
 // sweep's latency (ghost-row launches of the CA schedule, multi-GPU row partitions).
-template <class S, class XS, class Epi>
-int launch_march_fixed(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStream_t st) {
+// Chunks (workgroup row ranges) of a marching launch over the rows P.which selects; 0: nothing to do.
+template <class S>
+int64_t march_chunks(const S& P, int rows_per_block, int64_t capacity) {
     const int64_t grows = P.which == 0 ? P.L : P.which == 1 ? (P.L > 2 ? P.L - 2 : 0)
                           : P.which == 3 ? P.L + 2 * P.ext : (P.L >= 2 ? 2 : 1);
-    if (grows == 0) return MPBP_OK;
+    if (grows == 0) return 0;
     const int64_t strips = (P.n + kMB - 1) / kMB;
     int64_t chunks = P.which == 2 ? grows : (grows + rows_per_block - 1) / rows_per_block;
     if (P.which != 2) {
-        const int64_t one_round = march_capacity<S, XS, Epi>() / strips;
+        const int64_t one_round = capacity / strips;
         if (one_round > 0 && chunks > one_round && chunks * 4 <= one_round * 5) chunks = one_round;
     }
+    return chunks;
+}
+
+template <class S, class XS, class Epi>
+int launch_march_fixed(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStream_t st) {
+    const int64_t chunks = march_chunks(P, rows_per_block, march_capacity<k_march<S, XS, Epi>>());
+    if (chunks == 0) return MPBP_OK;
+    const int64_t strips = (P.n + kMB - 1) / kMB;
     k_march<S, XS, Epi><<<(unsigned)(chunks * strips), kMB, 0, st>>>(P, xs, (int)chunks, epi);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
+}
+
+// The first inner sweep with x0 = c2 b / diag staged and diag rebuilt from thn (k_march_init).
+template <class S, class Epi>
+int launch_march_init(const S& P, const double* b, double c2, Epi epi, int rows_per_block, hipStream_t st) {
+    return with_fixed_epi(epi, [&](const auto& e) {
+        using E = std::decay_t<decltype(e)>;
+        const int64_t chunks = march_chunks(P, rows_per_block, march_capacity<k_march_init<S, E>>());
+        if (chunks == 0) return (int)MPBP_OK;
+        const int64_t strips = (P.n + kMB - 1) / kMB;
+        k_march_init<S, E><<<(unsigned)(chunks * strips), kMB, 0, st>>>(P, b, c2, (int)chunks, e);
+        MPBP_HIP(hipGetLastError());
+        return (int)MPBP_OK;
+    });
 }
 
 template <class S, class XS, class Epi>
@@ -1486,6 +1724,10 @@ struct FStencilDevM : FStencilDev {
     template <bool EDGE, class TA, class XA>
     __device__ double row(int f, int gr, int gc, const TA& ta, const XA& xa, double* fd, const Cell& cl) const {
         return f_row<EDGE, TA, XA, false, M>(*this, f, gr, gc, ta, xa, fd, cl.face);
+    }
+    template <class TA>
+    __device__ double stage_diag(int f, int gr, int gc, const TA& ta, const Stage& s) const {
+        return f_stage_diag<M>(*this, f, gr, gc, ta, s);
     }
 };
 
@@ -1729,6 +1971,11 @@ const char* mpbp_version(void) { return "libmpbp 0.1 (gfx950)"; }
 int mpbp_set_march_rows(int32_t rows) {
     if (rows < 1 || rows > 4096) return set_error(MPBP_ERR_ARG, "march rows must be in [1, 4096]");
     g_march_rows = rows;
+    return MPBP_OK;
+}
+int mpbp_set_init_diag(int32_t mode) {
+    if (mode != 0 && mode != 1) return set_error(MPBP_ERR_ARG, "init diag mode must be 0 or 1");
+    g_init_diag = mode;
     return MPBP_OK;
 }
 const char* mpbp_last_error(void) { return g_err; }
@@ -2285,6 +2532,143 @@ int mpbp_gtg_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell
 
 }  // extern "C"
 
+// ================================================ Gt_F_G, 13-point diamond ====
+// Gt_F_G = ((-D) F) G couples every pressure cell with the 13 cells of the diamond |dr| + |dc| <= 2 (n >= 5;
+// every structural product kept, so every row has exactly these 13 entries).  The diamond layout stores the
+// values alone, slot-major (vals[s * N + cell], slots in (dr, dc) lexicographic order = the CSR row's column
+// order for a cell whose diamond does not wrap), and rebuilds the columns from the grid: 104 B per row
+// instead of SELL's 156 B of values + column indices.  A cell within two rows / columns of the periodic edge
+// has its columns in wrapped order; its wave sorts the 13 products by wrapped column (a transposition
+// network in registers) and sums them in that order -- the CSR SpMV's additions exactly, bit for bit.
+// Rebuilding the values themselves from thn (as the D / G / Gt_G sweeps do) would cost ~1000 fp64
+// operations per row (8 F rows of 10 entries, 80 + 96 products, first-touch accumulation): on this chip that
+// is slower than streaming the 104 B.
+namespace {
+constexpr int kQSlots = 13;
+__device__ __host__ constexpr int q13_dr(int s) { return s < 1 ? -2 : s < 4 ? -1 : s < 9 ? 0 : s < 12 ? 1 : 2; }
+__device__ __host__ constexpr int q13_dc(int s) {
+    return s < 1 ? 0 : s < 4 ? s - 2 : s < 9 ? s - 6 : s < 12 ? s - 10 : 0;
+}
+// slot of offset (dr, dc), or -1 outside the diamond
+__device__ inline int q13_slot(int dr, int dc) {
+    const int a = (dr < 0 ? -dr : dr) + (dc < 0 ? -dc : dc);
+    if (a > 2) return -1;
+    return dr == -2 ? 0 : dr == -1 ? 2 + dc : dr == 0 ? 6 + dc : dr == 1 ? 10 + dc : 12;
+}
+__device__ inline int q13_off(int d, int n) {   // periodic offset folded into [-2, 2], or 99
+    if (d > 2) d -= n;
+    if (d < -2) d += n;
+    return (d >= -2 && d <= 2) ? d : 99;
+}
+
+__global__ void k_q13_fill(Csr Q, int32_t n, double* vals, int* bad) {
+    const int32_t N = n * n;
+    const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= N) return;
+    const int gr = r / n, gc = r - (r / n) * n;
+    unsigned seen = 0;
+    bool ok = Q.rp[r + 1] - Q.rp[r] == kQSlots;
+    for (int32_t k = Q.rp[r]; ok && k < Q.rp[r + 1]; ++k) {
+        const int32_t j = Q.ci[k];
+        const int s = q13_slot(q13_off(j / n - gr, n), q13_off(j - (j / n) * n - gc, n));
+        if (s < 0 || ((seen >> s) & 1u)) {
+            ok = false;
+            break;
+        }
+        seen |= 1u << s;
+        vals[(int64_t)s * N + r] = Q.va[k];
+    }
+    if (!ok) atomicAdd(bad, 1);
+}
+
+template <class Epi>
+__global__ void __launch_bounds__(kBlock) k_q13(int32_t n, const double* __restrict__ vals,
+                                                const double* __restrict__ x, Epi epi) {
+    const int32_t N = n * n;
+    const int32_t cell = xcd_swizzle(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
+    if (cell >= N) return;
+    const typename Epi::P pe = epi.pre(cell);
+    const int gr = cell / n, gc = cell - (cell / n) * n;
+    double v[kQSlots];
+#pragma unroll
+    for (int s = 0; s < kQSlots; ++s) v[s] = __builtin_nontemporal_load(vals + (int64_t)s * N + cell);
+    const bool wraps = gr < 2 || gr >= n - 2 || gc < 2 || gc >= n - 2;
+    double acc = 0.0;
+    if (!__any(wraps)) {
+#pragma unroll
+        for (int s = 0; s < kQSlots; ++s) acc += v[s] * x[cell + q13_dr(s) * n + q13_dc(s)];
+    } else {   // (wrapped column, product) pairs sorted by column, then summed in that order
+        int32_t key[kQSlots];
+        double pr[kQSlots];
+#pragma unroll
+        for (int s = 0; s < kQSlots; ++s) {
+            int rr = gr + q13_dr(s), cc = gc + q13_dc(s);
+            rr = rr < 0 ? rr + n : rr >= n ? rr - n : rr;
+            cc = cc < 0 ? cc + n : cc >= n ? cc - n : cc;
+            key[s] = rr * n + cc;
+            pr[s] = v[s] * x[key[s]];
+        }
+#pragma unroll
+        for (int round = 0; round < kQSlots; ++round) {
+#pragma unroll
+            for (int i = round & 1; i + 1 < kQSlots; i += 2) {
+                const bool sw = key[i] > key[i + 1];
+                const int32_t ka = key[i], kb = key[i + 1];
+                const double pa = pr[i], pb = pr[i + 1];
+                key[i] = sw ? kb : ka;
+                key[i + 1] = sw ? ka : kb;
+                pr[i] = sw ? pb : pa;
+                pr[i + 1] = sw ? pa : pb;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < kQSlots; ++s) acc += pr[s];
+    }
+    epi(cell, acc, pe);
+}
+
+template <class Epi>
+int launch_q13(int32_t n, const double* vals, const double* x, Epi epi, hipStream_t st) {
+    k_q13<<<grid_for((int64_t)n * n), kBlock, 0, st>>>(n, vals, x, epi);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+}  // namespace
+
+extern "C" {
+int mpbp_q13_build(const mpbp_csr* Q, int32_t n, double* vals, void* stream) {
+    int rc = check_csr(Q);
+    if (rc) return rc;
+    if (n < 5 || (int64_t)n * n > INT32_MAX / kQSlots || Q->nrows != n * n || Q->ncols != n * n || !vals)
+        return set_error(MPBP_ERR_ARG, "q13_build: needs an n^2 x n^2 operator, n >= 5");
+    const hipStream_t st = as_stream(stream);
+    int* bad = nullptr;
+    MPBP_HIP(hipMallocAsync((void**)&bad, sizeof(int), st));
+    MPBP_HIP(hipMemsetAsync(bad, 0, sizeof(int), st));
+    k_q13_fill<<<grid_for((int64_t)n * n), kBlock, 0, st>>>(to_csr(Q), n, vals, bad);
+    MPBP_HIP(hipGetLastError());
+    int nbad = 0;
+    MPBP_HIP(hipMemcpyAsync(&nbad, bad, sizeof(int), hipMemcpyDeviceToHost, st));
+    MPBP_HIP(hipFreeAsync(bad, st));
+    MPBP_HIP(hipStreamSynchronize(st));
+    if (nbad) return set_error(MPBP_ERR_ARG, "q13_build: %d rows are not the 13-point diamond", nbad);
+    return MPBP_OK;
+}
+
+int mpbp_q13_spmv(int32_t n, const double* vals, int32_t mode, const double* x, const double* z, double* y,
+                  void* stream) {
+    if (n < 5 || (int64_t)n * n > INT32_MAX / kQSlots || !vals || !x || !y || (mode != MPBP_SPMV_STORE && !z))
+        return set_error(MPBP_ERR_ARG, "q13_spmv: bad args");
+    const hipStream_t st = as_stream(stream);
+    switch (mode) {
+    case MPBP_SPMV_STORE: return launch_q13(n, vals, x, EpiStore{y}, st);
+    case MPBP_SPMV_ADD: return launch_q13(n, vals, x, EpiAdd{z, y}, st);
+    case MPBP_SPMV_RESID: return launch_q13(n, vals, x, EpiResid{z, y}, st);
+    default: return set_error(MPBP_ERR_ARG, "q13_spmv: unknown mode %d", mode);
+    }
+}
+}  // extern "C"
+
 // ======================================================= Schur apply ====
 namespace {
 
@@ -2389,14 +2773,21 @@ int op_first_sweep(const OpRef& o, bool cheb, const double* b, const double* dia
         FStencilDev P;
         const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, &P);
         if (rc) return rc;
+        if (g_init_diag == 0)
+            return with_f_identities(P, [&](const auto& Q) {
+                return cheb ? launch_march(Q, xs, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, g_march_rows, st)
+                            : launch_march(Q, xs, EpiJacobi{nullptr, b, nullptr, sub, xo}, g_march_rows, st);
+            });
         return with_f_identities(P, [&](const auto& Q) {
-            return cheb ? launch_march(Q, xs, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, g_march_rows, st)
-                        : launch_march(Q, xs, EpiJacobi{nullptr, b, nullptr, sub, xo}, g_march_rows, st);
+            return cheb ? launch_march_init(Q, b, xs.c2, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, g_march_rows, st)
+                        : launch_march_init(Q, b, xs.c2, EpiJacobi{nullptr, b, nullptr, sub, xo}, g_march_rows, st);
         });
     }
     PGDev P;
     const int rc = make_pgstencil(&p->f_prm, p->f_cell, &q, &P);
     if (rc) return rc;
+    // Gt_G: the staged diagonal is streamed (8 B per row; rebuilding it from thn measured slower, 21.6 vs 16.1 us
+    // at 1024^2: the sweep is latency-bound and the rebuild lengthens its staging)
     const GtGStencilDev S{P};
     return cheb ? launch_march(S, xs, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, pg_rows(), st)
                 : launch_march(S, xs, EpiJacobi{nullptr, b, nullptr, sub, xo}, pg_rows(), st);
@@ -2647,8 +3038,12 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
     rc = inner_solve(c, MPBP_VEC_PRESSURE, P, p->diag_P, p->inner_P, p->np, Prhs, Pxa, nullptr, P0, P1, Pd, false);
     if (rc) return rc;
     // 4. x_b = Gt_F_G @ x_a                                                solve.py:267
-    rc = two_phase(c, MPBP_VEC_PRESSURE, Pxa, Q,
-                   [&](const OpRef& o) { return op_spmv(o, MPBP_SPMV_STORE, Pxa, nullptr, Pxb, c.st); });
+    //    (one GPU: the diamond layout when the plan has it)
+    if (p->q13 && !p->halo)
+        rc = mpbp_q13_spmv(p->q13_n, p->q13, MPBP_SPMV_STORE, Pxa, nullptr, Pxb, (void*)c.st);
+    else
+        rc = two_phase(c, MPBP_VEC_PRESSURE, Pxa, Q,
+                       [&](const OpRef& o) { return op_spmv(o, MPBP_SPMV_STORE, Pxa, nullptr, Pxb, c.st); });
     if (rc) return rc;
     // 5. x_p = Gt_G_factorization @ x_b                                    solve.py:271
     //    (one GPU: straight into the output, which G then reads; a partition needs x_p's ghost rows)

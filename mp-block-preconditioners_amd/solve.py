@@ -117,6 +117,27 @@ def _pg_stencil(D, G, GtG, f_stencil, pg_mode):
     return sp if ok else None
 
 
+def _q13_layout(Q: DeviceCSR, q_mode: str):
+    """(n, values[13 n^2]) of Gt_F_G in the diamond layout (mpbp_q13_build), or None (q_mode 'assembled', or
+    'auto' on an operator that is not the 13-point periodic-grid product)."""
+    if q_mode not in ("auto", "diamond", "assembled"):
+        raise ValueError("q_mode must be 'auto', 'diamond' or 'assembled'")
+    if q_mode == "assembled":
+        return None
+    n = math.isqrt(Q.shape[0])
+    if n * n != Q.shape[0] or Q.shape != (n * n, n * n) or n < 5:
+        if q_mode == "diamond":
+            raise ValueError("q_mode='diamond' needs Gt_F_G of an n x n grid, n >= 5")
+        return None
+    vals = torch.empty(13 * n * n, dtype=torch.float64, device=Q.device)
+    rc = lib().mpbp_q13_build(ctypes.byref(Q.cstruct()), n, ptr(vals), stream_handle())
+    if rc:
+        if q_mode == "diamond":
+            raise ValueError(f"q_mode='diamond': {lib().mpbp_last_error().decode()}")
+        return None
+    return n, vals
+
+
 def _capture(pc, v: torch.Tensor, out: torch.Tensor, capture_error_mode: str = "global"):
     """One pc.apply(v, out) captured into a torch.cuda.CUDAGraph (warm-up on a side stream first).
     capture_error_mode "thread_local" lets other threads (RCCL's proxy thread) keep making HIP calls that
@@ -146,7 +167,7 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
 
     def __init__(self, F, D, G, GtG=None, GtFG=None, inner_F: InnerSolver | None = None,
                  inner_P: InnerSolver | None = None, device=None, layout: str = "sell", f_mode: str = "auto",
-                 pg_mode: str = "auto"):
+                 pg_mode: str = "auto", q_mode: str = "auto"):
         dev = torch.device(device or (F.device if isinstance(F, DeviceCSR) else "cuda"))
         self.F, self.D, self.G = (_device_csr(M, dev) for M in (F, D, G))
         if GtG is None or GtFG is None:
@@ -182,6 +203,10 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
         # D, G, Gt_G likewise ("pg"): recomputed from the cell thn table when all three carry stencils of
         # one grid (get_big_A_matrix + commutator_products), else streamed from their stored copies.
         self.pg_stencil = _pg_stencil(self.D, self.G, self.GtG, self.f_stencil, pg_mode)
+        # Gt_F_G: "diamond" streams its values in the 13-point diamond layout (columns implicit in the grid,
+        # 104 B per row instead of 156), "assembled" the CSR / SELL copy; "auto" = diamond whenever Gt_F_G is
+        # the n^2 x n^2 periodic-grid product (n >= 5), else assembled.
+        self.q13 = _q13_layout(self.GtFG, q_mode)
         self._plan = self._make_plan()
         super().__init__(dtype=np.float64, shape=(nu + np_, nu + np_))
 
@@ -222,6 +247,8 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
         p.prof_events = None
         p.prof_capacity = 0
         p.prof_count = ctypes.POINTER(ctypes.c_int32)()
+        if self.q13 is not None:
+            p.q13, p.q13_n = self.q13[1].data_ptr(), self.q13[0]
         return p
 
     def sell_of(self, key):

@@ -147,3 +147,26 @@ def test_pg_mode_validation():
     _, _, F2, D2, G2 = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
     assert D2.stencil is None and G2.stencil is None           # n <= 2: no matrix-free forms
     assert mp.ApproxSchurPreconditioner(F2, D2, G2).pg_stencil is None
+
+
+@pytest.mark.parametrize("n", [3, 4, 5, 50, 256, 257, 300])
+@pytest.mark.parametrize("prm", PARAMS, ids=["visc", "stiff", "c0-neg-dp"])
+@pytest.mark.parametrize("inner", [INNERS[0], INNERS[1], INNERS[3]], ids=["c4c3", "j3c2", "j1c1"])
+def test_fused_first_sweep_rebuilt_diagonal(n, prm, inner, march_rows):
+    """The fused first inner sweep with the staged diagonal rebuilt from thn (k_march_init, default) equals the
+    one that streams the stored diagonal (k_march<XInit>) and the fully assembled apply, bit for bit -- every
+    parameter identity instance of the F policy, strips with ragged last columns (n = 257, 300), n = 3."""
+    import mp_block_preconditioners_amd as mp
+    from mp_block_preconditioners_amd._lib import check, lib
+    F, D, G, GtG, GtFG = _system(n, prm)
+    kw = dict(inner_F=mp.InnerSolver(*inner[0]), inner_P=mp.InnerSolver(*inner[1]))
+    ref_pc = mp.ApproxSchurPreconditioner(F, D, G, GtG, GtFG, f_mode="assembled", pg_mode="assembled", **kw)
+    pc = mp.ApproxSchurPreconditioner(F, D, G, GtG, GtFG, f_mode="stencil", pg_mode="stencil", **kw)
+    v = torch.from_numpy(np.random.default_rng(n + 7).standard_normal(ref_pc.shape[0])).cuda()
+    ref = ref_pc.apply(v)
+    try:
+        for mode in (1, 0):
+            check(lib().mpbp_set_init_diag(mode))
+            assert _bits(pc.apply(v), ref), (mode, rel_inf(pc.apply(v).cpu().numpy(), ref.cpu().numpy()))
+    finally:
+        check(lib().mpbp_set_init_diag(1))

@@ -6,6 +6,7 @@
 #
 # Steps:
 #   tests        pytest -m gpu (all GPU parity tests)          smoke     __graft_entry__.smoke()
+#   tests:F1,F2  pytest -m gpu of the named test files / node ids only
 #   bench        bench.py, N = 1 (the driver's command)        bench_csr bench.py --layout csr
 #   rows2_gloo   bench.py --gpus 2 --grid 512 over gloo on one GPU (the N > 1 path; launcher inside bench.py)
 #   selfhalo     bench.py --self-halo (partitioned apply over the RCCL self-exchange)
@@ -39,6 +40,8 @@ step() {
   case $s in
     tests) timeout -k 10 1000 python -u -m pytest tests/ -x -v --timeout 240 --timeout-method thread -m gpu \
              > "$OUT/pytest.log" 2>&1 ;;
+    tests:*) timeout -k 10 900 python -u -m pytest $(echo "${s#tests:}" | tr , ' ') -x -q --timeout 240 \
+               --timeout-method thread -m gpu > "$OUT/pytest_part.log" 2>&1 ;;
     smoke) timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench) timeout -k 10 300 python bench.py --steps 20 --warmup 5 > "$OUT/bench.log" 2>&1 ;;
     bench_csr) timeout -k 10 300 python bench.py --steps 20 --warmup 5 --layout csr --no-cpu-baseline \

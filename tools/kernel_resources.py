@@ -14,7 +14,7 @@ SRC = os.environ.get("MPBP_SRC") or os.path.join(ROOT, "mp-block-preconditioners
 def main():
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
            "-fno-fast-math", "-I" + os.path.join(ROOT, "include"), "--offload-device-only", "-c", SRC,
-           "-o", "/tmp/_mpbp_res.o", "-Rpass-analysis=kernel-resource-usage"]
+           "-o", "/tmp/_mpbp_res.o", *os.environ.get("MPBP_FLAGS", "").split(), "-Rpass-analysis=kernel-resource-usage"]
     out = subprocess.run(cmd, capture_output=True, text=True).stderr
     rows, cur = [], None
     for line in out.splitlines():
