@@ -105,6 +105,8 @@ def main():
     ap.add_argument("--no-spmv", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch the apply eagerly instead of a hipGraph")
     ap.add_argument("--no-check", action="store_true", help="N > 1: skip the bit-exact check against one GPU")
+    ap.add_argument("--no-solve", action="store_true",
+                    help="skip the solve-level section (FGMRES to 1e-8 on the manufactured problem, N = 1)")
     ap.add_argument("--partitioned-graph", action="store_true",
                     help="N > 1: capture the partitioned apply (RCCL halo groups included) into a hipGraph")
     args = ap.parse_args()
@@ -265,6 +267,10 @@ def main():
     if rank == 0 and not partitioned and not args.no_cpu_baseline:
         cpu = cpu_baseline(pc, v, args.cpu_seconds, kf, sf, kp, spp)
 
+    solve = None
+    if rank == 0 and not partitioned and not args.no_solve:
+        solve = solve_level(args)
+
     if rank == 0:
         scale = n * n / float(1024 * 1024)
         value = args.steps / dt * scale
@@ -314,8 +320,9 @@ def main():
                 "frac": spmv["csr_gbs"] / HBM_PEAK_GBS, "traffic": spmv_traffic,
                 "kernel": "k_csr_wave<EpiStore> (A u, 5N rows, CSR)", "bytes_per_launch": spmv["csr_bytes"],
                 "avg_launch_us": spmv["csr_us"],
-                "timing": "HIP events around 20 back-to-back launches (one kernel per matvec)"},
+                "timing": spmv.get("timing", "") + " (one kernel per matvec)"},
             "host_buffer_matvec": host_io,
+            "solve_level": solve,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -364,13 +371,17 @@ def single_gpu_check(dpc, n, args, iF, iP, rank, dist, torch):
                     f"vector (numpy seed 2048), built on each rank's GPU; {time.perf_counter() - t0:.1f} s"}
 
 
-def spmv_bench(A, gen, reps=20):
-    """The plain operator matvec b = A u (apply.py:72) in both layouts, HIP-event timed."""
+def spmv_bench(A, gen, reps=20, replays=5):
+    """The plain operator matvec b = A u (apply.py:72) in both layouts, HIP-event timed.
+
+    `reps` back-to-back launches are captured into one hipGraph and replayed `replays` times between two
+    events (the per-launch time then excludes the Python launch overhead, which an eager loop of 140-us
+    kernels partly exposes); the eager loop's time is reported beside it (`*_us_eager`)."""
     import torch
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     x = torch.randn(A.shape[1], dtype=torch.float64, device="cuda", generator=gen)
     y = torch.empty(A.shape[0], dtype=torch.float64, device="cuda")
-    res = {"nnz": A.nnz}
+    res = {"nnz": A.nnz, "timing": f"HIP events around {replays} replays of a hipGraph of {reps} launches"}
     AS = A.to_sell()
     csr_bytes = A.nnz * 12 + (A.shape[0] + 1) * 4 + (A.shape[0] + A.shape[1]) * 8 + A.blocks.count * 8
     for name, M, nbytes in (
@@ -383,9 +394,82 @@ def spmv_bench(A, gen, reps=20):
             M.matvec(x, out=y)
         ev[1].record()
         torch.cuda.synchronize()
-        s = ev[0].elapsed_time(ev[1]) / 1e3 / reps
-        res.update({f"{name}_gbs": nbytes / s / 1e9, f"{name}_us": s * 1e6, f"{name}_bytes": nbytes})
+        s_eager = ev[0].elapsed_time(ev[1]) / 1e3 / reps
+        s = s_eager
+        try:
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                M.matvec(x, out=y)
+            torch.cuda.current_stream().wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(reps):
+                    M.matvec(x, out=y)
+            g.replay()
+            torch.cuda.synchronize()
+            ev[0].record()
+            for _ in range(replays):
+                g.replay()
+            ev[1].record()
+            torch.cuda.synchronize()
+            s = ev[0].elapsed_time(ev[1]) / 1e3 / (reps * replays)
+            del g
+        except Exception as e:   # eager number only, and say why
+            res[f"{name}_graph_note"] = f"graph capture failed: {e}"
+        res.update({f"{name}_gbs": nbytes / s / 1e9, f"{name}_us": s * 1e6, f"{name}_bytes": nbytes,
+                    f"{name}_us_eager": s_eager * 1e6})
     return res
+
+
+SOLVE_CASES = (   # (n, eta_n, eta_s, preconditioners): BASELINE configs[1] / configs[3] at 256^2, configs[2] / [3] at 1024^2
+    (256, 100.0, 1.0, ("none", "chebyshev:4", "chebyshev:8", "mg:1")),
+    (256, 1e4, 1.0, ("none", "chebyshev:4", "chebyshev:8", "mg:1")),
+    (1024, 100.0, 1.0, ("chebyshev:4", "mg:1")),
+    (1024, 1e4, 1.0, ("chebyshev:4", "mg:1")),
+)
+
+
+def solve_level(args, cases=SOLVE_CASES, tol=1e-8, maxiter=150):
+    """What the applies/s headline buys: FGMRES (tol 1e-8, maxiter 150, x0 = 0, solve.py:285) on the reference's
+    manufactured problem (solve.py:52-80) with the approximate Schur preconditioner and different inner solves:
+    iterations, time to tolerance (the fgmres call; preconditioner set-up reported apart) and the velocity error."""
+    import numpy as np
+    import torch
+    import mp_block_preconditioners_amd as mp
+    out = []
+    for n, eta_n, eta_s, precs in cases:
+        bp = mp.MultiphaseBlockPreconditioner(n, args.xi, eta_n, eta_s)
+        A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+        u, b = mp.manufactured_problem(n, xi=args.xi, etan=eta_n, etas=eta_s)
+        bd = torch.from_numpy(b).cuda()
+        nb = float(torch.linalg.vector_norm(bd))
+        for name in precs:
+            t0 = time.perf_counter()
+            M = None
+            if name != "none":
+                kind, _, k = name.partition(":")
+                inner = mp.InnerSolver(kind, int(k))
+                M = mp.ApproxSchurPreconditioner(F, D, G, inner_F=inner, inner_P=inner)
+            torch.cuda.synchronize()
+            setup = time.perf_counter() - t0
+            hist = []
+            t0 = time.perf_counter()
+            x, info = mp.fgmres(A, bd, M=M, tol=tol, maxiter=maxiter, residuals=hist)
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            res = float(torch.linalg.vector_norm(bd - A.matvec(x))) / nb
+            err = float(np.max(np.abs(x.cpu().numpy()[: 4 * n * n] - u[: 4 * n * n])))
+            out.append({"n": n, "eta_n": eta_n, "eta_s": eta_s, "preconditioner": name, "iterations": len(hist) - 1,
+                        "converged": info == 0, "seconds": el, "setup_seconds": setup, "true_rel_residual": res,
+                        "velocity_max_error": err})
+            del M, x
+            torch.cuda.empty_cache()
+        del A, F, D, G, bp
+        torch.cuda.empty_cache()
+    return {"tol": tol, "maxiter": maxiter, "problem": "manufactured solution of solve.py:52-80, x0 = 0",
+            "inner": "chebyshev:K = K Chebyshev-Jacobi sweeps; mg:K = K multigrid V-cycles (V(2,2), Chebyshev smoothing)",
+            "runs": out}
 
 
 def cpu_baseline(pc, v, seconds, kf, sf, kp, spp):

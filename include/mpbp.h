@@ -57,6 +57,13 @@ extern "C" {
 /* inner solvers of the approximate Schur preconditioner */
 #define MPBP_INNER_JACOBI 0
 #define MPBP_INNER_CHEBYSHEV 1
+#define MPBP_INNER_MG 2         /* geometric multigrid V-cycles (plan.mg_F / plan.mg_P); sweeps = cycles */
+
+/* multigrid transfers: per field and axis, cell- or node-centred; which operator */
+#define MPBP_MG_CELL 0
+#define MPBP_MG_NODE 1
+#define MPBP_MG_P 0   /* prolongation, fine x coarse */
+#define MPBP_MG_R 1   /* restriction = P^T, coarse x fine */
 
 /* halo callback phases / vector kinds (multi-GPU row partition) */
 #define MPBP_HALO_BEGIN 0
@@ -130,6 +137,31 @@ typedef struct mpbp_inner_solver {
     double lmax;
 } mpbp_inner_solver;
 
+/* One level of a geometric multigrid hierarchy (Galerkin: A_{l+1} = R_l A_l P_l).  The coarsest level's A is
+ * solved by mpbp_mg.coarse_inv; R / P are unused there. */
+typedef struct mpbp_mg_level {
+    int32_t nrows;
+    int32_t pre, post;               /* Chebyshev-Jacobi smoothing sweeps (>= 1) */
+    int32_t reserved;
+    double lmin, lmax;               /* smoothing interval of diag(A)^-1 A */
+    mpbp_csr A;
+    mpbp_rowblocks A_blocks;
+    const double* diag;              /* device, nrows */
+    mpbp_csr R;                      /* to level + 1 */
+    mpbp_rowblocks R_blocks;
+    mpbp_csr P;                      /* from level + 1 */
+    mpbp_rowblocks P_blocks;
+    double *x, *t, *r, *d, *b;       /* device work vectors, nrows each */
+} mpbp_mg_level;
+
+typedef struct mpbp_mg {
+    int32_t nlevels;                 /* >= 2 */
+    int32_t cycles;                  /* V-cycles per solve, from x = 0 */
+    const mpbp_mg_level* levels;     /* host array */
+    mpbp_csr coarse_inv;             /* (pseudo-)inverse of the coarsest A, every entry stored */
+    mpbp_rowblocks coarse_inv_blocks;
+} mpbp_mg;
+
 typedef void (*mpbp_halo_fn)(void* ctx, int32_t vec_kind, double* x_ext, int32_t phase, void* stream);
 /* A velocity and a pressure vector's halos in one exchange, complete on `stream` when it returns. */
 typedef void (*mpbp_halo_pair_fn)(void* ctx, double* xu_ext, double* xp_ext, void* stream);
@@ -183,6 +215,8 @@ typedef struct mpbp_schur_plan {
     const double* q13;               /* optional (one GPU): Gt_F_G in the 13-point diamond layout
                                         (mpbp_q13_build), used instead of GtFG / Qs_* when set */
     int32_t q13_n;                   /* its grid size n */
+    const mpbp_mg* mg_F;             /* inner_F.kind == MPBP_INNER_MG: F's hierarchy (level 0 = F; one GPU) */
+    const mpbp_mg* mg_P;             /* inner_P.kind == MPBP_INNER_MG: Gt_G's hierarchy */
 } mpbp_schur_plan;
 
 const char* mpbp_version(void);
@@ -315,6 +349,17 @@ int mpbp_set_march_rows(int32_t rows);
 /* The first sweep of a matrix-free F inner solve stages x0 = c2 b / diag: mode 1 (default) rebuilds diag from the
  * thn tables inside the sweep (no diag stream), mode 0 streams the stored diagonal.  Same bits either way. */
 int mpbp_set_init_diag(int32_t mode);
+
+/* ---- geometric multigrid inner solves (the reference's pointer: solve.py:266, 274) ------------------ */
+/* P (which = MPBP_MG_P, fine x coarse) or R = P^T (MPBP_MG_R) of an n x n periodic grid (n even, >= 4) coarsened by 2,
+ * for nfields stacked fields; kinds (host) = {ky, kx} per field (MPBP_MG_CELL / MPBP_MG_NODE along rows / columns).
+ * Columns sorted, values exact dyadic rationals.  count writes row_nnz (device); fill needs row_ptr.  Setup. */
+int mpbp_mg_transfer_count(int32_t n, int32_t nfields, const int32_t* kinds, int32_t which, int32_t* row_nnz,
+                           void* stream);
+int mpbp_mg_transfer_fill(int32_t n, int32_t nfields, const int32_t* kinds, int32_t which, const int32_t* row_ptr,
+                          int32_t* col_idx, double* val, void* stream);
+/* x_out = mg->cycles V-cycles for levels[0].A x = b from x = 0 (sub - x when sub != NULL).  Graph-capturable. */
+int mpbp_mg_solve(const mpbp_mg* mg, const double* b, const double* sub, double* x_out, void* stream);
 
 /* ---- ghost rows over RCCL point-to-point (multi-GPU row partition) ------------------------------ */
 /* One RCCL group of neighbour sends / receives: the owned boundary rows (packed into one buffer per

@@ -4,6 +4,7 @@ include/mpbp.h).  Import name: ``mp_block_preconditioners_amd`` (a symlink to th
 """
 from ._lib import MpbpError, lib
 from .csr import DeviceCSR, DeviceSELL, spgemm
+from .mg import FIELDS_PRESSURE, FIELDS_VELOCITY, Multigrid
 from .preconditioner import MultiphaseBlockPreconditioner, thn, ths
 from .solve import (ApproxSchurPreconditioner, InnerSolver, fgmres, print_true_res_norm,
                     solve_with_approx_schur_pc, solve_without_pc)
@@ -14,5 +15,5 @@ __all__ = [
     "MpbpError", "lib", "DeviceCSR", "DeviceSELL", "spgemm", "MultiphaseBlockPreconditioner", "thn", "ths",
     "ApproxSchurPreconditioner", "InnerSolver", "fgmres", "print_true_res_norm",
     "solve_with_approx_schur_pc", "solve_without_pc", "fill_sol_and_RHS_vecs", "manufactured_problem", "manufactured_problem_constant", "max_norm",
-    "print_norms", "weighted_L1", "weighted_L2",
+    "print_norms", "weighted_L1", "weighted_L2", "Multigrid", "FIELDS_VELOCITY", "FIELDS_PRESSURE",
 ]

@@ -13,7 +13,9 @@ LIB_PATH = os.environ.get("MPBP_LIB") or os.path.join(HERE, "lib", "libmpbp.so")
 OP_A, OP_F, OP_D, OP_G = 0, 1, 2, 3
 OP_L_N, OP_L_S, OP_D_N, OP_D_S, OP_G_N, OP_G_S, OP_XI_N, OP_XI_S = range(4, 12)
 SPMV_STORE, SPMV_ADD, SPMV_RESID = 0, 1, 2
-INNER_JACOBI, INNER_CHEBYSHEV = 0, 1
+INNER_JACOBI, INNER_CHEBYSHEV, INNER_MG = 0, 1, 2
+MG_CELL, MG_NODE = 0, 1
+MG_P, MG_R = 0, 1
 HALO_BEGIN, HALO_END = 0, 1
 VEC_VELOCITY, VEC_PRESSURE = 0, 1
 PG_D, PG_G, PG_GTG = 0, 1, 2
@@ -53,6 +55,18 @@ class InnerSolverC(Structure):
     _fields_ = [("kind", c_int32), ("sweeps", c_int32), ("lmin", c_double), ("lmax", c_double)]
 
 
+class MgLevel(Structure):
+    _fields_ = [("nrows", c_int32), ("pre", c_int32), ("post", c_int32), ("reserved", c_int32),
+                ("lmin", c_double), ("lmax", c_double), ("A", Csr), ("A_blocks", RowBlocks), ("diag", c_void_p),
+                ("R", Csr), ("R_blocks", RowBlocks), ("P", Csr), ("P_blocks", RowBlocks),
+                ("x", c_void_p), ("t", c_void_p), ("r", c_void_p), ("d", c_void_p), ("b", c_void_p)]
+
+
+class Mg(Structure):
+    _fields_ = [("nlevels", c_int32), ("cycles", c_int32), ("levels", POINTER(MgLevel)), ("coarse_inv", Csr),
+                ("coarse_inv_blocks", RowBlocks)]
+
+
 HALO_FN = CFUNCTYPE(None, c_void_p, c_int32, c_void_p, c_int32, c_void_p)
 HALO_PAIR_FN = CFUNCTYPE(None, c_void_p, c_void_p, c_void_p, c_void_p)
 
@@ -75,7 +89,7 @@ class SchurPlan(Structure):
                 ("f_vface", c_void_p), ("f_part", RowPart), ("pg_stencil", c_int32), ("p_part", RowPart),
                 ("halo_first", c_int32), ("ca", c_int32), ("ca_reach_q", c_int32), ("wu_ext", c_void_p),
                 ("diag_F_ext", c_void_p), ("diag_P_ext", c_void_p), ("halo_pair", HALO_PAIR_FN),
-                ("q13", c_void_p), ("q13_n", c_int32)]
+                ("q13", c_void_p), ("q13_n", c_int32), ("mg_F", POINTER(Mg)), ("mg_P", POINTER(Mg))]
 
 
 _P = c_void_p
@@ -130,6 +144,9 @@ _SIGNATURES = {
     "mpbp_set_init_diag": ([c_int32], c_int),
     "mpbp_q13_build": ([POINTER(Csr), c_int32, c_void_p, c_void_p], c_int),
     "mpbp_q13_spmv": ([c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+    "mpbp_mg_transfer_count": ([c_int32, c_int32, _P, c_int32, _P, _P], c_int),
+    "mpbp_mg_transfer_fill": ([c_int32, c_int32, _P, c_int32, _P, _P, _P, _P], c_int),
+    "mpbp_mg_solve": ([POINTER(Mg), _P, _P, _P, _P], c_int),
     "mpbp_gather": ([c_int32, _P, _P, _P, _P], c_int),
     "mpbp_scatter": ([c_int32, _P, _P, _P, _P], c_int),
     "mpbp_event_create": ([POINTER(c_void_p)], c_int),
@@ -182,4 +199,5 @@ def stream_handle(stream=None):
 
 
 __all__ = ["lib", "check", "ptr", "stream_handle", "MpbpError", "Csr", "RowBlocks", "Sell", "RowPart", "StokesParams",
-           "InnerSolverC", "SchurPlan", "HALO_FN", "byref"]
+           "InnerSolverC", "SchurPlan", "HALO_FN", "byref",
+           "Mg", "MgLevel"]

@@ -567,6 +567,100 @@ __global__ void k_scatter(int32_t count, const int32_t* idx, const double* src, 
     if (i < count) dst[idx[i]] = src[i];
 }
 
+// ============================================================ multigrid transfers ====
+// Geometric coarsening of a periodic n x n MAC grid by 2 in each direction, field by field.  Along an axis a
+// field is cell-centred (MPBP_MG_CELL: fine 2i and 2i+1 lie around coarse i, linear weights 3/4, 1/4) or
+// node-centred (MPBP_MG_NODE: fine 2i sits on coarse i, fine 2i+1 halfway to coarse i+1).  P (fine <- coarse)
+// is the tensor product of the two 1D lists; R = P^T exactly.  Every weight is a dyadic rational, so the
+// values are exact and the columns of each row come out sorted (periodic wrap included).
+struct MgFields {
+    int32_t nfields;
+    int32_t ky[8], kx[8];
+};
+
+template <int CAP>
+__device__ inline void sort_pairs(int m, int* idx, double* w) {
+#pragma unroll
+    for (int a = 1; a < CAP; ++a)
+#pragma unroll
+        for (int b = CAP - 1; b >= a; --b)
+            if (b < m && idx[b - 1] > idx[b]) {
+                const int ti = idx[b - 1];
+                idx[b - 1] = idx[b];
+                idx[b] = ti;
+                const double tw = w[b - 1];
+                w[b - 1] = w[b];
+                w[b] = tw;
+            }
+}
+
+// P's 1D list for fine index f (coarse size nc): <= 2 entries.
+__device__ inline int mg_p1d(int kind, int nc, int f, int* idx, double* w) {
+    const int i = f >> 1;
+    if (kind == MPBP_MG_NODE && !(f & 1)) {
+        idx[0] = i;
+        w[0] = 1.0;
+        return 1;
+    }
+    const int j = (kind == MPBP_MG_CELL && !(f & 1)) ? (i + nc - 1) % nc : (i + 1) % nc;
+    idx[0] = i;
+    w[0] = kind == MPBP_MG_CELL ? 0.75 : 0.5;
+    idx[1] = j;
+    w[1] = kind == MPBP_MG_CELL ? 0.25 : 0.5;
+    sort_pairs<2>(2, idx, w);
+    return 2;
+}
+
+// R's 1D list for coarse index i (fine size nf) = column i of P: <= 4 entries.
+__device__ inline int mg_r1d(int kind, int nf, int i, int* idx, double* w) {
+    const int f = 2 * i;
+    int m;
+    if (kind == MPBP_MG_CELL) {
+        idx[0] = (f + nf - 1) % nf; w[0] = 0.25;
+        idx[1] = f;                 w[1] = 0.75;
+        idx[2] = f + 1;             w[2] = 0.75;
+        idx[3] = (f + 2) % nf;      w[3] = 0.25;
+        m = 4;
+    } else {
+        idx[0] = (f + nf - 1) % nf; w[0] = 0.5;
+        idx[1] = f;                 w[1] = 1.0;
+        idx[2] = f + 1;             w[2] = 0.5;
+        m = 3;
+    }
+    sort_pairs<4>(m, idx, w);
+    return m;
+}
+
+// which: MPBP_MG_P (rows = fine unknowns) or MPBP_MG_R (rows = coarse unknowns); n = fine grid size.
+__global__ void k_mg_transfer(MgFields F, int32_t n, int32_t which, int64_t nrows, const int32_t* rp,
+                              int32_t* row_nnz, int32_t* ci, double* va) {
+    const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= nrows) return;
+    const int nc = n / 2;
+    const int nr = which == MPBP_MG_P ? n : nc;       // grid size of the rows' level
+    const int nk = which == MPBP_MG_P ? nc : n;       // ... and of the columns' level
+    const int64_t per = (int64_t)nr * nr;
+    const int fld = (int)(row / per);
+    const int64_t cell = row - fld * per;
+    const int r = (int)(cell / nr), c = (int)(cell % nr);
+    int yi[4], xi[4];
+    double yw[4], xw[4];
+    const int my = which == MPBP_MG_P ? mg_p1d(F.ky[fld], nc, r, yi, yw) : mg_r1d(F.ky[fld], n, r, yi, yw);
+    const int mx = which == MPBP_MG_P ? mg_p1d(F.kx[fld], nc, c, xi, xw) : mg_r1d(F.kx[fld], n, c, xi, xw);
+    if (row_nnz) {
+        row_nnz[row] = my * mx;
+        return;
+    }
+    const int64_t off = (int64_t)fld * nk * nk;
+    int32_t k = rp[row];
+    for (int a = 0; a < my; ++a)
+        for (int b = 0; b < mx; ++b) {
+            ci[k] = (int32_t)(off + (int64_t)yi[a] * nk + xi[b]);
+            va[k] = yw[a] * xw[b];
+            ++k;
+        }
+}
+
 // ================================================================== SpMV ====
 // Row blocks are dealt round-robin over the 8 XCDs; give every XCD a contiguous run of
 // blocks instead, so the +-n stencil neighbours of a block's rows sit in the same L2.
@@ -2825,11 +2919,128 @@ int two_phase(const Ctx& c, int32_t kind, const double* x_ext, const OpPair& op,
     return launch(op.bd);
 }
 
+// ---- geometric multigrid inner solve (MPBP_INNER_MG) ----
+// The reference's own pointer for these inverses: "In IBAMR, we'd use Multigrid PC with Jacobi smoother"
+// (solve.py:266, 274).  V-cycles over the levels of an mpbp_mg hierarchy (Galerkin coarse operators
+// R A P, mpbp_mg_transfer_*): Chebyshev-Jacobi pre- and post-smoothing on each level, the coarsest level solved
+// by its dense (pseudo-)inverse.  Every step is an existing apply-path kernel (SpMV epilogues, Chebyshev
+// steps), so the cycle is graph-capturable and its operation order is the oracle's (oracle/mg_oracle.py).
+// Level 0 can be any operator of the plan (matrix-free stencil, SELL or CSR: the same bits).
+struct MgFine {
+    OpRef op;
+    const double* diag;
+    double *x, *t, *r, *d;   // two iterate buffers, residual, Chebyshev direction
+};
+
+OpRef mg_csr_op(const mpbp_csr& A, const mpbp_rowblocks& blk) {
+    return OpRef{&A, &blk, nullptr, nullptr, false, 0, SOP_NONE};
+}
+
+// K Chebyshev-Jacobi sweeps on [lmin, lmax].  zero: from x = 0 (the first sweep is the init pass: d = x =
+// c2[0] b / diag), else from the iterate in *cur (d starts at 0).  The last sweep writes `dst` (or the free
+// ping-pong buffer when dst is NULL), as sub - x when sub is set; *cur points at the result on return.
+int mg_smooth(const OpRef& o, int32_t nrows, const double* diag, double lmin, double lmax, int K, bool zero,
+              const double* b, double** cur, double* alt, double* d, double* dst, const double* sub, hipStream_t st) {
+    double c1[64] = {}, c2[64] = {};
+    if (K < 1 || K > 64) return set_error(MPBP_ERR_ARG, "mg: smoothing sweeps must be in [1, 64]");
+    cheb_coeffs(lmin, lmax, K, c1, c2);
+    double* x = *cur;
+    double* other = alt;
+    int s = 0;
+    if (zero) {
+        double* out0 = K == 1 ? (dst ? dst : other) : x;
+        int rc = mpbp_cheb_init(nrows, b, diag, c2[0], d, K == 1 ? sub : nullptr, out0, (void*)st);
+        if (rc) return rc;
+        if (K == 1) {
+            *cur = out0;
+            return MPBP_OK;
+        }
+        s = 1;
+    } else {
+        MPBP_HIP(hipMemsetAsync(d, 0, sizeof(double) * (size_t)nrows, st));
+    }
+    for (; s < K; ++s) {
+        const bool last = s == K - 1;
+        double* nxt = (last && dst) ? dst : other;
+        const int rc = op_cheb(o, x, b, diag, c1[s], c2[s], d, last ? sub : nullptr, nxt, st, last ? 0 : 1);
+        if (rc) return rc;
+        other = x;
+        x = nxt;
+    }
+    *cur = x;
+    return MPBP_OK;
+}
+
+// One V-cycle on level l for A_l x = b.  Level 0 uses `fine` (operator and buffers); coarser levels their
+// mpbp_mg_level.  *res receives the result's buffer (dst when given).
+int mg_vcycle(const mpbp_mg* m, int l, const MgFine& fine, const double* b, bool zero, double* xin, double* dst,
+              const double* sub, double** res, hipStream_t st) {
+    const mpbp_mg_level& L = m->levels[l];
+    const bool top = l == 0;
+    const OpRef o = top ? fine.op : mg_csr_op(L.A, L.A_blocks);
+    const double* diag = top ? fine.diag : L.diag;
+    double* bx = top ? fine.x : L.x;
+    double* bt = top ? fine.t : L.t;
+    double* alt = xin == bx ? bt : bx;
+    double* r = top ? fine.r : L.r;
+    double* d = top ? fine.d : L.d;
+    double* cur = xin;
+    int rc = mg_smooth(o, L.nrows, diag, L.lmin, L.lmax, L.pre, zero, b, &cur, alt, d, nullptr, nullptr, st);
+    if (rc) return rc;
+    alt = cur == bx ? bt : bx;
+    // r = b - A x ; b_c = R r
+    rc = op_spmv(o, MPBP_SPMV_RESID, cur, b, r, st);
+    if (rc) return rc;
+    const mpbp_mg_level& C = m->levels[l + 1];
+    rc = mpbp_spmv(&L.R, &L.R_blocks, MPBP_SPMV_STORE, r, nullptr, C.b, (void*)st);
+    if (rc) return rc;
+    double* xc = C.x;
+    if (l + 1 == m->nlevels - 1) {
+        rc = mpbp_spmv(&m->coarse_inv, &m->coarse_inv_blocks, MPBP_SPMV_STORE, C.b, nullptr, xc, (void*)st);
+    } else {
+        rc = mg_vcycle(m, l + 1, fine, C.b, true, C.x, nullptr, nullptr, &xc, st);
+    }
+    if (rc) return rc;
+    // x += P x_c (row-wise in place), then post-smoothing from x
+    rc = mpbp_spmv(&L.P, &L.P_blocks, MPBP_SPMV_ADD, xc, cur, cur, (void*)st);
+    if (rc) return rc;
+    rc = mg_smooth(o, L.nrows, diag, L.lmin, L.lmax, L.post, false, b, &cur, alt, d, dst, sub, st);
+    if (rc) return rc;
+    *res = cur;
+    return MPBP_OK;
+}
+
+// x_out = mg^-1 b by mg->cycles V-cycles from x = 0 (sub - that when sub != NULL).
+int mg_solve(const mpbp_mg* m, const MgFine& fine, const double* b, double* x_out, const double* sub, hipStream_t st) {
+    if (!m || m->nlevels < 2 || !m->levels || m->cycles < 1 || !m->coarse_inv.row_ptr)
+        return set_error(MPBP_ERR_ARG, "mg: hierarchy needs >= 2 levels, >= 1 cycle and the coarse inverse");
+    if (x_out == fine.x || x_out == fine.t || x_out == fine.r || x_out == fine.d || b == x_out)
+        return set_error(MPBP_ERR_ARG, "mg: x_out must not alias the level-0 work buffers or b");
+    double* cur = fine.x;
+    for (int k = 0; k < m->cycles; ++k) {
+        const bool last = k == m->cycles - 1;
+        double* res = nullptr;
+        const int rc = mg_vcycle(m, 0, fine, b, k == 0, cur, last ? x_out : nullptr, last ? sub : nullptr, &res, st);
+        if (rc) return rc;
+        cur = res;
+    }
+    return MPBP_OK;
+}
+
 // x = M^-1 b by `inner` sweeps from x0 = 0 (solve.py:251/254 F_inv / Gt_G_factorization roles).
 // The final iterate goes to dst (sub - iterate when sub != NULL); ping/pong hold the others.
 int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag, const mpbp_inner_solver& in,
                 int32_t nrows, const double* b, double* dst, const double* sub, double* ping, double* pong,
                 double* dir, bool profile) {
+    if (in.kind == MPBP_INNER_MG) {   // one GPU: V-cycles whose level 0 is this operator
+        const mpbp_mg* m = kind == MPBP_VEC_VELOCITY ? c.p->mg_F : c.p->mg_P;
+        if (!m || c.p->halo || !op.bd.empty)
+            return set_error(MPBP_ERR_ARG, "schur_apply: a multigrid inner solve needs plan.mg_%s on one GPU",
+                             kind == MPBP_VEC_VELOCITY ? "F" : "P");
+        if (m->levels[0].nrows != nrows) return set_error(MPBP_ERR_ARG, "schur_apply: mg level 0 size mismatch");
+        const MgFine f{op.in, diag, ping, pong, m->levels[0].r, dir};
+        return mg_solve(m, f, b, dst, sub, c.st);
+    }
     const int K = in.sweeps;
     double c1[64] = {}, c2[64] = {};   // zeros for Jacobi (never read uninitialised)
     if (K < 1 || K > 64) return set_error(MPBP_ERR_ARG, "inner sweeps must be in [1, 64]");
@@ -3059,3 +3270,68 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
     // 7. u = Finv_v - F_inv @ G_xp                                          solve.py:274-276
     return inner_solve(c, MPBP_VEC_VELOCITY, F, p->diag_F, p->inner_F, p->nu, W, out_u, Y, U0, U1, Ud, true);
 }
+
+// ======================================================= multigrid (C ABI) ====
+extern "C" {
+
+static int mg_fields(int32_t n, int32_t nfields, const int32_t* kinds, MgFields* F) {
+    if (n < 4 || (n & 1) || nfields < 1 || nfields > 8 || !kinds)
+        return set_error(MPBP_ERR_ARG, "mg_transfer: need even n >= 4 and 1..8 fields");
+    F->nfields = nfields;
+    for (int f = 0; f < nfields; ++f) {
+        F->ky[f] = kinds[2 * f];
+        F->kx[f] = kinds[2 * f + 1];
+        if ((F->ky[f] != MPBP_MG_CELL && F->ky[f] != MPBP_MG_NODE) || (F->kx[f] != MPBP_MG_CELL && F->kx[f] != MPBP_MG_NODE))
+            return set_error(MPBP_ERR_ARG, "mg_transfer: field kinds must be MPBP_MG_CELL or MPBP_MG_NODE");
+    }
+    if ((int64_t)nfields * n * n > INT32_MAX) return set_error(MPBP_ERR_ARG, "mg_transfer: too many rows");
+    return MPBP_OK;
+}
+
+static int64_t mg_rows(int32_t n, int32_t nfields, int32_t which) {
+    const int64_t m = which == MPBP_MG_P ? n : n / 2;
+    return (int64_t)nfields * m * m;
+}
+
+int mpbp_mg_transfer_count(int32_t n, int32_t nfields, const int32_t* kinds, int32_t which, int32_t* row_nnz,
+                           void* stream) {
+    MgFields F;
+    const int rc = mg_fields(n, nfields, kinds, &F);
+    if (rc) return rc;
+    if (!row_nnz || (which != MPBP_MG_P && which != MPBP_MG_R)) return set_error(MPBP_ERR_ARG, "mg_transfer: bad args");
+    const int64_t rows = mg_rows(n, nfields, which);
+    k_mg_transfer<<<grid_for(rows), kBlock, 0, as_stream(stream)>>>(F, n, which, rows, nullptr, row_nnz, nullptr, nullptr);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int mpbp_mg_transfer_fill(int32_t n, int32_t nfields, const int32_t* kinds, int32_t which, const int32_t* row_ptr,
+                          int32_t* col_idx, double* val, void* stream) {
+    MgFields F;
+    const int rc = mg_fields(n, nfields, kinds, &F);
+    if (rc) return rc;
+    if (!row_ptr || !col_idx || !val || (which != MPBP_MG_P && which != MPBP_MG_R))
+        return set_error(MPBP_ERR_ARG, "mg_transfer: bad args");
+    const int64_t rows = mg_rows(n, nfields, which);
+    k_mg_transfer<<<grid_for(rows), kBlock, 0, as_stream(stream)>>>(F, n, which, rows, row_ptr, nullptr, col_idx, val);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int mpbp_mg_solve(const mpbp_mg* mg, const double* b, const double* sub, double* x_out, void* stream) {
+    if (!mg || !b || !x_out || mg->nlevels < 2 || !mg->levels) return set_error(MPBP_ERR_ARG, "mg_solve: bad args");
+    const mpbp_mg_level& L = mg->levels[0];
+    if (check_csr(&L.A)) return MPBP_ERR_ARG;
+    for (int l = 0; l < mg->nlevels; ++l) {
+        const mpbp_mg_level& Q = mg->levels[l];
+        if (!Q.x || !Q.t || !Q.r || !Q.d || !Q.b || !Q.diag)
+            return set_error(MPBP_ERR_ARG, "mg_solve: level %d is missing work vectors", l);
+        if (l + 1 < mg->nlevels && (Q.R.nrows != mg->levels[l + 1].nrows || Q.P.ncols != mg->levels[l + 1].nrows ||
+                                    Q.R.ncols != Q.nrows || Q.P.nrows != Q.nrows))
+            return set_error(MPBP_ERR_ARG, "mg_solve: transfer shapes of level %d do not match", l);
+    }
+    const MgFine f{mg_csr_op(L.A, L.A_blocks), L.diag, L.x, L.t, L.r, L.d};
+    return mg_solve(mg, f, b, x_out, sub, as_stream(stream));
+}
+
+}  // extern "C"

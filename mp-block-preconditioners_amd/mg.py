@@ -1,0 +1,142 @@
+"""Geometric multigrid for the inner inverses F^-1 and Gt_G^-1 of the approximate Schur preconditioner.
+
+The reference approximates both inverses with ILUT (solve.py:250-254) and names the scalable choice in
+its own comments: "In IBAMR, we'd use Multigrid PC with Jacobi smoother" (solve.py:266, 274).  This is
+that choice on the GPU:
+
+* levels: the periodic n x n MAC grid coarsened by 2 per direction down to n <= ``coarsest`` (or odd n);
+* transfers: per field, linear interpolation along each axis -- cell-centred (p; u along y; v along x)
+  or node-centred (u along x, v along y) -- as CSR P, and R = P^T (``mpbp_mg_transfer_*``, exact values);
+* coarse operators: Galerkin A_{l+1} = R (A_l P) with the library's SpGEMM (every product kept);
+* smoother: Chebyshev-Jacobi on [lmax / ratio, lmax] with lmax the Gershgorin bound of diag(A)^-1 A;
+* coarsest level: its dense pseudo-inverse (computed once on the host), applied as a dense-row SpMV.
+
+``Multigrid.solve`` runs ``cycles`` V-cycles from x = 0 through ``mpbp_mg_solve`` (graph-capturable).
+Inside ``ApproxSchurPreconditioner`` (``InnerSolver("mg", cycles)``) level 0 is the apply's own F / Gt_G
+operator -- matrix-free when the plan is -- with the same bits.  oracle/mg_oracle.py restates the cycle.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr, stream_handle
+from .csr import DeviceCSR, csr_from_row_nnz, spgemm
+
+CELL, NODE = _lib.MG_CELL, _lib.MG_NODE
+# (row axis, column axis) kinds of [u_n, v_n, u_s, v_s]: u at (-(r+1/2) dy, c dx), v at (-r dy, (c+1/2) dx)
+# (utils.fill_sol_and_RHS_vecs), p at cell centres
+FIELDS_VELOCITY = ((CELL, NODE), (NODE, CELL), (CELL, NODE), (NODE, CELL))
+FIELDS_PRESSURE = ((CELL, CELL),)
+
+
+def transfer(n: int, fields, which: int, device) -> DeviceCSR:
+    """P (which = MG_P: fine x coarse) or R = P^T (MG_R) of the n x n grid, built on the GPU."""
+    kinds = np.ascontiguousarray(np.asarray(fields, dtype=np.int32).reshape(-1))
+    nf = len(fields)
+    rows = nf * (n * n if which == _lib.MG_P else (n // 2) ** 2)
+    cols = nf * ((n // 2) ** 2 if which == _lib.MG_P else n * n)
+    row_nnz = torch.empty(rows, dtype=torch.int32, device=device)
+    check(lib().mpbp_mg_transfer_count(n, nf, kinds.ctypes.data_as(ctypes.c_void_p), which, ptr(row_nnz),
+                                       stream_handle()))
+    rp, ci, va = csr_from_row_nnz(row_nnz, (rows, cols), device)
+    check(lib().mpbp_mg_transfer_fill(n, nf, kinds.ctypes.data_as(ctypes.c_void_p), which, ptr(rp), ptr(ci),
+                                      ptr(va), stream_handle()))
+    return DeviceCSR(rp, ci, va, (rows, cols))
+
+
+def dense_inverse_csr(A: DeviceCSR) -> tuple[DeviceCSR, np.ndarray]:
+    """The pseudo-inverse of a small operator as a CSR with every entry stored (rows of ncols entries)."""
+    Ad = A.to_scipy().toarray()
+    inv = np.ascontiguousarray(np.linalg.pinv(Ad))
+    m = inv.shape[0]
+    dev = A.device
+    rp = np.arange(0, m * m + 1, m, dtype=np.int32)
+    ci = np.tile(np.arange(m, dtype=np.int32), m)
+    M = DeviceCSR(torch.from_numpy(rp).to(dev), torch.from_numpy(ci).to(dev),
+                  torch.from_numpy(inv.reshape(-1).copy()).to(dev), (m, m), row_ptr_host=rp)
+    return M, inv
+
+
+class Multigrid:
+    """V-cycle hierarchy over a stacked-field operator A (DeviceCSR) of an n x n periodic grid.
+
+    fields   per stacked field, the (row axis, column axis) kinds -- FIELDS_VELOCITY for F, FIELDS_PRESSURE
+             for Gt_G
+    pre/post Chebyshev-Jacobi smoothing sweeps per level; ratio: lmin = lmax / ratio
+    cycles   V-cycles per solve (x0 = 0); coarsest: stop coarsening at n <= coarsest
+    """
+
+    def __init__(self, A: DeviceCSR, n: int, fields=FIELDS_PRESSURE, pre: int = 2, post: int = 2, cycles: int = 1,
+                 ratio: float = 4.0, coarsest: int = 8, diag: torch.Tensor | None = None):
+        nf = len(fields)
+        if A.shape != (nf * n * n, nf * n * n):
+            raise ValueError(f"operator {A.shape} is not {nf} fields of a {n} x {n} grid")
+        if n < 4 or n % 2 or n // 2 < 2:
+            raise ValueError("multigrid needs an even grid n >= 4")
+        if pre < 1 or post < 1 or cycles < 1:
+            raise ValueError("pre, post and cycles must be >= 1")
+        self.n, self.fields, self.pre, self.post, self.cycles, self.ratio = n, tuple(fields), pre, post, cycles, ratio
+        dev = A.device
+        self.device = dev
+        self.ops, self.diags, self.R, self.P, self.bounds, self.sizes = [], [], [], [], [], []
+        m = n
+        while True:
+            d = diag if (not self.ops and diag is not None) else A.diagonal()
+            lmax = A.gershgorin(d)
+            self.ops.append(A)
+            self.diags.append(d)
+            self.bounds.append((lmax / ratio, lmax))
+            self.sizes.append(m)
+            if m % 2 or m <= coarsest or m // 2 < 2:
+                break
+            P = transfer(m, fields, _lib.MG_P, dev)
+            R = transfer(m, fields, _lib.MG_R, dev)
+            self.P.append(P)
+            self.R.append(R)
+            A = spgemm(R, spgemm(A, P))
+            m //= 2
+        if len(self.ops) < 2:
+            raise ValueError(f"grid {n} gives a single level (coarsest={coarsest})")
+        self.coarse_inv, self.coarse_inv_host = dense_inverse_csr(self.ops[-1])
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.work = [[torch.zeros(M.shape[0], **f64) for _ in range(5)] for M in self.ops]
+        self._levels = (_lib.MgLevel * len(self.ops))()
+        empty_csr, empty_blk = _lib.Csr(0, 0, 0, None, None, None), _lib.RowBlocks(None, 0)
+        for l, M in enumerate(self.ops):
+            L = self._levels[l]
+            L.nrows, L.pre, L.post = M.shape[0], pre, post
+            L.lmin, L.lmax = self.bounds[l]
+            L.A, L.A_blocks, L.diag = M.cstruct(), M.blocks.cstruct(), self.diags[l].data_ptr()
+            if l < len(self.R):
+                L.R, L.R_blocks = self.R[l].cstruct(), self.R[l].blocks.cstruct()
+                L.P, L.P_blocks = self.P[l].cstruct(), self.P[l].blocks.cstruct()
+            else:
+                L.R = L.P = empty_csr
+                L.R_blocks = L.P_blocks = empty_blk
+            L.x, L.t, L.r, L.d, L.b = (w.data_ptr() for w in self.work[l])
+        self._mg = _lib.Mg(len(self.ops), cycles, ctypes.cast(self._levels, ctypes.POINTER(_lib.MgLevel)),
+                           self.coarse_inv.cstruct(), self.coarse_inv.blocks.cstruct())
+
+    @property
+    def nlevels(self) -> int:
+        return len(self.ops)
+
+    def cstruct(self) -> _lib.Mg:
+        return self._mg
+
+    def solve(self, b: torch.Tensor, out: torch.Tensor | None = None, sub: torch.Tensor | None = None) -> torch.Tensor:
+        """x = MG^-1 b (``cycles`` V-cycles from 0); sub - x when sub is given."""
+        n0 = self.ops[0].shape[0]
+        assert b.is_cuda and b.dtype == torch.float64 and b.numel() == n0
+        if out is None:
+            out = torch.empty(n0, dtype=torch.float64, device=self.device)
+        check(lib().mpbp_mg_solve(ctypes.byref(self._mg), ptr(b), ptr(sub), ptr(out), stream_handle()))
+        return out
+
+    def __repr__(self):
+        return (f"Multigrid(levels={self.sizes}, fields={len(self.fields)}, pre={self.pre}, post={self.post}, "
+                f"cycles={self.cycles}, ratio={self.ratio})")

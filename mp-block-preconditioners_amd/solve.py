@@ -30,28 +30,43 @@ from .preconditioner import MultiphaseBlockPreconditioner, PGStencil
 class InnerSolver:
     """Approximate inverse used for F^-1 and Gt_G^-1 inside the apply.
 
-    kind   "jacobi" (solve.py:149-159) or "chebyshev" (Chebyshev-Jacobi, BASELINE configs[3])
-    sweeps updates of x from x0 = 0 (sweeps - 1 SpMVs)
+    kind   "jacobi" (solve.py:149-159), "chebyshev" (Chebyshev-Jacobi, BASELINE configs[3]) or "mg" (geometric
+           multigrid V-cycles, the reference's pointer at solve.py:266/274; mg.Multigrid)
+    sweeps updates of x from x0 = 0 (sweeps - 1 SpMVs); for "mg" the number of V-cycles
     lmax   upper bound of spec(diag(M)^-1 M); None -> Gershgorin bound computed on the GPU
     lmin   lower end of the Chebyshev interval; None -> lmax / ratio
+    pre, post, smooth_ratio, coarsest   "mg" only: smoothing sweeps per level, smoothing interval
+           [lmax / smooth_ratio, lmax], coarsening stops at n <= coarsest
     """
     kind: str = "chebyshev"
     sweeps: int = 4
     lmin: float | None = None
     lmax: float | None = None
     ratio: float = 30.0
+    pre: int = 2
+    post: int = 2
+    smooth_ratio: float = 4.0
+    coarsest: int = 8
 
     def resolve(self, M: DeviceCSR, diag: torch.Tensor) -> "InnerSolver":
         if self.kind == "jacobi":
             return InnerSolver("jacobi", int(self.sweeps), 0.0, 0.0, self.ratio)
+        if self.kind == "mg":
+            return InnerSolver("mg", int(self.sweeps), 0.0, 0.0, self.ratio, int(self.pre), int(self.post),
+                               float(self.smooth_ratio), int(self.coarsest))
         if self.kind != "chebyshev":
             raise ValueError(f"unknown inner solver {self.kind!r}")
         lmax = float(self.lmax) if self.lmax is not None else M.gershgorin(diag)
         lmin = float(self.lmin) if self.lmin is not None else lmax / self.ratio
         return InnerSolver("chebyshev", int(self.sweeps), lmin, lmax, self.ratio)
 
+    def multigrid(self, M: DeviceCSR, n: int, fields, diag: torch.Tensor):
+        from .mg import Multigrid
+        return Multigrid(M, n, fields, pre=self.pre, post=self.post, cycles=int(self.sweeps),
+                         ratio=self.smooth_ratio, coarsest=self.coarsest, diag=diag)
+
     def cstruct(self):
-        kind = _lib.INNER_CHEBYSHEV if self.kind == "chebyshev" else _lib.INNER_JACOBI
+        kind = {"chebyshev": _lib.INNER_CHEBYSHEV, "jacobi": _lib.INNER_JACOBI, "mg": _lib.INNER_MG}[self.kind]
         return _lib.InnerSolverC(kind, int(self.sweeps), float(self.lmin or 0.0), float(self.lmax or 0.0))
 
 
@@ -183,6 +198,17 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
         self.diag_P = self.GtG.diagonal()
         self.inner_F = (inner_F or InnerSolver()).resolve(self.F, self.diag_F)
         self.inner_P = (inner_P or InnerSolver()).resolve(self.GtG, self.diag_P)
+        # multigrid inner solves: hierarchies over F (4 velocity fields) and Gt_G (pressure) of the n x n grid
+        self.mg_F = self.mg_P = None
+        if "mg" in (self.inner_F.kind, self.inner_P.kind):
+            from .mg import FIELDS_PRESSURE, FIELDS_VELOCITY
+            n = math.isqrt(np_)
+            if n * n != np_ or nu != 4 * np_:
+                raise ValueError("multigrid inner solves need the n x n MAC-grid operators")
+            if self.inner_F.kind == "mg":
+                self.mg_F = self.inner_F.multigrid(self.F, n, FIELDS_VELOCITY, self.diag_F)
+            if self.inner_P.kind == "mg":
+                self.mg_P = self.inner_P.multigrid(self.GtG, n, FIELDS_PRESSURE, self.diag_P)
         f64 = dict(dtype=torch.float64, device=dev)
         self._wu = [torch.empty(nu, **f64) for _ in range(4)]
         self._wu_owned = torch.empty(nu, **f64)
@@ -249,6 +275,10 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
         p.prof_count = ctypes.POINTER(ctypes.c_int32)()
         if self.q13 is not None:
             p.q13, p.q13_n = self.q13[1].data_ptr(), self.q13[0]
+        if self.mg_F is not None:
+            p.mg_F = ctypes.pointer(self.mg_F.cstruct())
+        if self.mg_P is not None:
+            p.mg_P = ctypes.pointer(self.mg_P.cstruct())
         return p
 
     def sell_of(self, key):
