@@ -3034,7 +3034,8 @@ int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag
                 double* dir, bool profile) {
     if (in.kind == MPBP_INNER_MG) {   // one GPU: V-cycles whose level 0 is this operator
         const mpbp_mg* m = kind == MPBP_VEC_VELOCITY ? c.p->mg_F : c.p->mg_P;
-        if (!m || c.p->halo || !op.bd.empty)
+        // (one GPU: op.in covers every row -- the assembled layouts' boundary part is an empty block list)
+        if (!m || c.p->halo)
             return set_error(MPBP_ERR_ARG, "schur_apply: a multigrid inner solve needs plan.mg_%s on one GPU",
                              kind == MPBP_VEC_VELOCITY ? "F" : "P");
         if (m->levels[0].nrows != nrows) return set_error(MPBP_ERR_ARG, "schur_apply: mg level 0 size mismatch");

@@ -185,8 +185,9 @@ def rccl_library_path() -> str:
 
 
 class RcclHalo:
-    """Ghost-row exchange in libmpbp (csrc/halo.cpp): one RCCL group of neighbour sends / receives per
-    sweep, issued from C inside mpbp_schur_apply -- no pack kernels, no Python callback, no all-gather.
+    """Ghost-row exchange in libmpbp (csrc/halo.cpp): one gather kernel packs a four-field vector's
+    boundary rows (before the group opens), then one RCCL group of neighbour sends / receives writes the
+    ghost rows; issued from C inside mpbp_schur_apply -- no Python callback, no all-gather.
     The communicator is libmpbp's own (its unique id travels over `group`); world = 1 exchanges with
     itself (the periodic wrap)."""
 
