@@ -152,6 +152,11 @@ typedef struct mpbp_mg_level {
     mpbp_csr P;                      /* from level + 1 */
     mpbp_rowblocks P_blocks;
     double *x, *t, *r, *d, *b;       /* device work vectors, nrows each */
+    /* optional SELL-64 copies (nslices > 0: used instead of the CSR form, same bits): the Galerkin coarse
+     * operators' long uniform rows (20-50 entries) stream better one row per lane */
+    mpbp_sell A_sell;
+    mpbp_sell R_sell;
+    mpbp_sell P_sell;
 } mpbp_mg_level;
 
 typedef struct mpbp_mg {
@@ -160,6 +165,8 @@ typedef struct mpbp_mg {
     const mpbp_mg_level* levels;     /* host array */
     mpbp_csr coarse_inv;             /* (pseudo-)inverse of the coarsest A, every entry stored */
     mpbp_rowblocks coarse_inv_blocks;
+    const double* coarse_dense;      /* optional: the same inverse column-major (m x m, m = coarsest nrows), applied
+                                      * by a dense kernel (one row per lane, the CSR row's order); NULL: CSR */
 } mpbp_mg;
 
 typedef void (*mpbp_halo_fn)(void* ctx, int32_t vec_kind, double* x_ext, int32_t phase, void* stream);

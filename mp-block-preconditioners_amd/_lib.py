@@ -59,12 +59,13 @@ class MgLevel(Structure):
     _fields_ = [("nrows", c_int32), ("pre", c_int32), ("post", c_int32), ("reserved", c_int32),
                 ("lmin", c_double), ("lmax", c_double), ("A", Csr), ("A_blocks", RowBlocks), ("diag", c_void_p),
                 ("R", Csr), ("R_blocks", RowBlocks), ("P", Csr), ("P_blocks", RowBlocks),
-                ("x", c_void_p), ("t", c_void_p), ("r", c_void_p), ("d", c_void_p), ("b", c_void_p)]
+                ("x", c_void_p), ("t", c_void_p), ("r", c_void_p), ("d", c_void_p), ("b", c_void_p),
+                ("A_sell", Sell), ("R_sell", Sell), ("P_sell", Sell)]
 
 
 class Mg(Structure):
     _fields_ = [("nlevels", c_int32), ("cycles", c_int32), ("levels", POINTER(MgLevel)), ("coarse_inv", Csr),
-                ("coarse_inv_blocks", RowBlocks)]
+                ("coarse_inv_blocks", RowBlocks), ("coarse_dense", c_void_p)]
 
 
 HALO_FN = CFUNCTYPE(None, c_void_p, c_int32, c_void_p, c_int32, c_void_p)

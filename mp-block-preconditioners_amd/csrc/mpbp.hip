@@ -1068,14 +1068,17 @@ __global__ void __launch_bounds__(kBlock) k_sell_rows(Sell S, const double* __re
     const double2* vp = S.val + (size_t)sl.w * 64 + lane;
     const int2* cp = S.col + (size_t)sl.w * 64 + lane;
     double acc = 0.0;
-    if (np <= kSellPairs) {
+    // pair-rows [j0, j0 + kSellPairs): every load of the batch first (slice padding is zero, so loads past a
+    // row's end are harmless), then the x gathers, then the products added in CSR order.  Rows of up to 16
+    // entries take one batch; longer ones (multigrid coarse operators: 20-50 entries) loop over batches.
+    auto batch = [&](int j0) {
         double2 v[kSellPairs];
         int2 c[kSellPairs];
 #pragma unroll
         for (int j = 0; j < kSellPairs; ++j) {
-            if (j < np) {
-                v[j] = ld_matrix<MPBP_SELL_NT != 0>(vp + (size_t)j * 64);
-                c[j] = ld_matrix<MPBP_SELL_NT != 0>(cp + (size_t)j * 64);
+            if (j0 + j < np) {   // wave-uniform
+                v[j] = ld_matrix<MPBP_SELL_NT != 0>(vp + (size_t)(j0 + j) * 64);
+                c[j] = ld_matrix<MPBP_SELL_NT != 0>(cp + (size_t)(j0 + j) * 64);
             } else {
                 v[j] = make_double2(0.0, 0.0);
                 c[j] = make_int2(0, 0);
@@ -1084,21 +1087,19 @@ __global__ void __launch_bounds__(kBlock) k_sell_rows(Sell S, const double* __re
         double x0[kSellPairs], x1[kSellPairs];
 #pragma unroll
         for (int j = 0; j < kSellPairs; ++j) {
-            x0[j] = (2 * j < len) ? x[c[j].x] : 0.0;
-            x1[j] = (2 * j + 1 < len) ? x[c[j].y] : 0.0;
+            x0[j] = (2 * (j0 + j) < len) ? x[c[j].x] : 0.0;
+            x1[j] = (2 * (j0 + j) + 1 < len) ? x[c[j].y] : 0.0;
         }
 #pragma unroll
         for (int j = 0; j < kSellPairs; ++j) {
-            if (2 * j < len) acc += v[j].x * x0[j];
-            if (2 * j + 1 < len) acc += v[j].y * x1[j];
+            if (2 * (j0 + j) < len) acc += v[j].x * x0[j];
+            if (2 * (j0 + j) + 1 < len) acc += v[j].y * x1[j];
         }
+    };
+    if (np <= kSellPairs) {
+        batch(0);
     } else {
-        for (int j = 0; 2 * j < len; ++j) {
-            const double2 vv = vp[(size_t)j * 64];
-            const int2 cc = cp[(size_t)j * 64];
-            acc += vv.x * x[cc.x];
-            if (2 * j + 1 < len) acc += vv.y * x[cc.y];
-        }
+        for (int j0 = 0; j0 < np; j0 += kSellPairs) batch(j0);
     }
     if (live) epi.template apply<MPBP_SELL_NT != 0>(r, acc, pe);
 }
@@ -2935,6 +2936,38 @@ struct MgFine {
 OpRef mg_csr_op(const mpbp_csr& A, const mpbp_rowblocks& blk) {
     return OpRef{&A, &blk, nullptr, nullptr, false, 0, SOP_NONE};
 }
+// A level's operator: its SELL-64 copy when it has one (same bits), else the CSR form.
+OpRef mg_level_op(const mpbp_mg_level& L) {
+    return L.A_sell.nslices > 0 ? OpRef{&L.A, nullptr, &L.A_sell, nullptr, false, 0, SOP_NONE}
+                                : mg_csr_op(L.A, L.A_blocks);
+}
+int mg_transfer(const mpbp_csr& M, const mpbp_rowblocks& blk, const mpbp_sell& S, int32_t mode, const double* x,
+                const double* z, double* y, hipStream_t st) {
+    return S.nslices > 0 ? mpbp_sell_spmv(&S, mode, x, z, y, (void*)st) : mpbp_spmv(&M, &blk, mode, x, z, y, (void*)st);
+}
+
+// y = M b for the coarsest level's dense (pseudo-)inverse, column-major: one row per lane, summed over the columns
+// in order from 0.0 (the CSR row's order, every entry stored).  Loads are issued 16 columns ahead of the sums.
+__global__ void __launch_bounds__(64) k_dense_cm(int32_t m, const double* __restrict__ Mt,
+                                                 const double* __restrict__ b, double* __restrict__ y) {
+    const int32_t i = blockIdx.x * 64 + threadIdx.x;
+    const int32_t ii = i < m ? i : 0;
+    double acc = 0.0;
+    constexpr int U = 16;
+    int32_t j = 0;
+    for (; j + U <= m; j += U) {
+        double a[U], bb[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            a[u] = Mt[(size_t)(j + u) * m + ii];
+            bb[u] = b[j + u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += a[u] * bb[u];
+    }
+    for (; j < m; ++j) acc += Mt[(size_t)j * m + ii] * b[j];
+    if (i < m) y[i] = acc;
+}
 
 // K Chebyshev-Jacobi sweeps on [lmin, lmax].  zero: from x = 0 (the first sweep is the init pass: d = x =
 // c2[0] b / diag), else from the iterate in *cur (d starts at 0).  The last sweep writes `dst` (or the free
@@ -2977,7 +3010,7 @@ int mg_vcycle(const mpbp_mg* m, int l, const MgFine& fine, const double* b, bool
               const double* sub, double** res, hipStream_t st) {
     const mpbp_mg_level& L = m->levels[l];
     const bool top = l == 0;
-    const OpRef o = top ? fine.op : mg_csr_op(L.A, L.A_blocks);
+    const OpRef o = top ? fine.op : mg_level_op(L);
     const double* diag = top ? fine.diag : L.diag;
     double* bx = top ? fine.x : L.x;
     double* bt = top ? fine.t : L.t;
@@ -2992,17 +3025,22 @@ int mg_vcycle(const mpbp_mg* m, int l, const MgFine& fine, const double* b, bool
     rc = op_spmv(o, MPBP_SPMV_RESID, cur, b, r, st);
     if (rc) return rc;
     const mpbp_mg_level& C = m->levels[l + 1];
-    rc = mpbp_spmv(&L.R, &L.R_blocks, MPBP_SPMV_STORE, r, nullptr, C.b, (void*)st);
+    rc = mg_transfer(L.R, L.R_blocks, L.R_sell, MPBP_SPMV_STORE, r, nullptr, C.b, st);
     if (rc) return rc;
     double* xc = C.x;
     if (l + 1 == m->nlevels - 1) {
-        rc = mpbp_spmv(&m->coarse_inv, &m->coarse_inv_blocks, MPBP_SPMV_STORE, C.b, nullptr, xc, (void*)st);
+        if (m->coarse_dense) {
+            k_dense_cm<<<grid_for(C.nrows, 64), 64, 0, st>>>(C.nrows, m->coarse_dense, C.b, xc);
+            MPBP_HIP(hipGetLastError());
+        } else {
+            rc = mpbp_spmv(&m->coarse_inv, &m->coarse_inv_blocks, MPBP_SPMV_STORE, C.b, nullptr, xc, (void*)st);
+        }
     } else {
         rc = mg_vcycle(m, l + 1, fine, C.b, true, C.x, nullptr, nullptr, &xc, st);
     }
     if (rc) return rc;
     // x += P x_c (row-wise in place), then post-smoothing from x
-    rc = mpbp_spmv(&L.P, &L.P_blocks, MPBP_SPMV_ADD, xc, cur, cur, (void*)st);
+    rc = mg_transfer(L.P, L.P_blocks, L.P_sell, MPBP_SPMV_ADD, xc, cur, cur, st);
     if (rc) return rc;
     rc = mg_smooth(o, L.nrows, diag, L.lmin, L.lmax, L.post, false, b, &cur, alt, d, dst, sub, st);
     if (rc) return rc;
@@ -3331,7 +3369,7 @@ int mpbp_mg_solve(const mpbp_mg* mg, const double* b, const double* sub, double*
                                     Q.R.ncols != Q.nrows || Q.P.nrows != Q.nrows))
             return set_error(MPBP_ERR_ARG, "mg_solve: transfer shapes of level %d do not match", l);
     }
-    const MgFine f{mg_csr_op(L.A, L.A_blocks), L.diag, L.x, L.t, L.r, L.d};
+    const MgFine f{mg_level_op(L), L.diag, L.x, L.t, L.r, L.d};
     return mg_solve(mg, f, b, x_out, sub, as_stream(stream));
 }
 

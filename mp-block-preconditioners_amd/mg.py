@@ -9,7 +9,11 @@ that choice on the GPU:
   or node-centred (u along x, v along y) -- as CSR P, and R = P^T (``mpbp_mg_transfer_*``, exact values);
 * coarse operators: Galerkin A_{l+1} = R (A_l P) with the library's SpGEMM (every product kept);
 * smoother: Chebyshev-Jacobi on [lmax / ratio, lmax] with lmax the Gershgorin bound of diag(A)^-1 A;
-* coarsest level: its dense pseudo-inverse (computed once on the host), applied as a dense-row SpMV.
+* coarsest level: its dense pseudo-inverse (computed once on the host), applied by a dense kernel (one row per
+  lane, the CSR row's order) from a column-major copy;
+* layouts: every level's operator and transfers also get a SELL-64 copy when their rows fit (< 256 entries):
+  the Galerkin coarse operators' long uniform rows (20-50 entries) stream at HBM speed one row per lane, where
+  the CSR kernel's per-wave chunks serve rows of <= 12 entries (same bits either way).
 
 ``Multigrid.solve`` runs ``cycles`` V-cycles from x = 0 through ``mpbp_mg_solve`` (graph-capturable).
 Inside ``ApproxSchurPreconditioner`` (``InnerSolver("mg", cycles)``) level 0 is the apply's own F / Gt_G
@@ -24,7 +28,7 @@ import torch
 
 from . import _lib
 from ._lib import check, lib, ptr, stream_handle
-from .csr import DeviceCSR, csr_from_row_nnz, spgemm
+from .csr import DeviceCSR, DeviceSELL, csr_from_row_nnz, spgemm
 
 CELL, NODE = _lib.MG_CELL, _lib.MG_NODE
 # (row axis, column axis) kinds of [u_n, v_n, u_s, v_s]: u at (-(r+1/2) dy, c dx), v at (-r dy, (c+1/2) dx)
@@ -48,6 +52,14 @@ def transfer(n: int, fields, which: int, device) -> DeviceCSR:
     return DeviceCSR(rp, ci, va, (rows, cols))
 
 
+def sell_copy(A: DeviceCSR) -> DeviceSELL | None:
+    """SELL-64 copy of A when every row has < 256 entries (the layout's row-length byte), else None."""
+    rp = A.row_ptr_host
+    if A.shape[0] == 0 or int(np.max(np.diff(rp))) > 255:
+        return None
+    return A.to_sell()
+
+
 def dense_inverse_csr(A: DeviceCSR) -> tuple[DeviceCSR, np.ndarray]:
     """The pseudo-inverse of a small operator as a CSR with every entry stored (rows of ncols entries)."""
     Ad = A.to_scipy().toarray()
@@ -68,10 +80,13 @@ class Multigrid:
              for Gt_G
     pre/post Chebyshev-Jacobi smoothing sweeps per level; ratio: lmin = lmax / ratio
     cycles   V-cycles per solve (x0 = 0); coarsest: stop coarsening at n <= coarsest
+    sell     SELL-64 copies of the operators / transfers and the dense coarse kernel (False: CSR throughout)
+    fine_sell  also a SELL copy of level 0's operator (the standalone solve's fine level)
     """
 
     def __init__(self, A: DeviceCSR, n: int, fields=FIELDS_PRESSURE, pre: int = 2, post: int = 2, cycles: int = 1,
-                 ratio: float = 4.0, coarsest: int = 8, diag: torch.Tensor | None = None):
+                 ratio: float = 4.0, coarsest: int = 8, diag: torch.Tensor | None = None, sell: bool = True,
+                 fine_sell: bool = True):
         nf = len(fields)
         if A.shape != (nf * n * n, nf * n * n):
             raise ValueError(f"operator {A.shape} is not {nf} fields of a {n} x {n} grid")
@@ -102,6 +117,13 @@ class Multigrid:
         if len(self.ops) < 2:
             raise ValueError(f"grid {n} gives a single level (coarsest={coarsest})")
         self.coarse_inv, self.coarse_inv_host = dense_inverse_csr(self.ops[-1])
+        # the dense kernel's column-major copy (None: the CSR form)
+        self.coarse_dense = (torch.from_numpy(np.ascontiguousarray(self.coarse_inv_host.T)).to(dev)
+                             if sell else None)
+        # SELL-64 copies of the operators (level 0 too: the standalone solve's fine level) and transfers
+        # (fine_sell=False: level 0's operator is the caller's own -- the Schur apply's matrix-free F / Gt_G)
+        self.sells = [[sell_copy(M) if sell and (l > 0 or fine_sell or grp is not self.ops) else None
+                       for l, M in enumerate(grp)] for grp in (self.ops, self.R, self.P)]
         f64 = dict(dtype=torch.float64, device=dev)
         self.work = [[torch.zeros(M.shape[0], **f64) for _ in range(5)] for M in self.ops]
         self._levels = (_lib.MgLevel * len(self.ops))()
@@ -118,8 +140,12 @@ class Multigrid:
                 L.R = L.P = empty_csr
                 L.R_blocks = L.P_blocks = empty_blk
             L.x, L.t, L.r, L.d, L.b = (w.data_ptr() for w in self.work[l])
+            for name, grp in zip(("A_sell", "R_sell", "P_sell"), self.sells):
+                S = grp[l] if l < len(grp) else None
+                setattr(L, name, S.cstruct() if S is not None else _lib.Sell(0, 0, 0, 0, None, None, None, None))
         self._mg = _lib.Mg(len(self.ops), cycles, ctypes.cast(self._levels, ctypes.POINTER(_lib.MgLevel)),
-                           self.coarse_inv.cstruct(), self.coarse_inv.blocks.cstruct())
+                           self.coarse_inv.cstruct(), self.coarse_inv.blocks.cstruct(),
+                           self.coarse_dense.data_ptr() if self.coarse_dense is not None else None)
 
     @property
     def nlevels(self) -> int:

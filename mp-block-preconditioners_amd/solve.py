@@ -63,7 +63,7 @@ class InnerSolver:
     def multigrid(self, M: DeviceCSR, n: int, fields, diag: torch.Tensor):
         from .mg import Multigrid
         return Multigrid(M, n, fields, pre=self.pre, post=self.post, cycles=int(self.sweeps),
-                         ratio=self.smooth_ratio, coarsest=self.coarsest, diag=diag)
+                         ratio=self.smooth_ratio, coarsest=self.coarsest, diag=diag, fine_sell=False)
 
     def cstruct(self):
         kind = {"chebyshev": _lib.INNER_CHEBYSHEV, "jacobi": _lib.INNER_JACOBI, "mg": _lib.INNER_MG}[self.kind]

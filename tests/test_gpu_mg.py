@@ -94,15 +94,19 @@ def test_hierarchy_bit_exact(n):
             _same_csr(mg.R[l], Rs[l])
 
 
+@pytest.mark.parametrize("sell", [True, False], ids=["sell", "csr"])
 @pytest.mark.parametrize("n,cycles,pre,post", [(16, 1, 2, 2), (32, 2, 2, 2), (64, 1, 1, 3), (64, 3, 2, 1)])
-def test_mg_solve_bit_exact(n, cycles, pre, post):
+def test_mg_solve_bit_exact(n, cycles, pre, post, sell):
+    """V-cycles vs the oracle: with the SELL-64 copies of every level and the dense coarse kernel (default), and
+    with the CSR forms throughout."""
     mp = _mp()
     from oracle import mg_oracle as mo
     _, (A, F, D, G), S = _system(n)
     GtG, _ = mp.MultiphaseBlockPreconditioner.commutator_products(F, D, G)
     rng = np.random.default_rng(n + cycles)
     for M, Mh, fields in ((F, S.F, mp.FIELDS_VELOCITY), (GtG, S.GtG, mp.FIELDS_PRESSURE)):
-        mg = mp.Multigrid(M, n, fields, pre=pre, post=post, cycles=cycles)
+        mg = mp.Multigrid(M, n, fields, pre=pre, post=post, cycles=cycles, sell=sell)
+        assert (mg.coarse_dense is not None) == sell and (mg.sells[0][1] is not None) == sell
         ora = mo.MgOracle(Mh, n, fields, pre=pre, post=post, cycles=cycles, bounds=mg.bounds,
                           coarse_inv=mg.coarse_inv_host)
         b = rng.standard_normal(M.shape[0])

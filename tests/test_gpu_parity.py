@@ -140,13 +140,16 @@ def test_spmv_bit_exact(n):
         assert np.array_equal(h1, co.spmv(M, x)) and np.array_equal(h2, co.spmv(M, 2.0 * x))
 
 
-def test_sell_ragged_rows_and_partial_slices():
-    """SELL-64 with ragged rows (0..40 entries, beyond the unrolled 16), partial slices, row ranges."""
+@pytest.mark.parametrize("maxlen", [40, 255])
+def test_sell_ragged_rows_and_partial_slices(maxlen):
+    """SELL-64 with ragged rows (0..maxlen entries: past the first 16-entry batch, up to the layout's 255),
+    partial slices, row ranges, a slice of uniform long rows (multigrid coarse operators), every epilogue."""
     mp = _mp()
     from oracle import csr_oracle as co
-    rng = np.random.default_rng(11)
-    lengths = rng.integers(0, 41, size=1000)
+    rng = np.random.default_rng(11 + maxlen)
+    lengths = rng.integers(0, maxlen + 1, size=1000)
     lengths[:64] = 0
+    lengths[128:192] = maxlen
     rows = np.repeat(np.arange(lengths.size), lengths)
     M = sp.csr_matrix((rng.standard_normal(rows.size), (rows, rng.integers(0, 3000, size=rows.size))),
                       shape=(lengths.size, 3000))
@@ -160,6 +163,9 @@ def test_sell_ragged_rows_and_partial_slices():
     got = y.cpu().numpy()
     sel = np.r_[3:100, 500:1000]
     assert _bits_equal(got[sel], ref[sel]) and np.all(got[np.r_[0:3, 100:500]] == 7.0)
+    z = rng.standard_normal(M.shape[0])
+    for mode in (1, 2):
+        assert _bits_equal(dM.to_sell().matvec(_cuda(x), mode=mode, z=_cuda(z)), co.spmv(M, x, z, mode=mode)), mode
 
 
 def test_spmv_long_rows_and_empty_rows():
