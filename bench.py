@@ -423,17 +423,25 @@ def spmv_bench(A, gen, reps=20, replays=5):
 
 
 SOLVE_CASES = (   # (n, eta_n, eta_s, preconditioners): BASELINE configs[1] / configs[3] at 256^2, configs[2] / [3] at 1024^2
-    (256, 100.0, 1.0, ("none", "chebyshev:4", "chebyshev:8", "mg:1")),
-    (256, 1e4, 1.0, ("none", "chebyshev:4", "chebyshev:8", "mg:1")),
-    (1024, 100.0, 1.0, ("chebyshev:4", "mg:1")),
-    (1024, 1e4, 1.0, ("chebyshev:4", "mg:1")),
+    (256, 100.0, 1.0, ("none", "chebyshev:4", "mg:1")),
+    (256, 1e4, 1.0, ("none", "chebyshev:4", "mg:1", "mg:2/mg:1")),
+    (1024, 100.0, 1.0, ("chebyshev:4", "mg:1", "mg:2/mg:1")),
+    (1024, 1e4, 1.0, ("chebyshev:4", "mg:1", "mg:2/mg:1")),
 )
 
 
-def solve_level(args, cases=SOLVE_CASES, tol=1e-8, maxiter=150):
+def inner_pair(mp, name):
+    """'kind:k' (both inner inverses) or 'kindF:kF/kindP:kP' -> (InnerSolver for F, InnerSolver for Gt_G)."""
+    f, _, p = name.partition("/")
+    mk = lambda s: mp.InnerSolver(s.partition(":")[0], int(s.partition(":")[2] or 4))  # noqa: E731
+    return mk(f), mk(p or f)
+
+
+def solve_level(args, cases=SOLVE_CASES, tol=1e-8, maxiter=150, reps=10):
     """What the applies/s headline buys: FGMRES (tol 1e-8, maxiter 150, x0 = 0, solve.py:285) on the reference's
     manufactured problem (solve.py:52-80) with the approximate Schur preconditioner and different inner solves:
-    iterations, time to tolerance (the fgmres call; preconditioner set-up reported apart) and the velocity error."""
+    iterations, time to tolerance (the fgmres call; preconditioner set-up reported apart), the velocity error, and
+    the preconditioner's own apply time (a hipGraph replayed `reps` times)."""
     import numpy as np
     import torch
     import mp_block_preconditioners_amd as mp
@@ -447,12 +455,24 @@ def solve_level(args, cases=SOLVE_CASES, tol=1e-8, maxiter=150):
         for name in precs:
             t0 = time.perf_counter()
             M = None
+            apply_ms = None
             if name != "none":
-                kind, _, k = name.partition(":")
-                inner = mp.InnerSolver(kind, int(k))
-                M = mp.ApproxSchurPreconditioner(F, D, G, inner_F=inner, inner_P=inner)
+                iF, iP = inner_pair(mp, name)
+                M = mp.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP)
             torch.cuda.synchronize()
             setup = time.perf_counter() - t0
+            if M is not None:
+                v = torch.randn(M.shape[0], dtype=torch.float64, device="cuda")
+                o = torch.empty_like(v)
+                g = M.capture(v, o)
+                g.replay()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    g.replay()
+                torch.cuda.synchronize()
+                apply_ms = (time.perf_counter() - t0) / reps * 1e3
+                del g, v, o
             hist = []
             t0 = time.perf_counter()
             x, info = mp.fgmres(A, bd, M=M, tol=tol, maxiter=maxiter, residuals=hist)
@@ -461,14 +481,15 @@ def solve_level(args, cases=SOLVE_CASES, tol=1e-8, maxiter=150):
             res = float(torch.linalg.vector_norm(bd - A.matvec(x))) / nb
             err = float(np.max(np.abs(x.cpu().numpy()[: 4 * n * n] - u[: 4 * n * n])))
             out.append({"n": n, "eta_n": eta_n, "eta_s": eta_s, "preconditioner": name, "iterations": len(hist) - 1,
-                        "converged": info == 0, "seconds": el, "setup_seconds": setup, "true_rel_residual": res,
-                        "velocity_max_error": err})
+                        "converged": info == 0, "seconds": el, "setup_seconds": setup, "apply_ms": apply_ms,
+                        "true_rel_residual": res, "velocity_max_error": err})
             del M, x
             torch.cuda.empty_cache()
         del A, F, D, G, bp
         torch.cuda.empty_cache()
     return {"tol": tol, "maxiter": maxiter, "problem": "manufactured solution of solve.py:52-80, x0 = 0",
-            "inner": "chebyshev:K = K Chebyshev-Jacobi sweeps; mg:K = K multigrid V-cycles (V(2,2), Chebyshev smoothing)",
+            "inner": "chebyshev:K = K Chebyshev-Jacobi sweeps; mg:K = K multigrid V-cycles (V(2,2), Chebyshev "
+                     "smoothing, Galerkin levels down to 8^2); 'F/P' names the two inner inverses separately",
             "runs": out}
 
 
