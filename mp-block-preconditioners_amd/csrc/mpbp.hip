@@ -2946,27 +2946,37 @@ int mg_transfer(const mpbp_csr& M, const mpbp_rowblocks& blk, const mpbp_sell& S
     return S.nslices > 0 ? mpbp_sell_spmv(&S, mode, x, z, y, (void*)st) : mpbp_spmv(&M, &blk, mode, x, z, y, (void*)st);
 }
 
-// y = M b for the coarsest level's dense (pseudo-)inverse, column-major: one row per lane, summed over the columns
-// in order from 0.0 (the CSR row's order, every entry stored).  Loads are issued 16 columns ahead of the sums.
-__global__ void __launch_bounds__(64) k_dense_cm(int32_t m, const double* __restrict__ Mt,
-                                                 const double* __restrict__ b, double* __restrict__ y) {
-    const int32_t i = blockIdx.x * 64 + threadIdx.x;
-    const int32_t ii = i < m ? i : 0;
+// y = M b for the coarsest level's dense (pseudo-)inverse, column-major (Mt[j * m + i] = M[i][j]).  A workgroup
+// owns kDR rows: its 1024 threads request a kDK-column slab of them at once (16 loads each, all in flight) into
+// LDS with the slab of b, then one lane per row adds the products over the columns in order from 0.0 -- the CSR
+// row's order with every entry stored (bit-identical to the CSR form of the same inverse).
+constexpr int kDR = 16, kDK = 1024, kDT = 1024;
+__global__ void __launch_bounds__(kDT) k_dense_cm(int32_t m, const double* __restrict__ Mt,
+                                                  const double* __restrict__ b, double* __restrict__ y) {
+    __shared__ double tile[kDK * kDR];   // [column][row]
+    __shared__ double bs[kDK];
+    const int32_t r0 = blockIdx.x * kDR;
+    const int t = threadIdx.x;
     double acc = 0.0;
-    constexpr int U = 16;
-    int32_t j = 0;
-    for (; j + U <= m; j += U) {
-        double a[U], bb[U];
+    for (int32_t j0 = 0; j0 < m; j0 += kDK) {
+        const int kc = min(kDK, m - j0);
+        constexpr int U = kDK * kDR / kDT;
+        double v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            a[u] = Mt[(size_t)(j + u) * m + ii];
-            bb[u] = b[j + u];
+            const int e = t + kDT * u, c = e / kDR, row = r0 + e % kDR;
+            v[u] = (c < kc && row < m) ? Mt[(size_t)(j0 + c) * m + row] : 0.0;
         }
+        const double bv = t < kc ? b[j0 + t] : 0.0;
 #pragma unroll
-        for (int u = 0; u < U; ++u) acc += a[u] * bb[u];
+        for (int u = 0; u < U; ++u) tile[t + kDT * u] = v[u];
+        bs[t] = bv;
+        __syncthreads();
+        if (t < kDR)
+            for (int c = 0; c < kc; ++c) acc += tile[c * kDR + t] * bs[c];
+        __syncthreads();
     }
-    for (; j < m; ++j) acc += Mt[(size_t)j * m + ii] * b[j];
-    if (i < m) y[i] = acc;
+    if (t < kDR && r0 + t < m) y[r0 + t] = acc;
 }
 
 // K Chebyshev-Jacobi sweeps on [lmin, lmax].  zero: from x = 0 (the first sweep is the init pass: d = x =
@@ -3030,7 +3040,7 @@ int mg_vcycle(const mpbp_mg* m, int l, const MgFine& fine, const double* b, bool
     double* xc = C.x;
     if (l + 1 == m->nlevels - 1) {
         if (m->coarse_dense) {
-            k_dense_cm<<<grid_for(C.nrows, 64), 64, 0, st>>>(C.nrows, m->coarse_dense, C.b, xc);
+            k_dense_cm<<<grid_for(C.nrows, kDR), kDT, 0, st>>>(C.nrows, m->coarse_dense, C.b, xc);
             MPBP_HIP(hipGetLastError());
         } else {
             rc = mpbp_spmv(&m->coarse_inv, &m->coarse_inv_blocks, MPBP_SPMV_STORE, C.b, nullptr, xc, (void*)st);

@@ -4,7 +4,8 @@ The reference approximates both inverses with ILUT (solve.py:250-254) and names 
 its own comments: "In IBAMR, we'd use Multigrid PC with Jacobi smoother" (solve.py:266, 274).  This is
 that choice on the GPU:
 
-* levels: the periodic n x n MAC grid coarsened by 2 per direction down to n <= ``coarsest`` (or odd n);
+* levels: the periodic n x n MAC grid coarsened by 2 per direction down to n <= ``coarsest`` (at least once;
+  odd n stops);
 * transfers: per field, linear interpolation along each axis -- cell-centred (p; u along y; v along x)
   or node-centred (u along x, v along y) -- as CSR P, and R = P^T (``mpbp_mg_transfer_*``, exact values);
 * coarse operators: Galerkin A_{l+1} = R (A_l P) with the library's SpGEMM (every product kept);
@@ -95,6 +96,7 @@ class Multigrid:
         if pre < 1 or post < 1 or cycles < 1:
             raise ValueError("pre, post and cycles must be >= 1")
         self.n, self.fields, self.pre, self.post, self.cycles, self.ratio = n, tuple(fields), pre, post, cycles, ratio
+        self.coarsest = coarsest
         dev = A.device
         self.device = dev
         self.ops, self.diags, self.R, self.P, self.bounds, self.sizes = [], [], [], [], [], []
@@ -106,7 +108,7 @@ class Multigrid:
             self.diags.append(d)
             self.bounds.append((lmax / ratio, lmax))
             self.sizes.append(m)
-            if m % 2 or m <= coarsest or m // 2 < 2:
+            if m % 2 or (m <= coarsest and len(self.ops) > 1) or m // 2 < 2:   # (at least one coarsening)
                 break
             P = transfer(m, fields, _lib.MG_P, dev)
             R = transfer(m, fields, _lib.MG_R, dev)

@@ -46,7 +46,7 @@ class InnerSolver:
     pre: int = 2
     post: int = 2
     smooth_ratio: float = 4.0
-    coarsest: int = 8
+    coarsest: int = 16     # dense coarsest inverse at 16^2: 1024 x 1024 for F (one fewer latency-bound level than 8^2)
 
     def resolve(self, M: DeviceCSR, diag: torch.Tensor) -> "InnerSolver":
         if self.kind == "jacobi":

@@ -56,10 +56,11 @@ def transfer(n: int, fields, which: str) -> sp.csr_matrix:
 
 
 def hierarchy(A: sp.csr_matrix, n: int, fields, coarsest: int = 8):
-    """[(A_l, n_l)], [P_l], [R_l] of the Galerkin hierarchy (same stopping rule as mg.Multigrid)."""
+    """[(A_l, n_l)], [P_l], [R_l] of the Galerkin hierarchy (same stopping rule as mg.Multigrid: coarsen by 2
+    until n <= coarsest, but at least once)."""
     ops, Ps, Rs = [(sp.csr_matrix(A), n)], [], []
     m = n
-    while not (m % 2 or m <= coarsest or m // 2 < 2):
+    while not (m % 2 or (m <= coarsest and len(ops) > 1) or m // 2 < 2):
         P, R = transfer(m, fields, "P"), transfer(m, fields, "R")
         A = co.spgemm(R, co.spgemm(A, P))
         Ps.append(P)

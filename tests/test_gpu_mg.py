@@ -73,16 +73,20 @@ def test_transfer_rejects_bad_grids():
             transfer(n, ((0, 0),), _lib.MG_P, torch.device("cuda"))
 
 
+@pytest.mark.parametrize("coarsest", [8, 16])
 @pytest.mark.parametrize("n", [16, 32])
-def test_hierarchy_bit_exact(n):
+def test_hierarchy_bit_exact(n, coarsest):
+    """Galerkin levels, transfers and smoothing bounds vs the oracle (coarsening stops at n <= coarsest, but
+    happens at least once: n = 16 with coarsest 16 still has the 8^2 level)."""
     mp = _mp()
     from oracle import mg_oracle as mo
     from oracle.schur_oracle import gershgorin
     _, (A, F, D, G), S = _system(n)
     GtG, _ = mp.MultiphaseBlockPreconditioner.commutator_products(F, D, G)
     for M, Mh, fields in ((F, S.F, mp.FIELDS_VELOCITY), (GtG, S.GtG, mp.FIELDS_PRESSURE)):
-        mg = mp.Multigrid(M, n, fields)
-        ops, Ps, Rs = mo.hierarchy(Mh, n, fields)
+        mg = mp.Multigrid(M, n, fields, coarsest=coarsest)
+        ops, Ps, Rs = mo.hierarchy(Mh, n, fields, coarsest)
+        assert len(ops) >= 2
         assert mg.sizes == [m for _, m in ops]
         for l, (Ml, _) in enumerate(ops):
             _same_csr(mg.ops[l], Ml)
@@ -142,9 +146,9 @@ def _oracle_mg_apply(S, pc, v):
     from oracle import mg_oracle as mo
     mF, mP = pc.mg_F, pc.mg_P
     oF = mo.MgOracle(S.F, mF.n, mF.fields, mF.pre, mF.post, mF.cycles, bounds=mF.bounds,
-                     coarse_inv=mF.coarse_inv_host)
+                     coarse_inv=mF.coarse_inv_host, coarsest=mF.coarsest)
     oP = mo.MgOracle(S.GtG, mP.n, mP.fields, mP.pre, mP.post, mP.cycles, bounds=mP.bounds,
-                     coarse_inv=mP.coarse_inv_host)
+                     coarse_inv=mP.coarse_inv_host, coarsest=mP.coarsest)
     nu = S.F.shape[0]
     Finv_v = oF.solve(v[:nu])
     rhs = co.spmv(S.D, Finv_v, v[nu:], mode=1)
