@@ -35,13 +35,15 @@ def parse_inner(s):
 
 
 def sweep_bytes(pc, layout, kind, sweeps, fused_init):
-    """Algorithmic HBM bytes of the F inner-solve sweeps bench.py times, averaged per launch.
+    """Algorithmic HBM bytes of the F inner-solve sweeps bench.py times: one (bytes, solve) per recorded launch of
+    one apply, in record order, and the kernel's name.
 
-    mpbp_schur_apply records events around sweeps s = 1 .. K-1 of both F solves (s = 2 .. K-1 when the
-    init pass is fused into sweep 1).  A sweep moves per F row: x_in, b, x_out (8 B each), the direction
-    d read (Chebyshev) and written (Chebyshev, not on the last sweep), the solve's `sub` on the second
-    solve's last sweep, and diag (assembled layouts); plus the matrix (assembled: 12 B per entry + index
-    data) or the thn tables (matrix-free: cell, u-face, v-face = 3 x 8 B per cell = 6 B per row)."""
+    mpbp_schur_apply records events around sweeps s = 1 .. K-1 of both F solves (s = 2 .. K-1 when the init pass is
+    fused into sweep 1).  A sweep moves per F row: x_in, b, x_out (8 B each), the direction d read (Chebyshev) and
+    written (Chebyshev, not on the last sweep), the solve's `sub` on the second solve's last sweep, and diag
+    (assembled layouts); plus the matrix (assembled: 12 B per entry + index data) or the thn tables (matrix-free:
+    cell, u-face, v-face = 3 x 8 B per cell = 6 B per row).  With G x_p recomputed in the second solve (fuse_g), its
+    sweeps read x_p (8 B per cell = 2 B per row) instead of b."""
     F = pc.F
     nF, nnzF = F.shape[0], F.nnz
     cheb = kind == "chebyshev"
@@ -56,16 +58,28 @@ def sweep_bytes(pc, layout, kind, sweeps, fused_init):
         kname = "k_sell_rows<EpiCheb> (F sweep, SELL-64)"
     else:
         fixed, kname = nnzF * 12 + (nF + 1) * 4 + F.blocks.count * 8, "k_csr_wave<EpiCheb> (F sweep, CSR)"
-    total, launches = 0, 0
+    fuse_g = bool(getattr(pc, "fuse_g", False))
+    out = []
     for solve in (1, 2):
         for s in range(2 if fused_init else 1, sweeps):
             last = s == sweeps - 1
-            streams = 3 + (0 if stencil else 1)                     # x_in, b, x_out (+ diag)
+            gx = fuse_g and solve == 2                              # b = G x_p recomputed: x_p, 8 B per cell
+            streams = 3 + (0 if stencil else 1) - (1 if gx else 0)  # x_in, b, x_out (+ diag)
             streams += (1 + (0 if last else 1)) if cheb else 0      # d read (+ write)
             streams += 1 if (last and solve == 2) else 0            # sub
-            total += fixed + nF * 8 * streams
-            launches += 1
-    return (total / launches if launches else float("nan")), kname
+            out.append((fixed + nF * 8 * streams + (nF // 4 * 8 if gx else 0), solve))
+    return out, kname
+
+
+def roofline_of(per_apply, sweep_ms, solve):
+    """Mean algorithmic bytes, mean HIP-event duration (s) and launch count of the recorded sweeps of one solve."""
+    if not per_apply or not sweep_ms:
+        return float("nan"), float("nan"), 0
+    sel = [(per_apply[i % len(per_apply)][0], ms) for i, ms in enumerate(sweep_ms)
+           if per_apply[i % len(per_apply)][1] == solve]
+    if not sel:
+        return float("nan"), float("nan"), 0
+    return (sum(b for b, _ in sel) / len(sel), sum(ms for _, ms in sel) / len(sel) / 1e3, len(sel))
 
 
 def main():
@@ -93,6 +107,8 @@ def main():
                     help="Gt_F_G: values in the 13-point diamond layout (columns implicit) or the assembled copy")
     ap.add_argument("--march-rows", type=int, default=4,
                     help="grid rows per workgroup of the marching stencil kernels (matrix-free F, D, G, Gt_G)")
+    ap.add_argument("--no-fuse-g", action="store_true",
+                    help="one GPU: launch G x_p separately instead of recomputing it inside the second F solve's sweeps")
     ap.add_argument("--no-ca", action="store_true",
                     help="row partition: exchange before every sweep instead of the communication-avoiding schedule")
     ap.add_argument("--self-halo", action="store_true",
@@ -160,7 +176,8 @@ def main():
         bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
         A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
         pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, layout=args.layout,
-                                          f_mode=args.f_mode, pg_mode=args.pg_mode, q_mode=args.q_mode)
+                                          f_mode=args.f_mode, pg_mode=args.pg_mode, q_mode=args.q_mode,
+                                          fuse_g=not args.no_fuse_g)
         del F, D, G
     else:
         from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
@@ -222,9 +239,12 @@ def main():
 
     # dominant kernel: the fused Chebyshev-Jacobi sweep over F
     fused_init = getattr(pc, "f_stencil", None) is not None and (not partitioned or pc.ca)
-    sbytes, kname = sweep_bytes(pc, args.layout, kf, sf, fused_init)
-    avg_sweep_s = (sum(sweep_ms) / len(sweep_ms) / 1e3) if sweep_ms else float("nan")
+    # the dominant kernel's roofline over the first F solve's plain sweeps (b streamed, 184.5 MB per launch at
+    # 1024^2); the second solve's sweeps (G x_p recomputed when fused) are reported beside it
+    per_apply, kname = sweep_bytes(pc, args.layout, kf, sf, fused_init)
+    sbytes, avg_sweep_s, n_timed = roofline_of(per_apply, sweep_ms, 1)
     achieved = sbytes / avg_sweep_s / 1e9
+    gbytes, g_s, g_timed = roofline_of(per_apply, sweep_ms, 2)
 
     spmv = None
     if A is not None and not args.no_spmv:
@@ -298,6 +318,7 @@ def main():
                        else "assembled",
                        "d_g_gtg": "matrix-free" if getattr(pc, "pg_stencil", None) is not None else "assembled",
                        "gt_f_g": "diamond-13" if getattr(pc, "q13", None) is not None else args.layout,
+                       "g_x_p": "recomputed in the second F solve" if getattr(pc, "fuse_g", False) else "kernel",
                        "launch": "hipgraph" if graph is not None else "eager",
                        **({"halo": f"{pc.halo_impl} ({'self-exchange' if world == 1 else 'neighbour'})",
                            "halo_schedule": (f"communication-avoiding: 2 exchanges per apply, ghost depth "
@@ -310,9 +331,15 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
                          "bytes_per_launch": sbytes, "avg_launch_us": avg_sweep_s * 1e6,
-                         "launches_timed": len(sweep_ms),
-                         "timing": "HIP events around each F sweep on the apply stream"
+                         "launches_timed": n_timed,
+                         "timing": "HIP events around each plain sweep of the first F solve on the apply stream"
                                    + ", eager pass of the same K applies after the timed loop"},
+            "roofline_second_f_solve": {
+                "bound": "hbm", "achieved": gbytes / g_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": gbytes / g_s / 1e9 / HBM_PEAK_GBS, "bytes_per_launch": gbytes, "avg_launch_us": g_s * 1e6,
+                "launches_timed": g_timed,
+                "kernel": kname + (" with G x_p recomputed per row (x_p read instead of W)"
+                                   if getattr(pc, "fuse_g", False) else "")},
             "spmv_A": spmv,
             # north_star's CSR SpMV target: the plain A u product (apply.py:72) on the scipy CSR arrays
             "roofline_csr_spmv": None if spmv is None else {

@@ -224,6 +224,9 @@ typedef struct mpbp_schur_plan {
     int32_t q13_n;                   /* its grid size n */
     const mpbp_mg* mg_F;             /* inner_F.kind == MPBP_INNER_MG: F's hierarchy (level 0 = F; one GPU) */
     const mpbp_mg* mg_P;             /* inner_P.kind == MPBP_INNER_MG: Gt_G's hierarchy */
+    int32_t fuse_g;                  /* 1 (one GPU, f_stencil and pg_stencil, Chebyshev F solve of >= 2 sweeps): the
+                                        second F solve recomputes its right-hand side G x_p inside each sweep (no G
+                                        launch, W never stored; bit-identical) */
 } mpbp_schur_plan;
 
 const char* mpbp_version(void);

@@ -90,7 +90,8 @@ class SchurPlan(Structure):
                 ("f_vface", c_void_p), ("f_part", RowPart), ("pg_stencil", c_int32), ("p_part", RowPart),
                 ("halo_first", c_int32), ("ca", c_int32), ("ca_reach_q", c_int32), ("wu_ext", c_void_p),
                 ("diag_F_ext", c_void_p), ("diag_P_ext", c_void_p), ("halo_pair", HALO_PAIR_FN),
-                ("q13", c_void_p), ("q13_n", c_int32), ("mg_F", POINTER(Mg)), ("mg_P", POINTER(Mg))]
+                ("q13", c_void_p), ("q13_n", c_int32), ("mg_F", POINTER(Mg)), ("mg_P", POINTER(Mg)),
+                ("fuse_g", c_int32)]
 
 
 _P = c_void_p

@@ -726,7 +726,9 @@ struct EpiJacobiT {   // x = (b - R x)/D in residual form (solve.py:158)
     }
     __device__ void operator()(int32_t r, double acc, const P& p) const { apply<false>(r, acc, p); }
 };
-template <bool FIXED = false, bool SUB = true, bool SD = true>
+// BX (FIXED instances of the marching kernels only): b is not loaded -- the kernel recomputes it per row and hands
+// it over with set_b (the second F solve's right-hand side W = G x_p, solve.py:273-274, never stored).
+template <bool FIXED = false, bool SUB = true, bool SD = true, bool BX = false>
 struct EpiChebT {
     const double* xin;
     const double* b;
@@ -740,7 +742,7 @@ struct EpiChebT {
     __device__ bool has_sub() const { return FIXED ? SUB : sub != nullptr; }
     __device__ bool stores_d() const { return FIXED ? SD : store_d != 0; }
     __device__ P pre(int32_t r) const { return {xin[r], ld_stream(b + r), diag ? diag[r] : 0.0, ld_stream(d + r), sub ? ld_stream(sub + r) : 0.0}; }
-    __device__ P pre_lite(int32_t r) const { return {0.0, ld_stream(b + r), 0.0, ld_stream(d + r), has_sub() ? ld_stream(sub + r) : 0.0}; }
+    __device__ P pre_lite(int32_t r) const { return {0.0, BX ? 0.0 : ld_stream(b + r), 0.0, ld_stream(d + r), has_sub() ? ld_stream(sub + r) : 0.0}; }
     template <bool NT = false>
     __device__ void apply(int32_t r, double acc, const P& p) const {
         const double z = (p.b - acc) / p.dg;
@@ -753,7 +755,7 @@ struct EpiChebT {
 };
 // EpiCheb for the first sweep after x0 = d0 = c2[0] b / diag: the previous direction is the staged x0
 // itself (x and diag supplied by the stencil via set_x / set_diag), so d is written but not read.
-template <bool FIXED = false, bool SUB = true, bool SD = true>
+template <bool FIXED = false, bool SUB = true, bool SD = true, bool BX = false>
 struct EpiChebFirstT {
     const double* b;
     double* d;
@@ -765,7 +767,7 @@ struct EpiChebFirstT {
     __device__ bool has_sub() const { return FIXED ? SUB : sub != nullptr; }
     __device__ bool stores_d() const { return FIXED ? SD : store_d != 0; }
     __device__ P pre(int32_t r) const { return {0.0, ld_stream(b + r), 0.0, sub ? ld_stream(sub + r) : 0.0}; }
-    __device__ P pre_lite(int32_t r) const { return {0.0, ld_stream(b + r), 0.0, has_sub() ? ld_stream(sub + r) : 0.0}; }
+    __device__ P pre_lite(int32_t r) const { return {0.0, BX ? 0.0 : ld_stream(b + r), 0.0, has_sub() ? ld_stream(sub + r) : 0.0}; }
     template <bool NT = false>
     __device__ void apply(int32_t r, double acc, const P& p) const {
         const double z = (p.b - acc) / p.dg;
@@ -803,9 +805,29 @@ __host__ inline int with_fixed_epi(const EpiChebFirst& e, Fn&& fn) {
 #undef MPBP_CHEBF
 }
 
+// The same, with b supplied by the kernel (BX): the F sweeps of the second F solve with W = G x_p recomputed.
+template <class Epi, class Fn>
+__host__ inline int with_fixed_epi_bx(const Epi& e, Fn&& fn) { return set_error(MPBP_ERR_ARG, "no BX epilogue"); }
+template <class Fn>
+__host__ inline int with_fixed_epi_bx(const EpiCheb& e, Fn&& fn) {
+#define MPBP_CHEB(SUB, SD) fn(EpiChebT<true, SUB, SD, true>{e.xin, e.b, e.diag, e.d, e.c1, e.c2, e.sub, e.xout, e.store_d})
+    return e.sub ? (e.store_d ? MPBP_CHEB(true, true) : MPBP_CHEB(true, false))
+                 : (e.store_d ? MPBP_CHEB(false, true) : MPBP_CHEB(false, false));
+#undef MPBP_CHEB
+}
+template <class Fn>
+__host__ inline int with_fixed_epi_bx(const EpiChebFirst& e, Fn&& fn) {
+#define MPBP_CHEBF(SUB, SD) fn(EpiChebFirstT<true, SUB, SD, true>{e.b, e.d, e.c1, e.c2, e.sub, e.xout, e.store_d})
+    return e.sub ? (e.store_d ? MPBP_CHEBF(true, true) : MPBP_CHEBF(true, false))
+                 : (e.store_d ? MPBP_CHEBF(false, true) : MPBP_CHEBF(false, false));
+#undef MPBP_CHEBF
+}
+
 // XI entry xi * a * (1 - a) as the assembly evaluates it (left to right).
 __device__ inline double xi_of(double xi, double a) { return xi * a * (1.0 - a); }
 
+template <class PT>
+__device__ inline void set_b(PT& p, double b) { p.b = b; }
 template <class PT>
 __device__ inline void set_diag(PT& p, double d) { p.dg = d; }
 template <class PT>
@@ -1417,6 +1439,53 @@ struct XInit {         // staged value = the first inner iterate: c2 * (b[i] / d
     __device__ double operator()(int32_t i) const { return c2 * (b[i] / dg[i]); }
 };
 
+// Right-hand-side sources of the marching F sweeps.  BNone: the epilogue loads b.  GxB: b is the velocity row of
+// W = G x_p (solve.py:273), recomputed per row from x_p and the staged cell thn with GStencilDev::row's arithmetic
+// (d_p, 1/dx, -1/dx and the wrapped neighbour's position exactly as there), so the second F solve of the apply
+// (solve.py:274) reads one pressure field (8 B per cell, cached neighbours) instead of W's four (32 B per cell),
+// and W is never written.  One GPU (whole-grid layouts).
+struct BNone {
+    static constexpr bool on = false;
+    struct Q {};
+    __device__ Q load(int, int) const { return {}; }
+    template <class TA>
+    __device__ double b(int, int, int, int, const TA&, const Q&) const { return 0.0; }
+};
+struct GxB {
+    static constexpr bool on = true;
+    const double* __restrict__ xp;
+    double d_p, inv, minv;
+    int n;
+    struct Q { double c, w, nn; };   // x_p at the cell and at its west and north neighbours (periodic)
+    // (gr, gc): wrapped grid coordinates of the cell
+    __device__ Q load(int gr, int gc) const {
+        const int gw = gc == 0 ? n - 1 : gc - 1, gn = gr == 0 ? n - 1 : gr - 1;
+        return {xp[gr * n + gc], xp[gr * n + gw], xp[gn * n + gc]};
+    }
+    // velocity row o (u_n, v_n, u_s, v_s) at the cell: TA::T(p, r, c) in the accessor's coordinates (gr, c), the
+    // cell's wrapped column gc decides the periodic order as GStencilDev::row does
+    template <class TA>
+    __device__ double b(int o, int gr, int c, int gc, const TA& ta, const Q& q) const {
+        const int p = o >> 1;
+        const double t0 = ta.T(p, gr, c);
+        double acc = 0.0;
+        if ((o & 1) == 0) {   // u row: entries p(gr, gc-1), p(gr, gc); the wrapped one sorts last
+            const double gu = 0.5 * (t0 + ta.T(p, gr, c - 1));
+            const double uC = (d_p * (inv * gu)) * q.c, uW = (d_p * (minv * gu)) * q.w;
+            const bool wrapw = gc == 0;
+            acc += wrapw ? uC : uW;
+            acc += wrapw ? uW : uC;
+        } else {              // v row: entries p(gr-1, gc), p(gr, gc)
+            const double gv = 0.5 * (t0 + ta.T(p, gr - 1, c));
+            const double vC = (d_p * (minv * gv)) * q.c, vN = (d_p * (inv * gv)) * q.nn;
+            const bool wrapn = gr == 0;
+            acc += wrapn ? vC : vN;
+            acc += wrapn ? vN : vC;
+        }
+        return acc;
+    }
+};
+
 // Row of tile values held between its loads and its LDS store: every lane's main column (xa, ta; tile columns
 // c0-1 .. c0+254) in VGPRs, the two halo columns c0+255 and c0+256 (h*, scalar) in SGPRs.
 #ifndef MPBP_HALO_SCALAR
@@ -1507,10 +1576,10 @@ __device__ inline bool march_rows(int which, int L, int ext, int chunk, int nchu
     return *la < *lb;
 }
 
-template <class S, class XS, class Epi>
+template <class S, class XS, class Epi, class BS = BNone>
 // (4 waves per SIMD asked for explicitly: the F Chebyshev instance would otherwise take 130 VGPRs -> 3)
 __global__ void __launch_bounds__(kMB) __attribute__((amdgpu_waves_per_eu(4, 8)))
-k_march(S P, XS xs, int nchunks, Epi epi) {
+k_march(S P, XS xs, int nchunks, Epi epi, BS bs = BS{}) {
     constexpr int NF = S::NF, NO = S::NOUT;
     __shared__ double sx[NF * 3 * kMTileW];
     __shared__ double st[3 * kMTileW];
@@ -1557,6 +1626,7 @@ k_march(S P, XS xs, int nchunks, Epi epi) {
 #pragma unroll
         for (int o = 0; o < NO; ++o) pe[o] = epi.pre_lite(P.out_row(o, lr, gcl));
         const typename S::Cell cl = P.cell_pre(P.wrap(P.r0 + lr), gcl);   // ghost rows wrap periodically
+        const typename BS::Q bq = bs.load(P.wrap(P.r0 + lr), gcl);
         __syncthreads();
         if constexpr (decltype(load_next)::value) load_tile_row(P, xs, P.r0 + lr + 2, gcA, okA, hc, tr);
         if (live) {
@@ -1577,6 +1647,7 @@ k_march(S P, XS xs, int nchunks, Epi epi) {
                                         : P.template row<false>(o, gr, gc, ta, xa, &dg, cl);
                 set_diag(pe[o], dg);
                 set_x(pe[o], xa.X(S::NF == 1 ? 0 : o, gr, gc));
+                if constexpr (BS::on) set_b(pe[o], bs.b(o, gr, gc, gc, ta, bq));
                 epi(P.out_row(o, lr, gc), acc, pe[o]);
             }
         }
@@ -1595,10 +1666,15 @@ k_march(S P, XS xs, int nchunks, Epi epi) {
 // rows' and the halo columns' neighbours).  Invariant at the start of step k: thn rows k-1 .. k+2 and x0 rows
 // k-1, k in LDS, b row k+1 (+ its S::Stage operands) in registers.
 constexpr int kTW = kMTileW + 2;
-template <int NF, class Stage>
+template <int NF, class Stage, class BS = BNone>
 struct InitRow {
     double xa[NF], h0[NF];   // b at the lane's main column and (lanes 0, 1) its halo column
     Stage sa, sh;            // the stencil's per-point operands for the diagonal (F: the u/v face thn)
+};
+template <int NF, class Stage>
+struct InitRow<NF, Stage, GxB> {
+    GxB::Q qa, qh;           // b recomputed from x_p (GxB): its operands at the main and the halo column
+    Stage sa, sh;
 };
 struct ThnRow {
     double ta, te;           // thn at the lane's main column; lanes 0..3 an extra column (c0+255, c0+256, c0-2, c0+257)
@@ -1620,29 +1696,37 @@ __device__ inline void store_thn_row(double* st, int slot, int tid, const ThnRow
     st[slot * kTW + tid + 1] = t.ta;
     if (tid < 4) st[slot * kTW + thn_extra_slot(tid)] = t.te;
 }
-template <class S>
+template <class S, class BS>
 __device__ inline void load_init_row(const S& P, const double* __restrict__ b, int gr, int gcA, bool okA,
-                                     const HaloCols& hc, InitRow<S::NF, typename S::Stage>& tr) {
+                                     const HaloCols& hc, InitRow<S::NF, typename S::Stage, BS>& tr, const BS& bs) {
     const int ca = okA ? gcA : 0;
+    if constexpr (BS::on) {
+        tr.qa = bs.load(P.wrap(gr), ca);
+        tr.qh = bs.load(P.wrap(gr), hc.gl);
+    } else {
 #pragma unroll
-    for (int f = 0; f < S::NF; ++f) {
-        const int32_t base = P.xrow(f, gr);
-        tr.xa[f] = b[base + ca];
-        tr.h0[f] = b[base + hc.gl];
+        for (int f = 0; f < S::NF; ++f) {
+            const int32_t base = P.xrow(f, gr);
+            tr.xa[f] = b[base + ca];
+            tr.h0[f] = b[base + hc.gl];
+        }
     }
     tr.sa = P.stage_pre(gr, ca);
     tr.sh = P.stage_pre(gr, hc.gl);
 }
 // x0 of staged grid row gr (ring slot `slot`) from b and the diagonal rebuilt over thn rows gr-1 .. gr+1.
-template <class S>
+template <class S, class BS>
 __device__ inline void store_init_row(const S& P, double c2, double* sx, const double* st, int slot, const int ts[3],
                                       int gr, int c0, int tid, int colA, bool okA, const HaloCols& hc,
-                                      const InitRow<S::NF, typename S::Stage>& tr) {
+                                      const InitRow<S::NF, typename S::Stage, BS>& tr, const BS& bs) {
     const TRingT<kTW, 2> ta{st, {ts[0], ts[1], ts[2]}, gr, c0};
 #pragma unroll
     for (int f = 0; f < S::NF; ++f) {
         const double dg = P.stage_diag(f, gr, colA, ta, tr.sa);
-        sx[(f * 3 + slot) * kMTileW + tid] = okA ? c2 * (tr.xa[f] / dg) : 0.0;
+        double bf;
+        if constexpr (BS::on) bf = bs.b(f, gr, colA, P.wrap(colA), ta, tr.qa);
+        else bf = tr.xa[f];
+        sx[(f * 3 + slot) * kMTileW + tid] = okA ? c2 * (bf / dg) : 0.0;
     }
     if (tid < 2) {   // lanes 0 and 1: the halo columns c0+255, c0+256
         const bool ok = tid == 0 ? hc.ok0 : hc.ok1;
@@ -1650,14 +1734,17 @@ __device__ inline void store_init_row(const S& P, double c2, double* sx, const d
 #pragma unroll
         for (int f = 0; f < S::NF; ++f) {
             const double dg = P.stage_diag(f, gr, col, ta, tr.sh);
-            sx[(f * 3 + slot) * kMTileW + kMB + tid] = ok ? c2 * (tr.h0[f] / dg) : 0.0;
+            double bf;
+            if constexpr (BS::on) bf = bs.b(f, gr, col, P.wrap(col), ta, tr.qh);
+            else bf = tr.h0[f];
+            sx[(f * 3 + slot) * kMTileW + kMB + tid] = ok ? c2 * (bf / dg) : 0.0;
         }
     }
 }
 
-template <class S, class Epi>
+template <class S, class Epi, class BS = BNone>
 __global__ void __launch_bounds__(kMB) __attribute__((amdgpu_waves_per_eu(4, 8)))
-k_march_init(S P, const double* __restrict__ b, double c2, int nchunks, Epi epi) {
+k_march_init(S P, const double* __restrict__ b, double c2, int nchunks, Epi epi, BS bs = BS{}) {
     constexpr int NF = S::NF, NO = S::NOUT;
     __shared__ double sx[NF * 3 * kMTileW];
     __shared__ double st[5 * kTW];
@@ -1685,40 +1772,41 @@ k_march_init(S P, const double* __restrict__ b, double c2, int nchunks, Epi epi)
     auto tslot = [&](int lr) { return (lr - la + 2) % 5; };   // thn ring slot of local row lr (lr >= la - 2)
     auto xslot = [&](int lr) { return (lr - la + 1) % 3; };   // x ring slot (lr >= la - 1)
     auto grow = [&](int lr) { return P.wrap(P.r0 + lr); };    // grid row (ghost rows wrap periodically)
-    typedef InitRow<NF, typename S::Stage> IR;
+    typedef InitRow<NF, typename S::Stage, BS> IR;
     // prologue: thn rows la-2 .. la+2, x0 rows la-1 and la; b row la+1 into registers
     {
         ThnRow t[5];
         IR r0, r1;
 #pragma unroll
         for (int i = 0; i < 5; ++i) load_thn_row(P, P.r0 + la - 2 + i, colA, tid, c0, t[i]);
-        load_init_row(P, b, P.r0 + la - 1, gcA, okA, hc, r0);
-        load_init_row(P, b, P.r0 + la, gcA, okA, hc, r1);
+        load_init_row(P, b, P.r0 + la - 1, gcA, okA, hc, r0, bs);
+        load_init_row(P, b, P.r0 + la, gcA, okA, hc, r1, bs);
 #pragma unroll
         for (int i = 0; i < 5; ++i) store_thn_row(st, i, tid, t[i]);
         __syncthreads();
         const int s0[3] = {tslot(la - 2), tslot(la - 1), tslot(la)};
-        store_init_row(P, c2, sx, st, xslot(la - 1), s0, grow(la - 1), c0, tid, colA, okA, hc, r0);
+        store_init_row(P, c2, sx, st, xslot(la - 1), s0, grow(la - 1), c0, tid, colA, okA, hc, r0, bs);
         const int s1[3] = {tslot(la - 1), tslot(la), tslot(la + 1)};
-        store_init_row(P, c2, sx, st, xslot(la), s1, grow(la), c0, tid, colA, okA, hc, r1);
+        store_init_row(P, c2, sx, st, xslot(la), s1, grow(la), c0, tid, colA, okA, hc, r1, bs);
     }
     IR tr;
     ThnRow tn;
-    load_init_row(P, b, P.r0 + la + 1, gcA, okA, hc, tr);
+    load_init_row(P, b, P.r0 + la + 1, gcA, okA, hc, tr, bs);
     auto step = [&](int lr, auto load_next) {
         {   // x0 of row lr+1 (thn rows lr .. lr+2)
             const int ts[3] = {tslot(lr), tslot(lr + 1), tslot(lr + 2)};
-            store_init_row(P, c2, sx, st, xslot(lr + 1), ts, grow(lr + 1), c0, tid, colA, okA, hc, tr);
+            store_init_row(P, c2, sx, st, xslot(lr + 1), ts, grow(lr + 1), c0, tid, colA, okA, hc, tr, bs);
         }
         const int gcl = live ? gc : 0;
         typename Epi::P pe[NO];
 #pragma unroll
         for (int o = 0; o < NO; ++o) pe[o] = epi.pre_lite(P.out_row(o, lr, gcl));
         const typename S::Cell cl = P.cell_pre(grow(lr), gcl);
+        const typename BS::Q bq = bs.load(grow(lr), gcl);
         __syncthreads();
         if constexpr (decltype(load_next)::value) {   // thn row lr+3 first: it is stored at the end of this step
             load_thn_row(P, P.r0 + lr + 3, colA, tid, c0, tn);
-            load_init_row(P, b, P.r0 + lr + 2, gcA, okA, hc, tr);
+            load_init_row(P, b, P.r0 + lr + 2, gcA, okA, hc, tr, bs);
         }
         if (live) {
             const int gr = grow(lr);
@@ -1732,6 +1820,7 @@ k_march_init(S P, const double* __restrict__ b, double c2, int nchunks, Epi epi)
                                         : P.template row<false>(o, gr, gc, ta, xa, &dg, cl);
                 set_diag(pe[o], dg);
                 set_x(pe[o], xa.X(S::NF == 1 ? 0 : o, gr, gc));
+                if constexpr (BS::on) set_b(pe[o], bs.b(o, gr, gc, gc, ta, bq));
                 epi(P.out_row(o, lr, gc), acc, pe[o]);
             }
         }
@@ -1776,33 +1865,39 @@ int64_t march_chunks(const S& P, int rows_per_block, int64_t capacity) {
     return chunks;
 }
 
-template <class S, class XS, class Epi>
-int launch_march_fixed(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStream_t st) {
-    const int64_t chunks = march_chunks(P, rows_per_block, march_capacity<k_march<S, XS, Epi>>());
+template <class S, class XS, class Epi, class BS = BNone>
+int launch_march_fixed(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStream_t st, const BS& bs = BS{}) {
+    const int64_t chunks = march_chunks(P, rows_per_block, march_capacity<k_march<S, XS, Epi, BS>>());
     if (chunks == 0) return MPBP_OK;
     const int64_t strips = (P.n + kMB - 1) / kMB;
-    k_march<S, XS, Epi><<<(unsigned)(chunks * strips), kMB, 0, st>>>(P, xs, (int)chunks, epi);
+    k_march<S, XS, Epi, BS><<<(unsigned)(chunks * strips), kMB, 0, st>>>(P, xs, (int)chunks, epi, bs);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
 
-// The first inner sweep with x0 = c2 b / diag staged and diag rebuilt from thn (k_march_init).
-template <class S, class Epi>
-int launch_march_init(const S& P, const double* b, double c2, Epi epi, int rows_per_block, hipStream_t st) {
-    return with_fixed_epi(epi, [&](const auto& e) {
+// The first inner sweep with x0 = c2 b / diag staged and diag rebuilt from thn (k_march_init).  BS = GxB: b is
+// W = G x_p recomputed per point (the second F solve of the apply).
+template <class S, class Epi, class BS = BNone>
+int launch_march_init(const S& P, const double* b, double c2, Epi epi, int rows_per_block, hipStream_t st,
+                      const BS& bs = BS{}) {
+    auto go = [&](const auto& e) {
         using E = std::decay_t<decltype(e)>;
-        const int64_t chunks = march_chunks(P, rows_per_block, march_capacity<k_march_init<S, E>>());
+        const int64_t chunks = march_chunks(P, rows_per_block, march_capacity<k_march_init<S, E, BS>>());
         if (chunks == 0) return (int)MPBP_OK;
         const int64_t strips = (P.n + kMB - 1) / kMB;
-        k_march_init<S, E><<<(unsigned)(chunks * strips), kMB, 0, st>>>(P, b, c2, (int)chunks, e);
+        k_march_init<S, E, BS><<<(unsigned)(chunks * strips), kMB, 0, st>>>(P, b, c2, (int)chunks, e, bs);
         MPBP_HIP(hipGetLastError());
         return (int)MPBP_OK;
-    });
+    };
+    if constexpr (BS::on) return with_fixed_epi_bx(epi, go);
+    else return with_fixed_epi(epi, go);
 }
 
-template <class S, class XS, class Epi>
-int launch_march(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStream_t st) {
-    return with_fixed_epi(epi, [&](const auto& e) { return launch_march_fixed(P, xs, e, rows_per_block, st); });
+template <class S, class XS, class Epi, class BS = BNone>
+int launch_march(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStream_t st, const BS& bs = BS{}) {
+    auto go = [&](const auto& e) { return launch_march_fixed(P, xs, e, rows_per_block, st, bs); };
+    if constexpr (BS::on) return with_fixed_epi_bx(epi, go);
+    else return with_fixed_epi(epi, go);
 }
 
 // F row of field f at a cell (k_march policy).
@@ -3138,6 +3233,52 @@ int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag
     return MPBP_OK;
 }
 
+// u = Finv_v - F^-1 (G x_p) (solve.py:273-276) with the second F solve's right-hand side W = G x_p recomputed
+// inside each of its sweeps from x_p (GxB) instead of a G launch writing W: one GPU, matrix-free F and G,
+// Chebyshev with K >= 2 sweeps.  Each row performs the IEEE operations of G's row followed by inner_solve's
+// sweep (bit-identical), and the solve reads one pressure field instead of W's four velocity fields.
+int f_solve_gx(const Ctx& c, const double* xp, const mpbp_inner_solver& in, double* dst, const double* sub,
+               double* ping, double* pong, double* dir, bool profile) {
+    const mpbp_schur_plan* p = c.p;
+    const int K = in.sweeps;
+    if (in.kind != MPBP_INNER_CHEBYSHEV || K < 2 || K > 64 || !(in.lmax > in.lmin) || !(in.lmin >= 0.0))
+        return set_error(MPBP_ERR_ARG, "schur_apply (fused G): needs a Chebyshev F solve of 2..64 sweeps");
+    double c1[64] = {}, c2[64] = {};
+    cheb_coeffs(in.lmin, in.lmax, K, c1, c2);
+    FStencilDev P;
+    int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &P);
+    if (rc) return rc;
+    PGDev G;
+    rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &G);
+    if (rc) return rc;
+    const GxB bs{xp, G.d_p, G.inv, G.minv, G.n};
+    double* cur = K == 2 ? dst : pong;
+    rc = with_f_identities(P, [&](const auto& Q) {
+        return launch_march_init(Q, nullptr, c2[0], EpiChebFirst{nullptr, dir, c1[1], c2[1], K == 2 ? sub : nullptr, cur,
+                                                                 K == 2 ? 0 : 1}, g_march_rows, c.st, bs);
+    });
+    if (rc) return rc;
+    for (int s = 2; s < K; ++s) {
+        const bool last = s == K - 1;
+        double* nxt = last ? dst : (cur == ping ? pong : ping);
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        const bool rec = profile && p->prof_events && p->prof_count && *p->prof_count < p->prof_capacity &&
+                         hipStreamIsCapturing(c.st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone;
+        if (rec) MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count], c.st));
+        rc = with_f_identities(P, [&](const auto& Q) {
+            return launch_march(Q, XPlain{cur}, EpiCheb{cur, nullptr, nullptr, dir, c1[s], c2[s], last ? sub : nullptr,
+                                                        nxt, last ? 0 : 1}, g_march_rows, c.st, bs);
+        });
+        if (rc) return rc;
+        if (rec) {
+            MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count + 1], c.st));
+            ++*p->prof_count;
+        }
+        cur = nxt;
+    }
+    return MPBP_OK;
+}
+
 // ---- communication-avoiding schedule (row partition) ----
 // A stencil operator over the owned rows and `ext` ghost rows each side.
 OpRef ext_op(const mpbp_schur_plan* p, int32_t sop, int ext) {
@@ -3312,6 +3453,10 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
     if (rc) return rc;
     if (Pxp != out_p)
         MPBP_HIP(hipMemcpyAsync(out_p, Pxp, sizeof(double) * (size_t)p->np, hipMemcpyDeviceToDevice, c.st));
+    // 6.+7. fused: the second F solve recomputes G x_p in its sweeps (one GPU, matrix-free F and G, Chebyshev F)
+    if (p->fuse_g && !p->halo && p->f_stencil && p->pg_stencil && p->inner_F.kind == MPBP_INNER_CHEBYSHEV &&
+        p->inner_F.sweeps >= 2)
+        return f_solve_gx(c, Pxp, p->inner_F, out_u, Y, U0, U1, Ud, true);
     // 6. G_xp = G @ x_p                                                     solve.py:273
     rc = two_phase(c, MPBP_VEC_PRESSURE, Pxp, G,
                    [&](const OpRef& o) { return op_spmv(o, MPBP_SPMV_STORE, Pxp, nullptr, W, c.st); });

@@ -182,7 +182,7 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
 
     def __init__(self, F, D, G, GtG=None, GtFG=None, inner_F: InnerSolver | None = None,
                  inner_P: InnerSolver | None = None, device=None, layout: str = "sell", f_mode: str = "auto",
-                 pg_mode: str = "auto", q_mode: str = "auto"):
+                 pg_mode: str = "auto", q_mode: str = "auto", fuse_g: bool = True):
         dev = torch.device(device or (F.device if isinstance(F, DeviceCSR) else "cuda"))
         self.F, self.D, self.G = (_device_csr(M, dev) for M in (F, D, G))
         if GtG is None or GtFG is None:
@@ -233,6 +233,10 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
         # 104 B per row instead of 156), "assembled" the CSR / SELL copy; "auto" = diamond whenever Gt_F_G is
         # the n^2 x n^2 periodic-grid product (n >= 5), else assembled.
         self.q13 = _q13_layout(self.GtFG, q_mode)
+        # the second F solve recomputes its right-hand side G x_p inside its sweeps (no G launch, W never stored)
+        # when F and G are both matrix-free and F's inner solve is Chebyshev with >= 2 sweeps; same bits
+        self.fuse_g = bool(fuse_g and self.f_stencil is not None and self.pg_stencil is not None
+                           and self.inner_F.kind == "chebyshev" and self.inner_F.sweeps >= 2)
         self._plan = self._make_plan()
         super().__init__(dtype=np.float64, shape=(nu + np_, nu + np_))
 
@@ -279,6 +283,7 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
             p.mg_F = ctypes.pointer(self.mg_F.cstruct())
         if self.mg_P is not None:
             p.mg_P = ctypes.pointer(self.mg_P.cstruct())
+        p.fuse_g = 1 if self.fuse_g else 0
         return p
 
     def sell_of(self, key):

@@ -170,3 +170,23 @@ def test_fused_first_sweep_rebuilt_diagonal(n, prm, inner, march_rows):
             assert _bits(pc.apply(v), ref), (mode, rel_inf(pc.apply(v).cpu().numpy(), ref.cpu().numpy()))
     finally:
         check(lib().mpbp_set_init_diag(1))
+
+
+@pytest.mark.parametrize("n", [3, 4, 5, 64, 257])
+@pytest.mark.parametrize("prm", PARAMS, ids=["visc", "stiff", "c0-neg-dp"])
+@pytest.mark.parametrize("sweeps", [2, 3, 4, 5])
+def test_second_f_solve_recomputes_g(n, prm, sweeps, march_rows):
+    """The second F solve with W = G x_p recomputed inside its sweeps (plan.fuse_g: no G launch) equals the
+    unfused apply (G kernel, then the sweeps reading W) bit for bit: first sweep (staged x0 = c2 W / diag) and
+    the plain sweeps, every parameter identity instance, the periodic edges, ragged strips (n = 257)."""
+    import mp_block_preconditioners_amd as mp
+    F, D, G, GtG, GtFG = _system(n, prm)
+    kw = dict(inner_F=mp.InnerSolver("chebyshev", sweeps), inner_P=mp.InnerSolver("chebyshev", 3))
+    fused = mp.ApproxSchurPreconditioner(F, D, G, GtG, GtFG, **kw)
+    plain = mp.ApproxSchurPreconditioner(F, D, G, GtG, GtFG, fuse_g=False, **kw)
+    assert fused.fuse_g and not plain.fuse_g
+    v = torch.from_numpy(np.random.default_rng(n + sweeps).standard_normal(fused.shape[0])).cuda()
+    a, b = fused.apply(v), plain.apply(v)
+    assert _bits(a, b), rel_inf(a.cpu().numpy(), b.cpu().numpy())
+    # Jacobi F solves keep the G launch
+    assert not mp.ApproxSchurPreconditioner(F, D, G, GtG, GtFG, inner_F=mp.InnerSolver("jacobi", 3)).fuse_g
