@@ -742,14 +742,22 @@ struct EpiChebT {
     __device__ bool has_sub() const { return FIXED ? SUB : sub != nullptr; }
     __device__ bool stores_d() const { return FIXED ? SD : store_d != 0; }
     __device__ P pre(int32_t r) const { return {xin[r], ld_stream(b + r), diag ? diag[r] : 0.0, ld_stream(d + r), sub ? ld_stream(sub + r) : 0.0}; }
-    __device__ P pre_lite(int32_t r) const { return {0.0, BX ? 0.0 : ld_stream(b + r), 0.0, ld_stream(d + r), has_sub() ? ld_stream(sub + r) : 0.0}; }
+#ifndef MPBP_GX_SUB_LATE
+#define MPBP_GX_SUB_LATE 1
+#endif
+    // BX && MPBP_GX_SUB_LATE: `sub` is loaded in the epilogue itself instead of ahead of the row -- the fused
+    // second solve's last sweep otherwise spills (128 VGPRs + 24 B scratch): 40.9 -> 38.9 us per launch
+    // (2541-2565 -> 2573-2640 applies/s, A/B on one box)
+    static constexpr bool kSubLate = BX && MPBP_GX_SUB_LATE;
+    __device__ P pre_lite(int32_t r) const { return {0.0, BX ? 0.0 : ld_stream(b + r), 0.0, ld_stream(d + r), (has_sub() && !kSubLate) ? ld_stream(sub + r) : 0.0}; }
     template <bool NT = false>
     __device__ void apply(int32_t r, double acc, const P& p) const {
         const double z = (p.b - acc) / p.dg;
         const double dn = c1 * p.d + c2 * z;
         if (stores_d()) st_stream<NT>(d + r, dn);
         const double x = p.x + dn;
-        st_stream<NT>(xout + r, has_sub() ? p.s - x : x);
+        const double sv = kSubLate && has_sub() ? ld_stream(sub + r) : p.s;
+        st_stream<NT>(xout + r, has_sub() ? sv - x : x);
     }
     __device__ void operator()(int32_t r, double acc, const P& p) const { apply<false>(r, acc, p); }
 };

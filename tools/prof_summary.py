@@ -15,8 +15,8 @@ import re
 
 def short(name):
     name = name.replace("(anonymous namespace)::", "")
-    m = re.match(r"(?:void )?([\w:]+(?:<[^()]*?>)?)", name)
-    return m.group(1) if m else name[:60]
+    name = re.sub(r"^void ", "", name)
+    return name.split("(")[0] if "(" in name else name[:120]   # the full template name, without the arguments
 
 
 def main():
