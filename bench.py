@@ -107,6 +107,7 @@ def main():
                     help="Gt_F_G: values in the 13-point diamond layout (columns implicit) or the assembled copy")
     ap.add_argument("--march-rows", type=int, default=4,
                     help="grid rows per workgroup of the marching stencil kernels (matrix-free F, D, G, Gt_G)")
+    ap.add_argument("--pg-direct", type=int, default=None, help="1: D / Gt_G sweeps as one thread per cell (no LDS)")
     ap.add_argument("--no-fuse-g", action="store_true",
                     help="one GPU: launch G x_p separately instead of recomputing it inside the second F solve's sweeps")
     ap.add_argument("--no-ca", action="store_true",
@@ -163,6 +164,8 @@ def main():
     import mp_block_preconditioners_amd as mp
     from mp_block_preconditioners_amd._lib import check as _check, lib as _lib
     _check(_lib().mpbp_set_march_rows(args.march_rows))
+    if args.pg_direct is not None:
+        _check(_lib().mpbp_set_pg_direct(args.pg_direct))
 
     if args.weak:
         n = int(round((args.n or 1024) * math.sqrt(world)))

@@ -33,12 +33,17 @@ def _bits(a, b):
 PARAMS = [(1.0, 100.0, 1.0, 1.0, -1.0, 1.0), (2.5, 1.0e4, 1.0, 0.5, -2.0, 2.5), (1.0, 1.0, 1.0, 0.0, -1.0, -0.75)]
 
 
-@pytest.fixture(params=[4, 1, 7], ids=["march4", "march1", "march7"])
+@pytest.fixture(params=[(4, 1), (4, 0), (1, 0), (7, 0)], ids=["direct", "march4", "march1", "march7"])
 def march_rows(request):
+    """Workgroup shapes of the marching kernels, and the direct one-thread-per-cell kernel for D / G / Gt_G
+    (mpbp_set_pg_direct): results must not depend on either."""
     from mp_block_preconditioners_amd._lib import check, lib
-    check(lib().mpbp_set_march_rows(request.param))
+    rows, direct = request.param
+    check(lib().mpbp_set_march_rows(rows))
+    check(lib().mpbp_set_pg_direct(direct))
     yield request.param
     check(lib().mpbp_set_march_rows(4))
+    check(lib().mpbp_set_pg_direct(1))
 
 
 def _system(n, prm, tables=None):
