@@ -401,7 +401,7 @@ def single_gpu_check(dpc, n, args, iF, iP, rank, dist, torch):
                     f"vector (numpy seed 2048), built on each rank's GPU; {time.perf_counter() - t0:.1f} s"}
 
 
-def spmv_bench(A, gen, reps=20, replays=5):
+def spmv_bench(A, gen, reps=20, replays=10, warm_replays=5):
     """The plain operator matvec b = A u (apply.py:72) in both layouts, HIP-event timed.
 
     `reps` back-to-back launches are captured into one hipGraph and replayed `replays` times between two
@@ -436,7 +436,8 @@ def spmv_bench(A, gen, reps=20, replays=5):
             with torch.cuda.graph(g):
                 for _ in range(reps):
                     M.matvec(x, out=y)
-            g.replay()
+            for _ in range(warm_replays):   # the clock settles under the sustained stream before timing
+                g.replay()
             torch.cuda.synchronize()
             ev[0].record()
             for _ in range(replays):

@@ -57,7 +57,7 @@ step() {
             python "$ROOTD/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-solve $BENCH_ARGS ;;
     pmc) for C in FETCH_SIZE WRITE_SIZE; do
            prof "pmc_apply_$C" 150 --pmc $C --output-format csv -d "$ROOTD/$OUT/pmc_apply_$C" -o pmc -- \
-             python "$ROOTD/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-spmv --no-graph || return 1
+             python "$ROOTD/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-spmv --no-graph --no-solve || return 1
            prof "pmc_spmv_$C" 120 --pmc $C --output-format csv -d "$ROOTD/$OUT/pmc_spmv_$C" -o pmc -- \
              python "$ROOTD/tools/spmv_ab.py" --reps 10 || return 1
          done ;;

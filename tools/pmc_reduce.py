@@ -34,14 +34,18 @@ def main():
     # F sweep kernels and their launch grids (threads)
     # (the marching kernel's grid depends on its rows per workgroup: matched by name only)
     # (the F policy may carry the parameter identities: FStencilDev or FStencilDevM<M>)
-    kernels = {"stencil": (("k_march<(anonymous namespace)::FStencilDev", "(anonymous namespace)::XPlain, "
-                            "(anonymous namespace)::EpiCheb>"), None),
+    # "stencil": the first F solve's plain sweeps (b streamed, no sub: EpiChebT<true, false, SD, false>), the
+    # launches bench.py's `roofline` times; tools/gpu.sh's pmc step writes them under pmc_apply_<counter>
+    kernels = {"stencil": (("k_march<(anonymous namespace)::FStencilDev", "(anonymous namespace)::XPlain, ",
+                            "EpiChebT<true, false, ", "BNone>"), args.n * args.n // 4),   # 4 rows x 256 cols / WG
                "sell": ("k_sell_rows<(anonymous namespace)::EpiCheb>", grid)}   # grid 4N: F rows, not Gt_G
     out = {"n": args.n, "source": args.run_dir}
     for lay, (kname, kgrid) in kernels.items():
         res = {}
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
             f = os.path.join(args.run_dir, f"pmc_{lay}_{c}", "pmc_counter_collection.csv")
+            if lay == "stencil" and not os.path.exists(f):
+                f = os.path.join(args.run_dir, f"pmc_apply_{c}", "pmc_counter_collection.csv")
             if os.path.exists(f):
                 res[c] = mean_counter(f, c, kname, kgrid)
         if "FETCH_SIZE" in res and res["FETCH_SIZE"][0] is not None and "WRITE_SIZE" in res:
