@@ -109,7 +109,7 @@ def main():
                     help="grid rows per workgroup of the marching stencil kernels (matrix-free F, D, G, Gt_G)")
     ap.add_argument("--pg-direct", type=int, default=None, help="1: D / Gt_G sweeps as one thread per cell (no LDS)")
     ap.add_argument("--no-fuse-g", action="store_true",
-                    help="one GPU: launch G x_p separately instead of recomputing it inside the second F solve's sweeps")
+                    help="launch G x_p separately instead of recomputing it inside the second F solve's sweeps")
     ap.add_argument("--no-ca", action="store_true",
                     help="row partition: exchange before every sweep instead of the communication-avoiding schedule")
     ap.add_argument("--self-halo", action="store_true",
@@ -187,7 +187,7 @@ def main():
         pc = DistributedSchurPreconditioner(n, args.xi, args.eta_n, args.eta_s, inner_F=iF, inner_P=iP,
                                             layout=args.layout, f_mode=args.f_mode, pg_mode=args.pg_mode,
                                             self_halo=args.self_halo, halo_overlap=args.halo_overlap,
-                                            ca=False if args.no_ca else "auto")
+                                            ca=False if args.no_ca else "auto", fuse_g=not args.no_fuse_g)
     gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
     v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda", generator=gen)
     out = torch.empty_like(v)

@@ -359,8 +359,8 @@ int mpbp_set_march_rows(int32_t rows);
 /* The first sweep of a matrix-free F inner solve stages x0 = c2 b / diag: mode 1 (default) rebuilds diag from the
  * thn tables inside the sweep (no diag stream), mode 0 streams the stored diagonal.  Same bits either way. */
 int mpbp_set_init_diag(int32_t mode);
-/* 1 (default): the matrix-free D, G and Gt_G sweeps on one GPU run as one thread per cell reading neighbours from
- * global memory (no LDS ring); 0: the marching kernel (always used under a row partition).  Bit-identical. */
+/* 1 (default): the matrix-free D, G and Gt_G sweeps run as one thread per cell reading neighbours from global memory
+ * (no LDS ring; row partitions and ghost layouts included); 0: the marching kernel.  Bit-identical either way. */
 int mpbp_set_pg_direct(int32_t on);
 
 /* ---- geometric multigrid inner solves (the reference's pointer: solve.py:266, 274) ------------------ */

@@ -1455,20 +1455,25 @@ struct XInit {         // staged value = the first inner iterate: c2 * (b[i] / d
 struct BNone {
     static constexpr bool on = false;
     struct Q {};
-    __device__ Q load(int, int) const { return {}; }
+    __device__ Q load(int, int, int) const { return {}; }
     template <class TA>
     __device__ double b(int, int, int, int, const TA&, const Q&) const { return 0.0; }
 };
-struct GxB {
+// PART: x_p in a row partition's ghost layout (L owned rows, h ghost rows each side); else the whole grid.
+template <bool PART>
+struct GxBT {
     static constexpr bool on = true;
     const double* __restrict__ xp;
     double d_p, inv, minv;
     int n;
+    int L = 0, h = 0;
     struct Q { double c, w, nn; };   // x_p at the cell and at its west and north neighbours (periodic)
-    // (gr, gc): wrapped grid coordinates of the cell
-    __device__ Q load(int gr, int gc) const {
+    __device__ int32_t row(int lr, int gr) const { return PART ? ext_row(1, 0, lr, L, h, n) : gr * n; }
+    // lr: the cell's local row in the partition layout, (gr, gc): its wrapped global grid coordinates
+    __device__ Q load(int lr, int gr, int gc) const {
         const int gw = gc == 0 ? n - 1 : gc - 1, gn = gr == 0 ? n - 1 : gr - 1;
-        return {xp[gr * n + gc], xp[gr * n + gw], xp[gn * n + gc]};
+        const int32_t rc = row(lr, gr), rn = row(lr - 1, gn);
+        return {xp[rc + gc], xp[rc + gw], xp[rn + gc]};
     }
     // velocity row o (u_n, v_n, u_s, v_s) at the cell: TA::T(p, r, c) in the accessor's coordinates (gr, c), the
     // cell's wrapped column gc decides the periodic order as GStencilDev::row does
@@ -1493,6 +1498,8 @@ struct GxB {
         return acc;
     }
 };
+using GxB = GxBT<false>;
+using GxBPart = GxBT<true>;
 
 // Row of tile values held between its loads and its LDS store: every lane's main column (xa, ta; tile columns
 // c0-1 .. c0+254) in VGPRs, the two halo columns c0+255 and c0+256 (h*, scalar) in SGPRs.
@@ -1634,7 +1641,7 @@ k_march(S P, XS xs, int nchunks, Epi epi, BS bs = BS{}) {
 #pragma unroll
         for (int o = 0; o < NO; ++o) pe[o] = epi.pre_lite(P.out_row(o, lr, gcl));
         const typename S::Cell cl = P.cell_pre(P.wrap(P.r0 + lr), gcl);   // ghost rows wrap periodically
-        const typename BS::Q bq = bs.load(P.wrap(P.r0 + lr), gcl);
+        const typename BS::Q bq = bs.load(lr, P.wrap(P.r0 + lr), gcl);
         __syncthreads();
         if constexpr (decltype(load_next)::value) load_tile_row(P, xs, P.r0 + lr + 2, gcA, okA, hc, tr);
         if (live) {
@@ -1665,7 +1672,7 @@ k_march(S P, XS xs, int nchunks, Epi epi, BS bs = BS{}) {
     step(lb - 1, std::false_type{});
 }
 
-// ---- direct kernel for the pressure-side stencils (D, G, Gt_G; one GPU) ----
+// ---- direct kernel for the pressure-side stencils (D, G, Gt_G) ----
 // One thread per cell, no LDS and no barrier: the stencil reads its neighbours straight from global memory (the
 // 8 MB pressure vectors and the thn table stay L2-resident), so a launch is n^2 / 256 independent workgroups at
 // full occupancy instead of one round of marching workgroups.  Same accessors' values, same row arithmetic.
@@ -1675,11 +1682,14 @@ k_march(S P, XS xs, int nchunks, Epi epi, BS bs = BS{}) {
 #define MPBP_PG_DIRECT 1
 #endif
 int g_pg_direct = MPBP_PG_DIRECT;
+// (lr: the thread's local row in the partition layout, gr: the same row's wrapped global index -- the row the
+// stencil's accessors are called around; a neighbour row r maps to local row lr + (r - gr))
 template <class S, class XS>
 struct XDirect {
     const S& P;
     const XS& xs;
-    __device__ double X(int f, int r, int c) const { return xs(P.xrow(f, r) + P.wrap(c)); }
+    int lr, gr;
+    __device__ double X(int f, int r, int c) const { return xs(P.xrow(f, P.r0 + lr + (r - gr)) + P.wrap(c)); }
 };
 struct TDirect {
     const double* __restrict__ cell;
@@ -1690,19 +1700,22 @@ struct TDirect {
         return sph ? 1.0 - v : v;
     }
 };
+// Rows [la, la + rows) of the partition (which = 2: rows 0 and L - 1), one thread per (row, column).
 template <class S, class XS, class Epi>
-__global__ void __launch_bounds__(256) k_direct(S P, XS xs, Epi epi) {
+__global__ void __launch_bounds__(256) k_direct(S P, XS xs, Epi epi, int la, int rows) {
     constexpr int NO = S::NOUT;
     const int n = P.n;
     const int64_t t = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
-    const bool live = t < (int64_t)n * n;
+    const bool live = t < (int64_t)rows * n;
     const int tt = live ? (int)t : 0;
-    const int gr = tt / n, gc = tt - gr * n;
+    const int li = tt / n, gc = tt - li * n;
+    const int lr = P.which == 2 ? (li == 0 ? 0 : P.L - 1) : la + li;
+    const int gr = P.wrap(P.r0 + lr);
     typename Epi::P pe[NO];
 #pragma unroll
-    for (int o = 0; o < NO; ++o) pe[o] = epi.pre_lite(P.out_row(o, gr, gc));
+    for (int o = 0; o < NO; ++o) pe[o] = epi.pre_lite(P.out_row(o, lr, gc));
     const typename S::Cell cl = P.cell_pre(gr, gc);
-    const XDirect<S, XS> xa{P, xs};
+    const XDirect<S, XS> xa{P, xs, lr, gr};
     const TDirect ta{P.cell, n};
     const bool edge = __builtin_amdgcn_readfirstlane(__any(gr == 0 || gr == n - 1 || gc == 0 || gc == n - 1)) != 0;
     if (!live) return;
@@ -1713,7 +1726,7 @@ __global__ void __launch_bounds__(256) k_direct(S P, XS xs, Epi epi) {
                                 : P.template row<false>(o, gr, gc, ta, xa, &dg, cl);
         set_diag(pe[o], dg);
         set_x(pe[o], xa.X(S::NF == 1 ? 0 : o, gr, gc));
-        epi(P.out_row(o, gr, gc), acc, pe[o]);
+        epi(P.out_row(o, lr, gc), acc, pe[o]);
     }
 }
 
@@ -1731,9 +1744,9 @@ struct InitRow {
     double xa[NF], h0[NF];   // b at the lane's main column and (lanes 0, 1) its halo column
     Stage sa, sh;            // the stencil's per-point operands for the diagonal (F: the u/v face thn)
 };
-template <int NF, class Stage>
-struct InitRow<NF, Stage, GxB> {
-    GxB::Q qa, qh;           // b recomputed from x_p (GxB): its operands at the main and the halo column
+template <int NF, class Stage, bool PT>
+struct InitRow<NF, Stage, GxBT<PT>> {
+    typename GxBT<PT>::Q qa, qh;   // b recomputed from x_p (GxB): its operands at the main and the halo column
     Stage sa, sh;
 };
 struct ThnRow {
@@ -1760,9 +1773,9 @@ template <class S, class BS>
 __device__ inline void load_init_row(const S& P, const double* __restrict__ b, int gr, int gcA, bool okA,
                                      const HaloCols& hc, InitRow<S::NF, typename S::Stage, BS>& tr, const BS& bs) {
     const int ca = okA ? gcA : 0;
-    if constexpr (BS::on) {
-        tr.qa = bs.load(P.wrap(gr), ca);
-        tr.qh = bs.load(P.wrap(gr), hc.gl);
+    if constexpr (BS::on) {   // (gr: the unwrapped global row; its local row is gr - r0)
+        tr.qa = bs.load(gr - P.r0, P.wrap(gr), ca);
+        tr.qh = bs.load(gr - P.r0, P.wrap(gr), hc.gl);
     } else {
 #pragma unroll
         for (int f = 0; f < S::NF; ++f) {
@@ -1862,7 +1875,7 @@ k_march_init(S P, const double* __restrict__ b, double c2, int nchunks, Epi epi,
 #pragma unroll
         for (int o = 0; o < NO; ++o) pe[o] = epi.pre_lite(P.out_row(o, lr, gcl));
         const typename S::Cell cl = P.cell_pre(grow(lr), gcl);
-        const typename BS::Q bq = bs.load(grow(lr), gcl);
+        const typename BS::Q bq = bs.load(lr, grow(lr), gcl);
         __syncthreads();
         if constexpr (decltype(load_next)::value) {   // thn row lr+3 first: it is stored at the end of this step
             load_thn_row(P, P.r0 + lr + 3, colA, tid, c0, tn);
@@ -1928,9 +1941,14 @@ int64_t march_chunks(const S& P, int rows_per_block, int64_t capacity) {
 template <class S, class XS, class Epi, class BS = BNone>
 int launch_march_fixed(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStream_t st, const BS& bs = BS{}) {
     if constexpr (!std::is_base_of_v<FStencilDev, S> && !BS::on) {   // D, G, Gt_G on one GPU: the direct kernel
-        if (g_pg_direct && P.which == 0 && P.h == 0) {
-            const int64_t cells = (int64_t)P.n * P.n;
-            k_direct<S, XS, Epi><<<(unsigned)((cells + 255) / 256), 256, 0, st>>>(P, xs, epi);
+        if (g_pg_direct) {
+            // rows as march_rows: 0 all owned, 1 rows 1 .. L-2, 2 rows 0 and L-1, 3 owned + ext ghost rows each side
+            const int la = P.which == 1 ? 1 : P.which == 3 ? -P.ext : 0;
+            const int lb = P.which == 1 ? P.L - 1 : P.which == 3 ? P.L + P.ext : P.L;
+            const int rows = P.which == 2 ? (P.L >= 2 ? 2 : 1) : lb - la;
+            if (rows <= 0) return MPBP_OK;
+            const int64_t cells = (int64_t)rows * P.n;
+            k_direct<S, XS, Epi><<<(unsigned)((cells + 255) / 256), 256, 0, st>>>(P, xs, epi, la, rows);
             MPBP_HIP(hipGetLastError());
             return MPBP_OK;
         }
@@ -3408,6 +3426,55 @@ int ca_inner_solve(const Ctx& c, int32_t sop, const double* b, const double* dia
     return MPBP_OK;
 }
 
+// The CA schedule's second F solve (owned rows) with W = G x_p recomputed inside its sweeps (GxB over x_p's ghost
+// layout, which holds S_F + 1 ghost rows each side -- the G launch's d_W = S_F plus its one-row reach): no G launch
+// and no W buffer; the same IEEE operations per row as ca_inner_solve after the G launch.
+int ca_f_solve_gx(const Ctx& c, const double* xp, const mpbp_inner_solver& in, double* dst, const double* sub,
+                  double* ping, double* pong, double* dir, bool profile) {
+    const mpbp_schur_plan* p = c.p;
+    const int K = in.sweeps;
+    if (in.kind != MPBP_INNER_CHEBYSHEV || K < 2 || K > 64 || !(in.lmax > in.lmin) || !(in.lmin >= 0.0))
+        return set_error(MPBP_ERR_ARG, "schur_apply (CA, fused G): needs a Chebyshev F solve of 2..64 sweeps");
+    double c1[64] = {}, c2[64] = {};
+    cheb_coeffs(in.lmin, in.lmax, K, c1, c2);
+    PGDev G;
+    int rc = make_pgstencil(&p->f_prm, p->f_cell, &p->p_part, &G);
+    if (rc) return rc;
+    const GxBPart bs{xp, G.d_p, G.inv, G.minv, G.n, G.L, G.h};
+    auto fpol = [&](int ext, FStencilDev* P) {
+        const mpbp_row_part q = stencil_part(ext_op(p, SOP_F, ext));
+        return make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, P);
+    };
+    FStencilDev P;
+    if ((rc = fpol(K - 2, &P))) return rc;
+    double* cur = K == 2 ? dst : pong;
+    rc = with_f_identities(P, [&](const auto& Q) {
+        return launch_march_init(Q, nullptr, c2[0], EpiChebFirst{nullptr, dir, c1[1], c2[1], K == 2 ? sub : nullptr, cur,
+                                                                 K == 2 ? 0 : 1}, g_march_rows, c.st, bs);
+    });
+    if (rc) return rc;
+    for (int s = 2; s < K; ++s) {
+        const bool last = s == K - 1;
+        double* nxt = last ? dst : (cur == ping ? pong : ping);
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        const bool rec = profile && p->prof_events && p->prof_count && *p->prof_count < p->prof_capacity &&
+                         hipStreamIsCapturing(c.st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone;
+        if (rec) MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count], c.st));
+        if ((rc = fpol(K - 1 - s, &P))) return rc;
+        rc = with_f_identities(P, [&](const auto& Q) {
+            return launch_march(Q, XPlain{cur}, EpiCheb{cur, nullptr, nullptr, dir, c1[s], c2[s], last ? sub : nullptr,
+                                                        nxt, last ? 0 : 1}, g_march_rows, c.st, bs);
+        });
+        if (rc) return rc;
+        if (rec) {
+            MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count + 1], c.st));
+            ++*p->prof_count;
+        }
+        cur = nxt;
+    }
+    return MPBP_OK;
+}
+
 // The exchange of one vector, complete before the next launch.
 void ca_exchange(const Ctx& c, int32_t kind, double* x_ext) {
     c.p->halo(c.p->halo_ctx, kind, x_ext, MPBP_HALO_BEGIN, (void*)c.st);
@@ -3457,6 +3524,9 @@ int schur_apply_ca(const Ctx& c, const double* v, double* out) {
     rc = ca_inner_solve(c, SOP_GTG, Pxb, p->diag_P_ext, p->inner_P, p->np_ext, Pxp, nullptr, P0, P1, Pd, d_xp, false);
     if (rc) return rc;
     MPBP_HIP(hipMemcpyAsync(out + p->nu, Pxp, sizeof(double) * (size_t)p->np, hipMemcpyDeviceToDevice, c.st));
+    // 6.+7. fused: the second F solve recomputes G x_p in its sweeps (Chebyshev F)   solve.py:273-276
+    if (p->fuse_g && p->inner_F.kind == MPBP_INNER_CHEBYSHEV && p->inner_F.sweeps >= 2)
+        return ca_f_solve_gx(c, Pxp, p->inner_F, out, Y, U0, U1, Ud, true);
     // 6. G x_p on owned + d_W ghost rows (into v's velocity buffer)          solve.py:273
     rc = op_spmv(ext_op(p, SOP_G, d_W), MPBP_SPMV_STORE, Pxp, nullptr, Vu, c.st);
     if (rc) return rc;

@@ -239,7 +239,7 @@ class DistributedSchurPreconditioner(PlanProfiling):
 
     def __init__(self, n, xi, eta_n, eta_s, c=1.0, d_u=-1.0, inner_F=None, inner_P=None, group=None,
                  device=None, layout="sell", f_mode="auto", pg_mode="auto", halo="auto", self_halo=False,
-                 halo_overlap=False, ca="auto"):
+                 halo_overlap=False, ca="auto", fuse_g=True):
         import torch.distributed as dist
         from .preconditioner import MultiphaseBlockPreconditioner
         from .solve import InnerSolver
@@ -292,6 +292,8 @@ class DistributedSchurPreconditioner(PlanProfiling):
                 raise ValueError(f"ca=True needs {max(hu, hp)} grid rows per rank, the smallest has {part.min_rows}")
         elif ca is True:
             raise ValueError("ca=True needs a row partition and the matrix-free F, D, G, Gt_G")
+        # CA schedule: the second F solve recomputes G x_p inside its sweeps from x_p's ghost rows (no G launch)
+        self.fuse_g = bool(fuse_g and self.ca and self.inner_F.kind == "chebyshev" and self.inner_F.sweeps >= 2)
         nu, np_ = part.n_owned(N_VEL_FIELDS), part.n_owned(N_P_FIELDS)
         nu_ext, np_ext = part.n_ext(N_VEL_FIELDS, self.h_u), part.n_ext(N_P_FIELDS, self.h_p)
         cm_u = torch.from_numpy(part.colmap(N_VEL_FIELDS, self.h_u)).to(dev)
@@ -402,6 +404,7 @@ class DistributedSchurPreconditioner(PlanProfiling):
         # then one launch per sweep
         p.halo_first = 1 if (self._rccl is not None and not self._rccl.overlap) else 0
         p.ca, p.ca_reach_q = (1 if self.ca else 0), self.ca_q
+        p.fuse_g = 1 if self.fuse_g else 0
         if self.ca:
             if self._rccl is not None and not self._rccl.overlap:   # v's two halves in one RCCL group
                 p.halo_pair = self._rccl.pair_fn

@@ -20,7 +20,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, layout, f_mode, kind, errfile, ca="auto"):
+def _worker(rank, world, port, n, layout, f_mode, kind, errfile, ca="auto", fuse_g=True):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         torch.cuda.set_device(0)
@@ -30,7 +30,8 @@ def _worker(rank, world, port, n, layout, f_mode, kind, errfile, ca="auto"):
         mpb.lib().mpbp_set_march_rows(kind)
         iF, iP = mpb.InnerSolver("chebyshev", 4), mpb.InnerSolver("chebyshev", 3)
         dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, layout=layout,
-                                             f_mode=f_mode, ca=ca)
+                                             f_mode=f_mode, ca=ca, fuse_g=fuse_g)
+        assert dpc.fuse_g == bool(fuse_g and dpc.ca)
         assert (dpc.f_stencil is not None) == (f_mode != "assembled")
         if ca is True:
             assert dpc.ca and dpc.h_u == dpc.ca_q + 2 + 1 + 3, (dpc.h_u, dpc.ca_q)
@@ -67,16 +68,19 @@ def test_distributed_apply_matches_single_gpu(world, n, layout, f_mode, kind, tm
         pytest.fail(f"distributed worker failed:\n{msg}")
 
 
-@pytest.mark.parametrize("world,n,layout,ca", [(2, 64, "sell", True), (2, 64, "sell", False), (3, 50, "csr", True),
-                                              (4, 40, "sell", True)])
-def test_distributed_apply_ca_schedule(world, n, layout, ca, tmp_path):
-    """The communication-avoiding schedule (2 exchanges per apply, ghost rows recomputed) and the per-sweep
-    one, 2-4 gloo ranks on one GPU, bit for bit against the single-GPU apply."""
+@pytest.mark.parametrize("world,n,layout,ca,fuse_g", [(2, 64, "sell", True, True), (2, 64, "sell", False, True),
+                                                     (3, 50, "csr", True, True), (4, 40, "sell", True, True),
+                                                     (2, 64, "sell", True, False), (3, 50, "sell", True, False)])
+def test_distributed_apply_ca_schedule(world, n, layout, ca, fuse_g, tmp_path):
+    """The communication-avoiding schedule (2 exchanges per apply, ghost rows recomputed; the second F solve with
+    G x_p recomputed from x_p's ghost rows, and with the G launch) and the per-sweep one, 2-4 gloo ranks on one
+    GPU, bit for bit against the single-GPU apply."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     errfile = str(tmp_path / "err.txt")
     try:
-        mp.spawn(_worker, args=(world, _free_port(), n, layout, "stencil", 4, errfile, ca), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), n, layout, "stencil", 4, errfile, ca, fuse_g), nprocs=world,
+                 join=True)
     except Exception:
         msg = open(errfile).read() if os.path.exists(errfile) else ""
         pytest.fail(f"distributed worker failed:\n{msg}")
