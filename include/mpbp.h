@@ -406,6 +406,16 @@ int mpbp_event_create(void** ev);
 int mpbp_event_destroy(void* ev);
 int mpbp_event_elapsed_ms(void* start, void* stop, float* ms);
 
+/* ---- FGMRES orthogonalisation (the outer Krylov loop of solve.py:285, pyamg.krylov.fgmres) ---------------- */
+/* h[0:k] = V w with V the k Krylov basis vectors of n doubles at row stride ld (device; 1 <= k <= 256).
+ * part: device scratch of mpbp_gs_part_size(n, k) doubles.  Deterministic (fixed reduction order). */
+int mpbp_gs_dot(const double* V, int64_t ld, int32_t k, const double* w, int64_t n, double* part, double* h,
+                void* stream);
+int64_t mpbp_gs_part_size(int64_t n, int32_t k);
+/* w_out = w - V^T h (w_out may alias w). */
+int mpbp_gs_update(const double* V, int64_t ld, int32_t k, const double* h, const double* w, int64_t n, double* w_out,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -155,6 +155,9 @@ _SIGNATURES = {
     "mpbp_event_create": ([POINTER(c_void_p)], c_int),
     "mpbp_event_destroy": ([_P], c_int),
     "mpbp_event_elapsed_ms": ([_P, _P, POINTER(ctypes.c_float)], c_int),
+    "mpbp_gs_dot": ([_P, c_int64, c_int32, _P, c_int64, _P, _P, _P], c_int),
+    "mpbp_gs_part_size": ([c_int64, c_int32], c_int64),
+    "mpbp_gs_update": ([_P, c_int64, c_int32, _P, _P, c_int64, _P, _P], c_int),
 }
 
 _lib = None

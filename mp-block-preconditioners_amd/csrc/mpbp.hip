@@ -2573,6 +2573,97 @@ int mpbp_event_elapsed_ms(void* start, void* stop, float* ms) {
 
 }  // extern "C"
 
+// ================================================= Krylov orthogonalisation ====
+// FGMRES's classical Gram-Schmidt passes over the Krylov basis V (k vectors of n doubles, row stride ld):
+// h = V w (mpbp_gs_dot) and w_out = w - V^T h (mpbp_gs_update).  rocBLAS's gemv over a k x 5 M row-major basis
+// streams at ~2 TB/s; these stream V once per pass at HBM speed.  Deterministic: the dot products are per-chunk
+// partial sums (each workgroup's in a fixed tree order) added chunk after chunk by one thread per vector.
+namespace {
+constexpr int kGsVec = 8;      // basis vectors per dot-product workgroup
+constexpr int kGsPer = 16;     // elements per thread per chunk
+constexpr int kGsChunk = kBlock * kGsPer;
+__global__ void __launch_bounds__(kBlock) k_gs_dot(const double* __restrict__ V, int64_t ld, int k,
+                                                   const double* __restrict__ w, int64_t n, double* part) {
+    const int64_t c = blockIdx.x;
+    const int i0 = blockIdx.y * kGsVec;
+    const int nv = min(kGsVec, k - i0);
+    double acc[kGsVec];
+#pragma unroll
+    for (int v = 0; v < kGsVec; ++v) acc[v] = 0.0;
+#pragma unroll 4
+    for (int u = 0; u < kGsPer; ++u) {
+        const int64_t e = c * kGsChunk + u * kBlock + threadIdx.x;
+        if (e < n) {
+            const double we = w[e];
+#pragma unroll
+            for (int v = 0; v < kGsVec; ++v)
+                if (v < nv) acc[v] += V[(int64_t)(i0 + v) * ld + e] * we;
+        }
+    }
+    __shared__ double red[kGsVec][kBlock / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int v = 0; v < kGsVec; ++v) {
+        double a = acc[v];
+        for (int off = 32; off > 0; off >>= 1) a += __shfl_down(a, off, 64);
+        if (lane == 0) red[v][wv] = a;
+    }
+    __syncthreads();
+    if (threadIdx.x < nv) {
+        double a = 0.0;
+        for (int q = 0; q < kBlock / 64; ++q) a += red[threadIdx.x][q];
+        part[c * k + i0 + threadIdx.x] = a;
+    }
+}
+__global__ void k_gs_sum(const double* part, int64_t nchunks, int k, double* h) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k) return;
+    double a = 0.0;
+    for (int64_t c = 0; c < nchunks; ++c) a += part[c * k + i];
+    h[i] = a;
+}
+__global__ void __launch_bounds__(kBlock) k_gs_update(const double* __restrict__ V, int64_t ld, int k,
+                                                      const double* __restrict__ h, const double* __restrict__ w,
+                                                      int64_t n, double* __restrict__ wo) {
+    __shared__ double hs[256];
+    for (int i = threadIdx.x; i < k; i += kBlock) hs[i] = h[i];
+    __syncthreads();
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= n) return;
+    double a = 0.0;
+    for (int i = 0; i < k; ++i) a += V[(int64_t)i * ld + e] * hs[i];
+    wo[e] = w[e] - a;
+}
+}  // namespace
+
+extern "C" {
+
+int mpbp_gs_dot(const double* V, int64_t ld, int32_t k, const double* w, int64_t n, double* part, double* h,
+                void* stream) {
+    if (!V || !w || !h || !part || k < 1 || k > 256 || n < 1 || ld < n)
+        return set_error(MPBP_ERR_ARG, "gs_dot: bad args (1 <= k <= 256, ld >= n)");
+    const int64_t nchunks = (n + kGsChunk - 1) / kGsChunk;
+    const dim3 grid((unsigned)nchunks, (unsigned)((k + kGsVec - 1) / kGsVec));
+    k_gs_dot<<<grid, kBlock, 0, as_stream(stream)>>>(V, ld, k, w, n, part);
+    MPBP_HIP(hipGetLastError());
+    k_gs_sum<<<grid_for(k), kBlock, 0, as_stream(stream)>>>(part, nchunks, k, h);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int64_t mpbp_gs_part_size(int64_t n, int32_t k) { return ((n + kGsChunk - 1) / kGsChunk) * (int64_t)k; }
+
+int mpbp_gs_update(const double* V, int64_t ld, int32_t k, const double* h, const double* w, int64_t n, double* w_out,
+                   void* stream) {
+    if (!V || !w || !h || !w_out || k < 1 || k > 256 || n < 1 || ld < n)
+        return set_error(MPBP_ERR_ARG, "gs_update: bad args (1 <= k <= 256, ld >= n)");
+    k_gs_update<<<grid_for(n), kBlock, 0, as_stream(stream)>>>(V, ld, k, h, w, n, w_out);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+}  // extern "C"
+
 // ============================================================== SELL ABI ====
 extern "C" {
 
@@ -3176,7 +3267,17 @@ int mg_smooth(const OpRef& o, int32_t nrows, const double* diag, double lmin, do
     double* x = *cur;
     double* other = alt;
     int s = 0;
-    if (zero) {
+    if (zero && K >= 2 && o.stencil && !o.stencil->halo && o.which == 0 && (o.sop == SOP_F || o.sop == SOP_GTG)) {
+        // whole-grid stencil level (level 0 of the Schur apply's hierarchies): the first sweep stages
+        // x0 = d0 = c2[0] b / diag itself (op_first_sweep, as the Chebyshev inner solve): no init launch, same bits
+        double* out1 = K == 2 ? (dst ? dst : other) : other;
+        const int rc = op_first_sweep(o, true, b, diag, c2[0], c1[1], c2[1], d, K == 2 ? sub : nullptr, out1, st,
+                                      K == 2 ? 0 : 1);
+        if (rc) return rc;
+        other = x;
+        x = out1;
+        s = 2;
+    } else if (zero) {
         double* out0 = K == 1 ? (dst ? dst : other) : x;
         int rc = mpbp_cheb_init(nrows, b, diag, c2[0], d, K == 1 ? sub : nullptr, out0, (void*)st);
         if (rc) return rc;

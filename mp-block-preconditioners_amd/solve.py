@@ -366,8 +366,9 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
     and the iteration count otherwise.  ``callback(xk)`` receives the current iterate as a CUDA
     tensor after every inner iteration (the reference's true-residual printer, solve.py:161-170).
     Orthogonalisation is classical Gram-Schmidt with one re-orthogonalisation pass (CGS2: two
-    batched GEMVs per iteration instead of j dependent dot products).  pyamg is not installed
-    here, so iteration counts against pyamg itself are unpinned.
+    batched projections per iteration instead of j dependent dot products), each pass one sweep over
+    the basis through libmpbp's mpbp_gs_dot / mpbp_gs_update (HBM-speed, deterministic reductions).
+    pyamg is not installed here, so iteration counts against pyamg itself are unpinned.
     """
     Aop = _as_operator(A)
     Mop = _as_operator(M)
@@ -386,6 +387,21 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
         return x, 0
     target = tol * normr if normr != 0.0 else tol
     it = 0
+    use_gs = b.is_cuda and b.dtype == torch.float64 and m + 1 <= 256
+    if use_gs:
+        part = torch.empty(int(lib().mpbp_gs_part_size(n, m + 1)), dtype=torch.float64, device=b.device)
+        hbuf = torch.empty(2, m + 1, dtype=torch.float64, device=b.device)
+
+    def project(Vk, w, k, slot):
+        """(h, w - Vk^T h) with h = Vk w for the first k basis vectors."""
+        if not use_gs:
+            h = Vk @ w
+            return h, w - Vk.T @ h
+        hv = hbuf[slot]
+        check(lib().mpbp_gs_dot(ptr(Vk), n, k, ptr(w), n, ptr(part), ptr(hv), stream_handle()))
+        check(lib().mpbp_gs_update(ptr(Vk), n, k, ptr(hv), ptr(w), n, ptr(w), stream_handle()))
+        return hv[:k].clone(), w
+
     while it < maxiter:
         beta = normr
         V = torch.zeros(m + 1, n, dtype=b.dtype, device=b.device)
@@ -398,11 +414,9 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
         k = 0
         for j in range(m):
             Z[j] = Mop(V[j]) if Mop is not None else V[j]
-            w = Aop(Z[j])
-            h = V[: j + 1] @ w
-            w = w - V[: j + 1].T @ h
-            h2 = V[: j + 1] @ w
-            w = w - V[: j + 1].T @ h2
+            w = Aop(Z[j]).contiguous()
+            h, w = project(V[: j + 1], w, j + 1, 0)
+            h2, w = project(V[: j + 1], w, j + 1, 1)
             hcol = (h + h2).cpu().numpy()
             hn = float(torch.linalg.vector_norm(w))
             H[: j + 1, j] = hcol

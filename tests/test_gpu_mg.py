@@ -160,12 +160,15 @@ def _oracle_mg_apply(S, pc, v):
 
 
 @pytest.mark.parametrize("n", [16, 64])
+@pytest.mark.parametrize("pre", [2, 3, 1])
 @pytest.mark.parametrize("layout,f_mode,pg_mode", [("sell", "auto", "auto"), ("csr", "assembled", "assembled")])
-def test_schur_apply_mg_bit_exact(n, layout, f_mode, pg_mode):
+def test_schur_apply_mg_bit_exact(n, layout, f_mode, pg_mode, pre):
+    """The Schur apply with multigrid inner solves vs the oracle; with matrix-free level-0 operators the first
+    pre-smoothing sweep stages its x0 itself (no init launch) -- pre = 2, 3 take that path, pre = 1 the init."""
     mp = _mp()
     _, (A, F, D, G), S = _system(n)
-    inner = mp.InnerSolver("mg", 1)
-    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=inner, inner_P=mp.InnerSolver("mg", 2), layout=layout,
+    inner = mp.InnerSolver("mg", 1, pre=pre)
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=inner, inner_P=mp.InnerSolver("mg", 2, pre=pre), layout=layout,
                                       f_mode=f_mode, pg_mode=pg_mode)
     if f_mode == "auto":
         assert pc.f_stencil is not None and pc.pg_stencil is not None   # level 0 runs matrix-free

@@ -414,3 +414,27 @@ def test_host_vector_length_checked():
     assert np.array_equal(A @ x, A.matvec(_cuda(x)).cpu().numpy())
     pc.release_staging()
     assert np.array_equal(pc.matvec(x), pc.apply(_cuda(x)).cpu().numpy())
+
+
+@pytest.mark.parametrize("k,n", [(1, 1000), (8, 4096), (37, 100003), (151, 5000)])
+def test_gram_schmidt_kernels(k, n):
+    """FGMRES's projections (mpbp_gs_dot: h = V w; mpbp_gs_update: w - V^T h) against torch's fp64 GEMVs, and
+    deterministic: two runs give the same bits."""
+    from mp_block_preconditioners_amd._lib import check, lib, ptr, stream_handle
+    g = torch.Generator(device="cuda").manual_seed(k)
+    V = torch.randn(k + 3, n, dtype=torch.float64, device="cuda", generator=g)   # extra rows: only k are read
+    w = torch.randn(n, dtype=torch.float64, device="cuda", generator=g)
+    part = torch.empty(int(lib().mpbp_gs_part_size(n, k)), dtype=torch.float64, device="cuda")
+    h = torch.empty(k, dtype=torch.float64, device="cuda")
+    check(lib().mpbp_gs_dot(ptr(V), n, k, ptr(w), n, ptr(part), ptr(h), stream_handle()))
+    ref = V[:k] @ w
+    assert float((h - ref).abs().max() / ref.abs().max()) < 1e-13
+    h2 = torch.empty_like(h)
+    check(lib().mpbp_gs_dot(ptr(V), n, k, ptr(w), n, ptr(part), ptr(h2), stream_handle()))
+    assert torch.equal(h, h2)
+    wo = torch.empty_like(w)
+    check(lib().mpbp_gs_update(ptr(V), n, k, ptr(h), ptr(w), n, ptr(wo), stream_handle()))
+    want = w - V[:k].T @ h
+    assert float((wo - want).abs().max() / want.abs().max()) < 1e-13
+    check(lib().mpbp_gs_update(ptr(V), n, k, ptr(h), ptr(w), n, ptr(w), stream_handle()))   # in place
+    assert torch.equal(w, wo)

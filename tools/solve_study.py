@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--pre", type=int, default=2)
     ap.add_argument("--post", type=int, default=2)
     ap.add_argument("--coarsest", type=int, default=16)
+    ap.add_argument("--smooth-ratio", type=float, default=4.0)
     ap.add_argument("--tol", type=float, default=1e-8)
     ap.add_argument("--maxiter", type=int, default=150)
     ap.add_argument("--reps", type=int, default=10)
@@ -43,7 +44,7 @@ def main():
     import mp_block_preconditioners_amd as mp
     if args.sell_wide is not None:
         mp._lib.check(mp.lib().mpbp_set_sell_wide_slices(args.sell_wide))
-    mgkw = dict(pre=args.pre, post=args.post, coarsest=args.coarsest)
+    mgkw = dict(pre=args.pre, post=args.post, coarsest=args.coarsest, smooth_ratio=args.smooth_ratio)
     for n in args.n:
         for eta_n in args.eta_n:
             bp = mp.MultiphaseBlockPreconditioner(n, 1.0, eta_n, 1.0)
@@ -78,7 +79,8 @@ def main():
                 err = float(np.max(np.abs(x.cpu().numpy()[: 4 * n * n] - u[: 4 * n * n])))
                 levels = {k: (m.sizes if m is not None else None) for k, m in (("F", M.mg_F), ("P", M.mg_P))}
                 nnz = {k: ([op.nnz for op in m.ops] if m is not None else None) for k, m in (("F", M.mg_F), ("P", M.mg_P))}
-                print(json.dumps({"tag": args.tag, "coarsest": args.coarsest, "n": n, "eta_n": eta_n, "combo": combo, "iterations": len(hist) - 1,
+                print(json.dumps({"tag": args.tag, "coarsest": args.coarsest, "pre": args.pre, "post": args.post,
+                                  "smooth_ratio": args.smooth_ratio, "n": n, "eta_n": eta_n, "combo": combo, "iterations": len(hist) - 1,
                                   "converged": info == 0, "solve_s": el, "setup_s": setup, "apply_ms": apply_ms,
                                   "ms_per_iteration": el / max(1, len(hist) - 1) * 1e3, "true_rel_residual": res,
                                   "velocity_max_error": err, "mg_levels": levels, "mg_nnz": nnz,
