@@ -358,7 +358,8 @@ def _as_operator(A):
     raise TypeError(f"unsupported operator {type(A)}")
 
 
-def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=None, residuals=None):
+def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=None, residuals=None,
+           capture_M=True):
     """Flexible GMRES with right preconditioning, all vectors in HBM.
 
     Same call shape as pyamg.krylov.fgmres (solve.py:207, 237, 285): convergence when the
@@ -369,9 +370,22 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
     batched projections per iteration instead of j dependent dot products), each pass one sweep over
     the basis through libmpbp's mpbp_gs_dot / mpbp_gs_update (HBM-speed, deterministic reductions).
     pyamg is not installed here, so iteration counts against pyamg itself are unpinned.
+    capture_M: an ApproxSchurPreconditioner M is captured once into a hipGraph and replayed per iteration (its
+    launches -- hundreds with multigrid inner solves -- then cost one graph launch; the iteration's host work never
+    starves the GPU); same results as eager applies.
     """
     Aop = _as_operator(A)
     Mop = _as_operator(M)
+    b_dev = b if isinstance(b, torch.Tensor) else None
+    if capture_M and isinstance(M, ApproxSchurPreconditioner) and (b_dev is None or b_dev.is_cuda):
+        m_in = torch.zeros(M.shape[0], dtype=torch.float64, device=M.device)
+        m_out = torch.empty_like(m_in)
+        m_graph = M.capture(m_in, m_out)
+
+        def Mop(x, out=None, _g=m_graph, _i=m_in, _o=m_out):   # noqa: F811
+            _i.copy_(x)
+            _g.replay()
+            return _o
     b = b if isinstance(b, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(b, dtype=np.float64)).cuda()
     n = b.numel()
     x = torch.zeros_like(b) if x0 is None else (

@@ -204,3 +204,21 @@ def test_fgmres_iterations_drop_with_mg():
             err = np.max(np.abs(x.cpu().numpy()[: 4 * n * n] - u[: 4 * n * n]))
             assert err < 5e-3   # O(h^2) discretisation error of the manufactured solution
     assert its["mg"][0] < 100 and its["mg"][0] < its["cheb4"][0], its
+
+
+def test_fgmres_captured_preconditioner_matches_eager():
+    """fgmres replays a hipGraph of the preconditioner apply (capture_M, default): the residual history and the
+    solution equal those with eager applies bit for bit (the apply is deterministic, the projections too)."""
+    mp = _mp()
+    n = 32
+    _, (A, F, D, G), _ = _system(n)
+    u, b = mp.manufactured_problem(n, etan=100.0, etas=1.0)
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("mg", 1), inner_P=mp.InnerSolver("mg", 1))
+    out = {}
+    for cap in (True, False):
+        hist = []
+        x, info = mp.fgmres(A, _cuda(b), M=pc, tol=1e-8, maxiter=60, residuals=hist, capture_M=cap)
+        out[cap] = (x.cpu().numpy(), hist, info)
+    assert out[True][2] == out[False][2] == 0
+    assert out[True][1] == out[False][1]
+    assert np.array_equal(_bits(out[True][0]), _bits(out[False][0]))
