@@ -2581,6 +2581,7 @@ int mpbp_event_elapsed_ms(void* start, void* stop, float* ms) {
 namespace {
 constexpr int kGsVec = 8;      // basis vectors per dot-product workgroup
 constexpr int kGsPer = 16;     // elements per thread per chunk
+constexpr int kGsBatch = 4;    // elements whose loads are issued together
 constexpr int kGsChunk = kBlock * kGsPer;
 __global__ void __launch_bounds__(kBlock) k_gs_dot(const double* __restrict__ V, int64_t ld, int k,
                                                    const double* __restrict__ w, int64_t n, double* part) {
@@ -2590,23 +2591,29 @@ __global__ void __launch_bounds__(kBlock) k_gs_dot(const double* __restrict__ V,
     double acc[kGsVec];
 #pragma unroll
     for (int v = 0; v < kGsVec; ++v) acc[v] = 0.0;
-#pragma unroll 4
-    for (int u = 0; u < kGsPer; ++u) {
-        const int64_t e = c * kGsChunk + u * kBlock + threadIdx.x;
-        if (e < n) {
-            const double we = w[e];
+    for (int u = 0; u < kGsPer; u += kGsBatch) {
+        double wv[kGsBatch], vv[kGsVec][kGsBatch];
 #pragma unroll
-            for (int v = 0; v < kGsVec; ++v)
-                if (v < nv) acc[v] += V[(int64_t)(i0 + v) * ld + e] * we;
+        for (int q = 0; q < kGsBatch; ++q) {   // every load of the batch in flight at once
+            const int64_t e = c * kGsChunk + (int64_t)(u + q) * kBlock + threadIdx.x;
+            const bool ok = e < n;
+            const int64_t ee = ok ? e : 0;
+            wv[q] = ok ? w[ee] : 0.0;
+#pragma unroll
+            for (int v = 0; v < kGsVec; ++v) vv[v][q] = v < nv ? V[(int64_t)(i0 + v) * ld + ee] : 0.0;
         }
+#pragma unroll
+        for (int q = 0; q < kGsBatch; ++q)
+#pragma unroll
+            for (int v = 0; v < kGsVec; ++v) acc[v] += vv[v][q] * wv[q];
     }
     __shared__ double red[kGsVec][kBlock / 64];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv_ = threadIdx.x >> 6;
 #pragma unroll
     for (int v = 0; v < kGsVec; ++v) {
         double a = acc[v];
         for (int off = 32; off > 0; off >>= 1) a += __shfl_down(a, off, 64);
-        if (lane == 0) red[v][wv] = a;
+        if (lane == 0) red[v][wv_] = a;
     }
     __syncthreads();
     if (threadIdx.x < nv) {
@@ -2615,12 +2622,20 @@ __global__ void __launch_bounds__(kBlock) k_gs_dot(const double* __restrict__ V,
         part[c * k + i0 + threadIdx.x] = a;
     }
 }
-__global__ void k_gs_sum(const double* part, int64_t nchunks, int k, double* h) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= k) return;
+// h[i] = the chunk partials of vector i, one workgroup per vector: strided per-thread sums, then a fixed tree.
+__global__ void __launch_bounds__(kBlock) k_gs_sum(const double* part, int64_t nchunks, int k, double* h) {
+    const int i = blockIdx.x;
     double a = 0.0;
-    for (int64_t c = 0; c < nchunks; ++c) a += part[c * k + i];
-    h[i] = a;
+    for (int64_t c = threadIdx.x; c < nchunks; c += kBlock) a += part[c * k + i];
+    for (int off = 32; off > 0; off >>= 1) a += __shfl_down(a, off, 64);
+    __shared__ double red[kBlock / 64];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int q = 0; q < kBlock / 64; ++q) t += red[q];
+        h[i] = t;
+    }
 }
 __global__ void __launch_bounds__(kBlock) k_gs_update(const double* __restrict__ V, int64_t ld, int k,
                                                       const double* __restrict__ h, const double* __restrict__ w,
@@ -2631,7 +2646,15 @@ __global__ void __launch_bounds__(kBlock) k_gs_update(const double* __restrict__
     const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (e >= n) return;
     double a = 0.0;
-    for (int i = 0; i < k; ++i) a += V[(int64_t)i * ld + e] * hs[i];
+    int i = 0;
+    for (; i + 8 <= k; i += 8) {   // 8 basis rows' loads in flight, then added in order
+        double v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = V[(int64_t)(i + q) * ld + e];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a += v[q] * hs[i + q];
+    }
+    for (; i < k; ++i) a += V[(int64_t)i * ld + e] * hs[i];
     wo[e] = w[e] - a;
 }
 }  // namespace
@@ -2646,7 +2669,7 @@ int mpbp_gs_dot(const double* V, int64_t ld, int32_t k, const double* w, int64_t
     const dim3 grid((unsigned)nchunks, (unsigned)((k + kGsVec - 1) / kGsVec));
     k_gs_dot<<<grid, kBlock, 0, as_stream(stream)>>>(V, ld, k, w, n, part);
     MPBP_HIP(hipGetLastError());
-    k_gs_sum<<<grid_for(k), kBlock, 0, as_stream(stream)>>>(part, nchunks, k, h);
+    k_gs_sum<<<k, kBlock, 0, as_stream(stream)>>>(part, nchunks, k, h);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
