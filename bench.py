@@ -175,6 +175,7 @@ def main():
     kp, spp = parse_inner(args.inner_p)
     iF, iP = mp.InnerSolver(kf, sf), mp.InnerSolver(kp, spp)
     A = None
+    t_setup = time.perf_counter()
     if not partitioned:
         bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
         A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
@@ -188,6 +189,8 @@ def main():
                                             layout=args.layout, f_mode=args.f_mode, pg_mode=args.pg_mode,
                                             self_halo=args.self_halo, halo_overlap=args.halo_overlap,
                                             ca=False if args.no_ca else "auto", fuse_g=not args.no_fuse_g)
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t_setup   # assembly, products, layouts, halo plans (the partitioned: per rank)
     gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
     v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda", generator=gen)
     out = torch.empty_like(v)
@@ -314,6 +317,7 @@ def main():
             "config": {"workload": f"{n}x{n} MAC grid, approx-commutator Schur preconditioner apply (BASELINE "
                                    f"{cfg}" + (")" if world == 1 else f", rows partitioned over {world} ranks)"),
                        "applies_per_s_of_this_grid": args.steps / dt,
+                       "setup_seconds": setup_s,
                        "n": n, "unknowns": 5 * n * n, "xi": args.xi, "eta_n": args.eta_n,
                        "eta_s": args.eta_s, "inner_F": f"{kf}:{sf}", "inner_P": f"{kp}:{spp}",
                        "parallelism": f"rows{world}" if world > 1 else "single", "layout": args.layout,

@@ -1,8 +1,5 @@
 #!/bin/bash
-# One-off GPU step (round 2): A/B of the CSR SpMV LDS swizzle (tools/spmv_ab.py per build, interleaved).
+# One-off GPU step (round 2): the N > 1 bench path rehearsed with 2 gloo ranks on one GPU at configs[4]'s 2048^2.
 cd "$GRAFT_REPO_ROOT" || exit 99
-O=gpurun_out/${TAG:-r02z}; mkdir -p $O
-for V in base swz base swz base swz; do
-  L=mp-block-preconditioners_amd/lib/variants/libmpbp_$V.so; [ $V = base ] && L=
-  MPBP_LIB=$L timeout -k 10 120 python tools/spmv_ab.py >> $O/spmv_$V.log 2>&1 || exit 1
-done
+O=gpurun_out/${TAG:-r02aa}; mkdir -p $O
+MPBP_BENCH_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --steps 5 --warmup 2 > $O/rows2_gloo_2048.log 2>&1
