@@ -693,6 +693,42 @@ struct EpiAdd {   // rhs = D Finv_v + v_p   (solve.py:259)
     __device__ void apply(int32_t r, double acc, const P& p) const { st_stream<NT>(y + r, acc + p.z); }
     __device__ void operator()(int32_t r, double acc, const P& p) const { apply<false>(r, acc, p); }
 };
+// The pressure solves' right-hand sides, written with the first Gt_G sweep's staged iterate beside them:
+// y = rhs and x0 = c2 (rhs / diag) -- the value that sweep would otherwise recompute at each staged point (XInit),
+// so the sweep stages x0 from memory (same bits).  EpiAddX0: rhs = D Finv_v + v_p (solve.py:259); EpiStoreX0:
+// x_b = Gt_F_G x_a (solve.py:267).
+struct EpiAddX0 {
+    const double* z;
+    double* y;
+    const double* diag;
+    double c2;
+    double* x0;
+    struct P { double z, pdiag; };
+    __device__ P pre(int32_t r) const { return {ld_stream(z + r), diag[r]}; }
+    __device__ P pre_lite(int32_t r) const { return pre(r); }
+    template <bool NT = false>
+    __device__ void apply(int32_t r, double acc, const P& p) const {
+        const double v = acc + p.z;
+        st_stream<NT>(y + r, v);
+        st_stream<NT>(x0 + r, c2 * (v / p.pdiag));
+    }
+    __device__ void operator()(int32_t r, double acc, const P& p) const { apply<false>(r, acc, p); }
+};
+struct EpiStoreX0 {
+    double* y;
+    const double* diag;
+    double c2;
+    double* x0;
+    struct P { double pdiag; };
+    __device__ P pre(int32_t r) const { return {diag[r]}; }
+    __device__ P pre_lite(int32_t r) const { return pre(r); }
+    template <bool NT = false>
+    __device__ void apply(int32_t r, double acc, const P& p) const {
+        st_stream<NT>(y + r, acc);
+        st_stream<NT>(x0 + r, c2 * (acc / p.pdiag));
+    }
+    __device__ void operator()(int32_t r, double acc, const P& p) const { apply<false>(r, acc, p); }
+};
 struct EpiResid {
     const double* z;
     double* y;
@@ -852,6 +888,10 @@ template <>
 __device__ inline void set_diag<EpiAdd::P>(EpiAdd::P&, double) {}
 template <>
 __device__ inline void set_diag<EpiResid::P>(EpiResid::P&, double) {}
+template <>
+__device__ inline void set_x<EpiAddX0::P>(EpiAddX0::P&, double) {}
+template <>
+__device__ inline void set_diag<EpiAddX0::P>(EpiAddX0::P&, double) {}
 
 // CSR SpMV over the same row blocks, one wavefront per 64-row quarter of a block and no block-wide
 // barrier.  Each wave streams its rows' [row_ptr[ra], row_ptr[rb]) entries in chunks of kWaveCap with
@@ -3385,11 +3425,30 @@ int mg_solve(const mpbp_mg* m, const MgFine& fine, const double* b, double* x_ou
     return MPBP_OK;
 }
 
+// rhs = D Finv_v + v_p with the first Gt_G sweep's x0 = c2 (rhs / diag_P) written beside it (one GPU, matrix-free D).
+int d_rhs_x0(const mpbp_schur_plan* p, const double* Y, const double* v_p, double* rhs, double c2, double* x0,
+             hipStream_t st) {
+    PGDev P;
+    const int rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &P);
+    if (rc) return rc;
+    return launch_march(DStencilDev{P}, XPlain{Y}, EpiAddX0{v_p, rhs, p->diag_P, c2, x0}, pg_rows(), st);
+}
+
+// The first sweep of a Gt_G Chebyshev solve staging a precomputed x0 = d0 (one GPU, matrix-free Gt_G).
+int gtg_first_sweep_x0(const mpbp_schur_plan* p, const double* x0, const double* b, double c1, double c2, double* d,
+                       const double* sub, double* xo, int store_d, hipStream_t st) {
+    PGDev P;
+    const int rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &P);
+    if (rc) return rc;
+    return launch_march(GtGStencilDev{P}, XPlain{x0}, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, pg_rows(), st);
+}
+
 // x = M^-1 b by `inner` sweeps from x0 = 0 (solve.py:251/254 F_inv / Gt_G_factorization roles).
-// The final iterate goes to dst (sub - iterate when sub != NULL); ping/pong hold the others.
+// The final iterate goes to dst (sub - iterate when sub != NULL); ping/pong hold the others.  x0_pre (Gt_G,
+// Chebyshev, fusable first sweep): the first iterate c2[0] b / diag already computed by b's producer.
 int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag, const mpbp_inner_solver& in,
                 int32_t nrows, const double* b, double* dst, const double* sub, double* ping, double* pong,
-                double* dir, bool profile) {
+                double* dir, bool profile, const double* x0_pre = nullptr) {
     if (in.kind == MPBP_INNER_MG) {   // one GPU: V-cycles whose level 0 is this operator
         const mpbp_mg* m = kind == MPBP_VEC_VELOCITY ? c.p->mg_F : c.p->mg_P;
         // (one GPU: op.in covers every row -- the assembled layouts' boundary part is an empty block list)
@@ -3414,8 +3473,11 @@ int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag
     int s = 1, rc = MPBP_OK;
     if (K >= 2 && can_fuse_init(op)) {   // sweep 1 recomputes x0 = d0 from b and diag: no init pass
         double* nxt = K == 2 ? dst : pong;
-        rc = op_first_sweep(op.in, cheb, b, diag, c2[0], c1[1], c2[1], dir, K == 2 ? sub : nullptr, nxt, c.st,
-                            K == 2 ? 0 : 1);
+        rc = (x0_pre && cheb && op.in.sop == SOP_GTG)
+                 ? gtg_first_sweep_x0(c.p, x0_pre, b, c1[1], c2[1], dir, K == 2 ? sub : nullptr, nxt, K == 2 ? 0 : 1,
+                                      c.st)
+                 : op_first_sweep(op.in, cheb, b, diag, c2[0], c1[1], c2[1], dir, K == 2 ? sub : nullptr, nxt, c.st,
+                                  K == 2 ? 0 : 1);
         if (rc) return rc;
         cur = nxt;
         s = 2;
@@ -3695,19 +3757,32 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
     double *Prhs = p->wp[0], *Pxa = p->wp[1], *Pxb = p->wp[2], *Pxp = p->wp[3];
     double *P0 = p->wp[4], *P1 = p->wp[5], *Pd = p->wp[6];
     int rc;
+    // one GPU, matrix-free D and Gt_G, Chebyshev Gt_G solves: b's producers (D, Gt_F_G) also write the first Gt_G
+    // sweep's x0 = c2[0] b / diag into P0 (the solve's ping buffer, first overwritten by its second sweep)
+    const bool px0 = p->pg_stencil && !p->halo && p->inner_P.kind == MPBP_INNER_CHEBYSHEV && p->inner_P.sweeps >= 2 &&
+                     p->inner_P.lmax > p->inner_P.lmin && p->inner_P.lmin >= 0.0 && p->inner_P.sweeps <= 64;
+    double pc1[64] = {}, pc2[64] = {};
+    if (px0) cheb_coeffs(p->inner_P.lmin, p->inner_P.lmax, p->inner_P.sweeps, pc1, pc2);
     // 1. Finv_v = F_inv @ v[:F.shape[1]]                                   solve.py:258
     rc = inner_solve(c, MPBP_VEC_VELOCITY, F, p->diag_F, p->inner_F, p->nu, v_u, Y, nullptr, U0, U1, Ud, true);
     if (rc) return rc;
     // 2. rhs_interim = D @ Finv_v + v[F.shape[1]:]                            solve.py:259
-    rc = two_phase(c, MPBP_VEC_VELOCITY, Y, D,
-                   [&](const OpRef& o) { return op_spmv(o, MPBP_SPMV_ADD, Y, v_p, Prhs, c.st); });
+    if (px0)
+        rc = d_rhs_x0(p, Y, v_p, Prhs, pc2[0], P0, c.st);
+    else
+        rc = two_phase(c, MPBP_VEC_VELOCITY, Y, D,
+                       [&](const OpRef& o) { return op_spmv(o, MPBP_SPMV_ADD, Y, v_p, Prhs, c.st); });
     if (rc) return rc;
     // 3. x_a = Gt_G_factorization @ rhs_interim                             solve.py:265
-    rc = inner_solve(c, MPBP_VEC_PRESSURE, P, p->diag_P, p->inner_P, p->np, Prhs, Pxa, nullptr, P0, P1, Pd, false);
+    rc = inner_solve(c, MPBP_VEC_PRESSURE, P, p->diag_P, p->inner_P, p->np, Prhs, Pxa, nullptr, P0, P1, Pd, false,
+                     px0 ? P0 : nullptr);
     if (rc) return rc;
     // 4. x_b = Gt_F_G @ x_a                                                solve.py:267
     //    (one GPU: the diamond layout when the plan has it)
-    if (p->q13 && !p->halo)
+    const bool qx0 = px0 && p->q13;
+    if (qx0)
+        rc = launch_q13(p->q13_n, p->q13, Pxa, EpiStoreX0{Pxb, p->diag_P, pc2[0], P0}, c.st);
+    else if (p->q13 && !p->halo)
         rc = mpbp_q13_spmv(p->q13_n, p->q13, MPBP_SPMV_STORE, Pxa, nullptr, Pxb, (void*)c.st);
     else
         rc = two_phase(c, MPBP_VEC_PRESSURE, Pxa, Q,
@@ -3716,7 +3791,8 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
     // 5. x_p = Gt_G_factorization @ x_b                                    solve.py:271
     //    (one GPU: straight into the output, which G then reads; a partition needs x_p's ghost rows)
     if (!p->halo) Pxp = out_p;
-    rc = inner_solve(c, MPBP_VEC_PRESSURE, P, p->diag_P, p->inner_P, p->np, Pxb, Pxp, nullptr, P0, P1, Pd, false);
+    rc = inner_solve(c, MPBP_VEC_PRESSURE, P, p->diag_P, p->inner_P, p->np, Pxb, Pxp, nullptr, P0, P1, Pd, false,
+                     qx0 ? P0 : nullptr);
     if (rc) return rc;
     if (Pxp != out_p)
         MPBP_HIP(hipMemcpyAsync(out_p, Pxp, sizeof(double) * (size_t)p->np, hipMemcpyDeviceToDevice, c.st));
