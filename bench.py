@@ -105,8 +105,9 @@ def main():
                     help="D, G, Gt_G: recompute from thn (stencil) or stream the stored operators")
     ap.add_argument("--q-mode", default="auto", choices=["auto", "diamond", "assembled"],
                     help="Gt_F_G: values in the 13-point diamond layout (columns implicit) or the assembled copy")
-    ap.add_argument("--march-rows", type=int, default=4,
-                    help="grid rows per workgroup of the marching stencil kernels (matrix-free F, D, G, Gt_G)")
+    ap.add_argument("--march-rows", type=int, default=0,
+                    help="grid rows per workgroup of the marching stencil kernels (matrix-free F, D, G, Gt_G); "
+                         "0: the count that fills one round of workgroups per launch")
     ap.add_argument("--pg-direct", type=int, default=None, help="1: D / Gt_G sweeps as one thread per cell (no LDS)")
     ap.add_argument("--no-fuse-g", action="store_true",
                     help="launch G x_p separately instead of recomputing it inside the second F solve's sweeps")
@@ -321,7 +322,7 @@ def main():
                        "n": n, "unknowns": 5 * n * n, "xi": args.xi, "eta_n": args.eta_n,
                        "eta_s": args.eta_s, "inner_F": f"{kf}:{sf}", "inner_P": f"{kp}:{spp}",
                        "parallelism": f"rows{world}" if world > 1 else "single", "layout": args.layout,
-                       "f_sweeps": f"matrix-free-march{args.march_rows}" if getattr(pc, "f_stencil", None) is not None
+                       "f_sweeps": f"matrix-free-march{args.march_rows or '-auto'}" if getattr(pc, "f_stencil", None) is not None
                        else "assembled",
                        "d_g_gtg": "matrix-free" if getattr(pc, "pg_stencil", None) is not None else "assembled",
                        "gt_f_g": "diamond-13" if getattr(pc, "q13", None) is not None else args.layout,

@@ -353,8 +353,9 @@ int mpbp_gtg_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell
                                const double* x_in, const double* b, double c1, double c2, double* d,
                                const double* sub, double* x_out, void* stream);
 
-/* Grid rows per workgroup of the marching stencil kernels (matrix-free F, D, G, Gt_G), process-wide; 4 (default)
- * is fastest on MI355X at 1024^2 (one round of workgroups).  Results are bit-identical for every value. */
+/* Grid rows per workgroup of the marching stencil kernels (matrix-free F, D, G, Gt_G), process-wide; 0 (default):
+ * per launch, the count that fills one round of workgroups (4 at 1024^2 on MI355X, 16 at 2048^2, 1 at 256^2 and
+ * 512^2; two rows for a 2048^2 grid split over 8 ranks).  Results are bit-identical for every value. */
 int mpbp_set_march_rows(int32_t rows);
 /* The first sweep of a matrix-free F inner solve stages x0 = c2 b / diag: mode 1 (default) rebuilds diag from the
  * thn tables inside the sweep (no diag stream), mode 0 streams the stored diagonal.  Same bits either way. */

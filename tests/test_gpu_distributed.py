@@ -56,7 +56,8 @@ def _worker(rank, world, port, n, layout, f_mode, kind, errfile, ca="auto", fuse
 @pytest.mark.parametrize("world,n,layout,f_mode,kind", [(2, 64, "sell", "stencil", 4), (2, 64, "sell", "assembled", 4),
                                                         (2, 64, "csr", "assembled", 2), (3, 50, "sell", "stencil", 1),
                                                         (4, 9, "csr", "stencil", 1), (2, 64, "sell", "stencil", 3),
-                                                        (3, 50, "sell", "stencil", 6), (4, 9, "sell", "stencil", 3)])
+                                                        (3, 50, "sell", "stencil", 6), (4, 9, "sell", "stencil", 3),
+                                                        (2, 64, "sell", "stencil", 0), (3, 50, "csr", "stencil", 0)])
 def test_distributed_apply_matches_single_gpu(world, n, layout, f_mode, kind, tmp_path):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")

@@ -33,7 +33,7 @@ def _bits(a, b):
 PARAMS = [(1.0, 100.0, 1.0, 1.0, -1.0, 1.0), (2.5, 1.0e4, 1.0, 0.5, -2.0, 2.5), (1.0, 1.0, 1.0, 0.0, -1.0, -0.75)]
 
 
-@pytest.fixture(params=[(4, 1), (4, 0), (1, 0), (7, 0)], ids=["direct", "march4", "march1", "march7"])
+@pytest.fixture(params=[(0, 1), (0, 0), (4, 0), (1, 0), (7, 0)], ids=["direct", "auto", "march4", "march1", "march7"])
 def march_rows(request):
     """Workgroup shapes of the marching kernels, and the direct one-thread-per-cell kernel for D / G / Gt_G
     (mpbp_set_pg_direct): results must not depend on either."""
@@ -42,7 +42,7 @@ def march_rows(request):
     check(lib().mpbp_set_march_rows(rows))
     check(lib().mpbp_set_pg_direct(direct))
     yield request.param
-    check(lib().mpbp_set_march_rows(4))
+    check(lib().mpbp_set_march_rows(0))
     check(lib().mpbp_set_pg_direct(1))
 
 
