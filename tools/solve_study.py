@@ -36,14 +36,11 @@ def main():
     ap.add_argument("--tol", type=float, default=1e-8)
     ap.add_argument("--maxiter", type=int, default=150)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--sell-wide", type=int, default=None, help="mpbp_set_sell_wide_slices (library default 2048)")
     ap.add_argument("--tag", default="")
     args = ap.parse_args()
     import numpy as np
     import torch
     import mp_block_preconditioners_amd as mp
-    if args.sell_wide is not None:
-        mp._lib.check(mp.lib().mpbp_set_sell_wide_slices(args.sell_wide))
     mgkw = dict(pre=args.pre, post=args.post, coarsest=args.coarsest, smooth_ratio=args.smooth_ratio)
     for n in args.n:
         for eta_n in args.eta_n:
