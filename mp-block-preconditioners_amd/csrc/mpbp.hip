@@ -907,14 +907,8 @@ __device__ inline void set_diag<EpiAddX0::P>(EpiAddX0::P&, double) {}
 // MPBP_CSR_TGATHER=0 selects the earlier order: gather in entry order, stage the products (6 KiB).
 // Measured dead end: no staging at all, each lane loading its own row (16-byte loads 96 B apart across
 // the wave) -- 567 us, the texture addresser then touches ~48 cache lines per wave-instruction.
-// MPBP_CSR_ALIAS: one 6 KiB LDS slot per wave instead of 9 KiB (36 -> 24 KiB per workgroup, LDS then
-// allows 6 waves per SIMD): the uniform path stages the columns, reads them back and only then stages
-// the values over them (the x gathers are in flight meanwhile); the general path's chunk is 512 entries.
-#ifndef MPBP_CSR_ALIAS
-#define MPBP_CSR_ALIAS 0
-#endif
 #ifndef MPBP_CSR_WAVECAP
-#define MPBP_CSR_WAVECAP (MPBP_CSR_ALIAS ? 512 : 768)
+#define MPBP_CSR_WAVECAP 768
 #endif
 #ifndef MPBP_CSR_TGATHER
 #define MPBP_CSR_TGATHER 1
@@ -957,9 +951,7 @@ __device__ inline double csr_wave_uniform(const Csr& A, const double* __restrict
     }
 #pragma unroll
     for (int j = 0; j < P; ++j) {
-#if !MPBP_CSR_ALIAS
         vs[lane + 64 * j] = v[j];
-#endif
         cs[lane + 64 * j] = cc[j];
     }
     wave_lds_sync();
@@ -967,15 +959,6 @@ __device__ inline double csr_wave_uniform(const Csr& A, const double* __restrict
     int2 c[P];
 #pragma unroll
     for (int i = 0; i < P; ++i) c[i] = cs[p0 + i];
-#if MPBP_CSR_ALIAS
-    (void)vs;
-    wave_lds_sync();   // every lane's column reads are done: the values go over them
-    double2* vv = reinterpret_cast<double2*>(cs);
-#pragma unroll
-    for (int j = 0; j < P; ++j) vv[lane + 64 * j] = v[j];
-#else
-    const double2* vv = vs;
-#endif
     double x0[P], x1[P];
     if constexpr (XB) {
         const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(x), (short)0, A.ncols * 8, 0x00020000);
@@ -991,43 +974,23 @@ __device__ inline double csr_wave_uniform(const Csr& A, const double* __restrict
             x1[i] = x[c[i].y];
         }
     }
-#if MPBP_CSR_ALIAS
-    wave_lds_sync();
-#endif
     double acc = 0.0;
 #pragma unroll
     for (int i = 0; i < P; ++i) {
-        const double2 q = vv[p0 + i];
+        const double2 q = vs[p0 + i];
         acc += q.x * x0[i];
         acc += q.y * x1[i];
     }
     return acc;
 }
 
-#ifndef MPBP_CSR_WPE
-#define MPBP_CSR_WPE 0
-#endif
-#if MPBP_CSR_WPE
-#define CSR_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(MPBP_CSR_WPE)))
-#else
-#define CSR_WAVES_ATTR
-#endif
 template <class Epi>
-__global__ void __launch_bounds__(kBlock) CSR_WAVES_ATTR k_csr_wave(Csr A, const double* __restrict__ x,
+__global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __restrict__ x,
                                                      const int2* __restrict__ blocks, int nblocks,
                                                      Epi epi) {
-#if MPBP_CSR_ALIAS
-    static_assert(MPBP_CSR_TGATHER && kWaveCap * 12 <= 6144, "one 6 KiB slot per wave");
-    __shared__ double2 slot[kBlock / 64][384];   // uniform: 768 columns, then 768 values; general: both
-    double2 (*vstage)[384] = slot;
-    int2* cstage[kBlock / 64];
-#pragma unroll
-    for (int i = 0; i < kBlock / 64; ++i) cstage[i] = reinterpret_cast<int2*>(slot[i]);
-#else
     __shared__ double2 vstage[kBlock / 64][kWaveCap / 2];
 #if MPBP_CSR_TGATHER
     __shared__ int2 cstage[kBlock / 64][kWaveCap / 2];
-#endif
 #endif
     const int b = xcd_swizzle(blockIdx.x, nblocks);
     const int2 blk = blocks[b];
@@ -1088,11 +1051,7 @@ __global__ void __launch_bounds__(kBlock) CSR_WAVES_ATTR k_csr_wave(Csr A, const
         const int32_t tend = min(ke, cb + kWaveCap) - cb;
 #if MPBP_CSR_TGATHER
         if (cb != (s & ~1)) wave_lds_sync();   // the previous chunk's reads are done
-#if MPBP_CSR_ALIAS
-        int2* cs = cstage[w] + kWaveCap;   // after the chunk's kWaveCap / 2 value pairs
-#else
         int2* cs = cstage[w];
-#endif
         const int32_t* cs1 = reinterpret_cast<const int32_t*>(cs);
 #pragma unroll
         for (int j = 0; j < kWavePairs; ++j) {
