@@ -157,7 +157,18 @@ typedef struct mpbp_mg_level {
     mpbp_sell A_sell;
     mpbp_sell R_sell;
     mpbp_sell P_sell;
+    /* row partition (mpbp_mg.part_levels > l): the halo kind of this level's vectors; nrows counts the owned rows,
+     * x / t / r hold owned + ghost rows (the ext layout), R's columns index that layout and P's the next level's
+     * (or, at the last partitioned level, the whole next level) */
+    int32_t halo_kind;
+    int32_t reserved2;
 } mpbp_mg_level;
+
+typedef void (*mpbp_halo_fn)(void* ctx, int32_t vec_kind, double* x_ext, int32_t phase, void* stream);
+/* A velocity and a pressure vector's halos in one exchange, complete on `stream` when it returns. */
+typedef void (*mpbp_halo_pair_fn)(void* ctx, double* xu_ext, double* xp_ext, void* stream);
+/* All-gather of a row-partitioned vector into the whole field-major vector on every rank (on `stream`). */
+typedef void (*mpbp_gather_fn)(void* ctx, int32_t gather_kind, const double* x_owned, double* x_full, void* stream);
 
 typedef struct mpbp_mg {
     int32_t nlevels;                 /* >= 2 */
@@ -167,11 +178,17 @@ typedef struct mpbp_mg {
     mpbp_rowblocks coarse_inv_blocks;
     const double* coarse_dense;      /* optional: the same inverse column-major (m x m, m = coarsest nrows), applied
                                       * by a dense kernel (one row per lane, the CSR row's order); NULL: CSR */
+    /* Row partition over ranks (multi-GPU; 0 / NULL on one GPU).  Levels [0, part_levels) are row-partitioned (each
+     * rank its grid rows, ghost rows refreshed through `halo` before every operator that reads them; level 0 inside
+     * mpbp_schur_apply through the plan's halo); the restriction into level part_levels leaves the rank's rows of
+     * that level in its r buffer, `gather` (gather_kind) assembles the whole level in its b, and the coarser levels
+     * run replicated on every rank.  1 <= part_levels <= nlevels - 1.  Same bits as the one-GPU hierarchy. */
+    int32_t part_levels;
+    int32_t gather_kind;
+    mpbp_halo_fn halo;
+    void* halo_ctx;                  /* passed to halo and gather */
+    mpbp_gather_fn gather;
 } mpbp_mg;
-
-typedef void (*mpbp_halo_fn)(void* ctx, int32_t vec_kind, double* x_ext, int32_t phase, void* stream);
-/* A velocity and a pressure vector's halos in one exchange, complete on `stream` when it returns. */
-typedef void (*mpbp_halo_pair_fn)(void* ctx, double* xu_ext, double* xp_ext, void* stream);
 
 /* The apply's operands.  On one GPU every matrix's columns index the full vector and the
  * *_bnd row blocks are empty.  Under a row partition the columns index the "ext" layout of the
@@ -222,7 +239,8 @@ typedef struct mpbp_schur_plan {
     const double* q13;               /* optional (one GPU): Gt_F_G in the 13-point diamond layout
                                         (mpbp_q13_build), used instead of GtFG / Qs_* when set */
     int32_t q13_n;                   /* its grid size n */
-    const mpbp_mg* mg_F;             /* inner_F.kind == MPBP_INNER_MG: F's hierarchy (level 0 = F; one GPU) */
+    const mpbp_mg* mg_F;             /* inner_F.kind == MPBP_INNER_MG: F's hierarchy (level 0 = F; row-partitioned
+                                        with part_levels >= 1 when halo is set) */
     const mpbp_mg* mg_P;             /* inner_P.kind == MPBP_INNER_MG: Gt_G's hierarchy */
     int32_t fuse_g;                  /* 1 (one GPU, f_stencil and pg_stencil, Chebyshev F solve of >= 2 sweeps): the
                                         second F solve recomputes its right-hand side G x_p inside each sweep (no G
@@ -372,7 +390,8 @@ int mpbp_mg_transfer_count(int32_t n, int32_t nfields, const int32_t* kinds, int
                            void* stream);
 int mpbp_mg_transfer_fill(int32_t n, int32_t nfields, const int32_t* kinds, int32_t which, const int32_t* row_ptr,
                           int32_t* col_idx, double* val, void* stream);
-/* x_out = mg->cycles V-cycles for levels[0].A x = b from x = 0 (sub - x when sub != NULL).  Graph-capturable. */
+/* x_out = mg->cycles V-cycles for levels[0].A x = b from x = 0 (sub - x when sub != NULL).  Graph-capturable.
+ * Row-partitioned hierarchies (part_levels > 0): b, sub, x_out hold the rank's owned rows of level 0. */
 int mpbp_mg_solve(const mpbp_mg* mg, const double* b, const double* sub, double* x_out, void* stream);
 
 /* ---- ghost rows over RCCL point-to-point (multi-GPU row partition) ------------------------------ */
@@ -395,8 +414,19 @@ int mpbp_halo_status(const mpbp_halo* halo);
 /* mpbp_halo_pair_fn over RCCL: one group with both vectors' neighbour sends / receives (IN_ORDER on
  * `stream`; the velocity rows gathered first). */
 void mpbp_halo_exchange_pair(void* ctx, double* xu_ext, double* xp_ext, void* stream);
+/* Mode of every kind defined so far (kinds added later take their own mode). */
 int mpbp_halo_set_mode(mpbp_halo* halo, int32_t mode);
 const char* mpbp_halo_last_error(const mpbp_halo* halo);
+/* Another vector layout on the same communicator: nfields fields of an n x n grid, owned rows [r0, r0 + rows),
+ * h ghost rows each side; returns its kind id for mpbp_halo_exchange (kinds 0 / 1 are the Schur apply's velocity /
+ * pressure vectors).  Used for the system vector of the partitioned operator A (apply.py:72, the FGMRES A @ x)
+ * and for the multigrid levels.  Setup. */
+int mpbp_halo_add_kind(mpbp_halo* halo, int32_t nfields, int32_t n, int32_t r0, int32_t rows, int32_t h, int32_t mode);
+/* An all-gather layout: rank k owns rows [r0s[k], r0s[k] + rows_s[k]) of each of nfields fields of an n x n grid
+ * (host arrays of world entries, covering the grid); returns its id for mpbp_halo_allgather.  Setup. */
+int mpbp_halo_add_gather(mpbp_halo* halo, int32_t nfields, int32_t n, const int32_t* r0s, const int32_t* rows_s);
+/* mpbp_gather_fn over RCCL: pad the owned rows, one ncclAllGather, one gather kernel into x_full (on `stream`). */
+void mpbp_halo_allgather(void* ctx, int32_t gather_kind, const double* x_owned, double* x_full, void* stream);
 
 /* gather: dst[i] = src[idx[i]] ; scatter: dst[idx[i]] = src[i]   (halo pack / unpack) */
 int mpbp_gather(int32_t count, const int32_t* idx, const double* src, double* dst, void* stream);
@@ -413,9 +443,22 @@ int mpbp_event_elapsed_ms(void* start, void* stop, float* ms);
 int mpbp_gs_dot(const double* V, int64_t ld, int32_t k, const double* w, int64_t n, double* part, double* h,
                 void* stream);
 int64_t mpbp_gs_part_size(int64_t n, int32_t k);
-/* w_out = w - V^T h (w_out may alias w). */
+/* w_out = w - V^T h (w_out may alias w: element-wise, each element read before it is written). */
 int mpbp_gs_update(const double* V, int64_t ld, int32_t k, const double* h, const double* w, int64_t n, double* w_out,
                    void* stream);
+/* Reproducible dot products (binned summation, 3 folds; the FGMRES of a row partition computes the same bits as on
+ * one GPU): acc[3i .. 3i+2] = the exact fold sums of V[i] . w over this rank's n entries (i < k).  bound_v (device,
+ * k) and bound_w (device, 1) bound |V[i][e]| and |w[e]| over EVERY rank's entries (a max-reduction of local
+ * maxima, mpbp_absmax); n_total is the length of the whole distributed vector.  The fold sums of different ranks
+ * add exactly (a sum-reduction in any order), and mpbp_rdot_finish gives h[i] = (S0 + S1) + S2 -- the same bits
+ * for every row partition, chunking and launch order.  Error <= about 2^-51 of bound_v[i] bound_w.  part: device
+ * scratch of mpbp_rdot_part_size(n, k) doubles. */
+int mpbp_rdot(const double* V, int64_t ld, int32_t k, const double* w, int64_t n, int64_t n_total,
+              const double* bound_v, const double* bound_w, double* part, double* acc, void* stream);
+int64_t mpbp_rdot_part_size(int64_t n, int32_t k);
+int mpbp_rdot_finish(int32_t k, const double* acc, double* h, void* stream);
+/* amax[0] = max_e |x[e]| (device scalar, overwritten; NaN if x holds one). */
+int mpbp_absmax(const double* x, int64_t n, double* amax, void* stream);
 
 #ifdef __cplusplus
 }

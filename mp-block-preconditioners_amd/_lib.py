@@ -60,16 +60,19 @@ class MgLevel(Structure):
                 ("lmin", c_double), ("lmax", c_double), ("A", Csr), ("A_blocks", RowBlocks), ("diag", c_void_p),
                 ("R", Csr), ("R_blocks", RowBlocks), ("P", Csr), ("P_blocks", RowBlocks),
                 ("x", c_void_p), ("t", c_void_p), ("r", c_void_p), ("d", c_void_p), ("b", c_void_p),
-                ("A_sell", Sell), ("R_sell", Sell), ("P_sell", Sell)]
-
-
-class Mg(Structure):
-    _fields_ = [("nlevels", c_int32), ("cycles", c_int32), ("levels", POINTER(MgLevel)), ("coarse_inv", Csr),
-                ("coarse_inv_blocks", RowBlocks), ("coarse_dense", c_void_p)]
+                ("A_sell", Sell), ("R_sell", Sell), ("P_sell", Sell), ("halo_kind", c_int32), ("reserved2", c_int32)]
 
 
 HALO_FN = CFUNCTYPE(None, c_void_p, c_int32, c_void_p, c_int32, c_void_p)
 HALO_PAIR_FN = CFUNCTYPE(None, c_void_p, c_void_p, c_void_p, c_void_p)
+GATHER_FN = CFUNCTYPE(None, c_void_p, c_int32, c_void_p, c_void_p, c_void_p)
+
+
+class Mg(Structure):
+    _fields_ = [("nlevels", c_int32), ("cycles", c_int32), ("levels", POINTER(MgLevel)), ("coarse_inv", Csr),
+                ("coarse_inv_blocks", RowBlocks), ("coarse_dense", c_void_p),
+                ("part_levels", c_int32), ("gather_kind", c_int32), ("halo", HALO_FN), ("halo_ctx", c_void_p),
+                ("gather", GATHER_FN)]
 
 
 class SchurPlan(Structure):
@@ -142,6 +145,9 @@ _SIGNATURES = {
     "mpbp_halo_status": ([_P], c_int),
     "mpbp_halo_set_mode": ([_P, c_int32], c_int),
     "mpbp_halo_last_error": ([_P], c_char_p),
+    "mpbp_halo_add_kind": ([_P, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32], c_int),
+    "mpbp_halo_add_gather": ([_P, c_int32, c_int32, _P, _P], c_int),
+    "mpbp_halo_allgather": ([_P, c_int32, _P, _P, _P], None),
     "mpbp_set_march_rows": ([c_int32], c_int),
     "mpbp_set_init_diag": ([c_int32], c_int),
     "mpbp_set_pg_direct": ([c_int32], c_int),
@@ -158,6 +164,10 @@ _SIGNATURES = {
     "mpbp_gs_dot": ([_P, c_int64, c_int32, _P, c_int64, _P, _P, _P], c_int),
     "mpbp_gs_part_size": ([c_int64, c_int32], c_int64),
     "mpbp_gs_update": ([_P, c_int64, c_int32, _P, _P, c_int64, _P, _P], c_int),
+    "mpbp_rdot": ([_P, c_int64, c_int32, _P, c_int64, c_int64, _P, _P, _P, _P, _P], c_int),
+    "mpbp_rdot_part_size": ([c_int64, c_int32], c_int64),
+    "mpbp_rdot_finish": ([c_int32, _P, _P, _P], c_int),
+    "mpbp_absmax": ([_P, c_int64, _P, _P], c_int),
 }
 
 _lib = None
@@ -205,5 +215,5 @@ def stream_handle(stream=None):
 
 
 __all__ = ["lib", "check", "ptr", "stream_handle", "MpbpError", "Csr", "RowBlocks", "Sell", "RowPart", "StokesParams",
-           "InnerSolverC", "SchurPlan", "HALO_FN", "byref",
+           "InnerSolverC", "SchurPlan", "HALO_FN", "GATHER_FN", "byref",
            "Mg", "MgLevel"]

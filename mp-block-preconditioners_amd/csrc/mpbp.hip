@@ -917,6 +917,12 @@ constexpr int kWaveCap = MPBP_CSR_WAVECAP;     // entries per wave chunk (64 row
 constexpr int kWavePairs = kWaveCap / 128;     // 16-byte loads per lane per chunk
 constexpr int kRowBatch = 8;                   // pairs of a row gathered at once (16 entries)
 
+// A wave-uniform int32 element through a scalar (constant address space) load.
+typedef __attribute__((address_space(4))) const int32_t cint32;
+__device__ inline int32_t ld_uniform_i32(const int32_t* p, int32_t i) {
+    return ((cint32*)p)[__builtin_amdgcn_readfirstlane(i)];
+}
+
 // Lanes of one wave exchange data through LDS: order the LDS writes before the reads (compiler
 // and wave scope; a wave's LDS operations complete in order).
 __device__ inline void wave_lds_sync() {
@@ -937,10 +943,19 @@ __device__ inline void wave_lds_sync() {
 #endif
 // XB: x gathered with buffer loads (one descriptor for x, a 32-bit byte offset per entry: no 64-bit
 // address arithmetic per gather); needs ncols * 8 < 2^31.
-template <int LEN, bool XB>
-__device__ inline double csr_wave_uniform(const Csr& A, const double* __restrict__ x, int32_t s, int lane,
-                                          double2* vs, int2* cs) {
+// Returns false (nothing stored) when some row of the wave does not hold LEN entries.  MPBP_CSR_SPEC=1: the
+// matrix loads are issued before that check -- they depend on the wave's first entry s alone (and stay inside
+// [s, s + 64 LEN) = the wave's entries), so their HBM latency overlaps the per-row row_ptr loads' instead of
+// following it.
+#ifndef MPBP_CSR_SPEC
+#define MPBP_CSR_SPEC 1
+#endif
+template <int LEN, bool XB, class Epi>
+__device__ inline bool csr_wave_uniform(const Csr& A, const double* __restrict__ x, int32_t s, int lane,
+                                        double2* vs, int2* cs, int32_t ks, int32_t ke, int32_t r, const Epi& epi,
+                                        const typename Epi::P& pe) {
     constexpr int P = LEN / 2;   // pairs per row == 16-byte loads per lane
+    if (!MPBP_CSR_SPEC && !__all(ke - ks == LEN)) return false;
     double2 v[P];
     int2 cc[P];
 #pragma unroll
@@ -949,6 +964,10 @@ __device__ inline double csr_wave_uniform(const Csr& A, const double* __restrict
         v[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const double2*>(A.va + k));
         cc[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const int2*>(A.ci + k));
     }
+    // (a compiler memory barrier: the loads above may not sink below the check, which would serialise them
+    // behind the row_ptr loads again; it emits no instruction and no wait)
+    if (MPBP_CSR_SPEC) asm volatile("" ::: "memory");
+    if (MPBP_CSR_SPEC && !__all(ke - ks == LEN)) return false;
 #pragma unroll
     for (int j = 0; j < P; ++j) {
         vs[lane + 64 * j] = v[j];
@@ -981,7 +1000,8 @@ __device__ inline double csr_wave_uniform(const Csr& A, const double* __restrict
         acc += q.x * x0[i];
         acc += q.y * x1[i];
     }
-    return acc;
+    epi.template apply<MPBP_CSR_NT != 0>(r, acc, pe);   // every lane holds a row here
+    return true;
 }
 
 template <class Epi>
@@ -995,38 +1015,37 @@ __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __rest
     const int b = xcd_swizzle(blockIdx.x, nblocks);
     const int2 blk = blocks[b];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int32_t ra = blk.x + 64 * w;
+    const int32_t ra = __builtin_amdgcn_readfirstlane(blk.x + 64 * w);
     if (ra >= blk.y) return;   // waves are independent: no workgroup barrier below
     const int32_t rb = min(ra + 64, blk.y);
     const int32_t r = ra + lane;
     const bool live = r < rb;
-    const int32_t s = A.rp[ra], e = A.rp[rb];
-    int32_t ks = 0, ke = 0;
+    // the wave's entry range through scalar loads (their own counter: the matrix loads of the uniform path wait for
+    // them alone), the rows' bounds through unconditional vector loads (lanes past the block re-read row ra)
+    const int32_t s = ld_uniform_i32(A.rp, ra), e = ld_uniform_i32(A.rp, rb);
+    const int32_t rr = live ? r : ra;
+    const int32_t ks = A.rp[rr], ke0 = A.rp[rr + 1];
+    const int32_t ke = live ? ke0 : ks;   // (an empty row for lanes past the block)
     typename Epi::P pe{};
-    if (live) {
-        ks = A.rp[r];
-        ke = A.rp[r + 1];
-        pe = epi.pre(r);
-    }
+    if (live) pe = epi.pre(r);
     double acc = 0.0;
     double2* vs = vstage[w];
     const double* vs1 = reinterpret_cast<const double*>(vs);
 #if MPBP_CSR_TGATHER && MPBP_CSR_UNIFORM
     {
         const int32_t len = (e - s) >> 6;   // wave-uniform
-        if (rb - ra == 64 && ((e - s) & 63) == 0 && (s & 1) == 0 && (len == 8 || len == 10 || len == 12) &&
-            __all(ke - ks == len)) {
+        if (rb - ra == 64 && ((e - s) & 63) == 0 && (s & 1) == 0 && (len == 8 || len == 10 || len == 12)) {
             constexpr bool XB = MPBP_CSR_XBUF != 0;
+            bool done;
             if (XB && A.ncols > 0 && A.ncols < (1 << 28))
-                acc = len == 12 ? csr_wave_uniform<12, XB>(A, x, s, lane, vs, cstage[w])
-                                : (len == 10 ? csr_wave_uniform<10, XB>(A, x, s, lane, vs, cstage[w])
-                                             : csr_wave_uniform<8, XB>(A, x, s, lane, vs, cstage[w]));
+                done = len == 12 ? csr_wave_uniform<12, XB>(A, x, s, lane, vs, cstage[w], ks, ke, r, epi, pe)
+                                 : (len == 10 ? csr_wave_uniform<10, XB>(A, x, s, lane, vs, cstage[w], ks, ke, r, epi, pe)
+                                              : csr_wave_uniform<8, XB>(A, x, s, lane, vs, cstage[w], ks, ke, r, epi, pe));
             else
-                acc = len == 12 ? csr_wave_uniform<12, false>(A, x, s, lane, vs, cstage[w])
-                                : (len == 10 ? csr_wave_uniform<10, false>(A, x, s, lane, vs, cstage[w])
-                                             : csr_wave_uniform<8, false>(A, x, s, lane, vs, cstage[w]));
-            epi.template apply<MPBP_CSR_NT != 0>(r, acc, pe);   // every lane holds a row here
-            return;
+                done = len == 12 ? csr_wave_uniform<12, false>(A, x, s, lane, vs, cstage[w], ks, ke, r, epi, pe)
+                                 : (len == 10 ? csr_wave_uniform<10, false>(A, x, s, lane, vs, cstage[w], ks, ke, r, epi, pe)
+                                              : csr_wave_uniform<8, false>(A, x, s, lane, vs, cstage[w], ks, ke, r, epi, pe));
+            if (done) return;
         }
     }
 #endif
@@ -1475,17 +1494,10 @@ struct XInit {         // staged value = the first inner iterate: c2 * (b[i] / d
     const double* __restrict__ b;
     const double* __restrict__ dg;
     double c2;
-#ifdef MPBP_EXP_XINIT_EARLY   // experiment: divide at load time (the loads are then waited for at once)
-    typedef double Raw;
-    __device__ Raw load(int32_t i) const { return c2 * (b[i] / dg[i]); }
-    __device__ Raw load_uniform(int32_t i) const { return c2 * (ld_uniform(b, i) / ld_uniform(dg, i)); }
-    __device__ double value(const Raw& r) const { return r; }
-#else
     typedef XInitRaw Raw;
     __device__ Raw load(int32_t i) const { return {b[i], dg[i]}; }
     __device__ Raw load_uniform(int32_t i) const { return {ld_uniform(b, i), ld_uniform(dg, i)}; }
     __device__ double value(const Raw& r) const { return c2 * (r.b / r.d); }
-#endif
     __device__ double operator()(int32_t i) const { return c2 * (b[i] / dg[i]); }
 };
 
@@ -1692,11 +1704,7 @@ k_march(S P, XS xs, int nchunks, Epi epi, BS bs = BS{}) {
             const TRing ta{st, {sm, s0, sp}, gr, c0};
             // the wrap-aware (sorting) form is exact for interior cells too: take it for the whole wave when
             // any of its cells is on the periodic edge, so a wave never runs both forms
-#ifdef MPBP_EXP_NO_EDGE   // timing experiment only (wrong results on the periodic edge)
-            const bool edge = false;
-#else
             const bool edge = __builtin_amdgcn_readfirstlane(__any(gr == 0 || gr == n - 1 || gc == 0 || gc == n - 1)) != 0;
-#endif
 #pragma unroll
             for (int o = 0; o < NO; ++o) {
                 double dg;
@@ -2683,9 +2691,10 @@ __global__ void __launch_bounds__(kBlock) k_gs_sum(const double* part, int64_t n
         h[i] = t;
     }
 }
+// (w and wo may alias: each thread reads w[e] before it writes wo[e], so neither is declared __restrict__)
 __global__ void __launch_bounds__(kBlock) k_gs_update(const double* __restrict__ V, int64_t ld, int k,
-                                                      const double* __restrict__ h, const double* __restrict__ w,
-                                                      int64_t n, double* __restrict__ wo) {
+                                                      const double* __restrict__ h, const double* w,
+                                                      int64_t n, double* wo) {
     __shared__ double hs[256];
     for (int i = threadIdx.x; i < k; i += kBlock) hs[i] = h[i];
     __syncthreads();
@@ -2702,6 +2711,122 @@ __global__ void __launch_bounds__(kBlock) k_gs_update(const double* __restrict__
     }
     for (; i < k; ++i) a += V[(int64_t)i * ld + e] * hs[i];
     wo[e] = w[e] - a;
+}
+// ---- reproducible dot products: binned summation (Demmel & Nguyen's pre-rounding, 3 folds) ----
+// Every term t = v w (|t| <= 2^E, E from the caller's bounds; N terms in the whole distributed vector) is split as
+// t = q0 + q1 + q2 + (dropped): q_f = fl(sigma_f + r) - sigma_f with sigma_f = 1.5 * 2^(E + (f+1) L - 53 f), L >= log2 N + 1,
+// r the remainder of the previous folds.  Each q_f is a multiple of ulp(sigma_f) and N of them sum to less than
+// 2^53 such ulps, so every partial sum of a fold is EXACT: the fold sums -- and h = (S0 + S1) + S2 -- depend only on
+// the set of terms, never on the order, the chunking, the launch configuration or the split of the vector over
+// ranks (the sums of the ranks' fold sums are exact too).  FGMRES therefore computes the same bits on one GPU and
+// on a row partition.  Accuracy: |h - sum t| <= N 2^(E + 3L - 159) + one rounding (about 2^-51 of the bound for
+// N = 2^24), against the N eps sum|t| of a plain sum.  A fold whose sigma would be subnormal is skipped (q = 0).
+constexpr int kRdVec = 4;      // basis vectors per workgroup
+constexpr int kRdFolds = 3;
+__device__ inline void rd_sigmas(double bound, int64_t ntot, double* sig) {
+    int E = 0;
+    (void)frexp(bound, &E);    // bound < 2^E
+    const int L = 65 - __clzll((unsigned long long)(ntot > 0 ? ntot : 1));
+    const bool finite = bound == bound && bound <= 1.7976931348623157e308;
+#pragma unroll
+    for (int f = 0; f < kRdFolds; ++f) {
+        const int ex = E + (f + 1) * L - 53 * f;
+        sig[f] = (!finite || (bound > 0.0 && E + L > 1023)) ? __longlong_as_double(0x7ff8000000000000LL)   // NaN / range
+                 : !(bound > 0.0) ? 0.0                              // all terms 0: nothing to fold
+                 : ex >= -1022 ? ldexp(1.5, ex) : 0.0;               // subnormal fold: skipped
+    }
+}
+__device__ inline void rd_fold(double t, const double* sig, double* acc) {
+    double r = t;
+#pragma unroll
+    for (int f = 0; f < kRdFolds; ++f) {
+        const double q = (sig[f] + r) - sig[f];
+        const double qq = sig[f] != 0.0 ? q : 0.0;
+        acc[f] += qq;
+        r -= qq;
+    }
+}
+__global__ void __launch_bounds__(kBlock) k_rdot(const double* __restrict__ V, int64_t ld, int k,
+                                                 const double* __restrict__ w, int64_t n, int64_t ntot,
+                                                 const double* __restrict__ bound_v, const double* __restrict__ bound_w,
+                                                 double* part) {
+    const int64_t c = blockIdx.x;
+    const int i0 = blockIdx.y * kRdVec;
+    const int nv = min(kRdVec, k - i0);
+    double sig[kRdVec][kRdFolds], acc[kRdVec][kRdFolds];
+    const double bw = bound_w[0];
+#pragma unroll
+    for (int v = 0; v < kRdVec; ++v) {
+        rd_sigmas(v < nv ? bound_v[i0 + v] * bw : 0.0, ntot, sig[v]);
+#pragma unroll
+        for (int f = 0; f < kRdFolds; ++f) acc[v][f] = 0.0;
+    }
+    for (int u = 0; u < kGsPer; u += kGsBatch) {
+        double wv[kGsBatch], vv[kRdVec][kGsBatch];
+#pragma unroll
+        for (int q = 0; q < kGsBatch; ++q) {   // every load of the batch in flight at once
+            const int64_t e = c * kGsChunk + (int64_t)(u + q) * kBlock + threadIdx.x;
+            const bool ok = e < n;
+            const int64_t ee = ok ? e : 0;
+            wv[q] = ok ? w[ee] : 0.0;
+#pragma unroll
+            for (int v = 0; v < kRdVec; ++v) vv[v][q] = v < nv ? V[(int64_t)(i0 + v) * ld + ee] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < kGsBatch; ++q)
+#pragma unroll
+            for (int v = 0; v < kRdVec; ++v) rd_fold(vv[v][q] * wv[q], sig[v], acc[v]);
+    }
+    // block reduction: exact additions, so the tree shape does not matter
+    __shared__ double red[kRdVec * kRdFolds][kBlock / 64];
+    const int lane = threadIdx.x & 63, wv_ = threadIdx.x >> 6;
+#pragma unroll
+    for (int v = 0; v < kRdVec; ++v)
+#pragma unroll
+        for (int f = 0; f < kRdFolds; ++f) {
+            double a = acc[v][f];
+            for (int off = 32; off > 0; off >>= 1) a += __shfl_down(a, off, 64);
+            if (lane == 0) red[v * kRdFolds + f][wv_] = a;
+        }
+    __syncthreads();
+    if (threadIdx.x < nv * kRdFolds) {
+        double a = 0.0;
+        for (int q = 0; q < kBlock / 64; ++q) a += red[threadIdx.x][q];
+        part[c * (3 * (int64_t)k) + 3 * i0 + threadIdx.x] = a;
+    }
+}
+// acc[j] = sum over chunks of part[c][j] (exact), one workgroup per fold sum
+__global__ void __launch_bounds__(kBlock) k_rdot_sum(const double* part, int64_t nchunks, int k3, double* acc) {
+    const int j = blockIdx.x;
+    double a = 0.0;
+    for (int64_t c = threadIdx.x; c < nchunks; c += kBlock) a += part[c * k3 + j];
+    for (int off = 32; off > 0; off >>= 1) a += __shfl_down(a, off, 64);
+    __shared__ double red[kBlock / 64];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int q = 0; q < kBlock / 64; ++q) t += red[q];
+        acc[j] = t;
+    }
+}
+__global__ void k_rdot_finish(int k, const double* acc, double* h) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < k) h[i] = (acc[3 * i] + acc[3 * i + 1]) + acc[3 * i + 2];
+}
+// amax = max |x| (non-negative doubles order like their bit patterns; NaN's pattern exceeds every finite one)
+__global__ void __launch_bounds__(kBlock) k_absmax(const double* __restrict__ x, int64_t n, unsigned long long* out) {
+    double m = 0.0;
+    for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (int64_t)gridDim.x * kBlock) {
+        const double a = fabs(x[e]);
+        m = (a > m || a != a) ? a : m;
+    }
+    unsigned long long b = (unsigned long long)__double_as_longlong(m);
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(b, off, 64);
+        b = o > b ? o : b;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(out, b);
 }
 }  // namespace
 
@@ -2721,6 +2846,44 @@ int mpbp_gs_dot(const double* V, int64_t ld, int32_t k, const double* w, int64_t
 }
 
 int64_t mpbp_gs_part_size(int64_t n, int32_t k) { return ((n + kGsChunk - 1) / kGsChunk) * (int64_t)k; }
+
+int64_t mpbp_rdot_part_size(int64_t n, int32_t k) { return ((n + kGsChunk - 1) / kGsChunk) * 3 * (int64_t)k; }
+
+int mpbp_rdot(const double* V, int64_t ld, int32_t k, const double* w, int64_t n, int64_t n_total,
+              const double* bound_v, const double* bound_w, double* part, double* acc, void* stream) {
+    if (!V || !w || !bound_v || !bound_w || !part || !acc || k < 1 || k > 256 || n < 0 || ld < n || n_total < n)
+        return set_error(MPBP_ERR_ARG, "rdot: bad args (1 <= k <= 256, ld >= n, n_total >= n)");
+    const hipStream_t st = as_stream(stream);
+    if (n == 0) {
+        MPBP_HIP(hipMemsetAsync(acc, 0, sizeof(double) * 3 * (size_t)k, st));
+        return MPBP_OK;
+    }
+    const int64_t nchunks = (n + kGsChunk - 1) / kGsChunk;
+    const dim3 grid((unsigned)nchunks, (unsigned)((k + kRdVec - 1) / kRdVec));
+    k_rdot<<<grid, kBlock, 0, st>>>(V, ld, k, w, n, n_total, bound_v, bound_w, part);
+    MPBP_HIP(hipGetLastError());
+    k_rdot_sum<<<3 * k, kBlock, 0, st>>>(part, nchunks, 3 * k, acc);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int mpbp_rdot_finish(int32_t k, const double* acc, double* h, void* stream) {
+    if (!acc || !h || k < 1) return set_error(MPBP_ERR_ARG, "rdot_finish: bad args");
+    k_rdot_finish<<<grid_for(k), kBlock, 0, as_stream(stream)>>>(k, acc, h);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int mpbp_absmax(const double* x, int64_t n, double* amax, void* stream) {
+    if (!amax || n < 0 || (n > 0 && !x)) return set_error(MPBP_ERR_ARG, "absmax: bad args");
+    const hipStream_t st = as_stream(stream);
+    MPBP_HIP(hipMemsetAsync(amax, 0, sizeof(double), st));
+    if (n == 0) return MPBP_OK;
+    const int64_t blocks = (n + kBlock * 16 - 1) / (kBlock * 16);
+    k_absmax<<<(unsigned)(blocks < 4096 ? blocks : 4096), kBlock, 0, st>>>(x, n, reinterpret_cast<unsigned long long*>(amax));
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
 
 int mpbp_gs_update(const double* V, int64_t ld, int32_t k, const double* h, const double* w, int64_t n, double* w_out,
                    void* stream) {
@@ -3274,18 +3437,46 @@ int two_phase(const Ctx& c, int32_t kind, const double* x_ext, const OpPair& op,
 // steps), so the cycle is graph-capturable and its operation order is the oracle's (oracle/mg_oracle.py).
 // Level 0 can be any operator of the plan (matrix-free stencil, SELL or CSR: the same bits).
 struct MgFine {
-    OpRef op;
+    OpPair op;               // level 0's operator (interior + boundary rows under a row partition)
     const double* diag;
     double *x, *t, *r, *d;   // two iterate buffers, residual, Chebyshev direction
+    mpbp_halo_fn halo;       // level 0's ghost-row exchange (NULL: one GPU)
+    void* hctx;
+    int32_t kind;
 };
+
+int pair_spmv(const OpPair& o, int32_t mode, const double* x, const double* z, double* y, hipStream_t st) {
+    const int rc = op_spmv(o.in, mode, x, z, y, st);
+    return rc ? rc : op_spmv(o.bd, mode, x, z, y, st);
+}
+int pair_cheb(const OpPair& o, const double* xin, const double* b, const double* dg, double c1, double c2, double* d,
+              const double* sub, double* xo, hipStream_t st, int store_d) {
+    const int rc = op_cheb(o.in, xin, b, dg, c1, c2, d, sub, xo, st, store_d);
+    return rc ? rc : op_cheb(o.bd, xin, b, dg, c1, c2, d, sub, xo, st, store_d);
+}
 
 OpRef mg_csr_op(const mpbp_csr& A, const mpbp_rowblocks& blk) {
     return OpRef{&A, &blk, nullptr, nullptr, false, 0, SOP_NONE};
 }
 // A level's operator: its SELL-64 copy when it has one (same bits), else the CSR form.
-OpRef mg_level_op(const mpbp_mg_level& L) {
-    return L.A_sell.nslices > 0 ? OpRef{&L.A, nullptr, &L.A_sell, nullptr, false, 0, SOP_NONE}
-                                : mg_csr_op(L.A, L.A_blocks);
+OpPair mg_level_op(const mpbp_mg_level& L) {
+    const OpRef none{nullptr, nullptr, nullptr, nullptr, true, 0, SOP_NONE};
+    return OpPair{L.A_sell.nslices > 0 ? OpRef{&L.A, nullptr, &L.A_sell, nullptr, false, 0, SOP_NONE}
+                                       : mg_csr_op(L.A, L.A_blocks), none};
+}
+// Ghost rows of a level-l vector (row-partitioned levels l < part_levels; level 0 through the caller's halo).
+void mg_exchange(const mpbp_mg* m, int l, const MgFine& f, double* x, hipStream_t st) {
+    if (l == 0) {
+        if (f.halo) {
+            f.halo(f.hctx, f.kind, x, MPBP_HALO_BEGIN, (void*)st);
+            f.halo(f.hctx, f.kind, x, MPBP_HALO_END, (void*)st);
+        }
+        return;
+    }
+    if (l < m->part_levels && m->halo) {
+        m->halo(m->halo_ctx, m->levels[l].halo_kind, x, MPBP_HALO_BEGIN, (void*)st);
+        m->halo(m->halo_ctx, m->levels[l].halo_kind, x, MPBP_HALO_END, (void*)st);
+    }
 }
 int mg_transfer(const mpbp_csr& M, const mpbp_rowblocks& blk, const mpbp_sell& S, int32_t mode, const double* x,
                 const double* z, double* y, hipStream_t st) {
@@ -3327,16 +3518,21 @@ __global__ void __launch_bounds__(kDT) k_dense_cm(int32_t m, const double* __res
 
 // K Chebyshev-Jacobi sweeps on [lmin, lmax].  zero: from x = 0 (the first sweep is the init pass: d = x =
 // c2[0] b / diag), else from the iterate in *cur (d starts at 0).  The last sweep writes `dst` (or the free
-// ping-pong buffer when dst is NULL), as sub - x when sub is set; *cur points at the result on return.
-int mg_smooth(const OpRef& o, int32_t nrows, const double* diag, double lmin, double lmax, int K, bool zero,
-              const double* b, double** cur, double* alt, double* d, double* dst, const double* sub, hipStream_t st) {
+// ping-pong buffer when dst is NULL), as sub - x when sub is set; *cur points at the result on return.  xch(x)
+// refreshes x's ghost rows before every sweep that reads them (a no-op on one GPU).
+template <class Xch>
+int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, double lmax, int K, bool zero,
+              const double* b, double** cur, double* alt, double* d, double* dst, const double* sub, hipStream_t st,
+              Xch&& xch) {
     double c1[64] = {}, c2[64] = {};
     if (K < 1 || K > 64) return set_error(MPBP_ERR_ARG, "mg: smoothing sweeps must be in [1, 64]");
     cheb_coeffs(lmin, lmax, K, c1, c2);
+    const OpRef& o = op.in;
     double* x = *cur;
     double* other = alt;
     int s = 0;
-    if (zero && K >= 2 && o.stencil && !o.stencil->halo && o.which == 0 && (o.sop == SOP_F || o.sop == SOP_GTG)) {
+    if (zero && K >= 2 && op.bd.empty && o.stencil && !o.stencil->halo && o.which == 0 &&
+        (o.sop == SOP_F || o.sop == SOP_GTG)) {
         // whole-grid stencil level (level 0 of the Schur apply's hierarchies): the first sweep stages
         // x0 = d0 = c2[0] b / diag itself (op_first_sweep, as the Chebyshev inner solve): no init launch, same bits
         double* out1 = K == 2 ? (dst ? dst : other) : other;
@@ -3361,7 +3557,8 @@ int mg_smooth(const OpRef& o, int32_t nrows, const double* diag, double lmin, do
     for (; s < K; ++s) {
         const bool last = s == K - 1;
         double* nxt = (last && dst) ? dst : other;
-        const int rc = op_cheb(o, x, b, diag, c1[s], c2[s], d, last ? sub : nullptr, nxt, st, last ? 0 : 1);
+        xch(x);
+        const int rc = pair_cheb(op, x, b, diag, c1[s], c2[s], d, last ? sub : nullptr, nxt, st, last ? 0 : 1);
         if (rc) return rc;
         other = x;
         x = nxt;
@@ -3371,12 +3568,16 @@ int mg_smooth(const OpRef& o, int32_t nrows, const double* diag, double lmin, do
 }
 
 // One V-cycle on level l for A_l x = b.  Level 0 uses `fine` (operator and buffers); coarser levels their
-// mpbp_mg_level.  *res receives the result's buffer (dst when given).
+// mpbp_mg_level.  *res receives the result's buffer (dst when given).  Row partition (m->part_levels > 0): levels
+// l < part_levels hold owned rows (vectors read by an operator carry ghost rows, refreshed by mg_exchange); the
+// restriction into level part_levels writes the rank's rows of that level into its r buffer, which is all-gathered
+// into its (whole-grid) b, and every coarser level runs replicated on each rank -- the same operators and
+// operands as on one GPU, so the same bits.
 int mg_vcycle(const mpbp_mg* m, int l, const MgFine& fine, const double* b, bool zero, double* xin, double* dst,
               const double* sub, double** res, hipStream_t st) {
     const mpbp_mg_level& L = m->levels[l];
     const bool top = l == 0;
-    const OpRef o = top ? fine.op : mg_level_op(L);
+    const OpPair o = top ? fine.op : mg_level_op(L);
     const double* diag = top ? fine.diag : L.diag;
     double* bx = top ? fine.x : L.x;
     double* bt = top ? fine.t : L.t;
@@ -3384,15 +3585,23 @@ int mg_vcycle(const mpbp_mg* m, int l, const MgFine& fine, const double* b, bool
     double* r = top ? fine.r : L.r;
     double* d = top ? fine.d : L.d;
     double* cur = xin;
-    int rc = mg_smooth(o, L.nrows, diag, L.lmin, L.lmax, L.pre, zero, b, &cur, alt, d, nullptr, nullptr, st);
+    auto xch = [&](double* v) { mg_exchange(m, l, fine, v, st); };
+    int rc = mg_smooth(o, L.nrows, diag, L.lmin, L.lmax, L.pre, zero, b, &cur, alt, d, nullptr, nullptr, st, xch);
     if (rc) return rc;
     alt = cur == bx ? bt : bx;
     // r = b - A x ; b_c = R r
-    rc = op_spmv(o, MPBP_SPMV_RESID, cur, b, r, st);
+    xch(cur);
+    rc = pair_spmv(o, MPBP_SPMV_RESID, cur, b, r, st);
     if (rc) return rc;
     const mpbp_mg_level& C = m->levels[l + 1];
-    rc = mg_transfer(L.R, L.R_blocks, L.R_sell, MPBP_SPMV_STORE, r, nullptr, C.b, st);
+    const bool gather = m->part_levels > 0 && l + 1 == m->part_levels;
+    if (l < m->part_levels) xch(r);
+    rc = mg_transfer(L.R, L.R_blocks, L.R_sell, MPBP_SPMV_STORE, r, nullptr, gather ? C.r : C.b, st);
     if (rc) return rc;
+    if (gather) {
+        if (!m->gather) return set_error(MPBP_ERR_ARG, "mg: a partitioned hierarchy needs its gather callback");
+        m->gather(m->halo_ctx, m->gather_kind, C.r, C.b, (void*)st);
+    }
     double* xc = C.x;
     if (l + 1 == m->nlevels - 1) {
         if (m->coarse_dense) {
@@ -3406,9 +3615,10 @@ int mg_vcycle(const mpbp_mg* m, int l, const MgFine& fine, const double* b, bool
     }
     if (rc) return rc;
     // x += P x_c (row-wise in place), then post-smoothing from x
+    mg_exchange(m, l + 1, fine, xc, st);
     rc = mg_transfer(L.P, L.P_blocks, L.P_sell, MPBP_SPMV_ADD, xc, cur, cur, st);
     if (rc) return rc;
-    rc = mg_smooth(o, L.nrows, diag, L.lmin, L.lmax, L.post, false, b, &cur, alt, d, dst, sub, st);
+    rc = mg_smooth(o, L.nrows, diag, L.lmin, L.lmax, L.post, false, b, &cur, alt, d, dst, sub, st, xch);
     if (rc) return rc;
     *res = cur;
     return MPBP_OK;
@@ -3457,12 +3667,14 @@ int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag
                 double* dir, bool profile, const double* x0_pre = nullptr) {
     if (in.kind == MPBP_INNER_MG) {   // one GPU: V-cycles whose level 0 is this operator
         const mpbp_mg* m = kind == MPBP_VEC_VELOCITY ? c.p->mg_F : c.p->mg_P;
-        // (one GPU: op.in covers every row -- the assembled layouts' boundary part is an empty block list)
-        if (!m || c.p->halo)
-            return set_error(MPBP_ERR_ARG, "schur_apply: a multigrid inner solve needs plan.mg_%s on one GPU",
+        if (!m)
+            return set_error(MPBP_ERR_ARG, "schur_apply: a multigrid inner solve needs plan.mg_%s",
                              kind == MPBP_VEC_VELOCITY ? "F" : "P");
+        if ((c.p->halo != nullptr) != (m->part_levels > 0))
+            return set_error(MPBP_ERR_ARG, "schur_apply: a %s apply needs a %s multigrid hierarchy",
+                             c.p->halo ? "row-partitioned" : "one-GPU", c.p->halo ? "row-partitioned" : "whole-grid");
         if (m->levels[0].nrows != nrows) return set_error(MPBP_ERR_ARG, "schur_apply: mg level 0 size mismatch");
-        const MgFine f{op.in, diag, ping, pong, m->levels[0].r, dir};
+        const MgFine f{op, diag, ping, pong, m->levels[0].r, dir, c.p->halo, c.p->halo_ctx, kind};
         return mg_solve(m, f, b, dst, sub, c.st);
     }
     const int K = in.sweeps;
@@ -3865,15 +4077,21 @@ int mpbp_mg_solve(const mpbp_mg* mg, const double* b, const double* sub, double*
     if (!mg || !b || !x_out || mg->nlevels < 2 || !mg->levels) return set_error(MPBP_ERR_ARG, "mg_solve: bad args");
     const mpbp_mg_level& L = mg->levels[0];
     if (check_csr(&L.A)) return MPBP_ERR_ARG;
+    if (mg->part_levels < 0 || mg->part_levels >= mg->nlevels || (mg->part_levels > 0 && (!mg->halo || !mg->gather)))
+        return set_error(MPBP_ERR_ARG, "mg_solve: part_levels must be in [0, nlevels) with halo and gather callbacks");
     for (int l = 0; l < mg->nlevels; ++l) {
         const mpbp_mg_level& Q = mg->levels[l];
         if (!Q.x || !Q.t || !Q.r || !Q.d || !Q.b || !Q.diag)
             return set_error(MPBP_ERR_ARG, "mg_solve: level %d is missing work vectors", l);
-        if (l + 1 < mg->nlevels && (Q.R.nrows != mg->levels[l + 1].nrows || Q.P.ncols != mg->levels[l + 1].nrows ||
-                                    Q.R.ncols != Q.nrows || Q.P.nrows != Q.nrows))
+        // (row-partitioned levels: the transfers' columns index the ghost layout, so only the row counts are checked)
+        const bool part = l < mg->part_levels;
+        if (l + 1 < mg->nlevels && (Q.P.nrows != Q.nrows ||
+                                    (!part && (Q.R.nrows != mg->levels[l + 1].nrows || Q.P.ncols != mg->levels[l + 1].nrows ||
+                                               Q.R.ncols != Q.nrows))))
             return set_error(MPBP_ERR_ARG, "mg_solve: transfer shapes of level %d do not match", l);
     }
-    const MgFine f{mg_level_op(L), L.diag, L.x, L.t, L.r, L.d};
+    const MgFine f{mg_level_op(L), L.diag, L.x, L.t, L.r, L.d, mg->part_levels > 0 ? mg->halo : nullptr, mg->halo_ctx,
+                   L.halo_kind};
     return mg_solve(mg, f, b, x_out, sub, as_stream(stream));
 }
 

@@ -48,14 +48,27 @@ class RowPartition:
     world: int
     rank: int
     ghosts: bool = False   # ghost slots even at world = 1 (the periodic self-exchange; tests the halo path)
+    bounds: tuple | None = None   # explicit ((r0, rows) per rank); default: n split evenly (the first n % world +1)
 
     def __post_init__(self):
         self.ghosts = self.ghosts or self.world > 1
-        base, rem = divmod(self.n, self.world)
-        self.r0 = self.rank * base + min(self.rank, rem)
-        self.L = base + (1 if self.rank < rem else 0)
+        if self.bounds is None:
+            base, rem = divmod(self.n, self.world)
+            self.bounds = tuple((k * base + min(k, rem), base + (1 if k < rem else 0)) for k in range(self.world))
+        self.bounds = tuple((int(a), int(b)) for a, b in self.bounds)
+        if len(self.bounds) != self.world or sum(b for _, b in self.bounds) != self.n:
+            raise ValueError(f"row bounds {self.bounds} do not cover the {self.n} grid rows once")
+        self.r0, self.L = self.bounds[self.rank]
         self.r1 = self.r0 + self.L
-        self.min_rows = base
+        self.min_rows = min(b for _, b in self.bounds)
+
+    def coarse(self, levels: int = 1) -> "RowPartition | None":
+        """The same ranks' rows of the grid coarsened `levels` times by 2 (rows [r0 / 2^l, r1 / 2^l)), or None when
+        some rank's rows do not halve exactly."""
+        f = 1 << levels
+        if self.n % f or any(a % f or b % f for a, b in self.bounds):
+            return None
+        return RowPartition(self.n // f, self.world, self.rank, self.ghosts, tuple((a // f, b // f) for a, b in self.bounds))
 
     @property
     def N(self):
@@ -112,6 +125,19 @@ def halo_reach(row_ptr: torch.Tensor, col_idx: torch.Tensor, row_gid: torch.Tens
     cgr = (col_idx.to(torch.int64) % N) // n
     d = torch.remainder(cgr - rgr, n)
     return int(torch.minimum(d, n - d).max().item())
+
+
+def ghost_depth(col_idx: torch.Tensor, n: int, r0: int, L: int) -> int:
+    """Deepest ghost row the columns `col_idx` (global ids of stacked n x n fields) reach outside the owned grid
+    rows [r0, r0 + L), periodic; 0 when every column is owned."""
+    if col_idx.numel() == 0:
+        return 0
+    gr = (col_idx.to(torch.int64) % (n * n)) // n
+    above = torch.remainder(r0 - gr, n)          # rows above r0 (1 = the row just above)
+    below = torch.remainder(gr - (r0 + L - 1), n)   # rows below the last owned row
+    inside = torch.remainder(gr - r0, n) < L
+    d = torch.where(inside, torch.zeros_like(gr), torch.minimum(above, below))
+    return int(d.max().item())
 
 
 def boundary_ranges(row_ptr: torch.Tensor, col_idx: torch.Tensor, n_owned_cols: int):
@@ -178,6 +204,33 @@ class HaloExchanger:
         self.end(x_ext)
 
 
+class Gatherer:
+    """All-gather of a row-partitioned nf-field vector into the whole field-major vector (gloo / host-staged; the
+    RCCL form is mpbp_halo_allgather): rank k owns rows [r0_k, r0_k + L_k) of every field of an n x n grid."""
+
+    def __init__(self, nf: int, n: int, bounds, rank: int, group=None):
+        import torch.distributed as dist
+        self.dist, self.group, self.nf, self.n, self.rank = dist, group, nf, n, rank
+        self.bounds = tuple(bounds)
+        self.lmax = max(b for _, b in self.bounds)
+        per = nf * self.lmax * n
+        self.send = torch.zeros(per, dtype=torch.float64)
+        self.recv = torch.zeros(len(self.bounds) * per, dtype=torch.float64)
+        idx = np.empty(nf * n * n, dtype=np.int64)
+        for k, (r0, L) in enumerate(self.bounds):
+            for f in range(nf):
+                idx[f * n * n + r0 * n: f * n * n + (r0 + L) * n] = k * per + f * self.lmax * n + np.arange(L * n)
+        self.idx = torch.from_numpy(idx)
+
+    def gather(self, x_owned: torch.Tensor, x_full: torch.Tensor):
+        L = self.bounds[self.rank][1]
+        own = x_owned[: self.nf * L * self.n].view(self.nf, L * self.n).cpu()
+        self.send.view(self.nf, self.lmax * self.n)[:, : L * self.n] = own
+        chunks = list(self.recv.view(len(self.bounds), -1).unbind(0))
+        self.dist.all_gather(chunks, self.send, group=self.group)
+        x_full[: self.idx.numel()] = self.recv[self.idx].to(x_full.device)
+
+
 def rccl_library_path() -> str:
     """The RCCL torch itself loaded (one RCCL per process), else ROCm's."""
     p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
@@ -212,6 +265,20 @@ class RcclHalo:
         self.overlap = overlap
         self.fn = _lib.HALO_FN(ctypes.cast(lib().mpbp_halo_exchange, ctypes.c_void_p).value)
         self.pair_fn = _lib.HALO_PAIR_FN(ctypes.cast(lib().mpbp_halo_exchange_pair, ctypes.c_void_p).value)
+        self.gather_fn = _lib.GATHER_FN(ctypes.cast(lib().mpbp_halo_allgather, ctypes.c_void_p).value)
+
+    def add_kind(self, part: RowPartition, nfields: int, h: int, overlap: bool | None = None) -> int:
+        """Another vector layout on this communicator (mpbp_halo_add_kind); returns its kind id."""
+        ov = self.overlap if overlap is None else overlap
+        return check(lib().mpbp_halo_add_kind(self.handle, nfields, part.n, part.r0, part.L, h,
+                                              _lib.HALO_OVERLAP if ov else _lib.HALO_IN_ORDER))
+
+    def add_gather(self, nfields: int, n: int, bounds) -> int:
+        """An all-gather layout (mpbp_halo_add_gather): bounds = ((r0, rows) per rank)."""
+        r0s = np.ascontiguousarray([a for a, _ in bounds], dtype=np.int32)
+        rows = np.ascontiguousarray([b for _, b in bounds], dtype=np.int32)
+        return check(lib().mpbp_halo_add_gather(self.handle, nfields, n, r0s.ctypes.data_as(ctypes.c_void_p),
+                                                rows.ctypes.data_as(ctypes.c_void_p)))
 
     def check(self):
         if lib().mpbp_halo_status(self.handle) != 0:
@@ -229,17 +296,310 @@ class RcclHalo:
             pass
 
 
+class _Halos:
+    """The ghost-row exchanges and all-gathers of one partitioned object: RCCL (libmpbp's halo object; the callbacks
+    are its C functions) or torch / gloo (host-staged; Python callbacks looked up by vector address)."""
+
+    def __init__(self, impl: str, rccl: "RcclHalo | None", group, device):
+        self.impl, self.rccl, self.group, self.device = impl, rccl, group, torch.device(device)
+        self._ex, self._gather, self._tensors = {}, {}, {}
+        if rccl is not None:
+            self.fn, self.gather_fn, self.ctx = rccl.fn, rccl.gather_fn, rccl.handle
+        else:
+            self.fn = _lib.HALO_FN(self._halo)
+            self.gather_fn = _lib.GATHER_FN(self._allgather)
+            self.ctx = None
+
+    def add_kind(self, part: RowPartition, nfields: int, h: int, kind: int | None = None) -> int:
+        if self.rccl is not None:
+            return self.rccl.add_kind(part, nfields, h) if kind is None else kind
+        k = len(self._ex) if kind is None else kind
+        while kind is None and k in self._ex:
+            k += 1
+        self._ex[k] = HaloExchanger(part, nfields, h, self.device, self.group)
+        return k
+
+    def add_gather(self, nfields: int, n: int, bounds, rank: int) -> int:
+        if self.rccl is not None:
+            return self.rccl.add_gather(nfields, n, bounds)
+        g = len(self._gather)
+        self._gather[g] = Gatherer(nfields, n, bounds, rank, self.group)
+        return g
+
+    def register(self, *tensors):
+        for t in tensors:
+            self._tensors[t.data_ptr()] = t
+
+    def _halo(self, ctx, kind, x_ptr, phase, stream):
+        x = self._tensors[int(x_ptr)]
+        ex = self._ex[int(kind)]
+        if phase == _lib.HALO_BEGIN:
+            ex.begin(x)
+        else:
+            ex.end(x)
+
+    def _allgather(self, ctx, gid, own_ptr, full_ptr, stream):
+        self._gather[int(gid)].gather(self._tensors[int(own_ptr)], self._tensors[int(full_ptr)])
+
+
+class PartitionedMultigrid:
+    """A multigrid hierarchy (mg.Multigrid, built on every rank from the global operator -- setup only) split over a
+    row partition for the partitioned Schur apply (solve.py:266 / 274's pointer, under north_star's row partition).
+
+    Level l + 1's rows of rank k are [ceil(r0 / 2), ceil(r1 / 2)) of its level-l rows [r0, r1) (exact halving when
+    the rows are even; a disjoint cover of the coarse grid in any case).  Levels [0, part_levels) are row-partitioned:
+    their operator, restriction and prolongation rows extracted with the columns renumbered into the ghost layout
+    (entry order kept), their vectors owned + ghost rows, ghost depths measured from the columns.  The restriction
+    into level part_levels leaves each rank's rows of that level, all-gathered into the whole level; the coarser
+    levels (and the dense coarsest inverse) run replicated on every rank.  Every operation is the one-GPU hierarchy's
+    on the same operands: bit-identical to Multigrid.solve / the one-GPU apply.  Partitioning stops at the coarsest
+    level, where a rank would hold fewer rows than the ghost depth, or below min_cells unknowns per rank."""
+
+    def __init__(self, g, part: RowPartition, nfields: int, group=None, min_cells: int = 1 << 14,
+                 max_part_levels: int | None = None):
+        self.g, self.part0, self.nf, self.group = g, part, nfields, group
+        dev = g.device
+        self.device = dev
+        nl = g.nlevels
+        self.parts = [part]
+        for l in range(1, nl):
+            p = self.parts[-1]
+            b = tuple(((a + 1) // 2, (a + L + 1) // 2 - (a + 1) // 2) for a, L in p.bounds)
+            self.parts.append(RowPartition(g.sizes[l], part.world, part.rank, part.ghosts, b))
+        world = part.world
+
+        def owned(l):
+            return torch.from_numpy(self.parts[l].owned_rows(nfields).astype(np.int32)).to(dev)
+
+        def depth(M, rows, l):   # ghost rows of level l read by M's rows `rows` (M's columns at level l)
+            if world == 1:
+                return 1
+            full = M.extract(rows, torch.arange(M.shape[1], dtype=torch.int32, device=dev), M.shape[1])
+            q = self.parts[l]
+            return ghost_depth(full.col_idx, q.n, q.r0, q.L)
+
+        def reduce_max(v):
+            if world == 1:
+                return v
+            import torch.distributed as dist
+            t = torch.tensor([v], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            return int(t.item())
+
+        self.h0 = reduce_max(max(1, depth(g.R[0], owned(1), 0)))   # level 0 ghosts the restriction reads
+        self.h = [self.h0]
+        P = nl - 1
+        cap = nl - 1 if max_part_levels is None else max(1, min(nl - 1, max_part_levels))
+        for l in range(1, nl - 1):
+            q = self.parts[l]
+            cells = nfields * q.n * q.n // world
+            hl = reduce_max(max(1, depth(g.ops[l], owned(l), l), depth(g.R[l], owned(l + 1), l),
+                                depth(g.P[l - 1], owned(l - 1), l)))
+            if l >= cap or cells < min_cells or q.min_rows < hl:
+                P = l
+                break
+            self.h.append(hl)
+        self.part_levels = P
+        self._owned = owned
+
+    def build(self, halos: _Halos, level0, diag0, h0: int, kind0: int | None = None, A0=None, cycles=None):
+        """Local operators, vectors and the mpbp_mg struct.  level0: (x, t) iterate buffers of level 0 (owned + ghost
+        rows at depth h0 >= self.h0; inside the Schur apply its own); diag0: level 0's owned diagonal; kind0: level 0's
+        halo kind (the Schur apply's velocity / pressure kind; None: a new one); A0: level 0's local operator for the
+        standalone solve (mpbp_mg_solve; None inside the Schur apply, whose level 0 is its own operator)."""
+        g, nf, P, dev = self.g, self.nf, self.part_levels, self.device
+        if h0 < self.h0:
+            raise ValueError(f"level 0 ghost depth {h0} < the restriction's {self.h0}")
+        self.h[0] = h0
+        from .mg import sell_copy
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.kinds, self.local, self.work = [], [], []
+        for l in range(P):
+            q = self.parts[l]
+            self.kinds.append(halos.add_kind(q, nf, self.h[l]) if (l > 0 or kind0 is None) else kind0)
+        gather_bounds = self.parts[P].bounds
+        self.gather_kind = halos.add_gather(nf, self.parts[P].n, gather_bounds, self.part0.rank)
+        self._levels = (_lib.MgLevel * g.nlevels)()
+        empty_sell = _lib.Sell(0, 0, 0, 0, None, None, None, None)
+        keep = []
+        for l in range(g.nlevels):
+            L = self._levels[l]
+            L.pre, L.post = g.pre, g.post
+            L.lmin, L.lmax = g.bounds[l]
+            if l >= P:   # replicated: the global level as it stands
+                G = g._levels[l]
+                for name, _ in _lib.MgLevel._fields_:
+                    setattr(L, name, getattr(G, name))
+                continue
+            q = self.parts[l]
+            rows = self._owned(l)
+            ext = q.n_ext(nf, self.h[l])
+            cm = torch.from_numpy(q.colmap(nf, self.h[l])).to(dev)
+            if l + 1 < P:
+                qn = self.parts[l + 1]
+                cm_next = torch.from_numpy(qn.colmap(nf, self.h[l + 1])).to(dev)
+                ext_next = qn.n_ext(nf, self.h[l + 1])
+            else:
+                ncoarse = g.ops[l + 1].shape[0]
+                cm_next, ext_next = torch.arange(ncoarse, dtype=torch.int32, device=dev), ncoarse
+            R = g.R[l].extract(self._owned(l + 1), cm, ext)
+            Pm = g.P[l].extract(rows, cm_next, ext_next)
+            own = q.n_owned(nf)
+            L.nrows = own
+            if l == 0:
+                L.A = A0.cstruct() if A0 is not None else _lib.Csr(0, 0, 0, None, None, None)
+                L.A_blocks = A0.blocks.cstruct() if A0 is not None else _lib.RowBlocks(None, 0)
+                L.diag = diag0.data_ptr()
+                SA = sell_copy(A0) if A0 is not None else None
+                L.A_sell = SA.cstruct() if SA is not None else empty_sell
+                keep += [A0, SA, diag0]
+                x, t = level0
+                r = torch.zeros(ext, **f64)
+                d, bb = torch.zeros(own, **f64), torch.zeros(own, **f64)
+            else:
+                A = g.ops[l].extract(rows, cm, ext)
+                dg = g.diags[l][rows.long()].contiguous()
+                L.A, L.A_blocks, L.diag = A.cstruct(), A.blocks.cstruct(), dg.data_ptr()
+                SA = sell_copy(A)
+                L.A_sell = SA.cstruct() if SA is not None else empty_sell
+                keep += [A, dg, SA]
+                x, t, r = (torch.zeros(ext, **f64) for _ in range(3))
+                d, bb = torch.zeros(own, **f64), torch.zeros(own, **f64)
+            SR, SP = sell_copy(R), sell_copy(Pm)
+            L.R, L.R_blocks, L.P, L.P_blocks = R.cstruct(), R.blocks.cstruct(), Pm.cstruct(), Pm.blocks.cstruct()
+            L.R_sell = SR.cstruct() if SR is not None else empty_sell
+            L.P_sell = SP.cstruct() if SP is not None else empty_sell
+            keep += [R, Pm, SR, SP]
+            L.x, L.t, L.r, L.d, L.b = (v.data_ptr() for v in (x, t, r, d, bb))
+            L.halo_kind = self.kinds[l]
+            self.work.append((x, t, r, d, bb))
+            halos.register(x, t, r, d, bb)
+        # the gather level's r (the rank's rows, written by the restriction) and b (the whole level) are the global
+        # level's full-size buffers
+        Gw = g.work[P]
+        halos.register(*Gw)
+        self._keep = keep
+        self._halos = halos
+        self._mg = _lib.Mg(g.nlevels, g.cycles if cycles is None else cycles,
+                           ctypes.cast(self._levels, ctypes.POINTER(_lib.MgLevel)),
+                           g.coarse_inv.cstruct(), g.coarse_inv.blocks.cstruct(),
+                           g.coarse_dense.data_ptr() if g.coarse_dense is not None else None,
+                           P, self.gather_kind, halos.fn, halos.ctx, halos.gather_fn)
+        return self
+
+    def cstruct(self):
+        return self._mg
+
+
+def _dist_info(group):
+    import torch.distributed as dist
+    return dist, dist.get_world_size(group), dist.get_rank(group), dist.get_backend(group)
+
+
+class DistributedMatrix:
+    """A row-partitioned operator of the MAC-grid system: the operator matvec b = A u of apply.py:72 and the FGMRES
+    operator of solve.py:285 (A @ xk, solve.py:166) over the ranks of `group`, one per GPU.
+
+    Rank k holds the rows of grid rows [r0, r1) of every one of `nfields` stacked n x n fields (A: the 5 fields
+    [u_n, v_n, u_s, v_s, p]), columns renumbered into the owned + ghost ("ext") layout (DeviceCSR.extract keeps each
+    row's entry order: every local row sum is the global one, bit for bit).  apply(x) takes and returns the rank's
+    owned entries: x is copied into the ext buffer, the ghost rows are exchanged (RCCL neighbour point-to-point over
+    xGMI -- overlap=True: on the halo's own high-priority stream, forked before and joined after the interior rows'
+    SpMV, so the transfer overlaps it), the interior rows (no ghost column) run on the CSR kernel meanwhile and the
+    boundary rows after the join.  With the gloo backend the ghosts are host-staged (HaloExchanger)."""
+
+    def __init__(self, M: DeviceCSR, n: int, nfields: int, group=None, halo: str = "auto", overlap: bool = True,
+                 self_halo: bool = False):
+        dist, world, rank, backend = _dist_info(group)
+        dev = M.device
+        if M.shape != (nfields * n * n, nfields * n * n):
+            raise ValueError(f"operator {M.shape} is not {nfields} fields of a {n} x {n} grid")
+        self.part = part = RowPartition(n, world, rank, ghosts=bool(self_halo))
+        self.nfields = nfields
+        self.partitioned = part.ghosts
+        self.halo_impl = halo if halo != "auto" else ("rccl" if backend == "nccl" else "torch")
+        rows = torch.from_numpy(part.owned_rows(nfields).astype(np.int32)).to(dev)
+        full = M.extract(rows, torch.arange(M.shape[1], dtype=torch.int32, device=dev), M.shape[1])
+        self.h = max(1, ghost_depth(full.col_idx, n, part.r0, part.L) if world > 1 else 1)
+        del full
+        self.n_own = part.n_owned(nfields)
+        self.n_ext = part.n_ext(nfields, self.h)
+        self.shape = (self.n_own, self.n_own)
+        self.A = M.extract(rows, torch.from_numpy(part.colmap(nfields, self.h)).to(dev), self.n_ext) \
+            if self.partitioned else M
+        if self.partitioned and world > 1:
+            inner, bnd = boundary_ranges(self.A.row_ptr, self.A.col_idx, self.n_own)
+        elif self.partitioned:   # one rank exchanging with itself: every row with a wrapped neighbour reads ghosts
+            inner, bnd = boundary_ranges(self.A.row_ptr, self.A.col_idx, self.n_own)
+        else:
+            inner, bnd = [(0, self.n_own)], []
+        self.blk_in = self.A.plan_blocks(rows=inner) if inner else None
+        self.blk_bd = self.A.plan_blocks(rows=bnd) if bnd else None
+        self.xe = torch.zeros(self.n_ext, dtype=torch.float64, device=dev)
+        self._rccl = self._ex = None
+        if self.partitioned:
+            if self.halo_impl == "rccl":
+                self._rccl = RcclHalo(part, 1, 1, group, overlap=False)
+                self.kind = self._rccl.add_kind(part, nfields, self.h, overlap=overlap)
+            else:
+                self._ex = HaloExchanger(part, nfields, self.h, dev, group)
+
+    @property
+    def device(self):
+        return self.xe.device
+
+    def apply(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        assert x.is_cuda and x.dtype == torch.float64 and x.numel() == self.n_own
+        if out is None:
+            out = torch.empty(self.n_own, dtype=torch.float64, device=x.device)
+        if not self.partitioned:
+            return self.A.matvec(x, out=out)
+        self.xe[: self.n_own].copy_(x)
+        st = stream_handle()
+        if self._rccl is not None:
+            lib().mpbp_halo_exchange(self._rccl.handle, self.kind, ptr(self.xe), _lib.HALO_BEGIN, st)
+        else:
+            self._ex.begin(self.xe)
+        if self.blk_in is not None:
+            self.A.matvec(self.xe, out=out, blocks=self.blk_in)
+        if self._rccl is not None:
+            lib().mpbp_halo_exchange(self._rccl.handle, self.kind, ptr(self.xe), _lib.HALO_END, st)
+        else:
+            self._ex.end(self.xe)
+        if self.blk_bd is not None:
+            self.A.matvec(self.xe, out=out, blocks=self.blk_bd)
+        if self._rccl is not None:
+            self._rccl.check()
+        return out
+
+    matvec = apply
+
+    def close(self):
+        if self._rccl is not None:
+            self._rccl.close()
+            self._rccl = None
+
+    def local_to_global_rows(self):
+        return self.part.owned_rows(self.nfields)
+
+
 class DistributedSchurPreconditioner(PlanProfiling):
     """The approximate-commutator apply over a row partition of the grid (one rank per GPU).
 
     Every rank assembles the global operators in its own HBM (setup only), keeps its rows with
     columns renumbered into the owned+ghost layout, and runs ``mpbp_schur_apply`` with halo
     callbacks; v and the result hold the rank's owned unknowns [u_n, v_n, u_s, v_s, p] rows r0..r1.
+    Inner solves: Jacobi / Chebyshev (the communication-avoiding schedule by default) or multigrid ("mg": one
+    PartitionedMultigrid per inner inverse, ghost rows exchanged per operator, the coarse levels replicated).
+
+    Graph capture (``capture``) needs the in-order RCCL halo.  A communicator whose exchanges were captured is kept
+    until the process exits (``close`` does not destroy it: with RCCL 2.26.6 ncclCommDestroy never returns once a
+    graph holding its point-to-point kernels has been instantiated and destroyed; csrc/halo.cpp).
     """
 
     def __init__(self, n, xi, eta_n, eta_s, c=1.0, d_u=-1.0, inner_F=None, inner_P=None, group=None,
                  device=None, layout="sell", f_mode="auto", pg_mode="auto", halo="auto", self_halo=False,
-                 halo_overlap=False, ca="auto", fuse_g=True):
+                 halo_overlap=False, ca="auto", fuse_g=True, mg_min_cells=1 << 14, mg_part_levels=None):
         import torch.distributed as dist
         from .preconditioner import MultiphaseBlockPreconditioner
         from .solve import InnerSolver
@@ -267,6 +627,7 @@ class DistributedSchurPreconditioner(PlanProfiling):
         # inner-solver bounds from the global operators: identical on every rank
         self.inner_F = (inner_F or InnerSolver()).resolve(F, F.diagonal())
         self.inner_P = (inner_P or InnerSolver()).resolve(GtG, GtG.diagonal())
+        mg_any = "mg" in (self.inner_F.kind, self.inner_P.kind)
         rows_u = torch.from_numpy(part.owned_rows(N_VEL_FIELDS).astype(np.int32)).to(dev)
         rows_p = torch.from_numpy(part.owned_rows(N_P_FIELDS).astype(np.int32)).to(dev)
 
@@ -277,12 +638,30 @@ class DistributedSchurPreconditioner(PlanProfiling):
         q = reach(GtFG, rows_p)
         self.h_u = max(1, reach(F, rows_u), reach(D, rows_p))
         self.h_p = max(1, reach(G, rows_u), reach(GtG, rows_p), q)
+        # multigrid inner solves: the global hierarchies (every rank, setup only), split over the partition; level 0's
+        # ghost layout must also serve the restriction's reach
+        self.mg_F = self.mg_P = None
+        if mg_any:
+            from .mg import FIELDS_PRESSURE, FIELDS_VELOCITY
+            if ca is True:
+                raise ValueError("ca=True needs Jacobi / Chebyshev inner solves (multigrid exchanges per operator)")
+            kw = dict(group=group, min_cells=mg_min_cells, max_part_levels=mg_part_levels)
+            if self.inner_F.kind == "mg":
+                gF = self.inner_F.multigrid(F, n, FIELDS_VELOCITY, F.diagonal())
+                self.mg_F = PartitionedMultigrid(gF, part, N_VEL_FIELDS, **kw) if self.partitioned else gF
+            if self.inner_P.kind == "mg":
+                gP = self.inner_P.multigrid(GtG, n, FIELDS_PRESSURE, GtG.diagonal())
+                self.mg_P = PartitionedMultigrid(gP, part, N_P_FIELDS, **kw) if self.partitioned else gP
+            if isinstance(self.mg_F, PartitionedMultigrid):
+                self.h_u = max(self.h_u, self.mg_F.h0)
+            if isinstance(self.mg_P, PartitionedMultigrid):
+                self.h_p = max(self.h_p, self.mg_P.h0)
         # communication-avoiding schedule (mpbp_schur_plan.ca): v's halo and x_b's halo only, deep enough for
         # every matrix-free operator to also compute the ghost rows its successors read
         if ca not in ("auto", True, False):
             raise ValueError("ca must be 'auto', True or False")
         self.ca, self.ca_q = False, q
-        if ca and part.ghosts and self.f_stencil is not None and self.pg_stencil is not None:
+        if ca and not mg_any and part.ghosts and self.f_stencil is not None and self.pg_stencil is not None:
             sf, sp = self.inner_F.sweeps - 1, self.inner_P.sweeps - 1
             hu, hp = q + sp + 1 + sf, max(q + sp, sf + 1 + sp, q)
             if max(hu, hp) <= part.min_rows:
@@ -337,27 +716,26 @@ class DistributedSchurPreconditioner(PlanProfiling):
         self._wu_owned = torch.zeros(nu, **f64)
         self._wp = [torch.zeros(np_ext, **f64) for _ in range(7)]
         self._wu_ext = torch.zeros(nu_ext if self.ca else 0, **f64)
-        self._tensors = {t.data_ptr(): t for t in self._wu + self._wp + ([self._wu_ext] if self.ca else [])}
         self._rccl = None
-        if not self.partitioned:
-            self._cb = _lib.HALO_FN()
-        elif self.halo_impl == "rccl":
-            self._rccl = RcclHalo(part, self.h_u, self.h_p, group, overlap=halo_overlap)
-            self._cb = self._rccl.fn
+        self._halos = None
+        if self.partitioned:
+            if self.halo_impl == "rccl":
+                self._rccl = RcclHalo(part, self.h_u, self.h_p, group, overlap=halo_overlap)
+            self._halos = _Halos(self.halo_impl, self._rccl, group, dev)
+            if self._rccl is None:
+                self._halos.add_kind(part, N_VEL_FIELDS, self.h_u, kind=_lib.VEC_VELOCITY)
+                self._halos.add_kind(part, N_P_FIELDS, self.h_p, kind=_lib.VEC_PRESSURE)
+            self._halos.register(*self._wu, *self._wp, *([self._wu_ext] if self.ca else []))
+            self._cb = self._halos.fn
+            # multigrid under the partition: level 0 is the apply's own F / Gt_G with its ping / pong buffers
+            if isinstance(self.mg_F, PartitionedMultigrid):
+                self.mg_F.build(self._halos, (self._wu[1], self._wu[2]), self.diag_F, self.h_u, kind0=_lib.VEC_VELOCITY)
+            if isinstance(self.mg_P, PartitionedMultigrid):
+                self.mg_P.build(self._halos, (self._wp[4], self._wp[5]), self.diag_P, self.h_p, kind0=_lib.VEC_PRESSURE)
         else:
-            self._ex = {_lib.VEC_VELOCITY: HaloExchanger(part, N_VEL_FIELDS, self.h_u, dev, group),
-                        _lib.VEC_PRESSURE: HaloExchanger(part, N_P_FIELDS, self.h_p, dev, group)}
-            self._cb = _lib.HALO_FN(self._halo)
+            self._cb = _lib.HALO_FN()
         self._prof = None
         self._plan = self._make_plan(world)
-
-    def _halo(self, ctx, kind, x_ptr, phase, stream):
-        x = self._tensors[int(x_ptr)]
-        ex = self._ex[int(kind)]
-        if phase == _lib.HALO_BEGIN:
-            ex.begin(x)
-        else:
-            ex.end(x)
 
     def _make_plan(self, world):
         p = _lib.SchurPlan()
@@ -400,6 +778,10 @@ class DistributedSchurPreconditioner(PlanProfiling):
         p.p_part = _lib.RowPart(self.part.r0, self.part.L, self.h_p if ghost else 0, 0)
         p.halo = self._cb
         p.halo_ctx = self._rccl.handle if self._rccl is not None else None
+        if self.mg_F is not None:
+            p.mg_F = ctypes.pointer(self.mg_F.cstruct())
+        if self.mg_P is not None:
+            p.mg_P = ctypes.pointer(self.mg_P.cstruct())
         # the in-order RCCL schedule gains nothing from splitting rows around the exchange: exchange first,
         # then one launch per sweep
         p.halo_first = 1 if (self._rccl is not None and not self._rccl.overlap) else 0
@@ -447,3 +829,33 @@ class DistributedSchurPreconditioner(PlanProfiling):
         """Global ids (in the [u_n, v_n, u_s, v_s, p] numbering) of this rank's v / out entries."""
         return np.concatenate([self.part.owned_rows(N_VEL_FIELDS),
                                4 * self.part.N + self.part.owned_rows(N_P_FIELDS)])
+
+
+def solve_distributed(n, xi, etan, etas, c=1.0, d=-1.0, b_vec=None, inner_F=None, inner_P=None, tol=1e-8,
+                      maxiter=150, restrt=None, group=None, self_halo=False, **pc_kw):
+    """solve.py:240-286 over a row partition (one rank per GPU): FGMRES (solve.fgmres over `group`) on the partitioned
+    operator A (DistributedMatrix) with the partitioned approximate-commutator preconditioner
+    (DistributedSchurPreconditioner).  b_vec: the global right-hand side on the host (default: the manufactured problem
+    of solve.py:52-80).  The solve is the one-GPU solve's, bit for bit (reproducible inner products).  Returns a dict:
+    x_local (this rank's rows of the iterate, CUDA), rows (their global ids), info, residuals, A, M."""
+    import torch.distributed as dist
+    from .preconditioner import MultiphaseBlockPreconditioner
+    from .solve import fgmres
+    from .utils import manufactured_problem
+    bp = MultiphaseBlockPreconditioner(n, xi, etan, etas)
+    A = bp.get_big_A_matrix(c=c, d_u=d)[0]
+    dA = DistributedMatrix(A, n, 5, group=group, self_halo=self_halo)
+    del A, bp
+    torch.cuda.empty_cache()
+    M = DistributedSchurPreconditioner(n, xi, etan, etas, c=c, d_u=d, inner_F=inner_F, inner_P=inner_P, group=group,
+                                       self_halo=self_halo, **pc_kw)
+    if b_vec is None:
+        _, b_vec = manufactured_problem(n, c, d, xi, etan, etas)
+    rows = dA.local_to_global_rows()
+    assert np.array_equal(rows, M.local_to_global_rows())
+    b = torch.from_numpy(np.ascontiguousarray(np.asarray(b_vec, dtype=np.float64)[rows])).cuda()
+    world = dist.get_world_size(group)
+    kgroup = (group if group is not None else dist.group.WORLD) if world > 1 else None
+    hist = []
+    x, info = fgmres(dA, b, M=M, tol=tol, maxiter=maxiter, restrt=restrt, residuals=hist, group=kgroup)
+    return {"x_local": x, "rows": rows, "info": info, "residuals": hist, "A": dA, "M": M}

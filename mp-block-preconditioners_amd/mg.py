@@ -61,8 +61,15 @@ def sell_copy(A: DeviceCSR) -> DeviceSELL | None:
     return A.to_sell()
 
 
+MAX_COARSE_ROWS = 8192   # the coarsest level's dense pseudo-inverse: 8192^2 doubles = 512 MB, an O(m^3) host pinv
+
+
 def dense_inverse_csr(A: DeviceCSR) -> tuple[DeviceCSR, np.ndarray]:
     """The pseudo-inverse of a small operator as a CSR with every entry stored (rows of ncols entries)."""
+    if A.shape[0] > MAX_COARSE_ROWS:
+        raise ValueError(f"coarsest level has {A.shape[0]} rows (> {MAX_COARSE_ROWS}): its dense pseudo-inverse would "
+                         f"need {A.shape[0] ** 2 * 8 / 1e9:.1f} GB and an O(m^3) factorisation; coarsening stops at an odd "
+                         "grid size, so use a grid n = m 2^k with a small m (or a larger `coarsest`)")
     Ad = A.to_scipy().toarray()
     inv = np.ascontiguousarray(np.linalg.pinv(Ad))
     m = inv.shape[0]
@@ -72,6 +79,16 @@ def dense_inverse_csr(A: DeviceCSR) -> tuple[DeviceCSR, np.ndarray]:
     M = DeviceCSR(torch.from_numpy(rp).to(dev), torch.from_numpy(ci).to(dev),
                   torch.from_numpy(inv.reshape(-1).copy()).to(dev), (m, m), row_ptr_host=rp)
     return M, inv
+
+
+def level_sizes(n: int, coarsest: int) -> list[int]:
+    """Grid sizes of the hierarchy: halve while even, down to <= coarsest (at least one coarsening)."""
+    sizes = [n]
+    m = n
+    while not (m % 2 or (m <= coarsest and len(sizes) > 1) or m // 2 < 2):
+        m //= 2
+        sizes.append(m)
+    return sizes
 
 
 class Multigrid:
@@ -99,6 +116,10 @@ class Multigrid:
         self.coarsest = coarsest
         dev = A.device
         self.device = dev
+        sizes = level_sizes(n, coarsest)
+        if nf * sizes[-1] ** 2 > MAX_COARSE_ROWS:   # refuse before any Galerkin product is formed
+            raise ValueError(f"grid {n} coarsens to {sizes} (stopping at an odd size): the coarsest level's "
+                             f"{nf * sizes[-1] ** 2} rows exceed the dense inverse's {MAX_COARSE_ROWS}")
         self.ops, self.diags, self.R, self.P, self.bounds, self.sizes = [], [], [], [], [], []
         m = n
         while True:

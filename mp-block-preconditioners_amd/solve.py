@@ -351,15 +351,109 @@ def _as_operator(A):
         return None
     if isinstance(A, DeviceCSR):
         return lambda x, out=None: A.matvec(x, out=out)
-    if isinstance(A, ApproxSchurPreconditioner):
+    if hasattr(A, "apply"):   # ApproxSchurPreconditioner, DistributedSchurPreconditioner, DistributedMatrix
         return lambda x, out=None: A.apply(x, out=out)
     if callable(A):
         return lambda x, out=None: A(x)
     raise TypeError(f"unsupported operator {type(A)}")
 
 
+_KCHUNK = 256   # basis vectors per mpbp_rdot / mpbp_gs_update launch
+
+
+class KrylovKernels:
+    """FGMRES's vector kernels on CUDA float64 vectors through libmpbp, optionally over the ranks of a row partition.
+
+    Inner products are reproducible (``mpbp_rdot``: binned sums whose fold sums add exactly, so the result depends only
+    on the set of terms); their bounds are max-reductions and their fold sums sum-reductions over ``group``.  Every other
+    step is element-wise in a fixed order (``mpbp_gs_update``).  FGMRES therefore computes the same bits on one GPU and
+    on any row partition whose operator and preconditioner applies are bit-exact (DistributedMatrix,
+    DistributedSchurPreconditioner): same residual history, same iterate."""
+
+    def __init__(self, n: int, kmax: int, device, group=None):
+        self.n, self.group, self.kmax = int(n), group, int(kmax)
+        self.device = torch.device(device)
+        self.backend = None
+        n_total = self.n
+        if group is not None:
+            import torch.distributed as dist
+            self.dist = dist
+            self.backend = dist.get_backend(group)
+            t = torch.tensor([self.n], dtype=torch.int64)
+            t = self._reduce(t.to(self.device) if self.backend == "nccl" else t, "sum")
+            n_total = int(t.item())
+        self.n_total = n_total
+        f64 = dict(dtype=torch.float64, device=self.device)
+        self.part = torch.empty(max(1, int(lib().mpbp_rdot_part_size(self.n, min(self.kmax, _KCHUNK)))), **f64)
+        self.acc = torch.empty(3 * self.kmax, **f64)
+        self.h = torch.empty(self.kmax, **f64)
+
+    def _reduce(self, t: torch.Tensor, op: str) -> torch.Tensor:
+        if self.group is None:
+            return t
+        rop = self.dist.ReduceOp.SUM if op == "sum" else self.dist.ReduceOp.MAX
+        if self.backend == "nccl" or t.device.type == "cpu":
+            self.dist.all_reduce(t, op=rop, group=self.group)
+            return t
+        c = t.cpu()   # gloo: host-staged
+        self.dist.all_reduce(c, op=rop, group=self.group)
+        t.copy_(c)
+        return t
+
+    def amax(self, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """out[0] = max |x| over every rank."""
+        check(lib().mpbp_absmax(ptr(x), x.numel(), ptr(out), stream_handle()))
+        return self._reduce(out, "max")
+
+    def fold_sums(self, V: torch.Tensor, ld: int, k: int, w: torch.Tensor, vb: torch.Tensor, wb: torch.Tensor):
+        """acc[:3k]: the exact fold sums of V[i] . w over every rank (basis rows in chunks of 256 per launch)."""
+        for i0 in range(0, k, _KCHUNK):
+            kc = min(_KCHUNK, k - i0)
+            check(lib().mpbp_rdot(ctypes.c_void_p(V.data_ptr() + 8 * i0 * ld), ld, kc, ptr(w), self.n, self.n_total,
+                                  ctypes.c_void_p(vb.data_ptr() + 8 * i0), ptr(wb), ptr(self.part),
+                                  ctypes.c_void_p(self.acc.data_ptr() + 24 * i0), stream_handle()))
+        return self._reduce(self.acc[: 3 * k], "sum")
+
+    def dots(self, V, ld, k, w, vb, wb) -> torch.Tensor:
+        """h[:k] = V[:k] w (device)."""
+        self.fold_sums(V, ld, k, w, vb, wb)
+        check(lib().mpbp_rdot_finish(k, ptr(self.acc), ptr(self.h), stream_handle()))
+        return self.h[:k]
+
+    def update(self, V, ld, k, h, w, out):
+        """out = w - V[:k]^T h (out may be w), the basis rows in chunks of 256 (a fixed order)."""
+        src = w
+        for i0 in range(0, k, _KCHUNK):
+            kc = min(_KCHUNK, k - i0)
+            check(lib().mpbp_gs_update(ctypes.c_void_p(V.data_ptr() + 8 * i0 * ld), ld, kc,
+                                       ctypes.c_void_p(h.data_ptr() + 8 * i0), ptr(src), self.n, ptr(out),
+                                       stream_handle()))
+            src = out
+        return out
+
+
+def _finish(a) -> float:
+    """h = (S0 + S1) + S2 from a fold-sum triple -- mpbp_rdot_finish's IEEE operations on the host."""
+    return (float(a[0]) + float(a[1])) + float(a[2])
+
+
+def _solve_upper(H, g, k):
+    """y = triu(H[:k, :k])^-1 g[:k] by back substitution in a fixed order (host IEEE arithmetic: the same bits on
+    every rank and in every process)."""
+    y = [0.0] * k
+    for i in range(k - 1, -1, -1):
+        t = float(g[i])
+        for j in range(i + 1, k):
+            t -= float(H[i, j]) * y[j]
+        y[i] = t / float(H[i, i])
+    return y
+
+
+_VB_SLACK = 1.0 + 2.0 ** -50   # |fl(w / s)| <= fl(max|w| / s) (1 + 2^-50): the new basis vector's bound
+
+
 def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=None, residuals=None,
-           capture_M=True):
+           capture_M=True, group=None, kernels=None):
     """Flexible GMRES with right preconditioning, all vectors in HBM.
 
     Same call shape as pyamg.krylov.fgmres (solve.py:207, 237, 285): convergence when the
@@ -368,75 +462,94 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
     tensor after every inner iteration (the reference's true-residual printer, solve.py:161-170).
     Orthogonalisation is classical Gram-Schmidt with one re-orthogonalisation pass (CGS2: two
     batched projections per iteration instead of j dependent dot products), each pass one sweep over
-    the basis through libmpbp's mpbp_gs_dot / mpbp_gs_update (HBM-speed, deterministic reductions).
+    the basis through libmpbp (``KrylovKernels``: reproducible inner products, ``mpbp_gs_update``).
     pyamg is not installed here, so iteration counts against pyamg itself are unpinned.
-    capture_M: an ApproxSchurPreconditioner M is captured once into a hipGraph and replayed per iteration (its
-    launches -- hundreds with multigrid inner solves -- then cost one graph launch; the iteration's host work never
-    starves the GPU); same results as eager applies.
+
+    group: the process group of a row partition -- b, x0 and the vectors A and M take and return are the rank's
+    owned rows (DistributedMatrix, DistributedSchurPreconditioner); the iterates are bit-identical to the one-GPU
+    solve's rows.  kernels: a KrylovKernels-compatible object (default: libmpbp's).
+    capture_M: an ApproxSchurPreconditioner M (or a partitioned one over the in-order RCCL halo) is captured once into
+    a hipGraph and replayed per iteration (its launches -- hundreds with multigrid inner solves -- then cost one graph
+    launch; the iteration's host work never starves the GPU); same results as eager applies.
     """
     Aop = _as_operator(A)
     Mop = _as_operator(M)
-    b_dev = b if isinstance(b, torch.Tensor) else None
-    if capture_M and isinstance(M, ApproxSchurPreconditioner) and (b_dev is None or b_dev.is_cuda):
-        m_in = torch.zeros(M.shape[0], dtype=torch.float64, device=M.device)
-        m_out = torch.empty_like(m_in)
-        m_graph = M.capture(m_in, m_out)
-
-        def Mop(x, out=None, _g=m_graph, _i=m_in, _o=m_out):   # noqa: F811
-            _i.copy_(x)
-            _g.replay()
-            return _o
     b = b if isinstance(b, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(b, dtype=np.float64)).cuda()
+    if kernels is None and not (b.is_cuda and b.dtype == torch.float64):
+        raise TypeError("fgmres runs on CUDA float64 vectors (libmpbp kernels); there is no CPU fallback")
     n = b.numel()
-    x = torch.zeros_like(b) if x0 is None else (
-        x0.clone() if isinstance(x0, torch.Tensor) else torch.from_numpy(np.asarray(x0, dtype=np.float64)).to(b.device))
     maxiter = int(maxiter) if maxiter is not None else min(n, 200)
     m = int(restrt) if restrt is not None else maxiter
+    if capture_M and M is not None and hasattr(M, "capture") and b.is_cuda:
+        try:
+            m_in = torch.zeros(M.shape[0], dtype=torch.float64, device=b.device)
+            m_out = torch.empty_like(m_in)
+            m_graph = M.capture(m_in, m_out)
+
+            def Mop(x, out=None, _g=m_graph, _i=m_in, _o=m_out):   # noqa: F811
+                _i.copy_(x)
+                _g.replay()
+                return _o
+        except NotImplementedError:   # e.g. a partitioned apply over the host-staged (gloo) halo: eager
+            pass
+    K = kernels if kernels is not None else KrylovKernels(n, m + 1, b.device, group)
+    f64 = dict(dtype=b.dtype, device=b.device)
+    x = torch.zeros_like(b) if x0 is None else (
+        x0.clone() if isinstance(x0, torch.Tensor) else torch.from_numpy(np.asarray(x0, dtype=np.float64)).to(b.device))
+    bnd = torch.empty(2, **f64)          # [max |r|, max |w|]
+
+    def norm(v, slot):
+        K.amax(v, bnd[slot:slot + 1])
+        a = K.fold_sums(v, n, 1, v, bnd[slot:slot + 1], bnd[slot:slot + 1])
+        return math.sqrt(_finish(a.cpu().tolist()))
+
+    def lincomb(xv, Zm, k, y):
+        """xv + Zm[:k]^T y (element-wise, basis vectors added in order)."""
+        ny = torch.from_numpy(-np.asarray(y[:k], dtype=np.float64)).to(b.device)
+        return K.update(Zm, n, k, ny, xv, torch.empty_like(xv))
+
     r = b - Aop(x)
-    normr = float(torch.linalg.vector_norm(r))
+    normr = norm(r, 0)
     if residuals is not None:
         residuals[:] = [normr]
-    normb = float(torch.linalg.vector_norm(b)) or 1.0
+    normb = norm(b, 1) or 1.0
     if normr < tol * normb:
         return x, 0
     target = tol * normr if normr != 0.0 else tol
     it = 0
-    use_gs = b.is_cuda and b.dtype == torch.float64 and m + 1 <= 256
-    if use_gs:
-        part = torch.empty(int(lib().mpbp_gs_part_size(n, m + 1)), dtype=torch.float64, device=b.device)
-        hbuf = torch.empty(2, m + 1, dtype=torch.float64, device=b.device)
-
-    def project(Vk, w, k, slot):
-        """(h, w - Vk^T h) with h = Vk w for the first k basis vectors."""
-        if not use_gs:
-            h = Vk @ w
-            return h, w - Vk.T @ h
-        hv = hbuf[slot]
-        check(lib().mpbp_gs_dot(ptr(Vk), n, k, ptr(w), n, ptr(part), ptr(hv), stream_handle()))
-        check(lib().mpbp_gs_update(ptr(Vk), n, k, ptr(hv), ptr(w), n, ptr(w), stream_handle()))
-        return hv[:k].clone(), w
-
+    w = torch.empty_like(b)
+    V = torch.zeros(m + 1, n, **f64)
+    Z = torch.zeros(m, n, **f64)
+    vb = torch.zeros(m + 1, **f64)       # max |V[i]| bounds (identical on every rank)
     while it < maxiter:
         beta = normr
-        V = torch.zeros(m + 1, n, dtype=b.dtype, device=b.device)
-        Z = torch.zeros(m, n, dtype=b.dtype, device=b.device)
+        V.zero_()
         H = np.zeros((m + 1, m))
         cs, sn = np.zeros(m), np.zeros(m)
         g = np.zeros(m + 1)
         g[0] = beta
-        V[0] = r / beta
+        torch.div(r, beta, out=V[0])
+        vb[0:1] = bnd[0:1] / beta * _VB_SLACK   # (bnd[0] = max |r| from norm(r))
         k = 0
         for j in range(m):
             Z[j] = Mop(V[j]) if Mop is not None else V[j]
-            w = Aop(Z[j]).contiguous()
-            h, w = project(V[: j + 1], w, j + 1, 0)
-            h2, w = project(V[: j + 1], w, j + 1, 1)
-            hcol = (h + h2).cpu().numpy()
-            hn = float(torch.linalg.vector_norm(w))
+            w.copy_(Aop(Z[j]))        # fgmres's own buffer: the operator's return value is never modified
+            hs = None
+            for _ in range(2):        # CGS2: h = V w, w -= V^T h, twice
+                K.amax(w, bnd[1:2])
+                h = K.dots(V, n, j + 1, w, vb, bnd[1:2])
+                K.update(V, n, j + 1, h, w, w)
+                hs = h.clone() if hs is None else hs + h
+            K.amax(w, bnd[1:2])
+            a = K.fold_sums(w, n, 1, w, bnd[1:2], bnd[1:2])
+            host = torch.cat([hs, a]).cpu().tolist()
+            hcol = np.asarray(host[: j + 1])
+            hn = math.sqrt(_finish(host[j + 1:]))
             H[: j + 1, j] = hcol
             H[j + 1, j] = hn
             if hn != 0.0:
-                V[j + 1] = w / hn
+                torch.div(w, hn, out=V[j + 1])
+                vb[j + 1:j + 2] = bnd[1:2] / hn * _VB_SLACK
             for i in range(j):                          # apply previous Givens rotations
                 t = cs[i] * H[i, j] + sn[i] * H[i + 1, j]
                 H[i + 1, j] = -sn[i] * H[i, j] + cs[i] * H[i + 1, j]
@@ -453,14 +566,12 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
             if residuals is not None:
                 residuals.append(res)
             if callback is not None:
-                y = np.linalg.solve(np.triu(H[:k, :k]), g[:k]) if k else np.zeros(0)
-                callback(x + Z[:k].T @ torch.from_numpy(y).to(b.device))
+                callback(lincomb(x, Z, k, _solve_upper(H, g, k)))
             if res <= target or it >= maxiter or hn == 0.0:
                 break
-        y = np.linalg.solve(np.triu(H[:k, :k]), g[:k])
-        x = x + Z[:k].T @ torch.from_numpy(y).to(b.device)
+        x = lincomb(x, Z, k, _solve_upper(H, g, k))
         r = b - Aop(x)
-        normr = float(torch.linalg.vector_norm(r))
+        normr = norm(r, 0)
         if normr <= target:
             return x, 0
     return x, it

@@ -1,0 +1,116 @@
+"""Row 17 on the CPU: the partitioned operator A u (apply.py:72) and the distributed FGMRES (solve.py:285) over gloo
+world_size 1 / 2 / 3, with the arithmetic on the oracle's kernels (oracle/csr_oracle.c, oracle/krylov_oracle.py) and the
+product's host logic: RowPartition / colmap / ghost_depth / boundary_ranges / HaloExchanger for A u, and
+solve.fgmres itself (the distributed reductions, bounds, Givens rotations, restarts) driven through the
+KrylovKernels interface.  The partitioned runs must reproduce the one-rank run bit for bit: same residual history,
+same iterate."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+PARAMS = dict(xi=1.0, eta_n=100.0, eta_s=1.0, c=1.0, d_u=-1.0, d_p=1.0, d_div=-1.0)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n, maxiter, restrt, outdir, errfile):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from mp_block_preconditioners_amd.distributed import (HaloExchanger, RowPartition, boundary_ranges,
+                                                              ghost_depth)
+        from mp_block_preconditioners_amd.solve import fgmres
+        from oracle import csr_oracle as co
+        from oracle.dist_oracle import dist_apply, extract_rows
+        from oracle.krylov_oracle import TorchKrylov
+        from oracle.schur_oracle import Inner, diagonal
+        from oracle.stokes_oracle import StokesSystem
+        s = StokesSystem(n, **PARAMS)
+        part = RowPartition(n, world, rank, ghosts=True)
+        group = dist.group.WORLD
+        # ---- A u over the partition (5 fields) ----
+        rows5 = part.owned_rows(5)
+        cols = extract_rows(s.A, rows5, np.arange(s.A.shape[1], dtype=np.int32), s.A.shape[1]).indices
+        hA = max(1, ghost_depth(torch.from_numpy(cols.astype(np.int64)), n, part.r0, part.L)) if world > 1 else 1
+        assert hA == 1
+        own = part.n_owned(5)
+        Aloc = extract_rows(s.A, rows5, part.colmap(5, hA), part.n_ext(5, hA))
+        inner, bnd = boundary_ranges(torch.from_numpy(Aloc.indptr), torch.from_numpy(Aloc.indices), own)
+        assert sum(b - a for a, b in inner + bnd) == own
+        exA = HaloExchanger(part, 5, hA, "cpu")
+
+        def Aop(x):
+            xe = torch.zeros(part.n_ext(5, hA), dtype=torch.float64)
+            xe[:own] = x
+            exA.exchange(xe)
+            return torch.from_numpy(co.spmv(Aloc, xe.numpy()))
+
+        rng = np.random.default_rng(3)
+        u = rng.standard_normal(5 * n * n)
+        got = Aop(torch.from_numpy(u[rows5].copy())).numpy()
+        assert np.array_equal(got.view(np.uint64), co.spmv(s.A, u)[rows5].view(np.uint64))
+        # ---- the approximate-commutator preconditioner over the partition (oracle kernels, Jacobi inner) ----
+        ru, rp_ = part.owned_rows(4), part.owned_rows(1)
+        cm_u, cm_p = part.colmap(4, 1), part.colmap(1, 3)
+        nu_ext, np_ext = part.n_ext(4, 1), part.n_ext(1, 3)
+        loc = dict(F=extract_rows(s.F, ru, cm_u, nu_ext), D=extract_rows(s.D, rp_, cm_u, nu_ext),
+                   G=extract_rows(s.G, ru, cm_p, np_ext), GtG=extract_rows(s.GtG, rp_, cm_p, np_ext),
+                   GtFG=extract_rows(s.GtFG, rp_, cm_p, np_ext), nu=part.n_owned(4), np=part.n_owned(1),
+                   nu_ext=nu_ext, np_ext=np_ext, diag_F=diagonal(s.F)[ru], diag_P=diagonal(s.GtG)[rp_])
+        ex_u, ex_p = HaloExchanger(part, 4, 1, "cpu"), HaloExchanger(part, 1, 3, "cpu")
+        iF, iP = Inner("jacobi", 3), Inner("jacobi", 2)
+
+        def Mop(v):
+            return torch.from_numpy(dist_apply(loc, ex_u, ex_p, v.numpy(), iF, iP))
+
+        b = torch.from_numpy(rng.standard_normal(5 * n * n)[rows5].copy())
+        hist = []
+        K = TorchKrylov(own, (restrt or maxiter) + 1, group=group if world > 1 else None)
+        x, info = fgmres(Aop, b, M=Mop, tol=1e-12, maxiter=maxiter, restrt=restrt, residuals=hist,
+                         group=group if world > 1 else None, kernels=K)
+        np.save(os.path.join(outdir, f"x_{world}_{rank}.npy"), x.numpy())
+        np.save(os.path.join(outdir, f"rows_{world}_{rank}.npy"), rows5)
+        np.save(os.path.join(outdir, f"hist_{world}_{rank}.npy"), np.asarray(hist))
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:   # surface the failure to the parent
+        with open(errfile, "a") as f:
+            f.write(f"rank {rank}: {type(e).__name__}: {e}\n")
+        raise
+
+
+def _run(world, n, maxiter, restrt, outdir, errfile):
+    try:
+        mp.spawn(_worker, args=(world, _free_port(), n, maxiter, restrt, outdir, errfile), nprocs=world, join=True)
+    except Exception:
+        msg = open(errfile).read() if os.path.exists(errfile) else ""
+        pytest.fail(f"distributed worker failed:\n{msg}")
+    x = np.zeros(5 * n * n)
+    for r in range(world):
+        x[np.load(os.path.join(outdir, f"rows_{world}_{r}.npy"))] = np.load(os.path.join(outdir, f"x_{world}_{r}.npy"))
+    hists = [np.load(os.path.join(outdir, f"hist_{world}_{r}.npy")) for r in range(world)]
+    for h in hists[1:]:
+        assert np.array_equal(h, hists[0])   # every rank holds the same Givens state
+    return x, hists[0]
+
+
+@pytest.mark.parametrize("n,maxiter,restrt", [(12, 25, None), (13, 30, 12)])
+def test_distributed_fgmres_matches_one_rank(n, maxiter, restrt, tmp_path, oracle_built):
+    """FGMRES with the partitioned A and the partitioned preconditioner on 2 and 3 gloo ranks: the residual history
+    and the iterate are bit-identical to the one-rank run (reproducible inner products), restarts included."""
+    errfile = str(tmp_path / "err.txt")
+    x1, h1 = _run(1, n, maxiter, restrt, str(tmp_path), errfile)
+    assert len(h1) == maxiter + 1 and h1[-1] < h1[0]
+    for world in (2, 3):
+        xw, hw = _run(world, n, maxiter, restrt, str(tmp_path), errfile)
+        assert np.array_equal(hw, h1), (world, np.max(np.abs(hw - h1)))
+        assert np.array_equal(xw.view(np.uint64), x1.view(np.uint64)), world

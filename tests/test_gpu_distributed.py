@@ -217,3 +217,207 @@ def test_rccl_two_gpus_matches_single_gpu(world, n, ca, tmp_path):
     except Exception:
         msg = open(errfile).read() if os.path.exists(errfile) else ""
         pytest.fail(f"RCCL worker failed:\n{msg}")
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# Row 17: the partitioned operator A u (DistributedMatrix) and FGMRES over the ranks; row 18: multigrid inner solves
+# under the row partition (PartitionedMultigrid).  gloo ranks share the one GPU (RCCL needs a GPU per rank); the RCCL
+# halo kinds are exercised by the self-exchange.
+
+def _spawn(fn, args, nprocs, errfile):
+    try:
+        mp.spawn(fn, args=args, nprocs=nprocs, join=True)
+    except Exception:
+        msg = open(errfile).read() if os.path.exists(errfile) else ""
+        pytest.fail(f"worker failed:\n{msg}")
+
+
+def _matrix_worker(rank, world, port, n, overlap, halo, errfile):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import mp_block_preconditioners_amd as mpb
+        from mp_block_preconditioners_amd.distributed import DistributedMatrix
+        bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+        A = bp.get_big_A_matrix(c=1.0, d_u=-1.0)[0]
+        dA = DistributedMatrix(A, n, 5, halo=halo, overlap=overlap, self_halo=(world == 1))
+        assert dA.partitioned and dA.h == 1
+        u = torch.from_numpy(np.random.default_rng(3).standard_normal(A.shape[0])).cuda()
+        gids = torch.from_numpy(dA.local_to_global_rows()).cuda()
+        ref = A.matvec(u)[gids]
+        for _ in range(3):
+            got = dA.apply(u[gids].contiguous())
+            assert torch.equal(got, ref), float((got - ref).abs().max())
+        dA.close()
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:
+        with open(errfile, "a") as f:
+            f.write(f"rank {rank}: {type(e).__name__}: {e}\n")
+        raise
+
+
+@pytest.mark.parametrize("world,n,overlap,halo", [(2, 64, False, "auto"), (3, 50, False, "auto"), (4, 9, False, "auto"),
+                                                  (1, 64, False, "rccl"), (1, 64, True, "rccl"), (1, 33, True, "rccl"),
+                                                  (1, 40, False, "torch")])
+def test_distributed_matrix_matches_global_spmv(world, n, overlap, halo, tmp_path):
+    """A u over the row partition (apply.py:72 on the 5-field system): the interior rows' SpMV, the ghost exchange
+    (gloo ranks; the RCCL self-exchange in order and overlapped on the halo's side stream), the boundary rows --
+    bit-identical to the rows of the one-GPU SpMV."""
+    errfile = str(tmp_path / "err.txt")
+    _spawn(_matrix_worker, (world, _free_port(), n, overlap, halo, errfile), world, errfile)
+
+
+def _inner_pair(spec):
+    import mp_block_preconditioners_amd as mpb
+    (kf, sf), (kp, sp) = spec
+    return mpb.InnerSolver(kf, sf), mpb.InnerSolver(kp, sp)
+
+
+def _mg_worker(rank, world, port, n, inner, min_cells, halo, errfile):
+    """The partitioned Schur apply with multigrid inner solves vs the one-GPU apply."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import mp_block_preconditioners_amd as mpb
+        from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner, PartitionedMultigrid
+        iF, iP = _inner_pair(inner)
+        dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, halo=halo,
+                                             self_halo=(world == 1), mg_min_cells=min_cells)
+        for m in (dpc.mg_F, dpc.mg_P):
+            if m is not None:
+                assert isinstance(m, PartitionedMultigrid) and 1 <= m.part_levels <= m.g.nlevels - 1
+                if min_cells == 0 and world > 1:
+                    assert m.part_levels >= 2, (m.part_levels, m.g.sizes)
+        bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+        _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+        pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP)
+        v = torch.from_numpy(np.random.default_rng(8).standard_normal(pc.shape[0])).cuda()
+        gids = torch.from_numpy(dpc.local_to_global_rows()).cuda()
+        ref = pc.apply(v)[gids]
+        for _ in range(2):
+            got = dpc.apply(v[gids].contiguous())
+            assert torch.equal(got, ref), float((got - ref).abs().max())
+        if halo == "rccl":   # in-order RCCL halo: the partitioned MG apply captured into a hipGraph
+            vin, out = v[gids].contiguous(), torch.zeros_like(ref)
+            g = dpc.capture(vin, out)
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref)
+            del g
+        dpc.close()
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:
+        with open(errfile, "a") as f:
+            f.write(f"rank {rank}: {type(e).__name__}: {e}\n")
+        raise
+
+
+MG1 = (("mg", 1), ("mg", 1))
+
+
+@pytest.mark.parametrize("world,n,inner,min_cells,halo", [
+    (2, 64, MG1, 1 << 14, "auto"), (2, 64, MG1, 0, "auto"), (4, 64, MG1, 0, "auto"), (3, 48, MG1, 0, "auto"),
+    (3, 50, MG1, 0, "auto"), (2, 64, (("mg", 2), ("chebyshev", 4)), 0, "auto"),
+    (2, 64, (("chebyshev", 4), ("mg", 1)), 0, "auto"), (1, 64, MG1, 0, "rccl"), (1, 32, MG1, 0, "torch")])
+def test_partitioned_multigrid_apply_matches_single_gpu(world, n, inner, min_cells, halo, tmp_path):
+    """Row 18: multigrid inner solves under the row partition -- level 0 the apply's own matrix-free F / Gt_G, the
+    Galerkin levels row-partitioned down to part_levels (ghost rows per operator), the coarser levels all-gathered and
+    replicated -- bit for bit against the one-GPU apply (2-4 gloo ranks; ceil-halved partitions at n = 50; the RCCL
+    self-exchange, captured)."""
+    errfile = str(tmp_path / "err.txt")
+    _spawn(_mg_worker, (world, _free_port(), n, inner, min_cells, halo, errfile), world, errfile)
+
+
+def _fgmres_worker(rank, world, port, n, inner, maxiter, outdir, errfile):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from mp_block_preconditioners_amd.distributed import solve_distributed
+        iF, iP = _inner_pair(inner)
+        res = solve_distributed(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, tol=1e-8, maxiter=maxiter,
+                                mg_min_cells=0)
+        np.save(os.path.join(outdir, f"x_{rank}.npy"), res["x_local"].cpu().numpy())
+        np.save(os.path.join(outdir, f"rows_{rank}.npy"), res["rows"])
+        np.save(os.path.join(outdir, f"hist_{rank}.npy"), np.asarray(res["residuals"]))
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:
+        with open(errfile, "a") as f:
+            f.write(f"rank {rank}: {type(e).__name__}: {e}\n")
+        raise
+
+
+@pytest.mark.parametrize("world,n,inner,maxiter", [(2, 32, (("chebyshev", 4), ("chebyshev", 4)), 40),
+                                                   (3, 48, MG1, 60), (2, 64, MG1, 60)])
+def test_distributed_fgmres_matches_single_gpu(world, n, inner, maxiter, tmp_path):
+    """Row 17: FGMRES (solve.py:285) over the row partition -- the partitioned A, the partitioned preconditioner,
+    reproducible inner products reduced over the ranks -- gives the one-GPU solve's residual history and iterate bit
+    for bit (the manufactured problem of solve.py:52-80)."""
+    import mp_block_preconditioners_amd as mpb
+    errfile = str(tmp_path / "err.txt")
+    _spawn(_fgmres_worker, (world, _free_port(), n, inner, maxiter, str(tmp_path), errfile), world, errfile)
+    bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    iF, iP = _inner_pair(inner)
+    pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP)
+    _, b = mpb.manufactured_problem(n, 1.0, -1.0, 1.0, 100.0, 1.0)
+    hist = []
+    x, info = mpb.fgmres(A, torch.from_numpy(b).cuda(), M=pc, tol=1e-8, maxiter=maxiter, residuals=hist)
+    x = x.cpu().numpy()
+    got = np.zeros_like(x)
+    for r in range(world):
+        h = np.load(os.path.join(str(tmp_path), f"hist_{r}.npy"))
+        assert np.array_equal(h, np.asarray(hist)), (r, len(h), len(hist))
+        got[np.load(os.path.join(str(tmp_path), f"rows_{r}.npy"))] = np.load(os.path.join(str(tmp_path), f"x_{r}.npy"))
+    assert np.array_equal(got.view(np.uint64), x.view(np.uint64))
+    if "mg" in inner[0]:
+        assert info == 0
+
+
+def _configs4_worker(rank, world, port, n, errfile):
+    """configs[4]: the 2048^2 apply row-partitioned over 8 ranks (256 grid rows each: the 8-GPU run's geometry, CA
+    ghost depths and halo sizes) on one GPU over gloo, bit for bit against the one-GPU apply."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import mp_block_preconditioners_amd as mpb
+        from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
+        iF, iP = mpb.InnerSolver("chebyshev", 4), mpb.InnerSolver("chebyshev", 4)
+        dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP)
+        assert dpc.ca and dpc.part.L == n // world
+        gids = torch.from_numpy(dpc.local_to_global_rows()).cuda()
+        v = torch.from_numpy(np.random.default_rng(2048).standard_normal(5 * n * n)).cuda()
+        got = dpc.apply(v[gids].contiguous())
+        torch.cuda.synchronize()
+        dpc.close()
+        del dpc
+        torch.cuda.empty_cache()
+        # the one-GPU reference, one rank at a time (bounds the GPU memory of 8 ranks sharing one card)
+        for turn in range(world):
+            if turn == rank:
+                bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+                _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+                pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP)
+                ref = pc.apply(v)[gids]
+                assert torch.equal(got, ref), float((got - ref).abs().max())
+                del pc, F, D, G, bp, ref
+                torch.cuda.empty_cache()
+            dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:
+        with open(errfile, "a") as f:
+            f.write(f"rank {rank}: {type(e).__name__}: {e}\n")
+        raise
+
+
+def test_configs4_2048_over_8_ranks(tmp_path):
+    """BASELINE configs[4] (2048^2, rows partitioned over 8 ranks) on one GPU: every rank's rows of the partitioned
+    apply equal the one-GPU apply's.  The RCCL-over-xGMI transport itself needs the 8-GPU node (bench.py --gpus 8)."""
+    errfile = str(tmp_path / "err.txt")
+    _spawn(_configs4_worker, (8, _free_port(), 2048, errfile), 8, errfile)

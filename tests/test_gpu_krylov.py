@@ -1,0 +1,109 @@
+"""FGMRES's vector kernels on the GPU: the reproducible inner products (mpbp_rdot / mpbp_rdot_finish, mpbp_absmax)
+bit for bit against oracle/krylov_oracle.py and independent of how the vector is split; and fgmres itself on the
+reproducible kernels (the aliasing-safe work buffer, deterministic reruns)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    from mp_block_preconditioners_amd._lib import check, lib, ptr, stream_handle
+    return check, lib, ptr, stream_handle
+
+
+def _rdot(V, k, w, ntot, vb, wb):
+    check, lib, ptr, sh = _lib()
+    n = w.numel()
+    part = torch.empty(max(1, int(lib().mpbp_rdot_part_size(n, k))), dtype=torch.float64, device="cuda")
+    acc = torch.empty(3 * k, dtype=torch.float64, device="cuda")
+    check(lib().mpbp_rdot(ptr(V), V.shape[1] if V.dim() == 2 else n, k, ptr(w), n, ntot, ptr(vb), ptr(wb), ptr(part),
+                          ptr(acc), sh()))
+    return acc
+
+
+@pytest.mark.parametrize("k,n", [(1, 1), (3, 1000), (8, 4097), (37, 100003), (151, 5000), (5, 2_000_003)])
+def test_rdot_matches_oracle_bit_for_bit(k, n):
+    from oracle.krylov_oracle import finish, rdot_folds
+    check, lib, ptr, sh = _lib()
+    rng = np.random.default_rng(k * 7 + n)
+    V = rng.standard_normal((k + 2, n)) * np.logspace(-6, 6, k + 2)[:, None]
+    w = rng.standard_normal(n)
+    vb, wb = np.max(np.abs(V[:k]), axis=1), float(np.max(np.abs(w)))
+    dV, dw = torch.from_numpy(V).cuda(), torch.from_numpy(w).cuda()
+    acc = _rdot(dV, k, dw, n, torch.from_numpy(vb).cuda(), torch.tensor([wb], dtype=torch.float64, device="cuda"))
+    ref = rdot_folds(V[:k], w, n, vb, wb)
+    assert np.array_equal(acc.cpu().numpy().view(np.uint64), ref.view(np.uint64))
+    h = torch.empty(k, dtype=torch.float64, device="cuda")
+    check(lib().mpbp_rdot_finish(k, ptr(acc), ptr(h), sh()))
+    assert np.array_equal(h.cpu().numpy().view(np.uint64), finish(ref).view(np.uint64))
+    assert np.max(np.abs(h.cpu().numpy() - V[:k] @ w) / (vb * wb)) < 1e-13
+    # absmax
+    am = torch.empty(1, dtype=torch.float64, device="cuda")
+    check(lib().mpbp_absmax(ptr(dw), n, ptr(am), sh()))
+    assert float(am) == wb
+
+
+def test_rdot_split_over_pieces_is_the_same():
+    """Fold sums of a vector cut into pieces (the ranks of a row partition) add exactly: same bits as the whole."""
+    rng = np.random.default_rng(4)
+    n, k = 300_001, 6
+    V = torch.from_numpy(rng.standard_normal((k, n))).cuda()
+    w = torch.from_numpy(rng.standard_normal(n) * 1e3).cuda()
+    vb = V.abs().amax(dim=1).contiguous()
+    wb = w.abs().amax().reshape(1)
+    whole = _rdot(V, k, w, n, vb, wb)
+    acc = torch.zeros_like(whole)
+    for a, b in ((0, 77_777), (77_777, 200_000), (200_000, n)):
+        acc += _rdot(V[:, a:b].contiguous(), k, w[a:b].contiguous(), n, vb, wb)
+    assert torch.equal(acc, whole)
+
+
+def test_rdot_nan_and_zero():
+    check, lib, ptr, sh = _lib()
+    w = torch.tensor([1.0, float("nan"), 2.0], dtype=torch.float64, device="cuda")
+    am = torch.empty(1, dtype=torch.float64, device="cuda")
+    check(lib().mpbp_absmax(ptr(w), 3, ptr(am), sh()))
+    assert torch.isnan(am).all()
+    acc = _rdot(w.reshape(1, 3).clone(), 1, w, 3, am, am)
+    assert torch.isnan(acc).any()
+    z = torch.zeros(10, dtype=torch.float64, device="cuda")
+    acc = _rdot(z.reshape(1, 10).clone(), 1, z, 10, z[:1], z[:1])
+    assert torch.equal(acc, torch.zeros(3, dtype=torch.float64, device="cuda"))
+
+
+def test_fgmres_operator_return_value_not_modified():
+    """a user operator that returns its input (identity) must not see fgmres's projections written into
+    it; FGMRES on the identity converges in one iteration to x = b."""
+    import mp_block_preconditioners_amd as mp
+    b = torch.from_numpy(np.random.default_rng(2).standard_normal(1000)).cuda()
+    seen = []
+
+    def ident(x):
+        seen.append(x)
+        return x
+
+    x, info = mp.fgmres(ident, b, tol=1e-12, maxiter=5)
+    assert info == 0
+    assert float((x - b).abs().max()) <= 1e-13 * float(b.abs().max())
+
+
+def test_fgmres_is_deterministic():
+    """Two solves of the same system give the same bits (reproducible reductions, captured preconditioner)."""
+    import mp_block_preconditioners_amd as mp
+    n = 32
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("mg", 1), inner_P=mp.InnerSolver("mg", 1))
+    _, b = mp.manufactured_problem(n, 1.0, -1.0, 1.0, 100.0, 1.0)
+    bd = torch.from_numpy(b).cuda()
+    runs = []
+    for _ in range(2):
+        hist = []
+        x, info = mp.fgmres(A, bd, M=pc, tol=1e-8, maxiter=60, residuals=hist)
+        assert info == 0
+        runs.append((x.clone(), list(hist)))
+    assert torch.equal(runs[0][0], runs[1][0]) and runs[0][1] == runs[1][1]
