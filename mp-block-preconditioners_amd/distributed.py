@@ -342,6 +342,17 @@ class _Halos:
         self._gather[int(gid)].gather(self._tensors[int(own_ptr)], self._tensors[int(full_ptr)])
 
 
+def level_partitions(part: RowPartition, sizes) -> list[RowPartition]:
+    """The row partition of every multigrid level: level l + 1's rows of a rank are [ceil(r0 / 2), ceil(r1 / 2)) of its
+    level-l rows [r0, r1) -- exact halving for even bounds, a disjoint cover of the coarse grid in any case."""
+    parts = [part]
+    for m in sizes[1:]:
+        p = parts[-1]
+        b = tuple(((a + 1) // 2, (a + L + 1) // 2 - (a + 1) // 2) for a, L in p.bounds)
+        parts.append(RowPartition(m, part.world, part.rank, part.ghosts, b))
+    return parts
+
+
 class PartitionedMultigrid:
     """A multigrid hierarchy (mg.Multigrid, built on every rank from the global operator -- setup only) split over a
     row partition for the partitioned Schur apply (solve.py:266 / 274's pointer, under north_star's row partition).
@@ -361,11 +372,7 @@ class PartitionedMultigrid:
         dev = g.device
         self.device = dev
         nl = g.nlevels
-        self.parts = [part]
-        for l in range(1, nl):
-            p = self.parts[-1]
-            b = tuple(((a + 1) // 2, (a + L + 1) // 2 - (a + 1) // 2) for a, L in p.bounds)
-            self.parts.append(RowPartition(g.sizes[l], part.world, part.rank, part.ghosts, b))
+        self.parts = level_partitions(part, g.sizes)
         world = part.world
 
         def owned(l):

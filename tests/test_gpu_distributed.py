@@ -289,8 +289,8 @@ def _mg_worker(rank, world, port, n, inner, min_cells, halo, errfile):
         for m in (dpc.mg_F, dpc.mg_P):
             if m is not None:
                 assert isinstance(m, PartitionedMultigrid) and 1 <= m.part_levels <= m.g.nlevels - 1
-                if min_cells == 0 and world > 1:
-                    assert m.part_levels >= 2, (m.part_levels, m.g.sizes)
+                if min_cells == 0 and world > 1:   # every level but the coarsest partitioned (where rows allow)
+                    assert m.part_levels >= min(2, m.g.nlevels - 1), (m.part_levels, m.g.sizes)
         bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
         _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
         pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP)
