@@ -306,6 +306,13 @@ int mpbp_csr_extract_fill(const mpbp_csr* A, const int32_t* rows, int32_t nrows_
 /* y = op(A x) over the rows of `blocks` (mode MPBP_SPMV_*; z unused for STORE). */
 int mpbp_spmv(const mpbp_csr* A, const mpbp_rowblocks* blocks, int32_t mode, const double* x,
               const double* z, double* y, void* stream);
+/* The same product at north_star's value bar: identical row_ptr / col_idx handling, each row's sum formed by a
+ * wavefront segmented reduction (pairs per lane, DPP cross-lane adds, fused multiply-adds) -- within 1e-12
+ * relative infinity norm of mpbp_spmv's sequential sums, not bit-identical; deterministic run to run.  Fast for
+ * stencil rows (64-row waves of 8, 10 or 12 entries from an even start); other waves take a plain loop.
+ * Replaces np.matmul(A, u_vec) (apply.py:72), whose BLAS sums are not sequential either. */
+int mpbp_spmv_seg(const mpbp_csr* A, const mpbp_rowblocks* blocks, int32_t mode, const double* x,
+                  const double* z, double* y, void* stream);
 /* x_out = b / diag (first Jacobi sweep from 0); x_out = sub - that when sub != NULL. */
 int mpbp_jacobi_init(int32_t nrows, const double* b, const double* diag, const double* sub,
                      double* x_out, void* stream);

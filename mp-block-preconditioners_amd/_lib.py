@@ -115,6 +115,7 @@ _SIGNATURES = {
     "mpbp_csr_extract_count": ([POINTER(Csr), _P, c_int32, _P, _P], c_int),
     "mpbp_csr_extract_fill": ([POINTER(Csr), _P, c_int32, _P, _P, _P, _P, _P], c_int),
     "mpbp_spmv": ([POINTER(Csr), POINTER(RowBlocks), c_int32, _P, _P, _P, _P], c_int),
+    "mpbp_spmv_seg": ([POINTER(Csr), POINTER(RowBlocks), c_int32, _P, _P, _P, _P], c_int),
     "mpbp_jacobi_init": ([c_int32, _P, _P, _P, _P, _P], c_int),
     "mpbp_jacobi_step": ([POINTER(Csr), POINTER(RowBlocks), _P, _P, _P, _P, _P, _P], c_int),
     "mpbp_cheb_init": ([c_int32, _P, _P, c_double, _P, _P, _P, _P], c_int),

@@ -106,13 +106,18 @@ class DeviceCSR:
 
     # -- kernels --------------------------------------------------------------------------------
     def matvec(self, x: torch.Tensor, out: torch.Tensor | None = None, mode=_lib.SPMV_STORE,
-               z: torch.Tensor | None = None, blocks=None) -> torch.Tensor:
+               z: torch.Tensor | None = None, blocks=None, order: str = "seq") -> torch.Tensor:
+        """y = A x (or z + A x / z - A x by `mode`).  order "seq": each row summed left to right in CSR order
+        (bit-identical to the oracle); "seg": a wavefront segmented reduction per row (mpbp_spmv_seg: within
+        1e-12 of "seq", the north_star bar for apply.py:72's np.matmul)."""
         assert x.dtype == torch.float64 and x.is_cuda and x.numel() >= self.shape[1]
+        if order not in ("seq", "seg"):
+            raise ValueError(f"order must be 'seq' or 'seg', not {order!r}")
         if out is None:
             out = torch.empty(self.shape[0], dtype=torch.float64, device=self.device)
         blk = (blocks or self.blocks).cstruct()
-        check(lib().mpbp_spmv(ctypes.byref(self.cstruct()), ctypes.byref(blk), mode, ptr(x), ptr(z), ptr(out),
-                              stream_handle()))
+        fn = lib().mpbp_spmv if order == "seq" else lib().mpbp_spmv_seg
+        check(fn(ctypes.byref(self.cstruct()), ctypes.byref(blk), mode, ptr(x), ptr(z), ptr(out), stream_handle()))
         return out
 
     def __matmul__(self, other):

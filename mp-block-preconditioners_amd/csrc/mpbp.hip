@@ -1126,6 +1126,103 @@ __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __rest
     if (live) epi.template apply<MPBP_CSR_NT != 0>(r, acc, pe);
 }
 
+// ---------------------------------------------------- CSR, segmented reduction ----
+// The same product under north_star's value bar instead of the oracle's order: identical row_ptr / col_idx
+// handling, row sums within 1e-12 (relative infinity norm) of the sequential ones (np.matmul's BLAS sums are
+// not sequential either, apply.py:72).  A uniform wave (64 rows of LEN = 2P entries from an even start, as in
+// k_csr_wave) needs no LDS transposition: each row's P entry pairs sit in P consecutive lanes of a G-lane group
+// (G = 4 for P = 4, else 8; lanes P..G-1 of a group repeat the group's last pair and add 0), a wave-instruction
+// covers 64/G whole rows (contiguous 16-byte loads), every lane multiplies its own pair (x gathered by its own
+// columns), and the group sums its pairs by DPP cross-lane adds (half-row mirror, then the two quad swaps; every
+// lane of the group ends with the same bits, commutativity).  The row sums then go through 512 B of LDS so the
+// epilogue runs one row per lane.  LDS 2 KiB per workgroup instead of 36 KiB: occupancy is set by registers.
+// Non-uniform waves take a plain lane-per-row loop (correct, not fast: tree order is for stencil operators).
+template <int CTRL>
+__device__ inline double dpp_f64(double v) {
+    const int2 h = __builtin_bit_cast(int2, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, h.x, CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, h.y, CTRL, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, make_int2(lo, hi));
+}
+constexpr int kDppQuadSwap2 = 0x4e;      // quad_perm [2,3,0,1]
+constexpr int kDppQuadSwap1 = 0xb1;      // quad_perm [1,0,3,2]
+constexpr int kDppHalfMirror = 0x141;    // row_half_mirror: lane k <- lane 7-k within 8
+
+template <int LEN, class Epi>
+__device__ inline bool csr_seg_uniform(const Csr& A, const double* __restrict__ x, int32_t s, int lane,
+                                       double* ys, int32_t ks, int32_t ke, int32_t r, const Epi& epi,
+                                       const typename Epi::P& pe) {
+    constexpr int P = LEN / 2;               // entry pairs per row
+    constexpr int G = P <= 4 ? 4 : 8;        // lanes per row group
+    constexpr int RPI = 64 / G;              // rows per wave-instruction
+    constexpr int NI = 64 / RPI;             // wave-instructions for the wave's 64 rows
+    const int k = lane % G, rg = lane / G;
+    const int kc = k < P ? k : P - 1;        // idle lanes re-read the group's last pair (same cache line)
+    double2 v[NI];
+    int2 c[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+        const int32_t q = s + 2 * ((j * RPI + rg) * P + kc);
+        v[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const double2*>(A.va + q));
+        c[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const int2*>(A.ci + q));
+    }
+    asm volatile("" ::: "memory");           // keep the matrix loads ahead of the row check (as MPBP_CSR_SPEC)
+    if (!__all(ke - ks == LEN)) return false;
+    const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(x), (short)0, A.ncols * 8, 0x00020000);
+    double t[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+        const double x0 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, c[j].x * 8, 0, 0));
+        const double x1 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, c[j].y * 8, 0, 0));
+        // (a bit mask, not a branch: the gathers of idle lanes stay unconditional, so they issue back to back)
+        const uint64_t keep = k < P ? ~0ull : 0ull;
+        t[j] = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, __builtin_fma(v[j].y, x1, v[j].x * x0)) & keep);
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+        if constexpr (G == 8) t[j] += dpp_f64<kDppHalfMirror>(t[j]);
+        t[j] += dpp_f64<kDppQuadSwap2>(t[j]);
+        t[j] += dpp_f64<kDppQuadSwap1>(t[j]);
+        if (k == 0) ys[j * RPI + rg] = t[j];
+    }
+    wave_lds_sync();
+    epi.template apply<MPBP_CSR_NT != 0>(r, ys[lane], pe);
+    return true;
+}
+
+template <class Epi>
+__global__ void __launch_bounds__(kBlock) k_csr_seg(Csr A, const double* __restrict__ x,
+                                                    const int2* __restrict__ blocks, int nblocks, Epi epi) {
+    __shared__ double ystage[kBlock / 64][64];
+    const int b = xcd_swizzle(blockIdx.x, nblocks);
+    const int2 blk = blocks[b];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int32_t ra = __builtin_amdgcn_readfirstlane(blk.x + 64 * w);
+    if (ra >= blk.y) return;
+    const int32_t rb = min(ra + 64, blk.y);
+    const int32_t r = ra + lane;
+    const bool live = r < rb;
+    const int32_t s = ld_uniform_i32(A.rp, ra), e = ld_uniform_i32(A.rp, rb);
+    const int32_t rr = live ? r : ra;
+    const int32_t ks = A.rp[rr], ke0 = A.rp[rr + 1];
+    const int32_t ke = live ? ke0 : ks;
+    typename Epi::P pe{};
+    if (live) pe = epi.pre(r);
+    const int32_t len = (e - s) >> 6;
+    if (rb - ra == 64 && ((e - s) & 63) == 0 && (s & 1) == 0 && A.ncols > 0 && A.ncols < (1 << 28)) {
+        // every lane is live here: the raw row end ke0, so no select on it waits for the row_ptr loads before
+        // the matrix loads issue
+        bool done = false;
+        if (len == 12) done = csr_seg_uniform<12>(A, x, s, lane, ystage[w], ks, ke0, r, epi, pe);
+        else if (len == 10) done = csr_seg_uniform<10>(A, x, s, lane, ystage[w], ks, ke0, r, epi, pe);
+        else if (len == 8) done = csr_seg_uniform<8>(A, x, s, lane, ystage[w], ks, ke0, r, epi, pe);
+        if (done) return;
+    }
+    double acc = 0.0;
+    for (int32_t kk = ks; kk < ke; ++kk) acc += A.va[kk] * x[A.ci[kk]];
+    if (live) epi.template apply<MPBP_CSR_NT != 0>(r, acc, pe);
+}
+
 // ------------------------------------------------------------------ SELL-64 ----
 // Sliced ELLPACK with one wavefront per slice: a slice is <= 64 consecutive rows, its entries
 // stored column-major in pairs -- pair-row j of the slice holds entries (2j, 2j+1) of every row,
@@ -2255,6 +2352,14 @@ int launch_rows(const mpbp_csr* A, const mpbp_rowblocks* blk, const double* x, E
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
+template <class Epi>
+int launch_rows_seg(const mpbp_csr* A, const mpbp_rowblocks* blk, const double* x, Epi epi, hipStream_t st) {
+    if (!blk || blk->count <= 0) return MPBP_OK;
+    k_csr_seg<Epi><<<blk->count, kBlock, 0, st>>>(to_csr(A), x, reinterpret_cast<const int2*>(blk->pairs),
+                                                   blk->count, epi);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
 
 template <class Epi>
 int launch_sell(const mpbp_sell* S, const double* x, Epi epi, hipStream_t st) {
@@ -2542,6 +2647,20 @@ int mpbp_spmv(const mpbp_csr* A, const mpbp_rowblocks* blocks, int32_t mode, con
     case MPBP_SPMV_ADD: return launch_rows(A, blocks, x, EpiAdd{z, y}, st);
     case MPBP_SPMV_RESID: return launch_rows(A, blocks, x, EpiResid{z, y}, st);
     default: return set_error(MPBP_ERR_ARG, "spmv: unknown mode %d", mode);
+    }
+}
+
+int mpbp_spmv_seg(const mpbp_csr* A, const mpbp_rowblocks* blocks, int32_t mode, const double* x,
+                  const double* z, double* y, void* stream) {
+    int rc = check_csr(A);
+    if (rc) return rc;
+    if (!x || !y || (mode != MPBP_SPMV_STORE && !z)) return set_error(MPBP_ERR_ARG, "spmv_seg: bad vectors");
+    const hipStream_t st = as_stream(stream);
+    switch (mode) {
+    case MPBP_SPMV_STORE: return launch_rows_seg(A, blocks, x, EpiStore{y}, st);
+    case MPBP_SPMV_ADD: return launch_rows_seg(A, blocks, x, EpiAdd{z, y}, st);
+    case MPBP_SPMV_RESID: return launch_rows_seg(A, blocks, x, EpiResid{z, y}, st);
+    default: return set_error(MPBP_ERR_ARG, "spmv_seg: unknown mode %d", mode);
     }
 }
 

@@ -32,8 +32,12 @@ def main():
     nbytes = A.nnz * 12 + (A.shape[0] + 1) * 4 + (A.shape[0] + A.shape[1]) * 8 + A.blocks.count * 8
     res = {"n": args.n, "nnz": A.nnz, "lib": os.environ.get("MPBP_LIB", "default")}
     flat = A.plan_blocks(groups=1)   # blocks in plain row order (no per-field interleave)
-    for name, M, blk in (("csr_wave", A, None), ("csr_wave_roworder", A, flat), ("sell", AS, None)):
+    runs = [("csr_wave", A, None, "seq"), ("csr_seg", A, None, "seg"), ("csr_wave_roworder", A, flat, "seq"),
+            ("sell", AS, None, None)]
+    for name, M, blk, order in runs:
         kw = {"blocks": blk} if blk is not None else {}
+        if order == "seg":
+            kw["order"] = "seg"
         for _ in range(5):
             M.matvec(x, out=y, **kw)
         torch.cuda.synchronize()
@@ -44,7 +48,8 @@ def main():
         torch.cuda.synchronize()
         us = ev[0].elapsed_time(ev[1]) * 1e3 / args.reps
         res[name] = {"us": round(us, 2), "gbs": round(nbytes / us / 1e3, 1),
-                     "bit_exact_vs_sell": bool(torch.equal(y.view(torch.int64), ref.view(torch.int64)))}
+                     "bit_exact_vs_sell": bool(torch.equal(y.view(torch.int64), ref.view(torch.int64))),
+                     "rel_inf_vs_sell": float((y - ref).abs().max() / ref.abs().max())}
     print(json.dumps(res), flush=True)
 
 
