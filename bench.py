@@ -109,6 +109,8 @@ def main():
                     help="grid rows per workgroup of the marching stencil kernels (matrix-free F, D, G, Gt_G); "
                          "0: the count that fills one round of workgroups per launch")
     ap.add_argument("--pg-direct", type=int, default=None, help="1: D / Gt_G sweeps as one thread per cell (no LDS)")
+    ap.add_argument("--mg-group-rows", type=int, default=None,
+                    help="multigrid levels / transfers with at most this many rows on the grouped CSR kernel (0: off)")
     ap.add_argument("--no-fuse-g", action="store_true",
                     help="launch G x_p separately instead of recomputing it inside the second F solve's sweeps")
     ap.add_argument("--no-ca", action="store_true",
@@ -126,7 +128,9 @@ def main():
     ap.add_argument("--no-solve", action="store_true",
                     help="skip the solve-level section (FGMRES to 1e-8 on the manufactured problem, N = 1)")
     ap.add_argument("--partitioned-graph", action="store_true",
-                    help="N > 1: capture the partitioned apply (RCCL halo groups included) into a hipGraph")
+                    help="(kept for old command lines: the default for RCCL ranks)")
+    ap.add_argument("--eager-partitioned", action="store_true",
+                    help="N > 1: launch the partitioned apply eagerly instead of replaying its hipGraph")
     args = ap.parse_args()
 
     # --gpus N > 1 without a launcher: start the N ranks as a child process BEFORE anything touches the GPU
@@ -167,6 +171,8 @@ def main():
     _check(_lib().mpbp_set_march_rows(args.march_rows))
     if args.pg_direct is not None:
         _check(_lib().mpbp_set_pg_direct(args.pg_direct))
+    if args.mg_group_rows is not None:
+        _check(_lib().mpbp_set_mg_group_rows(args.mg_group_rows))
 
     if args.weak:
         n = int(round((args.n or 1024) * math.sqrt(world)))
@@ -197,18 +203,25 @@ def main():
     out = torch.empty_like(v)
     torch.cuda.synchronize()
 
-    # One GPU: the apply is captured once into a hipGraph and replayed (22 launches -> 1).  N > 1 launches
-    # eagerly (the halo exchanges are RCCL groups issued from inside mpbp_schur_apply).  The timed loop
+    # The apply is captured once into a hipGraph and replayed (one GPU: 14 launches -> 1; N > 1 RCCL ranks: the
+    # gather kernels and RCCL point-to-point groups of the halo exchanges are recorded into the graph too, after
+    # one eager apply has opened the neighbour connections).  The gloo rehearsal launches eagerly (its halo is
+    # host-staged collectives between kernels, which a graph cannot hold).  The timed loop
     # records no events; the F-sweep durations for the roofline come from HIP events that
     # mpbp_schur_apply records around every F sweep on the apply stream, in an eager pass of the same K
     # applies right after the timed loop.
     sweeps_per_apply = 2 * max(sf - 1, 0)
     graph, graph_note = None, None
-    # partitioned applies are captured for the one-GPU self-exchange (measured, bit-exact) and, on request,
-    # for N > 1 (--partitioned-graph: cross-GPU RCCL point-to-point inside a graph is unmeasured here)
+    # partitioned applies are captured for the one-GPU self-exchange (bit-exact) and for N > 1 RCCL ranks
+    # (default; --eager-partitioned opts out); the side-stream overlap option cannot be captured
     use_graph = not args.no_graph and (not partitioned or (world == 1 and not args.halo_overlap) or
-                                       (args.partitioned_graph and not args.halo_overlap and backend == "nccl"))
+                                       (not args.eager_partitioned and not args.halo_overlap and backend == "nccl"))
     if use_graph:
+        if partitioned:   # open the RCCL neighbour connections outside the capture
+            pc.apply(v, out)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
         try:
             graph = pc.capture(v, out)
         except Exception as e:   # fall back to eager launches, and say so in the JSON line
@@ -246,8 +259,8 @@ def main():
 
     # dominant kernel: the fused Chebyshev-Jacobi sweep over F
     fused_init = getattr(pc, "f_stencil", None) is not None and (not partitioned or pc.ca)
-    # the dominant kernel's roofline over the first F solve's plain sweeps (b streamed, 184.5 MB per launch at
-    # 1024^2); the second solve's sweeps (G x_p recomputed when fused) are reported beside it
+    # the dominant kernel's roofline over the first F solve's plain sweeps (b streamed; 192.9 and 159.4 MB, mean
+    # 176.2 MB per launch at 1024^2); the second solve's sweeps (G x_p recomputed when fused) are reported beside it
     per_apply, kname = sweep_bytes(pc, args.layout, kf, sf, fused_init)
     sbytes, avg_sweep_s, n_timed = roofline_of(per_apply, sweep_ms, 1)
     achieved = sbytes / avg_sweep_s / 1e9

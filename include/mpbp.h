@@ -388,6 +388,9 @@ int mpbp_set_init_diag(int32_t mode);
 /* 1 (default): the matrix-free D, G and Gt_G sweeps run as one thread per cell reading neighbours from global memory
  * (no LDS ring; row partitions and ghost layouts included); 0: the marching kernel.  Bit-identical either way. */
 int mpbp_set_pg_direct(int32_t on);
+/* Multigrid levels and transfers with at most `rows` rows run on the grouped CSR kernel (several lanes per row,
+ * products in parallel, the row's sum in order by one lane: same bits); 0 disables it.  Default 65536. */
+int mpbp_set_mg_group_rows(int32_t rows);
 
 /* ---- geometric multigrid inner solves (the reference's pointer: solve.py:266, 274) ------------------ */
 /* P (which = MPBP_MG_P, fine x coarse) or R = P^T (MPBP_MG_R) of an n x n periodic grid (n even, >= 4) coarsened by 2,

@@ -152,6 +152,7 @@ _SIGNATURES = {
     "mpbp_set_march_rows": ([c_int32], c_int),
     "mpbp_set_init_diag": ([c_int32], c_int),
     "mpbp_set_pg_direct": ([c_int32], c_int),
+    "mpbp_set_mg_group_rows": ([c_int32], c_int),
     "mpbp_q13_build": ([POINTER(Csr), c_int32, c_void_p, c_void_p], c_int),
     "mpbp_q13_spmv": ([c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "mpbp_mg_transfer_count": ([c_int32, c_int32, _P, c_int32, _P, _P], c_int),

@@ -1223,6 +1223,62 @@ __global__ void __launch_bounds__(kBlock) k_csr_seg(Csr A, const double* __restr
     if (live) epi.template apply<MPBP_CSR_NT != 0>(r, acc, pe);
 }
 
+// ---------------------------------------------- CSR, G lanes per row (small levels) ----
+// The multigrid's small levels (<= 64^2 cells per field: 1-16 K rows of 20-46 entries) are latency-bound, not
+// bandwidth-bound: one lane per row walks its row in batches, each batch a matrix load -> x gather chain, so a
+// 4 K-row sweep took ~9 us for 2 MB.  Here G lanes share a row: each loads J of its entries (entries k, k + G, ...;
+// all loads of the row in flight at once), gathers x and forms the products v * x in parallel, writes them to
+// LDS, and the group's first lane adds them left to right from 0.0 -- the CSR row's sequential sum, bit for bit
+// (same products, same order, no FMA).  One latency chain per row instead of one per batch, and G times the lanes
+// for the few rows.  Rows longer than G * J entries take several chunks (correct for any CSR).  A DZ epilogue
+// reads the Chebyshev direction as +0.0 without loading it (the smoother's restart after a coarse correction,
+// same IEEE operations as a zeroed vector: no memset launch).
+constexpr int kGrpJ = 8;   // entries per lane per chunk
+template <class Epi>
+struct EpiZeroD : Epi {   // Epi = EpiCheb: d read as +0.0 (never loaded)
+    using P = typename Epi::P;
+    __device__ P pre(int32_t r) const {
+        return {this->xin[r], ld_stream(this->b + r), this->diag[r], 0.0, this->sub ? ld_stream(this->sub + r) : 0.0};
+    }
+};
+template <int G, class Epi>
+__global__ void __launch_bounds__(kBlock) k_csr_grp(Csr A, int32_t nrows, const double* __restrict__ x, Epi epi) {
+    constexpr int RPB = kBlock / G, CAP = G * kGrpJ;
+    __shared__ double prod[RPB * CAP];
+    const int g = threadIdx.x / G, k = threadIdx.x % G;
+    const int32_t r = xcd_swizzle(blockIdx.x, gridDim.x) * RPB + g;
+    const bool live = r < nrows;
+    const int32_t rr = live ? r : nrows - 1;
+    const int32_t ks = A.rp[rr], ke = live ? A.rp[rr + 1] : ks;
+    typename Epi::P pe{};
+    if (live && k == 0) pe = epi.pre(r);
+    double* pr = prod + g * CAP;
+    double acc = 0.0;
+    for (int32_t cb = ks; cb < ke; cb += CAP) {
+        double v[kGrpJ];
+        int32_t c[kGrpJ];
+#pragma unroll
+        for (int j = 0; j < kGrpJ; ++j) {
+            const int32_t e = cb + k + G * j;
+            const bool in = e < ke;
+            v[j] = in ? A.va[e] : 0.0;
+            c[j] = in ? A.ci[e] : 0;
+        }
+        double p[kGrpJ];
+#pragma unroll
+        for (int j = 0; j < kGrpJ; ++j) p[j] = v[j] * x[c[j]];
+        if (cb != ks) wave_lds_sync();   // the previous chunk's sums have read their slots
+#pragma unroll
+        for (int j = 0; j < kGrpJ; ++j) pr[k + G * j] = p[j];
+        wave_lds_sync();                 // a group never spans two waves (G divides 64)
+        if (k == 0) {
+            const int32_t cnt = min(ke - cb, (int32_t)CAP);
+            for (int32_t i = 0; i < cnt; ++i) acc += pr[i];
+        }
+    }
+    if (live && k == 0) epi(r, acc, pe);
+}
+
 // ------------------------------------------------------------------ SELL-64 ----
 // Sliced ELLPACK with one wavefront per slice: a slice is <= 64 consecutive rows, its entries
 // stored column-major in pairs -- pair-row j of the slice holds entries (2j, 2j+1) of every row,
@@ -2352,6 +2408,38 @@ int launch_rows(const mpbp_csr* A, const mpbp_rowblocks* blk, const double* x, E
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
+// Small-level CSR products through k_csr_grp: lanes per row from the mean row length (2: <= 16 entries, 4: <= 32,
+// 8: longer), so one chunk holds a multigrid coarse row (transfers 1-16 entries, Galerkin levels 20-46).
+int g_grp_rows = 65536;   // multigrid levels / transfers with at most this many rows use it (0: never)
+template <class Epi>
+int launch_grp(const mpbp_csr* A, const double* x, Epi epi, hipStream_t st) {
+    if (A->nrows <= 0) return MPBP_OK;
+    const int64_t avg = A->nnz / A->nrows;
+    auto go = [&](auto gc) {
+        constexpr int G = decltype(gc)::value;
+        constexpr int rpb = kBlock / G;
+        k_csr_grp<G, Epi><<<(unsigned)((A->nrows + rpb - 1) / rpb), kBlock, 0, st>>>(to_csr(A), A->nrows, x, epi);
+        MPBP_HIP(hipGetLastError());
+        return (int)MPBP_OK;
+    };
+    return avg <= 16 ? go(std::integral_constant<int, 2>{})
+                     : avg <= 32 ? go(std::integral_constant<int, 4>{}) : go(std::integral_constant<int, 8>{});
+}
+inline bool use_grp(const mpbp_csr& A) { return g_grp_rows > 0 && A.nrows > 0 && A.nrows <= g_grp_rows && A.nnz > 0; }
+int grp_spmv(const mpbp_csr* A, int32_t mode, const double* x, const double* z, double* y, hipStream_t st) {
+    switch (mode) {
+    case MPBP_SPMV_STORE: return launch_grp(A, x, EpiStore{y}, st);
+    case MPBP_SPMV_ADD: return launch_grp(A, x, EpiAdd{z, y}, st);
+    case MPBP_SPMV_RESID: return launch_grp(A, x, EpiResid{z, y}, st);
+    default: return set_error(MPBP_ERR_ARG, "grp_spmv: unknown mode %d", mode);
+    }
+}
+int grp_cheb(const mpbp_csr* A, const double* xin, const double* b, const double* dg, double c1, double c2, double* d,
+             const double* sub, double* xo, hipStream_t st, int store_d, bool dzero) {
+    const EpiCheb e{xin, b, dg, d, c1, c2, sub, xo, store_d};
+    return dzero ? launch_grp(A, xin, EpiZeroD<EpiCheb>{e}, st) : launch_grp(A, xin, e, st);
+}
+
 template <class Epi>
 int launch_rows_seg(const mpbp_csr* A, const mpbp_rowblocks* blk, const double* x, Epi epi, hipStream_t st) {
     if (!blk || blk->count <= 0) return MPBP_OK;
@@ -2406,6 +2494,11 @@ const char* mpbp_version(void) { return "libmpbp 0.1 (gfx950)"; }
 int mpbp_set_march_rows(int32_t rows) {
     if (rows < 0 || rows > 4096) return set_error(MPBP_ERR_ARG, "march rows must be 0 (auto) or in [1, 4096]");
     g_march_rows = rows;
+    return MPBP_OK;
+}
+int mpbp_set_mg_group_rows(int32_t rows) {
+    if (rows < 0) return set_error(MPBP_ERR_ARG, "mg group rows must be >= 0");
+    g_grp_rows = rows;
     return MPBP_OK;
 }
 int mpbp_set_pg_direct(int32_t on) {
@@ -3420,6 +3513,7 @@ struct OpRef {
     int32_t which;                    // stencil rows: 0 all, 1 interior, 2 boundary, 3 owned + ext ghost rows
     int32_t sop;
     int32_t ext = 0;                  // which = 3
+    int32_t grp = 0;                  // CSR rows through k_csr_grp (multigrid small levels)
 };
 
 // F and D read velocity vectors (f_part), G and Gt_G pressure vectors (p_part); D writes a pressure vector
@@ -3443,6 +3537,7 @@ int op_spmv(const OpRef& o, int32_t mode, const double* x, const double* z, doub
         const int32_t op = o.sop == SOP_D ? MPBP_PG_D : o.sop == SOP_G ? MPBP_PG_G : MPBP_PG_GTG;
         return mpbp_pg_stencil_spmv(&p->f_prm, p->f_cell, &q, op, mode, x, z, y, (void*)st);
     }
+    if (o.grp) return grp_spmv(o.csr, mode, x, z, y, st);
     return o.sell ? mpbp_sell_spmv(o.sell, mode, x, z, y, (void*)st)
                   : mpbp_spmv(o.csr, o.blk, mode, x, z, y, (void*)st);
 }
@@ -3461,8 +3556,10 @@ int op_jacobi(const OpRef& o, const double* xin, const double* b, const double* 
                   : mpbp_jacobi_step(o.csr, o.blk, xin, b, dg, sub, xo, (void*)st);
 }
 int op_cheb(const OpRef& o, const double* xin, const double* b, const double* dg, double c1, double c2, double* d,
-            const double* sub, double* xo, hipStream_t st, int store_d) {
+            const double* sub, double* xo, hipStream_t st, int store_d, bool dzero = false) {
     if (o.empty) return MPBP_OK;
+    if (o.grp) return grp_cheb(o.csr, xin, b, dg, c1, c2, d, sub, xo, st, store_d, dzero);
+    if (dzero) return set_error(MPBP_ERR_ARG, "cheb: a zero direction is only supported on the grouped CSR path");
     if (o.stencil) {
         const mpbp_schur_plan* p = o.stencil;
         const mpbp_row_part q = stencil_part(o);
@@ -3569,9 +3666,9 @@ int pair_spmv(const OpPair& o, int32_t mode, const double* x, const double* z, d
     return rc ? rc : op_spmv(o.bd, mode, x, z, y, st);
 }
 int pair_cheb(const OpPair& o, const double* xin, const double* b, const double* dg, double c1, double c2, double* d,
-              const double* sub, double* xo, hipStream_t st, int store_d) {
-    const int rc = op_cheb(o.in, xin, b, dg, c1, c2, d, sub, xo, st, store_d);
-    return rc ? rc : op_cheb(o.bd, xin, b, dg, c1, c2, d, sub, xo, st, store_d);
+              const double* sub, double* xo, hipStream_t st, int store_d, bool dzero = false) {
+    const int rc = op_cheb(o.in, xin, b, dg, c1, c2, d, sub, xo, st, store_d, dzero);
+    return rc ? rc : op_cheb(o.bd, xin, b, dg, c1, c2, d, sub, xo, st, store_d, dzero);
 }
 
 OpRef mg_csr_op(const mpbp_csr& A, const mpbp_rowblocks& blk) {
@@ -3580,6 +3677,7 @@ OpRef mg_csr_op(const mpbp_csr& A, const mpbp_rowblocks& blk) {
 // A level's operator: its SELL-64 copy when it has one (same bits), else the CSR form.
 OpPair mg_level_op(const mpbp_mg_level& L) {
     const OpRef none{nullptr, nullptr, nullptr, nullptr, true, 0, SOP_NONE};
+    if (use_grp(L.A)) return OpPair{OpRef{&L.A, &L.A_blocks, nullptr, nullptr, false, 0, SOP_NONE, 0, 1}, none};
     return OpPair{L.A_sell.nslices > 0 ? OpRef{&L.A, nullptr, &L.A_sell, nullptr, false, 0, SOP_NONE}
                                        : mg_csr_op(L.A, L.A_blocks), none};
 }
@@ -3599,12 +3697,13 @@ void mg_exchange(const mpbp_mg* m, int l, const MgFine& f, double* x, hipStream_
 }
 int mg_transfer(const mpbp_csr& M, const mpbp_rowblocks& blk, const mpbp_sell& S, int32_t mode, const double* x,
                 const double* z, double* y, hipStream_t st) {
+    if (use_grp(M)) return grp_spmv(&M, mode, x, z, y, st);
     return S.nslices > 0 ? mpbp_sell_spmv(&S, mode, x, z, y, (void*)st) : mpbp_spmv(&M, &blk, mode, x, z, y, (void*)st);
 }
 
 // y = M b for the coarsest level's dense (pseudo-)inverse, column-major (Mt[j * m + i] = M[i][j]).  A workgroup
-// owns kDR rows: its 1024 threads request a kDK-column slab of them at once (16 loads each, all in flight) into
-// LDS with the slab of b, then one lane per row adds the products over the columns in order from 0.0 -- the CSR
+// owns kDR rows: its 1024 threads request a kDK-column slab of them at once (16 loads each, all in flight), form
+// the slab's products with b in LDS, then one lane per row adds them over the columns in order from 0.0 -- the CSR
 // row's order with every entry stored (bit-identical to the CSR form of the same inverse).
 constexpr int kDR = 16, kDK = 1024, kDT = 1024;
 __global__ void __launch_bounds__(kDT) k_dense_cm(int32_t m, const double* __restrict__ Mt,
@@ -3624,12 +3723,15 @@ __global__ void __launch_bounds__(kDT) k_dense_cm(int32_t m, const double* __res
             v[u] = (c < kc && row < m) ? Mt[(size_t)(j0 + c) * m + row] : 0.0;
         }
         const double bv = t < kc ? b[j0 + t] : 0.0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) tile[t + kDT * u] = v[u];
         bs[t] = bv;
         __syncthreads();
+        // the slab's products M[row][col] * b[col] formed by all 1024 threads at once, so the summing lanes' loop is
+        // LDS reads and dependent adds only (22 -> ~6 us for the 1024-row coarsest F level)
+#pragma unroll
+        for (int u = 0; u < U; ++u) tile[t + kDT * u] = v[u] * bs[(t + kDT * u) / kDR];
+        __syncthreads();
         if (t < kDR)
-            for (int c = 0; c < kc; ++c) acc += tile[c * kDR + t] * bs[c];
+            for (int c = 0; c < kc; ++c) acc += tile[c * kDR + t];
         __syncthreads();
     }
     if (t < kDR && r0 + t < m) y[r0 + t] = acc;
@@ -3670,14 +3772,16 @@ int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, 
             return MPBP_OK;
         }
         s = 1;
-    } else {
-        MPBP_HIP(hipMemsetAsync(d, 0, sizeof(double) * (size_t)nrows, st));
     }
+    // restart from the iterate in *cur: d = 0 -- read as +0.0 by the grouped kernel's first sweep, else zeroed
+    bool dzero = !zero && op.in.grp && op.bd.empty;
+    if (!zero && !dzero) MPBP_HIP(hipMemsetAsync(d, 0, sizeof(double) * (size_t)nrows, st));
     for (; s < K; ++s) {
         const bool last = s == K - 1;
         double* nxt = (last && dst) ? dst : other;
         xch(x);
-        const int rc = pair_cheb(op, x, b, diag, c1[s], c2[s], d, last ? sub : nullptr, nxt, st, last ? 0 : 1);
+        const int rc = pair_cheb(op, x, b, diag, c1[s], c2[s], d, last ? sub : nullptr, nxt, st, last ? 0 : 1, dzero);
+        dzero = false;
         if (rc) return rc;
         other = x;
         x = nxt;

@@ -98,11 +98,21 @@ def test_hierarchy_bit_exact(n, coarsest):
             _same_csr(mg.R[l], Rs[l])
 
 
+@pytest.fixture(params=[65536, 0], ids=["grp", "nogrp"])
+def group_rows(request):
+    """Small multigrid levels on the grouped CSR kernel (default threshold) or on the SELL / CSR row kernels."""
+    from mp_block_preconditioners_amd._lib import check, lib
+    check(lib().mpbp_set_mg_group_rows(request.param))
+    yield request.param
+    check(lib().mpbp_set_mg_group_rows(65536))
+
+
 @pytest.mark.parametrize("sell", [True, False], ids=["sell", "csr"])
 @pytest.mark.parametrize("n,cycles,pre,post", [(16, 1, 2, 2), (32, 2, 2, 2), (64, 1, 1, 3), (64, 3, 2, 1)])
-def test_mg_solve_bit_exact(n, cycles, pre, post, sell):
+def test_mg_solve_bit_exact(n, cycles, pre, post, sell, group_rows):
     """V-cycles vs the oracle: with the SELL-64 copies of every level and the dense coarse kernel (default), and
-    with the CSR forms throughout."""
+    with the CSR forms throughout; the small levels and transfers on the grouped CSR kernel (several lanes per row,
+    the row's sum in order) or on the row kernels."""
     mp = _mp()
     from oracle import mg_oracle as mo
     _, (A, F, D, G), S = _system(n)
@@ -162,7 +172,7 @@ def _oracle_mg_apply(S, pc, v):
 @pytest.mark.parametrize("n", [16, 64])
 @pytest.mark.parametrize("pre", [2, 3, 1])
 @pytest.mark.parametrize("layout,f_mode,pg_mode", [("sell", "auto", "auto"), ("csr", "assembled", "assembled")])
-def test_schur_apply_mg_bit_exact(n, layout, f_mode, pg_mode, pre):
+def test_schur_apply_mg_bit_exact(n, layout, f_mode, pg_mode, pre, group_rows):
     """The Schur apply with multigrid inner solves vs the oracle; with matrix-free level-0 operators the first
     pre-smoothing sweep stages its x0 itself (no init launch) -- pre = 2, 3 take that path, pre = 1 the init."""
     mp = _mp()

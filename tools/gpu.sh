@@ -8,6 +8,7 @@
 #   tests        pytest -m gpu (all GPU parity tests)          smoke     __graft_entry__.smoke()
 #   tests:F1,F2  pytest -m gpu of the named test files / node ids only
 #   bench        bench.py, N = 1 (the driver's command)        bench_csr bench.py --layout csr
+#   bench:ARGS   bench.py ARGS ('+' for spaces; MPBP_BENCH_BACKEND etc. from the environment), appended to bench_args.log
 #   rows2_gloo   bench.py --gpus 2 --grid 512 over gloo on one GPU (the N > 1 path; launcher inside bench.py)
 #   selfhalo     bench.py --self-halo (partitioned apply over the RCCL self-exchange)
 #   probe        tools/capture_probe.py 256 1024 (hipGraph capture of the partitioned apply); probe:N1,N2 sizes
@@ -44,6 +45,8 @@ step() {
                --timeout-method thread -m gpu > "$OUT/pytest_part.log" 2>&1 ;;
     smoke) timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench) timeout -k 10 300 python bench.py --steps 20 --warmup 5 > "$OUT/bench.log" 2>&1 ;;
+    bench:*) local A=$(echo "${s#bench:}" | tr + ' ')   # bench.py with extra arguments ('+' for spaces)
+          timeout -k 10 400 python bench.py $A >> "$OUT/bench_args.log" 2>&1 ;;
     bench_csr) timeout -k 10 300 python bench.py --steps 20 --warmup 5 --layout csr --no-cpu-baseline \
                  > "$OUT/bench_csr.log" 2>&1 ;;
     rows2_gloo) MPBP_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --steps 5 --warmup 2 --grid 512 \
