@@ -109,6 +109,8 @@ def main():
                     help="grid rows per workgroup of the marching stencil kernels (matrix-free F, D, G, Gt_G); "
                          "0: the count that fills one round of workgroups per launch")
     ap.add_argument("--pg-direct", type=int, default=None, help="1: D / Gt_G sweeps as one thread per cell (no LDS)")
+    ap.add_argument("--svl-min-rows", type=int, default=None,
+                    help="multigrid levels above this many rows get a stencil-values copy (mg.SVL_MIN_ROWS; -1: none)")
     ap.add_argument("--mg-group-rows", type=int, default=None,
                     help="multigrid levels / transfers with at most this many rows on the grouped CSR kernel (0: off)")
     ap.add_argument("--no-fuse-g", action="store_true",
@@ -125,6 +127,8 @@ def main():
     ap.add_argument("--no-spmv", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch the apply eagerly instead of a hipGraph")
     ap.add_argument("--no-check", action="store_true", help="N > 1: skip the bit-exact check against one GPU")
+    ap.add_argument("--no-mg", action="store_true",
+                    help="skip the multigrid apply section (mg:1 / mg:1 applies/s and its dominant kernel's roofline)")
     ap.add_argument("--no-solve", action="store_true",
                     help="skip the solve-level section (FGMRES to 1e-8 on the manufactured problem, N = 1)")
     ap.add_argument("--partitioned-graph", action="store_true",
@@ -173,6 +177,9 @@ def main():
         _check(_lib().mpbp_set_pg_direct(args.pg_direct))
     if args.mg_group_rows is not None:
         _check(_lib().mpbp_set_mg_group_rows(args.mg_group_rows))
+    if args.svl_min_rows is not None:
+        from mp_block_preconditioners_amd import mg as _mg
+        _mg.SVL_MIN_ROWS = None if args.svl_min_rows < 0 else args.svl_min_rows
 
     if args.weak:
         n = int(round((args.n or 1024) * math.sqrt(world)))
@@ -182,6 +189,7 @@ def main():
     kp, spp = parse_inner(args.inner_p)
     iF, iP = mp.InnerSolver(kf, sf), mp.InnerSolver(kp, spp)
     A = None
+    mg_ops = None
     t_setup = time.perf_counter()
     if not partitioned:
         bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
@@ -189,6 +197,7 @@ def main():
         pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, layout=args.layout,
                                           f_mode=args.f_mode, pg_mode=args.pg_mode, q_mode=args.q_mode,
                                           fuse_g=not args.no_fuse_g)
+        mg_ops = (F, D, G) if not args.no_mg else None
         del F, D, G
     else:
         from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
@@ -303,6 +312,14 @@ def main():
                    "note": f"ApproxSchurPreconditioner.matvec on a host ndarray ({vh.nbytes / 1e6:.0f} MB in and "
                            "out over PCIe per call through page-locked staging buffers), eager apply; wall clock over 10 calls"}
 
+    mg_apply = None
+    if rank == 0 and not partitioned and mg_ops is not None and kf != "mg":
+        try:
+            mg_apply = mg_apply_bench(*mg_ops, args.steps, args.warmup, gen)
+        except Exception as e:   # reported, never fatal to the headline line
+            mg_apply = {"error": f"{type(e).__name__}: {e}"}
+    mg_ops = None
+
     cpu = None
     if rank == 0 and not partitioned and not args.no_cpu_baseline:
         cpu = cpu_baseline(pc, v, args.cpu_seconds, kf, sf, kp, spp)
@@ -370,6 +387,7 @@ def main():
                 "avg_launch_us": spmv["csr_us"],
                 "back_to_back_us": spmv["csr_us_graph"], "frac_back_to_back": spmv["csr_gbs_graph"] / HBM_PEAK_GBS,
                 "timing": spmv.get("timing", "") + " (one kernel per matvec)"},
+            "mg_apply": mg_apply,
             "host_buffer_matvec": host_io,
             "solve_level": solve,
             "cpu_baseline": cpu,
@@ -481,6 +499,66 @@ def spmv_bench(A, gen, reps=20, replays=10, warm_replays=5):
                     f"{name}_us_graph": s * 1e6, f"{name}_gbs_graph": nbytes / s / 1e9,
                     f"{name}_us_eager": s_eager * 1e6})
     return res
+
+
+def mg_apply_bench(F, D, G, steps, warmup, gen, reps=20):
+    """The apply with one multigrid V-cycle per inner inverse (mg:1 / mg:1: the configuration that converges FGMRES in
+    solve_level, solve.py:266 / 274's pointer), hipGraph-replayed as the headline apply, and the roofline of its
+    dominant kernel family: the level-1 F Galerkin operator's Chebyshev sweep on its SELL-64 copy (k_sell_rows<EpiCheb>,
+    8 launches per apply at 1024^2), HIP events around each of `reps` launches of that kernel on the level's own
+    buffers."""
+    import ctypes
+    import torch
+    import mp_block_preconditioners_amd as mp
+    from mp_block_preconditioners_amd._lib import check, lib, ptr, stream_handle
+    t0 = time.perf_counter()
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("mg", 1), inner_P=mp.InnerSolver("mg", 1))
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t0
+    v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda", generator=gen)
+    out = torch.empty_like(v)
+    g = pc.capture(v, out)
+    for _ in range(warmup):
+        g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.replay()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    del g
+    mg = pc.mg_F
+    S, M1, w, dg = mg.sells[0][1], mg.ops[1], mg.work[1], mg.diags[1]
+    c1, c2 = (ctypes.c_double * 2)(), (ctypes.c_double * 2)()
+    check(lib().mpbp_cheb_coeffs(mg.bounds[1][0], mg.bounds[1][1], 2, c1, c2))
+    x, xo, d, b = w[0], w[1], w[3], w[4]
+    x.normal_(generator=gen)
+    b.normal_(generator=gen)
+    d.zero_()
+    def sweep():
+        check(lib().mpbp_sell_cheb_step(ctypes.byref(S.cstruct()), ptr(x), ptr(b), ptr(dg), c1[1], c2[1], ptr(d),
+                                        None, ptr(xo), stream_handle()))
+    for _ in range(3):
+        sweep()
+    pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, e in pairs:
+        a.record()
+        sweep()
+        e.record()
+    torch.cuda.synchronize()
+    us = sum(a.elapsed_time(e) for a, e in pairs) * 1e3 / reps
+    rows = M1.shape[0]
+    # 12 B per entry (value + column) + 1 B row length per row + 16 B per slice descriptor; per row x (gathered,
+    # counted once), b, diag, d read, d written, x_out (8 B each)
+    nbytes = M1.nnz * 12 + rows * (1 + 6 * 8) + S.nslices * 16
+    return {"value": 1.0 / dt, "unit": "applies/s", "ms_per_step": dt * 1e3, "inner_F": "mg:1", "inner_P": "mg:1",
+            "setup_seconds": setup_s, "launch": "hipgraph",
+            "levels_F": mg.sizes, "levels_P": pc.mg_P.sizes,
+            "roofline": {"bound": "hbm", "achieved": nbytes / us / 1e3, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": nbytes / us / 1e3 / HBM_PEAK_GBS, "kernel": "k_sell_rows<EpiCheb> (level-1 F Galerkin "
+                         f"operator, {rows} rows x {M1.nnz / rows:.0f} entries, SELL-64)", "bytes_per_launch": nbytes,
+                         "avg_launch_us": us, "launches_per_apply": 8,
+                         "timing": f"mean of HIP event pairs around each of {reps} launches on the level's buffers"}}
 
 
 SOLVE_CASES = (   # (n, eta_n, eta_s, preconditioners): BASELINE configs[1] / configs[3] at 256^2, configs[2] / [3] at 1024^2

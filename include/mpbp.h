@@ -105,6 +105,22 @@ typedef struct mpbp_sell {
     const int32_t* col;
 } mpbp_sell;
 
+/* Stencil-values layout of a translation-invariant operator on `nfields` stacked m x m periodic fields (the
+ * multigrid's Galerkin levels: every row of field f holds the same `slots` (field, dr, dc) offsets): the values
+ * alone, slot-major (vals[s * nrows + row], slot order = an interior row's CSR column order), the columns rebuilt as
+ * row + delta[f * slots + s].  Interior rows (reach <= r, c < m - reach; m and reach even: the kernel takes
+ * interior cells in horizontal pairs with 16-byte value loads) sum in slot order; the rows within `reach`
+ * of the periodic edge (edge_rows, whose wrapped columns sort differently) are summed from the CSR form.  Same
+ * products in the same order as the CSR SpMV: bit-identical.  Built by the Python layer (mg.stencil_values). */
+typedef struct mpbp_svl {
+    int32_t nfields, m, reach, slots;
+    const int32_t* delta;            /* device, nfields * slots */
+    const double* vals;              /* device, slots * nrows */
+    const int32_t* edge_rows;        /* device, n_edge row ids */
+    int32_t n_edge;
+    int32_t reserved;
+} mpbp_svl;
+
 /* Grid-row partition of the 4 velocity fields (multi-GPU F stencil): the rank owns grid rows
  * [r0, r0 + rows) of every field, followed in its vectors by the ghost rows: `halo` rows above of
  * every field (field-major), then `halo` rows below of every field.  which: 0 all owned rows, 1 rows off the first/last owned grid row, 2 those
@@ -162,6 +178,8 @@ typedef struct mpbp_mg_level {
      * (or, at the last partitioned level, the whole next level) */
     int32_t halo_kind;
     int32_t reserved2;
+    /* optional stencil-values copy of A (NULL: none; used for levels above the grouped kernel's row limit) */
+    const mpbp_svl* A_svl;
 } mpbp_mg_level;
 
 typedef void (*mpbp_halo_fn)(void* ctx, int32_t vec_kind, double* x_ext, int32_t phase, void* stream);
@@ -281,6 +299,10 @@ int mpbp_spgemm_fill(const mpbp_csr* A, const mpbp_csr* B, double alpha, const i
  * mpbp_q13_spmv: y = Q x (modes as mpbp_spmv), the CSR SpMV's result bit for bit; replaces np.matmul(Gt_F_G, x_a)
  * (solve.py:267) -- the columns are implicit in the grid, so the layout streams 104 B per row instead of 156. */
 int mpbp_q13_build(const mpbp_csr* Q, int32_t n, double* vals, void* stream);
+/* y = op(A x) through the stencil-values layout V of A (edge rows from A's CSR arrays); modes as mpbp_spmv.  The
+ * CSR SpMV's result bit for bit. */
+int mpbp_svl_spmv(const mpbp_svl* V, const mpbp_csr* A, int32_t mode, const double* x, const double* z, double* y,
+                  void* stream);
 int mpbp_q13_spmv(int32_t n, const double* vals, int32_t mode, const double* x, const double* z, double* y,
                   void* stream);
 
@@ -391,6 +413,8 @@ int mpbp_set_pg_direct(int32_t on);
 /* Multigrid levels and transfers with at most `rows` rows run on the grouped CSR kernel (several lanes per row,
  * products in parallel, the row's sum in order by one lane: same bits); 0 disables it.  Default 65536. */
 int mpbp_set_mg_group_rows(int32_t rows);
+/* 1 (default): multigrid levels with a stencil-values copy (mpbp_mg_level.A_svl) use it; 0: their SELL / CSR form. */
+int mpbp_set_mg_svl(int32_t on);
 
 /* ---- geometric multigrid inner solves (the reference's pointer: solve.py:266, 274) ------------------ */
 /* P (which = MPBP_MG_P, fine x coarse) or R = P^T (MPBP_MG_R) of an n x n periodic grid (n even, >= 4) coarsened by 2,

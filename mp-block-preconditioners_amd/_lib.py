@@ -55,12 +55,19 @@ class InnerSolverC(Structure):
     _fields_ = [("kind", c_int32), ("sweeps", c_int32), ("lmin", c_double), ("lmax", c_double)]
 
 
+class Svl(Structure):
+    _fields_ = [("nfields", c_int32), ("m", c_int32), ("reach", c_int32), ("slots", c_int32),
+                ("delta", c_void_p), ("vals", c_void_p), ("edge_rows", c_void_p), ("n_edge", c_int32),
+                ("reserved", c_int32)]
+
+
 class MgLevel(Structure):
     _fields_ = [("nrows", c_int32), ("pre", c_int32), ("post", c_int32), ("reserved", c_int32),
                 ("lmin", c_double), ("lmax", c_double), ("A", Csr), ("A_blocks", RowBlocks), ("diag", c_void_p),
                 ("R", Csr), ("R_blocks", RowBlocks), ("P", Csr), ("P_blocks", RowBlocks),
                 ("x", c_void_p), ("t", c_void_p), ("r", c_void_p), ("d", c_void_p), ("b", c_void_p),
-                ("A_sell", Sell), ("R_sell", Sell), ("P_sell", Sell), ("halo_kind", c_int32), ("reserved2", c_int32)]
+                ("A_sell", Sell), ("R_sell", Sell), ("P_sell", Sell), ("halo_kind", c_int32), ("reserved2", c_int32),
+                ("A_svl", POINTER(Svl))]
 
 
 HALO_FN = CFUNCTYPE(None, c_void_p, c_int32, c_void_p, c_int32, c_void_p)
@@ -153,7 +160,9 @@ _SIGNATURES = {
     "mpbp_set_init_diag": ([c_int32], c_int),
     "mpbp_set_pg_direct": ([c_int32], c_int),
     "mpbp_set_mg_group_rows": ([c_int32], c_int),
+    "mpbp_set_mg_svl": ([c_int32], c_int),
     "mpbp_q13_build": ([POINTER(Csr), c_int32, c_void_p, c_void_p], c_int),
+    "mpbp_svl_spmv": ([POINTER(Svl), POINTER(Csr), c_int32, _P, _P, _P, _P], c_int),
     "mpbp_q13_spmv": ([c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "mpbp_mg_transfer_count": ([c_int32, c_int32, _P, c_int32, _P, _P], c_int),
     "mpbp_mg_transfer_fill": ([c_int32, c_int32, _P, c_int32, _P, _P, _P, _P], c_int),

@@ -1241,8 +1241,20 @@ struct EpiZeroD : Epi {   // Epi = EpiCheb: d read as +0.0 (never loaded)
         return {this->xin[r], ld_stream(this->b + r), this->diag[r], 0.0, this->sub ? ld_stream(this->sub + r) : 0.0};
     }
 };
-template <int G, class Epi>
-__global__ void __launch_bounds__(kBlock) k_csr_grp(Csr A, int32_t nrows, const double* __restrict__ x, Epi epi) {
+// The first Chebyshev sweep from x = 0 with the init pass folded in (XS = XInit gathers x0 = c2_0 (b / diag) at every
+// column, the same expression k_cheb_init stores): the epilogue's x and direction are the row's own x0.
+struct EpiChebFirstGrp : EpiChebFirst {
+    const double* diag;
+    double c2_0;
+    __device__ P pre(int32_t r) const {
+        P p = EpiChebFirst::pre(r);
+        p.dg = diag[r];
+        p.x = c2_0 * (p.b / p.dg);
+        return p;
+    }
+};
+template <int G, class XS, class Epi>
+__global__ void __launch_bounds__(kBlock) k_csr_grp(Csr A, int32_t nrows, XS xs, Epi epi) {
     constexpr int RPB = kBlock / G, CAP = G * kGrpJ;
     __shared__ double prod[RPB * CAP];
     const int g = threadIdx.x / G, k = threadIdx.x % G;
@@ -1266,7 +1278,7 @@ __global__ void __launch_bounds__(kBlock) k_csr_grp(Csr A, int32_t nrows, const 
         }
         double p[kGrpJ];
 #pragma unroll
-        for (int j = 0; j < kGrpJ; ++j) p[j] = v[j] * x[c[j]];
+        for (int j = 0; j < kGrpJ; ++j) p[j] = v[j] * xs(c[j]);
         if (cb != ks) wave_lds_sync();   // the previous chunk's sums have read their slots
 #pragma unroll
         for (int j = 0; j < kGrpJ; ++j) pr[k + G * j] = p[j];
@@ -1277,6 +1289,104 @@ __global__ void __launch_bounds__(kBlock) k_csr_grp(Csr A, int32_t nrows, const 
         }
     }
     if (live && k == 0) epi(r, acc, pe);
+}
+
+// ------------------------------------------------------------ stencil-values layout ----
+// The multigrid's large Galerkin levels (F level 1 at 1024^2: 1 M rows x 40 entries) stream 12 B per entry on SELL;
+// their rows all hold the same (field, dr, dc) offsets (translation-invariant operator on a periodic grid), so the
+// column indices are rebuilt as row + delta[f][s] and only the values are streamed, slot-major (coalesced per slot
+// across consecutive rows, nontemporal).  One thread per interior row (threads enumerate the interior cells of
+// every field densely, so no wave mixes the two paths): K products in slot order = the CSR row's column order;
+// the x gathers need no column load, so they issue beside the value loads.  Then one thread per edge row (within
+// `reach` of the periodic edge, where the wrapped columns sort differently): the CSR row, left to right.  Both the
+// CSR SpMV's additions exactly (bit-identical), at 8 B instead of 12 B per entry for all but the edge rows.
+struct Svl {
+    int nf, m, R, K;
+    const int32_t* delta;
+    const double* vals;
+    const int32_t* edge;
+    int n_edge;
+};
+#ifndef MPBP_SVL_BATCH
+#define MPBP_SVL_BATCH 8
+#endif
+constexpr int kSvB = MPBP_SVL_BATCH;  // slots per batch (values + gathers in flight together)
+constexpr int kSvMaxDelta = 256;     // nf * K
+constexpr int kSvEdgeG = 8;          // lanes per edge row (k_csr_grp's scheme: one latency chain per row)
+template <class XS, class Epi>
+__global__ void __launch_bounds__(kBlock) k_svl(Svl V, Csr A, int32_t nrows, XS xs, Epi epi) {
+    __shared__ int32_t sdelta[kSvMaxDelta];
+    __shared__ double prod[kBlock * kGrpJ];
+    for (int i = threadIdx.x; i < V.nf * V.K; i += kBlock) sdelta[i] = V.delta[i];
+    __syncthreads();
+    // interior: one thread per pair of horizontally adjacent cells (reach is even, so W = m - 2 reach is even and a
+    // pair starts on an even row id): 16-byte value loads, two rows' products, two ordered sums
+    const int W = V.m - 2 * V.R, W2 = W >> 1;
+    const int32_t per = W2 * W;                        // pairs per field
+    const int32_t ni = V.nf * per;
+    const int32_t ni_pad = (ni + 63) & ~63;            // edge rows start on a wave boundary
+    const int32_t t = (int32_t)xcd_swizzle(blockIdx.x, gridDim.x) * kBlock + (int32_t)threadIdx.x;
+    if (t < ni) {
+        const uint32_t f = (uint32_t)t / (uint32_t)per;
+        const uint32_t i = (uint32_t)t - f * (uint32_t)per;
+        const uint32_t q = i / (uint32_t)W2;
+        const int r = V.R + (int)q, c = V.R + 2 * (int)(i - q * (uint32_t)W2);
+        const int32_t row = ((int32_t)f * V.m + r) * V.m + c;
+        const typename Epi::P pe0 = epi.pre(row), pe1 = epi.pre(row + 1);
+        const int32_t* dl = sdelta + f * V.K;
+        const double* vp = V.vals + row;
+        double a0 = 0.0, a1 = 0.0;
+        for (int s0 = 0; s0 < V.K; s0 += kSvB) {
+            f64x2 v[kSvB];
+            double x0[kSvB], x1[kSvB];
+#pragma unroll
+            for (int j = 0; j < kSvB; ++j) {
+                const int sj = min(s0 + j, V.K - 1);   // (a tail batch re-reads the last slot and discards it)
+                v[j] = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(vp + (int64_t)sj * nrows));
+                const int32_t col = row + dl[sj];
+                x0[j] = xs(col);
+                x1[j] = xs(col + 1);
+            }
+#pragma unroll
+            for (int j = 0; j < kSvB; ++j)
+                if (s0 + j < V.K) {
+                    a0 += v[j].x * x0[j];
+                    a1 += v[j].y * x1[j];
+                }
+        }
+        epi(row, a0, pe0);
+        epi(row + 1, a1, pe1);
+    } else if (t >= ni_pad && (t - ni_pad) / kSvEdgeG < V.n_edge) {
+        // edge row: kSvEdgeG lanes load its CSR entries at once and form the products, the first lane sums them in
+        // order (k_csr_grp)
+        constexpr int G = kSvEdgeG, CAP = G * kGrpJ;
+        const int64_t u = t - ni_pad;
+        const int32_t row = V.edge[u / G];
+        const int k = (int)(u % G);
+        double* pr = prod + (threadIdx.x / G) * CAP;
+        typename Epi::P pe{};
+        if (k == 0) pe = epi.pre(row);
+        const int32_t ks = A.rp[row], ke = A.rp[row + 1];
+        double acc = 0.0;
+        for (int32_t cb = ks; cb < ke; cb += CAP) {
+            double p[kGrpJ];
+#pragma unroll
+            for (int j = 0; j < kGrpJ; ++j) {
+                const int32_t e = cb + k + G * j;
+                const bool in = e < ke;
+                p[j] = (in ? A.va[e] : 0.0) * xs(in ? A.ci[e] : row);
+            }
+            if (cb != ks) wave_lds_sync();
+#pragma unroll
+            for (int j = 0; j < kGrpJ; ++j) pr[k + G * j] = p[j];
+            wave_lds_sync();
+            if (k == 0) {
+                const int32_t cnt = min(ke - cb, (int32_t)CAP);
+                for (int32_t i = 0; i < cnt; ++i) acc += pr[i];
+            }
+        }
+        if (k == 0) epi(row, acc, pe);
+    }
 }
 
 // ------------------------------------------------------------------ SELL-64 ----
@@ -2410,15 +2520,16 @@ int launch_rows(const mpbp_csr* A, const mpbp_rowblocks* blk, const double* x, E
 }
 // Small-level CSR products through k_csr_grp: lanes per row from the mean row length (2: <= 16 entries, 4: <= 32,
 // 8: longer), so one chunk holds a multigrid coarse row (transfers 1-16 entries, Galerkin levels 20-46).
+int g_svl_on = 1;         // multigrid levels with a stencil-values copy use it (0: SELL / CSR instead)
 int g_grp_rows = 65536;   // multigrid levels / transfers with at most this many rows use it (0: never)
-template <class Epi>
-int launch_grp(const mpbp_csr* A, const double* x, Epi epi, hipStream_t st) {
+template <class Epi, class XS = XPlain>
+int launch_grp(const mpbp_csr* A, const XS& xs, Epi epi, hipStream_t st) {
     if (A->nrows <= 0) return MPBP_OK;
     const int64_t avg = A->nnz / A->nrows;
     auto go = [&](auto gc) {
         constexpr int G = decltype(gc)::value;
         constexpr int rpb = kBlock / G;
-        k_csr_grp<G, Epi><<<(unsigned)((A->nrows + rpb - 1) / rpb), kBlock, 0, st>>>(to_csr(A), A->nrows, x, epi);
+        k_csr_grp<G, XS, Epi><<<(unsigned)((A->nrows + rpb - 1) / rpb), kBlock, 0, st>>>(to_csr(A), A->nrows, xs, epi);
         MPBP_HIP(hipGetLastError());
         return (int)MPBP_OK;
     };
@@ -2427,19 +2538,68 @@ int launch_grp(const mpbp_csr* A, const double* x, Epi epi, hipStream_t st) {
 }
 inline bool use_grp(const mpbp_csr& A) { return g_grp_rows > 0 && A.nrows > 0 && A.nrows <= g_grp_rows && A.nnz > 0; }
 int grp_spmv(const mpbp_csr* A, int32_t mode, const double* x, const double* z, double* y, hipStream_t st) {
+    const XPlain xs{x};
     switch (mode) {
-    case MPBP_SPMV_STORE: return launch_grp(A, x, EpiStore{y}, st);
-    case MPBP_SPMV_ADD: return launch_grp(A, x, EpiAdd{z, y}, st);
-    case MPBP_SPMV_RESID: return launch_grp(A, x, EpiResid{z, y}, st);
+    case MPBP_SPMV_STORE: return launch_grp(A, xs, EpiStore{y}, st);
+    case MPBP_SPMV_ADD: return launch_grp(A, xs, EpiAdd{z, y}, st);
+    case MPBP_SPMV_RESID: return launch_grp(A, xs, EpiResid{z, y}, st);
     default: return set_error(MPBP_ERR_ARG, "grp_spmv: unknown mode %d", mode);
     }
 }
 int grp_cheb(const mpbp_csr* A, const double* xin, const double* b, const double* dg, double c1, double c2, double* d,
              const double* sub, double* xo, hipStream_t st, int store_d, bool dzero) {
     const EpiCheb e{xin, b, dg, d, c1, c2, sub, xo, store_d};
-    return dzero ? launch_grp(A, xin, EpiZeroD<EpiCheb>{e}, st) : launch_grp(A, xin, e, st);
+    const XPlain xs{xin};
+    return dzero ? launch_grp(A, xs, EpiZeroD<EpiCheb>{e}, st) : launch_grp(A, xs, e, st);
+}
+// First sweep from x = 0: x0 = d0 = c2_0 b / diag folded in (no k_cheb_init launch, same bits).
+int grp_cheb_first(const mpbp_csr* A, const double* b, const double* dg, double c2_0, double c1, double c2, double* d,
+                   const double* sub, double* xo, hipStream_t st, int store_d) {
+    EpiChebFirstGrp e;
+    static_cast<EpiChebFirst&>(e) = EpiChebFirst{b, d, c1, c2, sub, xo, store_d};
+    e.diag = dg;
+    e.c2_0 = c2_0;
+    return launch_grp(A, XInit{b, dg, c2_0}, e, st);
 }
 
+// Products through the stencil-values layout (k_svl).
+inline Svl to_svl(const mpbp_svl* V) {
+    return Svl{V->nfields, V->m, V->reach, V->slots, V->delta, V->vals, V->edge_rows, V->n_edge};
+}
+int check_svl(const mpbp_svl* V, const mpbp_csr* A) {
+    if (!V || !A || V->slots < 1 || V->nfields < 1 || V->nfields * V->slots > kSvMaxDelta || V->reach < 0 ||
+        V->m < 2 * V->reach + 2 || (V->m & 1) || (V->reach & 1) || (int64_t)V->nfields * V->m * V->m != A->nrows ||
+        (int64_t)V->slots * A->nrows > INT32_MAX || !V->delta || !V->vals ||
+        V->n_edge < 0 || (V->n_edge && !V->edge_rows))
+        return set_error(MPBP_ERR_ARG, "svl: layout does not match the operator");
+    return MPBP_OK;
+}
+template <class Epi, class XS = XPlain>
+int launch_svl(const mpbp_svl* V, const mpbp_csr* A, const XS& xs, Epi epi, hipStream_t st) {
+    const int64_t w = V->m - 2 * V->reach;
+    const int64_t threads = ((V->nfields * (w / 2) * w + 63) & ~(int64_t)63) + (int64_t)V->n_edge * kSvEdgeG;
+    if (threads <= 0) return MPBP_OK;
+    k_svl<XS, Epi><<<(unsigned)((threads + kBlock - 1) / kBlock), kBlock, 0, st>>>(to_svl(V), to_csr(A), A->nrows, xs,
+                                                                                    epi);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+int svl_spmv(const mpbp_svl* V, const mpbp_csr* A, int32_t mode, const double* x, const double* z, double* y,
+             hipStream_t st) {
+    const XPlain xs{x};
+    switch (mode) {
+    case MPBP_SPMV_STORE: return launch_svl(V, A, xs, EpiStore{y}, st);
+    case MPBP_SPMV_ADD: return launch_svl(V, A, xs, EpiAdd{z, y}, st);
+    case MPBP_SPMV_RESID: return launch_svl(V, A, xs, EpiResid{z, y}, st);
+    default: return set_error(MPBP_ERR_ARG, "svl_spmv: unknown mode %d", mode);
+    }
+}
+int svl_cheb(const mpbp_svl* V, const mpbp_csr* A, const double* xin, const double* b, const double* dg, double c1,
+             double c2, double* d, const double* sub, double* xo, hipStream_t st, int store_d, bool dzero) {
+    const EpiCheb e{xin, b, dg, d, c1, c2, sub, xo, store_d};
+    const XPlain xs{xin};
+    return dzero ? launch_svl(V, A, xs, EpiZeroD<EpiCheb>{e}, st) : launch_svl(V, A, xs, e, st);
+}
 template <class Epi>
 int launch_rows_seg(const mpbp_csr* A, const mpbp_rowblocks* blk, const double* x, Epi epi, hipStream_t st) {
     if (!blk || blk->count <= 0) return MPBP_OK;
@@ -2494,6 +2654,10 @@ const char* mpbp_version(void) { return "libmpbp 0.1 (gfx950)"; }
 int mpbp_set_march_rows(int32_t rows) {
     if (rows < 0 || rows > 4096) return set_error(MPBP_ERR_ARG, "march rows must be 0 (auto) or in [1, 4096]");
     g_march_rows = rows;
+    return MPBP_OK;
+}
+int mpbp_set_mg_svl(int32_t on) {
+    g_svl_on = on ? 1 : 0;
     return MPBP_OK;
 }
 int mpbp_set_mg_group_rows(int32_t rows) {
@@ -3452,6 +3616,15 @@ int launch_q13(int32_t n, const double* vals, const double* x, Epi epi, hipStrea
 }  // namespace
 
 extern "C" {
+int mpbp_svl_spmv(const mpbp_svl* V, const mpbp_csr* A, int32_t mode, const double* x, const double* z, double* y,
+                  void* stream) {
+    int rc = check_csr(A);
+    if (!rc) rc = check_svl(V, A);
+    if (rc) return rc;
+    if (!x || !y || (mode != MPBP_SPMV_STORE && !z)) return set_error(MPBP_ERR_ARG, "svl_spmv: bad vectors");
+    return svl_spmv(V, A, mode, x, z, y, as_stream(stream));
+}
+
 int mpbp_q13_build(const mpbp_csr* Q, int32_t n, double* vals, void* stream) {
     int rc = check_csr(Q);
     if (rc) return rc;
@@ -3514,6 +3687,7 @@ struct OpRef {
     int32_t sop;
     int32_t ext = 0;                  // which = 3
     int32_t grp = 0;                  // CSR rows through k_csr_grp (multigrid small levels)
+    const mpbp_svl* svl = nullptr;    // stencil-values layout of csr (multigrid large levels)
 };
 
 // F and D read velocity vectors (f_part), G and Gt_G pressure vectors (p_part); D writes a pressure vector
@@ -3538,6 +3712,7 @@ int op_spmv(const OpRef& o, int32_t mode, const double* x, const double* z, doub
         return mpbp_pg_stencil_spmv(&p->f_prm, p->f_cell, &q, op, mode, x, z, y, (void*)st);
     }
     if (o.grp) return grp_spmv(o.csr, mode, x, z, y, st);
+    if (o.svl) return svl_spmv(o.svl, o.csr, mode, x, z, y, st);
     return o.sell ? mpbp_sell_spmv(o.sell, mode, x, z, y, (void*)st)
                   : mpbp_spmv(o.csr, o.blk, mode, x, z, y, (void*)st);
 }
@@ -3559,6 +3734,7 @@ int op_cheb(const OpRef& o, const double* xin, const double* b, const double* dg
             const double* sub, double* xo, hipStream_t st, int store_d, bool dzero = false) {
     if (o.empty) return MPBP_OK;
     if (o.grp) return grp_cheb(o.csr, xin, b, dg, c1, c2, d, sub, xo, st, store_d, dzero);
+    if (o.svl) return svl_cheb(o.svl, o.csr, xin, b, dg, c1, c2, d, sub, xo, st, store_d, dzero);
     if (dzero) return set_error(MPBP_ERR_ARG, "cheb: a zero direction is only supported on the grouped CSR path");
     if (o.stencil) {
         const mpbp_schur_plan* p = o.stencil;
@@ -3678,6 +3854,8 @@ OpRef mg_csr_op(const mpbp_csr& A, const mpbp_rowblocks& blk) {
 OpPair mg_level_op(const mpbp_mg_level& L) {
     const OpRef none{nullptr, nullptr, nullptr, nullptr, true, 0, SOP_NONE};
     if (use_grp(L.A)) return OpPair{OpRef{&L.A, &L.A_blocks, nullptr, nullptr, false, 0, SOP_NONE, 0, 1}, none};
+    if (L.A_svl && g_svl_on)
+        return OpPair{OpRef{&L.A, &L.A_blocks, nullptr, nullptr, false, 0, SOP_NONE, 0, 0, L.A_svl}, none};
     return OpPair{L.A_sell.nslices > 0 ? OpRef{&L.A, nullptr, &L.A_sell, nullptr, false, 0, SOP_NONE}
                                        : mg_csr_op(L.A, L.A_blocks), none};
 }
@@ -3763,6 +3941,16 @@ int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, 
         other = x;
         x = out1;
         s = 2;
+    } else if (zero && K >= 2 && op.bd.empty && o.grp) {
+        // grouped small level: the first sweep gathers x0 = c2[0] b / diag itself (no init launch, same bits; on the
+        // large stencil-values levels the division per gathered entry costs more than the init launch: 110 vs 97 us)
+        double* out1 = K == 2 ? (dst ? dst : other) : other;
+        const int rc = grp_cheb_first(o.csr, b, diag, c2[0], c1[1], c2[1], d, K == 2 ? sub : nullptr, out1, st,
+                                      K == 2 ? 0 : 1);
+        if (rc) return rc;
+        other = x;
+        x = out1;
+        s = 2;
     } else if (zero) {
         double* out0 = K == 1 ? (dst ? dst : other) : x;
         int rc = mpbp_cheb_init(nrows, b, diag, c2[0], d, K == 1 ? sub : nullptr, out0, (void*)st);
@@ -3774,7 +3962,7 @@ int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, 
         s = 1;
     }
     // restart from the iterate in *cur: d = 0 -- read as +0.0 by the grouped kernel's first sweep, else zeroed
-    bool dzero = !zero && op.in.grp && op.bd.empty;
+    bool dzero = !zero && (op.in.grp || op.in.svl) && op.bd.empty;
     if (!zero && !dzero) MPBP_HIP(hipMemsetAsync(d, 0, sizeof(double) * (size_t)nrows, st));
     for (; s < K; ++s) {
         const bool last = s == K - 1;

@@ -61,6 +61,84 @@ def sell_copy(A: DeviceCSR) -> DeviceSELL | None:
     return A.to_sell()
 
 
+class StencilValues:
+    """Stencil-values layout (``mpbp_svl``) of a translation-invariant operator on nf stacked m x m periodic fields: every
+    row of field f holds the same K (field, dr, dc) offsets, so only the values are kept, slot-major, and the kernel
+    rebuilds an interior row's columns as row + delta[f][s].  Built on the GPU from the CSR arrays (``build``), which it
+    verifies: uniform row length, every row's wrapped offsets a permutation of the field's K slots, interior rows in
+    slot order (so the interior sums are the CSR row's, bit for bit).  Rows within `reach` of the periodic edge are
+    listed for the kernel's CSR path.  None when the operator is not of that form."""
+
+    def __init__(self, A: DeviceCSR, nf: int, m: int, reach: int, K: int, delta, vals, edge_rows):
+        self.A, self.nf, self.m, self.reach, self.slots = A, nf, m, reach, K
+        self.delta, self.vals, self.edge_rows = delta, vals, edge_rows
+        self._cs = _lib.Svl(nf, m, reach, K, delta.data_ptr(), vals.data_ptr(),
+                            edge_rows.data_ptr() if edge_rows.numel() else None, int(edge_rows.numel()), 0)
+
+    def cstruct(self):
+        return self._cs
+
+    @classmethod
+    def build(cls, A: DeviceCSR, nf: int, m: int) -> "StencilValues | None":
+        N = nf * m * m
+        if A.shape != (N, N) or A.nnz == 0 or m < 4:
+            return None
+        dev = A.device
+        rp = A.row_ptr.long()
+        lens = rp[1:] - rp[:-1]
+        K = int(lens[0])
+        if K < 1 or nf * K > 256 or not bool(torch.all(lens == K)):
+            return None
+        e = torch.arange(A.nnz, device=dev)
+        rows, pos = e // K, e % K
+        del e
+        mm = m * m
+        ci = A.col_idx.long()
+        f, cell = rows // mm, rows % mm
+        r, c = cell // m, cell % m
+        fc, cc = ci // mm, ci % mm
+        dr = (cc // m - r + m // 2) % m - m // 2
+        dc = (cc % m - c + m // 2) % m - m // 2
+        del cell, cc
+        R = int(torch.maximum(dr.abs().max(), dc.abs().max()))
+        if m % 2 or m < 2 * R + 4 or K * N > 2 ** 31 - 1:
+            return None
+        w = 2 * R + 1
+        table = torch.full((nf, nf, w, w), -1, dtype=torch.long, device=dev)
+        delta = torch.empty(nf, K, dtype=torch.int32, device=dev)
+        for f0 in range(nf):
+            base = f0 * mm + (m // 2) * m + m // 2
+            sl = slice(base * K, base * K + K)
+            table[f0, fc[sl], dr[sl] + R, dc[sl] + R] = torch.arange(K, device=dev)
+            delta[f0] = (ci[sl] - base).to(torch.int32)
+        slot = table[f, fc, dr + R, dc + R]
+        del fc, dr, dc, table
+        if bool((slot < 0).any()):
+            return None
+        seen = torch.bincount(rows * K + slot, minlength=N * K)
+        if not bool(torch.all(seen == 1)):
+            return None
+        del seen
+        if bool(((slot != pos) & (r >= R) & (r < m - R) & (c >= R) & (c < m - R)).any()):
+            return None
+        R += R & 1   # the kernel's interior cells go in pairs from an even column: an odd reach widens the edge band
+        interior = (r >= R) & (r < m - R) & (c >= R) & (c < m - R)
+        vals = torch.empty(K * N, dtype=torch.float64, device=dev)
+        vals[slot * N + rows] = A.val
+        row_int = interior.view(N, K)[:, 0]
+        edge = torch.nonzero(~row_int).reshape(-1).to(torch.int32)
+        return cls(A, nf, m, R, K, delta.reshape(-1).contiguous(), vals, edge)
+
+    def matvec(self, x: torch.Tensor, out: torch.Tensor | None = None, mode=_lib.SPMV_STORE,
+               z: torch.Tensor | None = None) -> torch.Tensor:
+        if out is None:
+            out = torch.empty(self.A.shape[0], dtype=torch.float64, device=self.A.device)
+        check(lib().mpbp_svl_spmv(ctypes.byref(self._cs), ctypes.byref(self.A.cstruct()), mode, ptr(x), ptr(z),
+                                  ptr(out), stream_handle()))
+        return out
+
+
+SVL_MIN_ROWS = 65536     # Multigrid's default: levels >= 1 above this many rows get a stencil-values copy
 MAX_COARSE_ROWS = 8192   # the coarsest level's dense pseudo-inverse: 8192^2 doubles = 512 MB, an O(m^3) host pinv
 
 
@@ -100,11 +178,13 @@ class Multigrid:
     cycles   V-cycles per solve (x0 = 0); coarsest: stop coarsening at n <= coarsest
     sell     SELL-64 copies of the operators / transfers and the dense coarse kernel (False: CSR throughout)
     fine_sell  also a SELL copy of level 0's operator (the standalone solve's fine level)
+    svl_min_rows  levels >= 1 with more rows get a stencil-values copy (StencilValues; None: never) -- used where the
+             grouped small-level kernel is not (mpbp_set_mg_group_rows)
     """
 
     def __init__(self, A: DeviceCSR, n: int, fields=FIELDS_PRESSURE, pre: int = 2, post: int = 2, cycles: int = 1,
                  ratio: float = 4.0, coarsest: int = 8, diag: torch.Tensor | None = None, sell: bool = True,
-                 fine_sell: bool = True):
+                 fine_sell: bool = True, svl_min_rows: int | None | str = "default"):
         nf = len(fields)
         if A.shape != (nf * n * n, nf * n * n):
             raise ValueError(f"operator {A.shape} is not {nf} fields of a {n} x {n} grid")
@@ -147,6 +227,12 @@ class Multigrid:
         # (fine_sell=False: level 0's operator is the caller's own -- the Schur apply's matrix-free F / Gt_G)
         self.sells = [[sell_copy(M) if sell and (l > 0 or fine_sell or grp is not self.ops) else None
                        for l, M in enumerate(grp)] for grp in (self.ops, self.R, self.P)]
+        # stencil-values copies of the large coarse levels (8 B per entry instead of 12 B; same bits)
+        if svl_min_rows == "default":
+            svl_min_rows = SVL_MIN_ROWS
+        self.svls = [StencilValues.build(M, nf, self.sizes[l])
+                     if (l > 0 and svl_min_rows is not None and M.shape[0] > svl_min_rows) else None
+                     for l, M in enumerate(self.ops)]
         f64 = dict(dtype=torch.float64, device=dev)
         self.work = [[torch.zeros(M.shape[0], **f64) for _ in range(5)] for M in self.ops]
         self._levels = (_lib.MgLevel * len(self.ops))()
@@ -166,6 +252,8 @@ class Multigrid:
             for name, grp in zip(("A_sell", "R_sell", "P_sell"), self.sells):
                 S = grp[l] if l < len(grp) else None
                 setattr(L, name, S.cstruct() if S is not None else _lib.Sell(0, 0, 0, 0, None, None, None, None))
+            if self.svls[l] is not None:
+                L.A_svl = ctypes.pointer(self.svls[l].cstruct())
         self._mg = _lib.Mg(len(self.ops), cycles, ctypes.cast(self._levels, ctypes.POINTER(_lib.MgLevel)),
                            self.coarse_inv.cstruct(), self.coarse_inv.blocks.cstruct(),
                            self.coarse_dense.data_ptr() if self.coarse_dense is not None else None)

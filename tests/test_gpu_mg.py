@@ -107,9 +107,49 @@ def group_rows(request):
     check(lib().mpbp_set_mg_group_rows(65536))
 
 
+@pytest.fixture(params=[False, True], ids=["rowlayouts", "svl"])
+def svl_all(request, monkeypatch):
+    """Every coarse level with a stencil-values copy (mg.SVL_MIN_ROWS = 0), or the default (none at these sizes)."""
+    from mp_block_preconditioners_amd import mg
+    if request.param:
+        monkeypatch.setattr(mg, "SVL_MIN_ROWS", 0)
+    return request.param
+
+
+@pytest.mark.parametrize("n", [16, 64])
+def test_stencil_values_spmv_bit_exact(n):
+    """The stencil-values layout of every coarse Galerkin level (F: 4 fields, 40 / 46 entries per row; Gt_G: 21 / 25)
+    against the oracle's sequential CSR sums, every mode; interior rows from the layout, edge rows from the CSR."""
+    mp = _mp()
+    from oracle import csr_oracle as co
+    from mp_block_preconditioners_amd.mg import StencilValues
+    _, (A, F, D, G), S = _system(n)
+    GtG, _ = mp.MultiphaseBlockPreconditioner.commutator_products(F, D, G)
+    rng = np.random.default_rng(7 + n)
+    built = 0
+    for M, fields in ((F, mp.FIELDS_VELOCITY), (GtG, mp.FIELDS_PRESSURE)):
+        mg = mp.Multigrid(M, n, fields, svl_min_rows=None)
+        for l in range(1, mg.nlevels):
+            V = StencilValues.build(mg.ops[l], len(fields), mg.sizes[l])
+            if mg.sizes[l] < 16 and V is None:   # (too small for the stencil's reach: the SELL / CSR forms serve it)
+                continue
+            assert V is not None, (len(fields), mg.sizes[l])
+            built += 1
+            assert V.edge_rows.numel() == len(fields) * (mg.sizes[l] ** 2 - (mg.sizes[l] - 2 * V.reach) ** 2)
+            Mh = mg.ops[l].to_scipy()
+            x = rng.standard_normal(Mh.shape[1])
+            z = rng.standard_normal(Mh.shape[0])
+            for mode in (0, 1, 2):
+                got = V.matvec(_cuda(x), mode=mode, z=_cuda(z))
+                assert np.array_equal(_bits(got), _bits(co.spmv(Mh, x, z, mode=mode))), (l, mode)
+    assert built >= 2
+    # not of the form: a non-uniform operator is refused
+    assert StencilValues.build(A, 5, n) is None
+
+
 @pytest.mark.parametrize("sell", [True, False], ids=["sell", "csr"])
 @pytest.mark.parametrize("n,cycles,pre,post", [(16, 1, 2, 2), (32, 2, 2, 2), (64, 1, 1, 3), (64, 3, 2, 1)])
-def test_mg_solve_bit_exact(n, cycles, pre, post, sell, group_rows):
+def test_mg_solve_bit_exact(n, cycles, pre, post, sell, group_rows, svl_all):
     """V-cycles vs the oracle: with the SELL-64 copies of every level and the dense coarse kernel (default), and
     with the CSR forms throughout; the small levels and transfers on the grouped CSR kernel (several lanes per row,
     the row's sum in order) or on the row kernels."""
@@ -172,7 +212,7 @@ def _oracle_mg_apply(S, pc, v):
 @pytest.mark.parametrize("n", [16, 64])
 @pytest.mark.parametrize("pre", [2, 3, 1])
 @pytest.mark.parametrize("layout,f_mode,pg_mode", [("sell", "auto", "auto"), ("csr", "assembled", "assembled")])
-def test_schur_apply_mg_bit_exact(n, layout, f_mode, pg_mode, pre, group_rows):
+def test_schur_apply_mg_bit_exact(n, layout, f_mode, pg_mode, pre, group_rows, svl_all):
     """The Schur apply with multigrid inner solves vs the oracle; with matrix-free level-0 operators the first
     pre-smoothing sweep stages its x0 itself (no init launch) -- pre = 2, 3 take that path, pre = 1 the init."""
     mp = _mp()
