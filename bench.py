@@ -504,9 +504,9 @@ def spmv_bench(A, gen, reps=20, replays=10, warm_replays=5):
 def mg_apply_bench(F, D, G, steps, warmup, gen, reps=20):
     """The apply with one multigrid V-cycle per inner inverse (mg:1 / mg:1: the configuration that converges FGMRES in
     solve_level, solve.py:266 / 274's pointer), hipGraph-replayed as the headline apply, and the roofline of its
-    dominant kernel family: the level-1 F Galerkin operator's Chebyshev sweep on its SELL-64 copy (k_sell_rows<EpiCheb>,
-    8 launches per apply at 1024^2), HIP events around each of `reps` launches of that kernel on the level's own
-    buffers."""
+    dominant kernel family: the level-1 F Galerkin operator's Chebyshev sweep (8 launches per apply at 1024^2) on the
+    layout the apply uses (stencil values, k_svl<EpiCheb>; else SELL-64), HIP events around each of `reps` launches
+    of that kernel on the level's own buffers."""
     import ctypes
     import torch
     import mp_block_preconditioners_amd as mp
@@ -528,7 +528,7 @@ def mg_apply_bench(F, D, G, steps, warmup, gen, reps=20):
     dt = (time.perf_counter() - t0) / steps
     del g
     mg = pc.mg_F
-    S, M1, w, dg = mg.sells[0][1], mg.ops[1], mg.work[1], mg.diags[1]
+    S, M1, w, dg, V = mg.sells[0][1], mg.ops[1], mg.work[1], mg.diags[1], mg.svls[1]
     c1, c2 = (ctypes.c_double * 2)(), (ctypes.c_double * 2)()
     check(lib().mpbp_cheb_coeffs(mg.bounds[1][0], mg.bounds[1][1], 2, c1, c2))
     x, xo, d, b = w[0], w[1], w[3], w[4]
@@ -536,8 +536,12 @@ def mg_apply_bench(F, D, G, steps, warmup, gen, reps=20):
     b.normal_(generator=gen)
     d.zero_()
     def sweep():
-        check(lib().mpbp_sell_cheb_step(ctypes.byref(S.cstruct()), ptr(x), ptr(b), ptr(dg), c1[1], c2[1], ptr(d),
-                                        None, ptr(xo), stream_handle()))
+        if V is not None:
+            check(lib().mpbp_svl_cheb_step(ctypes.byref(V.cstruct()), ctypes.byref(M1.cstruct()), ptr(x), ptr(b),
+                                           ptr(dg), c1[1], c2[1], ptr(d), None, ptr(xo), stream_handle()))
+        else:
+            check(lib().mpbp_sell_cheb_step(ctypes.byref(S.cstruct()), ptr(x), ptr(b), ptr(dg), c1[1], c2[1], ptr(d),
+                                            None, ptr(xo), stream_handle()))
     for _ in range(3):
         sweep()
     pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
@@ -548,15 +552,21 @@ def mg_apply_bench(F, D, G, steps, warmup, gen, reps=20):
     torch.cuda.synchronize()
     us = sum(a.elapsed_time(e) for a, e in pairs) * 1e3 / reps
     rows = M1.shape[0]
-    # 12 B per entry (value + column) + 1 B row length per row + 16 B per slice descriptor; per row x (gathered,
-    # counted once), b, diag, d read, d written, x_out (8 B each)
-    nbytes = M1.nnz * 12 + rows * (1 + 6 * 8) + S.nslices * 16
+    # per row x (gathered, counted once), b, diag, d read, d written, x_out (8 B each); the matrix: stencil values 8 B
+    # per entry (edge rows: their CSR entries, 12 B, + 4 B row_ptr), or SELL 12 B per entry + 1 B row length + 16 B
+    # per slice descriptor
+    if V is not None:
+        ne, K = int(V.edge_rows.numel()), V.slots
+        nbytes = (rows - ne) * K * 8 + ne * (K * 12 + 4) + rows * 6 * 8
+        kname = f"k_svl<EpiCheb> (level-1 F Galerkin operator, {rows} rows x {K} entries, stencil values)"
+    else:
+        nbytes = M1.nnz * 12 + rows * (1 + 6 * 8) + S.nslices * 16
+        kname = f"k_sell_rows<EpiCheb> (level-1 F Galerkin operator, {rows} rows x {M1.nnz / rows:.0f} entries, SELL-64)"
     return {"value": 1.0 / dt, "unit": "applies/s", "ms_per_step": dt * 1e3, "inner_F": "mg:1", "inner_P": "mg:1",
             "setup_seconds": setup_s, "launch": "hipgraph",
             "levels_F": mg.sizes, "levels_P": pc.mg_P.sizes,
             "roofline": {"bound": "hbm", "achieved": nbytes / us / 1e3, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": nbytes / us / 1e3 / HBM_PEAK_GBS, "kernel": "k_sell_rows<EpiCheb> (level-1 F Galerkin "
-                         f"operator, {rows} rows x {M1.nnz / rows:.0f} entries, SELL-64)", "bytes_per_launch": nbytes,
+                         "frac": nbytes / us / 1e3 / HBM_PEAK_GBS, "kernel": kname, "bytes_per_launch": nbytes,
                          "avg_launch_us": us, "launches_per_apply": 8,
                          "timing": f"mean of HIP event pairs around each of {reps} launches on the level's buffers"}}
 
@@ -565,14 +575,23 @@ SOLVE_CASES = (   # (n, eta_n, eta_s, preconditioners): BASELINE configs[1] / co
     (256, 100.0, 1.0, ("none", "chebyshev:4", "mg:1")),
     (256, 1e4, 1.0, ("none", "chebyshev:4", "mg:1", "mg:2/mg:1")),
     (1024, 100.0, 1.0, ("chebyshev:4", "mg:1", "mg:2/mg:1")),
-    (1024, 1e4, 1.0, ("chebyshev:4", "mg:1", "mg:2/mg:1")),
+    (1024, 1e4, 1.0, ("chebyshev:4", "mg:1", "mg:1@3,3", "mg:2/mg:1")),
 )
 
 
 def inner_pair(mp, name):
-    """'kind:k' (both inner inverses) or 'kindF:kF/kindP:kP' -> (InnerSolver for F, InnerSolver for Gt_G)."""
+    """'kind:k' (both inner inverses) or 'kindF:kF/kindP:kP' -> (InnerSolver for F, InnerSolver for Gt_G); a suffix
+    '@pre,post' sets the multigrid smoothing sweeps (default V(2,2))."""
+    name, _, smooth = name.partition("@")
+    mgkw = {}
+    if smooth:
+        pre, _, post = smooth.partition(",")
+        mgkw = dict(pre=int(pre), post=int(post or pre))
     f, _, p = name.partition("/")
-    mk = lambda s: mp.InnerSolver(s.partition(":")[0], int(s.partition(":")[2] or 4))  # noqa: E731
+
+    def mk(s):
+        kind, _, k = s.partition(":")
+        return mp.InnerSolver(kind, int(k or 4), **(mgkw if kind == "mg" else {}))
     return mk(f), mk(p or f)
 
 
@@ -628,7 +647,8 @@ def solve_level(args, cases=SOLVE_CASES, tol=1e-8, maxiter=150, reps=10):
         torch.cuda.empty_cache()
     return {"tol": tol, "maxiter": maxiter, "problem": "manufactured solution of solve.py:52-80, x0 = 0",
             "inner": "chebyshev:K = K Chebyshev-Jacobi sweeps; mg:K = K multigrid V-cycles (V(2,2), Chebyshev "
-                     "smoothing, Galerkin levels down to 8^2); 'F/P' names the two inner inverses separately",
+                     "smoothing, Galerkin levels down to 16^2, its dense inverse there; '@a,b': V(a,b)); 'F/P' names "
+                     "the two inner inverses separately",
             "runs": out}
 
 

@@ -303,6 +303,10 @@ int mpbp_q13_build(const mpbp_csr* Q, int32_t n, double* vals, void* stream);
  * CSR SpMV's result bit for bit. */
 int mpbp_svl_spmv(const mpbp_svl* V, const mpbp_csr* A, int32_t mode, const double* x, const double* z, double* y,
                   void* stream);
+/* One Chebyshev-Jacobi sweep (as mpbp_cheb_step) through the stencil-values layout: the multigrid's large-level
+ * smoothing sweep, bit-identical to the CSR form. */
+int mpbp_svl_cheb_step(const mpbp_svl* V, const mpbp_csr* A, const double* x_in, const double* b, const double* diag,
+                       double c1, double c2, double* d, const double* sub, double* x_out, void* stream);
 int mpbp_q13_spmv(int32_t n, const double* vals, int32_t mode, const double* x, const double* z, double* y,
                   void* stream);
 

@@ -3625,6 +3625,15 @@ int mpbp_svl_spmv(const mpbp_svl* V, const mpbp_csr* A, int32_t mode, const doub
     return svl_spmv(V, A, mode, x, z, y, as_stream(stream));
 }
 
+int mpbp_svl_cheb_step(const mpbp_svl* V, const mpbp_csr* A, const double* x_in, const double* b, const double* diag,
+                       double c1, double c2, double* d, const double* sub, double* x_out, void* stream) {
+    int rc = check_csr(A);
+    if (!rc) rc = check_svl(V, A);
+    if (rc) return rc;
+    if (!x_in || !b || !diag || !d || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "svl_cheb_step: bad vectors");
+    return svl_cheb(V, A, x_in, b, diag, c1, c2, d, sub, x_out, as_stream(stream), 1, false);
+}
+
 int mpbp_q13_build(const mpbp_csr* Q, int32_t n, double* vals, void* stream) {
     int rc = check_csr(Q);
     if (rc) return rc;
@@ -3941,9 +3950,11 @@ int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, 
         other = x;
         x = out1;
         s = 2;
-    } else if (zero && K >= 2 && op.bd.empty && o.grp) {
+    } else if (zero && K >= 2 && op.bd.empty && o.grp && o.csr->ncols == nrows) {
         // grouped small level: the first sweep gathers x0 = c2[0] b / diag itself (no init launch, same bits; on the
-        // large stencil-values levels the division per gathered entry costs more than the init launch: 110 vs 97 us)
+        // large stencil-values levels the division per gathered entry costs more than the init launch: 110 vs 97 us).
+        // Not on a row-partitioned level: its columns reach ghost rows, whose x0 only the exchange after an init
+        // pass provides (b and diag hold the owned rows alone)
         double* out1 = K == 2 ? (dst ? dst : other) : other;
         const int rc = grp_cheb_first(o.csr, b, diag, c2[0], c1[1], c2[1], d, K == 2 ? sub : nullptr, out1, st,
                                       K == 2 ? 0 : 1);

@@ -142,6 +142,23 @@ def test_stencil_values_spmv_bit_exact(n):
             for mode in (0, 1, 2):
                 got = V.matvec(_cuda(x), mode=mode, z=_cuda(z))
                 assert np.array_equal(_bits(got), _bits(co.spmv(Mh, x, z, mode=mode))), (l, mode)
+            # the smoothing sweep (mpbp_svl_cheb_step) == the CSR sweep, every output
+            import ctypes
+            from mp_block_preconditioners_amd._lib import check, lib, ptr, stream_handle
+            M, dg = mg.ops[l], mg.diags[l]
+            xd, bd = _cuda(x), _cuda(z)
+            outs = []
+            for fn in ("svl", "csr"):
+                d = _cuda(np.linspace(-1.0, 1.0, M.shape[0]))
+                xo = torch.empty_like(d)
+                if fn == "svl":
+                    check(lib().mpbp_svl_cheb_step(ctypes.byref(V.cstruct()), ctypes.byref(M.cstruct()), ptr(xd),
+                                                   ptr(bd), ptr(dg), 0.3, 0.7, ptr(d), None, ptr(xo), stream_handle()))
+                else:
+                    check(lib().mpbp_cheb_step(ctypes.byref(M.cstruct()), ctypes.byref(M.blocks.cstruct()), ptr(xd),
+                                               ptr(bd), ptr(dg), 0.3, 0.7, ptr(d), None, ptr(xo), stream_handle()))
+                outs.append((_bits(d), _bits(xo)))
+            assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
     assert built >= 2
     # not of the form: a non-uniform operator is refused
     assert StencilValues.build(A, 5, n) is None
