@@ -598,8 +598,9 @@ def inner_pair(mp, name):
 def solve_level(args, cases=SOLVE_CASES, tol=1e-8, maxiter=150, reps=10):
     """What the applies/s headline buys: FGMRES (tol 1e-8, maxiter 150, x0 = 0, solve.py:285) on the reference's
     manufactured problem (solve.py:52-80) with the approximate Schur preconditioner and different inner solves:
-    iterations, time to tolerance (the fgmres call; preconditioner set-up reported apart), the velocity error, and
-    the preconditioner's own apply time (a hipGraph replayed `reps` times)."""
+    iterations, time to tolerance (the fgmres call, replaying the apply's hipGraph; preconditioner set-up and the
+    graph capture reported apart), the velocity error, and the preconditioner's own apply time (the graph replayed
+    `reps` times)."""
     import numpy as np
     import torch
     import mp_block_preconditioners_amd as mp
@@ -619,10 +620,14 @@ def solve_level(args, cases=SOLVE_CASES, tol=1e-8, maxiter=150, reps=10):
                 M = mp.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP)
             torch.cuda.synchronize()
             setup = time.perf_counter() - t0
+            capture_s = None
             if M is not None:
                 v = torch.randn(M.shape[0], dtype=torch.float64, device="cuda")
                 o = torch.empty_like(v)
+                t0 = time.perf_counter()
                 g = M.capture(v, o)
+                torch.cuda.synchronize()
+                capture_s = time.perf_counter() - t0
                 g.replay()
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
@@ -630,6 +635,7 @@ def solve_level(args, cases=SOLVE_CASES, tol=1e-8, maxiter=150, reps=10):
                     g.replay()
                 torch.cuda.synchronize()
                 apply_ms = (time.perf_counter() - t0) / reps * 1e3
+                M._fgmres_graph = (v, o, g)   # the solve replays this capture (fgmres reuses a graph kept on M)
                 del g, v, o
             hist = []
             t0 = time.perf_counter()
@@ -639,7 +645,8 @@ def solve_level(args, cases=SOLVE_CASES, tol=1e-8, maxiter=150, reps=10):
             res = float(torch.linalg.vector_norm(bd - A.matvec(x))) / nb
             err = float(np.max(np.abs(x.cpu().numpy()[: 4 * n * n] - u[: 4 * n * n])))
             out.append({"n": n, "eta_n": eta_n, "eta_s": eta_s, "preconditioner": name, "iterations": len(hist) - 1,
-                        "converged": info == 0, "seconds": el, "setup_seconds": setup, "apply_ms": apply_ms,
+                        "converged": info == 0, "seconds": el, "setup_seconds": setup, "capture_seconds": capture_s,
+                        "apply_ms": apply_ms,
                         "true_rel_residual": res, "velocity_max_error": err})
             del M, x
             torch.cuda.empty_cache()

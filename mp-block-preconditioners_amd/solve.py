@@ -482,9 +482,19 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
     m = int(restrt) if restrt is not None else maxiter
     if capture_M and M is not None and hasattr(M, "capture") and b.is_cuda:
         try:
-            m_in = torch.zeros(M.shape[0], dtype=torch.float64, device=b.device)
-            m_out = torch.empty_like(m_in)
-            m_graph = M.capture(m_in, m_out)
+            # the captured apply is kept on M and reused by later solves with the same M (capturing and instantiating
+            # a multigrid apply's hundreds of launches costs tens of ms)
+            cached = getattr(M, "_fgmres_graph", None)
+            if cached is not None and cached[0].device == b.device:
+                m_in, m_out, m_graph = cached
+            else:
+                m_in = torch.zeros(M.shape[0], dtype=torch.float64, device=b.device)
+                m_out = torch.empty_like(m_in)
+                m_graph = M.capture(m_in, m_out)
+                try:
+                    M._fgmres_graph = (m_in, m_out, m_graph)
+                except AttributeError:
+                    pass
 
             def Mop(x, out=None, _g=m_graph, _i=m_in, _o=m_out):   # noqa: F811
                 _i.copy_(x)

@@ -63,6 +63,20 @@ def test_rdot_split_over_pieces_is_the_same():
     assert torch.equal(acc, whole)
 
 
+@pytest.mark.parametrize("n,where", [(5_242_881, -1), (5_242_880, 0), (1_000_003, 777_777), (255, 254), (8 * 256 * 1024 + 5, -3)])
+def test_absmax_large_vectors(n, where):
+    """mpbp_absmax over FGMRES-sized vectors (unrolled grid-stride loads, per-workgroup atomics): the exact max |x|,
+    wherever it sits (the unrolled body, the remainder loop, a negative entry)."""
+    check, lib, ptr, sh = _lib()
+    rng = np.random.default_rng(n)
+    w = rng.standard_normal(n)
+    w[where] = -1e3 * (1 + rng.random())
+    dw = torch.from_numpy(w).cuda()
+    am = torch.empty(1, dtype=torch.float64, device="cuda")
+    check(lib().mpbp_absmax(ptr(dw), n, ptr(am), sh()))
+    assert float(am) == float(np.max(np.abs(w)))
+
+
 def test_rdot_nan_and_zero():
     check, lib, ptr, sh = _lib()
     w = torch.tensor([1.0, float("nan"), 2.0], dtype=torch.float64, device="cuda")

@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--maxiter", type=int, default=150)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--solves", type=int, default=1, help="solves per combo (the last one reported; all in solve_times)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -67,18 +68,21 @@ def main():
                 torch.cuda.synchronize()
                 apply_ms = (time.perf_counter() - t0) / args.reps * 1e3
                 del g
-                hist = []
-                t0 = time.perf_counter()
-                x, info = mp.fgmres(A, bd, M=M, tol=args.tol, maxiter=args.maxiter, residuals=hist)
-                torch.cuda.synchronize()
-                el = time.perf_counter() - t0
+                times = []
+                for _ in range(args.solves):   # later solves reuse the captured apply (fgmres keeps it on M)
+                    hist = []
+                    t0 = time.perf_counter()
+                    x, info = mp.fgmres(A, bd, M=M, tol=args.tol, maxiter=args.maxiter, residuals=hist)
+                    torch.cuda.synchronize()
+                    times.append(time.perf_counter() - t0)
+                el = times[-1]
                 res = float(torch.linalg.vector_norm(bd - A.matvec(x))) / nb
                 err = float(np.max(np.abs(x.cpu().numpy()[: 4 * n * n] - u[: 4 * n * n])))
                 levels = {k: (m.sizes if m is not None else None) for k, m in (("F", M.mg_F), ("P", M.mg_P))}
                 nnz = {k: ([op.nnz for op in m.ops] if m is not None else None) for k, m in (("F", M.mg_F), ("P", M.mg_P))}
                 print(json.dumps({"tag": args.tag, "coarsest": args.coarsest, "pre": args.pre, "post": args.post,
                                   "smooth_ratio": args.smooth_ratio, "n": n, "eta_n": eta_n, "combo": combo, "iterations": len(hist) - 1,
-                                  "converged": info == 0, "solve_s": el, "setup_s": setup, "apply_ms": apply_ms,
+                                  "converged": info == 0, "solve_s": el, "solve_times": times, "setup_s": setup, "apply_ms": apply_ms,
                                   "ms_per_iteration": el / max(1, len(hist) - 1) * 1e3, "true_rel_residual": res,
                                   "velocity_max_error": err, "mg_levels": levels, "mg_nnz": nnz,
                                   "residuals": [float(r) for r in hist[:: max(1, len(hist) // 10)]]}), flush=True)
