@@ -80,54 +80,10 @@ class StencilValues:
 
     @classmethod
     def build(cls, A: DeviceCSR, nf: int, m: int) -> "StencilValues | None":
-        N = nf * m * m
-        if A.shape != (N, N) or A.nnz == 0 or m < 4:
+        if A.shape != (nf * m * m, nf * m * m) or A.nnz == 0:
             return None
-        dev = A.device
-        rp = A.row_ptr.long()
-        lens = rp[1:] - rp[:-1]
-        K = int(lens[0])
-        if K < 1 or nf * K > 256 or not bool(torch.all(lens == K)):
-            return None
-        e = torch.arange(A.nnz, device=dev)
-        rows, pos = e // K, e % K
-        del e
-        mm = m * m
-        ci = A.col_idx.long()
-        f, cell = rows // mm, rows % mm
-        r, c = cell // m, cell % m
-        fc, cc = ci // mm, ci % mm
-        dr = (cc // m - r + m // 2) % m - m // 2
-        dc = (cc % m - c + m // 2) % m - m // 2
-        del cell, cc
-        R = int(torch.maximum(dr.abs().max(), dc.abs().max()))
-        if m % 2 or m < 2 * R + 4 or K * N > 2 ** 31 - 1:
-            return None
-        w = 2 * R + 1
-        table = torch.full((nf, nf, w, w), -1, dtype=torch.long, device=dev)
-        delta = torch.empty(nf, K, dtype=torch.int32, device=dev)
-        for f0 in range(nf):
-            base = f0 * mm + (m // 2) * m + m // 2
-            sl = slice(base * K, base * K + K)
-            table[f0, fc[sl], dr[sl] + R, dc[sl] + R] = torch.arange(K, device=dev)
-            delta[f0] = (ci[sl] - base).to(torch.int32)
-        slot = table[f, fc, dr + R, dc + R]
-        del fc, dr, dc, table
-        if bool((slot < 0).any()):
-            return None
-        seen = torch.bincount(rows * K + slot, minlength=N * K)
-        if not bool(torch.all(seen == 1)):
-            return None
-        del seen
-        if bool(((slot != pos) & (r >= R) & (r < m - R) & (c >= R) & (c < m - R)).any()):
-            return None
-        R += R & 1   # the kernel's interior cells go in pairs from an even column: an odd reach widens the edge band
-        interior = (r >= R) & (r < m - R) & (c >= R) & (c < m - R)
-        vals = torch.empty(K * N, dtype=torch.float64, device=dev)
-        vals[slot * N + rows] = A.val
-        row_int = interior.view(N, K)[:, 0]
-        edge = torch.nonzero(~row_int).reshape(-1).to(torch.int32)
-        return cls(A, nf, m, R, K, delta.reshape(-1).contiguous(), vals, edge)
+        arrays = stencil_values_arrays(A.row_ptr, A.col_idx, A.val, nf, m)
+        return None if arrays is None else cls(A, nf, m, *arrays)
 
     def matvec(self, x: torch.Tensor, out: torch.Tensor | None = None, mode=_lib.SPMV_STORE,
                z: torch.Tensor | None = None) -> torch.Tensor:
@@ -136,6 +92,59 @@ class StencilValues:
         check(lib().mpbp_svl_spmv(ctypes.byref(self._cs), ctypes.byref(self.A.cstruct()), mode, ptr(x), ptr(z),
                                   ptr(out), stream_handle()))
         return out
+
+
+def stencil_values_arrays(row_ptr: torch.Tensor, col_idx: torch.Tensor, val: torch.Tensor, nf: int, m: int):
+    """(reach, K, delta[nf * K], vals[K * N] slot-major, edge_rows) of StencilValues from CSR arrays (any torch device),
+    or None when the operator is not translation-invariant in that sense (see StencilValues)."""
+    N = nf * m * m
+    if row_ptr.numel() != N + 1 or m < 4:
+        return None
+    dev = row_ptr.device
+    rp = row_ptr.long()
+    lens = rp[1:] - rp[:-1]
+    K = int(lens[0])
+    if K < 1 or nf * K > 256 or not bool(torch.all(lens == K)):
+        return None
+    e = torch.arange(col_idx.numel(), device=dev)
+    rows, pos = e // K, e % K
+    del e
+    mm = m * m
+    ci = col_idx.long()
+    f, cell = rows // mm, rows % mm
+    r, c = cell // m, cell % m
+    fc, cc = ci // mm, ci % mm
+    dr = (cc // m - r + m // 2) % m - m // 2
+    dc = (cc % m - c + m // 2) % m - m // 2
+    del cell, cc
+    R = int(torch.maximum(dr.abs().max(), dc.abs().max()))
+    if m % 2 or m < 2 * R + 4 or K * N > 2 ** 31 - 1:
+        return None
+    w = 2 * R + 1
+    table = torch.full((nf, nf, w, w), -1, dtype=torch.long, device=dev)
+    delta = torch.empty(nf, K, dtype=torch.int32, device=dev)
+    for f0 in range(nf):
+        base = f0 * mm + (m // 2) * m + m // 2
+        sl = slice(base * K, base * K + K)
+        table[f0, fc[sl], dr[sl] + R, dc[sl] + R] = torch.arange(K, device=dev)
+        delta[f0] = (ci[sl] - base).to(torch.int32)
+    slot = table[f, fc, dr + R, dc + R]
+    del fc, dr, dc, table
+    if bool((slot < 0).any()):
+        return None
+    seen = torch.bincount(rows * K + slot, minlength=N * K)
+    if not bool(torch.all(seen == 1)):
+        return None
+    del seen
+    if bool(((slot != pos) & (r >= R) & (r < m - R) & (c >= R) & (c < m - R)).any()):
+        return None
+    R += R & 1   # the kernel's interior cells go in pairs from an even column: an odd reach widens the edge band
+    interior = (r >= R) & (r < m - R) & (c >= R) & (c < m - R)
+    vals = torch.empty(K * N, dtype=torch.float64, device=dev)
+    vals[slot * N + rows] = val
+    row_int = interior.view(N, K)[:, 0]
+    edge = torch.nonzero(~row_int).reshape(-1).to(torch.int32)
+    return R, K, delta.reshape(-1).contiguous(), vals, edge
 
 
 SVL_MIN_ROWS = 65536     # Multigrid's default: levels >= 1 above this many rows get a stencil-values copy
