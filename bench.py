@@ -453,7 +453,21 @@ def spmv_bench(A, gen, reps=20, replays=10, warm_replays=5):
     res = {"nnz": A.nnz, "timing": f"mean of HIP event pairs around each of {reps} launches (after "
                                    f"{replays} graph replays of {reps} back-to-back launches, `*_us_graph`)"}
     AS = A.to_sell()
-    csr_bytes = A.nnz * 12 + (A.shape[0] + 1) * 4 + (A.shape[0] + A.shape[1]) * 8 + A.blocks.count * 8
+    # CSR algorithmic bytes: 12 B per entry (value + column) + x and y (8 B per row / column) + the row structure the
+    # kernel reads: with the row blocks' wave table (default) 32 B per block, and row_ptr (4 B per row) + the block's
+    # row range (8 B) only for waves the table does not flag uniform; without it row_ptr for every row
+    tb = A.blocks.table
+    if tb is not None:
+        import numpy as np
+        t = tb.cpu().numpy().reshape(-1, 8).astype(np.int64)
+        nonuni = 0
+        for w in range(4):
+            rows_w = np.clip(t[:, 1] - (t[:, 0] + 64 * w), 0, 64)
+            nonuni += int(rows_w[((t[:, 7] >> (8 * w)) & 255) == 0].sum())
+        struct_bytes = A.blocks.count * 32 + (nonuni * 4 + A.blocks.count * 8 if nonuni else 0)
+    else:
+        struct_bytes = (A.shape[0] + 1) * 4 + A.blocks.count * 8
+    csr_bytes = A.nnz * 12 + (A.shape[0] + A.shape[1]) * 8 + struct_bytes
     for name, M, nbytes in (
             ("csr", A, csr_bytes),              # per-wave chunked kernel (k_csr_wave)
             ("sell", AS, A.nnz * 12 + A.shape[0] + (A.shape[0] + A.shape[1]) * 8 + AS.nslices * 16)):

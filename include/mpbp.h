@@ -86,6 +86,13 @@ typedef struct mpbp_csr {
 typedef struct mpbp_rowblocks {
     const int32_t* pairs;
     int32_t count;
+    int32_t reserved;
+    /* optional wave table (NULL: the kernels read row_ptr): per block 8 int32 {start row, end row, row_ptr[min(start +
+     * 64 w, end)] for w = 0..4, uniform flags} -- byte w of the flags is LEN when the block's wave w covers 64 rows of
+     * LEN in {8, 10, 12} entries each from an even entry offset, else 0.  The CSR SpMV's waves then start their matrix
+     * loads from one scalar load of the table, with no row_ptr reads on uniform waves.  Built on the host from the same
+     * row_ptr as `pairs` (csr.RowBlockList); a plan belongs to its matrix's structure. */
+    const int32_t* table;
 } mpbp_rowblocks;
 
 #define MPBP_BLOCK_ROWS 256
@@ -419,6 +426,8 @@ int mpbp_set_pg_direct(int32_t on);
 int mpbp_set_mg_group_rows(int32_t rows);
 /* 1 (default): multigrid levels with a stencil-values copy (mpbp_mg_level.A_svl) use it; 0: their SELL / CSR form. */
 int mpbp_set_mg_svl(int32_t on);
+/* 1 (default): the CSR SpMV's waves start from mpbp_rowblocks.table when present; 0: from row_ptr (same bits). */
+int mpbp_set_csr_table(int32_t on);
 
 /* ---- geometric multigrid inner solves (the reference's pointer: solve.py:266, 274) ------------------ */
 /* P (which = MPBP_MG_P, fine x coarse) or R = P^T (MPBP_MG_R) of an n x n periodic grid (n even, >= 4) coarsened by 2,

@@ -33,7 +33,7 @@ class Csr(Structure):
 
 
 class RowBlocks(Structure):
-    _fields_ = [("pairs", c_void_p), ("count", c_int32)]
+    _fields_ = [("pairs", c_void_p), ("count", c_int32), ("reserved", c_int32), ("table", c_void_p)]
 
 
 class Sell(Structure):
@@ -161,6 +161,7 @@ _SIGNATURES = {
     "mpbp_set_pg_direct": ([c_int32], c_int),
     "mpbp_set_mg_group_rows": ([c_int32], c_int),
     "mpbp_set_mg_svl": ([c_int32], c_int),
+    "mpbp_set_csr_table": ([c_int32], c_int),
     "mpbp_q13_build": ([POINTER(Csr), c_int32, c_void_p, c_void_p], c_int),
     "mpbp_svl_spmv": ([POINTER(Svl), POINTER(Csr), c_int32, _P, _P, _P, _P], c_int),
     "mpbp_svl_cheb_step": ([POINTER(Svl), POINTER(Csr), _P, _P, _P, c_double, c_double, _P, _P, _P, _P], c_int),

@@ -96,7 +96,8 @@ class DeviceCSR:
             gid = np.minimum(starts // gsize, g - 1)
             order = np.lexsort((gid, starts - gid * gsize))   # by position within the field, then field
             pairs = pairs.reshape(-1, 2)[order].reshape(-1)
-        return RowBlockList(torch.from_numpy(np.ascontiguousarray(pairs)).to(self.device))
+        pairs = np.ascontiguousarray(pairs)
+        return RowBlockList(torch.from_numpy(pairs).to(self.device), rp, pairs)
 
     @property
     def blocks(self):
@@ -234,13 +235,47 @@ class DeviceSELL:
 
 
 class RowBlockList:
-    def __init__(self, pairs: torch.Tensor):
+    """Row blocks of a CSR matrix in HBM (mpbp_rowblocks): the (start, end) pairs and, when the host row_ptr is given,
+    the wave table (wave_table) the SpMV kernels start from."""
+
+    def __init__(self, pairs: torch.Tensor, row_ptr_host: np.ndarray | None = None, pairs_host: np.ndarray | None = None):
         self.pairs = pairs
         self.count = pairs.numel() // 2
-        self._cs = _lib.RowBlocks(pairs.data_ptr() if self.count else None, self.count)
+        self.table = None
+        if row_ptr_host is not None and self.count:
+            ph = pairs_host if pairs_host is not None else pairs.cpu().numpy()
+            self.table = torch.from_numpy(wave_table(row_ptr_host, ph.reshape(-1, 2))).to(pairs.device)
+        self._cs = _lib.RowBlocks(pairs.data_ptr() if self.count else None, self.count, 0,
+                                  self.table.data_ptr() if self.table is not None else None)
 
     def cstruct(self):
         return self._cs
+
+
+def wave_table(rp: np.ndarray, pairs: np.ndarray) -> np.ndarray:
+    """Per row block 8 int32 (include/mpbp.h, mpbp_rowblocks.table): start row, end row, row_ptr at the starts of its
+    four 64-row waves and at its end, and the waves' uniform-length flags (byte w = LEN in {8, 10, 12} when wave w's 64
+    rows all hold LEN entries from an even offset)."""
+    rp = np.asarray(rp, dtype=np.int64)
+    ra, rb = pairs[:, 0].astype(np.int64), pairs[:, 1].astype(np.int64)
+    t = np.zeros((pairs.shape[0], 8), dtype=np.int64)
+    t[:, 0], t[:, 1] = ra, rb
+    for w in range(5):
+        t[:, 2 + w] = rp[np.minimum(ra + 64 * w, rb)]
+    lens = np.diff(rp)
+    flags = np.zeros(pairs.shape[0], dtype=np.int64)
+    for w in range(4):
+        a = ra + 64 * w
+        full = rb - a >= 64
+        idx = np.nonzero(full)[0]
+        if idx.size:
+            rows = a[idx][:, None] + np.arange(64)[None, :]
+            L = lens[rows]
+            L0 = L[:, 0]
+            ok = np.all(L == L0[:, None], axis=1) & np.isin(L0, (8, 10, 12)) & (rp[a[idx]] % 2 == 0)
+            flags[idx] |= np.where(ok, L0, 0) << (8 * w)
+    t[:, 7] = flags
+    return t.astype(np.int32).reshape(-1)
 
 
 def csr_from_row_nnz(row_nnz: torch.Tensor, shape, device):

@@ -22,6 +22,7 @@ thread_local char g_err[1024] = "";
 // grid rows per workgroup of the marching kernels; 0 (default): the count that fills one round of workgroups
 // (measured best at every size: 256^2 1 row -> 13.5k applies/s vs 7.6k at 4; 1024^2 4; 2048^2 16 -> 753 vs 727)
 int g_march_rows = 0;
+int g_csr_table = 1;      // CSR SpMV waves start from the row blocks' wave table when it has one (0: from row_ptr)
 int g_init_diag = 1;      // fused first F sweep: 1 rebuilds the staged diagonal from thn, 0 streams diag
 #ifndef MPBP_PG_ROWS
 #define MPBP_PG_ROWS 0    // rows per workgroup of the D / G / Gt_G marching kernels (0: as F)
@@ -950,12 +951,13 @@ __device__ inline void wave_lds_sync() {
 #ifndef MPBP_CSR_SPEC
 #define MPBP_CSR_SPEC 1
 #endif
-template <int LEN, bool XB, class Epi>
+// TRUST: the wave table says the wave is uniform (no row check).
+template <int LEN, bool XB, class Epi, bool TRUST = false>
 __device__ inline bool csr_wave_uniform(const Csr& A, const double* __restrict__ x, int32_t s, int lane,
                                         double2* vs, int2* cs, int32_t ks, int32_t ke, int32_t r, const Epi& epi,
                                         const typename Epi::P& pe) {
     constexpr int P = LEN / 2;   // pairs per row == 16-byte loads per lane
-    if (!MPBP_CSR_SPEC && !__all(ke - ks == LEN)) return false;
+    if (!TRUST && !MPBP_CSR_SPEC && !__all(ke - ks == LEN)) return false;
     double2 v[P];
     int2 cc[P];
 #pragma unroll
@@ -967,7 +969,7 @@ __device__ inline bool csr_wave_uniform(const Csr& A, const double* __restrict__
     // (a compiler memory barrier: the loads above may not sink below the check, which would serialise them
     // behind the row_ptr loads again; it emits no instruction and no wait)
     if (MPBP_CSR_SPEC) asm volatile("" ::: "memory");
-    if (MPBP_CSR_SPEC && !__all(ke - ks == LEN)) return false;
+    if (!TRUST && MPBP_CSR_SPEC && !__all(ke - ks == LEN)) return false;
 #pragma unroll
     for (int j = 0; j < P; ++j) {
         vs[lane + 64 * j] = v[j];
@@ -1004,17 +1006,42 @@ __device__ inline bool csr_wave_uniform(const Csr& A, const double* __restrict__
     return true;
 }
 
+// The wave table (mpbp_rowblocks.table; MPBP_CSR_TABLE=0 ignores it): a wave flagged uniform starts its matrix loads
+// right after one scalar load of its block's 32-byte table entry -- no dependent row-range load, no row_ptr reads.
+#ifndef MPBP_CSR_TABLE
+#define MPBP_CSR_TABLE 1
+#endif
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(4))) const i32x4 ci32x4;
 template <class Epi>
 __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __restrict__ x,
                                                      const int2* __restrict__ blocks, int nblocks,
-                                                     Epi epi) {
+                                                     const int32_t* __restrict__ table, Epi epi) {
     __shared__ double2 vstage[kBlock / 64][kWaveCap / 2];
 #if MPBP_CSR_TGATHER
     __shared__ int2 cstage[kBlock / 64][kWaveCap / 2];
 #endif
     const int b = xcd_swizzle(blockIdx.x, nblocks);
-    const int2 blk = blocks[b];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#if MPBP_CSR_TABLE && MPBP_CSR_TGATHER && MPBP_CSR_UNIFORM
+    if (table && A.ncols > 0 && A.ncols < (1 << 28)) {
+        const i32x4 t0 = ((ci32x4*)table)[2 * b], t1 = ((ci32x4*)table)[2 * b + 1];
+        const int32_t ra = t0.x + 64 * w;
+        if (ra >= t0.y) return;
+        const int len = (t1.w >> (8 * w)) & 255;
+        if (len) {
+            const int32_t s = w == 0 ? t0.z : w == 1 ? t0.w : w == 2 ? t1.x : t1.y;
+            const int32_t r = ra + lane;
+            const typename Epi::P pe = epi.pre(r);
+            constexpr bool XB = MPBP_CSR_XBUF != 0;
+            if (len == 12) csr_wave_uniform<12, XB, Epi, true>(A, x, s, lane, vstage[w], cstage[w], 0, 0, r, epi, pe);
+            else if (len == 10) csr_wave_uniform<10, XB, Epi, true>(A, x, s, lane, vstage[w], cstage[w], 0, 0, r, epi, pe);
+            else csr_wave_uniform<8, XB, Epi, true>(A, x, s, lane, vstage[w], cstage[w], 0, 0, r, epi, pe);
+            return;
+        }
+    }
+#endif
+    const int2 blk = blocks[b];
     const int32_t ra = __builtin_amdgcn_readfirstlane(blk.x + 64 * w);
     if (ra >= blk.y) return;   // waves are independent: no workgroup barrier below
     const int32_t rb = min(ra + 64, blk.y);
@@ -2514,7 +2541,7 @@ template <class Epi>
 int launch_rows(const mpbp_csr* A, const mpbp_rowblocks* blk, const double* x, Epi epi, hipStream_t st) {
     if (!blk || blk->count <= 0) return MPBP_OK;
     k_csr_wave<Epi><<<blk->count, kBlock, 0, st>>>(to_csr(A), x, reinterpret_cast<const int2*>(blk->pairs),
-                                                    blk->count, epi);
+                                                    blk->count, g_csr_table ? blk->table : nullptr, epi);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
@@ -2654,6 +2681,10 @@ const char* mpbp_version(void) { return "libmpbp 0.1 (gfx950)"; }
 int mpbp_set_march_rows(int32_t rows) {
     if (rows < 0 || rows > 4096) return set_error(MPBP_ERR_ARG, "march rows must be 0 (auto) or in [1, 4096]");
     g_march_rows = rows;
+    return MPBP_OK;
+}
+int mpbp_set_csr_table(int32_t on) {
+    g_csr_table = on ? 1 : 0;
     return MPBP_OK;
 }
 int mpbp_set_mg_svl(int32_t on) {

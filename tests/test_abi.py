@@ -104,3 +104,30 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "libmpbp.so"))
     with pytest.raises(_lib.MpbpError, match="no CPU fallback"):
         _lib.lib()
+
+
+def test_wave_table_flags():
+    """The row blocks' wave table (csr.wave_table, mpbp_rowblocks.table) on the host: wave entry ranges from row_ptr, and
+    the uniform flag exactly for the 64-row waves of 8 / 10 / 12 entries each from an even offset."""
+    import numpy as np
+    from mp_block_preconditioners_amd.csr import wave_table
+    rng = np.random.default_rng(5)
+    lens = rng.integers(0, 20, size=1000)
+    lens[0:64] = 12          # uniform wave, even start
+    lens[64:128] = 10
+    lens[128:192] = 7        # uniform but not 8 / 10 / 12
+    lens[256:320] = 8
+    lens[300] = 9            # broken
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    pairs = np.array([[0, 256], [256, 512], [512, 700], [700, 1000]], dtype=np.int32)
+    t = wave_table(rp, pairs).reshape(-1, 8)
+    assert np.array_equal(t[:, 0], pairs[:, 0]) and np.array_equal(t[:, 1], pairs[:, 1])
+    for b, (ra, rb) in enumerate(pairs):
+        for w in range(5):
+            assert t[b, 2 + w] == rp[min(ra + 64 * w, rb)]
+        for w in range(4):
+            a = ra + 64 * w
+            L = lens[a:a + 64]
+            want = int(L[0]) if (rb - a >= 64 and np.all(L == L[0]) and L[0] in (8, 10, 12) and rp[a] % 2 == 0) else 0
+            assert (int(t[b, 7]) >> (8 * w)) & 255 == want, (b, w)
+    assert (int(t[0, 7]) & 255) == 12 and ((int(t[0, 7]) >> 8) & 255) == (10 if rp[64] % 2 == 0 else 0)

@@ -32,10 +32,12 @@ def main():
     nbytes = A.nnz * 12 + (A.shape[0] + 1) * 4 + (A.shape[0] + A.shape[1]) * 8 + A.blocks.count * 8
     res = {"n": args.n, "nnz": A.nnz, "lib": os.environ.get("MPBP_LIB", "default")}
     flat = A.plan_blocks(groups=1)   # blocks in plain row order (no per-field interleave)
-    runs = [("csr_wave", A, None, "seq"), ("csr_seg", A, None, "seg"), ("csr_wave_roworder", A, flat, "seq"),
-            ("sell", AS, None, None)]
+    from mp_block_preconditioners_amd._lib import check, lib
+    runs = [("csr_wave", A, None, "seq"), ("csr_wave_notable", A, None, "notable"), ("csr_seg", A, None, "seg"),
+            ("csr_wave_roworder", A, flat, "seq"), ("sell", AS, None, None)]
     for name, M, blk, order in runs:
         kw = {"blocks": blk} if blk is not None else {}
+        check(lib().mpbp_set_csr_table(0 if order == "notable" else 1))
         if order == "seg":
             kw["order"] = "seg"
         for _ in range(5):
