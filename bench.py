@@ -111,6 +111,8 @@ def main():
     ap.add_argument("--pg-direct", type=int, default=None, help="1: D / Gt_G sweeps as one thread per cell (no LDS)")
     ap.add_argument("--svl-min-rows", type=int, default=None,
                     help="multigrid levels above this many rows get a stencil-values copy (mg.SVL_MIN_ROWS; -1: none)")
+    ap.add_argument("--stored-transfers", action="store_true",
+                    help="multigrid transfers from their stored forms instead of matrix-free")
     ap.add_argument("--mg-group-rows", type=int, default=None,
                     help="multigrid levels / transfers with at most this many rows on the grouped CSR kernel (0: off)")
     ap.add_argument("--no-fuse-g", action="store_true",
@@ -175,6 +177,8 @@ def main():
     _check(_lib().mpbp_set_march_rows(args.march_rows))
     if args.pg_direct is not None:
         _check(_lib().mpbp_set_pg_direct(args.pg_direct))
+    if args.stored_transfers:
+        _check(_lib().mpbp_set_mg_mf_transfer(0))
     if args.mg_group_rows is not None:
         _check(_lib().mpbp_set_mg_group_rows(args.mg_group_rows))
     if args.svl_min_rows is not None:

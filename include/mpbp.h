@@ -213,6 +213,13 @@ typedef struct mpbp_mg {
     mpbp_halo_fn halo;
     void* halo_ctx;                  /* passed to halo and gather */
     mpbp_gather_fn gather;
+    /* optional (tr_nfields > 0): the transfers' field kinds (MPBP_MG_CELL / NODE along y and x per field, as
+     * mpbp_mg_transfer_fill) and level 0's grid size: the whole-grid levels' restriction and prolongation are then
+     * applied matrix-free, their weights and columns recomputed per row in the CSR form's order (same bits) */
+    int32_t tr_nfields;
+    int32_t tr_n0;
+    int32_t tr_ky[8];
+    int32_t tr_kx[8];
 } mpbp_mg;
 
 /* The apply's operands.  On one GPU every matrix's columns index the full vector and the
@@ -426,6 +433,8 @@ int mpbp_set_pg_direct(int32_t on);
 int mpbp_set_mg_group_rows(int32_t rows);
 /* 1 (default): multigrid levels with a stencil-values copy (mpbp_mg_level.A_svl) use it; 0: their SELL / CSR form. */
 int mpbp_set_mg_svl(int32_t on);
+/* 1 (default): whole-grid multigrid transfers matrix-free when mpbp_mg names the field kinds; 0: stored forms. */
+int mpbp_set_mg_mf_transfer(int32_t on);
 /* 1 (default): the CSR SpMV's waves start from mpbp_rowblocks.table when present; 0: from row_ptr (same bits). */
 int mpbp_set_csr_table(int32_t on);
 

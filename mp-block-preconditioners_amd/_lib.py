@@ -79,7 +79,8 @@ class Mg(Structure):
     _fields_ = [("nlevels", c_int32), ("cycles", c_int32), ("levels", POINTER(MgLevel)), ("coarse_inv", Csr),
                 ("coarse_inv_blocks", RowBlocks), ("coarse_dense", c_void_p),
                 ("part_levels", c_int32), ("gather_kind", c_int32), ("halo", HALO_FN), ("halo_ctx", c_void_p),
-                ("gather", GATHER_FN)]
+                ("gather", GATHER_FN), ("tr_nfields", c_int32), ("tr_n0", c_int32), ("tr_ky", c_int32 * 8),
+                ("tr_kx", c_int32 * 8)]
 
 
 class SchurPlan(Structure):
@@ -161,6 +162,7 @@ _SIGNATURES = {
     "mpbp_set_pg_direct": ([c_int32], c_int),
     "mpbp_set_mg_group_rows": ([c_int32], c_int),
     "mpbp_set_mg_svl": ([c_int32], c_int),
+    "mpbp_set_mg_mf_transfer": ([c_int32], c_int),
     "mpbp_set_csr_table": ([c_int32], c_int),
     "mpbp_q13_build": ([POINTER(Csr), c_int32, c_void_p, c_void_p], c_int),
     "mpbp_svl_spmv": ([POINTER(Svl), POINTER(Csr), c_int32, _P, _P, _P, _P], c_int),

@@ -23,6 +23,7 @@ thread_local char g_err[1024] = "";
 // (measured best at every size: 256^2 1 row -> 13.5k applies/s vs 7.6k at 4; 1024^2 4; 2048^2 16 -> 753 vs 727)
 int g_march_rows = 0;
 int g_csr_table = 1;      // CSR SpMV waves start from the row blocks' wave table when it has one (0: from row_ptr)
+int g_mg_mf_transfer = 1;   // whole-grid multigrid transfers matrix-free (0: their CSR / SELL / grouped forms)
 int g_init_diag = 1;      // fused first F sweep: 1 rebuilds the staged diagonal from thn, 0 streams diag
 #ifndef MPBP_PG_ROWS
 #define MPBP_PG_ROWS 0    // rows per workgroup of the D / G / Gt_G marching kernels (0: as F)
@@ -632,6 +633,33 @@ __device__ inline int mg_r1d(int kind, int nf, int i, int* idx, double* w) {
     }
     sort_pairs<4>(m, idx, w);
     return m;
+}
+
+// y = op(T x) for T = P or R of the n x n grid (n = fine size), matrix-free: each row rebuilds its tensor-product
+// weights and columns exactly as k_mg_transfer stores them (same order, same products), so the sums are the CSR
+// SpMV's bit for bit; no matrix stream, and the x gathers issue without waiting for column loads.
+template <class Epi>
+__global__ void __launch_bounds__(kBlock) k_mg_transfer_spmv(MgFields F, int32_t n, int32_t which, int32_t nrows,
+                                                             const double* __restrict__ x, Epi epi) {
+    const int32_t row = (int32_t)(blockIdx.x * kBlock + threadIdx.x);
+    if (row >= nrows) return;
+    const typename Epi::P pe = epi.pre(row);
+    const int nc = n / 2;
+    const int nr = which == MPBP_MG_P ? n : nc;
+    const int nk = which == MPBP_MG_P ? nc : n;
+    const uint32_t per = (uint32_t)nr * (uint32_t)nr;
+    const int fld = (int)((uint32_t)row / per);
+    const uint32_t cell = (uint32_t)row - (uint32_t)fld * per;
+    const int r = (int)(cell / (uint32_t)nr), c = (int)(cell - (uint32_t)r * (uint32_t)nr);
+    int yi[4], xi[4];
+    double yw[4], xw[4];
+    const int my = which == MPBP_MG_P ? mg_p1d(F.ky[fld], nc, r, yi, yw) : mg_r1d(F.ky[fld], n, r, yi, yw);
+    const int mx = which == MPBP_MG_P ? mg_p1d(F.kx[fld], nc, c, xi, xw) : mg_r1d(F.kx[fld], n, c, xi, xw);
+    const int32_t off = fld * nk * nk;
+    double acc = 0.0;
+    for (int a = 0; a < my; ++a)
+        for (int b = 0; b < mx; ++b) acc += (yw[a] * xw[b]) * x[off + yi[a] * nk + xi[b]];
+    epi(row, acc, pe);
 }
 
 // which: MPBP_MG_P (rows = fine unknowns) or MPBP_MG_R (rows = coarse unknowns); n = fine grid size.
@@ -2687,6 +2715,10 @@ int mpbp_set_csr_table(int32_t on) {
     g_csr_table = on ? 1 : 0;
     return MPBP_OK;
 }
+int mpbp_set_mg_mf_transfer(int32_t on) {
+    g_mg_mf_transfer = on ? 1 : 0;
+    return MPBP_OK;
+}
 int mpbp_set_mg_svl(int32_t on) {
     g_svl_on = on ? 1 : 0;
     return MPBP_OK;
@@ -3933,6 +3965,28 @@ void mg_exchange(const mpbp_mg* m, int l, const MgFine& f, double* x, hipStream_
         m->halo(m->halo_ctx, m->levels[l].halo_kind, x, MPBP_HALO_END, (void*)st);
     }
 }
+// Level l's restriction (which = MPBP_MG_R) or prolongation (MPBP_MG_P) matrix-free when the hierarchy names its
+// field kinds and the level is whole-grid (not row-partitioned); 1: launched, 0: not applicable.
+template <class Epi>
+int mg_transfer_mf(const mpbp_mg* m, int l, int32_t which, int32_t nrows, const double* x, Epi epi, hipStream_t st) {
+    k_mg_transfer_spmv<Epi><<<grid_for(nrows), kBlock, 0, st>>>(
+        [&] {
+            MgFields F{};
+            F.nfields = m->tr_nfields;
+            for (int f = 0; f < m->tr_nfields; ++f) {
+                F.ky[f] = m->tr_ky[f];
+                F.kx[f] = m->tr_kx[f];
+            }
+            return F;
+        }(),
+        m->tr_n0 >> l, which, nrows, x, epi);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+inline bool use_mf_transfer(const mpbp_mg* m, int l) {
+    return g_mg_mf_transfer && m->tr_nfields > 0 && m->tr_nfields <= 8 && l >= m->part_levels && (m->tr_n0 >> l) >= 4 &&
+           ((m->tr_n0 >> l) << l) == m->tr_n0;
+}
 int mg_transfer(const mpbp_csr& M, const mpbp_rowblocks& blk, const mpbp_sell& S, int32_t mode, const double* x,
                 const double* z, double* y, hipStream_t st) {
     if (use_grp(M)) return grp_spmv(&M, mode, x, z, y, st);
@@ -4069,7 +4123,8 @@ int mg_vcycle(const mpbp_mg* m, int l, const MgFine& fine, const double* b, bool
     const mpbp_mg_level& C = m->levels[l + 1];
     const bool gather = m->part_levels > 0 && l + 1 == m->part_levels;
     if (l < m->part_levels) xch(r);
-    rc = mg_transfer(L.R, L.R_blocks, L.R_sell, MPBP_SPMV_STORE, r, nullptr, gather ? C.r : C.b, st);
+    rc = use_mf_transfer(m, l) ? mg_transfer_mf(m, l, MPBP_MG_R, L.R.nrows, r, EpiStore{gather ? C.r : C.b}, st)
+                               : mg_transfer(L.R, L.R_blocks, L.R_sell, MPBP_SPMV_STORE, r, nullptr, gather ? C.r : C.b, st);
     if (rc) return rc;
     if (gather) {
         if (!m->gather) return set_error(MPBP_ERR_ARG, "mg: a partitioned hierarchy needs its gather callback");
@@ -4089,7 +4144,8 @@ int mg_vcycle(const mpbp_mg* m, int l, const MgFine& fine, const double* b, bool
     if (rc) return rc;
     // x += P x_c (row-wise in place), then post-smoothing from x
     mg_exchange(m, l + 1, fine, xc, st);
-    rc = mg_transfer(L.P, L.P_blocks, L.P_sell, MPBP_SPMV_ADD, xc, cur, cur, st);
+    rc = use_mf_transfer(m, l) ? mg_transfer_mf(m, l, MPBP_MG_P, L.P.nrows, xc, EpiAdd{cur, cur}, st)
+                               : mg_transfer(L.P, L.P_blocks, L.P_sell, MPBP_SPMV_ADD, xc, cur, cur, st);
     if (rc) return rc;
     rc = mg_smooth(o, L.nrows, diag, L.lmin, L.lmax, L.post, false, b, &cur, alt, d, dst, sub, st, xch);
     if (rc) return rc;

@@ -492,6 +492,8 @@ class PartitionedMultigrid:
                            g.coarse_inv.cstruct(), g.coarse_inv.blocks.cstruct(),
                            g.coarse_dense.data_ptr() if g.coarse_dense is not None else None,
                            P, self.gather_kind, halos.fn, halos.ctx, halos.gather_fn)
+        from .mg import set_transfer_kinds
+        set_transfer_kinds(self._mg, g.fields, g.n)   # (matrix-free transfers on the replicated levels only)
         return self
 
     def cstruct(self):

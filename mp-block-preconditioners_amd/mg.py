@@ -147,6 +147,15 @@ def stencil_values_arrays(row_ptr: torch.Tensor, col_idx: torch.Tensor, val: tor
     return R, K, delta.reshape(-1).contiguous(), vals, edge
 
 
+def set_transfer_kinds(mg_struct, fields, n0: int):
+    """mpbp_mg.tr_*: the transfers' field kinds and level 0's grid size (matrix-free whole-grid transfers)."""
+    mg_struct.tr_nfields = len(fields)
+    mg_struct.tr_n0 = int(n0)
+    for f, (ky, kx) in enumerate(fields):
+        mg_struct.tr_ky[f] = ky
+        mg_struct.tr_kx[f] = kx
+
+
 SVL_MIN_ROWS = 65536     # Multigrid's default: levels >= 1 above this many rows get a stencil-values copy
 MAX_COARSE_ROWS = 8192   # the coarsest level's dense pseudo-inverse: 8192^2 doubles = 512 MB, an O(m^3) host pinv
 
@@ -266,6 +275,12 @@ class Multigrid:
         self._mg = _lib.Mg(len(self.ops), cycles, ctypes.cast(self._levels, ctypes.POINTER(_lib.MgLevel)),
                            self.coarse_inv.cstruct(), self.coarse_inv.blocks.cstruct(),
                            self.coarse_dense.data_ptr() if self.coarse_dense is not None else None)
+        set_transfer_kinds(self._mg, self.fields, n)
+
+    def set_matrix_free_transfers(self, on: bool):
+        """Name (on) or hide (off) the field kinds in the hierarchy's struct: with them the whole-grid levels' transfers
+        run matrix-free (same bits as the stored P / R)."""
+        set_transfer_kinds(self._mg, self.fields if on else (), self.n)
 
     @property
     def nlevels(self) -> int:

@@ -107,6 +107,15 @@ def group_rows(request):
     check(lib().mpbp_set_mg_group_rows(65536))
 
 
+@pytest.fixture(params=[1, 0], ids=["mftransfer", "storedtransfer"])
+def mf_transfer(request):
+    """Whole-grid transfers matrix-free (default) or from their stored CSR / SELL / grouped forms."""
+    from mp_block_preconditioners_amd._lib import check, lib
+    check(lib().mpbp_set_mg_mf_transfer(request.param))
+    yield request.param
+    check(lib().mpbp_set_mg_mf_transfer(1))
+
+
 @pytest.fixture(params=[False, True], ids=["rowlayouts", "svl"])
 def svl_all(request, monkeypatch):
     """Every coarse level with a stencil-values copy (mg.SVL_MIN_ROWS = 0), or the default (none at these sizes)."""
@@ -166,7 +175,7 @@ def test_stencil_values_spmv_bit_exact(n):
 
 @pytest.mark.parametrize("sell", [True, False], ids=["sell", "csr"])
 @pytest.mark.parametrize("n,cycles,pre,post", [(16, 1, 2, 2), (32, 2, 2, 2), (64, 1, 1, 3), (64, 3, 2, 1)])
-def test_mg_solve_bit_exact(n, cycles, pre, post, sell, group_rows, svl_all):
+def test_mg_solve_bit_exact(n, cycles, pre, post, sell, group_rows, svl_all, mf_transfer):
     """V-cycles vs the oracle: with the SELL-64 copies of every level and the dense coarse kernel (default), and
     with the CSR forms throughout; the small levels and transfers on the grouped CSR kernel (several lanes per row,
     the row's sum in order) or on the row kernels."""
