@@ -1366,6 +1366,7 @@ struct Svl {
 #define MPBP_SVL_BATCH 8
 #endif
 constexpr int kSvB = MPBP_SVL_BATCH;  // slots per batch (values + gathers in flight together)
+
 constexpr int kSvMaxDelta = 256;     // nf * K
 constexpr int kSvEdgeG = 8;          // lanes per edge row (k_csr_grp's scheme: one latency chain per row)
 template <class XS, class Epi>
