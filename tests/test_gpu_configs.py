@@ -198,3 +198,39 @@ def test_1024_stiff_properties():
     pc_asm = mp.ApproxSchurPreconditioner(F, D, G, pc.GtG, pc.GtFG, inner_F=iF, inner_P=iP, f_mode="assembled",
                                           pg_mode="assembled")
     assert torch.equal(pc_asm.apply(v1), y1)                                              # matrix-free == assembled
+
+
+# ---- configs[2] with the multigrid inner solves (the bench's mg:1 / mg:1 apply) at 1024^2 ----------------------
+def test_1024_mg_apply_properties():
+    """The headline-size Schur apply with V(2,2) multigrid inner solves: linear (1e-12), deterministic, hipGraph
+    replay == eager, and every kernel choice the library makes for a level (stencil-values / SELL on the large
+    coarse levels, grouped / SELL on the small ones, matrix-free / stored transfers) gives the same bits -- the
+    256^2 oracle tests (tests/test_gpu_mg.py) pin those choices against oracle/mg_oracle.py."""
+    mp = _mp()
+    from mp_block_preconditioners_amd._lib import check, lib
+    n = 1024
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("mg", 1), inner_P=mp.InnerSolver("mg", 1))
+    gen = torch.Generator(device="cuda").manual_seed(11)
+    v1 = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda", generator=gen)
+    v2 = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda", generator=gen)
+    y1, y2 = pc.apply(v1).clone(), pc.apply(v2).clone()
+    y12 = pc.apply(2.0 * v1 - 0.5 * v2)
+    assert rel_inf(y12.cpu().numpy(), (2.0 * y1 - 0.5 * y2).cpu().numpy()) <= 1e-12      # linearity
+    assert torch.equal(pc.apply(v1), y1)                                                  # determinism
+    out = torch.empty_like(v1)
+    g = pc.capture(v1, out)
+    g.replay()
+    torch.cuda.synchronize()
+    y1h = y1.cpu().numpy()
+    assert _bits_equal(out, y1h)                                                          # graph == eager
+    try:
+        for setter, off in ((lib().mpbp_set_mg_svl, 0), (lib().mpbp_set_mg_group_rows, 0),
+                            (lib().mpbp_set_mg_mf_transfer, 0)):
+            check(setter(off))
+            assert _bits_equal(pc.apply(v1), y1h), setter
+    finally:
+        check(lib().mpbp_set_mg_svl(1))
+        check(lib().mpbp_set_mg_group_rows(65536))
+        check(lib().mpbp_set_mg_mf_transfer(1))
