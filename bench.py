@@ -598,7 +598,7 @@ SOLVE_CASES = (   # (n, eta_n, eta_s, preconditioners): BASELINE configs[1] / co
     (256, 100.0, 1.0, ("none", "chebyshev:4", "mg:1")),
     (256, 1e4, 1.0, ("none", "chebyshev:4", "mg:1", "mg:2/mg:1")),
     (1024, 100.0, 1.0, ("chebyshev:4", "mg:1", "mg:2/mg:1")),
-    (1024, 1e4, 1.0, ("chebyshev:4", "mg:1", "mg:1@3,3", "mg:2/mg:1")),
+    (1024, 1e4, 1.0, ("chebyshev:4", "mg:1", "mg:2/mg:1")),
 )
 
 

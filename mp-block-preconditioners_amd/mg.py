@@ -158,6 +158,12 @@ def set_transfer_kinds(mg_struct, fields, n0: int):
 
 SVL_MIN_ROWS = 65536     # Multigrid's default: levels >= 1 above this many rows get a stencil-values copy
 MAX_COARSE_ROWS = 8192   # the coarsest level's dense pseudo-inverse: 8192^2 doubles = 512 MB, an O(m^3) host pinv
+# Singular values below COARSE_RCOND * sigma_max of the coarsest operator are its null space.  Gt_G on the periodic
+# grid annihilates constants; after six Galerkin products that mode's singular value is roundoff, 8.5e-16 sigma_max at
+# 256^2 but 5.6e-15 at 1024^2 -- above numpy's default cut (1e-15), so the pseudo-inverse inverted it and the pressure
+# solve's output carried a ~1e17 constant.  The next singular values are 9e-2 (Gt_G) and, for F, 7.5e-6 (eta ratio
+# 100) / 7.5e-8 (10^4) (tools/coarse_spectrum.py): 1e-11 sits orders of magnitude from both.
+COARSE_RCOND = 1e-11
 
 
 def dense_inverse_csr(A: DeviceCSR) -> tuple[DeviceCSR, np.ndarray]:
@@ -167,7 +173,7 @@ def dense_inverse_csr(A: DeviceCSR) -> tuple[DeviceCSR, np.ndarray]:
                          f"need {A.shape[0] ** 2 * 8 / 1e9:.1f} GB and an O(m^3) factorisation; coarsening stops at an odd "
                          "grid size, so use a grid n = m 2^k with a small m (or a larger `coarsest`)")
     Ad = A.to_scipy().toarray()
-    inv = np.ascontiguousarray(np.linalg.pinv(Ad))
+    inv = np.ascontiguousarray(np.linalg.pinv(Ad, rcond=COARSE_RCOND))
     m = inv.shape[0]
     dev = A.device
     rp = np.arange(0, m * m + 1, m, dtype=np.int32)

@@ -26,6 +26,7 @@ from .schur_oracle import cheb_coeffs, gershgorin
 CELL, NODE = 0, 1
 FIELDS_VELOCITY = ((CELL, NODE), (NODE, CELL), (CELL, NODE), (NODE, CELL))
 FIELDS_PRESSURE = ((CELL, CELL),)
+COARSE_RCOND = 1e-11   # the coarsest operator's null-space cut (mg.py COARSE_RCOND: Gt_G's constant mode is roundoff)
 
 
 def p1d(nf: int, kind: int) -> sp.csr_matrix:
@@ -85,7 +86,8 @@ def smooth(A, diag, lmin, lmax, K, b, x=None, sub=None):
 
 class MgOracle:
     """V-cycles over ``hierarchy``.  bounds: per-level (lmin, lmax) (default Gershgorin / ratio); coarse_inv:
-    the coarsest level's pseudo-inverse (default numpy pinv)."""
+    the coarsest level's pseudo-inverse (default numpy pinv with singular values below COARSE_RCOND * sigma_max
+    dropped, the product's rule, mg.py COARSE_RCOND)."""
 
     def __init__(self, A, n, fields, pre=2, post=2, cycles=1, ratio=4.0, coarsest=8, bounds=None, coarse_inv=None):
         self.ops, self.P, self.R = hierarchy(A, n, fields, coarsest)
@@ -98,7 +100,7 @@ class MgOracle:
         self.bounds = bounds
         self.pre, self.post, self.cycles = pre, post, cycles
         Ac = self.ops[-1][0].toarray()
-        self.coarse_inv = np.linalg.pinv(Ac) if coarse_inv is None else np.asarray(coarse_inv)
+        self.coarse_inv = np.linalg.pinv(Ac, rcond=COARSE_RCOND) if coarse_inv is None else np.asarray(coarse_inv)
         m = self.coarse_inv.shape[0]
         self._cinv = sp.csr_matrix((self.coarse_inv.reshape(-1), np.tile(np.arange(m), m),
                                     np.arange(0, m * m + 1, m)), shape=(m, m))

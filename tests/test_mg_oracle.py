@@ -116,3 +116,20 @@ def test_mg_preconditioner_beats_chebyshev(mo, oracle_built):
         return np.concatenate([oF.solve(co.spmv(S.G, xp), sub=Fv), xp])
     it_cheb, it_mg = _fgmres_its(S.A, b, cheb), _fgmres_its(S.A, b, mg)
     assert it_mg < 70 and it_mg < it_cheb, (it_mg, it_cheb)
+
+
+@pytest.mark.parametrize("n", [32, 64])
+def test_coarse_inverse_drops_the_pressure_null_space(mo, n):
+    """mg.COARSE_RCOND: the coarsest Gt_G (periodic: constants in its null space) gets a rank m - 1 pseudo-inverse that
+    maps constants to ~0; the coarsest F keeps full rank.  (At 1024^2 numpy's default cut kept Gt_G's roundoff-level
+    constant mode and the pressure solve's output carried a ~1e17 constant: tools/coarse_spectrum.py.)"""
+    from mp_block_preconditioners_amd import mg
+    from oracle.stokes_oracle import StokesSystem
+    assert mo.COARSE_RCOND == mg.COARSE_RCOND
+    S = StokesSystem(n, 1.0, 100.0, 1.0, 1.0, -1.0, products=True)
+    oP = mo.MgOracle(S.GtG, n, mo.FIELDS_PRESSURE, coarsest=8)
+    oF = mo.MgOracle(S.F, n, mo.FIELDS_VELOCITY, coarsest=8)
+    m = oP.coarse_inv.shape[0]
+    assert np.linalg.matrix_rank(oP.coarse_inv, tol=1e-8 * np.abs(oP.coarse_inv).max()) == m - 1
+    assert np.abs(oP.coarse_inv @ np.ones(m)).max() <= 1e-10 * np.abs(oP.coarse_inv).max()
+    assert np.linalg.matrix_rank(oF.coarse_inv) == oF.coarse_inv.shape[0]
