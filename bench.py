@@ -50,7 +50,9 @@ def sweep_bytes(pc, layout, kind, sweeps, fused_init):
     stencil = getattr(pc, "f_stencil", None) is not None
     if stencil:
         prm = pc.f_stencil.prm   # the parameter identities compiled into the F policy (csrc: with_f_identities)
-        pol = ("FStencilDevM<7>" if prm.eta_n == 1.0 else "FStencilDevM<5>") \
+        n_f = int(prm.n)
+        pow2 = (n_f & (n_f - 1)) == 0
+        pol = ("FStencilDevM<7>" if prm.eta_n == 1.0 else ("FStencilDevM<13>" if pow2 else "FStencilDevM<5>")) \
             if (prm.d_u == -1.0 and prm.eta_s == 1.0) else "FStencilDev"
         fixed, kname = 3 * 8 * (nF // 4), f"k_march<{pol}, XPlain, EpiCheb> (F sweep, matrix-free)"
     elif layout == "sell":

@@ -1596,6 +1596,7 @@ struct FStencilDev {
     int pow2;      // n is a power of two: dx * dx is a power of two and v / (dx * dx) == v * idx2 exactly
     int ext = 0;   // which = 3: ghost rows computed on each side
     int oh = 0;    // ghost depth of the output's layout (== h)
+    double ce0 = 0.0, ce1 = 0.0;   // pow2: eta_n * idx2, eta_s * idx2 (exact: idx2 is a power of two)
 
     __device__ int wrap(int a) const { return a < 0 ? a + n : (a >= n ? a - n : a); }
     // index in x of (field f, grid row gr, column 0) for gr in [r0 - h, r0 + L + h)
@@ -1688,8 +1689,10 @@ __device__ inline double FStencilDev::stage_diag(int f, int gr, int gc, const TA
 // phase s at a cell, XA::X(f, gr, gc) the x entry of field f at a grid point (gr in [-1, n], gc in
 // [-1, n]; the accessors wrap).  Same operations as phase_L_row / F_row, same summation order.
 // M (exact parameter identities, compile time): bit 0 d_u == -1 (d_u * y is an exact negation, folded into
-// the products as a sign), bit 1 eta_n == 1, bit 2 eta_s == 1 (eta * y == y exactly).  Every entry keeps
-// the assembly's rounding; only multiplications whose result is exactly known are skipped.
+// the products as a sign), bit 1 eta_n == 1, bit 2 eta_s == 1 (eta * y == y exactly), bit 3 idx2 a power of
+// two: eta * (idx2 * y) == y * (eta * idx2) for every y (idx2 * y and eta * idx2 are exact scalings, so both
+// sides are the one rounding of the same real), one multiply per off-diagonal entry instead of two.  Every
+// entry keeps the assembly's rounding; only multiplications whose result is exactly known are skipped.
 template <bool EDGE, class TA, class XA, bool VIRT = false, int M = 0>
 __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, const TA& ta, const XA& xa,
                                double* fdiag, const double* face = nullptr) {
@@ -1700,6 +1703,10 @@ __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, cons
     const bool eta1 = p ? (M & 4) != 0 : (M & 2) != 0;
     auto dmul = [&](double y) -> double { return (M & 1) ? -y : P.d_u * y; };   // d_u * y
     auto emul = [&](double y) -> double { return eta1 ? y : eta * y; };          // eta * y
+    auto sc = [&](double y) -> double {                                          // eta * (idx2 * y)
+        if constexpr ((M & 8) != 0) return eta1 ? idx2 * y : y * (p ? P.ce1 : P.ce0);
+        else return emul(idx2 * y);
+    };
     const int fu = 2 * p, fv = 2 * p + 1;
     const int32_t kc = VIRT ? P.wrap(gr) * n + P.wrap(gc) : gr * n + gc;   // VIRT: (gr, gc) may lie one cell outside
     auto T = [&](int r, int c) -> double { return ta.T(p, r, c); };
@@ -1715,15 +1722,15 @@ __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, cons
         *fdiag = fd;
         // same field: N, W, C, E, S; the other component (v of this phase): (gr, gc-1), (gr, gc), (gr+1, gc-1),
         // (gr+1, gc)
-        const double lo[5] = {dmul(emul(idx2 * (iph_jph))) * xa.X(fu, gr - 1, gc),
-                              dmul(emul(idx2 * (tij))) * xa.X(fu, gr, gc - 1),
+        const double lo[5] = {dmul(sc(iph_jph)) * xa.X(fu, gr - 1, gc),
+                              dmul(sc(tij)) * xa.X(fu, gr, gc - 1),
                               fd * xa.X(fu, gr, gc),
-                              dmul(emul(P.pow2 ? tip1j * idx2 : tip1j / P.dxdx)) * xa.X(fu, gr, gc + 1),
-                              dmul(emul(idx2 * (iph_jmh))) * xa.X(fu, gr + 1, gc)};
-        const double hi[4] = {dmul(emul(idx2 * (tij - iph_jph))) * xa.X(fv, gr, gc - 1),
-                              dmul(emul(idx2 * (-tip1j + iph_jph))) * xa.X(fv, gr, gc),
-                              dmul(emul(idx2 * (iph_jmh - tij))) * xa.X(fv, gr + 1, gc - 1),
-                              dmul(emul(idx2 * (tip1j - iph_jmh))) * xa.X(fv, gr + 1, gc)};
+                              dmul((M & 8) ? sc(tip1j) : emul(P.pow2 ? tip1j * idx2 : tip1j / P.dxdx)) * xa.X(fu, gr, gc + 1),
+                              dmul(sc(iph_jmh)) * xa.X(fu, gr + 1, gc)};
+        const double hi[4] = {dmul(sc(tij - iph_jph)) * xa.X(fv, gr, gc - 1),
+                              dmul(sc(-tip1j + iph_jph)) * xa.X(fv, gr, gc),
+                              dmul(sc(iph_jmh - tij)) * xa.X(fv, gr + 1, gc - 1),
+                              dmul(sc(tip1j - iph_jmh)) * xa.X(fv, gr + 1, gc)};
         const double vcross = dmul(xi_ii);
         if (p == 1) acc += vcross * xcross;
         acc = add5<EDGE>(acc, lo, w);
@@ -1738,15 +1745,15 @@ __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, cons
         *fdiag = fd;
         // the other component (u of this phase): (gr-1, gc), (gr-1, gc+1), (gr, gc), (gr, gc+1); same field: N, W,
         // C, E, S
-        const double lo[4] = {dmul(emul(idx2 * (tijp1 - imh_jph))) * xa.X(fu, gr - 1, gc),
-                              dmul(emul(idx2 * (iph_jph - tijp1))) * xa.X(fu, gr - 1, gc + 1),
-                              dmul(emul(idx2 * (imh_jph - tij))) * xa.X(fu, gr, gc),
-                              dmul(emul(idx2 * (tij - iph_jph))) * xa.X(fu, gr, gc + 1)};
-        const double hi[5] = {dmul(emul(idx2 * tijp1)) * xa.X(fv, gr - 1, gc),
-                              dmul(emul(idx2 * imh_jph)) * xa.X(fv, gr, gc - 1),
+        const double lo[4] = {dmul(sc(tijp1 - imh_jph)) * xa.X(fu, gr - 1, gc),
+                              dmul(sc(iph_jph - tijp1)) * xa.X(fu, gr - 1, gc + 1),
+                              dmul(sc(imh_jph - tij)) * xa.X(fu, gr, gc),
+                              dmul(sc(tij - iph_jph)) * xa.X(fu, gr, gc + 1)};
+        const double hi[5] = {dmul(sc(tijp1)) * xa.X(fv, gr - 1, gc),
+                              dmul(sc(imh_jph)) * xa.X(fv, gr, gc - 1),
                               fd * xa.X(fv, gr, gc),
-                              dmul(emul(idx2 * iph_jph)) * xa.X(fv, gr, gc + 1),
-                              dmul(emul(idx2 * tij)) * xa.X(fv, gr + 1, gc)};
+                              dmul(sc(iph_jph)) * xa.X(fv, gr, gc + 1),
+                              dmul(sc(tij)) * xa.X(fv, gr + 1, gc)};
         const double vcross = dmul(xi_ii);
         if (p == 1) acc += vcross * xcross;
         acc = add4<EDGE>(acc, lo, w.r0, w.cl);
@@ -2383,7 +2390,13 @@ struct FStencilDevM : FStencilDev {
 // Calls fn with the F policy specialised for P's parameters (M = 0: none apply).
 template <class Fn>
 int with_f_identities(const FStencilDev& P, Fn&& fn) {
-    if (P.d_u == -1.0 && P.eta_s == 1.0) return P.eta_n == 1.0 ? fn(FStencilDevM<7>{P}) : fn(FStencilDevM<5>{P});
+#ifndef MPBP_F_POW2
+#define MPBP_F_POW2 1
+#endif
+    if (P.d_u == -1.0 && P.eta_s == 1.0) {
+        if (MPBP_F_POW2 && P.eta_n != 1.0 && P.pow2 && P.ce0 != 0.0 && __builtin_isfinite(P.ce0)) return fn(FStencilDevM<13>{P});
+        return P.eta_n == 1.0 ? fn(FStencilDevM<7>{P}) : fn(FStencilDevM<5>{P});
+    }
     return fn(P);
 }
 
@@ -2401,6 +2414,7 @@ struct PGDev {
     int r0, L, h, which;
     int ext = 0;   // which = 3: ghost rows computed on each side
     int oh = 0;    // ghost depth of the output's layout (D: pressure, G: velocity, Gt_G: == h)
+    int unit = 0;  // d_p == 1 and minv == -inv: Gt_G's eight products per phase are +-X^2 (GtGStencilDev::entries)
     __device__ int wrap(int a) const { return a < 0 ? a + n : (a >= n ? a - n : a); }
     template <int NFI>
     __device__ int32_t xrow_of(int f, int gr) const {
@@ -2486,6 +2500,32 @@ struct GtGStencilDev : PGDev {
     __device__ void entries(int vr, int vc, int gr, int gc, const TA& ta, double* e) const {
         const bool lastc = gc == n - 1, lastr = gr == n - 1;
         double cN = 0.0, cW = 0.0, cC = 0.0, cE = 0.0, cS = 0.0;
+        if (unit) {
+            // d_p == 1 and minv == -inv: with X = inv * (0.5 * (t0 + t_nb)) per face, every D entry is +-X and
+            // every G factor d_p * (+-inv * g) is +-X too (g is the same half sum), so the eight products below
+            // are +-X^2 -- the same roundings (RN(-a b) = -RN(a b)), same bits, 12 multiplies per phase, not 28
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const double t0 = ta.T(p, vr, vc), tE = ta.T(p, vr, vc + 1), tW = ta.T(p, vr, vc - 1);
+                const double tN = ta.T(p, vr - 1, vc), tS = ta.T(p, vr + 1, vc);
+                const double XW = inv * (0.5 * (t0 + tW)), XE = inv * (0.5 * (t0 + tE));
+                const double XN = inv * (0.5 * (t0 + tN)), XS = inv * (0.5 * (t0 + tS));
+                const double qW = XW * XW, qE = XE * XE, qN = XN * XN, qS = XS * XS;
+                // uC_C = -qW, uC_W = qW, uE_E = qE, uE_C = -qE, vC_C = -qN, vC_N = qN, vS_S = qS, vS_C = -qS
+                const double u1 = lastc ? -qE : -qW, u2 = lastc ? -qW : -qE;
+                const double v1 = lastr ? -qS : -qN, v2 = lastr ? -qN : -qS;
+                if (p == 0) {
+                    cC = u1; cW = qW; cE = qE; cN = qN; cS = qS;
+                } else {
+                    cC += u1; cW += qW; cE += qE; cN += qN; cS += qS;
+                }
+                cC += u2;
+                cC += v1;
+                cC += v2;
+            }
+            e[0] = -1.0 * cN; e[1] = -1.0 * cW; e[2] = -1.0 * cC; e[3] = -1.0 * cE; e[4] = -1.0 * cS;
+            return;
+        }
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
             const double t0 = ta.T(p, vr, vc), tE = ta.T(p, vr, vc + 1), tW = ta.T(p, vr, vc - 1);
@@ -3459,6 +3499,10 @@ static int make_fstencil(const mpbp_stokes_params* prm, const double* cell, cons
     *P = FStencilDev{prm->n, prm->xi, prm->eta_n, prm->eta_s, prm->c, prm->d_u, cell, uface, vface,
                      dx * dx, 1.0 / (dx * dx), -1.0 / (dx * dx), r0, L, h, which,
                      (prm->n & (prm->n - 1)) == 0 ? 1 : 0, ext, oh};
+    if (P->pow2) {   // idx2 = n^2 exactly: eta * idx2 is an exact scaling (f_row's M bit 3)
+        P->ce0 = prm->eta_n * P->idx2;
+        P->ce1 = prm->eta_s * P->idx2;
+    }
     return MPBP_OK;
 }
 
@@ -3532,6 +3576,10 @@ static int make_pgstencil(const mpbp_stokes_params* prm, const double* cell, con
             return set_error(MPBP_ERR_ARG, "pg_stencil: bad row partition");
     }
     *P = PGDev{prm->n, cell, prm->d_p, 1.0 / dx, -1.0 / dx, r0, L, h, which, ext, oh};
+#ifndef MPBP_GTG_UNIT
+#define MPBP_GTG_UNIT 1
+#endif
+    P->unit = MPBP_GTG_UNIT && P->d_p == 1.0 && P->minv == -P->inv;
     return MPBP_OK;
 }
 
