@@ -66,3 +66,13 @@ def test_stencil_values_refuses_other_operators():
     got = stencil_values_arrays(torch.from_numpy(I.indptr.astype(np.int32)), torch.from_numpy(I.indices.astype(np.int32)),
                                 torch.from_numpy(I.data), 1, n)
     assert got is not None and got[0] == 0 and got[1] == 1 and got[4].numel() == 0   # a diagonal: no edge rows
+
+
+def test_coarsest_level_size_is_capped():
+    """a grid that coarsens to a large odd size (1000 -> 125) must refuse the dense coarsest inverse
+    (4 * 125^2 = 62 500 rows: a 31 GB matrix and an O(m^3) pinv) with a clear error, before any allocation."""
+    from types import SimpleNamespace
+    from mp_block_preconditioners_amd import mg
+    assert mg.level_sizes(1000, 16) == [1000, 500, 250, 125]
+    with pytest.raises(ValueError, match="coarsest level has 62500 rows"):
+        mg.dense_inverse_csr(SimpleNamespace(shape=(62500, 62500)))
