@@ -531,6 +531,18 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
     V = torch.zeros(m + 1, n, **f64)
     Z = torch.zeros(m, n, **f64)
     vb = torch.zeros(m + 1, **f64)       # max |V[i]| bounds (identical on every rank)
+    # the iteration's scalars (h column, the norm's fold sums, the norm) reach the host through one pinned copy
+    # and an event: the next iteration's M and A applies are queued before the host waits, so the host's
+    # Givens step and the GPU's applies overlap (the last iteration's speculative apply is discarded)
+    on_gpu = b.is_cuda
+    hbuf = torch.empty(m + 5, dtype=torch.float64, pin_memory=on_gpu)
+    ev = torch.cuda.Event() if on_gpu else None
+
+    def head(j):
+        """Z[j] = M V[j], w = A Z[j]."""
+        Z[j] = Mop(V[j]) if Mop is not None else V[j]
+        w.copy_(Aop(Z[j]))        # fgmres's own buffer: the operator's return value is never modified
+
     while it < maxiter:
         beta = normr
         V.zero_()
@@ -541,9 +553,8 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
         torch.div(r, beta, out=V[0])
         vb[0:1] = bnd[0:1] / beta * _VB_SLACK   # (bnd[0] = max |r| from norm(r))
         k = 0
+        head(0)
         for j in range(m):
-            Z[j] = Mop(V[j]) if Mop is not None else V[j]
-            w.copy_(Aop(Z[j]))        # fgmres's own buffer: the operator's return value is never modified
             hs = None
             for _ in range(2):        # CGS2: h = V w, w -= V^T h, twice
                 K.amax(w, bnd[1:2])
@@ -552,14 +563,22 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
                 hs = h.clone() if hs is None else hs + h
             K.amax(w, bnd[1:2])
             a = K.fold_sums(w, n, 1, w, bnd[1:2], bnd[1:2])
-            host = torch.cat([hs, a]).cpu().tolist()
+            hn_d = torch.sqrt((a[0:1] + a[1:2]) + a[2:3])    # _finish, then the norm, on the device
+            inv = torch.reciprocal(hn_d)
+            torch.mul(w, inv, out=V[j + 1])
+            vb[j + 1:j + 2] = bnd[1:2] * inv * _VB_SLACK      # |fl(w_i inv)| <= fl(max|w| inv): rounding is monotone
+            hbuf[: j + 5].copy_(torch.cat([hs, a[:3], hn_d]), non_blocking=on_gpu)
+            if on_gpu:
+                ev.record()
+            if j + 1 < m and it + 1 < maxiter:
+                head(j + 1)           # speculative: queued behind the copy, runs while the host works
+            if on_gpu:
+                ev.synchronize()
+            host = hbuf[: j + 5].tolist()
             hcol = np.asarray(host[: j + 1])
-            hn = math.sqrt(_finish(host[j + 1:]))
+            hn = host[j + 4]
             H[: j + 1, j] = hcol
             H[j + 1, j] = hn
-            if hn != 0.0:
-                torch.div(w, hn, out=V[j + 1])
-                vb[j + 1:j + 2] = bnd[1:2] / hn * _VB_SLACK
             for i in range(j):                          # apply previous Givens rotations
                 t = cs[i] * H[i, j] + sn[i] * H[i + 1, j]
                 H[i + 1, j] = -sn[i] * H[i, j] + cs[i] * H[i + 1, j]
