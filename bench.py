@@ -382,7 +382,8 @@ def main():
                          "bytes_per_launch": sbytes, "avg_launch_us": avg_sweep_s * 1e6,
                          "launches_timed": n_timed,
                          "timing": "HIP events around each plain sweep of the first F solve on the apply stream"
-                                   + ", eager pass of the same K applies after the timed loop"},
+                                   + ", eager pass of the same K applies after the timed loop",
+                         "events": EVENT_NOTE},
             "roofline_second_f_solve": {
                 "bound": "hbm", "achieved": gbytes / g_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": gbytes / g_s / 1e9 / HBM_PEAK_GBS, "bytes_per_launch": gbytes, "avg_launch_us": g_s * 1e6,
@@ -397,7 +398,7 @@ def main():
                 "kernel": "k_csr_wave<EpiStore> (A u, 5N rows, CSR)", "bytes_per_launch": spmv["csr_bytes"],
                 "avg_launch_us": spmv["csr_us"],
                 "back_to_back_us": spmv["csr_us_graph"], "frac_back_to_back": spmv["csr_gbs_graph"] / HBM_PEAK_GBS,
-                "timing": spmv.get("timing", "") + " (one kernel per matvec)"},
+                "timing": spmv.get("timing", "") + " (one kernel per matvec)", "events": EVENT_NOTE},
             "mg_apply": mg_apply,
             "host_buffer_matvec": host_io,
             "solve_level": solve,
@@ -449,6 +450,12 @@ def single_gpu_check(dpc, n, args, iF, iP, rank, dist, torch):
                     f"vector (numpy seed 2048), built on each rank's GPU; {time.perf_counter() - t0:.1f} s"}
 
 
+EVENT_NOTE = ("hipEvents with a device-scope release (hipEventReleaseToDevice, mpbp_event_create_scoped): recording "
+              "one does not write the L2 back, so the kernel between a pair runs as inside the captured apply; "
+              "MPBP_EVENT_SCOPE=system: hipEventDefault") if os.environ.get("MPBP_EVENT_SCOPE", "device") != "system" \
+    else "hipEventDefault (system-scope release after every recorded event; MPBP_EVENT_SCOPE=system)"
+
+
 def spmv_bench(A, gen, reps=20, replays=10, warm_replays=5):
     """The plain operator matvec b = A u (apply.py:72) in both layouts, HIP-event timed.
 
@@ -458,6 +465,7 @@ def spmv_bench(A, gen, reps=20, replays=10, warm_replays=5):
     (`*_us_graph`: per launch including the drain / dispatch gap between dependent kernels), and the eager
     loop (`*_us_eager`)."""
     import torch
+    from mp_block_preconditioners_amd.solve import DeviceEvent
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     x = torch.randn(A.shape[1], dtype=torch.float64, device="cuda", generator=gen)
     y = torch.empty(A.shape[0], dtype=torch.float64, device="cuda")
@@ -513,13 +521,13 @@ def spmv_bench(A, gen, reps=20, replays=10, warm_replays=5):
             del g
         except Exception as e:   # eager number only, and say why
             res[f"{name}_graph_note"] = f"graph capture failed: {e}"
-        pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        pairs = [(DeviceEvent(), DeviceEvent()) for _ in range(reps)]
         for a, b in pairs:   # right after the graph replays: the clock is settled
             a.record()
             M.matvec(x, out=y)
             b.record()
         torch.cuda.synchronize()
-        s_launch = sum(a.elapsed_time(b) for a, b in pairs) / 1e3 / reps
+        s_launch = sum(a.elapsed_ms(b) for a, b in pairs) / 1e3 / reps
         res.update({f"{name}_gbs": nbytes / s_launch / 1e9, f"{name}_us": s_launch * 1e6, f"{name}_bytes": nbytes,
                     f"{name}_us_graph": s * 1e6, f"{name}_gbs_graph": nbytes / s / 1e9,
                     f"{name}_us_eager": s_eager * 1e6})
@@ -536,6 +544,7 @@ def mg_apply_bench(F, D, G, steps, warmup, gen, reps=20):
     import torch
     import mp_block_preconditioners_amd as mp
     from mp_block_preconditioners_amd._lib import check, lib, ptr, stream_handle
+    from mp_block_preconditioners_amd.solve import DeviceEvent
     t0 = time.perf_counter()
     pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("mg", 1), inner_P=mp.InnerSolver("mg", 1))
     torch.cuda.synchronize()
@@ -569,13 +578,13 @@ def mg_apply_bench(F, D, G, steps, warmup, gen, reps=20):
                                             None, ptr(xo), stream_handle()))
     for _ in range(3):
         sweep()
-    pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    pairs = [(DeviceEvent(), DeviceEvent()) for _ in range(reps)]
     for a, e in pairs:
         a.record()
         sweep()
         e.record()
     torch.cuda.synchronize()
-    us = sum(a.elapsed_time(e) for a, e in pairs) * 1e3 / reps
+    us = sum(a.elapsed_ms(e) for a, e in pairs) * 1e3 / reps
     rows = M1.shape[0]
     # per row x (gathered, counted once), b, diag, d read, d written, x_out (8 B each); the matrix: stencil values 8 B
     # per entry (edge rows: their CSR entries, 12 B, + 4 B row_ptr), or SELL 12 B per entry + 1 B row length + 16 B
@@ -593,7 +602,8 @@ def mg_apply_bench(F, D, G, steps, warmup, gen, reps=20):
             "roofline": {"bound": "hbm", "achieved": nbytes / us / 1e3, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": nbytes / us / 1e3 / HBM_PEAK_GBS, "kernel": kname, "bytes_per_launch": nbytes,
                          "avg_launch_us": us, "launches_per_apply": 8,
-                         "timing": f"mean of HIP event pairs around each of {reps} launches on the level's buffers"}}
+                         "timing": f"mean of HIP event pairs around each of {reps} launches on the level's buffers",
+                         "events": EVENT_NOTE}}
 
 
 SOLVE_CASES = (   # (n, eta_n, eta_s, preconditioners): BASELINE configs[1] / configs[3] at 256^2, configs[2] / [3] at 1024^2

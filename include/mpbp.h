@@ -490,6 +490,12 @@ int mpbp_scatter(int32_t count, const int32_t* idx, const double* src, double* d
 
 /* hipEvent helpers for callers without a HIP binding (bench profiling). */
 int mpbp_event_create(void** ev);
+/* device_scope = 1: the event's release is device scope (hipEventReleaseToDevice) -- recording it does not write
+ * the L2 back to memory, so a kernel timed between two such events runs as it does inside the captured apply (a
+ * system-scope release after every sweep drains the dirty L2 the next sweep would have read); 0: hipEventDefault. */
+int mpbp_event_create_scoped(void** ev, int32_t device_scope);
+/* hipEventRecord on `stream` (NULL: the default stream); skipped while the stream is capturing. */
+int mpbp_event_record(void* ev, void* stream);
 int mpbp_event_destroy(void* ev);
 int mpbp_event_elapsed_ms(void* start, void* stop, float* ms);
 

@@ -174,6 +174,8 @@ _SIGNATURES = {
     "mpbp_gather": ([c_int32, _P, _P, _P, _P], c_int),
     "mpbp_scatter": ([c_int32, _P, _P, _P, _P], c_int),
     "mpbp_event_create": ([POINTER(c_void_p)], c_int),
+    "mpbp_event_create_scoped": ([POINTER(c_void_p), c_int32], c_int),
+    "mpbp_event_record": ([c_void_p, c_void_p], c_int),
     "mpbp_event_destroy": ([_P], c_int),
     "mpbp_event_elapsed_ms": ([_P, _P, POINTER(ctypes.c_float)], c_int),
     "mpbp_gs_dot": ([_P, c_int64, c_int32, _P, c_int64, _P, _P, _P], c_int),

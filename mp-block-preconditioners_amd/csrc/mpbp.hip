@@ -3095,6 +3095,20 @@ int mpbp_event_create(void** ev) {
     return MPBP_OK;
 }
 
+int mpbp_event_create_scoped(void** ev, int32_t device_scope) {
+    hipEvent_t e;
+    MPBP_HIP(hipEventCreateWithFlags(&e, device_scope ? hipEventReleaseToDevice : hipEventDefault));
+    *ev = (void*)e;
+    return MPBP_OK;
+}
+
+int mpbp_event_record(void* ev, void* stream) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    MPBP_HIP(hipStreamIsCapturing(as_stream(stream), &cs));
+    if (cs == hipStreamCaptureStatusNone) MPBP_HIP(hipEventRecord((hipEvent_t)ev, as_stream(stream)));
+    return MPBP_OK;
+}
+
 int mpbp_event_destroy(void* ev) {
     MPBP_HIP(hipEventDestroy((hipEvent_t)ev));
     return MPBP_OK;

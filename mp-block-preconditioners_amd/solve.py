@@ -13,6 +13,7 @@ native call (``mpbp_schur_apply``) that is graph-capturable.
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 from dataclasses import dataclass
 
@@ -74,6 +75,36 @@ def _device_csr(M, device):
     return M if isinstance(M, DeviceCSR) else DeviceCSR.from_scipy(M, device)
 
 
+def event_device_scope() -> int:
+    """1 (default): profiling events release at device scope (mpbp_event_create_scoped), so recording one between two
+    sweeps does not write the L2 back to HBM and the timed sweep runs as it does inside the captured apply;
+    MPBP_EVENT_SCOPE=system restores hipEventDefault."""
+    return 0 if os.environ.get("MPBP_EVENT_SCOPE", "device") == "system" else 1
+
+
+class DeviceEvent:
+    """A timing hipEvent from libmpbp (device-scope release by default, event_device_scope)."""
+
+    def __init__(self):
+        self.h = ctypes.c_void_p()
+        check(lib().mpbp_event_create_scoped(ctypes.byref(self.h), event_device_scope()))
+
+    def record(self, stream=None):
+        check(lib().mpbp_event_record(self.h, stream if stream is not None else stream_handle()))
+
+    def elapsed_ms(self, end: "DeviceEvent") -> float:
+        ms = ctypes.c_float(0.0)
+        check(lib().mpbp_event_elapsed_ms(self.h, end.h, ctypes.byref(ms)))
+        return ms.value
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().mpbp_event_destroy(self.h)
+        except Exception:
+            pass
+
+
 class PlanProfiling:
     """hipEvent pairs recorded by mpbp_schur_apply around every inner-F SpMV sweep (bench.py)."""
 
@@ -81,7 +112,7 @@ class PlanProfiling:
         evs = (ctypes.c_void_p * (2 * capacity))()
         for i in range(2 * capacity):
             e = ctypes.c_void_p()
-            check(lib().mpbp_event_create(ctypes.byref(e)))
+            check(lib().mpbp_event_create_scoped(ctypes.byref(e), event_device_scope()))
             evs[i] = e
         cnt = ctypes.c_int32(0)
         self._prof = (evs, cnt, capacity)
