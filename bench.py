@@ -137,6 +137,8 @@ def main():
                     help="skip the solve-level section (FGMRES to 1e-8 on the manufactured problem, N = 1)")
     ap.add_argument("--partitioned-graph", action="store_true",
                     help="(kept for old command lines: the default for RCCL ranks)")
+    ap.add_argument("--global-products", action="store_true",
+                    help="N > 1: every rank forms the whole Gt_G / Gt_F_G (the default forms its own pressure rows)")
     ap.add_argument("--eager-partitioned", action="store_true",
                     help="N > 1: launch the partitioned apply eagerly instead of replaying its hipGraph")
     args = ap.parse_args()
@@ -210,7 +212,8 @@ def main():
         pc = DistributedSchurPreconditioner(n, args.xi, args.eta_n, args.eta_s, inner_F=iF, inner_P=iP,
                                             layout=args.layout, f_mode=args.f_mode, pg_mode=args.pg_mode,
                                             self_halo=args.self_halo, halo_overlap=args.halo_overlap,
-                                            ca=False if args.no_ca else "auto", fuse_g=not args.no_fuse_g)
+                                            ca=False if args.no_ca else "auto", fuse_g=not args.no_fuse_g,
+                                            local_products=not args.global_products)
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup   # assembly, products, layouts, halo plans (the partitioned: per rank)
     gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
@@ -358,6 +361,8 @@ def main():
                                    f"{cfg}" + (")" if world == 1 else f", rows partitioned over {world} ranks)"),
                        "applies_per_s_of_this_grid": args.steps / dt,
                        "setup_seconds": setup_s,
+                       **({"commutator_products": "rank-local rows" if getattr(pc, "local_products", False)
+                           else "global"} if world > 1 else {}),
                        "n": n, "unknowns": 5 * n * n, "xi": args.xi, "eta_n": args.eta_n,
                        "eta_s": args.eta_s, "inner_F": f"{kf}:{sf}", "inner_P": f"{kp}:{spp}",
                        "parallelism": f"rows{world}" if world > 1 else "single", "layout": args.layout,

@@ -35,7 +35,8 @@ import torch
 
 from . import _lib
 from ._lib import check, lib, ptr, stream_handle
-from .csr import DeviceCSR
+from .csr import DeviceCSR, spgemm
+from .preconditioner import PGStencil
 from .solve import PlanProfiling, _capture, _pg_stencil
 
 N_VEL_FIELDS = 4
@@ -113,6 +114,27 @@ class RowPartition:
         for f in range(nfields):
             cm[f * N + self.r0 * n: f * N + self.r1 * n] = f * L * n + np.arange(L * n, dtype=np.int32)
         return cm
+
+
+def _row_diagonal(M, row_gid: torch.Tensor) -> torch.Tensor:
+    """Diagonal of a row subset of an operator with global columns (row i of M is global row row_gid[i])."""
+    counts = (M.row_ptr[1:] - M.row_ptr[:-1]).to(torch.int64)
+    owner = torch.repeat_interleave(torch.arange(M.shape[0], device=M.col_idx.device), counts)
+    hit = M.col_idx.to(torch.int64) == row_gid.to(torch.int64)[owner]
+    d = torch.zeros(M.shape[0], dtype=torch.float64, device=M.val.device)
+    d[owner[hit]] = M.val[hit]
+    if int(hit.sum()) != M.shape[0]:
+        raise _lib.MpbpError("rank-local product: a row has no diagonal entry")
+    return d
+
+
+def _gtg_stencil(D, G):
+    """The matrix-free Gt_G policy of the global product (commutator_products), for a rank-local product."""
+    sd, sg = getattr(D, "stencil", None), getattr(G, "stencil", None)
+    if isinstance(sd, PGStencil) and sd.op == _lib.PG_D and isinstance(sg, PGStencil) and sg.op == _lib.PG_G \
+            and sd.same_grid(sg):
+        return PGStencil(sd.prm, sd.cell, _lib.PG_GTG)
+    return None
 
 
 def halo_reach(row_ptr: torch.Tensor, col_idx: torch.Tensor, row_gid: torch.Tensor, n: int) -> int:
@@ -608,7 +630,8 @@ class DistributedSchurPreconditioner(PlanProfiling):
 
     def __init__(self, n, xi, eta_n, eta_s, c=1.0, d_u=-1.0, inner_F=None, inner_P=None, group=None,
                  device=None, layout="sell", f_mode="auto", pg_mode="auto", halo="auto", self_halo=False,
-                 halo_overlap=False, ca="auto", fuse_g=True, mg_min_cells=1 << 14, mg_part_levels=None):
+                 halo_overlap=False, ca="auto", fuse_g=True, mg_min_cells=1 << 14, mg_part_levels=None,
+                 local_products=True):
         import torch.distributed as dist
         from .preconditioner import MultiphaseBlockPreconditioner
         from .solve import InnerSolver
@@ -626,27 +649,49 @@ class DistributedSchurPreconditioner(PlanProfiling):
         self.halo_impl = halo if halo != "auto" else ("rccl" if backend == "nccl" else "torch")
         bp = MultiphaseBlockPreconditioner(n, xi, eta_n, eta_s, device=dev)
         _, _, F, D, G = bp.get_big_A_matrix(c=c, d_u=d_u)
-        GtG, GtFG = bp.commutator_products(F, D, G)
+        rows_u = torch.from_numpy(part.owned_rows(N_VEL_FIELDS).astype(np.int32)).to(dev)
+        rows_p = torch.from_numpy(part.owned_rows(N_P_FIELDS).astype(np.int32)).to(dev)
+        mg_req = "mg" in ((inner_F or InnerSolver()).kind, (inner_P or InnerSolver()).kind)
+        # the commutator products: with Jacobi / Chebyshev inner solves only this rank's pressure rows of Gt_G and
+        # Gt_F_G (a product's row depends on that row of D alone: the same bits as the global product's row, for a
+        # 1 / world share of the SpGEMM work); multigrid builds its Galerkin hierarchy from the whole Gt_G
+        self.local_products = bool(local_products) and not mg_req and world > 1
+        if self.local_products:
+            D_own = D.extract(rows_p, torch.arange(D.shape[1], dtype=torch.int32, device=dev), D.shape[1])
+            GtG, GtFG = bp.commutator_products(F, D_own, G)
+            GtG.stencil = _gtg_stencil(D, G)
+            del D_own
+        else:
+            GtG, GtFG = bp.commutator_products(F, D, G)
         if f_mode not in ("auto", "stencil", "assembled"):
             raise ValueError("f_mode must be 'auto', 'stencil' or 'assembled'")
         if f_mode == "stencil" and F.stencil is None:
             raise ValueError("f_mode='stencil' needs n >= 3")
         self.f_stencil = F.stencil if f_mode in ("auto", "stencil") else None
         self.pg_stencil = _pg_stencil(D, G, GtG, self.f_stencil, pg_mode)
-        # inner-solver bounds from the global operators: identical on every rank
+        # inner-solver bounds from the global operators: identical on every rank (with rank-local products, Gt_G's
+        # Gershgorin bound is the maximum of the ranks' row bounds: the same maximum, exactly)
         self.inner_F = (inner_F or InnerSolver()).resolve(F, F.diagonal())
-        self.inner_P = (inner_P or InnerSolver()).resolve(GtG, GtG.diagonal())
+        if self.local_products:
+            ip = inner_P or InnerSolver()
+            if ip.kind == "chebyshev" and ip.lmax is None:
+                lmax = GtG.gershgorin(_row_diagonal(GtG, rows_p))
+                t = torch.tensor([lmax], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+                ip = InnerSolver("chebyshev", ip.sweeps, ip.lmin, float(t.item()), ip.ratio)
+            self.inner_P = ip.resolve(GtG, None)
+        else:
+            self.inner_P = (inner_P or InnerSolver()).resolve(GtG, GtG.diagonal())
         mg_any = "mg" in (self.inner_F.kind, self.inner_P.kind)
-        rows_u = torch.from_numpy(part.owned_rows(N_VEL_FIELDS).astype(np.int32)).to(dev)
-        rows_p = torch.from_numpy(part.owned_rows(N_P_FIELDS).astype(np.int32)).to(dev)
 
-        def reach(M, rows):
-            sub = M.extract(rows, torch.arange(M.shape[1], dtype=torch.int32, device=dev), M.shape[1])
+        def reach(M, rows, local=False):
+            sub = M if local else M.extract(rows, torch.arange(M.shape[1], dtype=torch.int32, device=dev), M.shape[1])
             return halo_reach(sub.row_ptr, sub.col_idx, rows, n)
 
-        q = reach(GtFG, rows_p)
+        lp = self.local_products
+        q = reach(GtFG, rows_p, lp)
         self.h_u = max(1, reach(F, rows_u), reach(D, rows_p))
-        self.h_p = max(1, reach(G, rows_u), reach(GtG, rows_p), q)
+        self.h_p = max(1, reach(G, rows_u), reach(GtG, rows_p, lp), q)
         # multigrid inner solves: the global hierarchies (every rank, setup only), split over the partition; level 0's
         # ghost layout must also serve the restriction's reach
         self.mg_F = self.mg_P = None
@@ -687,12 +732,24 @@ class DistributedSchurPreconditioner(PlanProfiling):
         cm_u = torch.from_numpy(part.colmap(N_VEL_FIELDS, self.h_u)).to(dev)
         cm_p = torch.from_numpy(part.colmap(N_P_FIELDS, self.h_p)).to(dev)
         if self.ca:
-            diag_F_glob, diag_P_glob = F.diagonal(), GtG.diagonal()
+            gp_rows = torch.from_numpy(part.ext_rows(N_P_FIELDS, self.h_p).astype(np.int32)).to(dev)
+            diag_F_glob = F.diagonal()
+            if lp:   # Gt_G's diagonal on the owned + ghost pressure rows, from those rows of the product alone
+                D_ext = D.extract(gp_rows, torch.arange(D.shape[1], dtype=torch.int32, device=dev), D.shape[1])
+                self.diag_P_ext = _row_diagonal(spgemm(D_ext, G, alpha=-1.0), gp_rows)
+                del D_ext
+            else:
+                diag_P_glob = GtG.diagonal()
         self.F = F.extract(rows_u, cm_u, nu_ext)
         self.D = D.extract(rows_p, cm_u, nu_ext)
         self.G = G.extract(rows_u, cm_p, np_ext)
-        self.GtG = GtG.extract(rows_p, cm_p, np_ext)
-        self.GtFG = GtFG.extract(rows_p, cm_p, np_ext)
+        if lp:   # already this rank's rows, in owned order
+            own = torch.arange(GtG.shape[0], dtype=torch.int32, device=dev)
+            self.GtG = GtG.extract(own, cm_p, np_ext)
+            self.GtFG = GtFG.extract(own, cm_p, np_ext)
+        else:
+            self.GtG = GtG.extract(rows_p, cm_p, np_ext)
+            self.GtFG = GtFG.extract(rows_p, cm_p, np_ext)
         del F, D, G, GtG, GtFG, bp
         torch.cuda.empty_cache()
         self.nu, self.np, self.nu_ext, self.np_ext = nu, np_, nu_ext, np_ext
@@ -701,10 +758,12 @@ class DistributedSchurPreconditioner(PlanProfiling):
         self.diag_P = self.GtG.diagonal()
         if self.ca:   # diagonals on owned + ghost rows (the CA schedule's ghost-row sweeps stage x0 = b / diag)
             gu = torch.from_numpy(part.ext_rows(N_VEL_FIELDS, self.h_u)).to(dev)
-            gp = torch.from_numpy(part.ext_rows(N_P_FIELDS, self.h_p)).to(dev)
             self.diag_F_ext = diag_F_glob[gu].contiguous()
-            self.diag_P_ext = diag_P_glob[gp].contiguous()
-            del diag_F_glob, diag_P_glob
+            if not lp:
+                gp = torch.from_numpy(part.ext_rows(N_P_FIELDS, self.h_p)).to(dev)
+                self.diag_P_ext = diag_P_glob[gp].contiguous()
+                del diag_P_glob
+            del diag_F_glob
 
         mats = {"F": (self.F, nu), "D": (self.D, nu), "G": (self.G, np_), "P": (self.GtG, np_),
                 "Q": (self.GtFG, np_)}
