@@ -53,6 +53,15 @@ extern "C" {
 #define MPBP_SPMV_STORE 0  /* y = A x          */
 #define MPBP_SPMV_ADD 1    /* y = A x + z      */
 #define MPBP_SPMV_RESID 2  /* y = z - A x      */
+/* OR'ed into mpbp_f_stencil_spmv's mode: the tolerance-mode F rows (MPBP_NUMERICS_FAST below) */
+#define MPBP_SPMV_FAST 0x100
+
+/* Numerics of the matrix-free F sweeps (mpbp_schur_plan.f_numerics).  EXACT: every row performs the assembly's IEEE
+ * operations in CSR order (bit-identical to the sequential oracle).  FAST: the same operator with its rows regrouped
+ * per coefficient and FMA-contracted, reciprocal diagonals (v_rcp_f64 + 2 Newton steps) -- north_star's bar, within
+ * 1e-12 relative inf-norm of the oracle apply; ~4x fewer fp64 VALU operations per row. */
+#define MPBP_NUMERICS_EXACT 0
+#define MPBP_NUMERICS_FAST 1
 
 /* inner solvers of the approximate Schur preconditioner */
 #define MPBP_INNER_JACOBI 0
@@ -277,6 +286,8 @@ typedef struct mpbp_schur_plan {
     int32_t fuse_g;                  /* 1 (one GPU, f_stencil and pg_stencil, Chebyshev F solve of >= 2 sweeps): the
                                         second F solve recomputes its right-hand side G x_p inside each sweep (no G
                                         launch, W never stored; bit-identical) */
+    int32_t f_numerics;              /* MPBP_NUMERICS_EXACT (0, default) or MPBP_NUMERICS_FAST: the matrix-free F
+                                        sweeps' rows (inner solves, multigrid level 0 smoothing and residuals) */
 } mpbp_schur_plan;
 
 const char* mpbp_version(void);
@@ -462,6 +473,14 @@ typedef struct mpbp_halo mpbp_halo;
 int mpbp_rccl_unique_id(const char* rccl_path, uint8_t* id_out);
 int mpbp_halo_create(const char* rccl_path, const uint8_t* id, int32_t world, int32_t rank, int32_t n,
                      int32_t r0, int32_t rows, int32_t h_u, int32_t h_p, mpbp_halo** out);
+/* Another halo object (its own kinds 0 / 1 for the given layout, buffers and stream) on base's communicator: one RCCL
+ * communicator per process group, reference-counted (released with its last object, unless captured -- see
+ * mpbp_halo_destroy).  Local: no collective.  Replaces a second mpbp_halo_create on the same group. */
+int mpbp_halo_create_shared(const mpbp_halo* base, int32_t n, int32_t r0, int32_t rows, int32_t h_u, int32_t h_p,
+                            mpbp_halo** out);
+/* The object's communicator (an opaque identity, for checks) and how many halo objects hold it. */
+const void* mpbp_halo_comm(const mpbp_halo* halo);
+int mpbp_halo_comm_refs(const mpbp_halo* halo);
 void mpbp_halo_destroy(mpbp_halo* halo);
 void mpbp_halo_exchange(void* halo, int32_t vec_kind, double* x_ext, int32_t phase, void* stream);
 int mpbp_halo_status(const mpbp_halo* halo);

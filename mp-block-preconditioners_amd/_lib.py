@@ -13,6 +13,8 @@ LIB_PATH = os.environ.get("MPBP_LIB") or os.path.join(HERE, "lib", "libmpbp.so")
 OP_A, OP_F, OP_D, OP_G = 0, 1, 2, 3
 OP_L_N, OP_L_S, OP_D_N, OP_D_S, OP_G_N, OP_G_S, OP_XI_N, OP_XI_S = range(4, 12)
 SPMV_STORE, SPMV_ADD, SPMV_RESID = 0, 1, 2
+SPMV_FAST = 0x100                     # mpbp_f_stencil_spmv: tolerance-mode F rows
+NUMERICS_EXACT, NUMERICS_FAST = 0, 1  # mpbp_schur_plan.f_numerics
 INNER_JACOBI, INNER_CHEBYSHEV, INNER_MG = 0, 1, 2
 MG_CELL, MG_NODE = 0, 1
 MG_P, MG_R = 0, 1
@@ -102,7 +104,7 @@ class SchurPlan(Structure):
                 ("halo_first", c_int32), ("ca", c_int32), ("ca_reach_q", c_int32), ("wu_ext", c_void_p),
                 ("diag_F_ext", c_void_p), ("diag_P_ext", c_void_p), ("halo_pair", HALO_PAIR_FN),
                 ("q13", c_void_p), ("q13_n", c_int32), ("mg_F", POINTER(Mg)), ("mg_P", POINTER(Mg)),
-                ("fuse_g", c_int32)]
+                ("fuse_g", c_int32), ("f_numerics", c_int32)]
 
 
 _P = c_void_p
@@ -148,6 +150,9 @@ _SIGNATURES = {
     "mpbp_rccl_unique_id": ([ctypes.c_char_p, _P], c_int),
     "mpbp_halo_create": ([ctypes.c_char_p, _P, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                           POINTER(c_void_p)], c_int),
+    "mpbp_halo_create_shared": ([_P, c_int32, c_int32, c_int32, c_int32, c_int32, POINTER(c_void_p)], c_int),
+    "mpbp_halo_comm": ([_P], c_void_p),
+    "mpbp_halo_comm_refs": ([_P], c_int),
     "mpbp_halo_destroy": ([_P], None),
     "mpbp_halo_exchange": ([_P, c_int32, _P, c_int32, _P], None),
     "mpbp_halo_exchange_pair": ([_P, _P, _P, _P], None),

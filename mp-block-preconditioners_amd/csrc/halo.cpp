@@ -30,10 +30,13 @@
 // RCCL is resolved at run time (dlopen of the library the caller names -- the one torch loaded, so the
 // process holds one RCCL), which keeps libmpbp free of a link-time RCCL dependency.
 //
-// Communicators: every halo object opens its own.  A communicator whose point-to-point kernels were captured
-// into a hipGraph is not destroyed (see mpbp_halo_destroy): with RCCL 2.26.6 ncclCommDestroy then never
-// returns.  Sharing one communicator between a captured apply and eager exchanges of another object would
-// interleave graph-replayed and eager operations on the same peer connections, so objects do not share.
+// Communicators: one per process group.  mpbp_halo_create opens it; mpbp_halo_create_shared gives another halo
+// object (its own vector kinds, buffers and stream) the same communicator, reference-counted -- the partitioned
+// operator and the partitioned preconditioner of one FGMRES solve hold one communicator per rank.  Every exchange is
+// issued on the caller's stream in program order, which is the same on every rank, so graph-replayed (the captured
+// preconditioner) and eager (the operator) operations on the communicator stay in one consistent order.  A
+// communicator whose point-to-point kernels were captured into a hipGraph is not destroyed when its last halo object
+// goes (see mpbp_halo_destroy): with RCCL 2.26.6 ncclCommDestroy then never returns.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -115,18 +118,25 @@ struct GatherKind {
     int32_t* full_idx = nullptr;   // device: nf * n * n
 };
 
+// A communicator shared by the halo objects of one process group (refs: the objects holding it).
+struct SharedComm {
+    ncclComm_t comm = nullptr;
+    int refs = 0;
+    bool captured = false;   // an exchange was recorded into a hipGraph (stream capture) on this communicator
+};
+
 }  // namespace
 
 struct mpbp_halo {
     Rccl rccl;
-    ncclComm_t comm = nullptr;
+    SharedComm* shared = nullptr;
+    ncclComm_t comm = nullptr;   // == shared->comm
     int world = 0, rank = 0, up = 0, down = 0;
     std::vector<Kind> kinds;
     std::vector<GatherKind> gathers;
     hipStream_t stream = nullptr;
     int default_mode = MPBP_HALO_IN_ORDER;
     int status = MPBP_OK;  // first error seen by mpbp_halo_exchange (its signature returns nothing)
-    bool captured = false; // an exchange was recorded into a hipGraph (stream capture) with this communicator
     char err[512] = "";
 };
 
@@ -146,6 +156,8 @@ int upload_idx(const std::vector<int32_t>& v, int32_t** out) {
         return halo_error(MPBP_ERR_HIP, "halo: index upload failed");
     return MPBP_OK;
 }
+
+int halo_init_local(mpbp_halo* H, int n, int r0, int rows, int h_u, int h_p);
 
 int make_kind(mpbp_halo* H, int nf, int n, int r0, int rows, int h, int mode) {
     if (nf < 1 || n < 1 || rows < 1 || r0 < 0 || h < 1 || h > rows || (int64_t)2 * nf * h * n > INT32_MAX ||
@@ -219,12 +231,57 @@ int mpbp_halo_create(const char* rccl_path, const uint8_t* id, int32_t world, in
     H->down = (rank + 1) % world;
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof(uid));
-    const ncclResult_t e = H->rccl.comm_init_rank(&H->comm, world, uid, rank);
+    H->shared = new (std::nothrow) SharedComm();
+    if (!H->shared) {
+        delete H;
+        return halo_error(MPBP_ERR_ARG, "halo_create: out of host memory");
+    }
+    const ncclResult_t e = H->rccl.comm_init_rank(&H->shared->comm, world, uid, rank);
     if (e != ncclSuccess) {
         halo_error(MPBP_ERR_HIP, "ncclCommInitRank: %s", H->rccl.error_string(e));
+        delete H->shared;
         delete H;
         return MPBP_ERR_HIP;
     }
+    H->shared->refs = 1;
+    H->comm = H->shared->comm;
+    const int rc2 = halo_init_local(H, n, r0, rows, h_u, h_p);
+    if (rc2) return rc2;
+    *out = H;
+    return MPBP_OK;
+}
+
+int mpbp_halo_create_shared(const mpbp_halo* base, int32_t n, int32_t r0, int32_t rows, int32_t h_u, int32_t h_p,
+                            mpbp_halo** out) {
+    if (!base || !base->shared || !out || n < 1 || rows < 1 || r0 < 0 || r0 + rows > n || h_u < 1 || h_p < 1 ||
+        h_u > rows || h_p > rows)
+        return halo_error(MPBP_ERR_ARG, "halo_create_shared: bad arguments (n %d r0 %d rows %d h %d/%d)", n, r0, rows,
+                          h_u, h_p);
+    mpbp_halo* H = new (std::nothrow) mpbp_halo();
+    if (!H) return halo_error(MPBP_ERR_ARG, "halo_create_shared: out of host memory");
+    H->rccl = base->rccl;
+    H->world = base->world;
+    H->rank = base->rank;
+    H->up = base->up;
+    H->down = base->down;
+    H->shared = base->shared;
+    H->comm = base->shared->comm;
+    ++H->shared->refs;
+    const int rc = halo_init_local(H, n, r0, rows, h_u, h_p);
+    if (rc) return rc;
+    *out = H;
+    return MPBP_OK;
+}
+
+const void* mpbp_halo_comm(const mpbp_halo* H) { return H && H->shared ? (const void*)H->shared->comm : nullptr; }
+
+int mpbp_halo_comm_refs(const mpbp_halo* H) { return H && H->shared ? H->shared->refs : 0; }
+
+}  // extern "C"
+
+namespace {
+// The object's own stream and the Schur apply's two vector kinds; on failure the object is destroyed.
+int halo_init_local(mpbp_halo* H, int n, int r0, int rows, int h_u, int h_p) {
     // The group's kernel is launched next to the interior sweep, which fills every CU: on a
     // highest-priority stream it is dispatched first instead of waiting for the sweep to drain.
     int least = 0, greatest = 0;
@@ -237,9 +294,11 @@ int mpbp_halo_create(const char* rccl_path, const uint8_t* id, int32_t world, in
         mpbp_halo_destroy(H);
         return halo_error(MPBP_ERR_HIP, "halo_create: stream / event / buffer creation failed");
     }
-    *out = H;
     return MPBP_OK;
 }
+}  // namespace
+
+extern "C" {
 
 int mpbp_halo_add_kind(mpbp_halo* H, int32_t nfields, int32_t n, int32_t r0, int32_t rows, int32_t h, int32_t mode) {
     if (!H) return halo_error(MPBP_ERR_ARG, "halo_add_kind: null halo");
@@ -312,10 +371,14 @@ void mpbp_halo_destroy(mpbp_halo* H) {
     // been instantiated and destroyed (measured: tools/capture_probe.py).  It is
     // released with the process instead (MPBP_HALO_CAPTURED_DESTROY=abort tries ncclCommAbort,
     // =destroy the plain destroy).
-    if (H->comm) {
-        const char* pol = std::getenv("MPBP_HALO_CAPTURED_DESTROY");
-        if (!H->captured || (pol && std::strcmp(pol, "destroy") == 0)) H->rccl.comm_destroy(H->comm);
-        else if (pol && std::strcmp(pol, "abort") == 0) H->rccl.comm_abort(H->comm);
+    if (H->shared && --H->shared->refs == 0) {   // the last object of the process group
+        SharedComm* sc = H->shared;
+        if (sc->comm) {
+            const char* pol = std::getenv("MPBP_HALO_CAPTURED_DESTROY");
+            if (!sc->captured || (pol && std::strcmp(pol, "destroy") == 0)) H->rccl.comm_destroy(sc->comm);
+            else if (pol && std::strcmp(pol, "abort") == 0) H->rccl.comm_abort(sc->comm);
+        }
+        delete sc;
     }
     // the RCCL library stays loaded: torch (or another communicator) may still use it
     delete H;
@@ -365,7 +428,7 @@ ncclResult_t halo_ops(mpbp_halo* H, const HaloBufs& b, hipStream_t on) {
 
 void note_capture(mpbp_halo* H, hipStream_t on) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(on, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) H->captured = true;
+    if (hipStreamIsCapturing(on, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) H->shared->captured = true;
 }
 
 ncclResult_t halo_group(mpbp_halo* H, const Kind& K, double* x_ext, hipStream_t on) {

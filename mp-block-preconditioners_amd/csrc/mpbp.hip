@@ -774,7 +774,9 @@ struct EpiResid {
 // `store_d` (the direction is stored except on a solve's last sweep).  The marching kernels get them as
 // template flags instead (FIXED = true; launch_march picks the instance): no load or store then sits under
 // a branch (the compiler's wait counts stay exact) and the unused operand costs no registers.
-template <bool FIXED = false, bool SUB = true>
+// RCP (tolerance-mode F policy only, FStencilFast): the diagonal handed over by set_diag is its reciprocal, so the
+// update multiplies instead of dividing.
+template <bool FIXED = false, bool SUB = true, bool RCP = false>
 struct EpiJacobiT {   // x = (b - R x)/D in residual form (solve.py:158)
     const double* xin;
     const double* b;
@@ -788,14 +790,14 @@ struct EpiJacobiT {   // x = (b - R x)/D in residual form (solve.py:158)
     __device__ P pre_lite(int32_t r) const { return {0.0, ld_stream(b + r), 0.0, has_sub() ? ld_stream(sub + r) : 0.0}; }
     template <bool NT = false>
     __device__ void apply(int32_t r, double acc, const P& p) const {
-        const double x = p.x + (p.b - acc) / p.dg;
+        const double x = p.x + (RCP ? (p.b - acc) * p.dg : (p.b - acc) / p.dg);
         st_stream<NT>(xout + r, has_sub() ? p.s - x : x);
     }
     __device__ void operator()(int32_t r, double acc, const P& p) const { apply<false>(r, acc, p); }
 };
 // BX (FIXED instances of the marching kernels only): b is not loaded -- the kernel recomputes it per row and hands
 // it over with set_b (the second F solve's right-hand side W = G x_p, solve.py:273-274, never stored).
-template <bool FIXED = false, bool SUB = true, bool SD = true, bool BX = false>
+template <bool FIXED = false, bool SUB = true, bool SD = true, bool BX = false, bool RCP = false>
 struct EpiChebT {
     const double* xin;
     const double* b;
@@ -819,7 +821,7 @@ struct EpiChebT {
     __device__ P pre_lite(int32_t r) const { return {0.0, BX ? 0.0 : ld_stream(b + r), 0.0, ld_stream(d + r), (has_sub() && !kSubLate) ? ld_stream(sub + r) : 0.0}; }
     template <bool NT = false>
     __device__ void apply(int32_t r, double acc, const P& p) const {
-        const double z = (p.b - acc) / p.dg;
+        const double z = RCP ? (p.b - acc) * p.dg : (p.b - acc) / p.dg;
         const double dn = c1 * p.d + c2 * z;
         if (stores_d()) st_stream<NT>(d + r, dn);
         const double x = p.x + dn;
@@ -830,7 +832,7 @@ struct EpiChebT {
 };
 // EpiCheb for the first sweep after x0 = d0 = c2[0] b / diag: the previous direction is the staged x0
 // itself (x and diag supplied by the stencil via set_x / set_diag), so d is written but not read.
-template <bool FIXED = false, bool SUB = true, bool SD = true, bool BX = false>
+template <bool FIXED = false, bool SUB = true, bool SD = true, bool BX = false, bool RCP = false>
 struct EpiChebFirstT {
     const double* b;
     double* d;
@@ -845,7 +847,7 @@ struct EpiChebFirstT {
     __device__ P pre_lite(int32_t r) const { return {0.0, BX ? 0.0 : ld_stream(b + r), 0.0, has_sub() ? ld_stream(sub + r) : 0.0}; }
     template <bool NT = false>
     __device__ void apply(int32_t r, double acc, const P& p) const {
-        const double z = (p.b - acc) / p.dg;
+        const double z = RCP ? (p.b - acc) * p.dg : (p.b - acc) / p.dg;
         const double dn = c1 * p.x + c2 * z;
         if (stores_d()) st_stream<NT>(d + r, dn);
         const double x = p.x + dn;
@@ -857,46 +859,56 @@ using EpiJacobi = EpiJacobiT<>;
 using EpiCheb = EpiChebT<>;
 using EpiChebFirst = EpiChebFirstT<>;
 
-// Run fn with the epilogue's run-time switches turned into template flags (other epilogues unchanged).
-template <class Epi, class Fn>
+// Run fn with the epilogue's run-time switches turned into template flags (other epilogues unchanged).  RCP: the
+// stencil hands over the reciprocal diagonal (FStencilFast), the solver epilogues multiply by it.
+template <bool RCP = false, class Epi, class Fn>
 __host__ inline int with_fixed_epi(const Epi& e, Fn&& fn) { return fn(e); }
-template <class Fn>
+template <bool RCP = false, class Fn>
 __host__ inline int with_fixed_epi(const EpiJacobi& e, Fn&& fn) {
-    return e.sub ? fn(EpiJacobiT<true, true>{e.xin, e.b, e.diag, e.sub, e.xout})
-                 : fn(EpiJacobiT<true, false>{e.xin, e.b, e.diag, e.sub, e.xout});
+    return e.sub ? fn(EpiJacobiT<true, true, RCP>{e.xin, e.b, e.diag, e.sub, e.xout})
+                 : fn(EpiJacobiT<true, false, RCP>{e.xin, e.b, e.diag, e.sub, e.xout});
 }
-template <class Fn>
+template <bool RCP = false, class Fn>
 __host__ inline int with_fixed_epi(const EpiCheb& e, Fn&& fn) {
-#define MPBP_CHEB(SUB, SD) fn(EpiChebT<true, SUB, SD>{e.xin, e.b, e.diag, e.d, e.c1, e.c2, e.sub, e.xout, e.store_d})
+#define MPBP_CHEB(SUB, SD) fn(EpiChebT<true, SUB, SD, false, RCP>{e.xin, e.b, e.diag, e.d, e.c1, e.c2, e.sub, e.xout, e.store_d})
     return e.sub ? (e.store_d ? MPBP_CHEB(true, true) : MPBP_CHEB(true, false))
                  : (e.store_d ? MPBP_CHEB(false, true) : MPBP_CHEB(false, false));
 #undef MPBP_CHEB
 }
-template <class Fn>
+template <bool RCP = false, class Fn>
 __host__ inline int with_fixed_epi(const EpiChebFirst& e, Fn&& fn) {
-#define MPBP_CHEBF(SUB, SD) fn(EpiChebFirstT<true, SUB, SD>{e.b, e.d, e.c1, e.c2, e.sub, e.xout, e.store_d})
+#define MPBP_CHEBF(SUB, SD) fn(EpiChebFirstT<true, SUB, SD, false, RCP>{e.b, e.d, e.c1, e.c2, e.sub, e.xout, e.store_d})
     return e.sub ? (e.store_d ? MPBP_CHEBF(true, true) : MPBP_CHEBF(true, false))
                  : (e.store_d ? MPBP_CHEBF(false, true) : MPBP_CHEBF(false, false));
 #undef MPBP_CHEBF
 }
 
 // The same, with b supplied by the kernel (BX): the F sweeps of the second F solve with W = G x_p recomputed.
-template <class Epi, class Fn>
+template <bool RCP = false, class Epi, class Fn>
 __host__ inline int with_fixed_epi_bx(const Epi& e, Fn&& fn) { return set_error(MPBP_ERR_ARG, "no BX epilogue"); }
-template <class Fn>
+template <bool RCP = false, class Fn>
 __host__ inline int with_fixed_epi_bx(const EpiCheb& e, Fn&& fn) {
-#define MPBP_CHEB(SUB, SD) fn(EpiChebT<true, SUB, SD, true>{e.xin, e.b, e.diag, e.d, e.c1, e.c2, e.sub, e.xout, e.store_d})
+#define MPBP_CHEB(SUB, SD) fn(EpiChebT<true, SUB, SD, true, RCP>{e.xin, e.b, e.diag, e.d, e.c1, e.c2, e.sub, e.xout, e.store_d})
     return e.sub ? (e.store_d ? MPBP_CHEB(true, true) : MPBP_CHEB(true, false))
                  : (e.store_d ? MPBP_CHEB(false, true) : MPBP_CHEB(false, false));
 #undef MPBP_CHEB
 }
-template <class Fn>
+template <bool RCP = false, class Fn>
 __host__ inline int with_fixed_epi_bx(const EpiChebFirst& e, Fn&& fn) {
-#define MPBP_CHEBF(SUB, SD) fn(EpiChebFirstT<true, SUB, SD, true>{e.b, e.d, e.c1, e.c2, e.sub, e.xout, e.store_d})
+#define MPBP_CHEBF(SUB, SD) fn(EpiChebFirstT<true, SUB, SD, true, RCP>{e.b, e.d, e.c1, e.c2, e.sub, e.xout, e.store_d})
     return e.sub ? (e.store_d ? MPBP_CHEBF(true, true) : MPBP_CHEBF(true, false))
                  : (e.store_d ? MPBP_CHEBF(false, true) : MPBP_CHEBF(false, false));
 #undef MPBP_CHEBF
 }
+
+// Epilogues a tolerance-mode policy may feed: those that ignore the diagonal, and the RCP solver epilogues.
+template <class E> struct RcpOk : std::false_type {};
+template <> struct RcpOk<EpiStore> : std::true_type {};
+template <> struct RcpOk<EpiAdd> : std::true_type {};
+template <> struct RcpOk<EpiResid> : std::true_type {};
+template <bool S> struct RcpOk<EpiJacobiT<true, S, true>> : std::true_type {};
+template <bool S, bool D, bool B> struct RcpOk<EpiChebT<true, S, D, B, true>> : std::true_type {};
+template <bool S, bool D, bool B> struct RcpOk<EpiChebFirstT<true, S, D, B, true>> : std::true_type {};
 
 // XI entry xi * a * (1 - a) as the assembly evaluates it (left to right).
 __device__ inline double xi_of(double xi, double a) { return xi * a * (1.0 - a); }
@@ -1580,6 +1592,7 @@ __device__ inline int32_t ext_row(int nf, int f, int lr, int L, int h, int n) {
 }
 
 struct FStencilDev {
+    static constexpr bool kFast = false;   // FStencilFast: tolerance-mode rows (rows4 / rdiag4, reciprocal diagonals)
     int n;
     double xi, eta_n, eta_s, c, d_u;
     const double* cell;
@@ -1976,6 +1989,7 @@ template <class S, class XS, class Epi, class BS = BNone>
 __global__ void __launch_bounds__(kMB) __attribute__((amdgpu_waves_per_eu(4, 8)))
 k_march(S P, XS xs, int nchunks, Epi epi, BS bs = BS{}) {
     constexpr int NF = S::NF, NO = S::NOUT;
+    static_assert(!S::kFast || RcpOk<Epi>::value, "a tolerance-mode policy hands over reciprocal diagonals");
     __shared__ double sx[NF * 3 * kMTileW];
     __shared__ double st[3 * kMTileW];
     const int n = P.n;
@@ -2028,6 +2042,17 @@ k_march(S P, XS xs, int nchunks, Epi epi, BS bs = BS{}) {
             const int gr = P.wrap(P.r0 + lr);
             const XRing xa{sx, {sm, s0, sp}, gr, c0};
             const TRing ta{st, {sm, s0, sp}, gr, c0};
+            if constexpr (S::kFast) {   // tolerance mode: the cell's rows at once, reciprocal diagonals
+                double acc[NO], rd[NO];
+                P.rows4(gr, gc, ta, xa, cl, acc, rd);
+#pragma unroll
+                for (int o = 0; o < NO; ++o) {
+                    set_diag(pe[o], rd[o]);
+                    set_x(pe[o], xa.X(o, gr, gc));
+                    if constexpr (BS::on) set_b(pe[o], bs.b(o, gr, gc, gc, ta, bq));
+                    epi(P.out_row(o, lr, gc), acc[o], pe[o]);
+                }
+            } else {
             // the wrap-aware (sorting) form is exact for interior cells too: take it for the whole wave when
             // any of its cells is on the periodic edge, so a wave never runs both forms
             const bool edge = __builtin_amdgcn_readfirstlane(__any(gr == 0 || gr == n - 1 || gc == 0 || gc == n - 1)) != 0;
@@ -2040,6 +2065,7 @@ k_march(S P, XS xs, int nchunks, Epi epi, BS bs = BS{}) {
                 set_x(pe[o], xa.X(S::NF == 1 ? 0 : o, gr, gc));
                 if constexpr (BS::on) set_b(pe[o], bs.b(o, gr, gc, gc, ta, bq));
                 epi(P.out_row(o, lr, gc), acc, pe[o]);
+            }
             }
         }
         __syncthreads();                                     // slot sm is rewritten next step
@@ -2169,6 +2195,30 @@ __device__ inline void store_init_row(const S& P, double c2, double* sx, const d
                                       int gr, int c0, int tid, int colA, bool okA, const HaloCols& hc,
                                       const InitRow<S::NF, typename S::Stage, BS>& tr, const BS& bs) {
     const TRingT<kTW, 2> ta{st, {ts[0], ts[1], ts[2]}, gr, c0};
+    if constexpr (S::kFast) {   // tolerance mode: x0 = c2 b (1 / diag), the four reciprocal diagonals at once
+        double rd[4];
+        P.rdiag4(gr, colA, ta, tr.sa, rd);
+#pragma unroll
+        for (int f = 0; f < S::NF; ++f) {
+            double bf;
+            if constexpr (BS::on) bf = bs.b(f, gr, colA, P.wrap(colA), ta, tr.qa);
+            else bf = tr.xa[f];
+            sx[(f * 3 + slot) * kMTileW + tid] = okA ? c2 * bf * rd[f] : 0.0;
+        }
+        if (tid < 2) {
+            const bool ok = tid == 0 ? hc.ok0 : hc.ok1;
+            const int col = c0 + kMB - 1 + tid;
+            P.rdiag4(gr, col, ta, tr.sh, rd);
+#pragma unroll
+            for (int f = 0; f < S::NF; ++f) {
+                double bf;
+                if constexpr (BS::on) bf = bs.b(f, gr, col, P.wrap(col), ta, tr.qh);
+                else bf = tr.h0[f];
+                sx[(f * 3 + slot) * kMTileW + kMB + tid] = ok ? c2 * bf * rd[f] : 0.0;
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int f = 0; f < S::NF; ++f) {
         const double dg = P.stage_diag(f, gr, colA, ta, tr.sa);
@@ -2195,6 +2245,7 @@ template <class S, class Epi, class BS = BNone>
 __global__ void __launch_bounds__(kMB) __attribute__((amdgpu_waves_per_eu(4, 8)))
 k_march_init(S P, const double* __restrict__ b, double c2, int nchunks, Epi epi, BS bs = BS{}) {
     constexpr int NF = S::NF, NO = S::NOUT;
+    static_assert(!S::kFast || RcpOk<Epi>::value, "a tolerance-mode policy hands over reciprocal diagonals");
     __shared__ double sx[NF * 3 * kMTileW];
     __shared__ double st[5 * kTW];
     const int n = P.n;
@@ -2257,7 +2308,21 @@ k_march_init(S P, const double* __restrict__ b, double c2, int nchunks, Epi epi,
             load_thn_row(P, P.r0 + lr + 3, colA, tid, c0, tn);
             load_init_row(P, b, P.r0 + lr + 2, gcA, okA, hc, tr, bs);
         }
-        if (live) {
+        if constexpr (S::kFast) if (live) {
+            const int gr = grow(lr);
+            const XRing xa{sx, {xslot(lr - 1), xslot(lr), xslot(lr + 1)}, gr, c0};
+            const TRingT<kTW, 2> ta{st, {tslot(lr - 1), tslot(lr), tslot(lr + 1)}, gr, c0};
+            double acc[NO], rd[NO];
+            P.rows4(gr, gc, ta, xa, cl, acc, rd);
+#pragma unroll
+            for (int o = 0; o < NO; ++o) {
+                set_diag(pe[o], rd[o]);
+                set_x(pe[o], xa.X(o, gr, gc));
+                if constexpr (BS::on) set_b(pe[o], bs.b(o, gr, gc, gc, ta, bq));
+                epi(P.out_row(o, lr, gc), acc[o], pe[o]);
+            }
+        }
+        if constexpr (!S::kFast) if (live) {
             const int gr = grow(lr);
             const XRing xa{sx, {xslot(lr - 1), xslot(lr), xslot(lr + 1)}, gr, c0};
             const TRingT<kTW, 2> ta{st, {tslot(lr - 1), tslot(lr), tslot(lr + 1)}, gr, c0};
@@ -2355,15 +2420,15 @@ int launch_march_init(const S& P, const double* b, double c2, Epi epi, int rows_
         MPBP_HIP(hipGetLastError());
         return (int)MPBP_OK;
     };
-    if constexpr (BS::on) return with_fixed_epi_bx(epi, go);
-    else return with_fixed_epi(epi, go);
+    if constexpr (BS::on) return with_fixed_epi_bx<S::kFast>(epi, go);
+    else return with_fixed_epi<S::kFast>(epi, go);
 }
 
 template <class S, class XS, class Epi, class BS = BNone>
 int launch_march(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStream_t st, const BS& bs = BS{}) {
     auto go = [&](const auto& e) { return launch_march_fixed(P, xs, e, rows_per_block, st, bs); };
-    if constexpr (BS::on) return with_fixed_epi_bx(epi, go);
-    else return with_fixed_epi(epi, go);
+    if constexpr (BS::on) return with_fixed_epi_bx<S::kFast>(epi, go);
+    else return with_fixed_epi<S::kFast>(epi, go);
 }
 
 // F row of field f at a cell (k_march policy).
@@ -2387,6 +2452,108 @@ struct FStencilDevM : FStencilDev {
     }
 };
 
+// ---- tolerance-mode F (plan numerics "fast"): north_star's 1e-12 bar instead of the assembly's bits ----
+// The same operator with its four rows per cell regrouped around the phase-n thn at the cell centres and at the grid
+// nodes (corner K(r, c): the average of the four cells around the node between rows r-1, r and columns c-1, c;
+// phase s uses 1 - t), FMA-contracted.  With a = d_u eta idx2 and -d_u xi h (1 - h) the XI coupling (h: the face
+// average), a u row (left / right cells A1 = T(r, c-1), A2 = T(r, c), nodes KN = K(r, c), KS = K(r+1, c)) is
+//   F u = wt u_C - d_u xi_h (u_C - u_o) + a [KN (u_N - u_C + v2 - v1) + A1 (u_W - u_C + v1 - v3)
+//                                           + A2 (u_E - u_C + v4 - v2) + KS (u_S - u_C + v3 - v4)]
+// (v1..v4 = v(r, c-1), v(r, c), v(r+1, c-1), v(r+1, c)), diag = wt - d_u xi_h - a (A1 + A2 + KN + KS) -- the
+// entries of preconditioner.py:100-179 collected per coefficient; a v row (:182-295) likewise with B1 = T(r-1, c),
+// B2 = T(r, c), KW = K(r, c), KE = K(r, c+1) and u1..u4 = u(r-1, c), u(r-1, c+1), u(r, c), u(r, c+1).  Per row
+// about 40 fp64 VALU operations (corners once per cell, a reciprocal diagonal by v_rcp_f64 and two Newton steps)
+// instead of ~170 for the bit-exact rows; every value stays within a few ulp of the assembled row (numpy check:
+// 3e-16 of max |F x|).  No periodic sorting: the sum has no order to reproduce.
+__device__ inline double rcp_nr(double y) {
+    double r = __builtin_amdgcn_rcp(y);
+    double e = __builtin_fma(-y, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-y, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
+struct FStencilFast : FStencilDev {
+    static constexpr bool kFast = true;
+    struct Nb { double nw, nn, ne, w, c, e, sw, s; };   // phase-n thn around (r, c) (the 3 x 3 block minus (r+1, c+1))
+    template <class TA>
+    __device__ static Nb nb(const TA& ta, int gr, int gc) {
+        return {ta.T(0, gr - 1, gc - 1), ta.T(0, gr - 1, gc), ta.T(0, gr - 1, gc + 1), ta.T(0, gr, gc - 1),
+                ta.T(0, gr, gc), ta.T(0, gr, gc + 1), ta.T(0, gr + 1, gc - 1), ta.T(0, gr + 1, gc)};
+    }
+    // per-cell coefficients, phase n: A1 = w, A2 = B2 = c, B1 = nn; nodes kc = K(r, c), ks = K(r+1, c), ke = K(r, c+1)
+    struct Co { double w, c, nn, kc, ks, ke, xu, xv; };
+    __device__ Co coeffs(const Nb& t) const {
+        const double wc = t.w + t.c;
+        Co k;
+        k.w = t.w; k.c = t.c; k.nn = t.nn;
+        k.kc = 0.25 * ((t.nw + t.nn) + wc);
+        k.ks = 0.25 * (wc + (t.sw + t.s));
+        k.ke = 0.25 * ((t.nn + t.ne) + (t.c + t.e));
+        const double hu = 0.5 * wc, hv = 0.5 * (t.nn + t.c);
+        const double mx = -d_u * xi;             // -d_u xi h (1 - h): the same for both phases (h_s = 1 - h_n)
+        k.xu = mx * (hu * (1.0 - hu));
+        k.xv = mx * (hv * (1.0 - hv));
+        return k;
+    }
+    __device__ double aco(int p) const { return d_u * (p ? eta_s : eta_n) * idx2; }
+    // the four rows (u_n, v_n, u_s, v_s) of cell (gr, gc) and their reciprocal diagonals
+    template <class TA, class XA>
+    __device__ void rows4(int gr, int gc, const TA& ta, const XA& xa, const Cell& cl, double* acc, double* rd) const {
+        const Co k = coeffs(nb(ta, gr, gc));
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int fu = 2 * p, fv = 2 * p + 1;
+            auto ph = [&](double t) { return p ? 1.0 - t : t; };
+            const double a = aco(p);
+            const double A1 = ph(k.w), A2 = ph(k.c), B1 = ph(k.nn), KC = ph(k.kc), KS = ph(k.ks), KE = ph(k.ke);
+            const double uC = xa.X(fu, gr, gc), uN = xa.X(fu, gr - 1, gc), uS = xa.X(fu, gr + 1, gc);
+            const double uW = xa.X(fu, gr, gc - 1), uE = xa.X(fu, gr, gc + 1), uNE = xa.X(fu, gr - 1, gc + 1);
+            const double vC = xa.X(fv, gr, gc), vN = xa.X(fv, gr - 1, gc), vS = xa.X(fv, gr + 1, gc);
+            const double vW = xa.X(fv, gr, gc - 1), vE = xa.X(fv, gr, gc + 1), vSW = xa.X(fv, gr + 1, gc - 1);
+            const double uo = xa.X(fu ^ 2, gr, gc), vo = xa.X(fv ^ 2, gr, gc);
+            // u row: v1 = vW, v2 = vC, v3 = vSW, v4 = vS
+            double br = KC * ((uN - uC) + (vC - vW));
+            br = __builtin_fma(A1, (uW - uC) + (vW - vSW), br);
+            br = __builtin_fma(A2, (uE - uC) + (vS - vC), br);
+            br = __builtin_fma(KS, (uS - uC) + (vSW - vS), br);
+            const double wu = c * ph(cl.face[0]);
+            acc[fu] = __builtin_fma(a, br, __builtin_fma(wu, uC, k.xu * (uC - uo)));
+            rd[fu] = rcp_nr(__builtin_fma(-a, (A1 + A2) + (KC + KS), wu + k.xu));
+            // v row: u1 = uN, u2 = uNE, u3 = uC, u4 = uE
+            double bv = B1 * ((vN - vC) + (uN - uNE));
+            bv = __builtin_fma(KC, (vW - vC) + (uC - uN), bv);
+            bv = __builtin_fma(KE, (vE - vC) + (uNE - uE), bv);
+            bv = __builtin_fma(A2, (vS - vC) + (uE - uC), bv);
+            const double wv = c * ph(cl.face[1]);
+            acc[fv] = __builtin_fma(a, bv, __builtin_fma(wv, vC, k.xv * (vC - vo)));
+            rd[fv] = rcp_nr(__builtin_fma(-a, (B1 + A2) + (KC + KE), wv + k.xv));
+        }
+    }
+    // the reciprocal diagonals of the four rows at a staged point (k_march_init: x0 = c2 b / diag)
+    template <class TA>
+    __device__ void rdiag4(int gr, int gc, const TA& ta, const Stage& sg, double* rd) const {
+        const Co k = coeffs(nb(ta, gr, gc));
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            auto ph = [&](double t) { return p ? 1.0 - t : t; };
+            const double a = aco(p);
+            const double A1 = ph(k.w), A2 = ph(k.c), B1 = ph(k.nn), KC = ph(k.kc), KS = ph(k.ks), KE = ph(k.ke);
+            rd[2 * p] = rcp_nr(__builtin_fma(-a, (A1 + A2) + (KC + KS), c * ph(sg.face[0]) + k.xu));
+            rd[2 * p + 1] = rcp_nr(__builtin_fma(-a, (B1 + A2) + (KC + KE), c * ph(sg.face[1]) + k.xv));
+        }
+    }
+};
+
+// Calls fn with the F policy the plan's numerics select: the tolerance-mode rows (fast) or the bit-exact rows
+// specialised for P's parameter identities.
+template <class Fn>
+int with_f_identities(const FStencilDev& P, Fn&& fn);
+template <class Fn>
+int with_f_policy(const FStencilDev& P, bool fast, Fn&& fn) {
+    if (fast) return fn(FStencilFast{P});
+    return with_f_identities(P, fn);
+}
+
 // Calls fn with the F policy specialised for P's parameters (M = 0: none apply).
 template <class Fn>
 int with_f_identities(const FStencilDev& P, Fn&& fn) {
@@ -2407,6 +2574,7 @@ int with_f_identities(const FStencilDev& P, Fn&& fn) {
 // order, then scaled by alpha = -1) and summed in CSR column order -- the assembled operators' results
 // bit for bit.  Needs n >= 3 (distinct periodic neighbours).
 struct PGDev {
+    static constexpr bool kFast = false;
     int n;
     const double* cell;
     double d_p, inv, minv;   // d_p, 1.0 / dx, -1.0 / dx  (dx == dy; evaluated as the assembly does)
@@ -3524,8 +3692,8 @@ static int make_fstencil(const mpbp_stokes_params* prm, const double* cell, cons
 
 namespace {
 template <class Epi>
-int launch_fstencil(const FStencilDev& P, const double* x, Epi epi, hipStream_t st) {
-    return with_f_identities(P, [&](const auto& Q) { return launch_march(Q, XPlain{x}, epi, g_march_rows, st); });
+int launch_fstencil(const FStencilDev& P, const double* x, Epi epi, hipStream_t st, bool fast = false) {
+    return with_f_policy(P, fast, [&](const auto& Q) { return launch_march(Q, XPlain{x}, epi, g_march_rows, st); });
 }
 
 }  // namespace
@@ -3538,35 +3706,44 @@ int mpbp_f_stencil_spmv(const mpbp_stokes_params* prm, const double* cell, const
     FStencilDev P;
     int rc = make_fstencil(prm, cell, uface, vface, part, &P);
     if (rc) return rc;
+    const bool fast = (mode & MPBP_SPMV_FAST) != 0;
+    mode &= ~MPBP_SPMV_FAST;
     if (!x || !y || (mode != MPBP_SPMV_STORE && !z)) return set_error(MPBP_ERR_ARG, "f_stencil_spmv: bad vectors");
     const hipStream_t st = as_stream(stream);
     switch (mode) {
-    case MPBP_SPMV_STORE: return launch_fstencil(P, x, EpiStore{y}, st);
-    case MPBP_SPMV_ADD: return launch_fstencil(P, x, EpiAdd{z, y}, st);
-    case MPBP_SPMV_RESID: return launch_fstencil(P, x, EpiResid{z, y}, st);
+    case MPBP_SPMV_STORE: return launch_fstencil(P, x, EpiStore{y}, st, fast);
+    case MPBP_SPMV_ADD: return launch_fstencil(P, x, EpiAdd{z, y}, st, fast);
+    case MPBP_SPMV_RESID: return launch_fstencil(P, x, EpiResid{z, y}, st, fast);
     default: return set_error(MPBP_ERR_ARG, "f_stencil_spmv: unknown mode %d", mode);
     }
+}
+
+static int f_stencil_jacobi_impl(const mpbp_stokes_params* prm, const double* cell, const double* uface,
+                                 const double* vface, const mpbp_row_part* part, const double* x_in,
+                                 const double* b, const double* sub, double* x_out, void* stream, bool fast) {
+    FStencilDev P;
+    int rc = make_fstencil(prm, cell, uface, vface, part, &P);
+    if (rc) return rc;
+    if (!x_in || !b || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "f_stencil_jacobi_step: bad vectors");
+    return launch_fstencil(P, x_in, EpiJacobi{x_in, b, nullptr, sub, x_out}, as_stream(stream), fast);
 }
 
 int mpbp_f_stencil_jacobi_step(const mpbp_stokes_params* prm, const double* cell, const double* uface,
                                const double* vface, const mpbp_row_part* part, const double* x_in,
                                const double* b, const double* sub, double* x_out, void* stream) {
-    FStencilDev P;
-    int rc = make_fstencil(prm, cell, uface, vface, part, &P);
-    if (rc) return rc;
-    if (!x_in || !b || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "f_stencil_jacobi_step: bad vectors");
-    return launch_fstencil(P, x_in, EpiJacobi{x_in, b, nullptr, sub, x_out}, as_stream(stream));
+    return f_stencil_jacobi_impl(prm, cell, uface, vface, part, x_in, b, sub, x_out, stream, false);
 }
 
 static int f_stencil_cheb_impl(const mpbp_stokes_params* prm, const double* cell, const double* uface,
                                const double* vface, const mpbp_row_part* part, const double* x_in,
                                const double* b, double c1, double c2, double* d, const double* sub,
-                               double* x_out, void* stream, int store_d) {
+                               double* x_out, void* stream, int store_d, bool fast = false) {
     FStencilDev P;
     int rc = make_fstencil(prm, cell, uface, vface, part, &P);
     if (rc) return rc;
     if (!x_in || !b || !d || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "f_stencil_cheb_step: bad vectors");
-    return launch_fstencil(P, x_in, EpiCheb{x_in, b, nullptr, d, c1, c2, sub, x_out, store_d}, as_stream(stream));
+    return launch_fstencil(P, x_in, EpiCheb{x_in, b, nullptr, d, c1, c2, sub, x_out, store_d}, as_stream(stream),
+                           fast);
 }
 
 int mpbp_f_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell, const double* uface,
@@ -3862,7 +4039,9 @@ int op_spmv(const OpRef& o, int32_t mode, const double* x, const double* z, doub
         const mpbp_schur_plan* p = o.stencil;
         const mpbp_row_part q = stencil_part(o);
         if (o.sop == SOP_F)
-            return mpbp_f_stencil_spmv(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, mode, x, z, y, (void*)st);
+            return mpbp_f_stencil_spmv(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q,
+                                       mode | (p->f_numerics == MPBP_NUMERICS_FAST ? MPBP_SPMV_FAST : 0), x, z, y,
+                                       (void*)st);
         const int32_t op = o.sop == SOP_D ? MPBP_PG_D : o.sop == SOP_G ? MPBP_PG_G : MPBP_PG_GTG;
         return mpbp_pg_stencil_spmv(&p->f_prm, p->f_cell, &q, op, mode, x, z, y, (void*)st);
     }
@@ -3878,8 +4057,8 @@ int op_jacobi(const OpRef& o, const double* xin, const double* b, const double* 
         const mpbp_schur_plan* p = o.stencil;
         const mpbp_row_part q = stencil_part(o);
         if (o.sop == SOP_F)
-            return mpbp_f_stencil_jacobi_step(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, xin, b, sub, xo,
-                                              (void*)st);
+            return f_stencil_jacobi_impl(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, xin, b, sub, xo, (void*)st,
+                                         p->f_numerics == MPBP_NUMERICS_FAST);
         return mpbp_gtg_stencil_jacobi_step(&p->f_prm, p->f_cell, &q, xin, b, sub, xo, (void*)st);
     }
     return o.sell ? mpbp_sell_jacobi_step(o.sell, xin, b, dg, sub, xo, (void*)st)
@@ -3896,7 +4075,7 @@ int op_cheb(const OpRef& o, const double* xin, const double* b, const double* dg
         const mpbp_row_part q = stencil_part(o);
         if (o.sop == SOP_F)
             return f_stencil_cheb_impl(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, xin, b, c1, c2, d, sub,
-                                       xo, (void*)st, store_d);
+                                       xo, (void*)st, store_d, p->f_numerics == MPBP_NUMERICS_FAST);
         return gtg_stencil_cheb_impl(&p->f_prm, p->f_cell, &q, xin, b, c1, c2, d, sub, xo, (void*)st, store_d);
     }
     return o.sell ? sell_cheb_impl(o.sell, xin, b, dg, c1, c2, d, sub, xo, (void*)st, store_d)
@@ -3924,12 +4103,13 @@ int op_first_sweep(const OpRef& o, bool cheb, const double* b, const double* dia
         FStencilDev P;
         const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, &P);
         if (rc) return rc;
+        const bool fast = p->f_numerics == MPBP_NUMERICS_FAST;
         if (g_init_diag == 0)
-            return with_f_identities(P, [&](const auto& Q) {
+            return with_f_policy(P, fast, [&](const auto& Q) {
                 return cheb ? launch_march(Q, xs, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, g_march_rows, st)
                             : launch_march(Q, xs, EpiJacobi{nullptr, b, nullptr, sub, xo}, g_march_rows, st);
             });
-        return with_f_identities(P, [&](const auto& Q) {
+        return with_f_policy(P, fast, [&](const auto& Q) {
             return cheb ? launch_march_init(Q, b, xs.c2, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, g_march_rows, st)
                         : launch_march_init(Q, b, xs.c2, EpiJacobi{nullptr, b, nullptr, sub, xo}, g_march_rows, st);
         });
@@ -4340,7 +4520,7 @@ int f_solve_gx(const Ctx& c, const double* xp, const mpbp_inner_solver& in, doub
     if (rc) return rc;
     const GxB bs{xp, G.d_p, G.inv, G.minv, G.n};
     double* cur = K == 2 ? dst : pong;
-    rc = with_f_identities(P, [&](const auto& Q) {
+    rc = with_f_policy(P, p->f_numerics == MPBP_NUMERICS_FAST, [&](const auto& Q) {
         return launch_march_init(Q, nullptr, c2[0], EpiChebFirst{nullptr, dir, c1[1], c2[1], K == 2 ? sub : nullptr, cur,
                                                                  K == 2 ? 0 : 1}, g_march_rows, c.st, bs);
     });
@@ -4352,7 +4532,7 @@ int f_solve_gx(const Ctx& c, const double* xp, const mpbp_inner_solver& in, doub
         const bool rec = profile && p->prof_events && p->prof_count && *p->prof_count < p->prof_capacity &&
                          hipStreamIsCapturing(c.st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone;
         if (rec) MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count], c.st));
-        rc = with_f_identities(P, [&](const auto& Q) {
+        rc = with_f_policy(P, p->f_numerics == MPBP_NUMERICS_FAST, [&](const auto& Q) {
             return launch_march(Q, XPlain{cur}, EpiCheb{cur, nullptr, nullptr, dir, c1[s], c2[s], last ? sub : nullptr,
                                                         nxt, last ? 0 : 1}, g_march_rows, c.st, bs);
         });
@@ -4444,7 +4624,7 @@ int ca_f_solve_gx(const Ctx& c, const double* xp, const mpbp_inner_solver& in, d
     FStencilDev P;
     if ((rc = fpol(K - 2, &P))) return rc;
     double* cur = K == 2 ? dst : pong;
-    rc = with_f_identities(P, [&](const auto& Q) {
+    rc = with_f_policy(P, p->f_numerics == MPBP_NUMERICS_FAST, [&](const auto& Q) {
         return launch_march_init(Q, nullptr, c2[0], EpiChebFirst{nullptr, dir, c1[1], c2[1], K == 2 ? sub : nullptr, cur,
                                                                  K == 2 ? 0 : 1}, g_march_rows, c.st, bs);
     });
@@ -4457,7 +4637,7 @@ int ca_f_solve_gx(const Ctx& c, const double* xp, const mpbp_inner_solver& in, d
                          hipStreamIsCapturing(c.st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone;
         if (rec) MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count], c.st));
         if ((rc = fpol(K - 1 - s, &P))) return rc;
-        rc = with_f_identities(P, [&](const auto& Q) {
+        rc = with_f_policy(P, p->f_numerics == MPBP_NUMERICS_FAST, [&](const auto& Q) {
             return launch_march(Q, XPlain{cur}, EpiCheb{cur, nullptr, nullptr, dir, c1[s], c2[s], last ? sub : nullptr,
                                                         nxt, last ? 0 : 1}, g_march_rows, c.st, bs);
         });

@@ -50,6 +50,7 @@ class RowPartition:
     rank: int
     ghosts: bool = False   # ghost slots even at world = 1 (the periodic self-exchange; tests the halo path)
     bounds: tuple | None = None   # explicit ((r0, rows) per rank); default: n split evenly (the first n % world +1)
+    allow_empty: bool = False     # coarse multigrid levels (level_partitions) may leave a rank without rows
 
     def __post_init__(self):
         self.ghosts = self.ghosts or self.world > 1
@@ -59,6 +60,11 @@ class RowPartition:
         self.bounds = tuple((int(a), int(b)) for a, b in self.bounds)
         if len(self.bounds) != self.world or sum(b for _, b in self.bounds) != self.n:
             raise ValueError(f"row bounds {self.bounds} do not cover the {self.n} grid rows once")
+        start = 0   # contiguous, in rank order, every rank at least one row (the halo and gather layouts assume it)
+        for k, (a, b) in enumerate(self.bounds):
+            if a != start or b < (0 if self.allow_empty else 1):
+                raise ValueError(f"row bounds {self.bounds}: rank {k} must start at row {start} and own >= 1 row")
+            start += b
         self.r0, self.L = self.bounds[self.rank]
         self.r1 = self.r0 + self.L
         self.min_rows = min(b for _, b in self.bounds)
@@ -69,7 +75,8 @@ class RowPartition:
         f = 1 << levels
         if self.n % f or any(a % f or b % f for a, b in self.bounds):
             return None
-        return RowPartition(self.n // f, self.world, self.rank, self.ghosts, tuple((a // f, b // f) for a, b in self.bounds))
+        return RowPartition(self.n // f, self.world, self.rank, self.ghosts, tuple((a // f, b // f) for a, b in self.bounds),
+                            allow_empty=True)
 
     @property
     def N(self):
@@ -266,7 +273,26 @@ class RcclHalo:
     The communicator is libmpbp's own (its unique id travels over `group`); world = 1 exchanges with
     itself (the periodic wrap)."""
 
-    def __init__(self, part: RowPartition, h_u: int, h_p: int, group=None, overlap: bool = False):
+    # one RCCL communicator per process group: the first RcclHalo of a group opens it (collective), later ones --
+    # the partitioned operator and preconditioner of one solve, the multigrid levels -- share it
+    # (mpbp_halo_create_shared, local), so a rank holds one communicator whatever it builds
+    _by_group: dict = {}
+
+    @staticmethod
+    def _group_key(part: RowPartition, group):
+        return (id(group) if group is not None else "WORLD", part.world, part.rank)
+
+    def __init__(self, part: RowPartition, h_u: int, h_p: int, group=None, overlap: bool = False, share: bool = True):
+        import weakref
+        key = self._group_key(part, group)
+        ref = RcclHalo._by_group.get(key) if share else None
+        base = ref() if ref is not None else None
+        if base is not None and base.handle:
+            self.handle = ctypes.c_void_p()
+            check(lib().mpbp_halo_create_shared(base.handle, part.n, part.r0, part.L, h_u, h_p,
+                                                ctypes.byref(self.handle)))
+            self._finish(overlap)
+            return
         path = rccl_library_path().encode()
         uid = (ctypes.c_uint8 * 128)()
         if part.world == 1:
@@ -283,6 +309,21 @@ class RcclHalo:
         self.handle = ctypes.c_void_p()
         check(lib().mpbp_halo_create(path, uid, part.world, part.rank, part.n, part.r0, part.L, h_u, h_p,
                                      ctypes.byref(self.handle)))
+        if share:
+            RcclHalo._by_group[key] = weakref.ref(self)
+        self._finish(overlap)
+
+    @property
+    def comm(self) -> int:
+        """Identity of the RCCL communicator this object exchanges over (mpbp_halo_comm)."""
+        return int(lib().mpbp_halo_comm(self.handle) or 0)
+
+    @property
+    def comm_refs(self) -> int:
+        """Halo objects of this process holding the same communicator."""
+        return int(lib().mpbp_halo_comm_refs(self.handle))
+
+    def _finish(self, overlap):
         check(lib().mpbp_halo_set_mode(self.handle, _lib.HALO_OVERLAP if overlap else _lib.HALO_IN_ORDER))
         self.overlap = overlap
         self.fn = _lib.HALO_FN(ctypes.cast(lib().mpbp_halo_exchange, ctypes.c_void_p).value)
@@ -352,16 +393,39 @@ class _Halos:
         for t in tensors:
             self._tensors[t.data_ptr()] = t
 
+    # ctypes prints and swallows an exception raised inside a callback, and the C apply would go on with stale ghost
+    # rows: the callbacks record the first failure instead, and check() raises it once the apply has returned (as
+    # RcclHalo.check does with mpbp_halo_status)
+    error = None
+
     def _halo(self, ctx, kind, x_ptr, phase, stream):
-        x = self._tensors[int(x_ptr)]
-        ex = self._ex[int(kind)]
-        if phase == _lib.HALO_BEGIN:
-            ex.begin(x)
-        else:
-            ex.end(x)
+        if self.error is not None:
+            return
+        try:
+            x = self._tensors[int(x_ptr)]
+            ex = self._ex[int(kind)]
+            if phase == _lib.HALO_BEGIN:
+                ex.begin(x)
+            else:
+                ex.end(x)
+        except BaseException as e:   # noqa: BLE001 -- re-raised by check()
+            self.error = e
 
     def _allgather(self, ctx, gid, own_ptr, full_ptr, stream):
-        self._gather[int(gid)].gather(self._tensors[int(own_ptr)], self._tensors[int(full_ptr)])
+        if self.error is not None:
+            return
+        try:
+            self._gather[int(gid)].gather(self._tensors[int(own_ptr)], self._tensors[int(full_ptr)])
+        except BaseException as e:   # noqa: BLE001
+            self.error = e
+
+    def check(self):
+        """Raise the first exception a host-staged exchange or gather hit during the last apply."""
+        if self.rccl is not None:
+            self.rccl.check()
+        if self.error is not None:
+            e, self.error = self.error, None
+            raise RuntimeError(f"halo exchange failed inside the apply: {type(e).__name__}: {e}") from e
 
 
 def level_partitions(part: RowPartition, sizes) -> list[RowPartition]:
@@ -371,7 +435,7 @@ def level_partitions(part: RowPartition, sizes) -> list[RowPartition]:
     for m in sizes[1:]:
         p = parts[-1]
         b = tuple(((a + 1) // 2, (a + L + 1) // 2 - (a + 1) // 2) for a, L in p.bounds)
-        parts.append(RowPartition(m, part.world, part.rank, part.ghosts, b))
+        parts.append(RowPartition(m, part.world, part.rank, part.ghosts, b, allow_empty=True))
     return parts
 
 
@@ -631,10 +695,11 @@ class DistributedSchurPreconditioner(PlanProfiling):
     def __init__(self, n, xi, eta_n, eta_s, c=1.0, d_u=-1.0, inner_F=None, inner_P=None, group=None,
                  device=None, layout="sell", f_mode="auto", pg_mode="auto", halo="auto", self_halo=False,
                  halo_overlap=False, ca="auto", fuse_g=True, mg_min_cells=1 << 14, mg_part_levels=None,
-                 local_products=True):
+                 local_products=True, numerics="exact"):
         import torch.distributed as dist
         from .preconditioner import MultiphaseBlockPreconditioner
-        from .solve import InnerSolver
+        from .solve import InnerSolver, _check_numerics
+        self.numerics = _check_numerics(numerics)
         dev = torch.device(device or "cuda")
         self.device = dev
         world = dist.get_world_size(group)
@@ -855,6 +920,7 @@ class DistributedSchurPreconditioner(PlanProfiling):
         p.halo_first = 1 if (self._rccl is not None and not self._rccl.overlap) else 0
         p.ca, p.ca_reach_q = (1 if self.ca else 0), self.ca_q
         p.fuse_g = 1 if self.fuse_g else 0
+        p.f_numerics = _lib.NUMERICS_FAST if self.numerics == "fast" else _lib.NUMERICS_EXACT
         if self.ca:
             if self._rccl is not None and not self._rccl.overlap:   # v's two halves in one RCCL group
                 p.halo_pair = self._rccl.pair_fn

@@ -44,9 +44,13 @@ class FStencil:
         self.prm = prm
         self.cell, self.uface, self.vface = tables
 
-    def matvec(self, x, out=None, mode=_lib.SPMV_STORE, z=None):
+    def matvec(self, x, out=None, mode=_lib.SPMV_STORE, z=None, numerics="exact"):
+        """y = F x (mode STORE), F x + z (ADD) or z - F x (RESID); numerics 'fast': the tolerance-mode rows."""
         if out is None:
             out = torch.empty(4 * self.prm.n * self.prm.n, dtype=torch.float64, device=x.device)
+        if numerics not in ("exact", "fast"):
+            raise ValueError("numerics must be 'exact' or 'fast'")
+        mode = int(mode) | (_lib.SPMV_FAST if numerics == "fast" else 0)
         check(lib().mpbp_f_stencil_spmv(ctypes.byref(self.prm), ptr(self.cell), ptr(self.uface), ptr(self.vface),
                                         None, mode, ptr(x), ptr(z), ptr(out), stream_handle()))
         return out

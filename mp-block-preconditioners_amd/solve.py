@@ -71,6 +71,19 @@ class InnerSolver:
         return _lib.InnerSolverC(kind, int(self.sweeps), float(self.lmin or 0.0), float(self.lmax or 0.0))
 
 
+NUMERICS = ("exact", "fast")
+
+
+def _check_numerics(numerics: str) -> str:
+    """'exact': the matrix-free F sweeps perform the assembly's IEEE operations in CSR order (bit-identical to the
+    sequential oracle); 'fast': the same operator regrouped per coefficient and FMA-contracted with reciprocal diagonals
+    (MPBP_NUMERICS_FAST), north_star's bar -- within 1e-12 relative inf-norm of the oracle apply.  Only the
+    matrix-free F rows change; every other kernel is the same in both."""
+    if numerics not in NUMERICS:
+        raise ValueError(f"numerics must be one of {NUMERICS}")
+    return numerics
+
+
 def _device_csr(M, device):
     return M if isinstance(M, DeviceCSR) else DeviceCSR.from_scipy(M, device)
 
@@ -213,8 +226,9 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
 
     def __init__(self, F, D, G, GtG=None, GtFG=None, inner_F: InnerSolver | None = None,
                  inner_P: InnerSolver | None = None, device=None, layout: str = "sell", f_mode: str = "auto",
-                 pg_mode: str = "auto", q_mode: str = "auto", fuse_g: bool = True):
+                 pg_mode: str = "auto", q_mode: str = "auto", fuse_g: bool = True, numerics: str = "exact"):
         dev = torch.device(device or (F.device if isinstance(F, DeviceCSR) else "cuda"))
+        self.numerics = _check_numerics(numerics)
         self.F, self.D, self.G = (_device_csr(M, dev) for M in (F, D, G))
         if GtG is None or GtFG is None:
             GtG, GtFG = MultiphaseBlockPreconditioner.commutator_products(self.F, self.D, self.G)
@@ -315,6 +329,7 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
         if self.mg_P is not None:
             p.mg_P = ctypes.pointer(self.mg_P.cstruct())
         p.fuse_g = 1 if self.fuse_g else 0
+        p.f_numerics = _lib.NUMERICS_FAST if self.numerics == "fast" else _lib.NUMERICS_EXACT
         return p
 
     def sell_of(self, key):
@@ -509,7 +524,18 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
     if kernels is None and not (b.is_cuda and b.dtype == torch.float64):
         raise TypeError("fgmres runs on CUDA float64 vectors (libmpbp kernels); there is no CPU fallback")
     n = b.numel()
-    maxiter = int(maxiter) if maxiter is not None else min(n, 200)
+    # the defaults follow the GLOBAL length (pyamg's min(n, 200) of the whole system): with a group every rank must run
+    # the same iterations -- a rank-local default would let one rank leave the loop while the others still wait in the
+    # inner products' all-reduces -- and the partitioned solve must stay the one-GPU solve bit for bit
+    n_glob = n
+    if group is not None and (maxiter is None or restrt is None):
+        import torch.distributed as dist
+        t = torch.tensor([n], dtype=torch.int64)
+        if dist.get_backend(group) == "nccl":
+            t = t.to(b.device)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        n_glob = int(t.item())
+    maxiter = int(maxiter) if maxiter is not None else min(n_glob, 200)
     m = int(restrt) if restrt is not None else maxiter
     if capture_M and M is not None and hasattr(M, "capture") and b.is_cuda:
         try:
@@ -595,7 +621,9 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
             K.amax(w, bnd[1:2])
             a = K.fold_sums(w, n, 1, w, bnd[1:2], bnd[1:2])
             hn_d = torch.sqrt((a[0:1] + a[1:2]) + a[2:3])    # _finish, then the norm, on the device
-            inv = torch.reciprocal(hn_d)
+            # an exact breakdown (hn == 0) makes V[j+1] zero rather than NaN: the speculative head(j+1) below then runs M
+            # and A on a finite vector (its result is discarded when the host sees hn == 0)
+            inv = torch.where(hn_d > 0, torch.reciprocal(hn_d), torch.zeros_like(hn_d))
             torch.mul(w, inv, out=V[j + 1])
             vb[j + 1:j + 2] = bnd[1:2] * inv * _VB_SLACK      # |fl(w_i inv)| <= fl(max|w| inv): rounding is monotone
             hbuf[: j + 5].copy_(torch.cat([hs, a[:3], hn_d]), non_blocking=on_gpu)

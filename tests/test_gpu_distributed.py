@@ -20,7 +20,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, layout, f_mode, kind, errfile, ca="auto", fuse_g=True):
+def _worker(rank, world, port, n, layout, f_mode, kind, errfile, ca="auto", fuse_g=True, numerics="exact"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         torch.cuda.set_device(0)
@@ -30,14 +30,16 @@ def _worker(rank, world, port, n, layout, f_mode, kind, errfile, ca="auto", fuse
         mpb.lib().mpbp_set_march_rows(kind)
         iF, iP = mpb.InnerSolver("chebyshev", 4), mpb.InnerSolver("chebyshev", 3)
         dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, layout=layout,
-                                             f_mode=f_mode, ca=ca, fuse_g=fuse_g)
+                                             f_mode=f_mode, ca=ca, fuse_g=fuse_g, numerics=numerics)
         assert dpc.fuse_g == bool(fuse_g and dpc.ca)
         assert (dpc.f_stencil is not None) == (f_mode != "assembled")
         if ca is True:
             assert dpc.ca and dpc.h_u == dpc.ca_q + 2 + 1 + 3, (dpc.h_u, dpc.ca_q)
         bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
         _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
-        pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, layout=layout, f_mode="assembled")
+        # the reference: the assembled one-GPU apply (exact numerics), or the one-GPU apply with the same fast rows
+        pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, layout=layout,
+                                           f_mode="assembled" if numerics == "exact" else "stencil", numerics=numerics)
         assert (pc.inner_F.lmin, pc.inner_F.lmax) == (dpc.inner_F.lmin, dpc.inner_F.lmax)
         v = torch.from_numpy(np.random.default_rng(5).standard_normal(pc.shape[0])).cuda()
         gids = torch.from_numpy(dpc.local_to_global_rows()).cuda()
@@ -85,6 +87,14 @@ def test_distributed_apply_ca_schedule(world, n, layout, ca, fuse_g, tmp_path):
     except Exception:
         msg = open(errfile).read() if os.path.exists(errfile) else ""
         pytest.fail(f"distributed worker failed:\n{msg}")
+
+
+@pytest.mark.parametrize("world,n,ca", [(2, 64, True), (3, 50, True), (2, 64, False)])
+def test_distributed_fast_numerics_matches_single_gpu(world, n, ca, tmp_path):
+    """Tolerance-mode F numerics under the row partition (the CA schedule's ghost-row sweeps and the per-sweep
+    schedule): the same fast rows per grid point, so the partitioned apply equals the one-GPU fast apply bit for bit."""
+    errfile = str(tmp_path / "err.txt")
+    _spawn(_worker, (world, _free_port(), n, "sell", "stencil", 4, errfile, ca, True, "fast"), world, errfile)
 
 
 def _self_halo_worker(_index, port, n, halo, f_mode, pg_mode, kind, graph, errfile, overlap=False, ca="auto",
@@ -377,6 +387,74 @@ def test_distributed_fgmres_matches_single_gpu(world, n, inner, maxiter, tmp_pat
     assert np.array_equal(got.view(np.uint64), x.view(np.uint64))
     if "mg" in inner[0]:
         assert info == 0
+
+
+def _shared_comm_worker(_index, port, n, errfile):
+    """solve_distributed over the RCCL self-exchange: the partitioned operator and preconditioner hold ONE
+    communicator (mpbp_halo_create_shared), and the solve with maxiter / restrt left at their defaults runs."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=0, world_size=1)
+        import mp_block_preconditioners_amd as mpb
+        from mp_block_preconditioners_amd.distributed import solve_distributed
+        res = solve_distributed(n, 1.0, 100.0, 1.0, inner_F=mpb.InnerSolver("mg", 1), inner_P=mpb.InnerSolver("mg", 1),
+                                tol=1e-8, self_halo=True, halo="rccl", mg_min_cells=0)
+        dA, M = res["A"], res["M"]
+        assert dA._rccl is not None and M._rccl is not None
+        assert dA._rccl.comm != 0 and dA._rccl.comm == M._rccl.comm, (dA._rccl.comm, M._rccl.comm)
+        assert M._rccl.comm_refs == 2, M._rccl.comm_refs
+        assert res["info"] == 0, (res["info"], len(res["residuals"]))
+        dA.close()
+        assert M._rccl.comm_refs == 1
+        M.close()
+        dist.destroy_process_group()
+    except BaseException as e:
+        with open(errfile, "a") as f:
+            f.write(f"{type(e).__name__}: {e}\n")
+        raise
+
+
+def test_solve_distributed_shares_one_communicator(tmp_path):
+    errfile = str(tmp_path / "err.txt")
+    _spawn(_shared_comm_worker, (_free_port(), 32, errfile), 1, errfile)
+
+
+def _default_maxiter_worker(rank, world, port, n, outdir, errfile):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import mp_block_preconditioners_amd as mpb
+        from mp_block_preconditioners_amd.distributed import solve_distributed
+        res = solve_distributed(n, 1.0, 100.0, 1.0, inner_F=mpb.InnerSolver("jacobi", 1),
+                                inner_P=mpb.InnerSolver("jacobi", 1), tol=1e-14, maxiter=None)
+        assert res["A"].n_own < 200   # the rank-local length is below pyamg's default cap of 200
+        np.save(os.path.join(outdir, f"hist_{rank}.npy"), np.asarray(res["residuals"]))
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:
+        with open(errfile, "a") as f:
+            f.write(f"rank {rank}: {type(e).__name__}: {e}\n")
+        raise
+
+
+def test_distributed_fgmres_default_maxiter(tmp_path):
+    """FGMRES's default maxiter / restart come from the GLOBAL length (min(n, 200)), identical on every
+    rank -- a rank-local default would leave one rank waiting in an all-reduce -- and equal to the one-GPU solve's."""
+    import mp_block_preconditioners_amd as mpb
+    n, world = 6, 2
+    errfile = str(tmp_path / "err.txt")
+    _spawn(_default_maxiter_worker, (world, _free_port(), n, str(tmp_path), errfile), world, errfile)
+    bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=mpb.InnerSolver("jacobi", 1), inner_P=mpb.InnerSolver("jacobi", 1))
+    _, b = mpb.manufactured_problem(n, 1.0, -1.0, 1.0, 100.0, 1.0)
+    hist = []
+    mpb.fgmres(A, torch.from_numpy(b).cuda(), M=pc, tol=1e-14, residuals=hist)
+    for r in range(world):
+        h = np.load(os.path.join(str(tmp_path), f"hist_{r}.npy"))
+        assert np.array_equal(h, np.asarray(hist)), (r, len(h), len(hist))
 
 
 def _configs4_worker(rank, world, port, n, errfile):

@@ -94,7 +94,11 @@ step() {
             -o pmc -- python $B || return 1
           prof sq2_apply 150 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS \
             SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_VMEM_RD SQ_LDS_BANK_CONFLICT --output-format csv \
-            -d "$ROOTD/$OUT/sq2_apply" -o pmc -- python $B || return 1 ;;
+            -d "$ROOTD/$OUT/sq2_apply" -o pmc -- python $B || return 1
+          # reduce on the box (the raw per-dispatch CSVs of a whole bench run exceed gpurun's 64 MiB copy-back)
+          mkdir -p "$OUT/sqraw" && mv "$OUT"/sq1_apply "$OUT"/sq2_apply "$OUT/sqraw/" &&
+            python tools/pmc_table.py "$OUT/sqraw" --json "$OUT/sq_apply.json" > "$OUT/sq_apply.txt" &&
+            rm -rf "$OUT/sqraw" ;;
     py:*) timeout -k 10 300 python -u "${s#py:}" > "$OUT/$(basename "${s#py:}" .py).log" 2>&1 ;;
     *) echo "unknown step $s"; return 98 ;;
   esac
