@@ -35,28 +35,34 @@ def parse_inner(s):
 
 
 def sweep_bytes(pc, layout, kind, sweeps, fused_init):
-    """Algorithmic HBM bytes of the F inner-solve sweeps bench.py times: one (bytes, solve) per recorded launch of
+    """Algorithmic HBM bytes of the F inner-solve launches bench.py times: one (bytes, solve) per recorded launch of
     one apply, in record order, and the kernel's name.
 
-    mpbp_schur_apply records events around sweeps s = 1 .. K-1 of both F solves (s = 2 .. K-1 when the init pass is
-    fused into sweep 1).  A sweep moves per F row: x_in, b, x_out (8 B each), the direction d read (Chebyshev) and
-    written (Chebyshev, not on the last sweep), the solve's `sub` on the second solve's last sweep, and diag
-    (assembled layouts); plus the matrix (assembled: 12 B per entry + index data) or the thn tables (matrix-free:
+    mpbp_schur_apply records events around the launches of sweeps s = 1 .. K-1 of both F solves (s = 2 .. K-1 when the
+    init pass is fused into sweep 1).  A sweep moves per F row: x_in, b, x_out (8 B each), the direction d read
+    (Chebyshev) and written (Chebyshev, not on the last sweep), the solve's `sub` on the second solve's last sweep, and
+    diag (assembled layouts); plus the matrix (assembled: 12 B per entry + index data) or the thn tables (matrix-free:
     cell, u-face, v-face = 3 x 8 B per cell = 6 B per row).  With G x_p recomputed in the second solve (fuse_g), its
-    sweeps read x_p (8 B per cell = 2 B per row) instead of b."""
+    sweeps read x_p (8 B per cell = 2 B per row) instead of b.  Tolerance-mode F solves of >= 4 sweeps run their last
+    two sweeps as ONE launch (k_march2): x_in, b, d_in read and x_out written once for the pair (x_s stays in LDS)."""
     F = pc.F
     nF, nnzF = F.shape[0], F.nnz
     cheb = kind == "chebyshev"
     stencil = getattr(pc, "f_stencil", None) is not None
+    fast = getattr(pc, "numerics", "exact") == "fast"
+    pair = stencil and fast and cheb and fused_init and sweeps >= 4
     if stencil:
         prm = pc.f_stencil.prm   # the parameter identities compiled into the F policy (csrc: with_f_identities)
         n_f = int(prm.n)
         pow2 = (n_f & (n_f - 1)) == 0
         pol = ("FStencilDevM<7>" if prm.eta_n == 1.0 else ("FStencilDevM<13>" if pow2 else "FStencilDevM<5>")) \
             if (prm.d_u == -1.0 and prm.eta_s == 1.0) else "FStencilDev"
-        if getattr(pc, "numerics", "exact") == "fast":
+        if fast:
             pol = "FStencilFast"
         fixed, kname = 3 * 8 * (nF // 4), f"k_march<{pol}, XPlain, EpiCheb> (F sweep, matrix-free)"
+        if pair:
+            kname = ("k_march2<FStencilFast> (the F solve's last two Chebyshev sweeps in one launch, matrix-free, "
+                     "tolerance mode)")
     elif layout == "sell":
         fixed = nnzF * 12 + nF * 1 + pc.sell_of("F").nslices * 16
         kname = "k_sell_rows<EpiCheb> (F sweep, SELL-64)"
@@ -65,13 +71,16 @@ def sweep_bytes(pc, layout, kind, sweeps, fused_init):
     fuse_g = bool(getattr(pc, "fuse_g", False))
     out = []
     for solve in (1, 2):
-        for s in range(2 if fused_init else 1, sweeps):
-            last = s == sweeps - 1
+        s = 2 if fused_init else 1
+        while s < sweeps:
+            pr = pair and s == sweeps - 2
+            last = s == sweeps - 1 or pr
             gx = fuse_g and solve == 2                              # b = G x_p recomputed: x_p, 8 B per cell
             streams = 3 + (0 if stencil else 1) - (1 if gx else 0)  # x_in, b, x_out (+ diag)
             streams += (1 + (0 if last else 1)) if cheb else 0      # d read (+ write)
             streams += 1 if (last and solve == 2) else 0            # sub
             out.append((fixed + nF * 8 * streams + (nF // 4 * 8 if gx else 0), solve))
+            s += 2 if pr else 1
     return out, kname
 
 
@@ -117,6 +126,14 @@ def main():
                     help="grid rows per workgroup of the marching stencil kernels (matrix-free F, D, G, Gt_G); "
                          "0: the count that fills one round of workgroups per launch")
     ap.add_argument("--pg-direct", type=int, default=None, help="1: D / Gt_G sweeps as one thread per cell (no LDS)")
+    ap.add_argument("--f-pair", type=int, default=None,
+                    help="fast numerics: 1 (default) runs an F solve's last two sweeps as one k_march2 launch, 0 as two")
+    ap.add_argument("--f-direct", type=int, default=None,
+                    help="fast numerics: 1 runs the single F sweeps on the direct kernel (one thread per cell, no LDS)")
+    ap.add_argument("--gtg-fused", type=int, default=None,
+                    help="1 (default): each Chebyshev Gt_G solve as one tiled launch; 0: one launch per sweep")
+    ap.add_argument("--mg-galerkin-mf", type=int, default=None,
+                    help="fast numerics: 1 (default) applies the F hierarchy's level 1 as R0 (F (P0 x)), 0 streams it")
     ap.add_argument("--svl-min-rows", type=int, default=None,
                     help="multigrid levels above this many rows get a stencil-values copy (mg.SVL_MIN_ROWS; -1: none)")
     ap.add_argument("--stored-transfers", action="store_true",
@@ -187,6 +204,14 @@ def main():
     _check(_lib().mpbp_set_march_rows(args.march_rows))
     if args.pg_direct is not None:
         _check(_lib().mpbp_set_pg_direct(args.pg_direct))
+    if args.f_pair is not None:
+        _check(_lib().mpbp_set_f_pair(args.f_pair))
+    if args.f_direct is not None:
+        _check(_lib().mpbp_set_f_direct(args.f_direct))
+    if args.gtg_fused is not None:
+        _check(_lib().mpbp_set_gtg_fused(args.gtg_fused))
+    if args.mg_galerkin_mf is not None:
+        _check(_lib().mpbp_set_mg_galerkin_mf(args.mg_galerkin_mf))
     if args.stored_transfers:
         _check(_lib().mpbp_set_mg_mf_transfer(0))
     if args.mg_group_rows is not None:
@@ -238,6 +263,12 @@ def main():
     # 5 warmup applies the 20 timed ones read ~9 % lower: the clocks ramp over ~35 ms of load,
     # profiles/r03w_warmup_sc1_ab.jsonl).
     sweeps_per_apply = 2 * max(sf - 1, 0)
+    # N > 1: the eager applies/s first, before any capture is attempted -- a capture that fails (or never returns) on a
+    # node where the RCCL point-to-point path was never run still leaves this number
+    eager_rate = None
+    if world > 1:
+        dte = timed_loop(lambda: pc.apply(v, out), args.steps, args.warmup, world, dist, torch)
+        eager_rate = args.steps / dte * (n * n / float(1024 * 1024))
     graph, graph_note = None, None
     # partitioned applies are captured for the one-GPU self-exchange (bit-exact) and for N > 1 RCCL ranks
     # (default; --eager-partitioned opts out); the side-stream overlap option cannot be captured
@@ -280,6 +311,7 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    launch = "hipgraph" if graph is not None else "eager"
 
     # N > 1: every rank compares its rows of the partitioned apply with the one-GPU apply of the global
     # system (built on its own GPU from the same operators), bit for bit; plus an order-free checksum of
@@ -287,6 +319,15 @@ def main():
     single = None
     if world > 1 and not args.no_check:
         single = single_gpu_check(pc, n, args, iF, iP, rank, dist, torch)
+    psolve = None
+    if world > 1 and not args.no_solve:
+        if graph is not None:
+            del graph
+            graph = None
+        try:
+            psolve = partitioned_solver_section(args, n, rank, world, dist, torch, backend)
+        except Exception as e:   # reported, never fatal to the headline line
+            psolve = {"error": f"{type(e).__name__}: {e}"}
 
     # dominant kernel: the fused Chebyshev-Jacobi sweep over F
     fused_init = getattr(pc, "f_stencil", None) is not None and (not partitioned or pc.ca)
@@ -380,7 +421,7 @@ def main():
                        "d_g_gtg": "matrix-free" if getattr(pc, "pg_stencil", None) is not None else "assembled",
                        "gt_f_g": "diamond-13" if getattr(pc, "q13", None) is not None else args.layout,
                        "g_x_p": "recomputed in the second F solve" if getattr(pc, "fuse_g", False) else "kernel",
-                       "launch": "hipgraph" if graph is not None else "eager",
+                       "launch": launch,
                        "before_timed_loop": ("the A u SpMV section, " if spmv is not None else "") +
                                             "the eager profiling pass (K applies), then W warmup applies",
                        **({"halo": f"{pc.halo_impl} ({'self-exchange' if world == 1 else 'neighbour'})",
@@ -391,6 +432,10 @@ def main():
                        **({"backend": backend} if world > 1 else {}),
                        **({"note": graph_note} if graph_note else {})},
             **({"bit_exact_vs_single_gpu": single["bit_exact"], "single_gpu_check": single} if single else {}),
+            **({"eager_applies_per_s": eager_rate,
+                "eager_note": "the same apply launched eagerly, timed (barrier + max over ranks) before any graph "
+                              "capture is attempted"} if eager_rate is not None else {}),
+            **(psolve or {}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
                          "bytes_per_launch": sbytes, "avg_launch_us": avg_sweep_s * 1e6,
@@ -422,6 +467,121 @@ def main():
     if partitioned:
         pc.close()
         dist.destroy_process_group()
+
+
+def timed_loop(fn, steps, warmup, world, dist, torch):
+    """Seconds for `steps` calls of fn after `warmup` untimed ones, barrier + synchronize on both sides, max over
+    ranks."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
+def partitioned_solver_section(args, n, rank, world, dist, torch, backend):
+    """What the N > 1 line measures beyond the Chebyshev-4 headline apply: the configuration that SOLVES (FGMRES,
+    solve.py:285, with one multigrid V-cycle per inner inverse -- the reference's pointer, solve.py:266 / 274) under the
+    same row partition.
+      mg_apply_partitioned: the mg:1 / mg:1 apply, applies/s in 1024^2-cell equivalents, eager (timed before any capture)
+        and hipGraph-replayed (RCCL ranks);
+      solve_distributed: FGMRES to 1e-8 on the manufactured problem (solve.py:52-80) over the ranks -- iterations,
+        seconds (max over ranks) -- and, on rank 0, the one-GPU FGMRES of the same system: the residual histories must be
+        identical bit for bit (reproducible inner products, bit-exact partitioned operator and preconditioner)."""
+    import numpy as np
+    import mp_block_preconditioners_amd as mp
+    from mp_block_preconditioners_amd.distributed import DistributedMatrix, DistributedSchurPreconditioner
+    scale = n * n / float(1024 * 1024)
+    mg1 = dict(inner_F=mp.InnerSolver("mg", 1), inner_P=mp.InnerSolver("mg", 1))
+    out = {}
+    t0 = time.perf_counter()
+    M = DistributedSchurPreconditioner(n, args.xi, args.eta_n, args.eta_s, numerics=args.numerics, **mg1)
+    torch.cuda.synchronize()
+    setup = time.perf_counter() - t0
+    gen = torch.Generator(device="cuda").manual_seed(77 + rank)
+    v = torch.randn(M.shape[0], dtype=torch.float64, device="cuda", generator=gen)
+    o = torch.empty_like(v)
+    dte = timed_loop(lambda: M.apply(v, o), args.steps, args.warmup, world, dist, torch)
+    mg = {"inner": "mg:1 / mg:1", "unit": "applies/s (1024^2-cell equivalents)", "setup_seconds": setup,
+          "eager_applies_per_s": args.steps / dte * scale, "f_numerics": args.numerics}
+    if backend == "nccl" and not args.eager_partitioned:
+        try:
+            g = M.capture(v, o)
+            dtg = timed_loop(lambda: g.replay(), args.steps, args.warmup, world, dist, torch)
+            mg.update({"applies_per_s": args.steps / dtg * scale, "launch": "hipgraph"})
+            del g
+        except Exception as e:
+            mg.update({"applies_per_s": mg["eager_applies_per_s"], "launch": "eager",
+                       "note": f"graph capture failed: {e}"})
+    else:
+        mg.update({"applies_per_s": mg["eager_applies_per_s"], "launch": "eager (host-staged gloo halo)"})
+    M.close()
+    del M
+    torch.cuda.empty_cache()
+    # FGMRES across the ranks (solve_distributed's steps, the fgmres call timed on its own)
+    bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
+    A = bp.get_big_A_matrix(c=1.0, d_u=-1.0)[0]
+    t0 = time.perf_counter()
+    dA = DistributedMatrix(A, n, 5)
+    del A, bp
+    torch.cuda.empty_cache()
+    Md = DistributedSchurPreconditioner(n, args.xi, args.eta_n, args.eta_s, numerics=args.numerics, **mg1)
+    torch.cuda.synchronize()
+    setup = time.perf_counter() - t0
+    _, b = mp.manufactured_problem(n, xi=args.xi, etan=args.eta_n, etas=args.eta_s)
+    rows = dA.local_to_global_rows()
+    bl = torch.from_numpy(np.ascontiguousarray(b[rows])).cuda()
+    group = dist.group.WORLD
+    hist = []
+    dist.barrier()
+    t0 = time.perf_counter()
+    x, info = mp.fgmres(dA, bl, M=Md, tol=1e-8, maxiter=150, residuals=hist, group=group)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    sd = {"inner": "mg:1 / mg:1", "tol": 1e-8, "maxiter": 150, "iterations": len(hist) - 1, "converged": info == 0,
+          "seconds": el, "setup_seconds": setup, "rel_residual": hist[-1] / hist[0] if hist and hist[0] else None,
+          "halo": Md.halo_impl, "communicators_per_rank": (Md._rccl.comm_refs if Md._rccl is not None else 0),
+          "f_numerics": args.numerics}
+    shared = None if Md._rccl is None or dA._rccl is None else bool(Md._rccl.comm == dA._rccl.comm)
+    dA.close()
+    Md.close()
+    del dA, Md, x
+    torch.cuda.empty_cache()
+    same = torch.tensor([1], dtype=torch.int64, device="cuda")
+    if rank == 0 and not args.no_check:
+        t0 = time.perf_counter()
+        bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
+        A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+        pc1 = mp.ApproxSchurPreconditioner(F, D, G, numerics=args.numerics, **mg1)
+        h1 = []
+        mp.fgmres(A, torch.from_numpy(b).cuda(), M=pc1, tol=1e-8, maxiter=150, residuals=h1)
+        same[0] = 1 if np.array_equal(np.asarray(h1), np.asarray(hist)) else 0
+        sd["single_gpu_iterations"] = len(h1) - 1
+        sd["single_gpu_check_seconds"] = time.perf_counter() - t0
+        del pc1, A, F, D, G, bp
+        torch.cuda.empty_cache()
+    dist.all_reduce(same, op=dist.ReduceOp.MIN)
+    if not args.no_check:
+        sd["bit_exact_vs_single_gpu"] = bool(same.item())
+        sd["check"] = "the residual history (every iteration's ||r||) equals the one-GPU FGMRES's bit for bit"
+    if shared is not None:
+        sd["operator_and_preconditioner_share_one_communicator"] = shared
+    return {"mg_apply_partitioned": mg, "solve_distributed": sd}
 
 
 def launch_ranks(n_ranks):

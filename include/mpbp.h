@@ -436,6 +436,18 @@ int mpbp_set_march_rows(int32_t rows);
 /* The first sweep of a matrix-free F inner solve stages x0 = c2 b / diag: mode 1 (default) rebuilds diag from the
  * thn tables inside the sweep (no diag stream), mode 0 streams the stored diagonal.  Same bits either way. */
 int mpbp_set_init_diag(int32_t mode);
+/* Tolerance-mode (MPBP_NUMERICS_FAST) F Chebyshev solves of >= 4 sweeps run their last two sweeps as one fused launch
+ * (k_march2: x_s stays in LDS, 38 B per F row instead of 84; bit-identical to two sweeps).  1 (default) or 0. */
+int mpbp_set_f_pair(int32_t on);
+/* Tolerance-mode F sweeps (plain and initial) on the direct kernel -- one thread per cell, neighbours through the
+ * caches, no LDS ring -- instead of the marching kernel.  0 (default) or 1. */
+int mpbp_set_f_direct(int32_t on);
+/* One-GPU Chebyshev Gt_G solves (2..6 sweeps, matrix-free Gt_G) as ONE tiled launch each (k_gtg_solve: b read once, the
+ * iterates in LDS; bit-identical to the per-sweep launches).  1 (default) or 0. */
+int mpbp_set_gtg_fused(int32_t on);
+/* Tolerance-mode F hierarchies (plan f_numerics FAST, one GPU, matrix-free level 0 and transfers): level 1 applied as
+ * R_0 (F (P_0 x)) instead of streaming its stored Galerkin matrix.  1 (default) or 0. */
+int mpbp_set_mg_galerkin_mf(int32_t on);
 /* 1 (default): the matrix-free D, G and Gt_G sweeps run as one thread per cell reading neighbours from global memory
  * (no LDS ring; row partitions and ghost layouts included); 0: the marching kernel.  Bit-identical either way. */
 int mpbp_set_pg_direct(int32_t on);

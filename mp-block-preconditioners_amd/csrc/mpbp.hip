@@ -25,6 +25,10 @@ int g_march_rows = 0;
 int g_csr_table = 1;      // CSR SpMV waves start from the row blocks' wave table when it has one (0: from row_ptr)
 int g_mg_mf_transfer = 1;   // whole-grid multigrid transfers matrix-free (0: their CSR / SELL / grouped forms)
 int g_init_diag = 1;      // fused first F sweep: 1 rebuilds the staged diagonal from thn, 0 streams diag
+int g_mg_gal = 1;          // tolerance-mode F hierarchies: level 1 as R_0 (F (P_0 x)) (MgGal; 0: its stored matrix)
+int g_f_direct = 0;        // tolerance-mode F sweeps on the direct kernel (one thread per cell, no LDS) instead of marching
+int g_gtg_fused = 1;       // one-GPU Chebyshev Gt_G solves of 2..6 sweeps as one k_gtg_solve launch (0: per sweep)
+int g_f_pair = 1;         // tolerance-mode F solves: the last two Chebyshev sweeps as one k_march2 launch (0: two)
 #ifndef MPBP_PG_ROWS
 #define MPBP_PG_ROWS 0    // rows per workgroup of the D / G / Gt_G marching kernels (0: as F)
 #endif
@@ -635,12 +639,69 @@ __device__ inline int mg_r1d(int kind, int nf, int i, int* idx, double* w) {
     return m;
 }
 
+// Unsigned division by a run-time invariant d (>= 1) with one high multiply (Granlund-Montgomery, round-up variant):
+// q = (umulhi(x, m) + x) >> s for every 32-bit x.
+struct DivU {
+    uint32_t m, s;
+};
+inline DivU divu(uint32_t d) {
+    uint32_t s = 0;
+    while ((uint64_t(1) << s) < d) ++s;
+    const uint64_t m = ((uint64_t(1) << 32) * ((uint64_t(1) << s) - d)) / d + 1;
+    return DivU{(uint32_t)m, s};
+}
+__device__ inline uint32_t divu(uint32_t x, DivU d) {
+    return (uint32_t)(((uint64_t)__umulhi(x, d.m) + x) >> d.s);
+}
+
+// P's 1D list for fine index f (coarse size nc), in increasing index order (= mg_p1d's sorted list)
+__device__ inline int mg_p1d_fast(int kind, int nc, int f, int* idx, double* w) {
+    const int i = f >> 1;
+    if (kind == MPBP_MG_NODE && !(f & 1)) {
+        idx[0] = i;
+        w[0] = 1.0;
+        return 1;
+    }
+    const double wi = kind == MPBP_MG_CELL ? 0.75 : 0.5, wj = kind == MPBP_MG_CELL ? 0.25 : 0.5;
+    const bool down = kind == MPBP_MG_CELL && !(f & 1);             // the other coarse point is i - 1, else i + 1
+    const int j = down ? (i == 0 ? nc - 1 : i - 1) : (i + 1 == nc ? 0 : i + 1);
+    const bool jfirst = j < i;
+    idx[0] = jfirst ? j : i;  w[0] = jfirst ? wj : wi;
+    idx[1] = jfirst ? i : j;  w[1] = jfirst ? wi : wj;
+    return 2;
+}
+// R's 1D list for coarse index i (fine size nf), in increasing index order (= mg_r1d's sorted list)
+__device__ inline int mg_r1d_fast(int kind, int nf, int i, int* idx, double* w) {
+    const int f = 2 * i;
+    if (kind == MPBP_MG_CELL) {   // f-1, f, f+1, f+2 with 1/4, 3/4, 3/4, 1/4; the wrapped one moves to its end
+        if (f == 0) {
+            idx[0] = 0; w[0] = 0.75; idx[1] = 1; w[1] = 0.75; idx[2] = 2 % nf; w[2] = 0.25; idx[3] = nf - 1; w[3] = 0.25;
+        } else if (f + 2 == nf) {
+            idx[0] = 0; w[0] = 0.25; idx[1] = f - 1; w[1] = 0.25; idx[2] = f; w[2] = 0.75; idx[3] = f + 1; w[3] = 0.75;
+        } else {
+            idx[0] = f - 1; w[0] = 0.25; idx[1] = f; w[1] = 0.75; idx[2] = f + 1; w[2] = 0.75; idx[3] = f + 2; w[3] = 0.25;
+        }
+        return 4;
+    }
+    if (f == 0) {                 // f-1, f, f+1 with 1/2, 1, 1/2
+        idx[0] = 0; w[0] = 1.0; idx[1] = 1; w[1] = 0.5; idx[2] = nf - 1; w[2] = 0.5;
+    } else {
+        idx[0] = f - 1; w[0] = 0.5; idx[1] = f; w[1] = 1.0; idx[2] = f + 1; w[2] = 0.5;
+    }
+    return 3;
+}
+
 // y = op(T x) for T = P or R of the n x n grid (n = fine size), matrix-free: each row rebuilds its tensor-product
 // weights and columns exactly as k_mg_transfer stores them (same order, same products), so the sums are the CSR
-// SpMV's bit for bit; no matrix stream, and the x gathers issue without waiting for column loads.
+// SpMV's bit for bit; no matrix stream, and the x gathers issue without waiting for column loads.  The row's field
+// and grid position come from two multiply-shift divisions and the 1D lists from selects (no integer division, no
+// sorting network: 28 -> ~8 us for the 1024^2 prolongation).
+struct MgDiv {
+    DivU per, nr;   // rows per field, grid size of the rows' level
+};
 template <class Epi>
-__global__ void __launch_bounds__(kBlock) k_mg_transfer_spmv(MgFields F, int32_t n, int32_t which, int32_t nrows,
-                                                             const double* __restrict__ x, Epi epi) {
+__global__ void __launch_bounds__(kBlock) k_mg_transfer_spmv(MgFields F, MgDiv dv, int32_t n, int32_t which,
+                                                             int32_t nrows, const double* __restrict__ x, Epi epi) {
     const int32_t row = (int32_t)(blockIdx.x * kBlock + threadIdx.x);
     if (row >= nrows) return;
     const typename Epi::P pe = epi.pre(row);
@@ -648,13 +709,13 @@ __global__ void __launch_bounds__(kBlock) k_mg_transfer_spmv(MgFields F, int32_t
     const int nr = which == MPBP_MG_P ? n : nc;
     const int nk = which == MPBP_MG_P ? nc : n;
     const uint32_t per = (uint32_t)nr * (uint32_t)nr;
-    const int fld = (int)((uint32_t)row / per);
+    const int fld = (int)divu((uint32_t)row, dv.per);
     const uint32_t cell = (uint32_t)row - (uint32_t)fld * per;
-    const int r = (int)(cell / (uint32_t)nr), c = (int)(cell - (uint32_t)r * (uint32_t)nr);
+    const int r = (int)divu(cell, dv.nr), c = (int)(cell - (uint32_t)r * (uint32_t)nr);
     int yi[4], xi[4];
     double yw[4], xw[4];
-    const int my = which == MPBP_MG_P ? mg_p1d(F.ky[fld], nc, r, yi, yw) : mg_r1d(F.ky[fld], n, r, yi, yw);
-    const int mx = which == MPBP_MG_P ? mg_p1d(F.kx[fld], nc, c, xi, xw) : mg_r1d(F.kx[fld], n, c, xi, xw);
+    const int my = which == MPBP_MG_P ? mg_p1d_fast(F.ky[fld], nc, r, yi, yw) : mg_r1d_fast(F.ky[fld], n, r, yi, yw);
+    const int mx = which == MPBP_MG_P ? mg_p1d_fast(F.kx[fld], nc, c, xi, xw) : mg_r1d_fast(F.kx[fld], n, c, xi, xw);
     const int32_t off = fld * nk * nk;
     double acc = 0.0;
     for (int a = 0; a < my; ++a)
@@ -1776,6 +1837,98 @@ __device__ inline double f_row(const FStencilDev& P, int f, int gr, int gc, cons
     return acc;
 }
 
+// ---- tolerance-mode F (plan numerics "fast"): north_star's 1e-12 bar instead of the assembly's bits ----
+// The same operator with its four rows per cell regrouped around the phase-n thn at the cell centres and at the grid
+// nodes (corner K(r, c): the average of the four cells around the node between rows r-1, r and columns c-1, c;
+// phase s uses 1 - t), FMA-contracted.  With a = d_u eta idx2 and -d_u xi h (1 - h) the XI coupling (h: the face
+// average), a u row (left / right cells A1 = T(r, c-1), A2 = T(r, c), nodes KN = K(r, c), KS = K(r+1, c)) is
+//   F u = wt u_C - d_u xi_h (u_C - u_o) + a [KN (u_N - u_C + v2 - v1) + A1 (u_W - u_C + v1 - v3)
+//                                           + A2 (u_E - u_C + v4 - v2) + KS (u_S - u_C + v3 - v4)]
+// (v1..v4 = v(r, c-1), v(r, c), v(r+1, c-1), v(r+1, c)), diag = wt - d_u xi_h - a (A1 + A2 + KN + KS) -- the
+// entries of preconditioner.py:100-179 collected per coefficient; a v row (:182-295) likewise with B1 = T(r-1, c),
+// B2 = T(r, c), KW = K(r, c), KE = K(r, c+1) and u1..u4 = u(r-1, c), u(r-1, c+1), u(r, c), u(r, c+1).  Per row
+// about 40 fp64 VALU operations (corners once per cell, a reciprocal diagonal by v_rcp_f64 and two Newton steps)
+// instead of ~170 for the bit-exact rows; every value stays within a few ulp of the assembled row (numpy check:
+// 3e-16 of max |F x|).  No periodic sorting: the sum has no order to reproduce.
+__device__ inline double rcp_nr(double y) {
+    double r = __builtin_amdgcn_rcp(y);
+    double e = __builtin_fma(-y, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-y, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
+struct FStencilFast : FStencilDev {
+    static constexpr bool kFast = true;
+    struct Nb { double nw, nn, ne, w, c, e, sw, s; };   // phase-n thn around (r, c) (the 3 x 3 block minus (r+1, c+1))
+    template <class TA>
+    __device__ static Nb nb(const TA& ta, int gr, int gc) {
+        return {ta.T(0, gr - 1, gc - 1), ta.T(0, gr - 1, gc), ta.T(0, gr - 1, gc + 1), ta.T(0, gr, gc - 1),
+                ta.T(0, gr, gc), ta.T(0, gr, gc + 1), ta.T(0, gr + 1, gc - 1), ta.T(0, gr + 1, gc)};
+    }
+    // per-cell coefficients, phase n: A1 = w, A2 = B2 = c, B1 = nn; nodes kc = K(r, c), ks = K(r+1, c), ke = K(r, c+1)
+    struct Co { double w, c, nn, kc, ks, ke, xu, xv; };
+    __device__ Co coeffs(const Nb& t) const {
+        const double wc = t.w + t.c;
+        Co k;
+        k.w = t.w; k.c = t.c; k.nn = t.nn;
+        k.kc = 0.25 * ((t.nw + t.nn) + wc);
+        k.ks = 0.25 * (wc + (t.sw + t.s));
+        k.ke = 0.25 * ((t.nn + t.ne) + (t.c + t.e));
+        const double hu = 0.5 * wc, hv = 0.5 * (t.nn + t.c);
+        const double mx = -d_u * xi;             // -d_u xi h (1 - h): the same for both phases (h_s = 1 - h_n)
+        k.xu = mx * (hu * (1.0 - hu));
+        k.xv = mx * (hv * (1.0 - hv));
+        return k;
+    }
+    __device__ double aco(int p) const { return d_u * (p ? eta_s : eta_n) * idx2; }
+    // the four rows (u_n, v_n, u_s, v_s) of cell (gr, gc) and their reciprocal diagonals
+    template <class TA, class XA>
+    __device__ void rows4(int gr, int gc, const TA& ta, const XA& xa, const Cell& cl, double* acc, double* rd) const {
+        const Co k = coeffs(nb(ta, gr, gc));
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int fu = 2 * p, fv = 2 * p + 1;
+            auto ph = [&](double t) { return p ? 1.0 - t : t; };
+            const double a = aco(p);
+            const double A1 = ph(k.w), A2 = ph(k.c), B1 = ph(k.nn), KC = ph(k.kc), KS = ph(k.ks), KE = ph(k.ke);
+            const double uC = xa.X(fu, gr, gc), uN = xa.X(fu, gr - 1, gc), uS = xa.X(fu, gr + 1, gc);
+            const double uW = xa.X(fu, gr, gc - 1), uE = xa.X(fu, gr, gc + 1), uNE = xa.X(fu, gr - 1, gc + 1);
+            const double vC = xa.X(fv, gr, gc), vN = xa.X(fv, gr - 1, gc), vS = xa.X(fv, gr + 1, gc);
+            const double vW = xa.X(fv, gr, gc - 1), vE = xa.X(fv, gr, gc + 1), vSW = xa.X(fv, gr + 1, gc - 1);
+            const double uo = xa.X(fu ^ 2, gr, gc), vo = xa.X(fv ^ 2, gr, gc);
+            // u row: v1 = vW, v2 = vC, v3 = vSW, v4 = vS
+            double br = KC * ((uN - uC) + (vC - vW));
+            br = __builtin_fma(A1, (uW - uC) + (vW - vSW), br);
+            br = __builtin_fma(A2, (uE - uC) + (vS - vC), br);
+            br = __builtin_fma(KS, (uS - uC) + (vSW - vS), br);
+            const double wu = c * ph(cl.face[0]);
+            acc[fu] = __builtin_fma(a, br, __builtin_fma(wu, uC, k.xu * (uC - uo)));
+            rd[fu] = rcp_nr(__builtin_fma(-a, (A1 + A2) + (KC + KS), wu + k.xu));
+            // v row: u1 = uN, u2 = uNE, u3 = uC, u4 = uE
+            double bv = B1 * ((vN - vC) + (uN - uNE));
+            bv = __builtin_fma(KC, (vW - vC) + (uC - uN), bv);
+            bv = __builtin_fma(KE, (vE - vC) + (uNE - uE), bv);
+            bv = __builtin_fma(A2, (vS - vC) + (uE - uC), bv);
+            const double wv = c * ph(cl.face[1]);
+            acc[fv] = __builtin_fma(a, bv, __builtin_fma(wv, vC, k.xv * (vC - vo)));
+            rd[fv] = rcp_nr(__builtin_fma(-a, (B1 + A2) + (KC + KE), wv + k.xv));
+        }
+    }
+    // the reciprocal diagonals of the four rows at a staged point (k_march_init: x0 = c2 b / diag)
+    template <class TA>
+    __device__ void rdiag4(int gr, int gc, const TA& ta, const Stage& sg, double* rd) const {
+        const Co k = coeffs(nb(ta, gr, gc));
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            auto ph = [&](double t) { return p ? 1.0 - t : t; };
+            const double a = aco(p);
+            const double A1 = ph(k.w), A2 = ph(k.c), B1 = ph(k.nn), KC = ph(k.kc), KS = ph(k.ks), KE = ph(k.ke);
+            rd[2 * p] = rcp_nr(__builtin_fma(-a, (A1 + A2) + (KC + KS), c * ph(sg.face[0]) + k.xu));
+            rd[2 * p + 1] = rcp_nr(__builtin_fma(-a, (B1 + A2) + (KC + KE), c * ph(sg.face[1]) + k.xv));
+        }
+    }
+};
+
 // ---- marching kernels: a workgroup owns a 256-column strip of `rows` consecutive grid rows and walks
 // down it with a 3-row LDS ring per staged field (+ thn).  Each step stages ONE new grid row (its loads
 // are issued before the current row is computed, so their latency hides under the arithmetic) instead
@@ -2103,9 +2256,10 @@ struct TDirect {
     }
 };
 // Rows [la, la + rows) of the partition (which = 2: rows 0 and L - 1), one thread per (row, column).
-template <class S, class XS, class Epi>
-__global__ void __launch_bounds__(256) k_direct(S P, XS xs, Epi epi, int la, int rows) {
+template <class S, class XS, class Epi, class BS = BNone>
+__global__ void __launch_bounds__(256) k_direct(S P, XS xs, Epi epi, int la, int rows, BS bs = BS{}) {
     constexpr int NO = S::NOUT;
+    static_assert(!S::kFast || RcpOk<Epi>::value, "a tolerance-mode policy hands over reciprocal diagonals");
     const int n = P.n;
     const int64_t t = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
     const bool live = t < (int64_t)rows * n;
@@ -2119,6 +2273,20 @@ __global__ void __launch_bounds__(256) k_direct(S P, XS xs, Epi epi, int la, int
     const typename S::Cell cl = P.cell_pre(gr, gc);
     const XDirect<S, XS> xa{P, xs, lr, gr};
     const TDirect ta{P.cell, n};
+    const typename BS::Q bq = bs.load(lr, gr, gc);
+    if constexpr (S::kFast) {   // tolerance-mode F: the cell's four rows at once, reciprocal diagonals
+        if (!live) return;
+        double acc[NO], rd[NO];
+        P.rows4(gr, gc, ta, xa, cl, acc, rd);
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+            set_diag(pe[o], rd[o]);
+            set_x(pe[o], xa.X(o, gr, gc));
+            if constexpr (BS::on) set_b(pe[o], bs.b(o, gr, gc, gc, ta, bq));
+            epi(P.out_row(o, lr, gc), acc[o], pe[o]);
+        }
+        return;
+    }
     const bool edge = __builtin_amdgcn_readfirstlane(__any(gr == 0 || gr == n - 1 || gc == 0 || gc == n - 1)) != 0;
     if (!live) return;
 #pragma unroll
@@ -2345,6 +2513,192 @@ k_march_init(S P, const double* __restrict__ b, double c2, int nchunks, Epi epi,
     step(lb - 1, std::false_type{});
 }
 
+// ---- two fused Chebyshev sweeps over F, tolerance mode (k_march2) ----
+// Sweeps s and s+1 of an F Chebyshev solve in one pass down the strip.  Level A stages x_{s-1} (x_in) in a 3-row
+// LDS ring and computes x_s, d_s of grid row t; x_s goes to a second ring, d_s (and b, the faces) stay in the lane's
+// registers -- level B, one row behind, computes x_{s+1} of row t-1 on the same column from that ring.  Per F row the
+// pair reads x_in, d_in, b (or x_p, GxB), thn and writes x_out (+ d_out unless the pair ends the solve): 38 B instead of
+// 84 B for two k_march sweeps; x_s and d_s never leave the CU.  Level A also computes x_s on the columns either side
+// of the strip (c0 - 1, c0 + 256: one extra pass of lanes 0, 1) for level B's stencil.  Each level performs exactly
+// the IEEE operations of one tolerance-mode k_march sweep (FStencilFast::rows4, the RCP Chebyshev update), so the pair
+// is bit-identical to two k_march sweeps.  Rows: level A [la-1, lb], level B [la, lb) -- under a row partition the
+// input needs one more ghost row each side than the output (the CA schedule's depths provide it).
+constexpr int kRA = kMB + 4;   // ring A (x_in) and the thn ring: columns c0-2 .. c0+257
+template <int W, int OFF>
+struct XRingW {
+    const double* x;   // [4][3][W]: tile column 0 is grid column c0 - OFF
+    int s[3];
+    int gr, c0;
+    __device__ double X(int f, int r, int c) const { return x[(f * 3 + s[r - gr + 1]) * W + (c - c0 + OFF)]; }
+};
+struct Fused2 {
+    const double* x_in;
+    const double* d_in;
+    const double* b;      // BNone: the right-hand side; GxB: unused (recomputed from x_p)
+    const double* sub;    // SUB: the solve's last sweep returns sub - x
+    double* x_out;
+    double* d_out;        // SD: level B's direction is stored
+    double c1a, c2a, c1b, c2b;
+};
+struct Stage2 {
+    double x[4], xh[4];   // x_in at the lane's column c0-2+tid and (lanes 0..3) c0+254+tid
+    double t, th;         // thn at the same columns
+};
+template <class BS>
+struct OpsA {             // level A's operands at one column of row t
+    double d[4], face[2];
+    typename BS::Q q;
+    double b[4];
+};
+
+template <bool SUB, bool SD, class BS>
+__global__ void __launch_bounds__(kMB) __attribute__((amdgpu_waves_per_eu(2, 8)))
+k_march2(FStencilFast P, Fused2 a, int nchunks, BS bs) {
+    __shared__ double ra[4 * 3 * kRA];
+    __shared__ double rb[4 * 3 * kMTileW];
+    __shared__ double st[5 * kRA];
+    const int n = P.n;
+    const int strips = (n + kMB - 1) / kMB;
+    const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int strip = bk % strips, chunk = bk / strips;
+    int la, lb;
+    if (!march_rows(P.which, P.L, P.ext, chunk, nchunks, &la, &lb)) return;
+    const int c0 = strip * kMB, tid = threadIdx.x;
+    const int cm = c0 - 2 + tid, ch = c0 + kMB - 2 + tid;   // staged columns (ch: lanes 0..3)
+    const bool okm = cm <= n + 1, okh = tid < 4 && ch <= n + 1;
+    const int gm = okm ? P.wrap(cm) : 0, gh = okh ? P.wrap(ch) : gm;
+    const int gc = c0 + tid;                                  // levels A and B: the lane's column
+    const bool liveA = gc <= n, liveB = gc < n;
+    const int gcl = liveB ? gc : 0;                           // operand column (column n: level A's halo, wraps to 0)
+    const int gca = liveA ? P.wrap(gc) : 0;
+    // lanes 0, 1: level A's halo columns c0-1, c0+256 (extra pass)
+    const int cx = tid == 0 ? c0 - 1 : c0 + kMB;
+    const bool liveX = tid < 2 && cx <= n;
+    const int gcx = liveX ? P.wrap(cx) : gca;
+    auto xslot = [&](int r) { return (r - la + 2) % 3; };   // ring A (rows >= la-2)
+    auto tslot = [&](int r) { return (r - la + 2) % 5; };   // thn ring
+    auto bslot = [&](int r) { return (r - la + 1) % 3; };   // ring B (rows >= la-1)
+    auto grow = [&](int lr) { return P.wrap(P.r0 + lr); };
+    // a row of the output layout: one GPU wraps level A's rows -1 and n periodically; a partition's ghost rows are in
+    // the ext layout
+    auto orow = [&](int lr) { return P.h == 0 ? P.wrap(lr) : lr; };
+    auto load_stage = [&](int lr, Stage2& g) {
+        const int gr = P.r0 + lr;
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            const int32_t base = P.xrow(f, gr);
+            g.x[f] = a.x_in[base + gm];
+            g.xh[f] = a.x_in[base + gh];
+        }
+        const int32_t tb = P.wrap(gr) * n;
+        g.t = P.cell[tb + gm];
+        g.th = P.cell[tb + gh];
+    };
+    auto store_stage = [&](int lr, const Stage2& g) {
+        const int xs = xslot(lr), ts = tslot(lr);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) ra[(f * 3 + xs) * kRA + tid] = okm ? g.x[f] : 0.0;
+        st[ts * kRA + tid] = okm ? g.t : 0.0;
+        if (tid < 4) {
+#pragma unroll
+            for (int f = 0; f < 4; ++f) ra[(f * 3 + xs) * kRA + kMB + tid] = okh ? g.xh[f] : 0.0;
+            st[ts * kRA + kMB + tid] = okh ? g.th : 0.0;
+        }
+    };
+    // level A's operands at (local row lr, wrapped column g): d_in, the faces, b (or G x_p's operands)
+    auto load_ops = [&](int lr, int g, OpsA<BS>& o) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) o.d[f] = a.d_in[P.out_row(f, orow(lr), g)];
+        const int32_t k = grow(lr) * n + g;
+        o.face[0] = P.uface[k];
+        o.face[1] = P.vface[k];
+        if constexpr (BS::on) o.q = bs.load(lr, grow(lr), g);
+        else {
+#pragma unroll
+            for (int f = 0; f < 4; ++f) o.b[f] = a.b[P.out_row(f, orow(lr), g)];
+        }
+    };
+    // level A at row lr, column c (virtual: -1 and n wrap): x_s into ring B, d_s and b returned
+    auto level_a = [&](int lr, int c, const OpsA<BS>& o, double* dA, double* bA) {
+        const int gr = grow(lr);
+        const XRingW<kRA, 2> xa{ra, {xslot(lr - 1), xslot(lr), xslot(lr + 1)}, gr, c0};
+        const TRingT<kRA, 2> ta{st, {tslot(lr - 1), tslot(lr), tslot(lr + 1)}, gr, c0};
+        const FStencilDev::Cell cl{{o.face[0], o.face[1]}};
+        double acc[4], rd[4];
+        P.rows4(gr, c, ta, xa, cl, acc, rd);
+        const int bsl = bslot(lr);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            double bf;
+            if constexpr (BS::on) bf = bs.b(f, gr, c, P.wrap(c), ta, o.q);
+            else bf = o.b[f];
+            const double z = (bf - acc[f]) * rd[f];
+            const double dn = a.c1a * o.d[f] + a.c2a * z;
+            rb[(f * 3 + bsl) * kMTileW + (c - c0 + 1)] = xa.X(f, gr, c) + dn;
+            dA[f] = dn;
+            bA[f] = bf;
+        }
+    };
+    // prologue: x_in and thn rows la-2, la-1 in the rings, row la in registers
+    Stage2 g;
+    {
+        Stage2 g0, g1;
+        load_stage(la - 2, g0);
+        load_stage(la - 1, g1);
+        load_stage(la, g);
+        store_stage(la - 2, g0);
+        store_stage(la - 1, g1);
+    }
+    double dP[4] = {0.0, 0.0, 0.0, 0.0}, bP[4] = {0.0, 0.0, 0.0, 0.0}, fP[2] = {0.0, 0.0};   // level A of row t-1
+    auto step = [&](int t, auto load_next) {
+        store_stage(t + 1, g);
+        OpsA<BS> oa, ox;
+        load_ops(t, gca, oa);
+        load_ops(t, gcx, ox);
+        double sv[4] = {0.0, 0.0, 0.0, 0.0};
+        const bool doB = t - 1 >= la;
+        if constexpr (SUB) {
+#pragma unroll
+            for (int f = 0; f < 4; ++f) sv[f] = a.sub[P.out_row(f, orow(t - 1), gcl)];
+        }
+        __syncthreads();
+        if constexpr (decltype(load_next)::value) load_stage(t + 2, g);
+        double dA[4] = {0.0, 0.0, 0.0, 0.0}, bA[4] = {0.0, 0.0, 0.0, 0.0};
+        if (liveA) level_a(t, gc, oa, dA, bA);
+        if (liveX) {
+            double dx[4], bx[4];
+            level_a(t, cx, ox, dx, bx);
+        }
+        __syncthreads();
+        if (doB && liveB) {   // level B: row t-1 from ring B
+            const int lr = t - 1, gr = grow(lr);
+            const XRingW<kMTileW, 1> xa{rb, {bslot(lr - 1), bslot(lr), bslot(lr + 1)}, gr, c0};
+            const TRingT<kRA, 2> ta{st, {tslot(lr - 1), tslot(lr), tslot(lr + 1)}, gr, c0};
+            const FStencilDev::Cell cl{{fP[0], fP[1]}};
+            double acc[4], rd[4];
+            P.rows4(gr, gc, ta, xa, cl, acc, rd);
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                const double z = (bP[f] - acc[f]) * rd[f];
+                const double dn = a.c1b * dP[f] + a.c2b * z;
+                const int32_t o = P.out_row(f, orow(lr), gc);
+                if constexpr (SD) a.d_out[o] = dn;
+                const double x = xa.X(f, gr, gc) + dn;
+                a.x_out[o] = SUB ? sv[f] - x : x;
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            dP[f] = dA[f];
+            bP[f] = bA[f];
+        }
+        fP[0] = oa.face[0];
+        fP[1] = oa.face[1];
+    };
+    for (int t = la - 1; t < lb; ++t) step(t, std::true_type{});
+    step(lb, std::false_type{});
+}
+
 // Workgroups of one marching-kernel instance the device holds at once (occupancy x CUs), queried once.
 template <auto K>
 int64_t march_capacity() {
@@ -2385,15 +2739,16 @@ int64_t march_chunks(const S& P, int rows_per_block, int64_t capacity) {
 
 template <class S, class XS, class Epi, class BS = BNone>
 int launch_march_fixed(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStream_t st, const BS& bs = BS{}) {
-    if constexpr (!std::is_base_of_v<FStencilDev, S> && !BS::on) {   // D, G, Gt_G on one GPU: the direct kernel
-        if (g_pg_direct) {
+    // D, G, Gt_G on one GPU, and (g_f_direct) the tolerance-mode F rows: the direct kernel
+    if constexpr ((!std::is_base_of_v<FStencilDev, S> && !BS::on) || S::kFast) {
+        if (S::kFast ? g_f_direct != 0 : g_pg_direct != 0) {
             // rows as march_rows: 0 all owned, 1 rows 1 .. L-2, 2 rows 0 and L-1, 3 owned + ext ghost rows each side
             const int la = P.which == 1 ? 1 : P.which == 3 ? -P.ext : 0;
             const int lb = P.which == 1 ? P.L - 1 : P.which == 3 ? P.L + P.ext : P.L;
             const int rows = P.which == 2 ? (P.L >= 2 ? 2 : 1) : lb - la;
             if (rows <= 0) return MPBP_OK;
             const int64_t cells = (int64_t)rows * P.n;
-            k_direct<S, XS, Epi><<<(unsigned)((cells + 255) / 256), 256, 0, st>>>(P, xs, epi, la, rows);
+            k_direct<S, XS, Epi, BS><<<(unsigned)((cells + 255) / 256), 256, 0, st>>>(P, xs, epi, la, rows, bs);
             MPBP_HIP(hipGetLastError());
             return MPBP_OK;
         }
@@ -2404,6 +2759,29 @@ int launch_march_fixed(const S& P, const XS& xs, Epi epi, int rows_per_block, hi
     k_march<S, XS, Epi, BS><<<(unsigned)(chunks * strips), kMB, 0, st>>>(P, xs, (int)chunks, epi, bs);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
+}
+
+// Sweeps s, s+1 of an F Chebyshev solve fused (k_march2, tolerance mode) over the rows P.which selects (0: the whole
+// grid, 3: owned + ext ghost rows; level A then covers ext + 1).  d_in may be d_out only when the pair does not store
+// its direction (SD false): level A reads d_in on its neighbours' rows and columns.
+template <bool SUB, bool SD, class BS>
+int launch_march2_t(const FStencilFast& P, const Fused2& a, hipStream_t st, const BS& bs) {
+    const int64_t chunks = march_chunks(P, g_march_rows, march_capacity<k_march2<SUB, SD, BS>>());
+    if (chunks == 0) return MPBP_OK;
+    const int64_t strips = (P.n + kMB - 1) / kMB;
+    k_march2<SUB, SD, BS><<<(unsigned)(chunks * strips), kMB, 0, st>>>(P, a, (int)chunks, bs);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+template <class BS = BNone>
+int launch_march2(const FStencilDev& Pd, const Fused2& a, hipStream_t st, const BS& bs = BS{}) {
+    const FStencilFast P{Pd};
+    if (P.which == 1 || P.which == 2) return set_error(MPBP_ERR_ARG, "march2: interior / boundary row splits unsupported");
+    if (!a.x_in || !a.d_in || !a.x_out || a.x_in == a.x_out || (!BS::on && !a.b) || (a.d_out && a.d_out == a.d_in))
+        return set_error(MPBP_ERR_ARG, "march2: bad vectors");
+    const bool sub = a.sub != nullptr, sd = a.d_out != nullptr;
+    return sub ? (sd ? launch_march2_t<true, true>(P, a, st, bs) : launch_march2_t<true, false>(P, a, st, bs))
+               : (sd ? launch_march2_t<false, true>(P, a, st, bs) : launch_march2_t<false, false>(P, a, st, bs));
 }
 
 // The first inner sweep with x0 = c2 b / diag staged and diag rebuilt from thn (k_march_init).  BS = GxB: b is
@@ -2449,98 +2827,6 @@ struct FStencilDevM : FStencilDev {
     template <class TA>
     __device__ double stage_diag(int f, int gr, int gc, const TA& ta, const Stage& s) const {
         return f_stage_diag<M>(*this, f, gr, gc, ta, s);
-    }
-};
-
-// ---- tolerance-mode F (plan numerics "fast"): north_star's 1e-12 bar instead of the assembly's bits ----
-// The same operator with its four rows per cell regrouped around the phase-n thn at the cell centres and at the grid
-// nodes (corner K(r, c): the average of the four cells around the node between rows r-1, r and columns c-1, c;
-// phase s uses 1 - t), FMA-contracted.  With a = d_u eta idx2 and -d_u xi h (1 - h) the XI coupling (h: the face
-// average), a u row (left / right cells A1 = T(r, c-1), A2 = T(r, c), nodes KN = K(r, c), KS = K(r+1, c)) is
-//   F u = wt u_C - d_u xi_h (u_C - u_o) + a [KN (u_N - u_C + v2 - v1) + A1 (u_W - u_C + v1 - v3)
-//                                           + A2 (u_E - u_C + v4 - v2) + KS (u_S - u_C + v3 - v4)]
-// (v1..v4 = v(r, c-1), v(r, c), v(r+1, c-1), v(r+1, c)), diag = wt - d_u xi_h - a (A1 + A2 + KN + KS) -- the
-// entries of preconditioner.py:100-179 collected per coefficient; a v row (:182-295) likewise with B1 = T(r-1, c),
-// B2 = T(r, c), KW = K(r, c), KE = K(r, c+1) and u1..u4 = u(r-1, c), u(r-1, c+1), u(r, c), u(r, c+1).  Per row
-// about 40 fp64 VALU operations (corners once per cell, a reciprocal diagonal by v_rcp_f64 and two Newton steps)
-// instead of ~170 for the bit-exact rows; every value stays within a few ulp of the assembled row (numpy check:
-// 3e-16 of max |F x|).  No periodic sorting: the sum has no order to reproduce.
-__device__ inline double rcp_nr(double y) {
-    double r = __builtin_amdgcn_rcp(y);
-    double e = __builtin_fma(-y, r, 1.0);
-    r = __builtin_fma(r, e, r);
-    e = __builtin_fma(-y, r, 1.0);
-    return __builtin_fma(r, e, r);
-}
-struct FStencilFast : FStencilDev {
-    static constexpr bool kFast = true;
-    struct Nb { double nw, nn, ne, w, c, e, sw, s; };   // phase-n thn around (r, c) (the 3 x 3 block minus (r+1, c+1))
-    template <class TA>
-    __device__ static Nb nb(const TA& ta, int gr, int gc) {
-        return {ta.T(0, gr - 1, gc - 1), ta.T(0, gr - 1, gc), ta.T(0, gr - 1, gc + 1), ta.T(0, gr, gc - 1),
-                ta.T(0, gr, gc), ta.T(0, gr, gc + 1), ta.T(0, gr + 1, gc - 1), ta.T(0, gr + 1, gc)};
-    }
-    // per-cell coefficients, phase n: A1 = w, A2 = B2 = c, B1 = nn; nodes kc = K(r, c), ks = K(r+1, c), ke = K(r, c+1)
-    struct Co { double w, c, nn, kc, ks, ke, xu, xv; };
-    __device__ Co coeffs(const Nb& t) const {
-        const double wc = t.w + t.c;
-        Co k;
-        k.w = t.w; k.c = t.c; k.nn = t.nn;
-        k.kc = 0.25 * ((t.nw + t.nn) + wc);
-        k.ks = 0.25 * (wc + (t.sw + t.s));
-        k.ke = 0.25 * ((t.nn + t.ne) + (t.c + t.e));
-        const double hu = 0.5 * wc, hv = 0.5 * (t.nn + t.c);
-        const double mx = -d_u * xi;             // -d_u xi h (1 - h): the same for both phases (h_s = 1 - h_n)
-        k.xu = mx * (hu * (1.0 - hu));
-        k.xv = mx * (hv * (1.0 - hv));
-        return k;
-    }
-    __device__ double aco(int p) const { return d_u * (p ? eta_s : eta_n) * idx2; }
-    // the four rows (u_n, v_n, u_s, v_s) of cell (gr, gc) and their reciprocal diagonals
-    template <class TA, class XA>
-    __device__ void rows4(int gr, int gc, const TA& ta, const XA& xa, const Cell& cl, double* acc, double* rd) const {
-        const Co k = coeffs(nb(ta, gr, gc));
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            const int fu = 2 * p, fv = 2 * p + 1;
-            auto ph = [&](double t) { return p ? 1.0 - t : t; };
-            const double a = aco(p);
-            const double A1 = ph(k.w), A2 = ph(k.c), B1 = ph(k.nn), KC = ph(k.kc), KS = ph(k.ks), KE = ph(k.ke);
-            const double uC = xa.X(fu, gr, gc), uN = xa.X(fu, gr - 1, gc), uS = xa.X(fu, gr + 1, gc);
-            const double uW = xa.X(fu, gr, gc - 1), uE = xa.X(fu, gr, gc + 1), uNE = xa.X(fu, gr - 1, gc + 1);
-            const double vC = xa.X(fv, gr, gc), vN = xa.X(fv, gr - 1, gc), vS = xa.X(fv, gr + 1, gc);
-            const double vW = xa.X(fv, gr, gc - 1), vE = xa.X(fv, gr, gc + 1), vSW = xa.X(fv, gr + 1, gc - 1);
-            const double uo = xa.X(fu ^ 2, gr, gc), vo = xa.X(fv ^ 2, gr, gc);
-            // u row: v1 = vW, v2 = vC, v3 = vSW, v4 = vS
-            double br = KC * ((uN - uC) + (vC - vW));
-            br = __builtin_fma(A1, (uW - uC) + (vW - vSW), br);
-            br = __builtin_fma(A2, (uE - uC) + (vS - vC), br);
-            br = __builtin_fma(KS, (uS - uC) + (vSW - vS), br);
-            const double wu = c * ph(cl.face[0]);
-            acc[fu] = __builtin_fma(a, br, __builtin_fma(wu, uC, k.xu * (uC - uo)));
-            rd[fu] = rcp_nr(__builtin_fma(-a, (A1 + A2) + (KC + KS), wu + k.xu));
-            // v row: u1 = uN, u2 = uNE, u3 = uC, u4 = uE
-            double bv = B1 * ((vN - vC) + (uN - uNE));
-            bv = __builtin_fma(KC, (vW - vC) + (uC - uN), bv);
-            bv = __builtin_fma(KE, (vE - vC) + (uNE - uE), bv);
-            bv = __builtin_fma(A2, (vS - vC) + (uE - uC), bv);
-            const double wv = c * ph(cl.face[1]);
-            acc[fv] = __builtin_fma(a, bv, __builtin_fma(wv, vC, k.xv * (vC - vo)));
-            rd[fv] = rcp_nr(__builtin_fma(-a, (B1 + A2) + (KC + KE), wv + k.xv));
-        }
-    }
-    // the reciprocal diagonals of the four rows at a staged point (k_march_init: x0 = c2 b / diag)
-    template <class TA>
-    __device__ void rdiag4(int gr, int gc, const TA& ta, const Stage& sg, double* rd) const {
-        const Co k = coeffs(nb(ta, gr, gc));
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            auto ph = [&](double t) { return p ? 1.0 - t : t; };
-            const double a = aco(p);
-            const double A1 = ph(k.w), A2 = ph(k.c), B1 = ph(k.nn), KC = ph(k.kc), KS = ph(k.ks), KE = ph(k.ke);
-            rd[2 * p] = rcp_nr(__builtin_fma(-a, (A1 + A2) + (KC + KS), c * ph(sg.face[0]) + k.xu));
-            rd[2 * p + 1] = rcp_nr(__builtin_fma(-a, (B1 + A2) + (KC + KE), c * ph(sg.face[1]) + k.xv));
-        }
     }
 };
 
@@ -2736,6 +3022,100 @@ struct GtGStencilDev : PGDev {
         return apply_v<EDGE>(gr, gc, gr, gc, ta, xa, dg);
     }
 };
+
+// ---- one Gt_G Chebyshev solve in one launch (k_gtg_solve) ----
+// The pressure solves x = Gt_G^-1 b of the apply (solve.py:265, 271) as K Chebyshev-Jacobi sweeps from x0 = 0, fused:
+// a workgroup owns a TW x TH tile of cells and stages b and thn over the tile plus a halo of H = K - 1 cells (its
+// level 0, x0 = d0 = c2_0 (b / diag), built there from the stored diagonal); level l = 1 .. H recomputes the tile with
+// halo H - l from level l - 1 in LDS, and the last level writes the tile.  Each row is GtGStencilDev::apply_v (the
+// matrix-free rows' IEEE operations) and each update the Chebyshev epilogue's (EpiChebFirst at level 1, EpiCheb after):
+// bit-identical to the K - 1 sweeps of the per-sweep path, for one launch and one pass over b instead of K - 1 passes
+// over x, d, b.  Halo cells are recomputed by neighbouring tiles (70 x 14 staged cells per 64 x 8 tile at K = 4).
+constexpr int kGTW = 64, kGTH = 8;
+struct ChebK {
+    double c1[8], c2[8];   // sweep s's coefficients (c2[0]: the initial iterate's)
+};
+template <int H>
+struct GtgTile {
+    static constexpr int RW = kGTW + 2 * H, RH = kGTH + 2 * H, N = RW * RH;
+};
+template <int H>
+struct TTile {   // thn of the staged tile; (r, c) in the tile's virtual grid coordinates
+    const double* t;
+    int rb, cb;
+    __device__ double T(int sph, int r, int c) const {
+        const double v = t[(r - rb) * GtgTile<H>::RW + (c - cb)];
+        return sph ? 1.0 - v : v;
+    }
+};
+template <int H>
+struct XTile {
+    const double* x;
+    int rb, cb;
+    __device__ double X(int, int r, int c) const { return x[(r - rb) * GtgTile<H>::RW + (c - cb)]; }
+};
+
+template <int H>
+__global__ void __launch_bounds__(256) k_gtg_solve(GtGStencilDev P, const double* __restrict__ b,
+                                                   const double* __restrict__ diag, ChebK ck, double* __restrict__ out) {
+    using G = GtgTile<H>;
+    __shared__ double ts[G::N], bs[G::N], xa[G::N], xb[G::N], ds[G::N];
+    const int n = P.n;
+    const int tx = (n + kGTW - 1) / kGTW;
+    const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int r0 = (bk / tx) * kGTH, c0 = (bk % tx) * kGTW;
+    const int rb = r0 - H, cb = c0 - H;   // virtual coordinates of staged cell 0
+    const int tid = threadIdx.x;
+    // level 0 over the whole staged region: thn, b, x0 = d0 = c2_0 (b / diag)
+    for (int i = tid; i < G::N; i += 256) {
+        const int rr = i / G::RW, cc = i - rr * G::RW;
+        const int32_t k = P.wrap(rb + rr) * n + P.wrap(cb + cc);
+        const double bv = b[k];
+        ts[i] = P.cell[k];
+        bs[i] = bv;
+        const double x0 = ck.c2[0] * (bv / diag[k]);
+        xa[i] = x0;
+        ds[i] = x0;
+    }
+    __syncthreads();
+    double* cur = xa;
+    double* nxt = xb;
+    const TTile<H> ta{ts, rb, cb};
+#pragma unroll 1
+    for (int l = 1; l <= H; ++l) {
+        const int h = H - l;                       // this level's halo
+        const int w = kGTW + 2 * h, rows = kGTH + 2 * h;
+        const XTile<H> xt{cur, rb, cb};
+        for (int i0 = 0; i0 < w * rows; i0 += 256) {
+            const int i = i0 + tid;
+            const bool live = i < w * rows;
+            const int ii = live ? i : 0;
+            const int lr = ii / w, lc = ii - lr * w;
+            const int vr = r0 - h + lr, vc = c0 - h + lc;        // virtual cell
+            const int gr = P.wrap(vr), gc = P.wrap(vc);
+            const int si = (vr - rb) * G::RW + (vc - cb);        // its staged index
+            const bool edge = __builtin_amdgcn_readfirstlane(__any(live && (gr == 0 || gr == n - 1 || gc == 0 ||
+                                                                            gc == n - 1))) != 0;
+            if (!live) continue;
+            double dg;
+            const double acc = edge ? P.template apply_v<true>(vr, vc, gr, gc, ta, xt, &dg)
+                                    : P.template apply_v<false>(vr, vc, gr, gc, ta, xt, &dg);
+            const double z = (bs[si] - acc) / dg;
+            const double dn = ck.c1[l] * ds[si] + ck.c2[l] * z;
+            const double x = cur[si] + dn;
+            if (l < H) {
+                nxt[si] = x;
+                ds[si] = dn;
+            } else if (vr < n && vc < n) {                        // the tile's own cells (h = 0: vr, vc >= 0)
+                out[vr * n + vc] = x;
+            }
+        }
+        __syncthreads();
+        double* t = cur;
+        cur = nxt;
+        nxt = t;
+    }
+}
 
 // One thread per (slice, lane): copy the CSR row into its column-major slots.
 __global__ void k_sell_fill(Csr A, const int4* slices, int nslices, uint8_t* rlen, double* val, int32_t* col) {
@@ -2942,6 +3322,26 @@ int mpbp_set_pg_direct(int32_t on) {
     return MPBP_OK;
 }
 
+int mpbp_set_mg_galerkin_mf(int32_t on) {
+    if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "mg_galerkin_mf must be 0 or 1");
+    g_mg_gal = on;
+    return MPBP_OK;
+}
+int mpbp_set_f_direct(int32_t on) {
+    if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "f_direct must be 0 or 1");
+    g_f_direct = on;
+    return MPBP_OK;
+}
+int mpbp_set_gtg_fused(int32_t on) {
+    if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "gtg_fused must be 0 or 1");
+    g_gtg_fused = on;
+    return MPBP_OK;
+}
+int mpbp_set_f_pair(int32_t on) {
+    if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "f_pair must be 0 or 1");
+    g_f_pair = on;
+    return MPBP_OK;
+}
 int mpbp_set_init_diag(int32_t mode) {
     if (mode != 0 && mode != 1) return set_error(MPBP_ERR_ARG, "init diag mode must be 0 or 1");
     g_init_diag = mode;
@@ -4020,6 +4420,19 @@ struct OpRef {
     int32_t ext = 0;                  // which = 3
     int32_t grp = 0;                  // CSR rows through k_csr_grp (multigrid small levels)
     const mpbp_svl* svl = nullptr;    // stencil-values layout of csr (multigrid large levels)
+    const struct MgGal* gal = nullptr;   // level 1 of an F hierarchy applied as R0 (F (P0 x)) (tolerance mode)
+};
+
+// Level 1 of the F hierarchy without its Galerkin matrix (tolerance mode): A_1 x = R_0 (F (P_0 x)) -- the same operator
+// as the stored product (mg_oracle's R A P) in exact arithmetic -- from the matrix-free transfers and the tolerance-mode
+// F sweep of level 0, through two fine-size temporaries (level 0's residual and direction buffers, dead while level 1
+// runs).  Per application: x_c and the thn read, two fine vectors written and read once, the level-1 epilogue operands;
+// ~115 MB at 1024^2 instead of streaming the 40-entry coarse rows' values (386 MB).
+struct MgGal {
+    const mpbp_mg* m;
+    OpRef fine;     // level 0's whole-grid F stencil
+    double* t0;     // fine-size temporaries
+    double* t1;
 };
 
 // F and D read velocity vectors (f_part), G and Gt_G pressure vectors (p_part); D writes a pressure vector
@@ -4033,8 +4446,31 @@ inline mpbp_row_part stencil_part(const OpRef& o) {
     return q;
 }
 
+template <class Epi>
+int mg_transfer_mf(const mpbp_mg* m, int l, int32_t which, int32_t nrows, const double* x, Epi epi, hipStream_t st);
+int op_spmv(const OpRef& o, int32_t mode, const double* x, const double* z, double* y, hipStream_t st);
+// t1 = F (P_0 x): the first two stages of a matrix-free Galerkin level-1 product
+int gal_fp(const MgGal& g, const double* x, hipStream_t st) {
+    const int rc = mg_transfer_mf(g.m, 0, MPBP_MG_P, g.m->levels[0].P.nrows, x, EpiStore{g.t0}, st);
+    return rc ? rc : op_spmv(g.fine, MPBP_SPMV_STORE, g.t0, nullptr, g.t1, st);
+}
+template <class Epi>
+int gal_r(const MgGal& g, Epi epi, hipStream_t st) {
+    return mg_transfer_mf(g.m, 0, MPBP_MG_R, g.m->levels[0].R.nrows, g.t1, epi, st);
+}
+
 int op_spmv(const OpRef& o, int32_t mode, const double* x, const double* z, double* y, hipStream_t st) {
     if (o.empty) return MPBP_OK;
+    if (o.gal) {
+        const int rc = gal_fp(*o.gal, x, st);
+        if (rc) return rc;
+        switch (mode) {
+        case MPBP_SPMV_STORE: return gal_r(*o.gal, EpiStore{y}, st);
+        case MPBP_SPMV_ADD: return gal_r(*o.gal, EpiAdd{z, y}, st);
+        case MPBP_SPMV_RESID: return gal_r(*o.gal, EpiResid{z, y}, st);
+        default: return set_error(MPBP_ERR_ARG, "galerkin spmv: unknown mode %d", mode);
+        }
+    }
     if (o.stencil) {
         const mpbp_schur_plan* p = o.stencil;
         const mpbp_row_part q = stencil_part(o);
@@ -4067,6 +4503,11 @@ int op_jacobi(const OpRef& o, const double* xin, const double* b, const double* 
 int op_cheb(const OpRef& o, const double* xin, const double* b, const double* dg, double c1, double c2, double* d,
             const double* sub, double* xo, hipStream_t st, int store_d, bool dzero = false) {
     if (o.empty) return MPBP_OK;
+    if (o.gal) {
+        if (dzero) return set_error(MPBP_ERR_ARG, "cheb: a zero direction is only supported on the grouped CSR path");
+        const int rc = gal_fp(*o.gal, xin, st);
+        return rc ? rc : gal_r(*o.gal, EpiCheb{xin, b, dg, d, c1, c2, sub, xo, store_d}, st);
+    }
     if (o.grp) return grp_cheb(o.csr, xin, b, dg, c1, c2, d, sub, xo, st, store_d, dzero);
     if (o.svl) return svl_cheb(o.svl, o.csr, xin, b, dg, c1, c2, d, sub, xo, st, store_d, dzero);
     if (dzero) return set_error(MPBP_ERR_ARG, "cheb: a zero direction is only supported on the grouped CSR path");
@@ -4212,6 +4653,7 @@ void mg_exchange(const mpbp_mg* m, int l, const MgFine& f, double* x, hipStream_
 // field kinds and the level is whole-grid (not row-partitioned); 1: launched, 0: not applicable.
 template <class Epi>
 int mg_transfer_mf(const mpbp_mg* m, int l, int32_t which, int32_t nrows, const double* x, Epi epi, hipStream_t st) {
+    const int32_t n = m->tr_n0 >> l, nr = which == MPBP_MG_P ? n : n / 2;
     k_mg_transfer_spmv<Epi><<<grid_for(nrows), kBlock, 0, st>>>(
         [&] {
             MgFields F{};
@@ -4222,7 +4664,7 @@ int mg_transfer_mf(const mpbp_mg* m, int l, int32_t which, int32_t nrows, const 
             }
             return F;
         }(),
-        m->tr_n0 >> l, which, nrows, x, epi);
+        MgDiv{divu((uint32_t)nr * (uint32_t)nr), divu((uint32_t)nr)}, n, which, nrows, x, epi);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
@@ -4337,6 +4779,13 @@ int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, 
     return MPBP_OK;
 }
 
+// Level 1 as R_0 (F (P_0 x)): tolerance-mode F stencil level 0 on one GPU, matrix-free transfers, level 1 smoothed.
+bool mg_gal_ok(const mpbp_mg* m, const MgFine& f) {
+    const OpRef& o = f.op.in;
+    return g_mg_gal && o.stencil && o.sop == SOP_F && o.stencil->f_numerics == MPBP_NUMERICS_FAST && o.which == 0 &&
+           f.op.bd.empty && !f.halo && !o.stencil->halo && m->nlevels > 2 && use_mf_transfer(m, 0) && f.r && f.d;
+}
+
 // One V-cycle on level l for A_l x = b.  Level 0 uses `fine` (operator and buffers); coarser levels their
 // mpbp_mg_level.  *res receives the result's buffer (dst when given).  Row partition (m->part_levels > 0): levels
 // l < part_levels hold owned rows (vectors read by an operator carry ghost rows, refreshed by mg_exchange); the
@@ -4347,7 +4796,13 @@ int mg_vcycle(const mpbp_mg* m, int l, const MgFine& fine, const double* b, bool
               const double* sub, double** res, hipStream_t st) {
     const mpbp_mg_level& L = m->levels[l];
     const bool top = l == 0;
-    const OpPair o = top ? fine.op : mg_level_op(L);
+    OpPair o = top ? fine.op : mg_level_op(L);
+    MgGal gal{m, fine.op.in, fine.r, fine.d};   // (fine.r, fine.d: dead while level 1 runs)
+    if (l == 1 && mg_gal_ok(m, fine)) {
+        o.in = OpRef{nullptr, nullptr, nullptr, nullptr, false, 0, SOP_NONE};
+        o.in.gal = &gal;
+        o.bd = OpRef{nullptr, nullptr, nullptr, nullptr, true, 0, SOP_NONE};
+    }
     const double* diag = top ? fine.diag : L.diag;
     double* bx = top ? fine.x : L.x;
     double* bt = top ? fine.t : L.t;
@@ -4422,6 +4877,43 @@ int d_rhs_x0(const mpbp_schur_plan* p, const double* Y, const double* v_p, doubl
     return launch_march(DStencilDev{P}, XPlain{Y}, EpiAddX0{v_p, rhs, p->diag_P, c2, x0}, pg_rows(), st);
 }
 
+// x = Gt_G^-1 b by the plan's Chebyshev inner solve in one k_gtg_solve launch (one GPU, matrix-free Gt_G, 2..6 sweeps).
+template <int H>
+int launch_gtg_solve_t(const GtGStencilDev& S, const double* b, const double* diag, const ChebK& ck, double* out,
+                       hipStream_t st) {
+    const int64_t tiles = (int64_t)((S.n + kGTW - 1) / kGTW) * ((S.n + kGTH - 1) / kGTH);
+    k_gtg_solve<H><<<(unsigned)tiles, 256, 0, st>>>(S, b, diag, ck, out);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+bool gtg_fused_ok(const mpbp_schur_plan* p) {
+    const mpbp_inner_solver& in = p->inner_P;
+    return g_gtg_fused && p->pg_stencil && !p->halo && in.kind == MPBP_INNER_CHEBYSHEV && in.sweeps >= 2 &&
+           in.sweeps <= 6 && in.lmax > in.lmin && in.lmin >= 0.0;
+}
+int gtg_solve_fused(const mpbp_schur_plan* p, const double* b, double* out, hipStream_t st) {
+    PGDev P;
+    const int rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &P);
+    if (rc) return rc;
+    const int K = p->inner_P.sweeps;
+    ChebK ck{};
+    double c1[64] = {}, c2[64] = {};
+    cheb_coeffs(p->inner_P.lmin, p->inner_P.lmax, K, c1, c2);
+    for (int s = 0; s < K; ++s) {
+        ck.c1[s] = c1[s];
+        ck.c2[s] = c2[s];
+    }
+    const GtGStencilDev S{P};
+    switch (K - 1) {
+    case 1: return launch_gtg_solve_t<1>(S, b, p->diag_P, ck, out, st);
+    case 2: return launch_gtg_solve_t<2>(S, b, p->diag_P, ck, out, st);
+    case 3: return launch_gtg_solve_t<3>(S, b, p->diag_P, ck, out, st);
+    case 4: return launch_gtg_solve_t<4>(S, b, p->diag_P, ck, out, st);
+    case 5: return launch_gtg_solve_t<5>(S, b, p->diag_P, ck, out, st);
+    default: return set_error(MPBP_ERR_ARG, "gtg_solve_fused: 2..6 sweeps");
+    }
+}
+
 // The first sweep of a Gt_G Chebyshev solve staging a precomputed x0 = d0 (one GPU, matrix-free Gt_G).
 int gtg_first_sweep_x0(const mpbp_schur_plan* p, const double* x0, const double* b, double c1, double c2, double* d,
                        const double* sub, double* xo, int store_d, hipStream_t st) {
@@ -4429,6 +4921,26 @@ int gtg_first_sweep_x0(const mpbp_schur_plan* p, const double* x0, const double*
     const int rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &P);
     if (rc) return rc;
     return launch_march(GtGStencilDev{P}, XPlain{x0}, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, pg_rows(), st);
+}
+
+// The last two sweeps of a tolerance-mode F Chebyshev solve fused (k_march2): one GPU whole grid, or (ext >= 0) the CA
+// schedule's owned + ext ghost rows.
+bool f_pair_ok(const mpbp_schur_plan* p) { return p->f_numerics == MPBP_NUMERICS_FAST && g_f_pair && p->f_stencil; }
+template <class BS = BNone>
+int f_pair(const mpbp_schur_plan* p, int ext, const double* x_in, const double* b, double* dir, double c1a, double c2a,
+           double c1b, double c2b, const double* sub, double* x_out, hipStream_t st, const BS& bs = BS{}) {
+    FStencilDev P;
+    int rc;
+    if (ext >= 0) {
+        OpRef o{nullptr, nullptr, nullptr, p, false, 3, SOP_F};
+        o.ext = ext;
+        const mpbp_row_part q = stencil_part(o);
+        rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, &P);
+    } else {
+        rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &P);
+    }
+    if (rc) return rc;
+    return launch_march2(P, Fused2{x_in, dir, b, sub, x_out, nullptr, c1a, c2a, c1b, c2b}, st, bs);
 }
 
 // x = M^-1 b by `inner` sweeps from x0 = 0 (solve.py:251/254 F_inv / Gt_G_factorization roles).
@@ -4477,8 +4989,12 @@ int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag
                   : mpbp_jacobi_init(nrows, b, diag, s0, cur, (void*)c.st);
         if (rc) return rc;
     }
-    for (; s < K; ++s) {
-        const bool last = s == K - 1;
+    // tolerance-mode F on one GPU: the last two sweeps as one fused launch
+    const bool pair_ok = cheb && f_pair_ok(c.p) && op.in.stencil && op.in.sop == SOP_F && op.bd.empty &&
+                         op.in.which == 0 && !c.p->halo;
+    while (s < K) {
+        const bool pair = pair_ok && s == K - 2;
+        const bool last = s == K - 1 || pair;
         double* nxt = last ? dst : (cur == ping ? pong : ping);
         const double* sb = last ? sub : nullptr;
         const mpbp_schur_plan* p = c.p;
@@ -4486,16 +5002,20 @@ int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag
         const bool rec = profile && p->prof_events && p->prof_count && *p->prof_count < p->prof_capacity &&
                          hipStreamIsCapturing(c.st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone;
         if (rec) MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count], c.st));
-        rc = two_phase(c, kind, cur, op, [&](const OpRef& o) {
-            return cheb ? op_cheb(o, cur, b, diag, c1[s], c2[s], dir, sb, nxt, c.st, last ? 0 : 1)
-                        : op_jacobi(o, cur, b, diag, sb, nxt, c.st);
-        });
+        if (pair)
+            rc = f_pair(p, -1, cur, b, dir, c1[s], c2[s], c1[s + 1], c2[s + 1], sb, nxt, c.st);
+        else
+            rc = two_phase(c, kind, cur, op, [&](const OpRef& o) {
+                return cheb ? op_cheb(o, cur, b, diag, c1[s], c2[s], dir, sb, nxt, c.st, last ? 0 : 1)
+                            : op_jacobi(o, cur, b, diag, sb, nxt, c.st);
+            });
         if (rc) return rc;
         if (rec) {
             MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count + 1], c.st));
             ++*p->prof_count;
         }
         cur = nxt;
+        s += pair ? 2 : 1;
     }
     return MPBP_OK;
 }
@@ -4525,23 +5045,28 @@ int f_solve_gx(const Ctx& c, const double* xp, const mpbp_inner_solver& in, doub
                                                                  K == 2 ? 0 : 1}, g_march_rows, c.st, bs);
     });
     if (rc) return rc;
-    for (int s = 2; s < K; ++s) {
-        const bool last = s == K - 1;
+    for (int s = 2; s < K;) {
+        const bool pair = f_pair_ok(p) && s == K - 2;
+        const bool last = s == K - 1 || pair;
         double* nxt = last ? dst : (cur == ping ? pong : ping);
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         const bool rec = profile && p->prof_events && p->prof_count && *p->prof_count < p->prof_capacity &&
                          hipStreamIsCapturing(c.st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone;
         if (rec) MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count], c.st));
-        rc = with_f_policy(P, p->f_numerics == MPBP_NUMERICS_FAST, [&](const auto& Q) {
-            return launch_march(Q, XPlain{cur}, EpiCheb{cur, nullptr, nullptr, dir, c1[s], c2[s], last ? sub : nullptr,
-                                                        nxt, last ? 0 : 1}, g_march_rows, c.st, bs);
-        });
+        if (pair)
+            rc = f_pair(p, -1, cur, nullptr, dir, c1[s], c2[s], c1[s + 1], c2[s + 1], sub, nxt, c.st, bs);
+        else
+            rc = with_f_policy(P, p->f_numerics == MPBP_NUMERICS_FAST, [&](const auto& Q) {
+                return launch_march(Q, XPlain{cur}, EpiCheb{cur, nullptr, nullptr, dir, c1[s], c2[s], last ? sub : nullptr,
+                                                            nxt, last ? 0 : 1}, g_march_rows, c.st, bs);
+            });
         if (rc) return rc;
         if (rec) {
             MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count + 1], c.st));
             ++*p->prof_count;
         }
         cur = nxt;
+        s += pair ? 2 : 1;
     }
     return MPBP_OK;
 }
@@ -4582,22 +5107,27 @@ int ca_inner_solve(const Ctx& c, int32_t sop, const double* b, const double* dia
     int rc = op_first_sweep(ext_op(p, sop, d_out + K - 2), cheb, b, diag_ext, c2[0], c1[1], c2[1], dir,
                             K == 2 ? sub : nullptr, cur, c.st, K == 2 ? 0 : 1);
     if (rc) return rc;
-    for (int s = 2; s < K; ++s) {
-        const bool last = s == K - 1;
+    for (int s = 2; s < K;) {
+        const bool pair = cheb && sop == SOP_F && f_pair_ok(p) && s == K - 2;
+        const bool last = s == K - 1 || pair;
         double* nxt = last ? dst : (cur == ping ? pong : ping);
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         const bool rec = profile && p->prof_events && p->prof_count && *p->prof_count < p->prof_capacity &&
                          hipStreamIsCapturing(c.st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone;
         if (rec) MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count], c.st));
         const OpRef o = ext_op(p, sop, d_out + K - 1 - s);
-        rc = cheb ? op_cheb(o, cur, b, nullptr, c1[s], c2[s], dir, last ? sub : nullptr, nxt, c.st, last ? 0 : 1)
-                  : op_jacobi(o, cur, b, nullptr, last ? sub : nullptr, nxt, c.st);
+        if (pair)   // level B on d_out ghost rows (the last sweep's), level A one deeper (sweep K-2's)
+            rc = f_pair(p, d_out, cur, b, dir, c1[s], c2[s], c1[s + 1], c2[s + 1], sub, nxt, c.st);
+        else
+            rc = cheb ? op_cheb(o, cur, b, nullptr, c1[s], c2[s], dir, last ? sub : nullptr, nxt, c.st, last ? 0 : 1)
+                      : op_jacobi(o, cur, b, nullptr, last ? sub : nullptr, nxt, c.st);
         if (rc) return rc;
         if (rec) {
             MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count + 1], c.st));
             ++*p->prof_count;
         }
         cur = nxt;
+        s += pair ? 2 : 1;
     }
     return MPBP_OK;
 }
@@ -4629,24 +5159,30 @@ int ca_f_solve_gx(const Ctx& c, const double* xp, const mpbp_inner_solver& in, d
                                                                  K == 2 ? 0 : 1}, g_march_rows, c.st, bs);
     });
     if (rc) return rc;
-    for (int s = 2; s < K; ++s) {
-        const bool last = s == K - 1;
+    for (int s = 2; s < K;) {
+        const bool pair = f_pair_ok(p) && s == K - 2;
+        const bool last = s == K - 1 || pair;
         double* nxt = last ? dst : (cur == ping ? pong : ping);
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         const bool rec = profile && p->prof_events && p->prof_count && *p->prof_count < p->prof_capacity &&
                          hipStreamIsCapturing(c.st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone;
         if (rec) MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count], c.st));
-        if ((rc = fpol(K - 1 - s, &P))) return rc;
-        rc = with_f_policy(P, p->f_numerics == MPBP_NUMERICS_FAST, [&](const auto& Q) {
-            return launch_march(Q, XPlain{cur}, EpiCheb{cur, nullptr, nullptr, dir, c1[s], c2[s], last ? sub : nullptr,
-                                                        nxt, last ? 0 : 1}, g_march_rows, c.st, bs);
-        });
+        if (pair) {
+            rc = f_pair(p, 0, cur, nullptr, dir, c1[s], c2[s], c1[s + 1], c2[s + 1], sub, nxt, c.st, bs);
+        } else {
+            if ((rc = fpol(K - 1 - s, &P))) return rc;
+            rc = with_f_policy(P, p->f_numerics == MPBP_NUMERICS_FAST, [&](const auto& Q) {
+                return launch_march(Q, XPlain{cur}, EpiCheb{cur, nullptr, nullptr, dir, c1[s], c2[s], last ? sub : nullptr,
+                                                            nxt, last ? 0 : 1}, g_march_rows, c.st, bs);
+            });
+        }
         if (rc) return rc;
         if (rec) {
             MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count + 1], c.st));
             ++*p->prof_count;
         }
         cur = nxt;
+        s += pair ? 2 : 1;
     }
     return MPBP_OK;
 }
@@ -4749,8 +5285,11 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
     int rc;
     // one GPU, matrix-free D and Gt_G, Chebyshev Gt_G solves: b's producers (D, Gt_F_G) also write the first Gt_G
     // sweep's x0 = c2[0] b / diag into P0 (the solve's ping buffer, first overwritten by its second sweep)
-    const bool px0 = p->pg_stencil && !p->halo && p->inner_P.kind == MPBP_INNER_CHEBYSHEV && p->inner_P.sweeps >= 2 &&
-                     p->inner_P.lmax > p->inner_P.lmin && p->inner_P.lmin >= 0.0 && p->inner_P.sweeps <= 64;
+    // ... unless each Gt_G solve runs as one fused launch (k_gtg_solve), which builds x0 itself
+    const bool gfuse = gtg_fused_ok(p);
+    const bool px0 = !gfuse && p->pg_stencil && !p->halo && p->inner_P.kind == MPBP_INNER_CHEBYSHEV &&
+                     p->inner_P.sweeps >= 2 && p->inner_P.lmax > p->inner_P.lmin && p->inner_P.lmin >= 0.0 &&
+                     p->inner_P.sweeps <= 64;
     double pc1[64] = {}, pc2[64] = {};
     if (px0) cheb_coeffs(p->inner_P.lmin, p->inner_P.lmax, p->inner_P.sweeps, pc1, pc2);
     // 1. Finv_v = F_inv @ v[:F.shape[1]]                                   solve.py:258
@@ -4764,8 +5303,9 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
                        [&](const OpRef& o) { return op_spmv(o, MPBP_SPMV_ADD, Y, v_p, Prhs, c.st); });
     if (rc) return rc;
     // 3. x_a = Gt_G_factorization @ rhs_interim                             solve.py:265
-    rc = inner_solve(c, MPBP_VEC_PRESSURE, P, p->diag_P, p->inner_P, p->np, Prhs, Pxa, nullptr, P0, P1, Pd, false,
-                     px0 ? P0 : nullptr);
+    rc = gfuse ? gtg_solve_fused(p, Prhs, Pxa, c.st)
+               : inner_solve(c, MPBP_VEC_PRESSURE, P, p->diag_P, p->inner_P, p->np, Prhs, Pxa, nullptr, P0, P1, Pd, false,
+                             px0 ? P0 : nullptr);
     if (rc) return rc;
     // 4. x_b = Gt_F_G @ x_a                                                solve.py:267
     //    (one GPU: the diamond layout when the plan has it)
@@ -4781,8 +5321,9 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
     // 5. x_p = Gt_G_factorization @ x_b                                    solve.py:271
     //    (one GPU: straight into the output, which G then reads; a partition needs x_p's ghost rows)
     if (!p->halo) Pxp = out_p;
-    rc = inner_solve(c, MPBP_VEC_PRESSURE, P, p->diag_P, p->inner_P, p->np, Pxb, Pxp, nullptr, P0, P1, Pd, false,
-                     qx0 ? P0 : nullptr);
+    rc = gfuse ? gtg_solve_fused(p, Pxb, Pxp, c.st)
+               : inner_solve(c, MPBP_VEC_PRESSURE, P, p->diag_P, p->inner_P, p->np, Pxb, Pxp, nullptr, P0, P1, Pd, false,
+                             qx0 ? P0 : nullptr);
     if (rc) return rc;
     if (Pxp != out_p)
         MPBP_HIP(hipMemcpyAsync(out_p, Pxp, sizeof(double) * (size_t)p->np, hipMemcpyDeviceToDevice, c.st));

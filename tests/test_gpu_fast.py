@@ -203,3 +203,60 @@ def test_numerics_argument_checked():
     _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
     with pytest.raises(ValueError):
         mp.ApproxSchurPreconditioner(F, D, G, numerics="approximate")
+
+
+@pytest.mark.parametrize("n,kf,kp", [(256, 4, 4), (255, 4, 3), (300, 6, 4), (64, 5, 2), (17, 4, 4)])
+def test_fused_pair_equals_two_sweeps(n, kf, kp):
+    """k_march2 (the last two sweeps of a fast F solve in one launch, x_s kept in LDS; also with G x_p recomputed in the
+    second solve) performs each sweep's IEEE operations: bit-identical to two k_march sweeps, on grids that are and are
+    not multiples of the 256-column strip."""
+    mp = _mp()
+    from mp_block_preconditioners_amd._lib import check, lib
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("chebyshev", kf),
+                                      inner_P=mp.InnerSolver("chebyshev", kp), numerics="fast")
+    assert pc.fuse_g
+    v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda",
+                    generator=torch.Generator(device="cuda").manual_seed(n))
+    try:
+        check(lib().mpbp_set_f_pair(0))
+        ref = pc.apply(v).clone()
+        check(lib().mpbp_set_f_pair(1))
+        got = pc.apply(v)
+    finally:
+        check(lib().mpbp_set_f_pair(1))
+    assert torch.equal(got, ref), float((got - ref).abs().max())
+    nofuse = mp.ApproxSchurPreconditioner(F, D, G, pc.GtG, pc.GtFG, inner_F=mp.InnerSolver("chebyshev", kf),
+                                          inner_P=mp.InnerSolver("chebyshev", kp), numerics="fast", fuse_g=False)
+    assert torch.equal(nofuse.apply(v), got)   # G x_p recomputed == G launched + W streamed, with the pair
+
+
+@pytest.mark.parametrize("n", [64, 256])
+def test_matrix_free_galerkin_level1(n):
+    """Fast F hierarchies apply level 1 as R_0 (F (P_0 x)) (MgGal) instead of streaming the stored Galerkin product:
+    the same operator, so the multigrid apply stays within 1e-10 of the stored-level-1 apply (and of the exact one)."""
+    mp = _mp()
+    from mp_block_preconditioners_amd._lib import check, lib
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    kw = dict(inner_F=mp.InnerSolver("mg", 1), inner_P=mp.InnerSolver("mg", 1))
+    fast = mp.ApproxSchurPreconditioner(F, D, G, numerics="fast", **kw)
+    assert len(fast.mg_F.sizes) > 2
+    v = torch.randn(fast.shape[0], dtype=torch.float64, device="cuda",
+                    generator=torch.Generator(device="cuda").manual_seed(n))
+    try:
+        check(lib().mpbp_set_mg_galerkin_mf(0))
+        stored = fast.apply(v).clone()
+        check(lib().mpbp_set_mg_galerkin_mf(1))
+        got = fast.apply(v).clone()
+    finally:
+        check(lib().mpbp_set_mg_galerkin_mf(1))
+    assert 0.0 < rel_inf(got.cpu().numpy(), stored.cpu().numpy()) <= 1e-10
+    exact = mp.ApproxSchurPreconditioner(F, D, G, fast.GtG, fast.GtFG, **kw)
+    assert rel_inf(got.cpu().numpy(), exact.apply(v).cpu().numpy()) <= 1e-10
+    out = torch.empty_like(v)
+    g = fast.capture(v, out)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, got)

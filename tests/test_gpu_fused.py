@@ -1,0 +1,63 @@
+"""Fused launches of the apply against the per-sweep launches they replace, bit for bit.
+
+k_gtg_solve runs a whole Chebyshev Gt_G solve (solve.py:265 / 271) as one tiled launch: level 0 (x0 = c2 b / diag)
+and every sweep recomputed over a shrinking halo in LDS, each row and update with the per-sweep kernels' IEEE
+operations -- so the apply must not change by a bit whether it is on (default) or off, in both F numerics, on grids
+smaller than, equal to and not a multiple of the 64 x 8 tile.  The exact apply with it on is also pinned against the
+oracle by tests/test_gpu_configs.py."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu(oracle_built):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@pytest.mark.parametrize("n", [3, 5, 17, 64, 100, 256, 300])
+@pytest.mark.parametrize("kp", [2, 3, 4, 6])
+@pytest.mark.parametrize("numerics", ["exact", "fast"])
+def test_fused_gtg_solve_equals_per_sweep(n, kp, numerics):
+    import mp_block_preconditioners_amd as mp
+    from mp_block_preconditioners_amd._lib import check, lib
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("chebyshev", 4),
+                                      inner_P=mp.InnerSolver("chebyshev", kp), numerics=numerics)
+    assert pc.pg_stencil is not None
+    v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda",
+                    generator=torch.Generator(device="cuda").manual_seed(n * 10 + kp))
+    try:
+        check(lib().mpbp_set_gtg_fused(0))
+        ref = pc.apply(v).clone()
+        check(lib().mpbp_set_gtg_fused(1))
+        got = pc.apply(v)
+    finally:
+        check(lib().mpbp_set_gtg_fused(1))
+    assert torch.equal(got, ref), float((got - ref).abs().max())
+
+
+def test_fused_gtg_solve_vs_oracle_256():
+    """configs[1] with the fused pressure solves: the whole apply bit-exact against oracle/schur_oracle.py."""
+    import mp_block_preconditioners_amd as mp
+    from oracle.schur_oracle import Inner, approx_schur_apply
+    from oracle.stokes_oracle import StokesSystem, theta_tables
+    n = 256
+    tabs = theta_tables(n)
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    bp.set_theta_tables(*tabs)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("chebyshev", 4),
+                                      inner_P=mp.InnerSolver("chebyshev", 5))
+    osys = StokesSystem(n, 1.0, 100.0, 1.0, 1.0, -1.0, tables=tabs)
+    v = np.random.default_rng(7).standard_normal(pc.shape[0])
+    got = pc.apply(torch.from_numpy(v).cuda()).cpu().numpy()
+    ref = approx_schur_apply(osys.F, osys.D, osys.G, osys.GtG, osys.GtFG, v,
+                             Inner("chebyshev", 4, pc.inner_F.lmin, pc.inner_F.lmax),
+                             Inner("chebyshev", 5, pc.inner_P.lmin, pc.inner_P.lmax))
+    assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))

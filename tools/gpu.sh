@@ -57,7 +57,8 @@ step() {
     probe:*) timeout -k 10 120 python -u tools/capture_probe.py $(echo "${s#probe:}" | tr , ' ') \
                > "$OUT/probe_${s#probe:}_${MPBP_HALO_CAPTURED_DESTROY:-leak}.log" 2>&1 ;;
     prof) prof prof 300 --kernel-trace --stats --output-format csv -d "$ROOTD/$OUT/prof" -o run -- \
-            python "$ROOTD/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-solve $BENCH_ARGS ;;
+            python "$ROOTD/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-solve $BENCH_ARGS &&
+          python tools/prof_summary.py "$OUT/prof/run_kernel_trace.csv" > "$OUT/prof_summary.md" 2>&1 ;;
     pmc) for C in FETCH_SIZE WRITE_SIZE; do
            prof "pmc_apply_$C" 150 --pmc $C --output-format csv -d "$ROOTD/$OUT/pmc_apply_$C" -o pmc -- \
              python "$ROOTD/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-spmv --no-graph --no-solve || return 1
