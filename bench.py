@@ -34,7 +34,7 @@ def parse_inner(s):
     return kind, int(k or 4)
 
 
-def sweep_bytes(pc, layout, kind, sweeps, fused_init):
+def sweep_bytes(pc, layout, kind, sweeps, fused_init, f_tile=False):
     """Algorithmic HBM bytes of the F inner-solve launches bench.py times: one (bytes, solve) per recorded launch of
     one apply, in record order, and the kernel's name.
 
@@ -61,8 +61,10 @@ def sweep_bytes(pc, layout, kind, sweeps, fused_init):
             pol = "FStencilFast"
         fixed, kname = 3 * 8 * (nF // 4), f"k_march<{pol}, XPlain, EpiCheb> (F sweep, matrix-free)"
         if pair:
-            kname = ("k_march2<FStencilFast> (the F solve's last two Chebyshev sweeps in one launch, matrix-free, "
-                     "tolerance mode)")
+            kname = ("k_ftile<pair> (the F solve's last two Chebyshev sweeps in one launch on 64 x 8 tiles, "
+                     "matrix-free, tolerance mode)" if f_tile else
+                     "k_march2<FStencilFast> (the F solve's last two Chebyshev sweeps in one marching launch, "
+                     "matrix-free, tolerance mode)")
     elif layout == "sell":
         fixed = nnzF * 12 + nF * 1 + pc.sell_of("F").nslices * 16
         kname = "k_sell_rows<EpiCheb> (F sweep, SELL-64)"
@@ -130,6 +132,9 @@ def main():
                     help="fast numerics: 1 (default) runs an F solve's last two sweeps as one k_march2 launch, 0 as two")
     ap.add_argument("--f-direct", type=int, default=None,
                     help="fast numerics: 1 runs the single F sweeps on the direct kernel (one thread per cell, no LDS)")
+    ap.add_argument("--f-tile", type=int, default=None,
+                    help="fast numerics: 1 (default) runs an F solve's x0 + first sweep and its last pair on 2D tiles, "
+                         "0 on the marching kernels")
     ap.add_argument("--gtg-fused", type=int, default=None,
                     help="1 (default): each Chebyshev Gt_G solve as one tiled launch; 0: one launch per sweep")
     ap.add_argument("--mg-galerkin-mf", type=int, default=None,
@@ -208,6 +213,8 @@ def main():
         _check(_lib().mpbp_set_f_pair(args.f_pair))
     if args.f_direct is not None:
         _check(_lib().mpbp_set_f_direct(args.f_direct))
+    if args.f_tile is not None:
+        _check(_lib().mpbp_set_f_tile(args.f_tile))
     if args.gtg_fused is not None:
         _check(_lib().mpbp_set_gtg_fused(args.gtg_fused))
     if args.mg_galerkin_mf is not None:
@@ -333,7 +340,9 @@ def main():
     fused_init = getattr(pc, "f_stencil", None) is not None and (not partitioned or pc.ca)
     # the dominant kernel's roofline over the first F solve's plain sweeps (b streamed; 192.9 and 159.4 MB, mean
     # 176.2 MB per launch at 1024^2); the second solve's sweeps (G x_p recomputed when fused) are reported beside it
-    per_apply, kname = sweep_bytes(pc, args.layout, kf, sf, fused_init)
+    # (csrc: the tiled F kernels need n >= 76 on one GPU; below that, or with --f-tile 0, the marching ones run)
+    f_tile = (args.f_tile is None or args.f_tile != 0) and n >= 76 and not partitioned
+    per_apply, kname = sweep_bytes(pc, args.layout, kf, sf, fused_init, f_tile)
     sbytes, avg_sweep_s, n_timed = roofline_of(per_apply, sweep_ms, 1)
     achieved = sbytes / avg_sweep_s / 1e9
     gbytes, g_s, g_timed = roofline_of(per_apply, sweep_ms, 2)
@@ -531,11 +540,13 @@ def partitioned_solver_section(args, n, rank, world, dist, torch, backend):
     del M
     torch.cuda.empty_cache()
     # FGMRES across the ranks (solve_distributed's steps, the fgmres call timed on its own)
-    bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
-    A = bp.get_big_A_matrix(c=1.0, d_u=-1.0)[0]
+    from mp_block_preconditioners_amd import _lib as L
+    from mp_block_preconditioners_amd.distributed import RowPartition
     t0 = time.perf_counter()
-    dA = DistributedMatrix(A, n, 5)
-    del A, bp
+    bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
+    own = torch.from_numpy(RowPartition(n, world, rank).owned_rows(5).astype(np.int32)).cuda()
+    dA = DistributedMatrix(bp.assemble_rows(L.OP_A, own, c=1.0, d_u=-1.0), n, 5, owned_rows=True)
+    del bp
     torch.cuda.empty_cache()
     Md = DistributedSchurPreconditioner(n, args.xi, args.eta_n, args.eta_s, numerics=args.numerics, **mg1)
     torch.cuda.synchronize()

@@ -307,6 +307,14 @@ int mpbp_stokes_fill(const mpbp_stokes_params* prm, int32_t op, const double* ce
                      int32_t* col_idx, double* val, void* stream);
 /* row_ptr[0] = 0, row_ptr[i+1] = row_ptr[i] + row_nnz[i] (device); *total (host) = row_ptr[n].
  * Setup: synchronises the stream. */
+/* The same for a subset of the operator's rows (a rank's owned + ghost rows, preconditioner.py:299-341 row by row):
+ * row i of the output is operator row rows[i] (0 <= rows[i] < mpbp_stokes_rows), with its global columns -- the
+ * global assembly's rows bit for bit, without assembling the others.  row_ptr is indexed by i (nrows + 1 entries). */
+int mpbp_stokes_count_rows(const mpbp_stokes_params* prm, int32_t op, const double* cell, const int32_t* rows,
+                           int32_t nrows, int32_t* row_nnz, void* stream);
+int mpbp_stokes_fill_rows(const mpbp_stokes_params* prm, int32_t op, const double* cell, const double* uface,
+                          const double* vface, const int32_t* rows, int32_t nrows, const int32_t* row_ptr,
+                          int32_t* col_idx, double* val, void* stream);
 int mpbp_exclusive_scan(const int32_t* row_nnz, int32_t* row_ptr, int64_t n, int64_t* total,
                         void* stream);
 
@@ -445,6 +453,9 @@ int mpbp_set_f_direct(int32_t on);
 /* One-GPU Chebyshev Gt_G solves (2..6 sweeps, matrix-free Gt_G) as ONE tiled launch each (k_gtg_solve: b read once, the
  * iterates in LDS; bit-identical to the per-sweep launches).  1 (default) or 0. */
 int mpbp_set_gtg_fused(int32_t on);
+/* One-GPU tolerance-mode F solves: x0 with the first sweep, and the last two sweeps, as 2D-tile launches (k_ftile: no
+ * LDS ring, one barrier per workgroup; bit-identical to the marching kernels).  1 (default) or 0. */
+int mpbp_set_f_tile(int32_t on);
 /* Tolerance-mode F hierarchies (plan f_numerics FAST, one GPU, matrix-free level 0 and transfers): level 1 applied as
  * R_0 (F (P_0 x)) instead of streaming its stored Galerkin matrix.  1 (default) or 0. */
 int mpbp_set_mg_galerkin_mf(int32_t on);

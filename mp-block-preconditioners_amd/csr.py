@@ -97,7 +97,13 @@ class DeviceCSR:
             order = np.lexsort((gid, starts - gid * gsize))   # by position within the field, then field
             pairs = pairs.reshape(-1, 2)[order].reshape(-1)
         pairs = np.ascontiguousarray(pairs)
-        return RowBlockList(torch.from_numpy(pairs).to(self.device), rp, pairs)
+        blk = RowBlockList(torch.from_numpy(pairs).to(self.device), rp, pairs)
+        blk.owner = self._identity()
+        return blk
+
+    def _identity(self):
+        """What a row-block plan (its wave table in particular) was built from: this matrix's row structure."""
+        return (self.row_ptr.data_ptr(), self.shape[0], self.nnz)
 
     @property
     def blocks(self):
@@ -116,7 +122,13 @@ class DeviceCSR:
             raise ValueError(f"order must be 'seq' or 'seg', not {order!r}")
         if out is None:
             out = torch.empty(self.shape[0], dtype=torch.float64, device=self.device)
-        blk = (blocks or self.blocks).cstruct()
+        bl = blocks or self.blocks
+        # the wave table's fast path trusts row lengths read from the row_ptr the plan was made from: blocks planned
+        # for another matrix (same shape, other pattern) would read wrong entries, so refuse them
+        owner = getattr(bl, "owner", None)
+        if owner is not None and owner != self._identity():
+            raise ValueError("matvec: these row blocks were planned for another matrix (plan_blocks on this one)")
+        blk = bl.cstruct()
         fn = lib().mpbp_spmv if order == "seq" else lib().mpbp_spmv_seg
         check(fn(ctypes.byref(self.cstruct()), ctypes.byref(blk), mode, ptr(x), ptr(z), ptr(out), stream_handle()))
         return out
@@ -242,6 +254,7 @@ class RowBlockList:
         self.pairs = pairs
         self.count = pairs.numel() // 2
         self.table = None
+        self.owner = None   # DeviceCSR._identity() of the matrix it was planned for (plan_blocks sets it)
         if row_ptr_host is not None and self.count:
             ph = pairs_host if pairs_host is not None else pairs.cpu().numpy()
             self.table = torch.from_numpy(wave_table(row_ptr_host, ph.reshape(-1, 2))).to(pairs.device)

@@ -28,11 +28,9 @@ int g_init_diag = 1;      // fused first F sweep: 1 rebuilds the staged diagonal
 int g_mg_gal = 1;          // tolerance-mode F hierarchies: level 1 as R_0 (F (P_0 x)) (MgGal; 0: its stored matrix)
 int g_f_direct = 0;        // tolerance-mode F sweeps on the direct kernel (one thread per cell, no LDS) instead of marching
 int g_gtg_fused = 1;       // one-GPU Chebyshev Gt_G solves of 2..6 sweeps as one k_gtg_solve launch (0: per sweep)
+int g_f_tile = 1;          // one-GPU tolerance-mode F: x0 + sweep 1, and the last pair, on 2D tiles (k_ftile)
 int g_f_pair = 1;         // tolerance-mode F solves: the last two Chebyshev sweeps as one k_march2 launch (0: two)
-#ifndef MPBP_PG_ROWS
-#define MPBP_PG_ROWS 0    // rows per workgroup of the D / G / Gt_G marching kernels (0: as F)
-#endif
-inline int pg_rows() { return MPBP_PG_ROWS > 0 ? MPBP_PG_ROWS : g_march_rows; }
+inline int pg_rows() { return g_march_rows; }   // rows per workgroup of the D / G / Gt_G marching kernels: as F
 
 int set_error(int code, const char* fmt, ...) {
     va_list ap;
@@ -55,38 +53,20 @@ constexpr int kBlock = 256;                    // 4 wave64 per workgroup, one ro
 
 inline int grid_for(int64_t n, int block = kBlock) { return (int)((n + block - 1) / block); }
 
-// Cache policy of the once-touched streams.  The SELL kernel reads its matrix (touched once per SpMV)
-// and writes its result with nontemporal hints (MPBP_SELL_NT, default on: +2-4 % on the 1024^2 A SpMV);
-// the stencil kernels keep default-policy loads and stores (their x / b / d vectors are re-read by the
-// next sweep from the cache; nontemporal costs them 3-7 %).  MPBP_NT_LOAD / MPBP_NT_STORE force the hint
-// on every epilogue load / store (experiment builds, tools/build_variants.py).
-#ifndef MPBP_SELL_NT
-#define MPBP_SELL_NT 1
-#endif
-#ifndef MPBP_NT_LOAD
-#define MPBP_NT_LOAD 0
-#endif
-#ifndef MPBP_NT_STORE
-#define MPBP_NT_STORE 0
-#endif
+// Cache policy of the once-touched streams.  The SELL and CSR kernels read their matrix (touched once per SpMV)
+// and write their result with nontemporal hints (+2-4 % on the 1024^2 A SpMV); the stencil kernels keep
+// default-policy loads and stores (their x / b / d vectors are re-read by the next sweep from the cache;
+// nontemporal costs them 3-7 %).
+constexpr bool kSellNT = true, kCsrNT = true;
 template <class T>
-__device__ inline T ld_stream(const T* p) {
-#if MPBP_NT_LOAD
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
-}
+__device__ inline T ld_stream(const T* p) { return *p; }
 template <bool NT = false, class T>
 __device__ inline void st_stream(T* p, T v) {
-    if constexpr (NT || MPBP_NT_STORE) __builtin_nontemporal_store(v, p);
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef int i32x2 __attribute__((ext_vector_type(2)));
-#ifndef MPBP_CSR_NT
-#define MPBP_CSR_NT 1
-#endif
 template <bool NT>
 __device__ inline double2 ld_matrix(const double2* p) {
     if constexpr (NT) {
@@ -346,21 +326,23 @@ __device__ void build_row(const StokesDev& P, int op, int32_t R, RowBuf& o) {
     }
 }
 
-__global__ void k_stokes_count(StokesDev P, int op, int64_t nrows, int32_t* row_nnz) {
-    const int64_t R = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (R >= nrows) return;
+// rows (optional): the operator rows to assemble, in order (a rank's owned + ghost rows); the output CSR's row i is
+// operator row rows[i] with its global columns.  NULL: every row.
+__global__ void k_stokes_count(StokesDev P, int op, int64_t nrows, int32_t* row_nnz, const int32_t* rows = nullptr) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nrows) return;
     RowBuf o;
-    build_row(P, op, (int32_t)R, o);
-    row_nnz[R] = o.m;
+    build_row(P, op, rows ? rows[i] : (int32_t)i, o);
+    row_nnz[i] = o.m;
 }
 
 __global__ void k_stokes_fill(StokesDev P, int op, int64_t nrows, const int32_t* rp, int32_t* ci,
-                              double* va) {
-    const int64_t R = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (R >= nrows) return;
+                              double* va, const int32_t* rows = nullptr) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nrows) return;
     RowBuf o;
-    build_row(P, op, (int32_t)R, o);
-    const int32_t base = rp[R];
+    build_row(P, op, rows ? rows[i] : (int32_t)i, o);
+    const int32_t base = rp[i];
     for (int k = 0; k < o.m; ++k) {
         ci[base + k] = o.col[k];
         va[base + k] = o.val[k];
@@ -872,13 +854,10 @@ struct EpiChebT {
     __device__ bool has_sub() const { return FIXED ? SUB : sub != nullptr; }
     __device__ bool stores_d() const { return FIXED ? SD : store_d != 0; }
     __device__ P pre(int32_t r) const { return {xin[r], ld_stream(b + r), diag ? diag[r] : 0.0, ld_stream(d + r), sub ? ld_stream(sub + r) : 0.0}; }
-#ifndef MPBP_GX_SUB_LATE
-#define MPBP_GX_SUB_LATE 1
-#endif
-    // BX && MPBP_GX_SUB_LATE: `sub` is loaded in the epilogue itself instead of ahead of the row -- the fused
+    // BX: `sub` is loaded in the epilogue itself instead of ahead of the row -- the fused
     // second solve's last sweep otherwise spills (128 VGPRs + 24 B scratch): 40.9 -> 38.9 us per launch
     // (2541-2565 -> 2573-2640 applies/s, A/B on one box)
-    static constexpr bool kSubLate = BX && MPBP_GX_SUB_LATE;
+    static constexpr bool kSubLate = BX;
     __device__ P pre_lite(int32_t r) const { return {0.0, BX ? 0.0 : ld_stream(b + r), 0.0, ld_stream(d + r), (has_sub() && !kSubLate) ? ld_stream(sub + r) : 0.0}; }
     template <bool NT = false>
     __device__ void apply(int32_t r, double acc, const P& p) const {
@@ -1006,16 +985,9 @@ __device__ inline void set_diag<EpiAddX0::P>(EpiAddX0::P&, double) {}
 // wave-instruction's x addresses the same stencil neighbour of 64 consecutive rows instead of all
 // neighbours of ~10 rows: fewer cache lines per instruction (153 vs 172 us for the 1024^2 A).  A 1024^2
 // A row block (12 entries per velocity row) is one chunk per wave.
-// MPBP_CSR_TGATHER=0 selects the earlier order: gather in entry order, stage the products (6 KiB).
 // Measured dead end: no staging at all, each lane loading its own row (16-byte loads 96 B apart across
 // the wave) -- 567 us, the texture addresser then touches ~48 cache lines per wave-instruction.
-#ifndef MPBP_CSR_WAVECAP
-#define MPBP_CSR_WAVECAP 768
-#endif
-#ifndef MPBP_CSR_TGATHER
-#define MPBP_CSR_TGATHER 1
-#endif
-constexpr int kWaveCap = MPBP_CSR_WAVECAP;     // entries per wave chunk (64 rows x 12 entries)
+constexpr int kWaveCap = 768;                 // entries per wave chunk (64 rows x 12 entries)
 constexpr int kWavePairs = kWaveCap / 128;     // 16-byte loads per lane per chunk
 constexpr int kRowBatch = 8;                   // pairs of a row gathered at once (16 entries)
 
@@ -1037,40 +1009,30 @@ __device__ inline void wave_lds_sync() {
 // F's rows 10) from an even start: its entries are exactly one chunk, lane l's row is pairs
 // [l*LEN/2, (l+1)*LEN/2) of it, so the loads, LDS transposition, gathers and sums unroll with no
 // per-entry bounds tests.  Same additions in the same order as the general loop (bit-exact).
-#ifndef MPBP_CSR_UNIFORM
-#define MPBP_CSR_UNIFORM 1
-#endif
-#ifndef MPBP_CSR_XBUF
-#define MPBP_CSR_XBUF 1
-#endif
 // XB: x gathered with buffer loads (one descriptor for x, a 32-bit byte offset per entry: no 64-bit
 // address arithmetic per gather); needs ncols * 8 < 2^31.
-// Returns false (nothing stored) when some row of the wave does not hold LEN entries.  MPBP_CSR_SPEC=1: the
+// Returns false (nothing stored) when some row of the wave does not hold LEN entries.  The
 // matrix loads are issued before that check -- they depend on the wave's first entry s alone (and stay inside
 // [s, s + 64 LEN) = the wave's entries), so their HBM latency overlaps the per-row row_ptr loads' instead of
 // following it.
-#ifndef MPBP_CSR_SPEC
-#define MPBP_CSR_SPEC 1
-#endif
 // TRUST: the wave table says the wave is uniform (no row check).
 template <int LEN, bool XB, class Epi, bool TRUST = false>
 __device__ inline bool csr_wave_uniform(const Csr& A, const double* __restrict__ x, int32_t s, int lane,
                                         double2* vs, int2* cs, int32_t ks, int32_t ke, int32_t r, const Epi& epi,
                                         const typename Epi::P& pe) {
     constexpr int P = LEN / 2;   // pairs per row == 16-byte loads per lane
-    if (!TRUST && !MPBP_CSR_SPEC && !__all(ke - ks == LEN)) return false;
     double2 v[P];
     int2 cc[P];
 #pragma unroll
     for (int j = 0; j < P; ++j) {
         const int32_t k = s + 2 * (lane + 64 * j);
-        v[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const double2*>(A.va + k));
-        cc[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const int2*>(A.ci + k));
+        v[j] = ld_matrix<kCsrNT>(reinterpret_cast<const double2*>(A.va + k));
+        cc[j] = ld_matrix<kCsrNT>(reinterpret_cast<const int2*>(A.ci + k));
     }
     // (a compiler memory barrier: the loads above may not sink below the check, which would serialise them
     // behind the row_ptr loads again; it emits no instruction and no wait)
-    if (MPBP_CSR_SPEC) asm volatile("" ::: "memory");
-    if (!TRUST && MPBP_CSR_SPEC && !__all(ke - ks == LEN)) return false;
+    asm volatile("" ::: "memory");
+    if (!TRUST && !__all(ke - ks == LEN)) return false;
 #pragma unroll
     for (int j = 0; j < P; ++j) {
         vs[lane + 64 * j] = v[j];
@@ -1103,15 +1065,12 @@ __device__ inline bool csr_wave_uniform(const Csr& A, const double* __restrict__
         acc += q.x * x0[i];
         acc += q.y * x1[i];
     }
-    epi.template apply<MPBP_CSR_NT != 0>(r, acc, pe);   // every lane holds a row here
+    epi.template apply<kCsrNT>(r, acc, pe);   // every lane holds a row here
     return true;
 }
 
-// The wave table (mpbp_rowblocks.table; MPBP_CSR_TABLE=0 ignores it): a wave flagged uniform starts its matrix loads
+// The wave table (mpbp_rowblocks.table; mpbp_set_csr_table(0) ignores it): a wave flagged uniform starts its matrix loads
 // right after one scalar load of its block's 32-byte table entry -- no dependent row-range load, no row_ptr reads.
-#ifndef MPBP_CSR_TABLE
-#define MPBP_CSR_TABLE 1
-#endif
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(4))) const i32x4 ci32x4;
 template <class Epi>
@@ -1119,12 +1078,9 @@ __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __rest
                                                      const int2* __restrict__ blocks, int nblocks,
                                                      const int32_t* __restrict__ table, Epi epi) {
     __shared__ double2 vstage[kBlock / 64][kWaveCap / 2];
-#if MPBP_CSR_TGATHER
     __shared__ int2 cstage[kBlock / 64][kWaveCap / 2];
-#endif
     const int b = xcd_swizzle(blockIdx.x, nblocks);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#if MPBP_CSR_TABLE && MPBP_CSR_TGATHER && MPBP_CSR_UNIFORM
     if (table && A.ncols > 0 && A.ncols < (1 << 28)) {
         const i32x4 t0 = ((ci32x4*)table)[2 * b], t1 = ((ci32x4*)table)[2 * b + 1];
         const int32_t ra = t0.x + 64 * w;
@@ -1134,14 +1090,13 @@ __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __rest
             const int32_t s = w == 0 ? t0.z : w == 1 ? t0.w : w == 2 ? t1.x : t1.y;
             const int32_t r = ra + lane;
             const typename Epi::P pe = epi.pre(r);
-            constexpr bool XB = MPBP_CSR_XBUF != 0;
+            constexpr bool XB = true;
             if (len == 12) csr_wave_uniform<12, XB, Epi, true>(A, x, s, lane, vstage[w], cstage[w], 0, 0, r, epi, pe);
             else if (len == 10) csr_wave_uniform<10, XB, Epi, true>(A, x, s, lane, vstage[w], cstage[w], 0, 0, r, epi, pe);
             else csr_wave_uniform<8, XB, Epi, true>(A, x, s, lane, vstage[w], cstage[w], 0, 0, r, epi, pe);
             return;
         }
     }
-#endif
     const int2 blk = blocks[b];
     const int32_t ra = __builtin_amdgcn_readfirstlane(blk.x + 64 * w);
     if (ra >= blk.y) return;   // waves are independent: no workgroup barrier below
@@ -1159,11 +1114,10 @@ __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __rest
     double acc = 0.0;
     double2* vs = vstage[w];
     const double* vs1 = reinterpret_cast<const double*>(vs);
-#if MPBP_CSR_TGATHER && MPBP_CSR_UNIFORM
     {
         const int32_t len = (e - s) >> 6;   // wave-uniform
         if (rb - ra == 64 && ((e - s) & 63) == 0 && (s & 1) == 0 && (len == 8 || len == 10 || len == 12)) {
-            constexpr bool XB = MPBP_CSR_XBUF != 0;
+            constexpr bool XB = true;
             bool done;
             if (XB && A.ncols > 0 && A.ncols < (1 << 28))
                 done = len == 12 ? csr_wave_uniform<12, XB>(A, x, s, lane, vs, cstage[w], ks, ke, r, epi, pe)
@@ -1176,7 +1130,6 @@ __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __rest
             if (done) return;
         }
     }
-#endif
     for (int32_t cb = s & ~1; cb < e; cb += kWaveCap) {
         double2 v[kWavePairs];
         int2 cc[kWavePairs];
@@ -1184,8 +1137,8 @@ __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __rest
         for (int j = 0; j < kWavePairs; ++j) {
             const int32_t k = cb + 2 * (lane + 64 * j);
             if (k + 1 < e) {
-                v[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const double2*>(A.va + k));
-                cc[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const int2*>(A.ci + k));
+                v[j] = ld_matrix<kCsrNT>(reinterpret_cast<const double2*>(A.va + k));
+                cc[j] = ld_matrix<kCsrNT>(reinterpret_cast<const int2*>(A.ci + k));
             } else if (k < e) {
                 v[j] = make_double2(A.va[k], 0.0);
                 cc[j] = make_int2(A.ci[k], 0);
@@ -1196,7 +1149,6 @@ __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __rest
         }
         int32_t t = max(ks, cb) - cb;                       // this lane's row within the chunk
         const int32_t tend = min(ke, cb + kWaveCap) - cb;
-#if MPBP_CSR_TGATHER
         if (cb != (s & ~1)) wave_lds_sync();   // the previous chunk's reads are done
         int2* cs = cstage[w];
         const int32_t* cs1 = reinterpret_cast<const int32_t*>(cs);
@@ -1230,28 +1182,8 @@ __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __rest
                 }
             }
         }
-#else
-        double x0[kWavePairs], x1[kWavePairs];
-#pragma unroll
-        for (int j = 0; j < kWavePairs; ++j) {
-            const int32_t k = cb + 2 * (lane + 64 * j);
-            x0[j] = (k >= s && k < e) ? x[cc[j].x] : 0.0;
-            x1[j] = (k + 1 >= s && k + 1 < e) ? x[cc[j].y] : 0.0;
-        }
-        if (cb != (s & ~1)) wave_lds_sync();   // the previous chunk's reads are done
-#pragma unroll
-        for (int j = 0; j < kWavePairs; ++j) vs[lane + 64 * j] = make_double2(v[j].x * x0[j], v[j].y * x1[j]);
-        wave_lds_sync();
-        if ((t & 1) && t < tend) acc += vs1[t++];
-        for (; t + 1 < tend; t += 2) {
-            const double2 q = vs[t >> 1];
-            acc += q.x;
-            acc += q.y;
-        }
-        if (t < tend) acc += vs1[t];
-#endif
     }
-    if (live) epi.template apply<MPBP_CSR_NT != 0>(r, acc, pe);
+    if (live) epi.template apply<kCsrNT>(r, acc, pe);
 }
 
 // ---------------------------------------------------- CSR, segmented reduction ----
@@ -1291,10 +1223,10 @@ __device__ inline bool csr_seg_uniform(const Csr& A, const double* __restrict__ 
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
         const int32_t q = s + 2 * ((j * RPI + rg) * P + kc);
-        v[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const double2*>(A.va + q));
-        c[j] = ld_matrix<MPBP_CSR_NT != 0>(reinterpret_cast<const int2*>(A.ci + q));
+        v[j] = ld_matrix<kCsrNT>(reinterpret_cast<const double2*>(A.va + q));
+        c[j] = ld_matrix<kCsrNT>(reinterpret_cast<const int2*>(A.ci + q));
     }
-    asm volatile("" ::: "memory");           // keep the matrix loads ahead of the row check (as MPBP_CSR_SPEC)
+    asm volatile("" ::: "memory");           // keep the matrix loads ahead of the row check (as csr_wave_uniform)
     if (!__all(ke - ks == LEN)) return false;
     const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(x), (short)0, A.ncols * 8, 0x00020000);
     double t[NI];
@@ -1314,7 +1246,7 @@ __device__ inline bool csr_seg_uniform(const Csr& A, const double* __restrict__ 
         if (k == 0) ys[j * RPI + rg] = t[j];
     }
     wave_lds_sync();
-    epi.template apply<MPBP_CSR_NT != 0>(r, ys[lane], pe);
+    epi.template apply<kCsrNT>(r, ys[lane], pe);
     return true;
 }
 
@@ -1348,7 +1280,7 @@ __global__ void __launch_bounds__(kBlock) k_csr_seg(Csr A, const double* __restr
     }
     double acc = 0.0;
     for (int32_t kk = ks; kk < ke; ++kk) acc += A.va[kk] * x[A.ci[kk]];
-    if (live) epi.template apply<MPBP_CSR_NT != 0>(r, acc, pe);
+    if (live) epi.template apply<kCsrNT>(r, acc, pe);
 }
 
 // ---------------------------------------------- CSR, G lanes per row (small levels) ----
@@ -1435,10 +1367,7 @@ struct Svl {
     const int32_t* edge;
     int n_edge;
 };
-#ifndef MPBP_SVL_BATCH
-#define MPBP_SVL_BATCH 8
-#endif
-constexpr int kSvB = MPBP_SVL_BATCH;  // slots per batch (values + gathers in flight together)
+constexpr int kSvB = 8;  // slots per batch (values + gathers in flight together)
 
 constexpr int kSvMaxDelta = 256;     // nf * K
 constexpr int kSvEdgeG = 8;          // lanes per edge row (k_csr_grp's scheme: one latency chain per row)
@@ -1560,8 +1489,8 @@ __global__ void __launch_bounds__(kBlock) k_sell_rows(Sell S, const double* __re
 #pragma unroll
         for (int j = 0; j < kSellPairs; ++j) {
             if (j0 + j < np) {   // wave-uniform
-                v[j] = ld_matrix<MPBP_SELL_NT != 0>(vp + (size_t)(j0 + j) * 64);
-                c[j] = ld_matrix<MPBP_SELL_NT != 0>(cp + (size_t)(j0 + j) * 64);
+                v[j] = ld_matrix<kSellNT>(vp + (size_t)(j0 + j) * 64);
+                c[j] = ld_matrix<kSellNT>(cp + (size_t)(j0 + j) * 64);
             } else {
                 v[j] = make_double2(0.0, 0.0);
                 c[j] = make_int2(0, 0);
@@ -1584,7 +1513,7 @@ __global__ void __launch_bounds__(kBlock) k_sell_rows(Sell S, const double* __re
     } else {
         for (int j0 = 0; j0 < np; j0 += kSellPairs) batch(j0);
     }
-    if (live) epi.template apply<MPBP_SELL_NT != 0>(r, acc, pe);
+    if (live) epi.template apply<kSellNT>(r, acc, pe);
 }
 
 // ------------------------------------------------------------- F stencil ----
@@ -1939,10 +1868,7 @@ struct FStencilFast : FStencilDev {
 //   (EDGE: the cell is on the grid's border, where periodic wrap reorders the row's columns);
 // and over the source XS of the staged input: the vector itself, or (first inner sweep) the inner
 // solver's x0 = c2 * (b / diag) recomputed from b and diag, so that sweep needs no init pass.
-#ifndef MPBP_MARCH_BLOCK
-#define MPBP_MARCH_BLOCK 256
-#endif
-constexpr int kMB = MPBP_MARCH_BLOCK;   // columns (threads) per marching workgroup
+constexpr int kMB = 256;   // columns (threads) per marching workgroup
 constexpr int kMTileW = kMB + 2;       // + one halo column each side
 struct XRing {
     const double* x;   // [NF][3][kMTileW]
@@ -1964,18 +1890,11 @@ using TRing = TRingT<kMTileW, 1>;
 
 // Staged sources: load(i) issues the loads of element i (raw registers, nothing consumes them yet), value(raw)
 // turns them into the staged value at LDS-store time -- so a tile row's loads stay in flight through the
-// previous row's compute even when the staged value needs arithmetic (XInit's division).  load_uniform(i) is the
-// same for a wave-uniform index: scalar loads (constant address space) into SGPRs, for the tile's two right-hand
-// halo columns, which every lane of a workgroup shares -- no VGPRs held for them between load and store.
-typedef __attribute__((address_space(4))) const double cdouble;
-__device__ inline double ld_uniform(const double* p, int32_t i) {
-    return ((cdouble*)p)[__builtin_amdgcn_readfirstlane(i)];
-}
+// previous row's compute even when the staged value needs arithmetic (XInit's division).
 struct XPlain {        // staged value = x[i]
     const double* __restrict__ x;
     typedef double Raw;
     __device__ Raw load(int32_t i) const { return x[i]; }
-    __device__ Raw load_uniform(int32_t i) const { return ld_uniform(x, i); }
     __device__ double value(const Raw& r) const { return r; }
     __device__ double operator()(int32_t i) const { return x[i]; }
 };
@@ -1988,7 +1907,6 @@ struct XInit {         // staged value = the first inner iterate: c2 * (b[i] / d
     double c2;
     typedef XInitRaw Raw;
     __device__ Raw load(int32_t i) const { return {b[i], dg[i]}; }
-    __device__ Raw load_uniform(int32_t i) const { return {ld_uniform(b, i), ld_uniform(dg, i)}; }
     __device__ double value(const Raw& r) const { return c2 * (r.b / r.d); }
     __device__ double operator()(int32_t i) const { return c2 * (b[i] / dg[i]); }
 };
@@ -2048,19 +1966,12 @@ using GxB = GxBT<false>;
 using GxBPart = GxBT<true>;
 
 // Row of tile values held between its loads and its LDS store: every lane's main column (xa, ta; tile columns
-// c0-1 .. c0+254) in VGPRs, the two halo columns c0+255 and c0+256 (h*, scalar) in SGPRs.
-#ifndef MPBP_HALO_SCALAR
-#define MPBP_HALO_SCALAR 0
-#endif
+// c0-1 .. c0+254) and (lanes 0, 1) the halo columns c0+255, c0+256 (h0, t0).  (Holding the halo columns in SGPRs
+// through scalar loads measured slower)
 template <int NF, class Raw>
 struct TileRow {
     Raw xa[NF], h0[NF];
-#if MPBP_HALO_SCALAR
-    Raw h1[NF];
-    double ta, t0, t1;
-#else
     double ta, t0;
-#endif
 };
 
 // Columns of the strip's right-hand halo (tile columns kMB, kMB + 1) and whether they exist.
@@ -2081,21 +1992,11 @@ __device__ inline void load_tile_row(const S& P, const XS& xs, int gr, int gcA, 
     for (int f = 0; f < S::NF; ++f) {
         const int32_t base = P.xrow(f, gr);
         tr.xa[f] = xs.load(base + ca);
-#if MPBP_HALO_SCALAR
-        tr.h0[f] = xs.load_uniform(base + hc.g0);
-        tr.h1[f] = xs.load_uniform(base + hc.g1);
-#else
         tr.h0[f] = xs.load(base + hc.gl);
-#endif
     }
     const int32_t tb = P.wrap(gr) * P.n;
     tr.ta = P.cell[tb + ca];
-#if MPBP_HALO_SCALAR
-    tr.t0 = ld_uniform(P.cell, tb + hc.g0);
-    tr.t1 = ld_uniform(P.cell, tb + hc.g1);
-#else
     tr.t0 = P.cell[tb + hc.gl];
-#endif
 }
 
 template <class XS, int NF>
@@ -2106,16 +2007,9 @@ __device__ inline void store_tile_row(const XS& xs, double* sx, double* st, int 
     st[slot * kMTileW + tid] = okA ? tr.ta : 0.0;
     if (tid < 2) {   // lanes 0 and 1 store the halo columns
         const bool ok = tid == 0 ? hc.ok0 : hc.ok1;
-#if MPBP_HALO_SCALAR
-#pragma unroll
-        for (int f = 0; f < NF; ++f)
-            sx[(f * 3 + slot) * kMTileW + kMB + tid] = ok ? xs.value(tid == 0 ? tr.h0[f] : tr.h1[f]) : 0.0;
-        st[slot * kMTileW + kMB + tid] = ok ? (tid == 0 ? tr.t0 : tr.t1) : 0.0;
-#else
 #pragma unroll
         for (int f = 0; f < NF; ++f) sx[(f * 3 + slot) * kMTileW + kMB + tid] = ok ? xs.value(tr.h0[f]) : 0.0;
         st[slot * kMTileW + kMB + tid] = ok ? tr.t0 : 0.0;
-#endif
     }
 }
 
@@ -2233,10 +2127,7 @@ k_march(S P, XS xs, int nchunks, Epi epi, BS bs = BS{}) {
 // full occupancy instead of one round of marching workgroups.  Same accessors' values, same row arithmetic.
 // Measured at 1024^2 (trace means, r02o vs r02l): D 17.7 -> 13.2 us, Gt_G sweeps 13.2 / 12.1 -> 11.9 / 11.3 us, the
 // Gt_G first sweep (5 divisions per cell for the staged x0) 15.6 either way.
-#ifndef MPBP_PG_DIRECT
-#define MPBP_PG_DIRECT 1
-#endif
-int g_pg_direct = MPBP_PG_DIRECT;
+int g_pg_direct = 1;   // mpbp_set_pg_direct(0): the marching kernel instead
 // (lr: the thread's local row in the partition layout, gr: the same row's wrapped global index -- the row the
 // stencil's accessors are called around; a neighbour row r maps to local row lr + (r - gr))
 template <class S, class XS>
@@ -2761,6 +2652,152 @@ int launch_march_fixed(const S& P, const XS& xs, Epi epi, int rows_per_block, hi
     return MPBP_OK;
 }
 
+// ---- two F sweeps per launch on a 2D tile, tolerance mode (k_ftile) ----
+// A workgroup owns a 64 x 8 tile of cells (two per lane: rows t>>6 and 4 + t>>6 of the tile, column t & 63).  Level A
+// runs on the tile plus a one-cell halo (66 x 10 cells): INIT, the pointwise first iterate x0 = d0 = c2_0 b / diag
+// (diag rebuilt from thn, FStencilFast::rdiag4); otherwise sweep s from x_in and d_in, its stencil read straight from
+// global memory (the caches serve the neighbours).  Level A's x goes to LDS (the 4 fields over the haloed tile, 21 KB)
+// and its d stays in the registers of the lane that owns the cell; level B (sweep 1, or s + 1) computes the tile from
+// LDS and writes x_out (and d_out when SD).  No ring, no march: every workgroup is independent, one barrier.  Each level
+// performs the IEEE operations of the marching kernels' tolerance-mode rows and updates, so k_ftile is bit-identical
+// to k_march_init + (k_march or) k_march2.  One GPU, whole grid.
+constexpr int kFTW = 64, kFTH = 8, kFRW = kFTW + 2, kFRH = kFTH + 2, kFRN = kFRW * kFRH;
+struct XGlob {   // x of the four fields at virtual grid coordinates (periodic), straight from global memory
+    const double* __restrict__ x;
+    int n;
+    __device__ double X(int f, int r, int c) const {
+        const int rr = r < 0 ? r + n : (r >= n ? r - n : r), cc = c < 0 ? c + n : (c >= n ? c - n : c);
+        return x[(f * n + rr) * n + cc];
+    }
+};
+struct XTileF {  // level A's x over the haloed tile in LDS: [4][kFRH][kFRW]
+    const double* x;
+    int rb, cb;
+    __device__ double X(int f, int r, int c) const { return x[(f * kFRH + (r - rb)) * kFRW + (c - cb)]; }
+};
+struct FTile {
+    const double* x_in;   // !INIT: x_{s-1}
+    const double* d_in;   // !INIT: d_{s-1}
+    const double* b;      // BNone: the right-hand side
+    const double* sub;    // SUB: level B returns sub - x
+    double* x_out;
+    double* d_out;        // SD
+    double c1a, c2a, c1b, c2b;   // INIT: c2a = c2_0 (c1a unused)
+};
+
+template <bool INIT, bool SUB, bool SD, class BS>
+__global__ void __launch_bounds__(256) k_ftile(FStencilFast P, FTile a, BS bs) {
+    __shared__ double xs[4 * kFRN];
+    const int n = P.n;
+    const int tx = (n + kFTW - 1) / kFTW;
+    const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int r0 = (bk / tx) * kFTH, c0 = (bk % tx) * kFTW;
+    const int rb = r0 - 1, cb = c0 - 1;
+    const int tid = threadIdx.x;
+    const TDirect ta{P.cell, n};
+    // level A at virtual cell (vr, vc): x into LDS; returns d (and b: BS recomputes it)
+    auto level_a = [&](int vr, int vc, double* dA) {
+        const int gr = P.wrap(vr), gc = P.wrap(vc);
+        const int32_t k = gr * n + gc;
+        double bv[4];
+        typename BS::Q q{};
+        if constexpr (BS::on) q = bs.load(gr, gr, gc);
+        else {
+#pragma unroll
+            for (int f = 0; f < 4; ++f) bv[f] = a.b[f * n * n + k];
+        }
+        const FStencilDev::Stage sg{{P.uface[k], P.vface[k]}};
+        const int si = (vr - rb) * kFRW + (vc - cb);
+        if constexpr (INIT) {
+            double rd[4];
+            P.rdiag4(gr, gc, ta, sg, rd);
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                const double bf = BS::on ? bs.b(f, gr, gc, gc, ta, q) : bv[f];
+                const double x0 = a.c2a * bf * rd[f];
+                xs[f * kFRN + si] = x0;
+                dA[f] = x0;
+            }
+        } else {
+            const XGlob xa{a.x_in, n};
+            double acc[4], rd[4];
+            P.rows4(gr, gc, ta, xa, FStencilDev::Cell{{sg.face[0], sg.face[1]}}, acc, rd);
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                const double bf = BS::on ? bs.b(f, gr, gc, gc, ta, q) : bv[f];
+                const double z = (bf - acc[f]) * rd[f];
+                const double dn = a.c1a * a.d_in[f * n * n + k] + a.c2a * z;
+                xs[f * kFRN + si] = xa.X(f, gr, gc) + dn;
+                dA[f] = dn;
+            }
+        }
+    };
+    const int lc = tid & 63, lr = tid >> 6;
+    double dA0[4], dA1[4];
+    level_a(r0 + lr, c0 + lc, dA0);
+    level_a(r0 + 4 + lr, c0 + lc, dA1);
+    // the halo ring: rows -1 and kFTH (66 cells each), columns -1 and kFTW of rows 0 .. kFTH-1: 148 cells
+    if (tid < 2 * kFRW + 2 * kFTH) {
+        int vr, vc;
+        if (tid < 2 * kFRW) {
+            vr = tid < kFRW ? r0 - 1 : r0 + kFTH;
+            vc = cb + (tid < kFRW ? tid : tid - kFRW);
+        } else {
+            const int j = tid - 2 * kFRW;
+            vr = r0 + (j >> 1);
+            vc = (j & 1) ? c0 + kFTW : c0 - 1;
+        }
+        double dh[4];
+        level_a(vr, vc, dh);
+    }
+    __syncthreads();
+    // level B on the tile's own cells
+    const XTileF xt{xs, rb, cb};
+    auto level_b = [&](int vr, int vc, const double* dA) {
+        if (vr >= n || vc >= n) return;   // a tile past the grid's last row / column
+        const int32_t k = vr * n + vc;
+        const FStencilDev::Cell cl{{P.uface[k], P.vface[k]}};
+        double acc[4], rd[4];
+        P.rows4(vr, vc, ta, xt, cl, acc, rd);
+        typename BS::Q q{};
+        if constexpr (BS::on) q = bs.load(vr, vr, vc);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            const double bf = BS::on ? bs.b(f, vr, vc, vc, ta, q) : a.b[f * n * n + k];
+            const double z = (bf - acc[f]) * rd[f];
+            const double dn = a.c1b * dA[f] + a.c2b * z;
+            const int32_t o = f * n * n + k;
+            if constexpr (SD) a.d_out[o] = dn;
+            const double x = xt.X(f, vr, vc) + dn;
+            a.x_out[o] = SUB ? a.sub[o] - x : x;
+        }
+    };
+    level_b(r0 + lr, c0 + lc, dA0);
+    level_b(r0 + 4 + lr, c0 + lc, dA1);
+}
+
+template <bool INIT, bool SUB, bool SD, class BS>
+int launch_ftile_t(const FStencilFast& P, const FTile& a, hipStream_t st, const BS& bs) {
+    const int64_t tiles = (int64_t)((P.n + kFTW - 1) / kFTW) * ((P.n + kFTH - 1) / kFTH);
+    k_ftile<INIT, SUB, SD, BS><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+// INIT: level A = x0, level B = sweep 1 (the solve's first two updates); else sweeps s, s + 1.  One GPU, whole grid.
+// Grids whose cells a tile and its halo wrap onto at most once each way (XGlob / TDirect wrap once).
+inline bool ftile_ok(int n) { return n >= kFTW + kFTH + 4; }
+template <bool INIT, class BS = BNone>
+int launch_ftile(const FStencilDev& Pd, const FTile& a, hipStream_t st, const BS& bs = BS{}) {
+    const FStencilFast P{Pd};
+    if (P.h != 0 || P.which != 0 || !ftile_ok(P.n)) return set_error(MPBP_ERR_ARG, "ftile: one GPU, whole grid, n >= 76");
+    if (!a.x_out || (!INIT && (!a.x_in || !a.d_in || a.x_in == a.x_out)) || (!BS::on && !a.b) ||
+        (a.d_out && (a.d_out == a.d_in || a.d_out == a.x_in)))
+        return set_error(MPBP_ERR_ARG, "ftile: bad vectors");
+    const bool sub = a.sub != nullptr, sd = a.d_out != nullptr;
+    return sub ? (sd ? launch_ftile_t<INIT, true, true>(P, a, st, bs) : launch_ftile_t<INIT, true, false>(P, a, st, bs))
+               : (sd ? launch_ftile_t<INIT, false, true>(P, a, st, bs) : launch_ftile_t<INIT, false, false>(P, a, st, bs));
+}
+
 // Sweeps s, s+1 of an F Chebyshev solve fused (k_march2, tolerance mode) over the rows P.which selects (0: the whole
 // grid, 3: owned + ext ghost rows; level A then covers ext + 1).  d_in may be d_out only when the pair does not store
 // its direction (SD false): level A reads d_in on its neighbours' rows and columns.
@@ -2843,11 +2880,8 @@ int with_f_policy(const FStencilDev& P, bool fast, Fn&& fn) {
 // Calls fn with the F policy specialised for P's parameters (M = 0: none apply).
 template <class Fn>
 int with_f_identities(const FStencilDev& P, Fn&& fn) {
-#ifndef MPBP_F_POW2
-#define MPBP_F_POW2 1
-#endif
     if (P.d_u == -1.0 && P.eta_s == 1.0) {
-        if (MPBP_F_POW2 && P.eta_n != 1.0 && P.pow2 && P.ce0 != 0.0 && __builtin_isfinite(P.ce0)) return fn(FStencilDevM<13>{P});
+        if (P.eta_n != 1.0 && P.pow2 && P.ce0 != 0.0 && __builtin_isfinite(P.ce0)) return fn(FStencilDevM<13>{P});
         return P.eta_n == 1.0 ? fn(FStencilDevM<7>{P}) : fn(FStencilDevM<5>{P});
     }
     return fn(P);
@@ -3337,6 +3371,11 @@ int mpbp_set_gtg_fused(int32_t on) {
     g_gtg_fused = on;
     return MPBP_OK;
 }
+int mpbp_set_f_tile(int32_t on) {
+    if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "f_tile must be 0 or 1");
+    g_f_tile = on;
+    return MPBP_OK;
+}
 int mpbp_set_f_pair(int32_t on) {
     if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "f_pair must be 0 or 1");
     g_f_pair = on;
@@ -3412,6 +3451,35 @@ int mpbp_stokes_fill(const mpbp_stokes_params* prm, int32_t op, const double* ce
     const int64_t rows = mpbp_stokes_rows(prm->n, op);
     if (rows < 0) return (int)rows;
     k_stokes_fill<<<grid_for(rows), kBlock, 0, as_stream(stream)>>>(P, op, rows, row_ptr, col_idx, val);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int mpbp_stokes_count_rows(const mpbp_stokes_params* prm, int32_t op, const double* cell, const int32_t* rows,
+                           int32_t nrows, int32_t* row_nnz, void* stream) {
+    StokesDev P;
+    int rc = make_stokes(prm, cell, nullptr, nullptr, &P);
+    if (rc) return rc;
+    if (mpbp_stokes_rows(prm->n, op) < 0) return set_error(MPBP_ERR_ARG, "stokes count rows: unknown operator %d", op);
+    if (nrows < 0 || (nrows > 0 && (!rows || !row_nnz))) return set_error(MPBP_ERR_ARG, "stokes count rows: bad args");
+    if (nrows == 0) return MPBP_OK;
+    k_stokes_count<<<grid_for(nrows), kBlock, 0, as_stream(stream)>>>(P, op, nrows, row_nnz, rows);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int mpbp_stokes_fill_rows(const mpbp_stokes_params* prm, int32_t op, const double* cell, const double* uface,
+                          const double* vface, const int32_t* rows, int32_t nrows, const int32_t* row_ptr,
+                          int32_t* col_idx, double* val, void* stream) {
+    StokesDev P;
+    int rc = make_stokes(prm, cell, uface, vface, &P);
+    if (rc) return rc;
+    if ((op == MPBP_OP_A || op == MPBP_OP_F) && (!uface || !vface))
+        return set_error(MPBP_ERR_ARG, "stokes fill rows: A/F need face tables");
+    if (mpbp_stokes_rows(prm->n, op) < 0) return set_error(MPBP_ERR_ARG, "stokes fill rows: unknown operator %d", op);
+    if (nrows < 0 || (nrows > 0 && (!rows || !row_ptr))) return set_error(MPBP_ERR_ARG, "stokes fill rows: bad args");
+    if (nrows == 0) return MPBP_OK;
+    k_stokes_fill<<<grid_for(nrows), kBlock, 0, as_stream(stream)>>>(P, op, nrows, row_ptr, col_idx, val, rows);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
@@ -4167,10 +4235,7 @@ static int make_pgstencil(const mpbp_stokes_params* prm, const double* cell, con
             return set_error(MPBP_ERR_ARG, "pg_stencil: bad row partition");
     }
     *P = PGDev{prm->n, cell, prm->d_p, 1.0 / dx, -1.0 / dx, r0, L, h, which, ext, oh};
-#ifndef MPBP_GTG_UNIT
-#define MPBP_GTG_UNIT 1
-#endif
-    P->unit = MPBP_GTG_UNIT && P->d_p == 1.0 && P->minv == -P->inv;
+    P->unit = P->d_p == 1.0 && P->minv == -P->inv;
     return MPBP_OK;
 }
 
@@ -4545,6 +4610,9 @@ int op_first_sweep(const OpRef& o, bool cheb, const double* b, const double* dia
         const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, &P);
         if (rc) return rc;
         const bool fast = p->f_numerics == MPBP_NUMERICS_FAST;
+        if (fast && cheb && g_f_tile && q.halo == 0 && o.which == 0 && ftile_ok(P.n))   // x0, sweep 1 on 2D tiles
+            return launch_ftile<true>(P, FTile{nullptr, nullptr, b, sub, xo, store_d ? d : nullptr, 0.0, c2_0, c1, c2},
+                                      st);
         if (g_init_diag == 0)
             return with_f_policy(P, fast, [&](const auto& Q) {
                 return cheb ? launch_march(Q, xs, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, g_march_rows, st)
@@ -4886,10 +4954,11 @@ int launch_gtg_solve_t(const GtGStencilDev& S, const double* b, const double* di
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
+// The tile's staged cells must wrap onto the grid at most once each way (P.wrap), so n >= a tile plus its halos.
 bool gtg_fused_ok(const mpbp_schur_plan* p) {
     const mpbp_inner_solver& in = p->inner_P;
     return g_gtg_fused && p->pg_stencil && !p->halo && in.kind == MPBP_INNER_CHEBYSHEV && in.sweeps >= 2 &&
-           in.sweeps <= 6 && in.lmax > in.lmin && in.lmin >= 0.0;
+           in.sweeps <= 6 && in.lmax > in.lmin && in.lmin >= 0.0 && p->f_prm.n >= kGTW + kGTH + 2 * (in.sweeps - 1);
 }
 int gtg_solve_fused(const mpbp_schur_plan* p, const double* b, double* out, hipStream_t st) {
     PGDev P;
@@ -4940,6 +5009,8 @@ int f_pair(const mpbp_schur_plan* p, int ext, const double* x_in, const double* 
         rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &P);
     }
     if (rc) return rc;
+    if (ext < 0 && g_f_tile && ftile_ok(P.n))   // one GPU: the pair on 2D tiles
+        return launch_ftile<false>(P, FTile{x_in, dir, b, sub, x_out, nullptr, c1a, c2a, c1b, c2b}, st, bs);
     return launch_march2(P, Fused2{x_in, dir, b, sub, x_out, nullptr, c1a, c2a, c1b, c2b}, st, bs);
 }
 
@@ -5040,6 +5111,10 @@ int f_solve_gx(const Ctx& c, const double* xp, const mpbp_inner_solver& in, doub
     if (rc) return rc;
     const GxB bs{xp, G.d_p, G.inv, G.minv, G.n};
     double* cur = K == 2 ? dst : pong;
+    if (p->f_numerics == MPBP_NUMERICS_FAST && g_f_tile && ftile_ok(P.n))   // x0 and sweep 1 on 2D tiles
+        rc = launch_ftile<true>(P, FTile{nullptr, nullptr, nullptr, K == 2 ? sub : nullptr, cur, K == 2 ? nullptr : dir,
+                                         0.0, c2[0], c1[1], c2[1]}, c.st, bs);
+    else
     rc = with_f_policy(P, p->f_numerics == MPBP_NUMERICS_FAST, [&](const auto& Q) {
         return launch_march_init(Q, nullptr, c2[0], EpiChebFirst{nullptr, dir, c1[1], c2[1], K == 2 ? sub : nullptr, cur,
                                                                  K == 2 ? 0 : 1}, g_march_rows, c.st, bs);

@@ -604,22 +604,31 @@ class DistributedMatrix:
     boundary rows after the join.  With the gloo backend the ghosts are host-staged (HaloExchanger)."""
 
     def __init__(self, M: DeviceCSR, n: int, nfields: int, group=None, halo: str = "auto", overlap: bool = True,
-                 self_halo: bool = False):
+                 self_halo: bool = False, owned_rows: bool = False):
+        """M: the global operator, or (owned_rows=True) just this rank's rows of it, in owned order, with global
+        columns (MultiphaseBlockPreconditioner.assemble_rows: rank-local setup)."""
         dist, world, rank, backend = _dist_info(group)
         dev = M.device
-        if M.shape != (nfields * n * n, nfields * n * n):
-            raise ValueError(f"operator {M.shape} is not {nfields} fields of a {n} x {n} grid")
+        N_all = nfields * n * n
         self.part = part = RowPartition(n, world, rank, ghosts=bool(self_halo))
+        if M.shape != ((part.n_owned(nfields) if owned_rows else N_all), N_all):
+            raise ValueError(f"operator {M.shape} is not {'this rank' + chr(39) + 's rows of ' if owned_rows else ''}"
+                             f"{nfields} fields of a {n} x {n} grid")
         self.nfields = nfields
         self.partitioned = part.ghosts
         self.halo_impl = halo if halo != "auto" else ("rccl" if backend == "nccl" else "torch")
         rows = torch.from_numpy(part.owned_rows(nfields).astype(np.int32)).to(dev)
-        full = M.extract(rows, torch.arange(M.shape[1], dtype=torch.int32, device=dev), M.shape[1])
+        if owned_rows:
+            full, rows = M, torch.arange(M.shape[0], dtype=torch.int32, device=dev)
+        else:
+            full = M.extract(rows, torch.arange(M.shape[1], dtype=torch.int32, device=dev), M.shape[1])
         self.h = max(1, ghost_depth(full.col_idx, n, part.r0, part.L) if world > 1 else 1)
         del full
         self.n_own = part.n_owned(nfields)
         self.n_ext = part.n_ext(nfields, self.h)
         self.shape = (self.n_own, self.n_own)
+        if owned_rows and not self.partitioned:
+            raise ValueError("owned_rows=True needs a row partition")
         self.A = M.extract(rows, torch.from_numpy(part.colmap(nfields, self.h)).to(dev), self.n_ext) \
             if self.partitioned else M
         if self.partitioned and world > 1:
@@ -713,37 +722,62 @@ class DistributedSchurPreconditioner(PlanProfiling):
         backend = dist.get_backend(group)
         self.halo_impl = halo if halo != "auto" else ("rccl" if backend == "nccl" else "torch")
         bp = MultiphaseBlockPreconditioner(n, xi, eta_n, eta_s, device=dev)
-        _, _, F, D, G = bp.get_big_A_matrix(c=c, d_u=d_u)
         rows_u = torch.from_numpy(part.owned_rows(N_VEL_FIELDS).astype(np.int32)).to(dev)
         rows_p = torch.from_numpy(part.owned_rows(N_P_FIELDS).astype(np.int32)).to(dev)
-        mg_req = "mg" in ((inner_F or InnerSolver()).kind, (inner_P or InnerSolver()).kind)
+        ik_f, ik_p = inner_F or InnerSolver(), inner_P or InnerSolver()
+        mg_req = "mg" in (ik_f.kind, ik_p.kind)
         # the commutator products: with Jacobi / Chebyshev inner solves only this rank's pressure rows of Gt_G and
         # Gt_F_G (a product's row depends on that row of D alone: the same bits as the global product's row, for a
         # 1 / world share of the SpGEMM work); multigrid builds its Galerkin hierarchy from the whole Gt_G
         self.local_products = bool(local_products) and not mg_req and world > 1
+        akw = dict(c=c, d_u=d_u)
+        Gs = None
         if self.local_products:
-            D_own = D.extract(rows_p, torch.arange(D.shape[1], dtype=torch.int32, device=dev), D.shape[1])
-            GtG, GtFG = bp.commutator_products(F, D_own, G)
+            # rank-local setup (preconditioner.py:299-341 row by row): F, D, G assembled on this rank's rows only
+            # (mpbp_stokes_*_rows, the global assembly's rows bit for bit), the products' right operands on the velocity
+            # rows a product row can reach -- grid rows within `sup` of the owned ones (the CA schedule's ghost depths
+            # included) -- in global row numbering; setup memory and work O(N / world + ghosts) instead of O(N)
+            st_F, st_D, st_G = bp.stencils(**akw)
+            F = bp.assemble_rows(_lib.OP_F, rows_u, **akw)
+            D = bp.assemble_rows(_lib.OP_D, rows_p, **akw)
+            G = bp.assemble_rows(_lib.OP_G, rows_u, **akw)
+            F.stencil, D.stencil, G.stencil = st_F, st_D, st_G
+            sweeps = lambda k: k.sweeps if k.kind in ("jacobi", "chebyshev") else 1   # noqa: E731
+            sup = min(n, sweeps(ik_f) + sweeps(ik_p) + 2)
+            grid_rows = np.unique(np.arange(part.r0 - sup, part.r1 + sup) % n) if part.L + 2 * sup < n \
+                else np.arange(n)
+            sup_u = np.sort(np.concatenate([f * part.N + (r * n + np.arange(n)) for f in range(N_VEL_FIELDS)
+                                            for r in grid_rows]))
+            sup_u = torch.from_numpy(sup_u.astype(np.int32)).to(dev)
+            Fs = bp.assemble_rows(_lib.OP_F, sup_u, global_shape=True, **akw)
+            Gs = bp.assemble_rows(_lib.OP_G, sup_u, global_shape=True, **akw)
+            GtG, GtFG = bp.commutator_products(Fs, D, Gs)   # this rank's pressure rows, global columns
             GtG.stencil = _gtg_stencil(D, G)
-            del D_own
+            del Fs
         else:
+            _, _, F, D, G = bp.get_big_A_matrix(**akw)
             GtG, GtFG = bp.commutator_products(F, D, G)
+        lp = self.local_products
         if f_mode not in ("auto", "stencil", "assembled"):
             raise ValueError("f_mode must be 'auto', 'stencil' or 'assembled'")
         if f_mode == "stencil" and F.stencil is None:
             raise ValueError("f_mode='stencil' needs n >= 3")
         self.f_stencil = F.stencil if f_mode in ("auto", "stencil") else None
         self.pg_stencil = _pg_stencil(D, G, GtG, self.f_stencil, pg_mode)
-        # inner-solver bounds from the global operators: identical on every rank (with rank-local products, Gt_G's
-        # Gershgorin bound is the maximum of the ranks' row bounds: the same maximum, exactly)
-        self.inner_F = (inner_F or InnerSolver()).resolve(F, F.diagonal())
+        # inner-solver bounds from the global operators: identical on every rank (rank-local: the Gershgorin bound is the
+        # maximum of the ranks' row bounds -- the same maximum, exactly)
+        def global_bound(M, rows):
+            t = torch.tensor([M.gershgorin(_row_diagonal(M, rows))], dtype=torch.float64,
+                             device=dev if backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            return float(t.item())
+        if lp and ik_f.kind == "chebyshev" and ik_f.lmax is None:
+            ik_f = InnerSolver("chebyshev", ik_f.sweeps, ik_f.lmin, global_bound(F, rows_u), ik_f.ratio)
+        self.inner_F = ik_f.resolve(F, None if lp else F.diagonal())
         if self.local_products:
-            ip = inner_P or InnerSolver()
+            ip = ik_p
             if ip.kind == "chebyshev" and ip.lmax is None:
-                lmax = GtG.gershgorin(_row_diagonal(GtG, rows_p))
-                t = torch.tensor([lmax], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
-                ip = InnerSolver("chebyshev", ip.sweeps, ip.lmin, float(t.item()), ip.ratio)
+                ip = InnerSolver("chebyshev", ip.sweeps, ip.lmin, global_bound(GtG, rows_p), ip.ratio)
             self.inner_P = ip.resolve(GtG, None)
         else:
             self.inner_P = (inner_P or InnerSolver()).resolve(GtG, GtG.diagonal())
@@ -753,10 +787,9 @@ class DistributedSchurPreconditioner(PlanProfiling):
             sub = M if local else M.extract(rows, torch.arange(M.shape[1], dtype=torch.int32, device=dev), M.shape[1])
             return halo_reach(sub.row_ptr, sub.col_idx, rows, n)
 
-        lp = self.local_products
         q = reach(GtFG, rows_p, lp)
-        self.h_u = max(1, reach(F, rows_u), reach(D, rows_p))
-        self.h_p = max(1, reach(G, rows_u), reach(GtG, rows_p, lp), q)
+        self.h_u = max(1, reach(F, rows_u, lp), reach(D, rows_p, lp))
+        self.h_p = max(1, reach(G, rows_u, lp), reach(GtG, rows_p, lp), q)
         # multigrid inner solves: the global hierarchies (every rank, setup only), split over the partition; level 0's
         # ghost layout must also serve the restriction's reach
         self.mg_F = self.mg_P = None
@@ -798,37 +831,43 @@ class DistributedSchurPreconditioner(PlanProfiling):
         cm_p = torch.from_numpy(part.colmap(N_P_FIELDS, self.h_p)).to(dev)
         if self.ca:
             gp_rows = torch.from_numpy(part.ext_rows(N_P_FIELDS, self.h_p).astype(np.int32)).to(dev)
-            diag_F_glob = F.diagonal()
+            if lp:   # F's diagonal on the owned + ghost velocity rows, from those rows alone
+                gu = torch.from_numpy(part.ext_rows(N_VEL_FIELDS, self.h_u).astype(np.int32)).to(dev)
+                self.diag_F_ext = _row_diagonal(bp.assemble_rows(_lib.OP_F, gu, **akw), gu)
+            else:
+                diag_F_glob = F.diagonal()
             if lp:   # Gt_G's diagonal on the owned + ghost pressure rows, from those rows of the product alone
-                D_ext = D.extract(gp_rows, torch.arange(D.shape[1], dtype=torch.int32, device=dev), D.shape[1])
-                self.diag_P_ext = _row_diagonal(spgemm(D_ext, G, alpha=-1.0), gp_rows)
+                D_ext = bp.assemble_rows(_lib.OP_D, gp_rows, **akw)
+                self.diag_P_ext = _row_diagonal(spgemm(D_ext, Gs, alpha=-1.0), gp_rows)
                 del D_ext
             else:
                 diag_P_glob = GtG.diagonal()
-        self.F = F.extract(rows_u, cm_u, nu_ext)
-        self.D = D.extract(rows_p, cm_u, nu_ext)
-        self.G = G.extract(rows_u, cm_p, np_ext)
         if lp:   # already this rank's rows, in owned order
-            own = torch.arange(GtG.shape[0], dtype=torch.int32, device=dev)
-            self.GtG = GtG.extract(own, cm_p, np_ext)
-            self.GtFG = GtFG.extract(own, cm_p, np_ext)
+            own_u = torch.arange(rows_u.numel(), dtype=torch.int32, device=dev)
+            own_p = torch.arange(rows_p.numel(), dtype=torch.int32, device=dev)
+            self.F = F.extract(own_u, cm_u, nu_ext)
+            self.D = D.extract(own_p, cm_u, nu_ext)
+            self.G = G.extract(own_u, cm_p, np_ext)
+            self.GtG = GtG.extract(own_p, cm_p, np_ext)
+            self.GtFG = GtFG.extract(own_p, cm_p, np_ext)
         else:
+            self.F = F.extract(rows_u, cm_u, nu_ext)
+            self.D = D.extract(rows_p, cm_u, nu_ext)
+            self.G = G.extract(rows_u, cm_p, np_ext)
             self.GtG = GtG.extract(rows_p, cm_p, np_ext)
             self.GtFG = GtFG.extract(rows_p, cm_p, np_ext)
-        del F, D, G, GtG, GtFG, bp
+        del F, D, G, GtG, GtFG, Gs, bp
         torch.cuda.empty_cache()
         self.nu, self.np, self.nu_ext, self.np_ext = nu, np_, nu_ext, np_ext
         self.shape = (nu + np_, nu + np_)
         self.diag_F = self.F.diagonal()
         self.diag_P = self.GtG.diagonal()
-        if self.ca:   # diagonals on owned + ghost rows (the CA schedule's ghost-row sweeps stage x0 = b / diag)
+        if self.ca and not lp:   # diagonals on owned + ghost rows (the CA schedule's ghost-row sweeps stage x0)
             gu = torch.from_numpy(part.ext_rows(N_VEL_FIELDS, self.h_u)).to(dev)
             self.diag_F_ext = diag_F_glob[gu].contiguous()
-            if not lp:
-                gp = torch.from_numpy(part.ext_rows(N_P_FIELDS, self.h_p)).to(dev)
-                self.diag_P_ext = diag_P_glob[gp].contiguous()
-                del diag_P_glob
-            del diag_F_glob
+            gp = torch.from_numpy(part.ext_rows(N_P_FIELDS, self.h_p)).to(dev)
+            self.diag_P_ext = diag_P_glob[gp].contiguous()
+            del diag_P_glob, diag_F_glob
 
         mats = {"F": (self.F, nu), "D": (self.D, nu), "G": (self.G, np_), "P": (self.GtG, np_),
                 "Q": (self.GtFG, np_)}
@@ -977,9 +1016,16 @@ def solve_distributed(n, xi, etan, etas, c=1.0, d=-1.0, b_vec=None, inner_F=None
     from .solve import fgmres
     from .utils import manufactured_problem
     bp = MultiphaseBlockPreconditioner(n, xi, etan, etas)
-    A = bp.get_big_A_matrix(c=c, d_u=d)[0]
-    dA = DistributedMatrix(A, n, 5, group=group, self_halo=self_halo)
-    del A, bp
+    world = dist.get_world_size(group)
+    if world > 1:   # rank-local: this rank's rows of A only
+        part = RowPartition(n, world, dist.get_rank(group))
+        rows = torch.from_numpy(part.owned_rows(5).astype(np.int32)).cuda()
+        dA = DistributedMatrix(bp.assemble_rows(_lib.OP_A, rows, c=c, d_u=d), n, 5, group=group, owned_rows=True,
+                               halo=pc_kw.get("halo", "auto"))
+    else:
+        dA = DistributedMatrix(bp.get_big_A_matrix(c=c, d_u=d)[0], n, 5, group=group, self_halo=self_halo,
+                               halo=pc_kw.get("halo", "auto"))
+    del bp
     torch.cuda.empty_cache()
     M = DistributedSchurPreconditioner(n, xi, etan, etas, c=c, d_u=d, inner_F=inner_F, inner_P=inner_P, group=group,
                                        self_halo=self_halo, **pc_kw)
@@ -988,7 +1034,6 @@ def solve_distributed(n, xi, etan, etas, c=1.0, d=-1.0, b_vec=None, inner_F=None
     rows = dA.local_to_global_rows()
     assert np.array_equal(rows, M.local_to_global_rows())
     b = torch.from_numpy(np.ascontiguousarray(np.asarray(b_vec, dtype=np.float64)[rows])).cuda()
-    world = dist.get_world_size(group)
     kgroup = (group if group is not None else dist.group.WORLD) if world > 1 else None
     hist = []
     x, info = fgmres(dA, b, M=M, tol=tol, maxiter=maxiter, restrt=restrt, residuals=hist, group=kgroup)

@@ -135,6 +135,41 @@ class MultiphaseBlockPreconditioner:
                                      ptr(va), stream_handle()))
         return DeviceCSR(rp, ci, va, (rows, cols))
 
+    def assemble_rows(self, op, rows: torch.Tensor, global_shape: bool = False, c=1.0, d_u=-1.0, d_p=1.0,
+                      d_div=-1.0) -> DeviceCSR:
+        """Rows `rows` (ascending global ids, device int32) of operator `op` with their global columns -- the
+        global assembly's rows bit for bit (mpbp_stokes_count_rows / _fill_rows) without assembling the others (a
+        rank's owned and ghost rows, preconditioner.py:299-341).  global_shape: the result has every row of the
+        operator, those outside `rows` empty (an operand a sparse product indexes by global row)."""
+        cell, uface, vface = self.theta_tables()
+        prm = self._params(c, d_u, d_p, d_div)
+        nglob = check(lib().mpbp_stokes_rows(self.n, op))
+        cols = check(lib().mpbp_stokes_cols(self.n, op))
+        rows = rows.to(device=self.device, dtype=torch.int32).contiguous()
+        m = rows.numel()
+        row_nnz = torch.empty(max(m, 1), dtype=torch.int32, device=self.device)[:m]
+        check(lib().mpbp_stokes_count_rows(ctypes.byref(prm), op, ptr(cell), ptr(rows), m, ptr(row_nnz),
+                                           stream_handle()))
+        rp, ci, va = csr_from_row_nnz(row_nnz, (m, cols), self.device)
+        check(lib().mpbp_stokes_fill_rows(ctypes.byref(prm), op, ptr(cell), ptr(uface), ptr(vface), ptr(rows), m,
+                                          ptr(rp), ptr(ci), ptr(va), stream_handle()))
+        if not global_shape:
+            return DeviceCSR(rp, ci, va, (m, cols))
+        if m > 1 and not bool((rows[1:] > rows[:-1]).all()):
+            raise ValueError("assemble_rows(global_shape=True) needs ascending rows")
+        counts = torch.zeros(nglob, dtype=torch.int64, device=self.device)
+        counts[rows.long()] = (rp[1:] - rp[:-1]).long()
+        grp = torch.zeros(nglob + 1, dtype=torch.int64, device=self.device)
+        torch.cumsum(counts, 0, out=grp[1:])
+        return DeviceCSR(grp.to(torch.int32), ci, va, (nglob, cols))
+
+    def stencils(self, c=1.0, d_u=-1.0, d_p=1.0, d_div=-1.0):
+        """(F, D, G) matrix-free forms (FStencil, PGStencil, PGStencil) without assembling the matrices (n >= 3)."""
+        if self.n < 3:
+            return None, None, None
+        prm, tabs = self._params(c, d_u, d_p, d_div), self.theta_tables()
+        return FStencil(prm, tabs), PGStencil(prm, tabs[0], _lib.PG_D), PGStencil(prm, tabs[0], _lib.PG_G)
+
     # -- the reference's interface ---------------------------------------------------------------
     def get_block_matrices(self, is_ths):
         """(L, D, XI, G) of one phase (preconditioner.py:86-297)."""

@@ -46,7 +46,14 @@ def _worker(rank, world, port, n, layout, f_mode, kind, errfile, ca="auto", fuse
         ref = pc.apply(v)[gids]
         for _ in range(2):
             got = dpc.apply(v[gids].contiguous())
-            assert torch.equal(got, ref), float((got - ref).abs().max())
+            if numerics == "fast" and not dpc.ca:
+                # the per-sweep schedule starts each F solve with the stored diagonal's x0 = c2 (b / diag) (an exchange
+                # follows it), the one-GPU fast solve with x0 = c2 b (1 / diag) from its recomputed diagonal: north_star's
+                # bar, not bits
+                err = float((got - ref).abs().max() / ref.abs().max())
+                assert err <= 1e-12, err
+            else:
+                assert torch.equal(got, ref), float((got - ref).abs().max())
         dist.barrier()
         dist.destroy_process_group()
     except BaseException as e:
@@ -91,8 +98,9 @@ def test_distributed_apply_ca_schedule(world, n, layout, ca, fuse_g, tmp_path):
 
 @pytest.mark.parametrize("world,n,ca", [(2, 64, True), (3, 50, True), (2, 64, False)])
 def test_distributed_fast_numerics_matches_single_gpu(world, n, ca, tmp_path):
-    """Tolerance-mode F numerics under the row partition (the CA schedule's ghost-row sweeps and the per-sweep
-    schedule): the same fast rows per grid point, so the partitioned apply equals the one-GPU fast apply bit for bit."""
+    """Tolerance-mode F numerics under the row partition: the CA schedule (the default) runs the same fast rows and
+    updates per grid point as one GPU -- bit for bit; the per-sweep schedule differs only in its initial iterate's
+    diagonal (stored vs recomputed) -- within 1e-12."""
     errfile = str(tmp_path / "err.txt")
     _spawn(_worker, (world, _free_port(), n, "sell", "stencil", 4, errfile, ca, True, "fast"), world, errfile)
 

@@ -19,7 +19,7 @@ def _need_gpu(oracle_built):
         pytest.skip("no GPU")
 
 
-@pytest.mark.parametrize("n", [3, 5, 17, 64, 100, 256, 300])
+@pytest.mark.parametrize("n", [3, 5, 17, 64, 82, 100, 128, 256, 300])
 @pytest.mark.parametrize("kp", [2, 3, 4, 6])
 @pytest.mark.parametrize("numerics", ["exact", "fast"])
 def test_fused_gtg_solve_equals_per_sweep(n, kp, numerics):
@@ -61,3 +61,28 @@ def test_fused_gtg_solve_vs_oracle_256():
                              Inner("chebyshev", 4, pc.inner_F.lmin, pc.inner_F.lmax),
                              Inner("chebyshev", 5, pc.inner_P.lmin, pc.inner_P.lmax))
     assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
+
+
+@pytest.mark.parametrize("n", [3, 5, 17, 64, 76, 100, 128, 255, 256, 300])
+@pytest.mark.parametrize("kf", [2, 3, 4, 5])
+@pytest.mark.parametrize("fuse_g", [True, False])
+def test_ftile_equals_marching(n, kf, fuse_g):
+    """k_ftile (x0 + the first sweep, and the last pair, of a fast F solve on 2D tiles) performs the marching kernels'
+    tolerance-mode operations: the apply is bit-identical with the tiles on and off (marching k_march_init, k_march,
+    k_march2), with G x_p recomputed in the second solve and launched separately."""
+    import mp_block_preconditioners_amd as mp
+    from mp_block_preconditioners_amd._lib import check, lib
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("chebyshev", kf),
+                                      inner_P=mp.InnerSolver("chebyshev", 4), numerics="fast", fuse_g=fuse_g)
+    v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda",
+                    generator=torch.Generator(device="cuda").manual_seed(n * 10 + kf))
+    try:
+        check(lib().mpbp_set_f_tile(0))
+        ref = pc.apply(v).clone()
+        check(lib().mpbp_set_f_tile(1))
+        got = pc.apply(v)
+    finally:
+        check(lib().mpbp_set_f_tile(1))
+    assert torch.equal(got, ref), float((got - ref).abs().max())

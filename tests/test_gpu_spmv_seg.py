@@ -126,3 +126,16 @@ def test_wave_table_same_bits(n):
                     assert np.array_equal(got.view(np.uint64), ref.view(np.uint64)), (M.shape, mode, on)
     finally:
         check(lib().mpbp_set_csr_table(1))
+
+
+def test_row_blocks_of_another_matrix_refused():
+    """the wave-table fast path trusts the row lengths of the row_ptr a plan was made from, so matvec refuses
+    blocks planned for another matrix of the same shape."""
+    import mp_block_preconditioners_amd as mp
+    bp = mp.MultiphaseBlockPreconditioner(16, 1.0, 100.0, 1.0)
+    A, _, F, _, _ = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    A2 = bp.get_big_A_matrix(c=1.0, d_u=-1.0)[0]
+    x = torch.randn(A.shape[1], dtype=torch.float64, device="cuda")
+    assert torch.equal(A.matvec(x, blocks=A.plan_blocks()), A.matvec(x))
+    with pytest.raises(ValueError):
+        A.matvec(x, blocks=A2.plan_blocks())
