@@ -2683,6 +2683,7 @@ struct FTile {
     double* x_out;
     double* d_out;        // SD
     double c1a, c2a, c1b, c2b;   // INIT: c2a = c2_0 (c1a unused)
+    int dzero = 0;        // !INIT: d_{s-1} is +0.0 (a restart: multigrid post-smoothing), d_in is not read
 };
 
 template <bool INIT, bool SUB, bool SD, class BS>
@@ -2726,7 +2727,8 @@ __global__ void __launch_bounds__(256) k_ftile(FStencilFast P, FTile a, BS bs) {
             for (int f = 0; f < 4; ++f) {
                 const double bf = BS::on ? bs.b(f, gr, gc, gc, ta, q) : bv[f];
                 const double z = (bf - acc[f]) * rd[f];
-                const double dn = a.c1a * a.d_in[f * n * n + k] + a.c2a * z;
+                const double dprev = a.dzero ? 0.0 : a.d_in[f * n * n + k];
+                const double dn = a.c1a * dprev + a.c2a * z;
                 xs[f * kFRN + si] = xa.X(f, gr, gc) + dn;
                 dA[f] = dn;
             }
@@ -2790,7 +2792,7 @@ template <bool INIT, class BS = BNone>
 int launch_ftile(const FStencilDev& Pd, const FTile& a, hipStream_t st, const BS& bs = BS{}) {
     const FStencilFast P{Pd};
     if (P.h != 0 || P.which != 0 || !ftile_ok(P.n)) return set_error(MPBP_ERR_ARG, "ftile: one GPU, whole grid, n >= 76");
-    if (!a.x_out || (!INIT && (!a.x_in || !a.d_in || a.x_in == a.x_out)) || (!BS::on && !a.b) ||
+    if (!a.x_out || (!INIT && (!a.x_in || (!a.d_in && !a.dzero) || a.x_in == a.x_out)) || (!BS::on && !a.b) ||
         (a.d_out && (a.d_out == a.d_in || a.d_out == a.x_in)))
         return set_error(MPBP_ERR_ARG, "ftile: bad vectors");
     const bool sub = a.sub != nullptr, sd = a.d_out != nullptr;
@@ -4786,6 +4788,9 @@ __global__ void __launch_bounds__(kDT) k_dense_cm(int32_t m, const double* __res
 // c2[0] b / diag), else from the iterate in *cur (d starts at 0).  The last sweep writes `dst` (or the free
 // ping-pong buffer when dst is NULL), as sub - x when sub is set; *cur points at the result on return.  xch(x)
 // refreshes x's ghost rows before every sweep that reads them (a no-op on one GPU).
+// The last two sweeps of a tolerance-mode F Chebyshev solve may run as one fused launch (k_march2 / k_ftile).
+bool f_pair_ok(const mpbp_schur_plan* p) { return p->f_numerics == MPBP_NUMERICS_FAST && g_f_pair && p->f_stencil; }
+
 template <class Xch>
 int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, double lmax, int K, bool zero,
               const double* b, double** cur, double* alt, double* d, double* dst, const double* sub, hipStream_t st,
@@ -4830,10 +4835,28 @@ int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, 
         }
         s = 1;
     }
+    // tolerance-mode F level 0 on one GPU: the last two sweeps as one tiled launch (k_ftile); a restart of two sweeps
+    // reads d as +0.0 there, so it needs no memset either
+    const bool tpair = K - s >= 2 && o.stencil && o.sop == SOP_F && op.bd.empty && !o.stencil->halo && o.which == 0 &&
+                       f_pair_ok(o.stencil) && g_f_tile && ftile_ok(o.stencil->f_prm.n);
     // restart from the iterate in *cur: d = 0 -- read as +0.0 by the grouped kernel's first sweep, else zeroed
-    bool dzero = !zero && (op.in.grp || op.in.svl) && op.bd.empty;
+    bool dzero = !zero && (((op.in.grp || op.in.svl) && op.bd.empty) || (tpair && s == K - 2));
     if (!zero && !dzero) MPBP_HIP(hipMemsetAsync(d, 0, sizeof(double) * (size_t)nrows, st));
     for (; s < K; ++s) {
+        if (tpair && s == K - 2) {
+            double* out = dst ? dst : other;
+            FStencilDev P;
+            const mpbp_schur_plan* p = o.stencil;
+            int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &P);
+            if (rc) return rc;
+            FTile a{x, d, b, sub, out, nullptr, c1[s], c2[s], c1[s + 1], c2[s + 1]};
+            a.dzero = dzero ? 1 : 0;
+            rc = launch_ftile<false>(P, a, st);
+            if (rc) return rc;
+            other = x;
+            x = out;
+            break;
+        }
         const bool last = s == K - 1;
         double* nxt = (last && dst) ? dst : other;
         xch(x);
@@ -4994,7 +5017,6 @@ int gtg_first_sweep_x0(const mpbp_schur_plan* p, const double* x0, const double*
 
 // The last two sweeps of a tolerance-mode F Chebyshev solve fused (k_march2): one GPU whole grid, or (ext >= 0) the CA
 // schedule's owned + ext ghost rows.
-bool f_pair_ok(const mpbp_schur_plan* p) { return p->f_numerics == MPBP_NUMERICS_FAST && g_f_pair && p->f_stencil; }
 template <class BS = BNone>
 int f_pair(const mpbp_schur_plan* p, int ext, const double* x_in, const double* b, double* dir, double c1a, double c2a,
            double c1b, double c2b, const double* sub, double* x_out, hipStream_t st, const BS& bs = BS{}) {

@@ -86,3 +86,25 @@ def test_ftile_equals_marching(n, kf, fuse_g):
     finally:
         check(lib().mpbp_set_f_tile(1))
     assert torch.equal(got, ref), float((got - ref).abs().max())
+
+
+@pytest.mark.parametrize("n", [128, 256])
+def test_ftile_multigrid_smoothing_equals_marching(n):
+    """Multigrid level 0 with fast F numerics: the pre-smoothing (x0 + one sweep) and the post-smoothing restart (two
+    sweeps from d = 0, read as +0.0 instead of a memset) on tiles are bit-identical to the marching sweeps."""
+    import mp_block_preconditioners_amd as mp
+    from mp_block_preconditioners_amd._lib import check, lib
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("mg", 1), inner_P=mp.InnerSolver("mg", 1),
+                                      numerics="fast")
+    v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda",
+                    generator=torch.Generator(device="cuda").manual_seed(n))
+    try:
+        check(lib().mpbp_set_f_tile(0))
+        ref = pc.apply(v).clone()
+        check(lib().mpbp_set_f_tile(1))
+        got = pc.apply(v)
+    finally:
+        check(lib().mpbp_set_f_tile(1))
+    assert torch.equal(got, ref), float((got - ref).abs().max())
