@@ -34,7 +34,7 @@ def parse_inner(s):
     return kind, int(k or 4)
 
 
-def sweep_bytes(pc, layout, kind, sweeps, fused_init, f_tile=False):
+def sweep_bytes(pc, layout, kind, sweeps, fused_init, f_tile=False, f_solve=False):
     """Algorithmic HBM bytes of the F inner-solve launches bench.py times: one (bytes, solve) per recorded launch of
     one apply, in record order, and the kernel's name.
 
@@ -44,7 +44,9 @@ def sweep_bytes(pc, layout, kind, sweeps, fused_init, f_tile=False):
     diag (assembled layouts); plus the matrix (assembled: 12 B per entry + index data) or the thn tables (matrix-free:
     cell, u-face, v-face = 3 x 8 B per cell = 6 B per row).  With G x_p recomputed in the second solve (fuse_g), its
     sweeps read x_p (8 B per cell = 2 B per row) instead of b.  Tolerance-mode F solves of >= 4 sweeps run their last
-    two sweeps as ONE launch (k_march2): x_in, b, d_in read and x_out written once for the pair (x_s stays in LDS)."""
+    two sweeps as ONE launch (k_march2): x_in, b, d_in read and x_out written once for the pair (x_s stays in LDS).
+    f_solve (one GPU, tolerance mode, 3 or 4 updates): each whole F solve is ONE launch (k_fsolve) reading b (or x_p),
+    the thn tables (and the second solve's sub) and writing x once."""
     F = pc.F
     nF, nnzF = F.shape[0], F.nnz
     cheb = kind == "chebyshev"
@@ -72,6 +74,14 @@ def sweep_bytes(pc, layout, kind, sweeps, fused_init, f_tile=False):
         fixed, kname = nnzF * 12 + (nF + 1) * 4 + F.blocks.count * 8, "k_csr_wave<EpiCheb> (F sweep, CSR)"
     fuse_g = bool(getattr(pc, "fuse_g", False))
     out = []
+    if stencil and fast and cheb and f_solve:
+        kname = ("k_fsolve (a whole F Chebyshev solve -- x0 and %d sweeps -- in one launch on 64 x 8 tiles, "
+                 "matrix-free, tolerance mode)" % (sweeps - 1))
+        for solve in (1, 2):
+            gx = fuse_g and solve == 2
+            rhs = nF // 4 * 8 if gx else nF * 8            # x_p (one field) or b (four)
+            out.append((fixed + rhs + nF * 8 + (nF * 8 if solve == 2 else 0), solve))
+        return out, kname
     for solve in (1, 2):
         s = 2 if fused_init else 1
         while s < sweeps:
@@ -135,6 +145,9 @@ def main():
     ap.add_argument("--f-tile", type=int, default=None,
                     help="fast numerics: 1 (default) runs an F solve's x0 + first sweep and its last pair on 2D tiles, "
                          "0 on the marching kernels")
+    ap.add_argument("--f-solve", type=int, default=None,
+                    help="fast numerics: 1 (default) runs each F solve of 3 or 4 updates as one k_fsolve launch, "
+                         "0 as k_ftile launches")
     ap.add_argument("--gtg-fused", type=int, default=None,
                     help="1 (default): each Chebyshev Gt_G solve as one tiled launch; 0: one launch per sweep")
     ap.add_argument("--mg-galerkin-mf", type=int, default=None,
@@ -217,6 +230,8 @@ def main():
         _check(_lib().mpbp_set_f_tile(args.f_tile))
     if args.gtg_fused is not None:
         _check(_lib().mpbp_set_gtg_fused(args.gtg_fused))
+    if args.f_solve is not None:
+        _check(_lib().mpbp_set_f_solve(args.f_solve))
     if args.mg_galerkin_mf is not None:
         _check(_lib().mpbp_set_mg_galerkin_mf(args.mg_galerkin_mf))
     if args.stored_transfers:
@@ -342,7 +357,10 @@ def main():
     # 176.2 MB per launch at 1024^2); the second solve's sweeps (G x_p recomputed when fused) are reported beside it
     # (csrc: the tiled F kernels need n >= 76 on one GPU; below that, or with --f-tile 0, the marching ones run)
     f_tile = (args.f_tile is None or args.f_tile != 0) and n >= 76 and not partitioned
-    per_apply, kname = sweep_bytes(pc, args.layout, kf, sf, fused_init, f_tile)
+    # (csrc fsolve_ok: 3 or 4 updates, n >= 72; else the k_ftile / marching launches)
+    f_solve = (args.f_solve is None or args.f_solve != 0) and not partitioned and \
+        ((sf == 4 and n >= 72) or (sf == 3 and n >= 70))
+    per_apply, kname = sweep_bytes(pc, args.layout, kf, sf, fused_init, f_tile, f_solve)
     sbytes, avg_sweep_s, n_timed = roofline_of(per_apply, sweep_ms, 1)
     achieved = sbytes / avg_sweep_s / 1e9
     gbytes, g_s, g_timed = roofline_of(per_apply, sweep_ms, 2)

@@ -456,6 +456,10 @@ int mpbp_set_gtg_fused(int32_t on);
 /* One-GPU tolerance-mode F solves: x0 with the first sweep, and the last two sweeps, as 2D-tile launches (k_ftile: no
  * LDS ring, one barrier per workgroup; bit-identical to the marching kernels).  1 (default) or 0. */
 int mpbp_set_f_tile(int32_t on);
+/* One-GPU tolerance-mode F solves of 3 or 4 Chebyshev updates (x0 and 2 or 3 sweeps) as ONE tiled launch each
+ * (k_fsolve: b, thn and faces read once, x written once, the iterates in LDS; bit-identical to the k_ftile launches).
+ * 1 (default) or 0 (k_ftile / marching launches). */
+int mpbp_set_f_solve(int32_t on);
 /* Tolerance-mode F hierarchies (plan f_numerics FAST, one GPU, matrix-free level 0 and transfers): level 1 applied as
  * R_0 (F (P_0 x)) instead of streaming its stored Galerkin matrix.  1 (default) or 0. */
 int mpbp_set_mg_galerkin_mf(int32_t on);

@@ -28,6 +28,7 @@ int g_init_diag = 1;      // fused first F sweep: 1 rebuilds the staged diagonal
 int g_mg_gal = 1;          // tolerance-mode F hierarchies: level 1 as R_0 (F (P_0 x)) (MgGal; 0: its stored matrix)
 int g_f_direct = 0;        // tolerance-mode F sweeps on the direct kernel (one thread per cell, no LDS) instead of marching
 int g_gtg_fused = 1;       // one-GPU Chebyshev Gt_G solves of 2..6 sweeps as one k_gtg_solve launch (0: per sweep)
+int g_f_solve = 1;         // one-GPU tolerance-mode F solves of 3 or 4 Chebyshev updates as one launch (k_fsolve)
 int g_f_tile = 1;          // one-GPU tolerance-mode F: x0 + sweep 1, and the last pair, on 2D tiles (k_ftile)
 int g_f_pair = 1;         // tolerance-mode F solves: the last two Chebyshev sweeps as one k_march2 launch (0: two)
 inline int pg_rows() { return g_march_rows; }   // rows per workgroup of the D / G / Gt_G marching kernels: as F
@@ -1811,7 +1812,8 @@ struct FStencilFast : FStencilDev {
     }
     __device__ double aco(int p) const { return d_u * (p ? eta_s : eta_n) * idx2; }
     // the four rows (u_n, v_n, u_s, v_s) of cell (gr, gc) and their reciprocal diagonals
-    template <class TA, class XA>
+    // RD = false: the diagonals are the caller's (k_ftile level B reuses level A's, computed by the same operations)
+    template <bool RD = true, class TA, class XA>
     __device__ void rows4(int gr, int gc, const TA& ta, const XA& xa, const Cell& cl, double* acc, double* rd) const {
         const Co k = coeffs(nb(ta, gr, gc));
 #pragma unroll
@@ -1832,7 +1834,8 @@ struct FStencilFast : FStencilDev {
             br = __builtin_fma(KS, (uS - uC) + (vSW - vS), br);
             const double wu = c * ph(cl.face[0]);
             acc[fu] = __builtin_fma(a, br, __builtin_fma(wu, uC, k.xu * (uC - uo)));
-            rd[fu] = rcp_nr(__builtin_fma(-a, (A1 + A2) + (KC + KS), wu + k.xu));
+            if constexpr (RD)
+                rd[fu] = rcp_nr(__builtin_fma(-a, (A1 + A2) + (KC + KS), wu + k.xu));
             // v row: u1 = uN, u2 = uNE, u3 = uC, u4 = uE
             double bv = B1 * ((vN - vC) + (uN - uNE));
             bv = __builtin_fma(KC, (vW - vC) + (uC - uN), bv);
@@ -1840,7 +1843,8 @@ struct FStencilFast : FStencilDev {
             bv = __builtin_fma(A2, (vS - vC) + (uE - uC), bv);
             const double wv = c * ph(cl.face[1]);
             acc[fv] = __builtin_fma(a, bv, __builtin_fma(wv, vC, k.xv * (vC - vo)));
-            rd[fv] = rcp_nr(__builtin_fma(-a, (B1 + A2) + (KC + KE), wv + k.xv));
+            if constexpr (RD)
+                rd[fv] = rcp_nr(__builtin_fma(-a, (B1 + A2) + (KC + KE), wv + k.xv));
         }
     }
     // the reciprocal diagonals of the four rows at a staged point (k_march_init: x0 = c2 b / diag)
@@ -2653,27 +2657,44 @@ int launch_march_fixed(const S& P, const XS& xs, Epi epi, int rows_per_block, hi
 }
 
 // ---- two F sweeps per launch on a 2D tile, tolerance mode (k_ftile) ----
-// A workgroup owns a 64 x 8 tile of cells (two per lane: rows t>>6 and 4 + t>>6 of the tile, column t & 63).  Level A
-// runs on the tile plus a one-cell halo (66 x 10 cells): INIT, the pointwise first iterate x0 = d0 = c2_0 b / diag
-// (diag rebuilt from thn, FStencilFast::rdiag4); otherwise sweep s from x_in and d_in, its stencil read straight from
-// global memory (the caches serve the neighbours).  Level A's x goes to LDS (the 4 fields over the haloed tile, 21 KB)
-// and its d stays in the registers of the lane that owns the cell; level B (sweep 1, or s + 1) computes the tile from
-// LDS and writes x_out (and d_out when SD).  No ring, no march: every workgroup is independent, one barrier.  Each level
-// performs the IEEE operations of the marching kernels' tolerance-mode rows and updates, so k_ftile is bit-identical
-// to k_march_init + (k_march or) k_march2.  One GPU, whole grid.
-constexpr int kFTW = 64, kFTH = 8, kFRW = kFTW + 2, kFRH = kFTH + 2, kFRN = kFRW * kFRH;
-struct XGlob {   // x of the four fields at virtual grid coordinates (periodic), straight from global memory
-    const double* __restrict__ x;
-    int n;
-    __device__ double X(int f, int r, int c) const {
-        const int rr = r < 0 ? r + n : (r >= n ? r - n : r), cc = c < 0 ? c + n : (c >= n ? c - n : c);
-        return x[(f * n + rr) * n + cc];
-    }
-};
-struct XTileF {  // level A's x over the haloed tile in LDS: [4][kFRH][kFRW]
+// A workgroup owns a 64 x 8 tile of cells (two per lane: rows t>>6 and 4 + t>>6 of the tile, column t & 63).  It first
+// stages, with coalesced loads, thn and (!INIT) x_in over the tile plus a two-cell halo (68 x 12 cells, 32.6 KB of LDS):
+// every stencil operand after that is an LDS read at a constant offset from the cell's slot, with no periodic wrap and
+// no 64-bit address arithmetic per neighbour.  Level A runs on the tile plus a one-cell halo (66 x 10 cells): INIT, the
+// pointwise first iterate x0 = d0 = c2_0 b / diag (diag rebuilt from thn, FStencilFast::rdiag4); otherwise sweep s from
+// x_in and d_in.  Level A's x replaces x_in in the same LDS slots (after a barrier: its stencil reads x_in around the
+// cell), its d and the reciprocal diagonals of the lane's two tile cells stay in registers; level B (sweep 1, or s + 1)
+// computes the tile from LDS, reusing those diagonals, and writes x_out (and d_out when SD).  Every workgroup is
+// independent.  Each level performs the IEEE operations of the marching kernels' tolerance-mode rows and updates, so
+// k_ftile is bit-identical to k_march_init + (k_march or) k_march2.  One GPU, whole grid.
+constexpr int kFTW = 64, kFTH = 8, kFSW = kFTW + 4, kFSH = kFTH + 4, kFSN = kFSW * kFSH;
+template <int W, int H>
+struct XTileT {  // 4 fields over a W x H block of LDS ([4][H][W]), slot (0, 0) = virtual grid cell (rb, cb)
     const double* x;
     int rb, cb;
-    __device__ double X(int f, int r, int c) const { return x[(f * kFRH + (r - rb)) * kFRW + (c - cb)]; }
+    __device__ double X(int f, int r, int c) const { return x[(f * H + (r - rb)) * W + (c - cb)]; }
+};
+constexpr int kFAW = kFTW + 2, kFAH = kFTH + 2, kFAN = kFAW * kFAH;   // level A's cells: the tile + 1 halo
+template <int W>
+struct TTileT {  // staged thn at virtual grid coordinates, W columns per staged row
+    const double* t;
+    int rb, cb;
+    __device__ double T(int sph, int r, int c) const {
+        const double v = t[(r - rb) * W + (c - cb)];
+        return sph ? 1.0 - v : v;
+    }
+};
+template <int W>
+struct TTileWT {  // staged thn at wrapped grid coordinates (GxBT::b: its wrap tests need the wrapped row / column)
+    const double* t;
+    int rb, cb, n;
+    __device__ double T(int sph, int r, int c) const {
+        int lr = r - rb, lc = c - cb;
+        lr = lr < 0 ? lr + n : (lr >= n ? lr - n : lr);
+        lc = lc < 0 ? lc + n : (lc >= n ? lc - n : lc);
+        const double v = t[lr * W + lc];
+        return sph ? 1.0 - v : v;
+    }
 };
 struct FTile {
     const double* x_in;   // !INIT: x_{s-1}
@@ -2687,17 +2708,54 @@ struct FTile {
 };
 
 template <bool INIT, bool SUB, bool SD, class BS>
-__global__ void __launch_bounds__(256) k_ftile(FStencilFast P, FTile a, BS bs) {
-    __shared__ double xs[4 * kFRN];
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) k_ftile(FStencilFast P, FTile a, BS bs) {
+    __shared__ double xs[INIT ? 1 : 4 * kFSN];   // !INIT: x_in over the tile + 2 halo
+    __shared__ double ts[kFSN];                   // thn over the tile + 2 halo
+    __shared__ double xl[4 * kFAN];               // level A's x over the tile + 1 halo
     const int n = P.n;
     const int tx = (n + kFTW - 1) / kFTW;
     const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
     const int r0 = (bk / tx) * kFTH, c0 = (bk % tx) * kFTW;
-    const int rb = r0 - 1, cb = c0 - 1;
+    const int rb = r0 - 2, cb = c0 - 2;
     const int tid = threadIdx.x;
-    const TDirect ta{P.cell, n};
-    // level A at virtual cell (vr, vc): x into LDS; returns d (and b: BS recomputes it)
-    auto level_a = [&](int vr, int vc, double* dA) {
+    const int nn = n * n;
+    // stage thn (and x_in) over rows r0-2 .. r0+9, columns c0-2 .. c0+65: every load issued before the first LDS store
+    {
+        constexpr int IT = (kFSN + 255) / 256, NF = INIT ? 1 : 5;
+        double v[IT][NF];
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256;
+            if (i < kFSN) {
+                const int sr = i / kFSW, sc = i - sr * kFSW;
+                const int32_t k = P.wrap(rb + sr) * n + P.wrap(cb + sc);
+                v[it][0] = P.cell[k];
+                if constexpr (!INIT) {
+#pragma unroll
+                    for (int f = 0; f < 4; ++f) v[it][1 + f] = a.x_in[f * nn + k];
+                }
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256;
+            if (i < kFSN) {
+                ts[i] = v[it][0];
+                if constexpr (!INIT) {
+#pragma unroll
+                    for (int f = 0; f < 4; ++f) xs[f * kFSN + i] = v[it][1 + f];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const TTileT<kFSW> tt{ts, rb, cb};
+    const TTileWT<kFSW> tw{ts, rb, cb, n};
+    const XTileT<kFSW, kFSH> xa{xs, rb, cb};
+    const XTileT<kFAW, kFAH> xb{xl, rb + 1, cb + 1};
+    // level A at virtual cell (vr, vc): its x (xn), d (dA) and the reciprocal diagonals (rd)
+    auto level_a = [&](int vr, int vc, double* dA, double* rd) {
+        const int si = (vr - rb - 1) * kFAW + (vc - cb - 1);
         const int gr = P.wrap(vr), gc = P.wrap(vc);
         const int32_t k = gr * n + gc;
         double bv[4];
@@ -2705,77 +2763,75 @@ __global__ void __launch_bounds__(256) k_ftile(FStencilFast P, FTile a, BS bs) {
         if constexpr (BS::on) q = bs.load(gr, gr, gc);
         else {
 #pragma unroll
-            for (int f = 0; f < 4; ++f) bv[f] = a.b[f * n * n + k];
+            for (int f = 0; f < 4; ++f) bv[f] = a.b[f * nn + k];
         }
         const FStencilDev::Stage sg{{P.uface[k], P.vface[k]}};
-        const int si = (vr - rb) * kFRW + (vc - cb);
         if constexpr (INIT) {
-            double rd[4];
-            P.rdiag4(gr, gc, ta, sg, rd);
+            P.rdiag4(vr, vc, tt, sg, rd);
 #pragma unroll
             for (int f = 0; f < 4; ++f) {
-                const double bf = BS::on ? bs.b(f, gr, gc, gc, ta, q) : bv[f];
+                const double bf = BS::on ? bs.b(f, gr, gc, gc, tw, q) : bv[f];
                 const double x0 = a.c2a * bf * rd[f];
-                xs[f * kFRN + si] = x0;
+                xl[f * kFAN + si] = x0;
                 dA[f] = x0;
             }
         } else {
-            const XGlob xa{a.x_in, n};
-            double acc[4], rd[4];
-            P.rows4(gr, gc, ta, xa, FStencilDev::Cell{{sg.face[0], sg.face[1]}}, acc, rd);
+            double acc[4];
+            P.rows4(vr, vc, tt, xa, FStencilDev::Cell{{sg.face[0], sg.face[1]}}, acc, rd);
 #pragma unroll
             for (int f = 0; f < 4; ++f) {
-                const double bf = BS::on ? bs.b(f, gr, gc, gc, ta, q) : bv[f];
+                const double bf = BS::on ? bs.b(f, gr, gc, gc, tw, q) : bv[f];
                 const double z = (bf - acc[f]) * rd[f];
-                const double dprev = a.dzero ? 0.0 : a.d_in[f * n * n + k];
+                const double dprev = a.dzero ? 0.0 : a.d_in[f * nn + k];
                 const double dn = a.c1a * dprev + a.c2a * z;
-                xs[f * kFRN + si] = xa.X(f, gr, gc) + dn;
+                xl[f * kFAN + si] = xa.X(f, vr, vc) + dn;
                 dA[f] = dn;
             }
         }
     };
     const int lc = tid & 63, lr = tid >> 6;
-    double dA0[4], dA1[4];
-    level_a(r0 + lr, c0 + lc, dA0);
-    level_a(r0 + 4 + lr, c0 + lc, dA1);
+    double dA0[4], dA1[4], rd0[4], rd1[4];
+    level_a(r0 + lr, c0 + lc, dA0, rd0);
+    level_a(r0 + 4 + lr, c0 + lc, dA1, rd1);
     // the halo ring: rows -1 and kFTH (66 cells each), columns -1 and kFTW of rows 0 .. kFTH-1: 148 cells
-    if (tid < 2 * kFRW + 2 * kFTH) {
-        int vr, vc;
-        if (tid < 2 * kFRW) {
-            vr = tid < kFRW ? r0 - 1 : r0 + kFTH;
-            vc = cb + (tid < kFRW ? tid : tid - kFRW);
+    constexpr int kRing = 2 * (kFTW + 2) + 2 * kFTH;
+    if (tid < kRing) {
+        int hr, hc;
+        if (tid < 2 * (kFTW + 2)) {
+            const int j = tid < kFTW + 2 ? tid : tid - (kFTW + 2);
+            hr = tid < kFTW + 2 ? r0 - 1 : r0 + kFTH;
+            hc = c0 - 1 + j;
         } else {
-            const int j = tid - 2 * kFRW;
-            vr = r0 + (j >> 1);
-            vc = (j & 1) ? c0 + kFTW : c0 - 1;
+            const int j = tid - 2 * (kFTW + 2);
+            hr = r0 + (j >> 1);
+            hc = (j & 1) ? c0 + kFTW : c0 - 1;
         }
-        double dh[4];
-        level_a(vr, vc, dh);
+        double dh[4], rh[4];
+        level_a(hr, hc, dh, rh);
     }
     __syncthreads();
     // level B on the tile's own cells
-    const XTileF xt{xs, rb, cb};
-    auto level_b = [&](int vr, int vc, const double* dA) {
+    auto level_b = [&](int vr, int vc, const double* dA, const double* rdA) {
         if (vr >= n || vc >= n) return;   // a tile past the grid's last row / column
         const int32_t k = vr * n + vc;
         const FStencilDev::Cell cl{{P.uface[k], P.vface[k]}};
-        double acc[4], rd[4];
-        P.rows4(vr, vc, ta, xt, cl, acc, rd);
+        double acc[4], rdx[4];
+        P.template rows4<false>(vr, vc, tt, xb, cl, acc, rdx);
         typename BS::Q q{};
         if constexpr (BS::on) q = bs.load(vr, vr, vc);
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
-            const double bf = BS::on ? bs.b(f, vr, vc, vc, ta, q) : a.b[f * n * n + k];
-            const double z = (bf - acc[f]) * rd[f];
+            const double bf = BS::on ? bs.b(f, vr, vc, vc, tw, q) : a.b[f * nn + k];
+            const double z = (bf - acc[f]) * rdA[f];
             const double dn = a.c1b * dA[f] + a.c2b * z;
-            const int32_t o = f * n * n + k;
+            const int32_t o = f * nn + k;
             if constexpr (SD) a.d_out[o] = dn;
-            const double x = xt.X(f, vr, vc) + dn;
+            const double x = xb.X(f, vr, vc) + dn;
             a.x_out[o] = SUB ? a.sub[o] - x : x;
         }
     };
-    level_b(r0 + lr, c0 + lc, dA0);
-    level_b(r0 + 4 + lr, c0 + lc, dA1);
+    level_b(r0 + lr, c0 + lc, dA0, rd0);
+    level_b(r0 + 4 + lr, c0 + lc, dA1, rd1);
 }
 
 template <bool INIT, bool SUB, bool SD, class BS>
@@ -2786,7 +2842,7 @@ int launch_ftile_t(const FStencilFast& P, const FTile& a, hipStream_t st, const 
     return MPBP_OK;
 }
 // INIT: level A = x0, level B = sweep 1 (the solve's first two updates); else sweeps s, s + 1.  One GPU, whole grid.
-// Grids whose cells a tile and its halo wrap onto at most once each way (XGlob / TDirect wrap once).
+// Grids whose cells a tile and its staged halo wrap onto at most once each way.
 inline bool ftile_ok(int n) { return n >= kFTW + kFTH + 4; }
 template <bool INIT, class BS = BNone>
 int launch_ftile(const FStencilDev& Pd, const FTile& a, hipStream_t st, const BS& bs = BS{}) {
@@ -2798,6 +2854,179 @@ int launch_ftile(const FStencilDev& Pd, const FTile& a, hipStream_t st, const BS
     const bool sub = a.sub != nullptr, sd = a.d_out != nullptr;
     return sub ? (sd ? launch_ftile_t<INIT, true, true>(P, a, st, bs) : launch_ftile_t<INIT, true, false>(P, a, st, bs))
                : (sd ? launch_ftile_t<INIT, false, true>(P, a, st, bs) : launch_ftile_t<INIT, false, false>(P, a, st, bs));
+}
+
+// ---- a whole tolerance-mode F Chebyshev solve in one launch (k_fsolve) ----
+// x = F^-1 b by K = H + 1 Chebyshev-Jacobi updates from x0 = 0 (the first is the pointwise x0 = d0 = c2_0 b / diag),
+// on the 64 x 8 tiles of k_ftile: thn is staged over the tile plus H + 1 halo cells, level 0 builds x0 over the tile
+// plus H, and level l = 1 .. H recomputes the tile plus H - l from level l - 1 (LDS ping-pong), the last writing x.
+// Every cell a workgroup computes has one owning lane for all its levels: the lane's two tile cells (as k_ftile) and
+// cell t of each halo ring r = 1 .. H (140 + 8 r cells, lane t < that), so its d, b, faces and reciprocal diagonals
+// stay in that lane's registers from level 0 on.  Each level performs the IEEE operations of the marching kernels'
+// tolerance-mode rows and updates: bit-identical to k_ftile<INIT> + k_ftile pair (H = 3) or + k_ftile sweep.  HBM:
+// b (or x_p), thn, faces in, x out once -- against x, d, b re-read per launch by the two-launch solve.
+template <int H>
+struct FsTile {
+    static constexpr int RW = kFTW + 2 * H, RH = kFTH + 2 * H, N = RW * RH;   // x levels: the tile + H
+    static constexpr int TW = RW + 2, TH = RH + 2, TN = TW * TH;             // thn: the tile + H + 1
+};
+struct FSolve {
+    const double* b;      // BNone: the right-hand side
+    const double* sub;    // the result is sub - x when set
+    double* x_out;
+    double c2_0;
+    double c1[4], c2[4];  // updates 1 .. H
+};
+// ring r's cell j: rows r0 - r and r0 + TH - 1 + r (all 64 + 2r columns), then columns c0 - r and c0 + TW - 1 + r of
+// the rows between
+__device__ inline void fs_ring_cell(int r, int j, int r0, int c0, int& vr, int& vc) {
+    const int w = kFTW + 2 * r;
+    if (j < 2 * w) {
+        vr = j < w ? r0 - r : r0 + kFTH - 1 + r;
+        vc = c0 - r + (j < w ? j : j - w);
+    } else {
+        const int k = j - 2 * w;
+        vr = r0 - r + 1 + (k >> 1);
+        vc = (k & 1) ? c0 + kFTW - 1 + r : c0 - r;
+    }
+}
+
+template <int H, bool SUB, class BS>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8)))
+k_fsolve(FStencilFast P, FSolve a, BS bs) {
+    using T = FsTile<H>;
+    constexpr int NS = H + 1;   // owned cells with updates after x0: the two tile cells and rings 1 .. H - 1
+    __shared__ double ts[T::TN];
+    __shared__ double xa[4 * T::N], xb[4 * T::N];
+    const int n = P.n, nn = n * n;
+    const int tx = (n + kFTW - 1) / kFTW;
+    const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int r0 = (bk / tx) * kFTH, c0 = (bk % tx) * kFTW;
+    const int rbt = r0 - H - 1, cbt = c0 - H - 1, rb = r0 - H, cb = c0 - H;
+    const int tid = threadIdx.x;
+    {
+        constexpr int IT = (T::TN + 255) / 256;
+        double v[IT];
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256;
+            if (i < T::TN) {
+                const int sr = i / T::TW, sc = i - sr * T::TW;
+                v[it] = P.cell[P.wrap(rbt + sr) * n + P.wrap(cbt + sc)];
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256;
+            if (i < T::TN) ts[i] = v[it];
+        }
+    }
+    __syncthreads();
+    const TTileT<T::TW> tt{ts, rbt, cbt};
+    const TTileWT<T::TW> tw{ts, rbt, cbt, n};
+    const int lr = tid >> 6, lc = tid & 63;
+    // the owned cells: slot 0, 1 the tile cells, slot 1 + r ring r (r = 1 .. H; slot H + 1 only needs x0)
+    int cr[NS + 1], cc[NS + 1];
+    bool own[NS + 1];
+    cr[0] = r0 + lr; cc[0] = c0 + lc; own[0] = true;
+    cr[1] = r0 + 4 + lr; cc[1] = c0 + lc; own[1] = true;
+#pragma unroll
+    for (int r = 1; r <= H; ++r) {
+        own[1 + r] = tid < 140 + 8 * r;
+        fs_ring_cell(r, own[1 + r] ? tid : 0, r0, c0, cr[1 + r], cc[1 + r]);
+    }
+    double d[NS][4], rd[NS][4], bv[NS][4], fc[NS][2];
+    // level 0: x0 = d0 = c2_0 b / diag over the tile + H
+#pragma unroll
+    for (int sl = 0; sl <= NS; ++sl) {
+        if (!own[sl]) continue;
+        const int vr = cr[sl], vc = cc[sl];
+        const int gr = P.wrap(vr), gc = P.wrap(vc);
+        const int32_t k = gr * n + gc;
+        const FStencilDev::Stage sg{{P.uface[k], P.vface[k]}};
+        double b4[4], r4[4];
+        typename BS::Q q{};
+        if constexpr (BS::on) q = bs.load(gr, gr, gc);
+        P.rdiag4(vr, vc, tt, sg, r4);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) b4[f] = BS::on ? bs.b(f, gr, gc, gc, tw, q) : a.b[f * nn + k];
+        const int si = (vr - rb) * T::RW + (vc - cb);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            const double x0 = a.c2_0 * b4[f] * r4[f];
+            xa[f * T::N + si] = x0;
+            if (sl < NS) {
+                d[sl][f] = x0;
+                rd[sl][f] = r4[f];
+                bv[sl][f] = b4[f];
+            }
+        }
+        if (sl < NS) {
+            fc[sl][0] = sg.face[0];
+            fc[sl][1] = sg.face[1];
+        }
+    }
+    // levels 1 .. H
+    double* cur = xa;
+    double* nxt = xb;
+#pragma unroll
+    for (int l = 1; l <= H; ++l) {
+        __syncthreads();
+        const XTileT<T::RW, T::RH> xt{cur, rb, cb};
+        const double c1 = a.c1[l - 1], c2 = a.c2[l - 1];
+#pragma unroll
+        for (int sl = 0; sl < NS; ++sl) {
+            if (sl >= 2 && (sl - 1 > H - l || !own[sl])) continue;   // ring r = sl - 1 lives through level H - r
+            const int vr = cr[sl], vc = cc[sl];
+            if (l == H && (vr >= n || vc >= n)) continue;             // a tile past the grid's last row / column
+            double acc[4], rdx[4];
+            P.template rows4<false>(vr, vc, tt, xt, FStencilDev::Cell{{fc[sl][0], fc[sl][1]}}, acc, rdx);
+            const int si = (vr - rb) * T::RW + (vc - cb);
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                const double z = (bv[sl][f] - acc[f]) * rd[sl][f];
+                const double dn = c1 * d[sl][f] + c2 * z;
+                const double x = cur[f * T::N + si] + dn;
+                if (l < H) {
+                    nxt[f * T::N + si] = x;
+                    d[sl][f] = dn;
+                } else {
+                    const int32_t o = f * nn + vr * n + vc;
+                    a.x_out[o] = SUB ? a.sub[o] - x : x;
+                }
+            }
+        }
+        double* t = cur;
+        cur = nxt;
+        nxt = t;
+    }
+}
+
+// Grids a tile's staged thn (tile + H + 1 each side) wraps onto at most once.
+template <int H>
+inline bool fsolve_ok_n(int n) { return n >= FsTile<H>::TW && n >= FsTile<H>::TH; }
+template <int H, class BS>
+int launch_fsolve_t(const FStencilFast& P, const FSolve& a, hipStream_t st, const BS& bs) {
+    const int64_t tiles = (int64_t)((P.n + kFTW - 1) / kFTW) * ((P.n + kFTH - 1) / kFTH);
+    if (a.sub) k_fsolve<H, true, BS><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
+    else k_fsolve<H, false, BS><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+// One GPU, whole grid, K = 3 or 4 Chebyshev updates (x0 and H = K - 1 stencil sweeps).
+inline bool fsolve_ok(int K, int n) { return (K == 3 && fsolve_ok_n<2>(n)) || (K == 4 && fsolve_ok_n<3>(n)); }
+template <class BS = BNone>
+int launch_fsolve(const FStencilDev& Pd, int K, const double* c1, const double* c2, const double* b, const double* sub,
+                  double* x_out, hipStream_t st, const BS& bs = BS{}) {
+    const FStencilFast P{Pd};
+    if (P.h != 0 || P.which != 0 || !fsolve_ok(K, P.n)) return set_error(MPBP_ERR_ARG, "fsolve: one GPU, whole grid");
+    if (!x_out || (!BS::on && !b) || x_out == b) return set_error(MPBP_ERR_ARG, "fsolve: bad vectors");
+    FSolve a{b, sub, x_out, c2[0], {}, {}};
+    for (int l = 1; l < K; ++l) {
+        a.c1[l - 1] = c1[l];
+        a.c2[l - 1] = c2[l];
+    }
+    return K == 3 ? launch_fsolve_t<2>(P, a, st, bs) : launch_fsolve_t<3>(P, a, st, bs);
 }
 
 // Sweeps s, s+1 of an F Chebyshev solve fused (k_march2, tolerance mode) over the rows P.which selects (0: the whole
@@ -3043,6 +3272,34 @@ struct GtGStencilDev : PGDev {
         }
         e[0] = -1.0 * cN; e[1] = -1.0 * cW; e[2] = -1.0 * cC; e[3] = -1.0 * cE; e[4] = -1.0 * cS;
     }
+    // entries N and W alone, by the operations entries() performs for them (k_gtg_solve: with minv == -inv, the E entry
+    // of a cell is bit for bit the W entry of its east neighbour and S the N entry of its south one)
+    template <class TA>
+    __device__ void entries_nw(int vr, int vc, const TA& ta, double* eN, double* eW) const {
+        double cN = 0.0, cW = 0.0;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const double t0 = ta.T(p, vr, vc), tW = ta.T(p, vr, vc - 1), tN = ta.T(p, vr - 1, vc);
+            double qW, qN;
+            if (unit) {
+                const double XW = inv * (0.5 * (t0 + tW)), XN = inv * (0.5 * (t0 + tN));
+                qW = XW * XW;
+                qN = XN * XN;
+            } else {
+                const double DuC = minv * (0.5 * (t0 + tW)), DvC = inv * (0.5 * (t0 + tN));
+                const double gC = 0.5 * (t0 + tW), gN = 0.5 * (t0 + tN);
+                qW = DuC * (d_p * (minv * gC));
+                qN = DvC * (d_p * (inv * gN));
+            }
+            if (p == 0) {
+                cW = qW; cN = qN;
+            } else {
+                cW += qW; cN += qN;
+            }
+        }
+        *eN = -1.0 * cN;
+        *eW = -1.0 * cW;
+    }
     // Gt_G x at a cell: the five entries summed in CSR column order (EDGE: sorted by wrapped column)
     template <bool EDGE, class TA, class XA>
     __device__ double apply_v(int vr, int vc, int gr, int gc, const TA& ta, const XA& xa, double* dg) const {
@@ -3062,11 +3319,15 @@ struct GtGStencilDev : PGDev {
 // ---- one Gt_G Chebyshev solve in one launch (k_gtg_solve) ----
 // The pressure solves x = Gt_G^-1 b of the apply (solve.py:265, 271) as K Chebyshev-Jacobi sweeps from x0 = 0, fused:
 // a workgroup owns a TW x TH tile of cells and stages b and thn over the tile plus a halo of H = K - 1 cells (its
-// level 0, x0 = d0 = c2_0 (b / diag), built there from the stored diagonal); level l = 1 .. H recomputes the tile with
-// halo H - l from level l - 1 in LDS, and the last level writes the tile.  Each row is GtGStencilDev::apply_v (the
-// matrix-free rows' IEEE operations) and each update the Chebyshev epilogue's (EpiChebFirst at level 1, EpiCheb after):
-// bit-identical to the K - 1 sweeps of the per-sweep path, for one launch and one pass over b instead of K - 1 passes
-// over x, d, b.  Halo cells are recomputed by neighbouring tiles (70 x 14 staged cells per 64 x 8 tile at K = 4).
+// level 0, x0 = d0 = c2_0 (b / diag), built there from the stored diagonal).  The matrix entries depend on thn only, so
+// they are built once per launch, not once per level: the N, W and C entries of every cell of level 1's region (plus
+// N one row below it and W one column right of it) go to LDS, and a cell's E and S entries are its east neighbour's W
+// and its south neighbour's N (bit for bit when minv == -inv, which gtg_fused_ok requires).  Level l = 1 .. H then
+// recomputes the tile with halo H - l from level l - 1 in LDS with five LDS entries, and the last level writes the tile.
+// Each row is GtGStencilDev::apply_v's IEEE operations (the entries', the products', add5's column order) and each
+// update the Chebyshev epilogue's (EpiChebFirst at level 1, EpiCheb after): bit-identical to the K - 1 sweeps of the
+// per-sweep path, for one launch and one pass over b instead of K - 1 passes over x, d, b.  thn's LDS is reused for the
+// levels' ping-pong buffer once the entries are built.
 constexpr int kGTW = 64, kGTH = 8;
 struct ChebK {
     double c1[8], c2[8];   // sweep s's coefficients (c2[0]: the initial iterate's)
@@ -3074,6 +3335,7 @@ struct ChebK {
 template <int H>
 struct GtgTile {
     static constexpr int RW = kGTW + 2 * H, RH = kGTH + 2 * H, N = RW * RH;
+    static constexpr int EW = RW - 1, EH = RH - 1, EN = EW * EH;   // entries: staged rows / columns 1 .. R - 1
 };
 template <int H>
 struct TTile {   // thn of the staged tile; (r, c) in the tile's virtual grid coordinates
@@ -3084,73 +3346,122 @@ struct TTile {   // thn of the staged tile; (r, c) in the tile's virtual grid co
         return sph ? 1.0 - v : v;
     }
 };
-template <int H>
-struct XTile {
-    const double* x;
-    int rb, cb;
-    __device__ double X(int, int r, int c) const { return x[(r - rb) * GtgTile<H>::RW + (c - cb)]; }
+struct GtgE {   // the LDS entries: [EH][EW] each, slot 0 = staged cell (1, 1)
+    double* n;
+    double* w;
+    double* c;
 };
+
+// Level L (1 .. H) of k_gtg_solve: the tile with halo H - L from level L - 1 in `cur` (compile-time extents, so the
+// cell index splits with a multiply-shift).
+template <int H, int L>
+__device__ inline void gtg_level(const GtGStencilDev& P, const GtgE& E, const double* bs, double* ds, const double* cur,
+                                 double* nxt, const ChebK& ck, double* __restrict__ out, int r0, int c0) {
+    using G = GtgTile<H>;
+    constexpr int h = H - L, w = kGTW + 2 * h, cells = w * (kGTH + 2 * h);
+    const int n = P.n, tid = threadIdx.x;
+    const double c1 = ck.c1[L], c2 = ck.c2[L];
+#pragma unroll
+    for (int i0 = 0; i0 < cells; i0 += 256) {
+        const int i = i0 + tid;
+        const bool live = i < cells;
+        const int ii = live ? i : 0;
+        const int lr = ii / w, lc = ii - lr * w;
+        const int vr = r0 - h + lr, vc = c0 - h + lc;        // virtual cell
+        const int gr = P.wrap(vr), gc = P.wrap(vc);
+        const int si = (lr + L) * G::RW + (lc + L);          // its staged index
+        const int ei = (lr + L - 1) * G::EW + (lc + L - 1);  // its entry index
+        const bool edge = __builtin_amdgcn_readfirstlane(__any(live && (gr == 0 || gr == n - 1 || gc == 0 ||
+                                                                        gc == n - 1))) != 0;
+        if (live) {
+            const double dg = E.c[ei];
+            const double p[5] = {E.n[ei] * cur[si - G::RW], E.w[ei] * cur[si - 1], dg * cur[si],
+                                 E.w[ei + 1] * cur[si + 1], E.n[ei + G::EW] * cur[si + G::RW]};
+            const Wrap wr{gr == 0, gr == n - 1, gc == 0, gc == n - 1};
+            const double acc = edge ? add5<true>(0.0, p, wr) : add5<false>(0.0, p, wr);
+            const double z = (bs[si] - acc) / dg;
+            const double dn = c1 * ds[si] + c2 * z;
+            const double x = cur[si] + dn;
+            if constexpr (L < H) {
+                nxt[si] = x;
+                ds[si] = dn;
+            } else if (vr < n && vc < n) {                    // the tile's own cells (h = 0: vr, vc >= 0)
+                out[vr * n + vc] = x;
+            }
+        }
+    }
+}
+template <int H, int L>
+__device__ inline void gtg_levels(const GtGStencilDev& P, const GtgE& E, const double* bs, double* ds, double* cur,
+                                  double* nxt, const ChebK& ck, double* __restrict__ out, int r0, int c0) {
+    gtg_level<H, L>(P, E, bs, ds, cur, nxt, ck, out, r0, c0);
+    if constexpr (L < H) {
+        __syncthreads();
+        gtg_levels<H, L + 1>(P, E, bs, ds, nxt, cur, ck, out, r0, c0);
+    }
+}
 
 template <int H>
 __global__ void __launch_bounds__(256) k_gtg_solve(GtGStencilDev P, const double* __restrict__ b,
                                                    const double* __restrict__ diag, ChebK ck, double* __restrict__ out) {
     using G = GtgTile<H>;
-    __shared__ double ts[G::N], bs[G::N], xa[G::N], xb[G::N], ds[G::N];
+    __shared__ double bs[G::N], xa[G::N], xb[G::N], ds[G::N];   // xb: thn until the entries are built
+    __shared__ double en[G::EN], ew[G::EN], ec[G::EN];
+    double* ts = xb;
     const int n = P.n;
     const int tx = (n + kGTW - 1) / kGTW;
     const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
     const int r0 = (bk / tx) * kGTH, c0 = (bk % tx) * kGTW;
     const int rb = r0 - H, cb = c0 - H;   // virtual coordinates of staged cell 0
     const int tid = threadIdx.x;
-    // level 0 over the whole staged region: thn, b, x0 = d0 = c2_0 (b / diag)
-    for (int i = tid; i < G::N; i += 256) {
-        const int rr = i / G::RW, cc = i - rr * G::RW;
-        const int32_t k = P.wrap(rb + rr) * n + P.wrap(cb + cc);
-        const double bv = b[k];
-        ts[i] = P.cell[k];
-        bs[i] = bv;
-        const double x0 = ck.c2[0] * (bv / diag[k]);
-        xa[i] = x0;
-        ds[i] = x0;
-    }
-    __syncthreads();
-    double* cur = xa;
-    double* nxt = xb;
-    const TTile<H> ta{ts, rb, cb};
-#pragma unroll 1
-    for (int l = 1; l <= H; ++l) {
-        const int h = H - l;                       // this level's halo
-        const int w = kGTW + 2 * h, rows = kGTH + 2 * h;
-        const XTile<H> xt{cur, rb, cb};
-        for (int i0 = 0; i0 < w * rows; i0 += 256) {
-            const int i = i0 + tid;
-            const bool live = i < w * rows;
-            const int ii = live ? i : 0;
-            const int lr = ii / w, lc = ii - lr * w;
-            const int vr = r0 - h + lr, vc = c0 - h + lc;        // virtual cell
-            const int gr = P.wrap(vr), gc = P.wrap(vc);
-            const int si = (vr - rb) * G::RW + (vc - cb);        // its staged index
-            const bool edge = __builtin_amdgcn_readfirstlane(__any(live && (gr == 0 || gr == n - 1 || gc == 0 ||
-                                                                            gc == n - 1))) != 0;
-            if (!live) continue;
-            double dg;
-            const double acc = edge ? P.template apply_v<true>(vr, vc, gr, gc, ta, xt, &dg)
-                                    : P.template apply_v<false>(vr, vc, gr, gc, ta, xt, &dg);
-            const double z = (bs[si] - acc) / dg;
-            const double dn = ck.c1[l] * ds[si] + ck.c2[l] * z;
-            const double x = cur[si] + dn;
-            if (l < H) {
-                nxt[si] = x;
-                ds[si] = dn;
-            } else if (vr < n && vc < n) {                        // the tile's own cells (h = 0: vr, vc >= 0)
-                out[vr * n + vc] = x;
+    // level 0 over the whole staged region: thn, b, x0 = d0 = c2_0 (b / diag); every load issued before the first
+    // LDS store, so one memory latency covers the staging
+    {
+        constexpr int IT = (G::N + 255) / 256;
+        double bv[IT], tv[IT], dv[IT];
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256;
+            if (i < G::N) {
+                const int rr = i / G::RW, cc = i - rr * G::RW;
+                const int32_t k = P.wrap(rb + rr) * n + P.wrap(cb + cc);
+                bv[it] = b[k];
+                tv[it] = P.cell[k];
+                dv[it] = diag[k];
             }
         }
-        __syncthreads();
-        double* t = cur;
-        cur = nxt;
-        nxt = t;
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256;
+            if (i < G::N) {
+                ts[i] = tv[it];
+                bs[i] = bv[it];
+                const double x0 = ck.c2[0] * (bv[it] / dv[it]);
+                xa[i] = x0;
+                ds[i] = x0;
+            }
+        }
     }
+    __syncthreads();
+    // the entries: N, W (and, inside level 1's region, C) of staged rows / columns 1 .. R - 1
+    {
+        const TTile<H> ta{ts, rb, cb};
+        for (int i = tid; i < G::EN; i += 256) {
+            const int er = i / G::EW, ec_ = i - er * G::EW;
+            const int vr = rb + 1 + er, vc = cb + 1 + ec_;
+            if (er < G::EH - 1 && ec_ < G::EW - 1) {     // a level-1 cell: all five (C needs the E and S neighbours)
+                double e[5];
+                P.entries(vr, vc, P.wrap(vr), P.wrap(vc), ta, e);
+                en[i] = e[0];
+                ew[i] = e[1];
+                ec[i] = e[2];
+            } else {
+                P.entries_nw(vr, vc, ta, &en[i], &ew[i]);
+            }
+        }
+    }
+    __syncthreads();
+    gtg_levels<H, 1>(P, GtgE{en, ew, ec}, bs, ds, xa, xb, ck, out, r0, c0);
 }
 
 // One thread per (slice, lane): copy the CSR row into its column-major slots.
@@ -3376,6 +3687,11 @@ int mpbp_set_gtg_fused(int32_t on) {
 int mpbp_set_f_tile(int32_t on) {
     if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "f_tile must be 0 or 1");
     g_f_tile = on;
+    return MPBP_OK;
+}
+int mpbp_set_f_solve(int32_t on) {
+    if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "f_solve must be 0 or 1");
+    g_f_solve = on;
     return MPBP_OK;
 }
 int mpbp_set_f_pair(int32_t on) {
@@ -4977,11 +5293,17 @@ int launch_gtg_solve_t(const GtGStencilDev& S, const double* b, const double* di
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
+// k_gtg_solve reads a cell's E and S entries as its neighbours' W and N: bit for bit when minv == -inv.
+bool gtg_symmetric(const mpbp_schur_plan* p) {
+    PGDev P;
+    return make_pgstencil(&p->f_prm, p->f_cell, nullptr, &P) == MPBP_OK && P.minv == -P.inv;
+}
 // The tile's staged cells must wrap onto the grid at most once each way (P.wrap), so n >= a tile plus its halos.
 bool gtg_fused_ok(const mpbp_schur_plan* p) {
     const mpbp_inner_solver& in = p->inner_P;
     return g_gtg_fused && p->pg_stencil && !p->halo && in.kind == MPBP_INNER_CHEBYSHEV && in.sweeps >= 2 &&
-           in.sweeps <= 6 && in.lmax > in.lmin && in.lmin >= 0.0 && p->f_prm.n >= kGTW + kGTH + 2 * (in.sweeps - 1);
+           in.sweeps <= 6 && in.lmax > in.lmin && in.lmin >= 0.0 && p->f_prm.n >= kGTW + kGTH + 2 * (in.sweeps - 1) &&
+           gtg_symmetric(p);
 }
 int gtg_solve_fused(const mpbp_schur_plan* p, const double* b, double* out, hipStream_t st) {
     PGDev P;
@@ -5039,6 +5361,22 @@ int f_pair(const mpbp_schur_plan* p, int ext, const double* x_in, const double* 
 // x = M^-1 b by `inner` sweeps from x0 = 0 (solve.py:251/254 F_inv / Gt_G_factorization roles).
 // The final iterate goes to dst (sub - iterate when sub != NULL); ping/pong hold the others.  x0_pre (Gt_G,
 // Chebyshev, fusable first sweep): the first iterate c2[0] b / diag already computed by b's producer.
+// fn() bracketed by the plan's profiling events (mpbp_schur_plan.prof_events) when asked and not capturing.
+template <class Fn>
+int profiled(const mpbp_schur_plan* p, bool profile, hipStream_t st, Fn&& fn) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const bool rec = profile && p->prof_events && p->prof_count && *p->prof_count < p->prof_capacity &&
+                     hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone;
+    if (rec) MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count], st));
+    const int rc = fn();
+    if (rc) return rc;
+    if (rec) {
+        MPBP_HIP(record_event((hipEvent_t)p->prof_events[2 * *p->prof_count + 1], st));
+        ++*p->prof_count;
+    }
+    return MPBP_OK;
+}
+
 int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag, const mpbp_inner_solver& in,
                 int32_t nrows, const double* b, double* dst, const double* sub, double* ping, double* pong,
                 double* dir, bool profile, const double* x0_pre = nullptr) {
@@ -5063,6 +5401,14 @@ int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag
         cheb_coeffs(in.lmin, in.lmax, K, c1, c2);
     } else if (in.kind != MPBP_INNER_JACOBI) {
         return set_error(MPBP_ERR_ARG, "unknown inner solver %d", in.kind);
+    }
+    // tolerance-mode F on one GPU: the whole solve as one launch
+    if (cheb && f_pair_ok(c.p) && g_f_solve && op.in.stencil && op.in.sop == SOP_F && op.bd.empty && op.in.which == 0 &&
+        !c.p->halo && fsolve_ok(K, c.p->f_prm.n)) {
+        FStencilDev P;
+        int rc = make_fstencil(&c.p->f_prm, c.p->f_cell, c.p->f_uface, c.p->f_vface, nullptr, &P);
+        if (rc) return rc;
+        return profiled(c.p, profile, c.st, [&] { return launch_fsolve(P, K, c1, c2, b, sub, dst, c.st); });
     }
     double* cur = (K == 1) ? dst : ping;
     int s = 1, rc = MPBP_OK;
@@ -5132,6 +5478,8 @@ int f_solve_gx(const Ctx& c, const double* xp, const mpbp_inner_solver& in, doub
     rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &G);
     if (rc) return rc;
     const GxB bs{xp, G.d_p, G.inv, G.minv, G.n};
+    if (f_pair_ok(p) && g_f_solve && fsolve_ok(K, P.n))   // the whole solve as one launch
+        return profiled(p, profile, c.st, [&] { return launch_fsolve(P, K, c1, c2, nullptr, sub, dst, c.st, bs); });
     double* cur = K == 2 ? dst : pong;
     if (p->f_numerics == MPBP_NUMERICS_FAST && g_f_tile && ftile_ok(P.n))   // x0 and sweep 1 on 2D tiles
         rc = launch_ftile<true>(P, FTile{nullptr, nullptr, nullptr, K == 2 ? sub : nullptr, cur, K == 2 ? nullptr : dir,

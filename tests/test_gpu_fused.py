@@ -79,12 +79,40 @@ def test_ftile_equals_marching(n, kf, fuse_g):
     v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda",
                     generator=torch.Generator(device="cuda").manual_seed(n * 10 + kf))
     try:
+        check(lib().mpbp_set_f_solve(0))   # the whole-solve launch would take over kf = 3, 4 either way
         check(lib().mpbp_set_f_tile(0))
         ref = pc.apply(v).clone()
         check(lib().mpbp_set_f_tile(1))
         got = pc.apply(v)
     finally:
         check(lib().mpbp_set_f_tile(1))
+        check(lib().mpbp_set_f_solve(1))
+    assert torch.equal(got, ref), float((got - ref).abs().max())
+
+
+@pytest.mark.parametrize("n", [3, 5, 64, 70, 71, 72, 76, 100, 128, 255, 256, 300])
+@pytest.mark.parametrize("kf", [2, 3, 4, 5])
+@pytest.mark.parametrize("fuse_g", [True, False])
+def test_fsolve_equals_ftile(n, kf, fuse_g):
+    """k_fsolve (a whole fast F solve of 3 or 4 updates in one tiled launch: x0 and every sweep over a shrinking halo,
+    each cell's state in its owning lane) performs the k_ftile launches' operations: the apply is bit-identical with it
+    on and off, with G x_p recomputed in the second solve and launched separately, on grids below, at and above its
+    minimum (n >= 70 for 3 updates, 72 for 4) and not multiples of the 64 x 8 tile."""
+    import mp_block_preconditioners_amd as mp
+    from mp_block_preconditioners_amd._lib import check, lib
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("chebyshev", kf),
+                                      inner_P=mp.InnerSolver("chebyshev", 4), numerics="fast", fuse_g=fuse_g)
+    v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda",
+                    generator=torch.Generator(device="cuda").manual_seed(n * 10 + kf + 7))
+    try:
+        check(lib().mpbp_set_f_solve(0))
+        ref = pc.apply(v).clone()
+        check(lib().mpbp_set_f_solve(1))
+        got = pc.apply(v)
+    finally:
+        check(lib().mpbp_set_f_solve(1))
     assert torch.equal(got, ref), float((got - ref).abs().max())
 
 

@@ -10,6 +10,7 @@
 #   bench        bench.py, N = 1 (the driver's command)        bench_csr bench.py --layout csr
 #   bench:ARGS   bench.py ARGS ('+' for spaces; MPBP_BENCH_BACKEND etc. from the environment), appended to bench_args.log
 #   rows2_gloo   bench.py --gpus 2 --grid 512 over gloo on one GPU (the N > 1 path; launcher inside bench.py)
+#   gloo:N       bench.py --gpus N (configs[4]'s 2048^2) over gloo on one GPU: the N > 1 line's sections rehearsed
 #   selfhalo     bench.py --self-halo (partitioned apply over the RCCL self-exchange)
 #   probe        tools/capture_probe.py 256 1024 (hipGraph capture of the partitioned apply); probe:N1,N2 sizes
 #   prof         rocprofv3 --kernel-trace --stats of bench.py
@@ -51,6 +52,8 @@ step() {
                  > "$OUT/bench_csr.log" 2>&1 ;;
     rows2_gloo) MPBP_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --steps 5 --warmup 2 --grid 512 \
                   > "$OUT/rows2_gloo.log" 2>&1 ;;
+    gloo:*) MPBP_BENCH_BACKEND=gloo timeout -k 10 900 python bench.py --gpus ${s#gloo:} --steps 5 --warmup 2 \
+              > "$OUT/gloo_${s#gloo:}.log" 2>&1 ;;
     selfhalo) timeout -k 10 300 python bench.py --self-halo --steps 20 --warmup 5 --no-cpu-baseline --no-spmv \
                 > "$OUT/selfhalo.log" 2>&1 ;;
     probe) timeout -k 10 120 python -u tools/capture_probe.py 256 1024 > "$OUT/probe.log" 2>&1 ;;
