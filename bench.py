@@ -374,7 +374,7 @@ def main():
         try:
             with open(pmc_files[-1]) as f:
                 pm = json.load(f)
-            key = "stencil" if getattr(pc, "f_stencil", None) is not None else args.layout
+            key = ("fsolve" if f_solve else "stencil") if getattr(pc, "f_stencil", None) is not None else args.layout
             if int(pm.get("n", -1)) == n and key in pm:
                 traffic = pm[key]["traffic_bytes_corrected"]
             if spmv is not None and int(pm.get("n", -1)) == n and "csr_spmv_A" in pm:
@@ -467,9 +467,14 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
                          "bytes_per_launch": sbytes, "avg_launch_us": avg_sweep_s * 1e6,
                          "launches_timed": n_timed,
-                         "timing": "HIP events around each plain sweep of the first F solve on the apply stream"
-                                   + ", eager pass of the same K applies after the timed loop",
-                         "events": EVENT_NOTE},
+                         "timing": ("HIP events around the first F solve's launch" if f_solve else
+                                    "HIP events around each plain sweep of the first F solve")
+                                   + " on the apply stream, eager pass of the same K applies after the timed loop",
+                         "events": EVENT_NOTE,
+                         **({"note": "the whole solve is one launch: b, thn and faces read and x written once (HBM "
+                                     "bytes a third of the two-launch path's 285.6 MB), so the kernel is bound by fp64 "
+                                     "VALU issue, not HBM -- its SQ counters are in profiles/ (DESIGN.md section 4)"}
+                            if f_solve else {})},
             "roofline_second_f_solve": {
                 "bound": "hbm", "achieved": gbytes / g_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": gbytes / g_s / 1e9 / HBM_PEAK_GBS, "bytes_per_launch": gbytes, "avg_launch_us": g_s * 1e6,

@@ -25,7 +25,8 @@ int g_march_rows = 0;
 int g_csr_table = 1;      // CSR SpMV waves start from the row blocks' wave table when it has one (0: from row_ptr)
 int g_mg_mf_transfer = 1;   // whole-grid multigrid transfers matrix-free (0: their CSR / SELL / grouped forms)
 int g_init_diag = 1;      // fused first F sweep: 1 rebuilds the staged diagonal from thn, 0 streams diag
-int g_mg_gal = 1;          // tolerance-mode F hierarchies: level 1 as R_0 (F (P_0 x)) (MgGal; 0: its stored matrix)
+int g_mg_gal = 2;          // tolerance-mode F hierarchies: level 1 as R_0 (F (P_0 x)): 2 one k_gal1 launch, 1 three
+                           // launches (MgGal), 0 its stored Galerkin matrix
 int g_f_direct = 0;        // tolerance-mode F sweeps on the direct kernel (one thread per cell, no LDS) instead of marching
 int g_gtg_fused = 1;       // one-GPU Chebyshev Gt_G solves of 2..6 sweeps as one k_gtg_solve launch (0: per sweep)
 int g_f_solve = 1;         // one-GPU tolerance-mode F solves of 3 or 4 Chebyshev updates as one launch (k_fsolve)
@@ -1921,7 +1922,7 @@ struct XInit {         // staged value = the first inner iterate: c2 * (b[i] / d
 // (solve.py:274) reads one pressure field (8 B per cell, cached neighbours) instead of W's four (32 B per cell),
 // and W is never written.  One GPU (whole-grid layouts).
 struct BNone {
-    static constexpr bool on = false;
+    static constexpr bool on = false, part = false;
     struct Q {};
     __device__ Q load(int, int, int) const { return {}; }
     template <class TA>
@@ -1930,7 +1931,7 @@ struct BNone {
 // PART: x_p in a row partition's ghost layout (L owned rows, h ghost rows each side); else the whole grid.
 template <bool PART>
 struct GxBT {
-    static constexpr bool on = true;
+    static constexpr bool on = true, part = PART;
     const double* __restrict__ xp;
     double d_p, inv, minv;
     int n;
@@ -1947,19 +1948,23 @@ struct GxBT {
     // cell's wrapped column gc decides the periodic order as GStencilDev::row does
     template <class TA>
     __device__ double b(int o, int gr, int c, int gc, const TA& ta, const Q& q) const {
+        return b_at(o, gr, c, gc == 0, gr == 0, ta, q);
+    }
+    // the same with ta at coordinates (r, c) of the accessor's own and the cell's periodic position given as flags:
+    // wrapw, its grid column is 0 (its west neighbour wraps); wrapn, its grid row is 0
+    template <class TA>
+    __device__ double b_at(int o, int r, int c, bool wrapw, bool wrapn, const TA& ta, const Q& q) const {
         const int p = o >> 1;
-        const double t0 = ta.T(p, gr, c);
+        const double t0 = ta.T(p, r, c);
         double acc = 0.0;
         if ((o & 1) == 0) {   // u row: entries p(gr, gc-1), p(gr, gc); the wrapped one sorts last
-            const double gu = 0.5 * (t0 + ta.T(p, gr, c - 1));
+            const double gu = 0.5 * (t0 + ta.T(p, r, c - 1));
             const double uC = (d_p * (inv * gu)) * q.c, uW = (d_p * (minv * gu)) * q.w;
-            const bool wrapw = gc == 0;
             acc += wrapw ? uC : uW;
             acc += wrapw ? uW : uC;
         } else {              // v row: entries p(gr-1, gc), p(gr, gc)
-            const double gv = 0.5 * (t0 + ta.T(p, gr - 1, c));
+            const double gv = 0.5 * (t0 + ta.T(p, r - 1, c));
             const double vC = (d_p * (minv * gv)) * q.c, vN = (d_p * (inv * gv)) * q.nn;
-            const bool wrapn = gr == 0;
             acc += wrapn ? vC : vN;
             acc += wrapn ? vN : vC;
         }
@@ -2891,19 +2896,34 @@ __device__ inline void fs_ring_cell(int r, int j, int r0, int c0, int& vr, int& 
     }
 }
 
-template <int H, bool SUB, class BS>
+// PART (row partition, the CA schedule): the tiles cover the owned rows and P.ext ghost rows each side; b and x are
+// in the partition's ghost layout (P.xrow, P.out_row), the thn tables global.  Rows past b's ghost depth (padding of
+// the last tile row and its halo, which no output reads) load a clamped row.
+template <int H, bool SUB, bool PART, class BS>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8)))
 k_fsolve(FStencilFast P, FSolve a, BS bs) {
     using T = FsTile<H>;
     constexpr int NS = H + 1;   // owned cells with updates after x0: the two tile cells and rings 1 .. H - 1
+    constexpr int PW = T::RW + 1, PN = PW * (T::RH + 1);   // BS: x_p over the tile + H, + its west / north neighbours
     __shared__ double ts[T::TN];
     __shared__ double xa[4 * T::N], xb[4 * T::N];
+    __shared__ double ps[BS::on ? PN : 1];
     const int n = P.n, nn = n * n;
     const int tx = (n + kFTW - 1) / kFTW;
     const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
-    const int r0 = (bk / tx) * kFTH, c0 = (bk % tx) * kFTW;
+    const int lo = PART ? P.r0 - P.ext : 0, hi = PART ? P.r0 + P.L + P.ext : n;   // output rows [lo, hi)
+    const int r0 = lo + (bk / tx) * kFTH, c0 = (bk % tx) * kFTW;
     const int rbt = r0 - H - 1, cbt = c0 - H - 1, rb = r0 - H, cb = c0 - H;
     const int tid = threadIdx.x;
+    // a row of the input layouts: the virtual row itself (one GPU: wrapped) or, clamped to the ghost depth, local
+    auto in_row = [&](int vr, int h) {
+        if constexpr (PART) {
+            const int lr = vr - P.r0;
+            return lr < -h ? -h : (lr >= P.L + h ? P.L + h - 1 : lr);
+        } else {
+            return P.wrap(vr);
+        }
+    };
     {
         constexpr int IT = (T::TN + 255) / 256;
         double v[IT];
@@ -2921,9 +2941,26 @@ k_fsolve(FStencilFast P, FSolve a, BS bs) {
             if (i < T::TN) ts[i] = v[it];
         }
     }
+    if constexpr (BS::on) {
+        constexpr int IT = (PN + 255) / 256;
+        double v[IT];
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256;
+            if (i < PN) {
+                const int sr = i / PW, sc = i - sr * PW;
+                const int pr = in_row(rb - 1 + sr, PART ? bs.h : 0);
+                v[it] = bs.xp[(PART ? ext_row(1, 0, pr, P.L, bs.h, n) : pr * n) + P.wrap(cb - 1 + sc)];
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256;
+            if (i < PN) ps[i] = v[it];
+        }
+    }
     __syncthreads();
     const TTileT<T::TW> tt{ts, rbt, cbt};
-    const TTileWT<T::TW> tw{ts, rbt, cbt, n};
     const int lr = tid >> 6, lc = tid & 63;
     // the owned cells: slot 0, 1 the tile cells, slot 1 + r ring r (r = 1 .. H; slot H + 1 only needs x0)
     int cr[NS + 1], cc[NS + 1];
@@ -2945,11 +2982,17 @@ k_fsolve(FStencilFast P, FSolve a, BS bs) {
         const int32_t k = gr * n + gc;
         const FStencilDev::Stage sg{{P.uface[k], P.vface[k]}};
         double b4[4], r4[4];
-        typename BS::Q q{};
-        if constexpr (BS::on) q = bs.load(gr, gr, gc);
         P.rdiag4(vr, vc, tt, sg, r4);
+        if constexpr (BS::on) {   // b = G x_p, x_p and thn from LDS at virtual coordinates
+            const int pi = (vr - rb + 1) * PW + (vc - cb + 1);
+            const typename BS::Q q{ps[pi], ps[pi - 1], ps[pi - PW]};
 #pragma unroll
-        for (int f = 0; f < 4; ++f) b4[f] = BS::on ? bs.b(f, gr, gc, gc, tw, q) : a.b[f * nn + k];
+            for (int f = 0; f < 4; ++f) b4[f] = bs.b_at(f, vr, vc, gc == 0, gr == 0, tt, q);
+        } else {
+            const int br = in_row(vr, P.h);
+#pragma unroll
+            for (int f = 0; f < 4; ++f) b4[f] = a.b[(PART ? ext_row(4, f, br, P.L, P.h, n) : (f * n + br) * n) + gc];
+        }
         const int si = (vr - rb) * T::RW + (vc - cb);
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
@@ -2978,7 +3021,7 @@ k_fsolve(FStencilFast P, FSolve a, BS bs) {
         for (int sl = 0; sl < NS; ++sl) {
             if (sl >= 2 && (sl - 1 > H - l || !own[sl])) continue;   // ring r = sl - 1 lives through level H - r
             const int vr = cr[sl], vc = cc[sl];
-            if (l == H && (vr >= n || vc >= n)) continue;             // a tile past the grid's last row / column
+            if (l == H && (vr >= hi || vc >= n)) continue;            // a tile past the last row / column
             double acc[4], rdx[4];
             P.template rows4<false>(vr, vc, tt, xt, FStencilDev::Cell{{fc[sl][0], fc[sl][1]}}, acc, rdx);
             const int si = (vr - rb) * T::RW + (vc - cb);
@@ -2991,7 +3034,7 @@ k_fsolve(FStencilFast P, FSolve a, BS bs) {
                     nxt[f * T::N + si] = x;
                     d[sl][f] = dn;
                 } else {
-                    const int32_t o = f * nn + vr * n + vc;
+                    const int32_t o = PART ? P.out_row(f, vr - P.r0, vc) : f * nn + vr * n + vc;
                     a.x_out[o] = SUB ? a.sub[o] - x : x;
                 }
             }
@@ -3005,28 +3048,45 @@ k_fsolve(FStencilFast P, FSolve a, BS bs) {
 // Grids a tile's staged thn (tile + H + 1 each side) wraps onto at most once.
 template <int H>
 inline bool fsolve_ok_n(int n) { return n >= FsTile<H>::TW && n >= FsTile<H>::TH; }
-template <int H, class BS>
+template <int H, bool PART, class BS>
 int launch_fsolve_t(const FStencilFast& P, const FSolve& a, hipStream_t st, const BS& bs) {
-    const int64_t tiles = (int64_t)((P.n + kFTW - 1) / kFTW) * ((P.n + kFTH - 1) / kFTH);
-    if (a.sub) k_fsolve<H, true, BS><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
-    else k_fsolve<H, false, BS><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
+    const int rows = PART ? P.L + 2 * P.ext : P.n;
+    const int64_t tiles = (int64_t)((P.n + kFTW - 1) / kFTW) * ((rows + kFTH - 1) / kFTH);
+    if (a.sub) k_fsolve<H, true, PART, BS><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
+    else k_fsolve<H, false, PART, BS><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
-// One GPU, whole grid, K = 3 or 4 Chebyshev updates (x0 and H = K - 1 stencil sweeps).
+// K = 3 or 4 Chebyshev updates (x0 and H = K - 1 stencil sweeps); columns wrap at most once per tile.
 inline bool fsolve_ok(int K, int n) { return (K == 3 && fsolve_ok_n<2>(n)) || (K == 4 && fsolve_ok_n<3>(n)); }
+// One GPU, whole grid (P.h == 0), or a row partition's owned rows + P.ext ghost rows (P.which == 3), b's ghost depth
+// P.h >= P.ext + H (+ 1 for x_p's with GxBPart).
 template <class BS = BNone>
 int launch_fsolve(const FStencilDev& Pd, int K, const double* c1, const double* c2, const double* b, const double* sub,
                   double* x_out, hipStream_t st, const BS& bs = BS{}) {
     const FStencilFast P{Pd};
-    if (P.h != 0 || P.which != 0 || !fsolve_ok(K, P.n)) return set_error(MPBP_ERR_ARG, "fsolve: one GPU, whole grid");
+    const bool part = P.h != 0;
+    int xp_h = 0;   // x_p's ghost depth (GxBPart)
+    if constexpr (BS::on) {
+        if (BS::part != part) return set_error(MPBP_ERR_ARG, "fsolve: G x_p's layout does not match F's");
+        if constexpr (BS::part) xp_h = bs.h;
+    }
+    if (!fsolve_ok(K, P.n) || (!part && P.which != 0) ||
+        (part && (P.which != 3 || P.h < P.ext + K - 1 || P.oh < P.ext || (BS::on && xp_h < P.ext + K))))
+        return set_error(MPBP_ERR_ARG, "fsolve: one GPU whole grid, or owned + ext rows with b ext + K - 1 deep");
     if (!x_out || (!BS::on && !b) || x_out == b) return set_error(MPBP_ERR_ARG, "fsolve: bad vectors");
     FSolve a{b, sub, x_out, c2[0], {}, {}};
     for (int l = 1; l < K; ++l) {
         a.c1[l - 1] = c1[l];
         a.c2[l - 1] = c2[l];
     }
-    return K == 3 ? launch_fsolve_t<2>(P, a, st, bs) : launch_fsolve_t<3>(P, a, st, bs);
+    constexpr bool bpart = BS::on && BS::part;   // GxBPart launches only the partitioned kernel, GxB the other
+    if constexpr (BS::on) {
+        return K == 3 ? launch_fsolve_t<2, bpart>(P, a, st, bs) : launch_fsolve_t<3, bpart>(P, a, st, bs);
+    } else {
+        if (part) return K == 3 ? launch_fsolve_t<2, true>(P, a, st, bs) : launch_fsolve_t<3, true>(P, a, st, bs);
+        return K == 3 ? launch_fsolve_t<2, false>(P, a, st, bs) : launch_fsolve_t<3, false>(P, a, st, bs);
+    }
 }
 
 // Sweeps s, s+1 of an F Chebyshev solve fused (k_march2, tolerance mode) over the rows P.which selects (0: the whole
@@ -3272,34 +3332,6 @@ struct GtGStencilDev : PGDev {
         }
         e[0] = -1.0 * cN; e[1] = -1.0 * cW; e[2] = -1.0 * cC; e[3] = -1.0 * cE; e[4] = -1.0 * cS;
     }
-    // entries N and W alone, by the operations entries() performs for them (k_gtg_solve: with minv == -inv, the E entry
-    // of a cell is bit for bit the W entry of its east neighbour and S the N entry of its south one)
-    template <class TA>
-    __device__ void entries_nw(int vr, int vc, const TA& ta, double* eN, double* eW) const {
-        double cN = 0.0, cW = 0.0;
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            const double t0 = ta.T(p, vr, vc), tW = ta.T(p, vr, vc - 1), tN = ta.T(p, vr - 1, vc);
-            double qW, qN;
-            if (unit) {
-                const double XW = inv * (0.5 * (t0 + tW)), XN = inv * (0.5 * (t0 + tN));
-                qW = XW * XW;
-                qN = XN * XN;
-            } else {
-                const double DuC = minv * (0.5 * (t0 + tW)), DvC = inv * (0.5 * (t0 + tN));
-                const double gC = 0.5 * (t0 + tW), gN = 0.5 * (t0 + tN);
-                qW = DuC * (d_p * (minv * gC));
-                qN = DvC * (d_p * (inv * gN));
-            }
-            if (p == 0) {
-                cW = qW; cN = qN;
-            } else {
-                cW += qW; cN += qN;
-            }
-        }
-        *eN = -1.0 * cN;
-        *eW = -1.0 * cW;
-    }
     // Gt_G x at a cell: the five entries summed in CSR column order (EDGE: sorted by wrapped column)
     template <bool EDGE, class TA, class XA>
     __device__ double apply_v(int vr, int vc, int gr, int gc, const TA& ta, const XA& xa, double* dg) const {
@@ -3318,24 +3350,22 @@ struct GtGStencilDev : PGDev {
 
 // ---- one Gt_G Chebyshev solve in one launch (k_gtg_solve) ----
 // The pressure solves x = Gt_G^-1 b of the apply (solve.py:265, 271) as K Chebyshev-Jacobi sweeps from x0 = 0, fused:
-// a workgroup owns a TW x TH tile of cells and stages b and thn over the tile plus a halo of H = K - 1 cells (its
-// level 0, x0 = d0 = c2_0 (b / diag), built there from the stored diagonal).  The matrix entries depend on thn only, so
-// they are built once per launch, not once per level: the N, W and C entries of every cell of level 1's region (plus
-// N one row below it and W one column right of it) go to LDS, and a cell's E and S entries are its east neighbour's W
-// and its south neighbour's N (bit for bit when minv == -inv, which gtg_fused_ok requires).  Level l = 1 .. H then
-// recomputes the tile with halo H - l from level l - 1 in LDS with five LDS entries, and the last level writes the tile.
-// Each row is GtGStencilDev::apply_v's IEEE operations (the entries', the products', add5's column order) and each
-// update the Chebyshev epilogue's (EpiChebFirst at level 1, EpiCheb after): bit-identical to the K - 1 sweeps of the
-// per-sweep path, for one launch and one pass over b instead of K - 1 passes over x, d, b.  thn's LDS is reused for the
-// levels' ping-pong buffer once the entries are built.
-constexpr int kGTW = 64, kGTH = 8;
+// a workgroup owns a TW x TH tile of cells and stages b and thn over the tile plus a halo of H = K - 1 cells, and
+// x0 = d0 = c2_0 (b / diag) there from the stored diagonal (level 0).  Level l = 1 .. H recomputes the tile with halo
+// H - l from level l - 1 (LDS ping-pong), the last writing the tile.  As in k_fsolve every cell has one owning lane for
+// all its levels (the lane's two tile cells, and cell t of each halo ring r = 1 .. H - 1), which builds the cell's five
+// entries once (GtGStencilDev::entries, from the staged thn) and keeps them, b and d in registers: a level reads only
+// the five x values of the stencil from LDS.  Each row is GtGStencilDev::apply_v's IEEE operations (the entries', the
+// products', add5's column order) and each update the Chebyshev epilogue's (EpiChebFirst at level 1, EpiCheb after):
+// bit-identical to the K - 1 sweeps of the per-sweep path, for one launch and one pass over b instead of K - 1 passes
+// over x, d, b.
+constexpr int kGTW = kFTW, kGTH = kFTH;   // the 64 x 8 tile and ring numbering of k_fsolve (fs_ring_cell)
 struct ChebK {
     double c1[8], c2[8];   // sweep s's coefficients (c2[0]: the initial iterate's)
 };
 template <int H>
 struct GtgTile {
     static constexpr int RW = kGTW + 2 * H, RH = kGTH + 2 * H, N = RW * RH;
-    static constexpr int EW = RW - 1, EH = RH - 1, EN = EW * EH;   // entries: staged rows / columns 1 .. R - 1
 };
 template <int H>
 struct TTile {   // thn of the staged tile; (r, c) in the tile's virtual grid coordinates
@@ -3346,76 +3376,24 @@ struct TTile {   // thn of the staged tile; (r, c) in the tile's virtual grid co
         return sph ? 1.0 - v : v;
     }
 };
-struct GtgE {   // the LDS entries: [EH][EW] each, slot 0 = staged cell (1, 1)
-    double* n;
-    double* w;
-    double* c;
-};
 
-// Level L (1 .. H) of k_gtg_solve: the tile with halo H - L from level L - 1 in `cur` (compile-time extents, so the
-// cell index splits with a multiply-shift).
-template <int H, int L>
-__device__ inline void gtg_level(const GtGStencilDev& P, const GtgE& E, const double* bs, double* ds, const double* cur,
-                                 double* nxt, const ChebK& ck, double* __restrict__ out, int r0, int c0) {
-    using G = GtgTile<H>;
-    constexpr int h = H - L, w = kGTW + 2 * h, cells = w * (kGTH + 2 * h);
-    const int n = P.n, tid = threadIdx.x;
-    const double c1 = ck.c1[L], c2 = ck.c2[L];
-#pragma unroll
-    for (int i0 = 0; i0 < cells; i0 += 256) {
-        const int i = i0 + tid;
-        const bool live = i < cells;
-        const int ii = live ? i : 0;
-        const int lr = ii / w, lc = ii - lr * w;
-        const int vr = r0 - h + lr, vc = c0 - h + lc;        // virtual cell
-        const int gr = P.wrap(vr), gc = P.wrap(vc);
-        const int si = (lr + L) * G::RW + (lc + L);          // its staged index
-        const int ei = (lr + L - 1) * G::EW + (lc + L - 1);  // its entry index
-        const bool edge = __builtin_amdgcn_readfirstlane(__any(live && (gr == 0 || gr == n - 1 || gc == 0 ||
-                                                                        gc == n - 1))) != 0;
-        if (live) {
-            const double dg = E.c[ei];
-            const double p[5] = {E.n[ei] * cur[si - G::RW], E.w[ei] * cur[si - 1], dg * cur[si],
-                                 E.w[ei + 1] * cur[si + 1], E.n[ei + G::EW] * cur[si + G::RW]};
-            const Wrap wr{gr == 0, gr == n - 1, gc == 0, gc == n - 1};
-            const double acc = edge ? add5<true>(0.0, p, wr) : add5<false>(0.0, p, wr);
-            const double z = (bs[si] - acc) / dg;
-            const double dn = c1 * ds[si] + c2 * z;
-            const double x = cur[si] + dn;
-            if constexpr (L < H) {
-                nxt[si] = x;
-                ds[si] = dn;
-            } else if (vr < n && vc < n) {                    // the tile's own cells (h = 0: vr, vc >= 0)
-                out[vr * n + vc] = x;
-            }
-        }
-    }
-}
-template <int H, int L>
-__device__ inline void gtg_levels(const GtGStencilDev& P, const GtgE& E, const double* bs, double* ds, double* cur,
-                                  double* nxt, const ChebK& ck, double* __restrict__ out, int r0, int c0) {
-    gtg_level<H, L>(P, E, bs, ds, cur, nxt, ck, out, r0, c0);
-    if constexpr (L < H) {
-        __syncthreads();
-        gtg_levels<H, L + 1>(P, E, bs, ds, nxt, cur, ck, out, r0, c0);
-    }
-}
-
-template <int H>
+// PART: the tiles cover a row partition's owned rows and P.ext ghost rows each side (the CA schedule); b and diag in
+// its ghost layout (depth P.h >= P.ext + H; deeper rows, read only for cells no output depends on, clamped), out in
+// the output layout (depth P.oh).
+template <int H, bool PART>
 __global__ void __launch_bounds__(256) k_gtg_solve(GtGStencilDev P, const double* __restrict__ b,
                                                    const double* __restrict__ diag, ChebK ck, double* __restrict__ out) {
     using G = GtgTile<H>;
-    __shared__ double bs[G::N], xa[G::N], xb[G::N], ds[G::N];   // xb: thn until the entries are built
-    __shared__ double en[G::EN], ew[G::EN], ec[G::EN];
-    double* ts = xb;
+    constexpr int NS = H + 1;   // owned cells with sweeps: the two tile cells and rings 1 .. H - 1
+    __shared__ double ts[G::N], bs[G::N], xa[G::N], xb[G::N];
     const int n = P.n;
     const int tx = (n + kGTW - 1) / kGTW;
     const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
-    const int r0 = (bk / tx) * kGTH, c0 = (bk % tx) * kGTW;
+    const int lo = PART ? P.r0 - P.ext : 0, hi = PART ? P.r0 + P.L + P.ext : n;   // output rows [lo, hi)
+    const int r0 = lo + (bk / tx) * kGTH, c0 = (bk % tx) * kGTW;
     const int rb = r0 - H, cb = c0 - H;   // virtual coordinates of staged cell 0
     const int tid = threadIdx.x;
-    // level 0 over the whole staged region: thn, b, x0 = d0 = c2_0 (b / diag); every load issued before the first
-    // LDS store, so one memory latency covers the staging
+    // level 0 over the whole staged region: thn, b, x0 = c2_0 (b / diag); every load issued before the first LDS store
     {
         constexpr int IT = (G::N + 255) / 256;
         double bv[IT], tv[IT], dv[IT];
@@ -3424,10 +3402,16 @@ __global__ void __launch_bounds__(256) k_gtg_solve(GtGStencilDev P, const double
             const int i = tid + it * 256;
             if (i < G::N) {
                 const int rr = i / G::RW, cc = i - rr * G::RW;
-                const int32_t k = P.wrap(rb + rr) * n + P.wrap(cb + cc);
-                bv[it] = b[k];
-                tv[it] = P.cell[k];
-                dv[it] = diag[k];
+                const int gr = P.wrap(rb + rr), gc = P.wrap(cb + cc);
+                int32_t kb = gr * n + gc;
+                if constexpr (PART) {
+                    int lr = rb + rr - P.r0;
+                    lr = lr < -P.h ? -P.h : (lr >= P.L + P.h ? P.L + P.h - 1 : lr);
+                    kb = ext_row(1, 0, lr, P.L, P.h, n) + gc;
+                }
+                bv[it] = b[kb];
+                tv[it] = P.cell[gr * n + gc];
+                dv[it] = diag[kb];
             }
         }
 #pragma unroll
@@ -3436,32 +3420,173 @@ __global__ void __launch_bounds__(256) k_gtg_solve(GtGStencilDev P, const double
             if (i < G::N) {
                 ts[i] = tv[it];
                 bs[i] = bv[it];
-                const double x0 = ck.c2[0] * (bv[it] / dv[it]);
-                xa[i] = x0;
-                ds[i] = x0;
+                xa[i] = ck.c2[0] * (bv[it] / dv[it]);
             }
         }
     }
     __syncthreads();
-    // the entries: N, W (and, inside level 1's region, C) of staged rows / columns 1 .. R - 1
-    {
-        const TTile<H> ta{ts, rb, cb};
-        for (int i = tid; i < G::EN; i += 256) {
-            const int er = i / G::EW, ec_ = i - er * G::EW;
-            const int vr = rb + 1 + er, vc = cb + 1 + ec_;
-            if (er < G::EH - 1 && ec_ < G::EW - 1) {     // a level-1 cell: all five (C needs the E and S neighbours)
-                double e[5];
-                P.entries(vr, vc, P.wrap(vr), P.wrap(vc), ta, e);
-                en[i] = e[0];
-                ew[i] = e[1];
-                ec[i] = e[2];
+    // the owned cells (slot 0, 1: the tile's; slot 1 + r: ring r), their entries, b and d0 = x0
+    const TTile<H> ta{ts, rb, cb};
+    const int lr = tid >> 6, lc = tid & 63;
+    int cr[NS], cc[NS], si[NS];
+    bool own[NS], edge[NS];
+    double e[NS][5], bo[NS], d[NS];
+    cr[0] = r0 + lr; cc[0] = c0 + lc; own[0] = true;
+    cr[1] = r0 + 4 + lr; cc[1] = c0 + lc; own[1] = true;
+#pragma unroll
+    for (int r = 1; r < H; ++r) {
+        own[1 + r] = tid < 140 + 8 * r;
+        fs_ring_cell(r, own[1 + r] ? tid : 0, r0, c0, cr[1 + r], cc[1 + r]);
+    }
+#pragma unroll
+    for (int sl = 0; sl < NS; ++sl) {
+        const int vr = cr[sl], vc = cc[sl], gr = P.wrap(vr), gc = P.wrap(vc);
+        si[sl] = (vr - rb) * G::RW + (vc - cb);
+        edge[sl] = __builtin_amdgcn_readfirstlane(__any(own[sl] && (gr == 0 || gr == n - 1 || gc == 0 ||
+                                                                    gc == n - 1))) != 0;
+        if (own[sl]) {
+            P.entries(vr, vc, gr, gc, ta, e[sl]);
+            bo[sl] = bs[si[sl]];
+            d[sl] = xa[si[sl]];
+        }
+    }
+    double* cur = xa;
+    double* nxt = xb;
+#pragma unroll
+    for (int l = 1; l <= H; ++l) {
+        if (l > 1) __syncthreads();
+        const double c1 = ck.c1[l], c2 = ck.c2[l];
+#pragma unroll
+        for (int sl = 0; sl < NS; ++sl) {
+            if (sl >= 2 && (sl - 1 > H - l || !own[sl])) continue;   // ring r = sl - 1 lives through level H - r
+            const int vr = cr[sl], vc = cc[sl];
+            if (l == H && (vr >= hi || vc >= n)) continue;            // a tile past the last row / column
+            const int i = si[sl];
+            const double p[5] = {e[sl][0] * cur[i - G::RW], e[sl][1] * cur[i - 1], e[sl][2] * cur[i],
+                                 e[sl][3] * cur[i + 1], e[sl][4] * cur[i + G::RW]};
+            const int gr = P.wrap(vr), gc = P.wrap(vc);
+            const Wrap wr{gr == 0, gr == n - 1, gc == 0, gc == n - 1};
+            const double acc = edge[sl] ? add5<true>(0.0, p, wr) : add5<false>(0.0, p, wr);
+            const double z = (bo[sl] - acc) / e[sl][2];
+            const double dn = c1 * d[sl] + c2 * z;
+            const double x = cur[i] + dn;
+            if (l < H) {
+                nxt[i] = x;
+                d[sl] = dn;
             } else {
-                P.entries_nw(vr, vc, ta, &en[i], &ew[i]);
+                out[PART ? P.out_row(0, vr - P.r0, vc) : vr * n + vc] = x;
             }
+        }
+        double* t = cur;
+        cur = nxt;
+        nxt = t;
+    }
+}
+
+// ---- multigrid level 1 of a tolerance-mode F hierarchy in one launch (k_gal1) ----
+// A_1 x = R_0 (F (P_0 x)) (MgGal) with the two fine-size intermediates kept in LDS: a workgroup owns a 32 x 4 tile of
+// coarse cells (a 64 x 8 fine block), stages the coarse x of its four fields over the tile + 2 and thn over the fine
+// block + 2, builds t0 = P_0 x on the fine block + 2 (68 x 12), t1 = F t0 on the fine block + 1 (66 x 10, the
+// tolerance-mode rows), and R_0 t1 on its coarse rows, handing each to the level's epilogue.  Each value is built by
+// the operations of the three launches it replaces (k_mg_transfer_spmv's 1D lists and product order, FStencilFast::rows4),
+// so the result is bit-identical; HBM: x, thn and the epilogue operands once, no fine vector written or read.
+constexpr int kG1W = 32, kG1H = 4;                          // coarse tile
+constexpr int kG1FW = 2 * kG1W + 2, kG1FH = 2 * kG1H + 2;   // t1: fine [2 c0 - 1, 2 c0 + 2 W + 1)
+constexpr int kG1PW = kG1FW + 2, kG1PH = kG1FH + 2;         // t0 and thn: one more fine cell each side
+constexpr int kG1CW = kG1W + 4, kG1CH = kG1H + 4;           // coarse x: [c0 - 2, c0 + W + 2)
+template <class Epi>
+__global__ void __launch_bounds__(256) k_gal1(FStencilFast P, MgFields tr, const double* __restrict__ x, Epi epi) {
+    constexpr int CN = kG1CW * kG1CH, PN = kG1PW * kG1PH, FN = kG1FW * kG1FH;
+    __shared__ double xs[4 * CN];
+    __shared__ double ts[PN];
+    __shared__ double t0[4 * PN];
+    __shared__ double t1[4 * FN];
+    const int n = P.n, nc = n >> 1, ncc = nc * nc;
+    const int tx = (nc + kG1W - 1) / kG1W;
+    const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int cr0 = (bk / tx) * kG1H, cc0 = (bk % tx) * kG1W;     // the coarse tile
+    const int fr0 = 2 * cr0, fc0 = 2 * cc0;                      // its fine block
+    const int tid = threadIdx.x;
+    auto wrapc = [&](int a) { return a < 0 ? a + nc : (a >= nc ? a - nc : a); };
+    // a grid index to its slot in a staged window starting at virtual index `base` (the window is < the grid)
+    auto slot = [](int i, int base, int m) { int l = i - base; return l < 0 ? l + m : (l >= m ? l - m : l); };
+    {   // stage the coarse x (4 fields) and thn, every load before the first LDS store
+        constexpr int IX = (4 * CN + 255) / 256, IT = (PN + 255) / 256;
+        double vx[IX], vt[IT];
+#pragma unroll
+        for (int it = 0; it < IX; ++it) {
+            const int i = tid + it * 256;
+            if (i < 4 * CN) {
+                const int f = i / CN, j = i - f * CN, r = j / kG1CW, c = j - r * kG1CW;
+                vx[it] = x[f * ncc + wrapc(cr0 - 2 + r) * nc + wrapc(cc0 - 2 + c)];
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256;
+            if (i < PN) {
+                const int r = i / kG1PW, c = i - r * kG1PW;
+                vt[it] = P.cell[P.wrap(fr0 - 2 + r) * n + P.wrap(fc0 - 2 + c)];
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < IX; ++it)
+            if (tid + it * 256 < 4 * CN) xs[tid + it * 256] = vx[it];
+#pragma unroll
+        for (int it = 0; it < IT; ++it)
+            if (tid + it * 256 < PN) ts[tid + it * 256] = vt[it];
+    }
+    __syncthreads();
+    // t0 = P_0 x on the fine block + 2
+    for (int i = tid; i < PN; i += 256) {
+        const int r = i / kG1PW, c = i - r * kG1PW;
+        const int gr = P.wrap(fr0 - 2 + r), gc = P.wrap(fc0 - 2 + c);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            int yi[4], xi[4];
+            double yw[4], xw[4];
+            const int my = mg_p1d_fast(tr.ky[f], nc, gr, yi, yw), mx = mg_p1d_fast(tr.kx[f], nc, gc, xi, xw);
+            double acc = 0.0;
+            for (int a = 0; a < my; ++a) {
+                const double* xr = xs + f * CN + slot(yi[a], cr0 - 2, nc) * kG1CW;
+                for (int b = 0; b < mx; ++b) acc += (yw[a] * xw[b]) * xr[slot(xi[b], cc0 - 2, nc)];
+            }
+            t0[f * PN + i] = acc;
         }
     }
     __syncthreads();
-    gtg_levels<H, 1>(P, GtgE{en, ew, ec}, bs, ds, xa, xb, ck, out, r0, c0);
+    // t1 = F t0 on the fine block + 1
+    {
+        const TTileT<kG1PW> tt{ts, fr0 - 2, fc0 - 2};
+        const XTileT<kG1PW, kG1PH> xt{t0, fr0 - 2, fc0 - 2};
+        for (int i = tid; i < FN; i += 256) {
+            const int r = i / kG1FW, c = i - r * kG1FW;
+            const int vr = fr0 - 1 + r, vc = fc0 - 1 + c;
+            const int32_t k = P.wrap(vr) * n + P.wrap(vc);
+            double acc[4], rd[4];
+            P.template rows4<false>(vr, vc, tt, xt, FStencilDev::Cell{{P.uface[k], P.vface[k]}}, acc, rd);
+#pragma unroll
+            for (int f = 0; f < 4; ++f) t1[f * FN + i] = acc[f];
+        }
+    }
+    __syncthreads();
+    // R_0 t1 on the tile's coarse rows (4 fields x 128 cells), each to the epilogue
+    for (int j = tid; j < 4 * kG1W * kG1H; j += 256) {
+        const int f = j / (kG1W * kG1H), cell = j - f * (kG1W * kG1H);
+        const int cr = cr0 + cell / kG1W, cc = cc0 + cell % kG1W;
+        if (cr >= nc || cc >= nc) continue;
+        const int32_t row = f * ncc + cr * nc + cc;
+        const typename Epi::P pe = epi.pre(row);
+        int yi[4], xi[4];
+        double yw[4], xw[4];
+        const int my = mg_r1d_fast(tr.ky[f], n, cr, yi, yw), mx = mg_r1d_fast(tr.kx[f], n, cc, xi, xw);
+        double acc = 0.0;
+        for (int a = 0; a < my; ++a) {
+            const double* tr1 = t1 + f * FN + slot(yi[a], fr0 - 1, n) * kG1FW;
+            for (int b = 0; b < mx; ++b) acc += (yw[a] * xw[b]) * tr1[slot(xi[b], fc0 - 1, n)];
+        }
+        epi(row, acc, pe);
+    }
 }
 
 // One thread per (slice, lane): copy the CSR row into its column-major slots.
@@ -3670,7 +3795,7 @@ int mpbp_set_pg_direct(int32_t on) {
 }
 
 int mpbp_set_mg_galerkin_mf(int32_t on) {
-    if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "mg_galerkin_mf must be 0 or 1");
+    if (on < 0 || on > 2) return set_error(MPBP_ERR_ARG, "mg_galerkin_mf must be 0, 1 or 2");
     g_mg_gal = on;
     return MPBP_OK;
 }
@@ -4842,9 +4967,41 @@ int gal_r(const MgGal& g, Epi epi, hipStream_t st) {
     return mg_transfer_mf(g.m, 0, MPBP_MG_R, g.m->levels[0].R.nrows, g.t1, epi, st);
 }
 
+// The whole level-1 product as one k_gal1 launch (g_mg_gal == 2): four fields, a grid the staged windows wrap once.
+template <class Epi>
+int gal_fused(const MgGal& g, const double* x, Epi epi, hipStream_t st, bool* done) {
+    *done = false;
+    const mpbp_schur_plan* p = g.fine.stencil;
+    if (g_mg_gal != 2 || g.m->tr_nfields != 4 || p->f_prm.n < 2 * kG1CW || (p->f_prm.n & 1)) return MPBP_OK;
+    FStencilDev Pd;
+    const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &Pd);
+    if (rc) return rc;
+    MgFields F{};
+    F.nfields = 4;
+    for (int f = 0; f < 4; ++f) {
+        F.ky[f] = g.m->tr_ky[f];
+        F.kx[f] = g.m->tr_kx[f];
+    }
+    const int nc = p->f_prm.n / 2;
+    const int64_t tiles = (int64_t)((nc + kG1W - 1) / kG1W) * ((nc + kG1H - 1) / kG1H);
+    k_gal1<Epi><<<(unsigned)tiles, 256, 0, st>>>(FStencilFast{Pd}, F, x, epi);
+    MPBP_HIP(hipGetLastError());
+    *done = true;
+    return MPBP_OK;
+}
+
 int op_spmv(const OpRef& o, int32_t mode, const double* x, const double* z, double* y, hipStream_t st) {
     if (o.empty) return MPBP_OK;
     if (o.gal) {
+        bool done = false;
+        int rf = MPBP_OK;
+        switch (mode) {
+        case MPBP_SPMV_STORE: rf = gal_fused(*o.gal, x, EpiStore{y}, st, &done); break;
+        case MPBP_SPMV_ADD: rf = gal_fused(*o.gal, x, EpiAdd{z, y}, st, &done); break;
+        case MPBP_SPMV_RESID: rf = gal_fused(*o.gal, x, EpiResid{z, y}, st, &done); break;
+        default: break;
+        }
+        if (rf || done) return rf;
         const int rc = gal_fp(*o.gal, x, st);
         if (rc) return rc;
         switch (mode) {
@@ -4888,6 +5045,9 @@ int op_cheb(const OpRef& o, const double* xin, const double* b, const double* dg
     if (o.empty) return MPBP_OK;
     if (o.gal) {
         if (dzero) return set_error(MPBP_ERR_ARG, "cheb: a zero direction is only supported on the grouped CSR path");
+        bool done = false;
+        const int rf = gal_fused(*o.gal, xin, EpiCheb{xin, b, dg, d, c1, c2, sub, xo, store_d}, st, &done);
+        if (rf || done) return rf;
         const int rc = gal_fp(*o.gal, xin, st);
         return rc ? rc : gal_r(*o.gal, EpiCheb{xin, b, dg, d, c1, c2, sub, xo, store_d}, st);
     }
@@ -5288,28 +5448,32 @@ int d_rhs_x0(const mpbp_schur_plan* p, const double* Y, const double* v_p, doubl
 template <int H>
 int launch_gtg_solve_t(const GtGStencilDev& S, const double* b, const double* diag, const ChebK& ck, double* out,
                        hipStream_t st) {
-    const int64_t tiles = (int64_t)((S.n + kGTW - 1) / kGTW) * ((S.n + kGTH - 1) / kGTH);
-    k_gtg_solve<H><<<(unsigned)tiles, 256, 0, st>>>(S, b, diag, ck, out);
+    const bool part = S.h != 0;
+    const int rows = part ? S.L + 2 * S.ext : S.n;
+    const int64_t tiles = (int64_t)((S.n + kGTW - 1) / kGTW) * ((rows + kGTH - 1) / kGTH);
+    if (part) k_gtg_solve<H, true><<<(unsigned)tiles, 256, 0, st>>>(S, b, diag, ck, out);
+    else k_gtg_solve<H, false><<<(unsigned)tiles, 256, 0, st>>>(S, b, diag, ck, out);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
-// k_gtg_solve reads a cell's E and S entries as its neighbours' W and N: bit for bit when minv == -inv.
-bool gtg_symmetric(const mpbp_schur_plan* p) {
-    PGDev P;
-    return make_pgstencil(&p->f_prm, p->f_cell, nullptr, &P) == MPBP_OK && P.minv == -P.inv;
-}
 // The tile's staged cells must wrap onto the grid at most once each way (P.wrap), so n >= a tile plus its halos.
-bool gtg_fused_ok(const mpbp_schur_plan* p) {
+// part: under a row partition (the CA schedule's solves), else one GPU.
+bool gtg_fused_ok(const mpbp_schur_plan* p, bool part = false) {
     const mpbp_inner_solver& in = p->inner_P;
-    return g_gtg_fused && p->pg_stencil && !p->halo && in.kind == MPBP_INNER_CHEBYSHEV && in.sweeps >= 2 &&
-           in.sweeps <= 6 && in.lmax > in.lmin && in.lmin >= 0.0 && p->f_prm.n >= kGTW + kGTH + 2 * (in.sweeps - 1) &&
-           gtg_symmetric(p);
+    return g_gtg_fused && p->pg_stencil && (p->halo != nullptr) == part && in.kind == MPBP_INNER_CHEBYSHEV &&
+           in.sweeps >= 2 && in.sweeps <= 6 && in.lmax > in.lmin && in.lmin >= 0.0 &&
+           p->f_prm.n >= kGTW + kGTH + 2 * (in.sweeps - 1);
 }
-int gtg_solve_fused(const mpbp_schur_plan* p, const double* b, double* out, hipStream_t st) {
+// part: the CA schedule's owned + ext ghost rows (b and diag in the pressure ghost layout), else one GPU.
+int gtg_solve_fused(const mpbp_schur_plan* p, const double* b, double* out, hipStream_t st,
+                    const mpbp_row_part* part = nullptr, const double* diag = nullptr) {
     PGDev P;
-    const int rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &P);
+    const int rc = make_pgstencil(&p->f_prm, p->f_cell, part, &P);
     if (rc) return rc;
     const int K = p->inner_P.sweeps;
+    if (part && (P.which != 3 || P.h < P.ext + K - 1 || P.oh < P.ext || !diag))
+        return set_error(MPBP_ERR_ARG, "gtg_solve_fused: owned + ext rows need b ext + K - 1 deep and the ext diagonal");
+    if (!part) diag = p->diag_P;
     ChebK ck{};
     double c1[64] = {}, c2[64] = {};
     cheb_coeffs(p->inner_P.lmin, p->inner_P.lmax, K, c1, c2);
@@ -5319,11 +5483,11 @@ int gtg_solve_fused(const mpbp_schur_plan* p, const double* b, double* out, hipS
     }
     const GtGStencilDev S{P};
     switch (K - 1) {
-    case 1: return launch_gtg_solve_t<1>(S, b, p->diag_P, ck, out, st);
-    case 2: return launch_gtg_solve_t<2>(S, b, p->diag_P, ck, out, st);
-    case 3: return launch_gtg_solve_t<3>(S, b, p->diag_P, ck, out, st);
-    case 4: return launch_gtg_solve_t<4>(S, b, p->diag_P, ck, out, st);
-    case 5: return launch_gtg_solve_t<5>(S, b, p->diag_P, ck, out, st);
+    case 1: return launch_gtg_solve_t<1>(S, b, diag, ck, out, st);
+    case 2: return launch_gtg_solve_t<2>(S, b, diag, ck, out, st);
+    case 3: return launch_gtg_solve_t<3>(S, b, diag, ck, out, st);
+    case 4: return launch_gtg_solve_t<4>(S, b, diag, ck, out, st);
+    case 5: return launch_gtg_solve_t<5>(S, b, diag, ck, out, st);
     default: return set_error(MPBP_ERR_ARG, "gtg_solve_fused: 2..6 sweeps");
     }
 }
@@ -5548,6 +5712,20 @@ int ca_inner_solve(const Ctx& c, int32_t sop, const double* b, const double* dia
         MPBP_HIP(hipGetLastError());
         return MPBP_OK;
     }
+    // Gt_G: the whole Chebyshev solve as one tiled launch over the owned + d_out ghost rows (bit-identical)
+    if (cheb && sop == SOP_GTG && !sub && gtg_fused_ok(p, true)) {
+        const mpbp_row_part q = stencil_part(ext_op(p, SOP_GTG, d_out));
+        if (q.halo >= d_out + K - 1) return gtg_solve_fused(p, b, dst, c.st, &q, diag_ext);
+    }
+    // tolerance-mode F: the whole solve as one tiled launch over the owned + d_out ghost rows
+    if (cheb && sop == SOP_F && f_pair_ok(p) && g_f_solve && fsolve_ok(K, p->f_prm.n)) {
+        const mpbp_row_part q = stencil_part(ext_op(p, SOP_F, d_out));
+        FStencilDev P;
+        int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, &P);
+        if (rc) return rc;
+        if (P.h >= d_out + K - 1)
+            return profiled(p, profile, c.st, [&] { return launch_fsolve(P, K, c1, c2, b, sub, dst, c.st); });
+    }
     double* cur = K == 2 ? dst : pong;
     int rc = op_first_sweep(ext_op(p, sop, d_out + K - 2), cheb, b, diag_ext, c2[0], c1[1], c2[1], dir,
                             K == 2 ? sub : nullptr, cur, c.st, K == 2 ? 0 : 1);
@@ -5597,6 +5775,11 @@ int ca_f_solve_gx(const Ctx& c, const double* xp, const mpbp_inner_solver& in, d
         return make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, P);
     };
     FStencilDev P;
+    if (f_pair_ok(p) && g_f_solve && fsolve_ok(K, p->f_prm.n) && bs.h >= K) {   // the whole solve as one launch
+        if ((rc = fpol(0, &P))) return rc;
+        if (P.h >= K - 1)
+            return profiled(p, profile, c.st, [&] { return launch_fsolve(P, K, c1, c2, nullptr, sub, dst, c.st, bs); });
+    }
     if ((rc = fpol(K - 2, &P))) return rc;
     double* cur = K == 2 ? dst : pong;
     rc = with_f_policy(P, p->f_numerics == MPBP_NUMERICS_FAST, [&](const auto& Q) {

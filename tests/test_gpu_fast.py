@@ -232,7 +232,7 @@ def test_fused_pair_equals_two_sweeps(n, kf, kp):
     assert torch.equal(nofuse.apply(v), got)   # G x_p recomputed == G launched + W streamed, with the pair
 
 
-@pytest.mark.parametrize("n", [64, 256])
+@pytest.mark.parametrize("n", [64, 72, 100, 128, 256])
 def test_matrix_free_galerkin_level1(n):
     """Fast F hierarchies apply level 1 as R_0 (F (P_0 x)) (MgGal) instead of streaming the stored Galerkin product:
     the same operator, so the multigrid apply stays within 1e-10 of the stored-level-1 apply (and of the exact one)."""
@@ -251,8 +251,9 @@ def test_matrix_free_galerkin_level1(n):
         check(lib().mpbp_set_mg_galerkin_mf(1))
         got = fast.apply(v).clone()
     finally:
-        check(lib().mpbp_set_mg_galerkin_mf(1))
+        check(lib().mpbp_set_mg_galerkin_mf(2))
     assert 0.0 < rel_inf(got.cpu().numpy(), stored.cpu().numpy()) <= 1e-10
+    assert torch.equal(fast.apply(v), got)   # one k_gal1 launch (the default) == the three launches, bit for bit
     exact = mp.ApproxSchurPreconditioner(F, D, G, fast.GtG, fast.GtFG, **kw)
     assert rel_inf(got.cpu().numpy(), exact.apply(v).cpu().numpy()) <= 1e-10
     out = torch.empty_like(v)

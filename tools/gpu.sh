@@ -14,6 +14,7 @@
 #   selfhalo     bench.py --self-halo (partitioned apply over the RCCL self-exchange)
 #   probe        tools/capture_probe.py 256 1024 (hipGraph capture of the partitioned apply); probe:N1,N2 sizes
 #   prof         rocprofv3 --kernel-trace --stats of bench.py
+#   profmg       the same with the headline apply's inner solves one multigrid V-cycle each (mg:1 / mg:1)
 #   pmc          FETCH_SIZE / WRITE_SIZE passes: the apply's F sweeps and the A SpMV
 #   sq           SQ counter passes over the F sweep (tools/pmc_sweep.py) and the CSR SpMV (tools/spmv_ab.py)
 #   sqapply      SQ counter passes over bench.py's eager apply (every kernel of the apply; tools/pmc_table.py)
@@ -62,6 +63,10 @@ step() {
     prof) prof prof 300 --kernel-trace --stats --output-format csv -d "$ROOTD/$OUT/prof" -o run -- \
             python "$ROOTD/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-solve $BENCH_ARGS &&
           python tools/prof_summary.py "$OUT/prof/run_kernel_trace.csv" > "$OUT/prof_summary.md" 2>&1 ;;
+    profmg) prof prof_mg 300 --kernel-trace --stats --output-format csv -d "$ROOTD/$OUT/prof_mg" -o run -- \
+              python "$ROOTD/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-solve --no-mg --no-spmv \
+              --inner-f mg:1 --inner-p mg:1 &&
+            python tools/prof_summary.py "$OUT/prof_mg/run_kernel_trace.csv" > "$OUT/prof_mg_summary.md" 2>&1 ;;
     pmc) for C in FETCH_SIZE WRITE_SIZE; do
            prof "pmc_apply_$C" 150 --pmc $C --output-format csv -d "$ROOTD/$OUT/pmc_apply_$C" -o pmc -- \
              python "$ROOTD/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-spmv --no-graph --no-solve || return 1

@@ -38,13 +38,19 @@ def main():
     # launches bench.py's `roofline` times; tools/gpu.sh's pmc step writes them under pmc_apply_<counter>
     kernels = {"stencil": (("k_march<(anonymous namespace)::FStencilDev", "(anonymous namespace)::XPlain, ",
                             "EpiChebT<true, false, ", "BNone>"), args.n * args.n // 4),   # 4 rows x 256 cols / WG
-               "sell": ("k_sell_rows<(anonymous namespace)::EpiCheb>", grid)}   # grid 4N: F rows, not Gt_G
+               "sell": ("k_sell_rows<(anonymous namespace)::EpiCheb>", grid),   # grid 4N: F rows, not Gt_G
+               # round 4: the whole-solve F launch (the first solve: b streamed, no sub; the second: G x_p, sub), the
+               # fused Gt_G solve and Gt_F_G on the diamond -- every kernel of the default apply but D
+               "fsolve": (("k_fsolve<3, false, (anonymous namespace)::BNone>",), None),
+               "fsolve_gx": (("k_fsolve<3, true, (anonymous namespace)::GxBT<false> >",), None),
+               "gtg_solve": (("k_gtg_solve<3>",), None),
+               "q13": (("k_q13<(anonymous namespace)::EpiStore>",), None)}
     out = {"n": args.n, "source": args.run_dir}
     for lay, (kname, kgrid) in kernels.items():
         res = {}
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
             f = os.path.join(args.run_dir, f"pmc_{lay}_{c}", "pmc_counter_collection.csv")
-            if lay == "stencil" and not os.path.exists(f):
+            if lay not in ("sell",) and not os.path.exists(f):
                 f = os.path.join(args.run_dir, f"pmc_apply_{c}", "pmc_counter_collection.csv")
             if os.path.exists(f):
                 res[c] = mean_counter(f, c, kname, kgrid)
