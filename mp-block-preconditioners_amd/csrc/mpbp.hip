@@ -25,8 +25,8 @@ int g_march_rows = 0;
 int g_csr_table = 1;      // CSR SpMV waves start from the row blocks' wave table when it has one (0: from row_ptr)
 int g_mg_mf_transfer = 1;   // whole-grid multigrid transfers matrix-free (0: their CSR / SELL / grouped forms)
 int g_init_diag = 1;      // fused first F sweep: 1 rebuilds the staged diagonal from thn, 0 streams diag
-int g_mg_gal = 2;          // tolerance-mode F hierarchies: level 1 as R_0 (F (P_0 x)): 2 one k_gal1 launch, 1 three
-                           // launches (MgGal), 0 its stored Galerkin matrix
+int g_mg_gal = 1;          // tolerance-mode F hierarchies: level 1 as R_0 (F (P_0 x)): 1 three launches (MgGal), 2 one
+                           // k_gal1 launch (measured slower), 0 its stored Galerkin matrix
 int g_f_direct = 0;        // tolerance-mode F sweeps on the direct kernel (one thread per cell, no LDS) instead of marching
 int g_gtg_fused = 1;       // one-GPU Chebyshev Gt_G solves of 2..6 sweeps as one k_gtg_solve launch (0: per sweep)
 int g_f_solve = 1;         // one-GPU tolerance-mode F solves of 3 or 4 Chebyshev updates as one launch (k_fsolve)

@@ -136,3 +136,31 @@ def test_ftile_multigrid_smoothing_equals_marching(n):
     finally:
         check(lib().mpbp_set_f_tile(1))
     assert torch.equal(got, ref), float((got - ref).abs().max())
+
+
+@pytest.mark.parametrize("n", [5, 17, 64, 128])
+@pytest.mark.parametrize("kf", [3, 5])
+def test_fdirect_equals_marching(n, kf):
+    """mpbp_set_f_direct(1): the per-sweep tolerance-mode F launches on the direct kernel (one thread per cell) perform
+    the marching kernels' rows4 operations -- the apply is bit-identical (whole-solve and tile launches off)."""
+    import mp_block_preconditioners_amd as mp
+    from mp_block_preconditioners_amd._lib import check, lib
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("chebyshev", kf),
+                                      inner_P=mp.InnerSolver("chebyshev", 4), numerics="fast")
+    v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda",
+                    generator=torch.Generator(device="cuda").manual_seed(n * 10 + kf + 3))
+    try:
+        check(lib().mpbp_set_f_solve(0))
+        check(lib().mpbp_set_f_tile(0))
+        check(lib().mpbp_set_f_pair(0))
+        ref = pc.apply(v).clone()
+        check(lib().mpbp_set_f_direct(1))
+        got = pc.apply(v)
+    finally:
+        check(lib().mpbp_set_f_direct(0))
+        check(lib().mpbp_set_f_pair(1))
+        check(lib().mpbp_set_f_tile(1))
+        check(lib().mpbp_set_f_solve(1))
+    assert torch.equal(got, ref), float((got - ref).abs().max())
