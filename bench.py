@@ -358,7 +358,8 @@ def main():
     # (csrc: the tiled F kernels need n >= 76 on one GPU; below that, or with --f-tile 0, the marching ones run)
     f_tile = (args.f_tile is None or args.f_tile != 0) and n >= 76 and not partitioned
     # (csrc fsolve_ok: 3 or 4 updates, n >= 72; else the k_ftile / marching launches)
-    f_solve = (args.f_solve is None or args.f_solve != 0) and not partitioned and \
+    # (one GPU, or a row partition on the communication-avoiding schedule: its solves run k_fsolve over owned + ghost rows)
+    f_solve = (args.f_solve is None or args.f_solve != 0) and (not partitioned or bool(getattr(pc, "ca", False))) and \
         ((sf == 4 and n >= 72) or (sf == 3 and n >= 70))
     per_apply, kname = sweep_bytes(pc, args.layout, kf, sf, fused_init, f_tile, f_solve)
     sbytes, avg_sweep_s, n_timed = roofline_of(per_apply, sweep_ms, 1)

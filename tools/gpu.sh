@@ -17,6 +17,7 @@
 #   profmg       the same with the headline apply's inner solves one multigrid V-cycle each (mg:1 / mg:1)
 #   pmc          FETCH_SIZE / WRITE_SIZE passes: the apply's F sweeps and the A SpMV
 #   sq           SQ counter passes over the F sweep (tools/pmc_sweep.py) and the CSR SpMV (tools/spmv_ab.py)
+#   spmvattr     FETCH_SIZE / WRITE_SIZE of the A SpMV against the same matrix with its x gathers in a 32 KB window
 #   sqapply      SQ counter passes over bench.py's eager apply (every kernel of the apply; tools/pmc_table.py)
 #   py:FILE      python FILE (any experiment script), 300 s
 #   ab:V1,V2,..  A/B of experiment builds (tools/build_variants.py): bench.py per variant (V or V@ARGS, '+' for
@@ -73,6 +74,11 @@ step() {
            prof "pmc_spmv_$C" 120 --pmc $C --output-format csv -d "$ROOTD/$OUT/pmc_spmv_$C" -o pmc -- \
              python "$ROOTD/tools/spmv_ab.py" --reps 10 || return 1
          done ;;
+    spmvattr) for C in FETCH_SIZE WRITE_SIZE; do
+           prof "spmvattr_$C" 150 --pmc $C --output-format csv -d "$ROOTD/$OUT/spmvattr/pmc_$C" -o pmc -- \
+             python "$ROOTD/tools/spmv_attr.py" --reps 10 || return 1
+         done && python tools/spmv_attr.py --reduce "$OUT/spmvattr" > "$OUT/spmv_attr.json" 2>&1 &&
+         timeout -k 10 120 python tools/spmv_attr.py --reps 50 >> "$OUT/spmv_attr.json" 2>&1 ;;
     sq) for W in "pmc_sweep.py --layout stencil" "spmv_ab.py --reps 10"; do
           local tag=${W%%.py*}
           prof "sq1_$tag" 120 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
