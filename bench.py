@@ -148,6 +148,10 @@ def main():
     ap.add_argument("--f-solve", type=int, default=None,
                     help="fast numerics: 1 (default) runs each F solve of 3 or 4 updates as one k_fsolve launch, "
                          "0 as k_ftile launches")
+    ap.add_argument("--q13-sym", type=int, default=None,
+                    help="fast numerics: 1 (default) reads Gt_F_G's diamond upper half only (symmetric product); 0: all 13")
+    ap.add_argument("--gtg-drhs", type=int, default=None,
+                    help="1 (default): the first fused Gt_G solve builds rhs = D Finv_v + v_p itself; 0: a D launch")
     ap.add_argument("--gtg-fused", type=int, default=None,
                     help="1 (default): each Chebyshev Gt_G solve as one tiled launch; 0: one launch per sweep")
     ap.add_argument("--mg-galerkin-mf", type=int, default=None,
@@ -232,6 +236,10 @@ def main():
         _check(_lib().mpbp_set_gtg_fused(args.gtg_fused))
     if args.f_solve is not None:
         _check(_lib().mpbp_set_f_solve(args.f_solve))
+    if args.gtg_drhs is not None:
+        _check(_lib().mpbp_set_gtg_drhs(args.gtg_drhs))
+    if args.q13_sym is not None:
+        _check(_lib().mpbp_set_q13_sym(args.q13_sym))
     if args.mg_galerkin_mf is not None:
         _check(_lib().mpbp_set_mg_galerkin_mf(args.mg_galerkin_mf))
     if args.stored_transfers:

@@ -28,7 +28,10 @@ int g_init_diag = 1;      // fused first F sweep: 1 rebuilds the staged diagonal
 int g_mg_gal = 1;          // tolerance-mode F hierarchies: level 1 as R_0 (F (P_0 x)): 1 three launches (MgGal), 2 one
                            // k_gal1 launch (measured slower), 0 its stored Galerkin matrix
 int g_f_direct = 0;        // tolerance-mode F sweeps on the direct kernel (one thread per cell, no LDS) instead of marching
-int g_gtg_fused = 1;       // one-GPU Chebyshev Gt_G solves of 2..6 sweeps as one k_gtg_solve launch (0: per sweep)
+int g_gtg_tpb = 512;        // k_gtg_solve workgroup: 512 lanes (one tile cell + one ring cell each) or 256
+int g_gtg_fused = 1;
+int g_gtg_drhs = 1;
+int g_q13_sym = 1;          // tolerance mode: Gt_F_G x read from the diamond's upper half (symmetric product)         // the first fused Gt_G solve builds rhs = D Finv_v + v_p itself (no D launch)       // one-GPU Chebyshev Gt_G solves of 2..6 sweeps as one k_gtg_solve launch (0: per sweep)
 int g_f_solve = 1;         // one-GPU tolerance-mode F solves of 3 or 4 Chebyshev updates as one launch (k_fsolve)
 int g_f_tile = 1;          // one-GPU tolerance-mode F: x0 + sweep 1, and the last pair, on 2D tiles (k_ftile)
 int g_f_pair = 1;         // tolerance-mode F solves: the last two Chebyshev sweeps as one k_march2 launch (0: two)
@@ -1828,10 +1831,13 @@ struct FStencilFast : FStencilDev {
             const double vC = xa.X(fv, gr, gc), vN = xa.X(fv, gr - 1, gc), vS = xa.X(fv, gr + 1, gc);
             const double vW = xa.X(fv, gr, gc - 1), vE = xa.X(fv, gr, gc + 1), vSW = xa.X(fv, gr + 1, gc - 1);
             const double uo = xa.X(fu ^ 2, gr, gc), vo = xa.X(fv ^ 2, gr, gc);
+            // the node (r, c) and centre (r, c) terms are shared by the u and v rows: the v row's are -tn (the same
+            // differences negated: exact) and tc (the same sum, operands swapped: exact)
+            const double tn = (uN - uC) + (vC - vW), tc = (uE - uC) + (vS - vC);
             // u row: v1 = vW, v2 = vC, v3 = vSW, v4 = vS
-            double br = KC * ((uN - uC) + (vC - vW));
+            double br = KC * tn;
             br = __builtin_fma(A1, (uW - uC) + (vW - vSW), br);
-            br = __builtin_fma(A2, (uE - uC) + (vS - vC), br);
+            br = __builtin_fma(A2, tc, br);
             br = __builtin_fma(KS, (uS - uC) + (vSW - vS), br);
             const double wu = c * ph(cl.face[0]);
             acc[fu] = __builtin_fma(a, br, __builtin_fma(wu, uC, k.xu * (uC - uo)));
@@ -1839,9 +1845,9 @@ struct FStencilFast : FStencilDev {
                 rd[fu] = rcp_nr(__builtin_fma(-a, (A1 + A2) + (KC + KS), wu + k.xu));
             // v row: u1 = uN, u2 = uNE, u3 = uC, u4 = uE
             double bv = B1 * ((vN - vC) + (uN - uNE));
-            bv = __builtin_fma(KC, (vW - vC) + (uC - uN), bv);
+            bv = __builtin_fma(KC, -tn, bv);
             bv = __builtin_fma(KE, (vE - vC) + (uNE - uE), bv);
-            bv = __builtin_fma(A2, (vS - vC) + (uE - uC), bv);
+            bv = __builtin_fma(A2, tc, bv);
             const double wv = c * ph(cl.face[1]);
             acc[fv] = __builtin_fma(a, bv, __builtin_fma(wv, vC, k.xv * (vC - vo)));
             if constexpr (RD)
@@ -3380,12 +3386,26 @@ struct TTile {   // thn of the staged tile; (r, c) in the tile's virtual grid co
 // PART: the tiles cover a row partition's owned rows and P.ext ghost rows each side (the CA schedule); b and diag in
 // its ghost layout (depth P.h >= P.ext + H; deeper rows, read only for cells no output depends on, clamped), out in
 // the output layout (depth P.oh).
-template <int H, bool PART>
-__global__ void __launch_bounds__(256) k_gtg_solve(GtGStencilDev P, const double* __restrict__ b,
-                                                   const double* __restrict__ diag, ChebK ck, double* __restrict__ out) {
+// TPB = 512: one tile cell and at most one ring cell per lane (rings 1 .. H - 1 numbered across the workgroup), so a
+// level's critical path is half as long and the smaller register state lets more waves share the CU.
+// DB (one GPU): the right-hand side is rhs = D Y + v_p (solve.py:259), built at every staged cell with
+// DStencilDev::row's operations and EpiAdd's sum from thn staged one cell wider and Y (the four velocity fields) from
+// memory: the D launch, and rhs's write and re-read, disappear.
+struct GtgD {
+    const double* Y;    // Finv_v: u_n, v_n, u_s, v_s
+    const double* vp;   // v's pressure part
+};
+template <int H, bool PART, int TPB, bool DB>
+__global__ void __launch_bounds__(TPB) k_gtg_solve(GtGStencilDev P, const double* __restrict__ b,
+                                                   const double* __restrict__ diag, ChebK ck, double* __restrict__ out,
+                                                   GtgD dv) {
     using G = GtgTile<H>;
-    constexpr int NS = H + 1;   // owned cells with sweeps: the two tile cells and rings 1 .. H - 1
-    __shared__ double ts[G::N], bs[G::N], xa[G::N], xb[G::N];
+    constexpr int TW = DB ? G::RW + 2 : G::RW, TN = DB ? TW * (G::RH + 2) : G::N;   // staged thn
+    constexpr int NM = TPB == 256 ? 2 : 1;           // tile cells per lane
+    constexpr int NR = TPB == 256 ? H - 1 : 1;       // ring slots per lane (rings 1 .. H - 1)
+    constexpr int NS = NM + NR;
+    static_assert(TPB == 256 || 140 * (H - 1) + 4 * H * (H - 1) <= 512, "512 lanes own at most one ring cell each");
+    __shared__ double ts[TN], bs[G::N], xa[G::N], xb[G::N];
     const int n = P.n;
     const int tx = (n + kGTW - 1) / kGTW;
     const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -3394,12 +3414,64 @@ __global__ void __launch_bounds__(256) k_gtg_solve(GtGStencilDev P, const double
     const int rb = r0 - H, cb = c0 - H;   // virtual coordinates of staged cell 0
     const int tid = threadIdx.x;
     // level 0 over the whole staged region: thn, b, x0 = c2_0 (b / diag); every load issued before the first LDS store
-    {
-        constexpr int IT = (G::N + 255) / 256;
-        double bv[IT], tv[IT], dv[IT];
+    if constexpr (DB) {
+        const int nn = n * n;
+        {   // thn one cell wider than the staged region
+            constexpr int IT = (TN + TPB - 1) / TPB;
+            double tv[IT];
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                const int i = tid + it * TPB;
+                if (i < TN) {
+                    const int rr = i / TW, cc = i - rr * TW;
+                    tv[it] = P.cell[P.wrap(rb - 1 + rr) * n + P.wrap(cb - 1 + cc)];
+                }
+            }
+#pragma unroll
+            for (int it = 0; it < IT; ++it)
+                if (tid + it * TPB < TN) ts[tid + it * TPB] = tv[it];
+        }
+        __syncthreads();
+        const TTileT<TW> tD{ts, rb - 1, cb - 1};
+        for (int i = tid; i < G::N; i += TPB) {
+            const int rr = i / G::RW, cc = i - rr * G::RW;
+            const int vr = rb + rr, vc = cb + cc, gr = P.wrap(vr), gc = P.wrap(vc);
+            const int ge = gc == n - 1 ? 0 : gc + 1, gs = gr == n - 1 ? 0 : gr + 1;
+            const int32_t k = gr * n + gc;
+            double yv[8];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                yv[4 * q + 0] = dv.Y[2 * q * nn + gr * n + ge];         // u at the east face
+                yv[4 * q + 1] = dv.Y[2 * q * nn + k];                   // u at the cell's west face
+                yv[4 * q + 2] = dv.Y[(2 * q + 1) * nn + k];             // v at its north face
+                yv[4 * q + 3] = dv.Y[(2 * q + 1) * nn + gs * n + gc];   // v at the south face
+            }
+            const double vpk = dv.vp[k], dgk = diag[k];
+            const bool lastc = gc == n - 1, lastr = gr == n - 1;   // the wrapped neighbour sorts first (DStencilDev)
+            double acc = 0.0;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const double t0 = tD.T(q, vr, vc), tE = tD.T(q, vr, vc + 1), tWv = tD.T(q, vr, vc - 1);
+                const double tN = tD.T(q, vr - 1, vc), tS = tD.T(q, vr + 1, vc);
+                const double uE = (P.inv * (0.5 * (t0 + tE))) * yv[4 * q + 0];
+                const double uC = (P.minv * (0.5 * (t0 + tWv))) * yv[4 * q + 1];
+                const double vC = (P.inv * (0.5 * (t0 + tN))) * yv[4 * q + 2];
+                const double vS = (P.minv * (0.5 * (t0 + tS))) * yv[4 * q + 3];
+                acc += lastc ? uE : uC;
+                acc += lastc ? uC : uE;
+                acc += lastr ? vS : vC;
+                acc += lastr ? vC : vS;
+            }
+            const double bvv = acc + vpk;   // EpiAdd
+            bs[i] = bvv;
+            xa[i] = ck.c2[0] * (bvv / dgk);
+        }
+    } else {
+        constexpr int IT = (G::N + TPB - 1) / TPB;
+        double bv[IT], tv[IT], dv_[IT];
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            const int i = tid + it * 256;
+            const int i = tid + it * TPB;
             if (i < G::N) {
                 const int rr = i / G::RW, cc = i - rr * G::RW;
                 const int gr = P.wrap(rb + rr), gc = P.wrap(cb + cc);
@@ -3411,32 +3483,48 @@ __global__ void __launch_bounds__(256) k_gtg_solve(GtGStencilDev P, const double
                 }
                 bv[it] = b[kb];
                 tv[it] = P.cell[gr * n + gc];
-                dv[it] = diag[kb];
+                dv_[it] = diag[kb];
             }
         }
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            const int i = tid + it * 256;
+            const int i = tid + it * TPB;
             if (i < G::N) {
                 ts[i] = tv[it];
                 bs[i] = bv[it];
-                xa[i] = ck.c2[0] * (bv[it] / dv[it]);
+                xa[i] = ck.c2[0] * (bv[it] / dv_[it]);
             }
         }
     }
     __syncthreads();
     // the owned cells (slot 0, 1: the tile's; slot 1 + r: ring r), their entries, b and d0 = x0
-    const TTile<H> ta{ts, rb, cb};
+    const TTileT<TW> ta{ts, DB ? rb - 1 : rb, DB ? cb - 1 : cb};
     const int lr = tid >> 6, lc = tid & 63;
-    int cr[NS], cc[NS], si[NS];
+    int cr[NS], cc[NS], si[NS], rr[NS];
     bool own[NS], edge[NS];
     double e[NS][5], bo[NS], d[NS];
-    cr[0] = r0 + lr; cc[0] = c0 + lc; own[0] = true;
-    cr[1] = r0 + 4 + lr; cc[1] = c0 + lc; own[1] = true;
 #pragma unroll
-    for (int r = 1; r < H; ++r) {
-        own[1 + r] = tid < 140 + 8 * r;
-        fs_ring_cell(r, own[1 + r] ? tid : 0, r0, c0, cr[1 + r], cc[1 + r]);
+    for (int m = 0; m < NM; ++m) {
+        cr[m] = r0 + lr + 4 * m; cc[m] = c0 + lc; own[m] = true; rr[m] = 0;
+    }
+    if constexpr (TPB == 256) {
+#pragma unroll
+        for (int r = 1; r < H; ++r) {
+            own[NM + r - 1] = tid < 140 + 8 * r;
+            rr[NM + r - 1] = r;
+            fs_ring_cell(r, own[NM + r - 1] ? tid : 0, r0, c0, cr[NM + r - 1], cc[NM + r - 1]);
+        }
+    } else if constexpr (NR > 0) {
+        int r = 0, j = tid;   // rings 1 .. H - 1 numbered ring 1 first: lane t owns cell t of that sequence
+#pragma unroll
+        for (int q = 1; q < H; ++q)
+            if (r == 0) {
+                if (j < 140 + 8 * q) r = q;
+                else j -= 140 + 8 * q;
+            }
+        own[NM] = r != 0;
+        rr[NM] = r;
+        fs_ring_cell(r ? r : 1, r ? j : 0, r0, c0, cr[NM], cc[NM]);
     }
 #pragma unroll
     for (int sl = 0; sl < NS; ++sl) {
@@ -3458,7 +3546,8 @@ __global__ void __launch_bounds__(256) k_gtg_solve(GtGStencilDev P, const double
         const double c1 = ck.c1[l], c2 = ck.c2[l];
 #pragma unroll
         for (int sl = 0; sl < NS; ++sl) {
-            if (sl >= 2 && (sl - 1 > H - l || !own[sl])) continue;   // ring r = sl - 1 lives through level H - r
+            if (TPB == 256 && sl >= NM && sl - NM + 1 > H - l) continue;   // (compile time) ring sl - NM + 1 is done
+            if (sl >= NM && (!own[sl] || rr[sl] > H - l)) continue;        // ring rr lives through level H - rr
             const int vr = cr[sl], vc = cc[sl];
             if (l == H && (vr >= hi || vc >= n)) continue;            // a tile past the last row / column
             const int i = si[sl];
@@ -3805,8 +3894,19 @@ int mpbp_set_f_direct(int32_t on) {
     return MPBP_OK;
 }
 int mpbp_set_gtg_fused(int32_t on) {
-    if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "gtg_fused must be 0 or 1");
-    g_gtg_fused = on;
+    if (on != 0 && on != 1 && on != 256 && on != 512) return set_error(MPBP_ERR_ARG, "gtg_fused must be 0, 1, 256 or 512");
+    g_gtg_fused = on != 0;
+    if (on == 256 || on == 512) g_gtg_tpb = on;
+    return MPBP_OK;
+}
+int mpbp_set_q13_sym(int32_t on) {
+    if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "q13_sym must be 0 or 1");
+    g_q13_sym = on;
+    return MPBP_OK;
+}
+int mpbp_set_gtg_drhs(int32_t on) {
+    if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "gtg_drhs must be 0 or 1");
+    g_gtg_drhs = on;
     return MPBP_OK;
 }
 int mpbp_set_f_tile(int32_t on) {
@@ -4792,7 +4892,12 @@ __global__ void k_q13_fill(Csr Q, int32_t n, double* vals, int* bad) {
     if (!ok) atomicAdd(bad, 1);
 }
 
-template <class Epi>
+// SYM (tolerance mode): Gt_F_G = G^T F G is symmetric, so its values are read from the upper half of the diamond
+// alone -- slots 6 .. 12 ((0, 0) .. (2, 0)) at the cell, and slot 12 - s at the cell's neighbour (dr_s, dc_s) for the
+// lower slots s = 0 .. 5, Q(c, c + o) = Q(c + o, c) -- 56 instead of 104 B of values per row (the mirrored reads are the
+// neighbouring rows' own, cached).  The stored product is symmetric to rounding (|Q - Q^T| ~ 1.5e-16 |Q|): within the
+// tolerance mode's bar, not bit-exact.
+template <class Epi, bool SYM = false>
 __global__ void __launch_bounds__(kBlock) k_q13(int32_t n, const double* __restrict__ vals,
                                                 const double* __restrict__ x, Epi epi) {
     const int32_t N = n * n;
@@ -4801,9 +4906,21 @@ __global__ void __launch_bounds__(kBlock) k_q13(int32_t n, const double* __restr
     const typename Epi::P pe = epi.pre(cell);
     const int gr = cell / n, gc = cell - (cell / n) * n;
     double v[kQSlots];
-#pragma unroll
-    for (int s = 0; s < kQSlots; ++s) v[s] = __builtin_nontemporal_load(vals + (int64_t)s * N + cell);
     const bool wraps = gr < 2 || gr >= n - 2 || gc < 2 || gc >= n - 2;
+    if constexpr (SYM) {
+#pragma unroll
+        for (int s = 6; s < kQSlots; ++s) v[s] = vals[(int64_t)s * N + cell];
+#pragma unroll
+        for (int s = 0; s < 6; ++s) {
+            int rr = gr + q13_dr(s), cc = gc + q13_dc(s);
+            rr = rr < 0 ? rr + n : rr >= n ? rr - n : rr;
+            cc = cc < 0 ? cc + n : cc >= n ? cc - n : cc;
+            v[s] = vals[(int64_t)(12 - s) * N + rr * n + cc];
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < kQSlots; ++s) v[s] = __builtin_nontemporal_load(vals + (int64_t)s * N + cell);
+    }
     double acc = 0.0;
     if (!__any(wraps)) {
 #pragma unroll
@@ -4839,8 +4956,9 @@ __global__ void __launch_bounds__(kBlock) k_q13(int32_t n, const double* __restr
 }
 
 template <class Epi>
-int launch_q13(int32_t n, const double* vals, const double* x, Epi epi, hipStream_t st) {
-    k_q13<<<grid_for((int64_t)n * n), kBlock, 0, st>>>(n, vals, x, epi);
+int launch_q13(int32_t n, const double* vals, const double* x, Epi epi, hipStream_t st, bool sym = false) {
+    if (sym) k_q13<Epi, true><<<grid_for((int64_t)n * n), kBlock, 0, st>>>(n, vals, x, epi);
+    else k_q13<Epi, false><<<grid_for((int64_t)n * n), kBlock, 0, st>>>(n, vals, x, epi);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
@@ -5447,12 +5565,27 @@ int d_rhs_x0(const mpbp_schur_plan* p, const double* Y, const double* v_p, doubl
 // x = Gt_G^-1 b by the plan's Chebyshev inner solve in one k_gtg_solve launch (one GPU, matrix-free Gt_G, 2..6 sweeps).
 template <int H>
 int launch_gtg_solve_t(const GtGStencilDev& S, const double* b, const double* diag, const ChebK& ck, double* out,
-                       hipStream_t st) {
+                       hipStream_t st, GtgD dv = GtgD{}) {
     const bool part = S.h != 0;
     const int rows = part ? S.L + 2 * S.ext : S.n;
     const int64_t tiles = (int64_t)((S.n + kGTW - 1) / kGTW) * ((rows + kGTH - 1) / kGTH);
-    if (part) k_gtg_solve<H, true><<<(unsigned)tiles, 256, 0, st>>>(S, b, diag, ck, out);
-    else k_gtg_solve<H, false><<<(unsigned)tiles, 256, 0, st>>>(S, b, diag, ck, out);
+    const bool db = dv.Y != nullptr;
+    if (db && part) return set_error(MPBP_ERR_ARG, "gtg_solve: the fused D right-hand side is one-GPU only");
+    // 512 lanes own rings 1 .. H - 1 one cell each (140 (H - 1) + 4 H (H - 1) <= 512 cells): H <= 4
+    if constexpr (H <= 4) {
+        if (g_gtg_tpb == 512) {
+            if (db) k_gtg_solve<H, false, 512, true><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, ck, out, dv);
+            else if (part) k_gtg_solve<H, true, 512, false><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, ck, out, dv);
+            else k_gtg_solve<H, false, 512, false><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, ck, out, dv);
+            MPBP_HIP(hipGetLastError());
+            return MPBP_OK;
+        }
+    }
+    {
+        if (db) k_gtg_solve<H, false, 256, true><<<(unsigned)tiles, 256, 0, st>>>(S, b, diag, ck, out, dv);
+        else if (part) k_gtg_solve<H, true, 256, false><<<(unsigned)tiles, 256, 0, st>>>(S, b, diag, ck, out, dv);
+        else k_gtg_solve<H, false, 256, false><<<(unsigned)tiles, 256, 0, st>>>(S, b, diag, ck, out, dv);
+    }
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
@@ -5465,8 +5598,9 @@ bool gtg_fused_ok(const mpbp_schur_plan* p, bool part = false) {
            p->f_prm.n >= kGTW + kGTH + 2 * (in.sweeps - 1);
 }
 // part: the CA schedule's owned + ext ghost rows (b and diag in the pressure ghost layout), else one GPU.
+// dv.Y set (one GPU): b is not read; rhs = D dv.Y + dv.vp is built inside (k_gtg_solve<DB>).
 int gtg_solve_fused(const mpbp_schur_plan* p, const double* b, double* out, hipStream_t st,
-                    const mpbp_row_part* part = nullptr, const double* diag = nullptr) {
+                    const mpbp_row_part* part = nullptr, const double* diag = nullptr, GtgD dv = GtgD{}) {
     PGDev P;
     const int rc = make_pgstencil(&p->f_prm, p->f_cell, part, &P);
     if (rc) return rc;
@@ -5483,11 +5617,11 @@ int gtg_solve_fused(const mpbp_schur_plan* p, const double* b, double* out, hipS
     }
     const GtGStencilDev S{P};
     switch (K - 1) {
-    case 1: return launch_gtg_solve_t<1>(S, b, diag, ck, out, st);
-    case 2: return launch_gtg_solve_t<2>(S, b, diag, ck, out, st);
-    case 3: return launch_gtg_solve_t<3>(S, b, diag, ck, out, st);
-    case 4: return launch_gtg_solve_t<4>(S, b, diag, ck, out, st);
-    case 5: return launch_gtg_solve_t<5>(S, b, diag, ck, out, st);
+    case 1: return launch_gtg_solve_t<1>(S, b, diag, ck, out, st, dv);
+    case 2: return launch_gtg_solve_t<2>(S, b, diag, ck, out, st, dv);
+    case 3: return launch_gtg_solve_t<3>(S, b, diag, ck, out, st, dv);
+    case 4: return launch_gtg_solve_t<4>(S, b, diag, ck, out, st, dv);
+    case 5: return launch_gtg_solve_t<5>(S, b, diag, ck, out, st, dv);
     default: return set_error(MPBP_ERR_ARG, "gtg_solve_fused: 2..6 sweeps");
     }
 }
@@ -5923,6 +6057,11 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
     // 1. Finv_v = F_inv @ v[:F.shape[1]]                                   solve.py:258
     rc = inner_solve(c, MPBP_VEC_VELOCITY, F, p->diag_F, p->inner_F, p->nu, v_u, Y, nullptr, U0, U1, Ud, true);
     if (rc) return rc;
+    // 2.+3. fused: the first Gt_G solve builds rhs = D Finv_v + v_p itself          solve.py:259, 265
+    if (gfuse && g_gtg_drhs && p->pg_stencil && !px0) {
+        rc = gtg_solve_fused(p, nullptr, Pxa, c.st, nullptr, nullptr, GtgD{Y, v_p});
+        if (rc) return rc;
+    } else {
     // 2. rhs_interim = D @ Finv_v + v[F.shape[1]:]                            solve.py:259
     if (px0)
         rc = d_rhs_x0(p, Y, v_p, Prhs, pc2[0], P0, c.st);
@@ -5935,13 +6074,14 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
                : inner_solve(c, MPBP_VEC_PRESSURE, P, p->diag_P, p->inner_P, p->np, Prhs, Pxa, nullptr, P0, P1, Pd, false,
                              px0 ? P0 : nullptr);
     if (rc) return rc;
+    }
     // 4. x_b = Gt_F_G @ x_a                                                solve.py:267
     //    (one GPU: the diamond layout when the plan has it)
     const bool qx0 = px0 && p->q13;
     if (qx0)
         rc = launch_q13(p->q13_n, p->q13, Pxa, EpiStoreX0{Pxb, p->diag_P, pc2[0], P0}, c.st);
-    else if (p->q13 && !p->halo)
-        rc = mpbp_q13_spmv(p->q13_n, p->q13, MPBP_SPMV_STORE, Pxa, nullptr, Pxb, (void*)c.st);
+    else if (p->q13 && !p->halo)   // tolerance mode: the symmetric product's upper half (k_q13<SYM>)
+        rc = launch_q13(p->q13_n, p->q13, Pxa, EpiStore{Pxb}, c.st, g_q13_sym && p->f_numerics == MPBP_NUMERICS_FAST);
     else
         rc = two_phase(c, MPBP_VEC_PRESSURE, Pxa, Q,
                        [&](const OpRef& o) { return op_spmv(o, MPBP_SPMV_STORE, Pxa, nullptr, Pxb, c.st); });

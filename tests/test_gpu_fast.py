@@ -263,3 +263,31 @@ def test_matrix_free_galerkin_level1(n):
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(out, got)
+
+
+@pytest.mark.parametrize("n", [5, 16, 100, 256])
+def test_q13_symmetric_half(n):
+    """Tolerance mode reads Gt_F_G's diamond upper half (mpbp_set_q13_sym, default): the apply stays within 1e-13
+    relative of the 13-slot apply (the stored product is symmetric to ~1.5e-16) and within 1e-12 of the oracle's;
+    the exact mode never takes it."""
+    mp = _mp()
+    from mp_block_preconditioners_amd._lib import check, lib
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    kw = dict(inner_F=mp.InnerSolver("chebyshev", 4), inner_P=mp.InnerSolver("chebyshev", 4))
+    fast = mp.ApproxSchurPreconditioner(F, D, G, numerics="fast", **kw)
+    exact = mp.ApproxSchurPreconditioner(F, D, G, fast.GtG, fast.GtFG, **kw)
+    v = torch.randn(fast.shape[0], dtype=torch.float64, device="cuda",
+                    generator=torch.Generator(device="cuda").manual_seed(n + 11))
+    try:
+        check(lib().mpbp_set_q13_sym(0))
+        full = fast.apply(v).clone()
+        ex0 = exact.apply(v).clone()
+        check(lib().mpbp_set_q13_sym(1))
+        half = fast.apply(v).clone()
+        ex1 = exact.apply(v).clone()
+    finally:
+        check(lib().mpbp_set_q13_sym(1))
+    assert rel_inf(half.cpu().numpy(), full.cpu().numpy()) <= 1e-13
+    assert rel_inf(half.cpu().numpy(), ex0.cpu().numpy()) <= 1e-12
+    assert torch.equal(ex0, ex1)

@@ -164,3 +164,30 @@ def test_fdirect_equals_marching(n, kf):
         check(lib().mpbp_set_f_tile(1))
         check(lib().mpbp_set_f_solve(1))
     assert torch.equal(got, ref), float((got - ref).abs().max())
+
+
+@pytest.mark.parametrize("n", [82, 100, 128, 256])
+@pytest.mark.parametrize("numerics", ["exact", "fast"])
+def test_gtg_solve_builds_rhs_equals_d_launch(n, numerics):
+    """The first fused Gt_G solve building rhs = D Finv_v + v_p per staged cell (DStencilDev::row's operations, EpiAdd's
+    sum) is bit-identical to the D launch writing rhs, in both numerics, with 256- and 512-lane workgroups."""
+    import mp_block_preconditioners_amd as mp
+    from mp_block_preconditioners_amd._lib import check, lib
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("chebyshev", 4),
+                                      inner_P=mp.InnerSolver("chebyshev", 4), numerics=numerics)
+    v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda",
+                    generator=torch.Generator(device="cuda").manual_seed(n + 5))
+    try:
+        check(lib().mpbp_set_gtg_drhs(0))
+        ref = pc.apply(v).clone()
+        check(lib().mpbp_set_gtg_drhs(1))
+        got = pc.apply(v).clone()
+        check(lib().mpbp_set_gtg_fused(256))
+        got256 = pc.apply(v).clone()
+    finally:
+        check(lib().mpbp_set_gtg_drhs(1))
+        check(lib().mpbp_set_gtg_fused(512))
+    assert torch.equal(got, ref), float((got - ref).abs().max())
+    assert torch.equal(got256, ref), float((got256 - ref).abs().max())

@@ -18,7 +18,9 @@
 #   pmc          FETCH_SIZE / WRITE_SIZE passes: the apply's F sweeps and the A SpMV
 #   sq           SQ counter passes over the F sweep (tools/pmc_sweep.py) and the CSR SpMV (tools/spmv_ab.py)
 #   spmvattr     FETCH_SIZE / WRITE_SIZE of the A SpMV against the same matrix with its x gathers in a 32 KB window
+#   sqmg         the same over the multigrid apply (mg:1 / mg:1 inner solves; extra bench args in $SQMG_ARGS)
 #   sqapply      SQ counter passes over bench.py's eager apply (every kernel of the apply; tools/pmc_table.py)
+#   setup:ARGS   tools/setup_timing.py ARGS ('+' for spaces): the partitioned preconditioner's setup over gloo ranks on one GPU
 #   py:FILE      python FILE (any experiment script), 300 s
 #   ab:V1,V2,..  A/B of experiment builds (tools/build_variants.py): bench.py per variant (V or V@ARGS, '+' for
 #                spaces; variant "base" = the product library); extra bench args for all in $BENCH_ARGS
@@ -103,7 +105,8 @@ step() {
             [ "$V" = base ] && L=
             MPBP_LIB=$L timeout -k 10 120 python tools/spmv_ab.py >> "$OUT/spmv_$V.log" 2>&1 || return 1
           done ;;
-    sqapply) local B="$ROOTD/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-spmv --no-graph"
+    sqapply|sqmg) local B="$ROOTD/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-spmv --no-graph"
+          [ "$s" = sqmg ] && B="$B --no-mg --no-solve --inner-f mg:1 --inner-p mg:1 $SQMG_ARGS"
           prof sq1_apply 150 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
             SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU --output-format csv -d "$ROOTD/$OUT/sq1_apply" \
             -o pmc -- python $B || return 1
@@ -112,8 +115,9 @@ step() {
             -d "$ROOTD/$OUT/sq2_apply" -o pmc -- python $B || return 1
           # reduce on the box (the raw per-dispatch CSVs of a whole bench run exceed gpurun's 64 MiB copy-back)
           mkdir -p "$OUT/sqraw" && mv "$OUT"/sq1_apply "$OUT"/sq2_apply "$OUT/sqraw/" &&
-            python tools/pmc_table.py "$OUT/sqraw" --json "$OUT/sq_apply.json" > "$OUT/sq_apply.txt" &&
+            python tools/pmc_table.py "$OUT/sqraw" --json "$OUT/sq_$s.json" > "$OUT/sq_$s.txt" &&
             rm -rf "$OUT/sqraw" ;;
+    setup:*) timeout -k 10 600 python -u tools/setup_timing.py $(echo "${s#setup:}" | tr + ' ') >> "$OUT/setup_timing.log" 2>&1 ;;
     py:*) timeout -k 10 300 python -u "${s#py:}" > "$OUT/$(basename "${s#py:}" .py).log" 2>&1 ;;
     *) echo "unknown step $s"; return 98 ;;
   esac

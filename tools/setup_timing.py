@@ -1,0 +1,70 @@
+"""Setup time of the row-partitioned preconditioner (rank-local assembly, DistributedSchurPreconditioner) at configs[4]'s
+2048^2 over W gloo ranks that all share one GPU (the 8-GPU geometry rehearsed on one card; the max over ranks is
+printed).  Builds run in the order given (--order); the first pays the process's cold start.
+
+    python tools/setup_timing.py [--world 8] [--n 2048]
+"""
+import argparse
+import json
+import os
+import socket
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def worker(rank, world, port, n, order, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import mp_block_preconditioners_amd as mpb
+    from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
+    out = {}
+    for numerics in order:
+        dist.barrier()
+        t0 = time.perf_counter()
+        dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=mpb.InnerSolver("chebyshev", 4),
+                                             inner_P=mpb.InnerSolver("chebyshev", 4), numerics=numerics)
+        torch.cuda.synchronize()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        out[f"{len(out) + 1}_{numerics}"] = float(el.item())
+        dpc.close()
+        del dpc
+        torch.cuda.empty_cache()
+    if rank == 0:
+        q.put(out)
+    dist.destroy_process_group()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--n", type=int, default=2048)
+    ap.add_argument("--order", default="exact,fast,fast", help="numerics of the successive builds")
+    a = ap.parse_args()
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    order = a.order.split(",")
+    procs = [ctx.Process(target=worker, args=(r, a.world, port, a.n, order, q)) for r in range(a.world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+    print(json.dumps({"n": a.n, "world": a.world, "backend": "gloo, every rank on one GPU",
+                      "setup_seconds_max_over_ranks": res,
+                      "note": "DistributedSchurPreconditioner construction: rank-local F / D / G rows, commutator "
+                              "products of the owned rows, Chebyshev bounds, CA ghost diagonals, halo plan"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
