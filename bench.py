@@ -148,6 +148,8 @@ def main():
     ap.add_argument("--f-solve", type=int, default=None,
                     help="fast numerics: 1 (default) runs each F solve of 3 or 4 updates as one k_fsolve launch, "
                          "0 as k_ftile launches")
+    ap.add_argument("--solve-numerics", default="exact", choices=["fast", "exact"],
+                    help="N > 1: numerics of the partitioned multigrid apply and the distributed FGMRES section")
     ap.add_argument("--q13-sym", type=int, default=None,
                     help="fast numerics: 1 (default) reads Gt_F_G's diamond upper half only (symmetric product); 0: all 13")
     ap.add_argument("--gtg-drhs", type=int, default=None,
@@ -545,10 +547,14 @@ def partitioned_solver_section(args, n, rank, world, dist, torch, backend):
     import mp_block_preconditioners_amd as mp
     from mp_block_preconditioners_amd.distributed import DistributedMatrix, DistributedSchurPreconditioner
     scale = n * n / float(1024 * 1024)
+    # the multigrid solve runs the exact numerics: the partition's per-operator exchange schedule starts its smoothing
+    # from the stored diagonal (x0 = c2 (b / diag)) where the one-GPU fast hierarchy recomputes the reciprocal, so only
+    # the exact mode makes the residual histories comparable bit for bit (--solve-numerics overrides)
+    snum = args.solve_numerics
     mg1 = dict(inner_F=mp.InnerSolver("mg", 1), inner_P=mp.InnerSolver("mg", 1))
     out = {}
     t0 = time.perf_counter()
-    M = DistributedSchurPreconditioner(n, args.xi, args.eta_n, args.eta_s, numerics=args.numerics, **mg1)
+    M = DistributedSchurPreconditioner(n, args.xi, args.eta_n, args.eta_s, numerics=snum, **mg1)
     torch.cuda.synchronize()
     setup = time.perf_counter() - t0
     gen = torch.Generator(device="cuda").manual_seed(77 + rank)
@@ -556,7 +562,7 @@ def partitioned_solver_section(args, n, rank, world, dist, torch, backend):
     o = torch.empty_like(v)
     dte = timed_loop(lambda: M.apply(v, o), args.steps, args.warmup, world, dist, torch)
     mg = {"inner": "mg:1 / mg:1", "unit": "applies/s (1024^2-cell equivalents)", "setup_seconds": setup,
-          "eager_applies_per_s": args.steps / dte * scale, "f_numerics": args.numerics}
+          "eager_applies_per_s": args.steps / dte * scale, "f_numerics": snum}
     if backend == "nccl" and not args.eager_partitioned:
         try:
             g = M.capture(v, o)
@@ -580,7 +586,7 @@ def partitioned_solver_section(args, n, rank, world, dist, torch, backend):
     dA = DistributedMatrix(bp.assemble_rows(L.OP_A, own, c=1.0, d_u=-1.0), n, 5, owned_rows=True)
     del bp
     torch.cuda.empty_cache()
-    Md = DistributedSchurPreconditioner(n, args.xi, args.eta_n, args.eta_s, numerics=args.numerics, **mg1)
+    Md = DistributedSchurPreconditioner(n, args.xi, args.eta_n, args.eta_s, numerics=snum, **mg1)
     torch.cuda.synchronize()
     setup = time.perf_counter() - t0
     _, b = mp.manufactured_problem(n, xi=args.xi, etan=args.eta_n, etas=args.eta_s)
@@ -599,7 +605,7 @@ def partitioned_solver_section(args, n, rank, world, dist, torch, backend):
     sd = {"inner": "mg:1 / mg:1", "tol": 1e-8, "maxiter": 150, "iterations": len(hist) - 1, "converged": info == 0,
           "seconds": el, "setup_seconds": setup, "rel_residual": hist[-1] / hist[0] if hist and hist[0] else None,
           "halo": Md.halo_impl, "communicators_per_rank": (Md._rccl.comm_refs if Md._rccl is not None else 0),
-          "f_numerics": args.numerics}
+          "f_numerics": snum}
     shared = None if Md._rccl is None or dA._rccl is None else bool(Md._rccl.comm == dA._rccl.comm)
     dA.close()
     Md.close()
@@ -610,15 +616,17 @@ def partitioned_solver_section(args, n, rank, world, dist, torch, backend):
         t0 = time.perf_counter()
         bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
         A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
-        pc1 = mp.ApproxSchurPreconditioner(F, D, G, numerics=args.numerics, **mg1)
+        pc1 = mp.ApproxSchurPreconditioner(F, D, G, numerics=snum, **mg1)
         h1 = []
         # the partitioned hierarchy applies its level 1 from the stored Galerkin product; a one-GPU fast hierarchy
         # defaults to R0 (F (P0 x)) (the same operator, other roundings): compare against the stored form
         L.check(L.lib().mpbp_set_mg_galerkin_mf(0))
+        L.check(L.lib().mpbp_set_q13_sym(0))
         try:
             mp.fgmres(A, torch.from_numpy(b).cuda(), M=pc1, tol=1e-8, maxiter=150, residuals=h1)
         finally:
             L.check(L.lib().mpbp_set_mg_galerkin_mf(1))
+            L.check(L.lib().mpbp_set_q13_sym(1))
         same[0] = 1 if np.array_equal(np.asarray(h1), np.asarray(hist)) else 0
         sd["single_gpu_iterations"] = len(h1) - 1
         sd["single_gpu_check_seconds"] = time.perf_counter() - t0
@@ -628,7 +636,7 @@ def partitioned_solver_section(args, n, rank, world, dist, torch, backend):
     if not args.no_check:
         sd["bit_exact_vs_single_gpu"] = bool(same.item())
         sd["check"] = ("the residual history (every iteration's ||r||) equals the one-GPU FGMRES's bit for bit (one GPU "
-                       "with multigrid level 1 from its stored Galerkin matrix, as the partitioned hierarchy)")
+                       "with multigrid level 1 from its stored Galerkin matrix and Gt_F_G's full rows, as the partition)")
     if shared is not None:
         sd["operator_and_preconditioner_share_one_communicator"] = shared
     return {"mg_apply_partitioned": mg, "solve_distributed": sd}
@@ -659,7 +667,12 @@ def single_gpu_check(dpc, n, args, iF, iP, rank, dist, torch):
     del F, D, G
     vg = torch.from_numpy(np.random.default_rng(2048).standard_normal(pc.shape[0])).cuda()
     gids = torch.from_numpy(dpc.local_to_global_rows()).cuda()
-    ref = pc.apply(vg)[gids]
+    from mp_block_preconditioners_amd._lib import check, lib
+    check(lib().mpbp_set_q13_sym(0))   # the partition multiplies Gt_F_G's full rows: the one-GPU twin does too
+    try:
+        ref = pc.apply(vg)[gids]
+    finally:
+        check(lib().mpbp_set_q13_sym(1))
     got = dpc.apply(vg[gids].contiguous())
     torch.cuda.synchronize()
     same = torch.tensor([1 if torch.equal(got, ref) else 0], dtype=torch.int64, device="cuda")

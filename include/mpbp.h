@@ -457,7 +457,8 @@ int mpbp_set_f_direct(int32_t on);
 int mpbp_set_gtg_drhs(int32_t on);
 /* Tolerance mode (plan f_numerics FAST), one GPU: Gt_F_G x on the diamond reads only the symmetric product's upper
  * half (slots 6..12; the lower entries mirrored from the neighbouring rows): 56 instead of 104 B of values per row,
- * within the mode's 1e-12 bar.  1 (default) or 0 (all 13 slots, bit-exact to the CSR product). */
+ * within the mode's 1e-12 bar.  1 (default) or 0 (all 13 slots: bit-exact to the CSR product, which the row-partitioned
+ * apply multiplies -- the one-GPU apply it is compared with bit for bit sets 0). */
 int mpbp_set_q13_sym(int32_t on);
 int mpbp_set_gtg_fused(int32_t on);   /* also 256 / 512: on, with that many lanes per workgroup (default 512) */
 /* One-GPU tolerance-mode F solves: x0 with the first sweep, and the last two sweeps, as 2D-tile launches (k_ftile: no

@@ -31,7 +31,8 @@ int g_f_direct = 0;        // tolerance-mode F sweeps on the direct kernel (one 
 int g_gtg_tpb = 512;        // k_gtg_solve workgroup: 512 lanes (one tile cell + one ring cell each) or 256
 int g_gtg_fused = 1;
 int g_gtg_drhs = 1;
-int g_q13_sym = 1;          // tolerance mode: Gt_F_G x read from the diamond's upper half (symmetric product)         // the first fused Gt_G solve builds rhs = D Finv_v + v_p itself (no D launch)       // one-GPU Chebyshev Gt_G solves of 2..6 sweeps as one k_gtg_solve launch (0: per sweep)
+int g_q13_sym = 1;          // tolerance mode, one GPU: Gt_F_G x read from the diamond's upper half (symmetric product;
+                           // the row-partitioned apply multiplies full rows: its one-GPU twin sets this to 0)         // the first fused Gt_G solve builds rhs = D Finv_v + v_p itself (no D launch)       // one-GPU Chebyshev Gt_G solves of 2..6 sweeps as one k_gtg_solve launch (0: per sweep)
 int g_f_solve = 1;         // one-GPU tolerance-mode F solves of 3 or 4 Chebyshev updates as one launch (k_fsolve)
 int g_f_tile = 1;          // one-GPU tolerance-mode F: x0 + sweep 1, and the last pair, on 2D tiles (k_ftile)
 int g_f_pair = 1;         // tolerance-mode F solves: the last two Chebyshev sweeps as one k_march2 launch (0: two)
@@ -6079,7 +6080,8 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
     //    (one GPU: the diamond layout when the plan has it)
     const bool qx0 = px0 && p->q13;
     if (qx0)
-        rc = launch_q13(p->q13_n, p->q13, Pxa, EpiStoreX0{Pxb, p->diag_P, pc2[0], P0}, c.st);
+        rc = launch_q13(p->q13_n, p->q13, Pxa, EpiStoreX0{Pxb, p->diag_P, pc2[0], P0}, c.st,
+                        g_q13_sym && p->f_numerics == MPBP_NUMERICS_FAST);
     else if (p->q13 && !p->halo)   // tolerance mode: the symmetric product's upper half (k_q13<SYM>)
         rc = launch_q13(p->q13_n, p->q13, Pxa, EpiStore{Pxb}, c.st, g_q13_sym && p->f_numerics == MPBP_NUMERICS_FAST);
     else

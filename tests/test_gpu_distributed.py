@@ -43,7 +43,11 @@ def _worker(rank, world, port, n, layout, f_mode, kind, errfile, ca="auto", fuse
         assert (pc.inner_F.lmin, pc.inner_F.lmax) == (dpc.inner_F.lmin, dpc.inner_F.lmax)
         v = torch.from_numpy(np.random.default_rng(5).standard_normal(pc.shape[0])).cuda()
         gids = torch.from_numpy(dpc.local_to_global_rows()).cuda()
-        ref = pc.apply(v)[gids]
+        mpb.lib().mpbp_set_q13_sym(0)   # the partition multiplies Gt_F_G's full rows: so does the one-GPU reference
+        try:
+            ref = pc.apply(v)[gids]
+        finally:
+            mpb.lib().mpbp_set_q13_sym(1)
         for _ in range(2):
             got = dpc.apply(v[gids].contiguous())
             if numerics == "fast" and not dpc.ca:

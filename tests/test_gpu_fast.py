@@ -267,7 +267,7 @@ def test_matrix_free_galerkin_level1(n):
 
 @pytest.mark.parametrize("n", [5, 16, 100, 256])
 def test_q13_symmetric_half(n):
-    """Tolerance mode reads Gt_F_G's diamond upper half (mpbp_set_q13_sym, default): the apply stays within 1e-13
+    """Tolerance mode reads Gt_F_G's diamond upper half (mpbp_set_q13_sym, default 1): the apply stays within 1e-13
     relative of the 13-slot apply (the stored product is symmetric to ~1.5e-16) and within 1e-12 of the oracle's;
     the exact mode never takes it."""
     mp = _mp()
