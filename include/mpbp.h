@@ -469,9 +469,8 @@ int mpbp_set_f_tile(int32_t on);
  * 1 (default) or 0 (k_ftile / marching launches). */
 int mpbp_set_f_solve(int32_t on);
 /* Tolerance-mode F hierarchies (plan f_numerics FAST, one GPU, matrix-free level 0 and transfers): level 1 applied as
- * R_0 (F (P_0 x)) instead of streaming its stored Galerkin matrix: 1 (default) as three launches through fine-size
- * temporaries, 2 as one launch with the fine intermediates in LDS (k_gal1; same bits, measured slower), 0 the stored
- * matrix. */
+ * R_0 (F (P_0 x)) instead of streaming its stored Galerkin matrix: 2 (default) as one launch with the fine
+ * intermediates in LDS (k_gal1), 1 as three launches through fine-size temporaries (same bits), 0 the stored matrix. */
 int mpbp_set_mg_galerkin_mf(int32_t on);
 /* 1 (default): the matrix-free D, G and Gt_G sweeps run as one thread per cell reading neighbours from global memory
  * (no LDS ring; row partitions and ghost layouts included); 0: the marching kernel.  Bit-identical either way. */

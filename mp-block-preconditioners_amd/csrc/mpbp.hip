@@ -25,8 +25,8 @@ int g_march_rows = 0;
 int g_csr_table = 1;      // CSR SpMV waves start from the row blocks' wave table when it has one (0: from row_ptr)
 int g_mg_mf_transfer = 1;   // whole-grid multigrid transfers matrix-free (0: their CSR / SELL / grouped forms)
 int g_init_diag = 1;      // fused first F sweep: 1 rebuilds the staged diagonal from thn, 0 streams diag
-int g_mg_gal = 1;          // tolerance-mode F hierarchies: level 1 as R_0 (F (P_0 x)): 1 three launches (MgGal), 2 one
-                           // k_gal1 launch (measured slower), 0 its stored Galerkin matrix
+int g_mg_gal = 2;          // tolerance-mode F hierarchies: level 1 as R_0 (F (P_0 x)): 2 one k_gal1 launch, 1 three
+                           // launches (MgGal), 0 its stored Galerkin matrix
 int g_f_direct = 0;        // tolerance-mode F sweeps on the direct kernel (one thread per cell, no LDS) instead of marching
 int g_gtg_tpb = 512;        // k_gtg_solve workgroup: 512 lanes (one tile cell + one ring cell each) or 256
 int g_gtg_fused = 1;
@@ -3584,7 +3584,46 @@ constexpr int kG1W = 32, kG1H = 4;                          // coarse tile
 constexpr int kG1FW = 2 * kG1W + 2, kG1FH = 2 * kG1H + 2;   // t1: fine [2 c0 - 1, 2 c0 + 2 W + 1)
 constexpr int kG1PW = kG1FW + 2, kG1PH = kG1FH + 2;         // t0 and thn: one more fine cell each side
 constexpr int kG1CW = kG1W + 4, kG1CH = kG1H + 4;           // coarse x: [c0 - 2, c0 + W + 2)
-template <class Epi>
+// a grid index to its slot in a staged window starting at virtual index `base` (the window is < the grid)
+__device__ inline int g1_slot(int i, int base, int m) { int l = i - base; return l < 0 ? l + m : (l >= m ? l - m : l); }
+// P_0's row at fine (gr, gc) of a field with compile-time kinds: k_mg_transfer_spmv's list order and products
+template <int KY, int KX>
+__device__ inline double g1_p(const double* xf, int gr, int gc, int nc, int rb, int cb) {
+    int yi[2], xi[2];
+    double yw[2], xw[2];
+    const int my = mg_p1d_fast(KY, nc, gr, yi, yw), mx = mg_p1d_fast(KX, nc, gc, xi, xw);
+    double acc = 0.0;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        if (a >= my) break;
+        const double* xr = xf + g1_slot(yi[a], rb, nc) * kG1CW;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            if (b >= mx) break;
+            acc += (yw[a] * xw[b]) * xr[g1_slot(xi[b], cb, nc)];
+        }
+    }
+    return acc;
+}
+// R_0's row at coarse (cr, cc): 4 (cell) x 3 or 4 entries, compile-time counts
+template <int KY, int KX>
+__device__ inline double g1_r(const double* tf, int cr, int cc, int n, int rb, int cb) {
+    constexpr int MY = KY == MPBP_MG_CELL ? 4 : 3, MX = KX == MPBP_MG_CELL ? 4 : 3;
+    int yi[4], xi[4];
+    double yw[4], xw[4];
+    mg_r1d_fast(KY, n, cr, yi, yw);
+    mg_r1d_fast(KX, n, cc, xi, xw);
+    double acc = 0.0;
+#pragma unroll
+    for (int a = 0; a < MY; ++a) {
+        const double* tr1 = tf + g1_slot(yi[a], rb, n) * kG1FW;
+#pragma unroll
+        for (int b = 0; b < MX; ++b) acc += (yw[a] * xw[b]) * tr1[g1_slot(xi[b], cb, n)];
+    }
+    return acc;
+}
+// MAC: the F hierarchy's kinds (u: rows cell-, columns node-centred; v: the reverse) at compile time
+template <class Epi, bool MAC = false>
 __global__ void __launch_bounds__(256) k_gal1(FStencilFast P, MgFields tr, const double* __restrict__ x, Epi epi) {
     constexpr int CN = kG1CW * kG1CH, PN = kG1PW * kG1PH, FN = kG1FW * kG1FH;
     __shared__ double xs[4 * CN];
@@ -3633,6 +3672,11 @@ __global__ void __launch_bounds__(256) k_gal1(FStencilFast P, MgFields tr, const
         const int gr = P.wrap(fr0 - 2 + r), gc = P.wrap(fc0 - 2 + c);
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
+            if constexpr (MAC) {
+                t0[f * PN + i] = (f & 1) ? g1_p<MPBP_MG_NODE, MPBP_MG_CELL>(xs + f * CN, gr, gc, nc, cr0 - 2, cc0 - 2)
+                                         : g1_p<MPBP_MG_CELL, MPBP_MG_NODE>(xs + f * CN, gr, gc, nc, cr0 - 2, cc0 - 2);
+                continue;
+            }
             int yi[4], xi[4];
             double yw[4], xw[4];
             const int my = mg_p1d_fast(tr.ky[f], nc, gr, yi, yw), mx = mg_p1d_fast(tr.kx[f], nc, gc, xi, xw);
@@ -3661,6 +3705,22 @@ __global__ void __launch_bounds__(256) k_gal1(FStencilFast P, MgFields tr, const
     }
     __syncthreads();
     // R_0 t1 on the tile's coarse rows (4 fields x 128 cells), each to the epilogue
+    if constexpr (MAC) {   // lane t: cell t & 127 of fields (t >> 7) and (t >> 7) + 2 -- one kind pair per wave
+        const int cell = tid & (kG1W * kG1H - 1), fp = tid >> 7;
+        const int cr = cr0 + cell / kG1W, cc = cc0 + cell % kG1W;
+        if (cr < nc && cc < nc) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int f = fp + 2 * h;
+                const int32_t row = f * ncc + cr * nc + cc;
+                const typename Epi::P pe = epi.pre(row);
+                const double acc = fp ? g1_r<MPBP_MG_NODE, MPBP_MG_CELL>(t1 + f * FN, cr, cc, n, fr0 - 1, fc0 - 1)
+                                      : g1_r<MPBP_MG_CELL, MPBP_MG_NODE>(t1 + f * FN, cr, cc, n, fr0 - 1, fc0 - 1);
+                epi(row, acc, pe);
+            }
+        }
+        return;
+    }
     for (int j = tid; j < 4 * kG1W * kG1H; j += 256) {
         const int f = j / (kG1W * kG1H), cell = j - f * (kG1W * kG1H);
         const int cr = cr0 + cell / kG1W, cc = cc0 + cell % kG1W;
@@ -5103,7 +5163,11 @@ int gal_fused(const MgGal& g, const double* x, Epi epi, hipStream_t st, bool* do
     }
     const int nc = p->f_prm.n / 2;
     const int64_t tiles = (int64_t)((nc + kG1W - 1) / kG1W) * ((nc + kG1H - 1) / kG1H);
-    k_gal1<Epi><<<(unsigned)tiles, 256, 0, st>>>(FStencilFast{Pd}, F, x, epi);
+    bool mac = true;   // the F hierarchy's MAC kinds (mg.FIELDS_VELOCITY)
+    for (int f = 0; f < 4; ++f)
+        mac = mac && F.ky[f] == ((f & 1) ? MPBP_MG_NODE : MPBP_MG_CELL) && F.kx[f] == ((f & 1) ? MPBP_MG_CELL : MPBP_MG_NODE);
+    if (mac) k_gal1<Epi, true><<<(unsigned)tiles, 256, 0, st>>>(FStencilFast{Pd}, F, x, epi);
+    else k_gal1<Epi, false><<<(unsigned)tiles, 256, 0, st>>>(FStencilFast{Pd}, F, x, epi);
     MPBP_HIP(hipGetLastError());
     *done = true;
     return MPBP_OK;

@@ -253,9 +253,9 @@ def test_matrix_free_galerkin_level1(n):
         check(lib().mpbp_set_mg_galerkin_mf(2))
         one = fast.apply(v).clone()
     finally:
-        check(lib().mpbp_set_mg_galerkin_mf(1))
+        check(lib().mpbp_set_mg_galerkin_mf(2))
     assert 0.0 < rel_inf(got.cpu().numpy(), stored.cpu().numpy()) <= 1e-10
-    assert torch.equal(one, got)   # one k_gal1 launch == the three launches (the default), bit for bit
+    assert torch.equal(one, got)   # one k_gal1 launch (the default) == the three launches, bit for bit
     exact = mp.ApproxSchurPreconditioner(F, D, G, fast.GtG, fast.GtFG, **kw)
     assert rel_inf(got.cpu().numpy(), exact.apply(v).cpu().numpy()) <= 1e-10
     out = torch.empty_like(v)
