@@ -159,6 +159,9 @@ def main():
     ap.add_argument("--mg-galerkin-mf", type=int, default=None,
                     help="fast numerics: 2 (default) applies the F hierarchy's level 1 as R0 (F (P0 x)) in one k_gal1 "
                          "launch, 1 in three launches, 0 streams its stored Galerkin matrix")
+    ap.add_argument("--mg-galerkin-mf-p", type=int, default=None,
+                    help="fast numerics: 1 (default) applies the pressure hierarchy's level 1 as R0 (Gt_G (P0 x)) "
+                         "(one k_gal1p launch with --mg-galerkin-mf 2), 0 streams its stored Galerkin matrix")
     ap.add_argument("--svl-min-rows", type=int, default=None,
                     help="multigrid levels above this many rows get a stencil-values copy (mg.SVL_MIN_ROWS; -1: none)")
     ap.add_argument("--stored-transfers", action="store_true",
@@ -245,6 +248,8 @@ def main():
         _check(_lib().mpbp_set_q13_sym(args.q13_sym))
     if args.mg_galerkin_mf is not None:
         _check(_lib().mpbp_set_mg_galerkin_mf(args.mg_galerkin_mf))
+    if args.mg_galerkin_mf_p is not None:
+        _check(_lib().mpbp_set_mg_galerkin_mf_p(args.mg_galerkin_mf_p))
     if args.stored_transfers:
         _check(_lib().mpbp_set_mg_mf_transfer(0))
     if args.mg_group_rows is not None:

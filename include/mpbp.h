@@ -472,6 +472,9 @@ int mpbp_set_f_solve(int32_t on);
  * R_0 (F (P_0 x)) instead of streaming its stored Galerkin matrix: 2 (default) as one launch with the fine
  * intermediates in LDS (k_gal1), 1 as three launches through fine-size temporaries (same bits), 0 the stored matrix. */
 int mpbp_set_mg_galerkin_mf(int32_t on);
+/* The same for the pressure (Gt_G) hierarchy's level 1 -- R_0 (Gt_G (P_0 x)), one k_gal1p launch when
+ * mpbp_set_mg_galerkin_mf is 2 -- in tolerance mode.  1 (default) or 0 (its stored Galerkin matrix). */
+int mpbp_set_mg_galerkin_mf_p(int32_t on);
 /* 1 (default): the matrix-free D, G and Gt_G sweeps run as one thread per cell reading neighbours from global memory
  * (no LDS ring; row partitions and ghost layouts included); 0: the marching kernel.  Bit-identical either way. */
 int mpbp_set_pg_direct(int32_t on);

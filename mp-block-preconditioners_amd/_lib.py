@@ -171,6 +171,7 @@ _SIGNATURES = {
     "mpbp_set_f_solve": ([c_int32], c_int),
     "mpbp_set_gtg_drhs": ([c_int32], c_int),
     "mpbp_set_q13_sym": ([c_int32], c_int),
+    "mpbp_set_mg_galerkin_mf_p": ([c_int32], c_int),
     "mpbp_stokes_count_rows": ([POINTER(StokesParams), c_int32, _P, _P, c_int32, _P, _P], c_int),
     "mpbp_stokes_fill_rows": ([POINTER(StokesParams), c_int32, _P, _P, _P, _P, c_int32, _P, _P, _P, _P], c_int),
     "mpbp_set_mg_galerkin_mf": ([c_int32], c_int),

@@ -25,6 +25,7 @@ int g_march_rows = 0;
 int g_csr_table = 1;      // CSR SpMV waves start from the row blocks' wave table when it has one (0: from row_ptr)
 int g_mg_mf_transfer = 1;   // whole-grid multigrid transfers matrix-free (0: their CSR / SELL / grouped forms)
 int g_init_diag = 1;      // fused first F sweep: 1 rebuilds the staged diagonal from thn, 0 streams diag
+int g_mg_gal_p = 1;        // ... the pressure (Gt_G) hierarchy's level 1 too, as R_0 (Gt_G (P_0 x)) (k_gal1p)
 int g_mg_gal = 2;          // tolerance-mode F hierarchies: level 1 as R_0 (F (P_0 x)): 2 one k_gal1 launch, 1 three
                            // launches (MgGal), 0 its stored Galerkin matrix
 int g_f_direct = 0;        // tolerance-mode F sweeps on the direct kernel (one thread per cell, no LDS) instead of marching
@@ -3739,6 +3740,88 @@ __global__ void __launch_bounds__(256) k_gal1(FStencilFast P, MgFields tr, const
     }
 }
 
+// The pressure hierarchy's level 1 the same way (tolerance mode): A_1 x = R_0 (Gt_G (P_0 x)) on a 32 x 8 coarse tile
+// (a 64 x 16 fine block), one field, cell-centred both ways; Gt_G's rows by GtGStencilDev::entries and add5 (the
+// matrix-free level-0 sweep's operations), the transfers' by k_mg_transfer_spmv's: bit-identical to the three launches.
+constexpr int kG1PH2 = 8;                                     // coarse tile rows (pressure)
+constexpr int kGPFH = 2 * kG1PH2 + 2, kGPPH = kGPFH + 2;       // fine t1 / t0 rows
+template <class Epi>
+__global__ void __launch_bounds__(256) k_gal1p(GtGStencilDev P, const double* __restrict__ x, Epi epi) {
+    constexpr int CH = kG1PH2 + 4, CN = kG1CW * CH, PN = kG1PW * kGPPH, FN = kG1FW * kGPFH;
+    __shared__ double xs[CN];
+    __shared__ double ts[PN];
+    __shared__ double t0[PN];
+    __shared__ double t1[FN];
+    const int n = P.n, nc = n >> 1;
+    const int tx = (nc + kG1W - 1) / kG1W;
+    const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int cr0 = (bk / tx) * kG1PH2, cc0 = (bk % tx) * kG1W;
+    const int fr0 = 2 * cr0, fc0 = 2 * cc0;
+    const int tid = threadIdx.x;
+    auto wrapc = [&](int a) { return a < 0 ? a + nc : (a >= nc ? a - nc : a); };
+    {
+        constexpr int IX = (CN + 255) / 256, IT = (PN + 255) / 256;
+        double vx[IX], vt[IT];
+#pragma unroll
+        for (int it = 0; it < IX; ++it) {
+            const int i = tid + it * 256;
+            if (i < CN) {
+                const int r = i / kG1CW, c = i - r * kG1CW;
+                vx[it] = x[wrapc(cr0 - 2 + r) * nc + wrapc(cc0 - 2 + c)];
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256;
+            if (i < PN) {
+                const int r = i / kG1PW, c = i - r * kG1PW;
+                vt[it] = P.cell[P.wrap(fr0 - 2 + r) * n + P.wrap(fc0 - 2 + c)];
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < IX; ++it)
+            if (tid + it * 256 < CN) xs[tid + it * 256] = vx[it];
+#pragma unroll
+        for (int it = 0; it < IT; ++it)
+            if (tid + it * 256 < PN) ts[tid + it * 256] = vt[it];
+    }
+    __syncthreads();
+    for (int i = tid; i < PN; i += 256) {   // t0 = P_0 x on the fine block + 2
+        const int r = i / kG1PW, c = i - r * kG1PW;
+        t0[i] = g1_p<MPBP_MG_CELL, MPBP_MG_CELL>(xs, P.wrap(fr0 - 2 + r), P.wrap(fc0 - 2 + c), nc, cr0 - 2, cc0 - 2);
+    }
+    __syncthreads();
+    {   // t1 = Gt_G t0 on the fine block + 1
+        const TTileT<kG1PW> ta{ts, fr0 - 2, fc0 - 2};
+        for (int i0 = 0; i0 < FN; i0 += 256) {
+            const int i = i0 + tid;
+            const bool live = i < FN;
+            const int ii = live ? i : 0;
+            const int r = ii / kG1FW, c = ii - r * kG1FW;
+            const int vr = fr0 - 1 + r, vc = fc0 - 1 + c, gr = P.wrap(vr), gc = P.wrap(vc);
+            const bool edge = __builtin_amdgcn_readfirstlane(__any(live && (gr == 0 || gr == n - 1 || gc == 0 ||
+                                                                            gc == n - 1))) != 0;
+            if (!live) continue;
+            double e[5];
+            P.entries(vr, vc, gr, gc, ta, e);
+            const int si = (r + 1) * kG1PW + (c + 1);
+            const double pr[5] = {e[0] * t0[si - kG1PW], e[1] * t0[si - 1], e[2] * t0[si], e[3] * t0[si + 1],
+                                  e[4] * t0[si + kG1PW]};
+            const Wrap wr{gr == 0, gr == n - 1, gc == 0, gc == n - 1};
+            t1[i] = edge ? add5<true>(0.0, pr, wr) : add5<false>(0.0, pr, wr);
+        }
+    }
+    __syncthreads();
+    {   // R_0 t1 on the tile's 256 coarse rows, each to the epilogue
+        const int cr = cr0 + tid / kG1W, cc = cc0 + tid % kG1W;
+        if (cr < nc && cc < nc) {
+            const int32_t row = cr * nc + cc;
+            const typename Epi::P pe = epi.pre(row);
+            epi(row, g1_r<MPBP_MG_CELL, MPBP_MG_CELL>(t1, cr, cc, n, fr0 - 1, fc0 - 1), pe);
+        }
+    }
+}
+
 // One thread per (slice, lane): copy the CSR row into its column-major slots.
 __global__ void k_sell_fill(Csr A, const int4* slices, int nslices, uint8_t* rlen, double* val, int32_t* col) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3947,6 +4030,11 @@ int mpbp_set_pg_direct(int32_t on) {
 int mpbp_set_mg_galerkin_mf(int32_t on) {
     if (on < 0 || on > 2) return set_error(MPBP_ERR_ARG, "mg_galerkin_mf must be 0, 1 or 2");
     g_mg_gal = on;
+    return MPBP_OK;
+}
+int mpbp_set_mg_galerkin_mf_p(int32_t on) {
+    if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "mg_galerkin_mf_p must be 0 or 1");
+    g_mg_gal_p = on;
     return MPBP_OK;
 }
 int mpbp_set_f_direct(int32_t on) {
@@ -5151,6 +5239,20 @@ template <class Epi>
 int gal_fused(const MgGal& g, const double* x, Epi epi, hipStream_t st, bool* done) {
     *done = false;
     const mpbp_schur_plan* p = g.fine.stencil;
+    if (g.fine.sop == SOP_GTG) {   // the pressure hierarchy: one field, cell-centred (mg.FIELDS_PRESSURE)
+        if (g_mg_gal != 2 || g.m->tr_nfields != 1 || g.m->tr_ky[0] != MPBP_MG_CELL || g.m->tr_kx[0] != MPBP_MG_CELL ||
+            p->f_prm.n < 2 * kG1CW || (p->f_prm.n & 1))
+            return MPBP_OK;
+        PGDev Pg;
+        const int rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &Pg);
+        if (rc) return rc;
+        const int nc = p->f_prm.n / 2;
+        const int64_t tiles = (int64_t)((nc + kG1W - 1) / kG1W) * ((nc + kG1PH2 - 1) / kG1PH2);
+        k_gal1p<Epi><<<(unsigned)tiles, 256, 0, st>>>(GtGStencilDev{Pg}, x, epi);
+        MPBP_HIP(hipGetLastError());
+        *done = true;
+        return MPBP_OK;
+    }
     if (g_mg_gal != 2 || g.m->tr_nfields != 4 || p->f_prm.n < 2 * kG1CW || (p->f_prm.n & 1)) return MPBP_OK;
     FStencilDev Pd;
     const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &Pd);
@@ -5436,8 +5538,17 @@ __global__ void __launch_bounds__(kDT) k_dense_cm(int32_t m, const double* __res
 #pragma unroll
         for (int u = 0; u < U; ++u) tile[t + kDT * u] = v[u] * bs[(t + kDT * u) / kDR];
         __syncthreads();
-        if (t < kDR)
-            for (int c = 0; c < kc; ++c) acc += tile[c * kDR + t];
+        if (t < kDR) {   // 32 LDS reads in flight ahead of each run of dependent adds (same order)
+            int c = 0;
+            for (; c + 32 <= kc; c += 32) {
+                double q[32];
+#pragma unroll
+                for (int u = 0; u < 32; ++u) q[u] = tile[(c + u) * kDR + t];
+#pragma unroll
+                for (int u = 0; u < 32; ++u) acc += q[u];
+            }
+            for (; c < kc; ++c) acc += tile[c * kDR + t];
+        }
         __syncthreads();
     }
     if (t < kDR && r0 + t < m) y[r0 + t] = acc;
@@ -5532,8 +5643,9 @@ int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, 
 // Level 1 as R_0 (F (P_0 x)): tolerance-mode F stencil level 0 on one GPU, matrix-free transfers, level 1 smoothed.
 bool mg_gal_ok(const mpbp_mg* m, const MgFine& f) {
     const OpRef& o = f.op.in;
-    return g_mg_gal && o.stencil && o.sop == SOP_F && o.stencil->f_numerics == MPBP_NUMERICS_FAST && o.which == 0 &&
-           f.op.bd.empty && !f.halo && !o.stencil->halo && m->nlevels > 2 && use_mf_transfer(m, 0) && f.r && f.d;
+    return g_mg_gal && o.stencil && (o.sop == SOP_F || (o.sop == SOP_GTG && g_mg_gal_p)) &&
+           o.stencil->f_numerics == MPBP_NUMERICS_FAST && o.which == 0 && f.op.bd.empty && !f.halo && !o.stencil->halo &&
+           m->nlevels > 2 && use_mf_transfer(m, 0) && f.r && f.d;
 }
 
 // One V-cycle on level l for A_l x = b.  Level 0 uses `fine` (operator and buffers); coarser levels their

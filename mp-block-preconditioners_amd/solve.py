@@ -585,8 +585,10 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
     target = tol * normr if normr != 0.0 else tol
     it = 0
     w = torch.empty_like(b)
-    V = torch.zeros(m + 1, n, **f64)
-    Z = torch.zeros(m, n, **f64)
+    # the basis and the preconditioned directions are only read in the rows already written (dots, update and lincomb
+    # take the first j + 1 / k rows): left uninitialised -- two (m + 1) x n memsets (7.6 GB at 1024^2) saved
+    V = torch.empty(m + 1, n, **f64)
+    Z = torch.empty(m, n, **f64)
     vb = torch.zeros(m + 1, **f64)       # max |V[i]| bounds (identical on every rank)
     # the iteration's scalars (h column, the norm's fold sums, the norm) reach the host through one pinned copy
     # and an event: the next iteration's M and A applies are queued before the host waits, so the host's
@@ -602,7 +604,6 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
 
     while it < maxiter:
         beta = normr
-        V.zero_()
         H = np.zeros((m + 1, m))
         cs, sn = np.zeros(m), np.zeros(m)
         g = np.zeros(m + 1)

@@ -265,6 +265,39 @@ def test_matrix_free_galerkin_level1(n):
     assert torch.equal(out, got)
 
 
+@pytest.mark.parametrize("n", [64, 72, 80, 100, 128, 256])
+def test_matrix_free_galerkin_level1_pressure(n):
+    """The pressure hierarchy's level 1 as R_0 (Gt_G (P_0 x)) (mpbp_set_mg_galerkin_mf_p): within 1e-10 of its stored
+    Galerkin matrix, and the one-launch k_gal1p bit-identical to the three launches it fuses."""
+    mp = _mp()
+    from mp_block_preconditioners_amd._lib import check, lib
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    fast = mp.ApproxSchurPreconditioner(F, D, G, numerics="fast", inner_F=mp.InnerSolver("chebyshev", 4),
+                                        inner_P=mp.InnerSolver("mg", 1))
+    assert len(fast.mg_P.sizes) > 2
+    v = torch.randn(fast.shape[0], dtype=torch.float64, device="cuda",
+                    generator=torch.Generator(device="cuda").manual_seed(n + 1))
+    try:
+        check(lib().mpbp_set_mg_galerkin_mf_p(0))
+        stored = fast.apply(v).clone()
+        check(lib().mpbp_set_mg_galerkin_mf_p(1))
+        check(lib().mpbp_set_mg_galerkin_mf(1))
+        three = fast.apply(v).clone()
+        check(lib().mpbp_set_mg_galerkin_mf(2))
+        one = fast.apply(v).clone()
+    finally:
+        check(lib().mpbp_set_mg_galerkin_mf(2))
+        check(lib().mpbp_set_mg_galerkin_mf_p(1))
+    assert 0.0 < rel_inf(three.cpu().numpy(), stored.cpu().numpy()) <= 1e-10
+    assert torch.equal(one, three), float((one - three).abs().max())
+    out = torch.empty_like(v)
+    g = fast.capture(v, out)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, one)
+
+
 @pytest.mark.parametrize("n", [5, 16, 100, 256])
 def test_q13_symmetric_half(n):
     """Tolerance mode reads Gt_F_G's diamond upper half (mpbp_set_q13_sym, default 1): the apply stays within 1e-13

@@ -15,6 +15,7 @@
 #   probe        tools/capture_probe.py 256 1024 (hipGraph capture of the partitioned apply); probe:N1,N2 sizes
 #   prof         rocprofv3 --kernel-trace --stats of bench.py
 #   profmg       the same with the headline apply's inner solves one multigrid V-cycle each (mg:1 / mg:1)
+#   profsolve    the same over tools/solve_prof.py (FGMRES to 1e-8 on 1024^2, mg:1 inner solves; args in $SOLVE_ARGS)
 #   pmc          FETCH_SIZE / WRITE_SIZE passes: the apply's F sweeps and the A SpMV
 #   sq           SQ counter passes over the F sweep (tools/pmc_sweep.py) and the CSR SpMV (tools/spmv_ab.py)
 #   spmvattr     FETCH_SIZE / WRITE_SIZE of the A SpMV against the same matrix with its x gathers in a 32 KB window
@@ -70,6 +71,9 @@ step() {
               python "$ROOTD/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-solve --no-mg --no-spmv \
               --inner-f mg:1 --inner-p mg:1 &&
             python tools/prof_summary.py "$OUT/prof_mg/run_kernel_trace.csv" > "$OUT/prof_mg_summary.md" 2>&1 ;;
+    profsolve) prof prof_solve 300 --kernel-trace --stats --output-format csv -d "$ROOTD/$OUT/prof_solve" -o run -- \
+                 python "$ROOTD/tools/solve_prof.py" --reps 2 $SOLVE_ARGS &&
+               python tools/prof_summary.py "$OUT/prof_solve/run_kernel_trace.csv" > "$OUT/prof_solve_summary.md" 2>&1 ;;
     pmc) for C in FETCH_SIZE WRITE_SIZE; do
            prof "pmc_apply_$C" 150 --pmc $C --output-format csv -d "$ROOTD/$OUT/pmc_apply_$C" -o pmc -- \
              python "$ROOTD/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-spmv --no-graph --no-solve || return 1
