@@ -576,6 +576,15 @@ int mpbp_gs_update(const double* V, int64_t ld, int32_t k, const double* h, cons
 int mpbp_rdot(const double* V, int64_t ld, int32_t k, const double* w, int64_t n, int64_t n_total,
               const double* bound_v, const double* bound_w, double* part, double* acc, void* stream);
 int64_t mpbp_rdot_part_size(int64_t n, int32_t k);
+/* CGS2's first update and second projection in one pass over V (FGMRES, solve.py): w_out = w - V^T h (mpbp_gs_update's
+ * bits; w_out may be w) and acc[3i + f] = the exact fold sums of V[i] . w_out (mpbp_rdot's, finished by
+ * mpbp_rdot_finish), with the fold extractors from the a-priori bound (bound_w[0] + sum_i bound_v[i] |h[i]|)(1 + 2^-40)
+ * on |w_out| (bound_w[0] = max |w| over all ranks) -- identical on every rank, so the sums stay reproducible.
+ * 1 <= k <= 256; part: mpbp_rdot_part_size(n, k) doubles.  Replaces the reference's pyamg fgmres orthogonalisation
+ * step (solve.py:285; pyamg is absent, see oracle/krylov_oracle.py). */
+int mpbp_gs_update_rdot(const double* V, int64_t ld, int32_t k, const double* h, const double* w, int64_t n,
+                        int64_t n_total, const double* bound_v, const double* bound_w, double* w_out, double* part,
+                        double* acc, void* stream);
 int mpbp_rdot_finish(int32_t k, const double* acc, double* h, void* stream);
 /* amax[0] = max_e |x[e]| (device scalar, overwritten; NaN if x holds one). */
 int mpbp_absmax(const double* x, int64_t n, double* amax, void* stream);

@@ -199,6 +199,7 @@ _SIGNATURES = {
     "mpbp_gs_update": ([_P, c_int64, c_int32, _P, _P, c_int64, _P, _P], c_int),
     "mpbp_rdot": ([_P, c_int64, c_int32, _P, c_int64, c_int64, _P, _P, _P, _P, _P], c_int),
     "mpbp_rdot_part_size": ([c_int64, c_int32], c_int64),
+    "mpbp_gs_update_rdot": ([_P, c_int64, c_int32, _P, _P, c_int64, c_int64, _P, _P, _P, _P, _P, _P], c_int),
     "mpbp_rdot_finish": ([c_int32, _P, _P, _P], c_int),
     "mpbp_absmax": ([_P, c_int64, _P, _P], c_int),
 }

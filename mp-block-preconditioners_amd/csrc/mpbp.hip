@@ -4617,6 +4617,95 @@ __global__ void __launch_bounds__(kBlock) k_rdot(const double* __restrict__ V, i
         part[c * (3 * (int64_t)k) + 3 * i0 + threadIdx.x] = a;
     }
 }
+// CGS2's first update and second projection in one kernel: wo = w - V^T h (k_gs_update's operations, same bits) and
+// the exact fold sums of V[i] . wo (k_rdot's pre-rounding).  The extractors cannot wait for max|wo|, so they come from
+// the a-priori bound B = (max|w| + sum_i bound_v[i] |h[i]|) (1 + 2^-40) >= max|wo| -- the same in every workgroup and
+// on every rank (its inputs are global), so the fold sums stay exact and reproducible; the looser bound costs accuracy
+// only below 2^-58 of it.  A workgroup updates its chunk (16 elements per thread, kept in LDS), then forms the
+// products vector group by vector group as k_rdot does, re-reading the chunk's basis entries it has just streamed
+// (from the L2 / MALL while they last) instead of a second full pass -- and wo is never re-read.
+__global__ void __launch_bounds__(kBlock) k_gs_update_rdot(const double* __restrict__ V, int64_t ld, int k,
+                                                           const double* __restrict__ h, const double* w, int64_t n,
+                                                           int64_t ntot, const double* __restrict__ bound_v,
+                                                           const double* __restrict__ bound_w, double* wo,
+                                                           double* __restrict__ part) {
+    __shared__ double hs[256];
+    __shared__ double sg[256 * kRdFolds];
+    __shared__ double red[kBlock / 64][kRdVec * kRdFolds];
+    __shared__ double bnd;
+    const int tid = threadIdx.x, lane = tid & 63, wq = tid >> 6;
+    for (int i = tid; i < k; i += kBlock) hs[i] = h[i];
+    __syncthreads();
+    if (tid == 0) {
+        double b = bound_w[0];
+        for (int i = 0; i < k; ++i) b += bound_v[i] * fabs(hs[i]);
+        bnd = b * (1.0 + 0x1p-40);
+    }
+    __syncthreads();
+    for (int i = tid; i < k; i += kBlock) rd_sigmas(bound_v[i] * bnd, ntot, sg + kRdFolds * i);
+    const int64_t c = blockIdx.x;
+    __shared__ double w1[kGsChunk];   // the updated chunk, [u][thread]
+    for (int u = 0; u < kGsPer; ++u) {   // the update, element by element (k_gs_update's order of operations)
+        const int64_t e = c * kGsChunk + (int64_t)u * kBlock + tid;
+        const bool ok = e < n;
+        const int64_t ee = ok ? e : 0;
+        double a = 0.0;
+        int i = 0;
+        for (; i + 8 <= k; i += 8) {
+            double v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = V[(int64_t)(i + q) * ld + ee];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) a += v[q] * hs[i + q];
+        }
+        for (; i < k; ++i) a += V[(int64_t)i * ld + ee] * hs[i];
+        const double r = ok ? w[ee] - a : 0.0;
+        w1[u * kBlock + tid] = r;
+        if (ok) wo[ee] = r;
+    }
+    __syncthreads();   // (sg; each thread reads back only its own w1 entries)
+    for (int i0 = 0; i0 < k; i0 += kRdVec) {   // the products, kRdVec basis vectors at a time (k_rdot's folds)
+        const int nv = min(kRdVec, k - i0);
+        double acc[kRdVec][kRdFolds], sig[kRdVec][kRdFolds];
+#pragma unroll
+        for (int v = 0; v < kRdVec; ++v)
+#pragma unroll
+            for (int f = 0; f < kRdFolds; ++f) {
+                acc[v][f] = 0.0;
+                sig[v][f] = v < nv ? sg[kRdFolds * (i0 + v) + f] : 0.0;
+            }
+        for (int u = 0; u < kGsPer; u += kGsBatch) {
+            double vv[kRdVec][kGsBatch];
+#pragma unroll
+            for (int q = 0; q < kGsBatch; ++q) {
+                const int64_t e = c * kGsChunk + (int64_t)(u + q) * kBlock + tid;
+                const int64_t ee = e < n ? e : 0;
+#pragma unroll
+                for (int v = 0; v < kRdVec; ++v) vv[v][q] = v < nv ? V[(int64_t)(i0 + v) * ld + ee] : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < kGsBatch; ++q)
+#pragma unroll
+                for (int v = 0; v < kRdVec; ++v) rd_fold(vv[v][q] * w1[(u + q) * kBlock + tid], sig[v], acc[v]);
+        }
+#pragma unroll
+        for (int v = 0; v < kRdVec; ++v)
+#pragma unroll
+            for (int f = 0; f < kRdFolds; ++f) {
+                double x = acc[v][f];
+                for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+                if (lane == 0) red[wq][kRdFolds * v + f] = x;
+            }
+        __syncthreads();
+        if (tid < kRdFolds * nv) {   // the group's partials over the 4 waves (exact)
+            double t = 0.0;
+#pragma unroll
+            for (int q = 0; q < kBlock / 64; ++q) t += red[q][tid];
+            part[c * (kRdFolds * (int64_t)k) + kRdFolds * i0 + tid] = t;
+        }
+        __syncthreads();
+    }
+}
 // acc[j] = sum over chunks of part[c][j] (exact), one workgroup per fold sum
 __global__ void __launch_bounds__(kBlock) k_rdot_sum(const double* part, int64_t nchunks, int k3, double* acc) {
     const int j = blockIdx.x;
@@ -4703,6 +4792,21 @@ int mpbp_rdot(const double* V, int64_t ld, int32_t k, const double* w, int64_t n
     const int64_t nchunks = (n + kGsChunk - 1) / kGsChunk;
     const dim3 grid((unsigned)nchunks, (unsigned)((k + kRdVec - 1) / kRdVec));
     k_rdot<<<grid, kBlock, 0, st>>>(V, ld, k, w, n, n_total, bound_v, bound_w, part);
+    MPBP_HIP(hipGetLastError());
+    k_rdot_sum<<<3 * k, kBlock, 0, st>>>(part, nchunks, 3 * k, acc);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int mpbp_gs_update_rdot(const double* V, int64_t ld, int32_t k, const double* h, const double* w, int64_t n,
+                        int64_t n_total, const double* bound_v, const double* bound_w, double* w_out, double* part,
+                        double* acc, void* stream) {
+    if (!V || !w || !h || !w_out || !bound_v || !bound_w || !part || !acc || k < 1 || k > 256 || n < 1 || ld < n ||
+        n_total < n)
+        return set_error(MPBP_ERR_ARG, "gs_update_rdot: bad args (1 <= k <= 256, ld >= n >= 1, n_total >= n)");
+    const hipStream_t st = as_stream(stream);
+    const int64_t nchunks = (n + kGsChunk - 1) / kGsChunk;
+    k_gs_update_rdot<<<(unsigned)nchunks, kBlock, 0, st>>>(V, ld, k, h, w, n, n_total, bound_v, bound_w, w_out, part);
     MPBP_HIP(hipGetLastError());
     k_rdot_sum<<<3 * k, kBlock, 0, st>>>(part, nchunks, 3 * k, acc);
     MPBP_HIP(hipGetLastError());

@@ -466,6 +466,16 @@ class KrylovKernels:
         check(lib().mpbp_rdot_finish(k, ptr(self.acc), ptr(self.h), stream_handle()))
         return self.h[:k]
 
+    def update_dots(self, V, ld, k, h, w, vb, wb) -> torch.Tensor:
+        """CGS2's first update and second projection in one pass over V[:k] (k <= 256): w <- w - V[:k]^T h in place
+        (``update``'s bits), then h2 = V[:k] w, its fold extractors from the a-priori bound wb[0] + sum vb |h| (wb[0]:
+        max |w| before the update, over every rank) -- reproducible over any row partition like ``dots``."""
+        check(lib().mpbp_gs_update_rdot(ptr(V), ld, k, ptr(h), ptr(w), self.n, self.n_total, ptr(vb), ptr(wb), ptr(w),
+                                         ptr(self.part), ptr(self.acc), stream_handle()))
+        self._reduce(self.acc[: 3 * k], "sum")
+        check(lib().mpbp_rdot_finish(k, ptr(self.acc), ptr(self.h), stream_handle()))
+        return self.h[:k]
+
     def update(self, V, ld, k, h, w, out):
         """out = w - V[:k]^T h (out may be w), the basis rows in chunks of 256 (a fixed order)."""
         src = w
@@ -499,7 +509,7 @@ _VB_SLACK = 1.0 + 2.0 ** -50   # |fl(w / s)| <= fl(max|w| / s) (1 + 2^-50): the 
 
 
 def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=None, residuals=None,
-           capture_M=True, group=None, kernels=None):
+           capture_M=True, group=None, kernels=None, fused_cgs2=False):
     """Flexible GMRES with right preconditioning, all vectors in HBM.
 
     Same call shape as pyamg.krylov.fgmres (solve.py:207, 237, 285): convergence when the
@@ -514,6 +524,10 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
     group: the process group of a row partition -- b, x0 and the vectors A and M take and return are the rank's
     owned rows (DistributedMatrix, DistributedSchurPreconditioner); the iterates are bit-identical to the one-GPU
     solve's rows.  kernels: a KrylovKernels-compatible object (default: libmpbp's).
+    fused_cgs2: CGS2's first update and second projection in one kernel (``update_dots``; the second projection's fold
+    extractors from an a-priori bound on the updated vector), meant to save one of the four passes over the basis per
+    iteration.  Off by default: its re-read of the chunk's basis entries misses the caches at 1024^2 and it measured no
+    faster; False: the two projections apart (max |w| measured before each).
     capture_M: an ApproxSchurPreconditioner M (or a partitioned one over the in-order RCCL halo) is captured once into
     a hipGraph and replayed per iteration (its launches -- hundreds with multigrid inner solves -- then cost one graph
     launch; the iteration's host work never starves the GPU); same results as eager applies.
@@ -560,6 +574,7 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
         except NotImplementedError:   # e.g. a partitioned apply over the host-staged (gloo) halo: eager
             pass
     K = kernels if kernels is not None else KrylovKernels(n, m + 1, b.device, group)
+    fused = fused_cgs2 and hasattr(K, "update_dots")
     f64 = dict(dtype=b.dtype, device=b.device)
     x = torch.zeros_like(b) if x0 is None else (
         x0.clone() if isinstance(x0, torch.Tensor) else torch.from_numpy(np.asarray(x0, dtype=np.float64)).to(b.device))
@@ -614,11 +629,20 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
         head(0)
         for j in range(m):
             hs = None
-            for _ in range(2):        # CGS2: h = V w, w -= V^T h, twice
+            if fused and j + 1 <= 256:
+                # CGS2 in three passes over the basis instead of four: h1 = V w; (w -= V^T h1, h2 = V w) in one pass;
+                # w -= V^T h2
                 K.amax(w, bnd[1:2])
-                h = K.dots(V, n, j + 1, w, vb, bnd[1:2])
+                hs = K.dots(V, n, j + 1, w, vb, bnd[1:2]).clone()
+                h = K.update_dots(V, n, j + 1, hs, w, vb, bnd[1:2])
                 K.update(V, n, j + 1, h, w, w)
-                hs = h.clone() if hs is None else hs + h
+                hs = hs + h
+            else:
+                for _ in range(2):        # CGS2: h = V w, w -= V^T h, twice
+                    K.amax(w, bnd[1:2])
+                    h = K.dots(V, n, j + 1, w, vb, bnd[1:2])
+                    K.update(V, n, j + 1, h, w, w)
+                    hs = h.clone() if hs is None else hs + h
             K.amax(w, bnd[1:2])
             a = K.fold_sums(w, n, 1, w, bnd[1:2], bnd[1:2])
             hn_d = torch.sqrt((a[0:1] + a[1:2]) + a[2:3])    # _finish, then the norm, on the device

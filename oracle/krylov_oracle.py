@@ -8,7 +8,9 @@ Arnoldi with Givens rotations over dot products and axpys.  mp-block-preconditio
   sums of each fold are exact), 3 folds, extractor exponents from a bound on the terms;
 * ``mpbp_gs_update`` -- w - V^T h with the basis vectors added in order;
 
-restated here in numpy: ``rd_sigmas`` / ``rdot_folds`` / ``rdot`` / ``gs_update``.  Because every fold sum is exact,
+* ``mpbp_gs_update_rdot`` -- CGS2's first update and second projection fused, the extractors from an a-priori bound;
+
+restated here in numpy: ``rd_sigmas`` / ``rdot_folds`` / ``rdot`` / ``gs_update`` / ``gs_update_rdot``.  Because every fold sum is exact,
 numpy's (pairwise) sum gives the same bits as the GPU's tree of partial sums, whatever the split of the vector.
 ``TorchKrylov`` has the KrylovKernels interface over CPU torch tensors (and a gloo group), so tests can drive the
 product's fgmres host logic -- the distributed reductions, bounds, Givens rotations -- on the CPU.
@@ -88,6 +90,21 @@ def gs_update(V, k, h, w) -> np.ndarray:
     return w - a
 
 
+def update_bound(bw: float, bv, h, k: int) -> float:
+    """The a-priori bound on |w - V^T h| the fused CGS2 pass takes its extractors from (mpbp.hip k_gs_update_rdot):
+    (max|w| + sum_i bv[i] |h[i]|, added in order) (1 + 2^-40)."""
+    b = float(bw)
+    for i in range(k):
+        b = b + float(bv[i]) * abs(float(h[i]))
+    return b * (1.0 + 2.0 ** -40)
+
+
+def gs_update_rdot(V, k, h, w, ntot, bv, bw):
+    """(w - V^T h, the fold sums of V[i] . (w - V^T h) under update_bound's extractors) (mpbp_gs_update_rdot)."""
+    r = gs_update(V, k, h, w)
+    return r, rdot_folds(np.atleast_2d(V)[:k], r, ntot, bv, update_bound(bw, bv, h, k))
+
+
 class TorchKrylov:
     """KrylovKernels' interface (solve.py) on CPU torch float64 tensors, optionally over a gloo group."""
 
@@ -133,3 +150,13 @@ class TorchKrylov:
             r = gs_update(Vm[i0:i0 + kc], kc, h.numpy()[i0:i0 + kc], r)
         out.copy_(torch.from_numpy(r))
         return out
+
+    def update_dots(self, V, ld, k, h, w, vb, wb):
+        """w <- w - V[:k]^T h in place, then h2 = V[:k] w under the a-priori bound (KrylovKernels.update_dots)."""
+        Vm = V.reshape(-1)[: k * ld].view(k, ld)[:, : self.n].numpy() if V.dim() == 1 else V[:k, : self.n].numpy()
+        r, a = gs_update_rdot(Vm, k, h.numpy()[:k], w.numpy()[: self.n], self.n_total, vb.numpy()[:k], float(wb[0]))
+        w.copy_(torch.from_numpy(r))
+        self.acc[: 3 * k] = torch.from_numpy(a)
+        self._reduce(self.acc[: 3 * k], "sum")
+        self.h[:k] = torch.from_numpy(finish(self.acc[: 3 * k].numpy()))
+        return self.h[:k]

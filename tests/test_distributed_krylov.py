@@ -22,7 +22,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, maxiter, restrt, outdir, errfile):
+def _worker(rank, world, port, n, maxiter, restrt, outdir, errfile, fused=False):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -76,7 +76,7 @@ def _worker(rank, world, port, n, maxiter, restrt, outdir, errfile):
         hist = []
         K = TorchKrylov(own, (restrt or maxiter) + 1, group=group if world > 1 else None)
         x, info = fgmres(Aop, b, M=Mop, tol=1e-12, maxiter=maxiter, restrt=restrt, residuals=hist,
-                         group=group if world > 1 else None, kernels=K)
+                         group=group if world > 1 else None, kernels=K, fused_cgs2=fused)
         np.save(os.path.join(outdir, f"x_{world}_{rank}.npy"), x.numpy())
         np.save(os.path.join(outdir, f"rows_{world}_{rank}.npy"), rows5)
         np.save(os.path.join(outdir, f"hist_{world}_{rank}.npy"), np.asarray(hist))
@@ -88,9 +88,10 @@ def _worker(rank, world, port, n, maxiter, restrt, outdir, errfile):
         raise
 
 
-def _run(world, n, maxiter, restrt, outdir, errfile):
+def _run(world, n, maxiter, restrt, outdir, errfile, fused=False):
     try:
-        mp.spawn(_worker, args=(world, _free_port(), n, maxiter, restrt, outdir, errfile), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), n, maxiter, restrt, outdir, errfile, fused), nprocs=world,
+                 join=True)
     except Exception:
         msg = open(errfile).read() if os.path.exists(errfile) else ""
         pytest.fail(f"distributed worker failed:\n{msg}")
@@ -103,14 +104,15 @@ def _run(world, n, maxiter, restrt, outdir, errfile):
     return x, hists[0]
 
 
-@pytest.mark.parametrize("n,maxiter,restrt", [(12, 25, None), (13, 30, 12)])
-def test_distributed_fgmres_matches_one_rank(n, maxiter, restrt, tmp_path, oracle_built):
+@pytest.mark.parametrize("n,maxiter,restrt,fused", [(12, 25, None, False), (13, 30, 12, False), (12, 25, None, True)])
+def test_distributed_fgmres_matches_one_rank(n, maxiter, restrt, fused, tmp_path, oracle_built):
     """FGMRES with the partitioned A and the partitioned preconditioner on 2 and 3 gloo ranks: the residual history
-    and the iterate are bit-identical to the one-rank run (reproducible inner products), restarts included."""
+    and the iterate are bit-identical to the one-rank run (reproducible inner products), restarts included -- also with
+    CGS2's first update and second projection fused (update_dots: the extractor bound from global quantities)."""
     errfile = str(tmp_path / "err.txt")
-    x1, h1 = _run(1, n, maxiter, restrt, str(tmp_path), errfile)
+    x1, h1 = _run(1, n, maxiter, restrt, str(tmp_path), errfile, fused)
     assert len(h1) == maxiter + 1 and h1[-1] < h1[0]
     for world in (2, 3):
-        xw, hw = _run(world, n, maxiter, restrt, str(tmp_path), errfile)
+        xw, hw = _run(world, n, maxiter, restrt, str(tmp_path), errfile, fused)
         assert np.array_equal(hw, h1), (world, np.max(np.abs(hw - h1)))
         assert np.array_equal(xw.view(np.uint64), x1.view(np.uint64)), world

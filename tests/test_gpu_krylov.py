@@ -122,3 +122,56 @@ def test_fgmres_is_deterministic():
         assert info == 0
         runs.append((x.clone(), list(hist)))
     assert torch.equal(runs[0][0], runs[1][0]) and runs[0][1] == runs[1][1]
+
+
+@pytest.mark.parametrize("k,n", [(1, 1), (3, 1000), (8, 4097), (31, 70_001), (32, 4096), (33, 100_003), (40, 5000),
+                                 (151, 20_000), (256, 3000), (12, 5_242_880)])
+def test_gs_update_rdot_matches_oracle_bit_for_bit(k, n):
+    """mpbp_gs_update_rdot (CGS2's first update and second projection in one pass) against
+    oracle/krylov_oracle.py's gs_update_rdot: the updated vector bit-identical to mpbp_gs_update's, the fold sums to
+    the restatement's under the a-priori bound -- with basis counts below, at and above the 32 kept in registers."""
+    from oracle.krylov_oracle import finish, gs_update_rdot
+    check, lib, ptr, sh = _lib()
+    rng = np.random.default_rng(k * 11 + n)
+    V = rng.standard_normal((k, n)) / np.sqrt(n)
+    w = rng.standard_normal(n)
+    h = V @ w
+    vb = np.max(np.abs(V), axis=1) * (1.0 + 2.0 ** -50)
+    wb = float(np.max(np.abs(w)))
+    dV, dw = torch.from_numpy(V).cuda(), torch.from_numpy(w).cuda()
+    dh, dvb = torch.from_numpy(h).cuda(), torch.from_numpy(vb).cuda()
+    dwb = torch.tensor([wb], dtype=torch.float64, device="cuda")
+    ref_w, ref_acc = gs_update_rdot(V, k, h, w, n, vb, wb)
+    upd = torch.empty_like(dw)
+    check(lib().mpbp_gs_update(ptr(dV), n, k, ptr(dh), ptr(dw), n, ptr(upd), sh()))
+    part = torch.empty(max(1, int(lib().mpbp_rdot_part_size(n, k))), dtype=torch.float64, device="cuda")
+    acc = torch.empty(3 * k, dtype=torch.float64, device="cuda")
+    check(lib().mpbp_gs_update_rdot(ptr(dV), n, k, ptr(dh), ptr(dw), n, n, ptr(dvb), ptr(dwb), ptr(dw), ptr(part),
+                                    ptr(acc), sh()))
+    assert torch.equal(dw, upd)                                         # in place, mpbp_gs_update's bits
+    assert np.array_equal(dw.cpu().numpy().view(np.uint64), ref_w.view(np.uint64))
+    assert np.array_equal(acc.cpu().numpy().view(np.uint64), ref_acc.view(np.uint64))
+    h2 = finish(ref_acc)
+    assert np.max(np.abs(h2 - V @ ref_w)) <= 1e-12 * np.max(vb) * wb   # the second projection itself
+
+
+def test_fgmres_fused_cgs2_matches_two_pass():
+    """FGMRES with the fused CGS2 pass (fused_cgs2=True) and with the two projections apart: same convergence on the
+    reference's problem (the second projection's bits differ only through its looser extractor bound)."""
+    import mp_block_preconditioners_amd as mp
+    n = 64
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("mg", 1), inner_P=mp.InnerSolver("mg", 1))
+    _, b = mp.manufactured_problem(n, 1.0, -1.0, 1.0, 100.0, 1.0)
+    bd = torch.from_numpy(b).cuda()
+    out = {}
+    for fused in (True, False):
+        hist = []
+        x, info = mp.fgmres(A, bd, M=pc, tol=1e-10, maxiter=100, residuals=hist, fused_cgs2=fused)
+        assert info == 0
+        out[fused] = (x, hist)
+    (x1, h1), (x2, h2) = out[True], out[False]
+    assert abs(len(h1) - len(h2)) <= 1
+    assert np.allclose(h1[: min(len(h1), len(h2))], h2[: min(len(h1), len(h2))], rtol=1e-6, atol=0)
+    assert float((x1 - x2).abs().max()) <= 1e-8 * float(x2.abs().max())

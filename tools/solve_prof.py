@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--inner", default="mg:1")
     ap.add_argument("--numerics", default="fast")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--cgs2", default="fused,apart", help="FGMRES orthogonalisations to time, in order")
     args = ap.parse_args()
     import torch
     import mp_block_preconditioners_amd as mp
@@ -49,15 +50,15 @@ def main():
         A.matvec(v)
     torch.cuda.synchronize()
     a_ms = (time.perf_counter() - t0) / 10 * 1e3
-    for r in range(args.reps):
+    for r, mode in ((r, mode) for mode in args.cgs2.split(",") for r in range(args.reps)):
         torch.cuda.empty_cache()
         hist = []
         t0 = time.perf_counter()
-        x, info = mp.fgmres(A, bd, M=M, tol=1e-8, maxiter=150, residuals=hist)
+        x, info = mp.fgmres(A, bd, M=M, tol=1e-8, maxiter=150, residuals=hist, fused_cgs2=mode == "fused")
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         it = len(hist) - 1
-        print(json.dumps({"rep": r, "seconds": el, "iterations": it, "converged": info == 0, "apply_ms": apply_ms,
+        print(json.dumps({"cgs2": mode, "rep": r, "seconds": el, "iterations": it, "converged": info == 0, "apply_ms": apply_ms,
                           "A_ms": a_ms, "other_ms_per_iteration": (el * 1e3 - it * (apply_ms + a_ms)) / max(it, 1)}),
               flush=True)
         del x
