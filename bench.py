@@ -148,8 +148,9 @@ def main():
     ap.add_argument("--f-solve", type=int, default=None,
                     help="fast numerics: 1 (default) runs each F solve of 3 or 4 updates as one k_fsolve launch, "
                          "0 as k_ftile launches")
-    ap.add_argument("--solve-numerics", default="exact", choices=["fast", "exact"],
-                    help="N > 1: numerics of the partitioned multigrid apply and the distributed FGMRES section")
+    ap.add_argument("--solve-numerics", default=None, choices=["fast", "exact"],
+                    help="N > 1: numerics of the partitioned multigrid apply and the distributed FGMRES section "
+                         "(default: --numerics)")
     ap.add_argument("--q13-sym", type=int, default=None,
                     help="fast numerics: 1 (default) reads Gt_F_G's diamond upper half only (symmetric product); 0: all 13")
     ap.add_argument("--gtg-drhs", type=int, default=None,
@@ -503,9 +504,12 @@ def main():
             "roofline_csr_spmv": None if spmv is None else {
                 "bound": "hbm", "achieved": spmv["csr_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": spmv["csr_gbs"] / HBM_PEAK_GBS, "traffic": spmv_traffic,
-                "kernel": "k_csr_wave<EpiStore> (A u, 5N rows, CSR)", "bytes_per_launch": spmv["csr_bytes"],
-                "avg_launch_us": spmv["csr_us"],
+                "kernel": "k_csr_wave<EpiStore> (A u, 5N rows, CSR; LDS-DMA staging)",
+                "bytes_per_launch": spmv["csr_bytes"], "avg_launch_us": spmv["csr_us"],
                 "back_to_back_us": spmv["csr_us_graph"], "frac_back_to_back": spmv["csr_gbs_graph"] / HBM_PEAK_GBS,
+                "same_run_stream": spmv.get("calibration"),
+                "frac_of_measured_stream": (spmv["csr_gbs"] / spmv["calibration"]["spmv_shape"]["gbs"]
+                                            if spmv.get("calibration") else None),
                 "timing": spmv.get("timing", "") + " (one kernel per matvec)", "events": EVENT_NOTE},
             "mg_apply": mg_apply,
             "host_buffer_matvec": host_io,
@@ -553,10 +557,10 @@ def partitioned_solver_section(args, n, rank, world, dist, torch, backend):
     import mp_block_preconditioners_amd as mp
     from mp_block_preconditioners_amd.distributed import DistributedMatrix, DistributedSchurPreconditioner
     scale = n * n / float(1024 * 1024)
-    # the multigrid solve runs the exact numerics: the partition's per-operator exchange schedule starts its smoothing
-    # from the stored diagonal (x0 = c2 (b / diag)) where the one-GPU fast hierarchy recomputes the reciprocal, so only
-    # the exact mode makes the residual histories comparable bit for bit (--solve-numerics overrides)
-    snum = args.solve_numerics
+    # the headline's numerics (--solve-numerics overrides): the partition's per-operator schedule starts its fast F
+    # smoothing from the fast reciprocal diagonals as one GPU does (k_f_fast_init), so the residual histories are
+    # comparable bit for bit in both numerics
+    snum = args.solve_numerics or args.numerics
     mg1 = dict(inner_F=mp.InnerSolver("mg", 1), inner_P=mp.InnerSolver("mg", 1))
     out = {}
     t0 = time.perf_counter()
@@ -610,9 +614,9 @@ def partitioned_solver_section(args, n, rank, world, dist, torch, backend):
     el = float(t.item())
     sd = {"inner": "mg:1 / mg:1", "tol": 1e-8, "maxiter": 150, "iterations": len(hist) - 1, "converged": info == 0,
           "seconds": el, "setup_seconds": setup, "rel_residual": hist[-1] / hist[0] if hist and hist[0] else None,
-          "halo": Md.halo_impl, "communicators_per_rank": (Md._rccl.comm_refs if Md._rccl is not None else 0),
+          "halo": Md.halo_impl, "preconditioner_comm_refs": (Md._rccl.comm_refs if Md._rccl is not None else 0),
           "f_numerics": snum}
-    shared = None if Md._rccl is None or dA._rccl is None else bool(Md._rccl.comm == dA._rccl.comm)
+    own_comm = None if Md._rccl is None or dA._rccl is None else bool(Md._rccl.comm != dA._rccl.comm)
     dA.close()
     Md.close()
     del dA, Md, x
@@ -622,17 +626,13 @@ def partitioned_solver_section(args, n, rank, world, dist, torch, backend):
         t0 = time.perf_counter()
         bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
         A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
-        pc1 = mp.ApproxSchurPreconditioner(F, D, G, numerics=snum, **mg1)
-        h1 = []
         # the partitioned hierarchy applies its level 1 from the stored Galerkin product; a one-GPU fast hierarchy
-        # defaults to R0 (F (P0 x)) (the same operator, other roundings): compare against the stored form
-        L.check(L.lib().mpbp_set_mg_galerkin_mf(0))
-        L.check(L.lib().mpbp_set_q13_sym(0))
-        try:
-            mp.fgmres(A, torch.from_numpy(b).cuda(), M=pc1, tol=1e-8, maxiter=150, residuals=h1)
-        finally:
-            L.check(L.lib().mpbp_set_mg_galerkin_mf(2))
-            L.check(L.lib().mpbp_set_q13_sym(1))
+        # defaults to R0 (F (P0 x)) (the same operator, other roundings): compare against the stored form, with
+        # Gt_F_G's full rows as the partition multiplies them
+        pc1 = mp.ApproxSchurPreconditioner(F, D, G, numerics=snum, **mg1,
+                                           kernel_opts={"mg_galerkin_mf": 0, "mg_galerkin_mf_p": 0, "q13_sym": 0})
+        h1 = []
+        mp.fgmres(A, torch.from_numpy(b).cuda(), M=pc1, tol=1e-8, maxiter=150, residuals=h1)
         same[0] = 1 if np.array_equal(np.asarray(h1), np.asarray(hist)) else 0
         sd["single_gpu_iterations"] = len(h1) - 1
         sd["single_gpu_check_seconds"] = time.perf_counter() - t0
@@ -643,8 +643,8 @@ def partitioned_solver_section(args, n, rank, world, dist, torch, backend):
         sd["bit_exact_vs_single_gpu"] = bool(same.item())
         sd["check"] = ("the residual history (every iteration's ||r||) equals the one-GPU FGMRES's bit for bit (one GPU "
                        "with multigrid level 1 from its stored Galerkin matrix and Gt_F_G's full rows, as the partition)")
-    if shared is not None:
-        sd["operator_and_preconditioner_share_one_communicator"] = shared
+    if own_comm is not None:   # A u's eager side-stream exchanges never share a communicator with graph-replayed ones
+        sd["operator_has_its_own_communicator"] = own_comm
     return {"mg_apply_partitioned": mg, "solve_distributed": sd}
 
 
@@ -668,17 +668,13 @@ def single_gpu_check(dpc, n, args, iF, iP, rank, dist, torch):
     t0 = time.perf_counter()
     bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
     _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    # (the partition multiplies Gt_F_G's full rows: the one-GPU twin does too, q13_sym = 0)
     pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, layout=args.layout, f_mode=args.f_mode,
-                                      pg_mode=args.pg_mode, numerics=args.numerics)
+                                      pg_mode=args.pg_mode, numerics=args.numerics, kernel_opts={"q13_sym": 0})
     del F, D, G
     vg = torch.from_numpy(np.random.default_rng(2048).standard_normal(pc.shape[0])).cuda()
     gids = torch.from_numpy(dpc.local_to_global_rows()).cuda()
-    from mp_block_preconditioners_amd._lib import check, lib
-    check(lib().mpbp_set_q13_sym(0))   # the partition multiplies Gt_F_G's full rows: the one-GPU twin does too
-    try:
-        ref = pc.apply(vg)[gids]
-    finally:
-        check(lib().mpbp_set_q13_sym(1))
+    ref = pc.apply(vg)[gids]
     got = dpc.apply(vg[gids].contiguous())
     torch.cuda.synchronize()
     same = torch.tensor([1 if torch.equal(got, ref) else 0], dtype=torch.int64, device="cuda")
@@ -774,7 +770,56 @@ def spmv_bench(A, gen, reps=20, replays=10, warm_replays=5):
         res.update({f"{name}_gbs": nbytes / s_launch / 1e9, f"{name}_us": s_launch * 1e6, f"{name}_bytes": nbytes,
                     f"{name}_us_graph": s * 1e6, f"{name}_gbs_graph": nbytes / s / 1e9,
                     f"{name}_us_eager": s_eager * 1e6})
+    res["calibration"] = hbm_calibration(csr_bytes, reps)
     return res
+
+
+def hbm_calibration(nbytes, reps=20):
+    """Same-run, same-size HBM reference rates for the CSR SpMV roofline (mpbp_hbm_stream, timed like the SpMV: a HIP
+    event pair around each of `reps` launches after 30 warm launches): `read` streams nbytes once in order; `spmv_shape`
+    moves the SpMV's own stream shape without its x gathers (per 64-row wave 9 KiB read in order + 512 B written), about
+    the same byte count.  frac_of_measured_stream = the SpMV's GB/s over spmv_shape's: what separates the kernel from
+    the box.  Plus the memory clock rocm-smi reports (None where it cannot be read)."""
+    import torch
+    from mp_block_preconditioners_amd._lib import check, lib, ptr, stream_handle
+    from mp_block_preconditioners_amd.solve import DeviceEvent
+    src = torch.empty(nbytes // 8 + 2048, dtype=torch.float64, device="cuda")
+    src.fill_(0.5)
+    nw = nbytes // (576 * 16)
+    dst = torch.empty(max(256, nw * 64), dtype=torch.float64, device="cuda")
+    out = {}
+    for name, mode, moved in (("read", 0, nbytes // 16 * 16), ("spmv_shape", 1, nw * (576 * 16 + 512))):
+        def launch():
+            check(lib().mpbp_hbm_stream(ptr(src), nbytes, mode, ptr(dst), stream_handle()))
+        for _ in range(30):
+            launch()
+        pairs = [(DeviceEvent(), DeviceEvent()) for _ in range(reps)]
+        for a, b in pairs:
+            a.record()
+            launch()
+            b.record()
+        torch.cuda.synchronize()
+        us = sum(a.elapsed_ms(b) for a, b in pairs) * 1e3 / reps
+        out[name] = {"bytes": moved, "avg_launch_us": us, "gbs": moved / us / 1e3, "frac_of_peak": moved / us / 1e3 / HBM_PEAK_GBS}
+    del src, dst
+    torch.cuda.empty_cache()
+    out["memory_clock"] = memory_clock()
+    return out
+
+
+def memory_clock():
+    """The current memory clock as rocm-smi prints it (MCLK), or None."""
+    import re
+    import subprocess
+    try:
+        txt = subprocess.run(["rocm-smi", "--showclocks"], capture_output=True, text=True, timeout=20).stdout
+    except (OSError, subprocess.SubprocessError):
+        return None
+    for line in txt.splitlines():
+        if "mclk" in line.lower():
+            m = re.search(r"\(([0-9.]+\s*[MG]hz)\)", line, re.I)
+            return m.group(1) if m else line.strip()
+    return None
 
 
 def mg_apply_bench(F, D, G, steps, warmup, gen, reps=20, numerics="exact"):

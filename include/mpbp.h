@@ -204,6 +204,8 @@ typedef void (*mpbp_halo_pair_fn)(void* ctx, double* xu_ext, double* xp_ext, voi
 /* All-gather of a row-partitioned vector into the whole field-major vector on every rank (on `stream`). */
 typedef void (*mpbp_gather_fn)(void* ctx, int32_t gather_kind, const double* x_owned, double* x_full, void* stream);
 
+struct mpbp_kernel_opts;   /* kernel choices: see "kernel choices" below */
+
 typedef struct mpbp_mg {
     int32_t nlevels;                 /* >= 2 */
     int32_t cycles;                  /* V-cycles per solve, from x = 0 */
@@ -229,6 +231,7 @@ typedef struct mpbp_mg {
     int32_t tr_n0;
     int32_t tr_ky[8];
     int32_t tr_kx[8];
+    const struct mpbp_kernel_opts* opts; /* optional: kernel choices of a standalone mpbp_mg_solve (NULL: defaults) */
 } mpbp_mg;
 
 /* The apply's operands.  On one GPU every matrix's columns index the full vector and the
@@ -288,6 +291,8 @@ typedef struct mpbp_schur_plan {
                                         launch, W never stored; bit-identical) */
     int32_t f_numerics;              /* MPBP_NUMERICS_EXACT (0, default) or MPBP_NUMERICS_FAST: the matrix-free F
                                         sweeps' rows (inner solves, multigrid level 0 smoothing and residuals) */
+    const struct mpbp_kernel_opts* opts; /* optional: this plan's kernel choices (NULL: the process defaults); they
+                                        also govern the plan's multigrid hierarchies inside the apply */
 } mpbp_schur_plan;
 
 const char* mpbp_version(void);
@@ -340,6 +345,9 @@ int mpbp_svl_spmv(const mpbp_svl* V, const mpbp_csr* A, int32_t mode, const doub
  * smoothing sweep, bit-identical to the CSR form. */
 int mpbp_svl_cheb_step(const mpbp_svl* V, const mpbp_csr* A, const double* x_in, const double* b, const double* diag,
                        double c1, double c2, double* d, const double* sub, double* x_out, void* stream);
+/* out[0] = max |Q(c, c + o) - Q(c + o, c)| over the diamond, out[1] = max |Q| (host doubles; synchronises the stream):
+ * whether tolerance mode may read the symmetric half (mpbp_kernel_opts.q13_sym) for this product.  Setup. */
+int mpbp_q13_asymmetry(int32_t n, const double* vals, double* out, void* stream);
 int mpbp_q13_spmv(int32_t n, const double* vals, int32_t mode, const double* x, const double* z, double* y,
                   void* stream);
 
@@ -370,6 +378,11 @@ int mpbp_spmv(const mpbp_csr* A, const mpbp_rowblocks* blocks, int32_t mode, con
  * relative infinity norm of mpbp_spmv's sequential sums, not bit-identical; deterministic run to run.  Fast for
  * stencil rows (64-row waves of 8, 10 or 12 entries from an even start); other waves take a plain loop.
  * Replaces np.matmul(A, u_vec) (apply.py:72), whose BLAS sums are not sequential either. */
+/* HBM calibration for the bench's roofline lines (measurement only, no result): mode 0 reads `bytes` of src once in
+ * order; mode 1 reads floor(bytes / 9 KiB) 9-KiB chunks in order and writes 64 doubles of dst per chunk -- the CSR
+ * SpMV's stream shape (a wave of 64 twelve-entry rows) without its x gathers.  dst: mode 0 a 256-double sink (never
+ * written on real data), mode 1 bytes / 144 doubles. */
+int mpbp_hbm_stream(const void* src, int64_t bytes, int32_t mode, double* dst, void* stream);
 int mpbp_spmv_seg(const mpbp_csr* A, const mpbp_rowblocks* blocks, int32_t mode, const double* x,
                   const double* z, double* y, void* stream);
 /* x_out = b / diag (first Jacobi sweep from 0); x_out = sub - that when sub != NULL. */
@@ -436,56 +449,65 @@ int mpbp_gtg_stencil_jacobi_step(const mpbp_stokes_params* prm, const double* ce
 int mpbp_gtg_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell, const mpbp_row_part* part,
                                const double* x_in, const double* b, double c1, double c2, double* d,
                                const double* sub, double* x_out, void* stream);
+/* A whole Chebyshev-Jacobi solve of Gt_G x = b from x = 0 (sweeps = 2..6 updates on [lmin, lmax], diag = Gt_G's
+ * diagonal) as ONE tiled launch (k_gtg_solve: b read once, the iterates in LDS) -- the apply's fused pressure solve,
+ * solve.py:265 / 271; bit-identical to mpbp_gtg_stencil_cheb_step sweeps from x0 = c2 b / diag.  One GPU; the grid must
+ * hold a tile and its halos (n >= 72 + 2 (sweeps - 1)), else MPBP_ERR_ARG and nothing is launched. */
+int mpbp_gtg_stencil_cheb_solve(const mpbp_stokes_params* prm, const double* cell, const double* b, const double* diag,
+                                double lmin, double lmax, int32_t sweeps, double* x_out, void* stream);
 
-/* Grid rows per workgroup of the marching stencil kernels (matrix-free F, D, G, Gt_G), process-wide; 0 (default):
- * per launch, the count that fills one round of workgroups (4 at 1024^2 on MI355X, 16 at 2048^2, 1 at 256^2 and
- * 512^2; two rows for a 2048^2 grid split over 8 ranks).  Results are bit-identical for every value. */
+/* ---- kernel choices ------------------------------------------------------------------------------ */
+/* Which kernel form runs each step.  Every choice gives the same results as every other (bit-identical), except
+ * q13_sym (tolerance mode only, within its 1e-12 bar).  A plan (mpbp_schur_plan.opts, mpbp_mg.opts) carries its own
+ * copy, so preconditioners with different choices coexist in one process and a captured graph holds the choices its
+ * plan had; opts == NULL, and the plan-less entry points (mpbp_spmv, mpbp_f_stencil_*, ...), use the process
+ * defaults, which the mpbp_set_* calls below change (mpbp_kernel_opts_default snapshots them for a new plan). */
+typedef struct mpbp_kernel_opts {
+    int32_t march_rows;        /* grid rows per workgroup of the marching stencil kernels (matrix-free F, D, G, Gt_G);
+                                  0 (default): per launch, the count that fills one round of workgroups */
+    int32_t init_diag;         /* first F sweep stages x0 = c2 b / diag: 1 (default) rebuilds diag from thn, 0 streams it */
+    int32_t f_pair;            /* tolerance mode: an F solve's last two sweeps as one k_march2 launch (1, default) */
+    int32_t f_direct;          /* tolerance-mode F sweeps on the direct kernel, one thread per cell (0, default) */
+    int32_t gtg_fused;         /* one-GPU Chebyshev Gt_G solves of 2..6 sweeps as ONE k_gtg_solve launch (1, default) */
+    int32_t gtg_tpb;           /* k_gtg_solve workgroup lanes: 512 (default) or 256 */
+    int32_t gtg_drhs;          /* the first fused Gt_G solve builds rhs = D Finv_v + v_p itself (1, default) */
+    int32_t q13_sym;           /* tolerance mode, one GPU: Gt_F_G x from the diamond's upper half (1, default; cleared
+                                  per plan when mpbp_q13_asymmetry finds the product not symmetric) */
+    int32_t f_tile;            /* one-GPU tolerance-mode F: x0 + sweep 1 and the last pair on 2D tiles (1, default) */
+    int32_t f_solve;           /* one-GPU tolerance-mode F solves of 3 or 4 updates as ONE k_fsolve launch (1, default) */
+    int32_t mg_galerkin_mf;    /* tolerance-mode F hierarchies: level 1 as R_0 (F (P_0 x)): 2 (default) one k_gal1 launch,
+                                  1 three launches, 0 its stored Galerkin matrix */
+    int32_t mg_galerkin_mf_p;  /* the pressure hierarchy's level 1 as R_0 (Gt_G (P_0 x)) (1, default) */
+    int32_t pg_direct;         /* matrix-free D, G, Gt_G sweeps one thread per cell (1, default) or marching (0) */
+    int32_t mg_group_rows;     /* multigrid levels / transfers with <= this many rows on the grouped CSR kernel (65536) */
+    int32_t mg_svl;            /* multigrid levels with a stencil-values copy use it (1, default) */
+    int32_t mg_mf_transfer;    /* whole-grid multigrid transfers matrix-free when the kinds are known (1, default) */
+    int32_t csr_table;         /* CSR SpMV waves start from the row blocks' wave table when present (1, default) */
+    int32_t reserved[7];
+} mpbp_kernel_opts;
+/* *out = the calling thread's current choices: its mpbp_kernel_opts_set_thread scope, else the process defaults. */
+void mpbp_kernel_opts_default(mpbp_kernel_opts* out);
+/* Kernel choices for the plan-less entry points called from THIS thread (a plan's own opts still win inside its apply);
+ * NULL returns the thread to the process defaults.  *prev (optional) receives the previous thread choice, to restore
+ * it.  The struct must stay valid while installed. */
+int mpbp_kernel_opts_set_thread(const mpbp_kernel_opts* o, const mpbp_kernel_opts** prev);
+/* Process defaults (see mpbp_kernel_opts for each field's meaning; results are bit-identical for every value, q13_sym
+ * aside).  Plans built before a call keep their own copies. */
 int mpbp_set_march_rows(int32_t rows);
-/* The first sweep of a matrix-free F inner solve stages x0 = c2 b / diag: mode 1 (default) rebuilds diag from the
- * thn tables inside the sweep (no diag stream), mode 0 streams the stored diagonal.  Same bits either way. */
 int mpbp_set_init_diag(int32_t mode);
-/* Tolerance-mode (MPBP_NUMERICS_FAST) F Chebyshev solves of >= 4 sweeps run their last two sweeps as one fused launch
- * (k_march2: x_s stays in LDS, 38 B per F row instead of 84; bit-identical to two sweeps).  1 (default) or 0. */
 int mpbp_set_f_pair(int32_t on);
-/* Tolerance-mode F sweeps (plain and initial) on the direct kernel -- one thread per cell, neighbours through the
- * caches, no LDS ring -- instead of the marching kernel.  0 (default) or 1. */
 int mpbp_set_f_direct(int32_t on);
-/* One-GPU Chebyshev Gt_G solves (2..6 sweeps, matrix-free Gt_G) as ONE tiled launch each (k_gtg_solve: b read once, the
- * iterates in LDS; bit-identical to the per-sweep launches).  1 (default) or 0. */
-/* One GPU, fused Gt_G solves: the first builds its right-hand side rhs = D Finv_v + v_p (solve.py:259) at every staged
- * cell instead of a D launch writing rhs (bit-identical).  1 (default) or 0. */
 int mpbp_set_gtg_drhs(int32_t on);
-/* Tolerance mode (plan f_numerics FAST), one GPU: Gt_F_G x on the diamond reads only the symmetric product's upper
- * half (slots 6..12; the lower entries mirrored from the neighbouring rows): 56 instead of 104 B of values per row,
- * within the mode's 1e-12 bar.  1 (default) or 0 (all 13 slots: bit-exact to the CSR product, which the row-partitioned
- * apply multiplies -- the one-GPU apply it is compared with bit for bit sets 0). */
 int mpbp_set_q13_sym(int32_t on);
-int mpbp_set_gtg_fused(int32_t on);   /* also 256 / 512: on, with that many lanes per workgroup (default 512) */
-/* One-GPU tolerance-mode F solves: x0 with the first sweep, and the last two sweeps, as 2D-tile launches (k_ftile: no
- * LDS ring, one barrier per workgroup; bit-identical to the marching kernels).  1 (default) or 0. */
+int mpbp_set_gtg_fused(int32_t on);   /* also 256 / 512: on, with that many lanes per workgroup */
 int mpbp_set_f_tile(int32_t on);
-/* One-GPU tolerance-mode F solves of 3 or 4 Chebyshev updates (x0 and 2 or 3 sweeps) as ONE tiled launch each
- * (k_fsolve: b, thn and faces read once, x written once, the iterates in LDS; bit-identical to the k_ftile launches).
- * 1 (default) or 0 (k_ftile / marching launches). */
 int mpbp_set_f_solve(int32_t on);
-/* Tolerance-mode F hierarchies (plan f_numerics FAST, one GPU, matrix-free level 0 and transfers): level 1 applied as
- * R_0 (F (P_0 x)) instead of streaming its stored Galerkin matrix: 2 (default) as one launch with the fine
- * intermediates in LDS (k_gal1), 1 as three launches through fine-size temporaries (same bits), 0 the stored matrix. */
 int mpbp_set_mg_galerkin_mf(int32_t on);
-/* The same for the pressure (Gt_G) hierarchy's level 1 -- R_0 (Gt_G (P_0 x)), one k_gal1p launch when
- * mpbp_set_mg_galerkin_mf is 2 -- in tolerance mode.  1 (default) or 0 (its stored Galerkin matrix). */
 int mpbp_set_mg_galerkin_mf_p(int32_t on);
-/* 1 (default): the matrix-free D, G and Gt_G sweeps run as one thread per cell reading neighbours from global memory
- * (no LDS ring; row partitions and ghost layouts included); 0: the marching kernel.  Bit-identical either way. */
 int mpbp_set_pg_direct(int32_t on);
-/* Multigrid levels and transfers with at most `rows` rows run on the grouped CSR kernel (several lanes per row,
- * products in parallel, the row's sum in order by one lane: same bits); 0 disables it.  Default 65536. */
 int mpbp_set_mg_group_rows(int32_t rows);
-/* 1 (default): multigrid levels with a stencil-values copy (mpbp_mg_level.A_svl) use it; 0: their SELL / CSR form. */
 int mpbp_set_mg_svl(int32_t on);
-/* 1 (default): whole-grid multigrid transfers matrix-free when mpbp_mg names the field kinds; 0: stored forms. */
 int mpbp_set_mg_mf_transfer(int32_t on);
-/* 1 (default): the CSR SpMV's waves start from mpbp_rowblocks.table when present; 0: from row_ptr (same bits). */
 int mpbp_set_csr_table(int32_t on);
 
 /* ---- geometric multigrid inner solves (the reference's pointer: solve.py:266, 274) ------------------ */

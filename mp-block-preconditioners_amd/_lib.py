@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("MPBP_LIB") or os.path.join(HERE, "lib", "libmpbp.so")
 OP_A, OP_F, OP_D, OP_G = 0, 1, 2, 3
 OP_L_N, OP_L_S, OP_D_N, OP_D_S, OP_G_N, OP_G_S, OP_XI_N, OP_XI_S = range(4, 12)
 SPMV_STORE, SPMV_ADD, SPMV_RESID = 0, 1, 2
+OK, ERR_ARG = 0, -1                    # mpbp.h return codes (MPBP_OK, MPBP_ERR_ARG)
 SPMV_FAST = 0x100                     # mpbp_f_stencil_spmv: tolerance-mode F rows
 NUMERICS_EXACT, NUMERICS_FAST = 0, 1  # mpbp_schur_plan.f_numerics
 INNER_JACOBI, INNER_CHEBYSHEV, INNER_MG = 0, 1, 2
@@ -77,12 +78,53 @@ HALO_PAIR_FN = CFUNCTYPE(None, c_void_p, c_void_p, c_void_p, c_void_p)
 GATHER_FN = CFUNCTYPE(None, c_void_p, c_int32, c_void_p, c_void_p, c_void_p)
 
 
+class KernelOpts(Structure):
+    """mpbp_kernel_opts: which kernel form runs each step (include/mpbp.h "kernel choices")."""
+    _fields_ = [("march_rows", c_int32), ("init_diag", c_int32), ("f_pair", c_int32), ("f_direct", c_int32),
+                ("gtg_fused", c_int32), ("gtg_tpb", c_int32), ("gtg_drhs", c_int32), ("q13_sym", c_int32),
+                ("f_tile", c_int32), ("f_solve", c_int32), ("mg_galerkin_mf", c_int32), ("mg_galerkin_mf_p", c_int32),
+                ("pg_direct", c_int32), ("mg_group_rows", c_int32), ("mg_svl", c_int32), ("mg_mf_transfer", c_int32),
+                ("csr_table", c_int32), ("reserved", c_int32 * 7)]
+
+
+def kernel_opts(overrides=None) -> KernelOpts:
+    """A plan's kernel choices: this thread's current ones (a kernel_options block, else the process defaults set by
+    mpbp_set_*) at this moment, with `overrides` (a dict of KernelOpts field names) applied.  Unknown names raise."""
+    o = KernelOpts()
+    lib().mpbp_kernel_opts_default(ctypes.byref(o))
+    names = {f for f, _ in KernelOpts._fields_ if f != "reserved"}
+    for k, v in (overrides or {}).items():
+        if k not in names:
+            raise ValueError(f"unknown kernel option {k!r} (known: {sorted(names)})")
+        setattr(o, k, int(v))
+    return o
+
+
+class kernel_options:
+    """Context manager: kernel choices for this thread inside the block -- the current ones with `overrides` applied
+    (mpbp_kernel_opts_set_thread): the plan-less entry points (mpbp_spmv, mpbp_f_stencil_*, mpbp_pg_stencil_*, ...)
+    use them, and plans created inside the block start from them; the previous thread choice is restored on exit.
+    Plans created before keep their own copies."""
+
+    def __init__(self, **overrides):
+        self.opts = kernel_opts(overrides)
+        self._prev = ctypes.c_void_p()
+
+    def __enter__(self):
+        check(lib().mpbp_kernel_opts_set_thread(ctypes.byref(self.opts), ctypes.byref(self._prev)))
+        return self.opts
+
+    def __exit__(self, *exc):
+        check(lib().mpbp_kernel_opts_set_thread(self._prev, None))
+        return False
+
+
 class Mg(Structure):
     _fields_ = [("nlevels", c_int32), ("cycles", c_int32), ("levels", POINTER(MgLevel)), ("coarse_inv", Csr),
                 ("coarse_inv_blocks", RowBlocks), ("coarse_dense", c_void_p),
                 ("part_levels", c_int32), ("gather_kind", c_int32), ("halo", HALO_FN), ("halo_ctx", c_void_p),
                 ("gather", GATHER_FN), ("tr_nfields", c_int32), ("tr_n0", c_int32), ("tr_ky", c_int32 * 8),
-                ("tr_kx", c_int32 * 8)]
+                ("tr_kx", c_int32 * 8), ("opts", POINTER(KernelOpts))]
 
 
 class SchurPlan(Structure):
@@ -104,7 +146,7 @@ class SchurPlan(Structure):
                 ("halo_first", c_int32), ("ca", c_int32), ("ca_reach_q", c_int32), ("wu_ext", c_void_p),
                 ("diag_F_ext", c_void_p), ("diag_P_ext", c_void_p), ("halo_pair", HALO_PAIR_FN),
                 ("q13", c_void_p), ("q13_n", c_int32), ("mg_F", POINTER(Mg)), ("mg_P", POINTER(Mg)),
-                ("fuse_g", c_int32), ("f_numerics", c_int32)]
+                ("fuse_g", c_int32), ("f_numerics", c_int32), ("opts", POINTER(KernelOpts))]
 
 
 _P = c_void_p
@@ -162,6 +204,11 @@ _SIGNATURES = {
     "mpbp_halo_add_kind": ([_P, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32], c_int),
     "mpbp_halo_add_gather": ([_P, c_int32, c_int32, _P, _P], c_int),
     "mpbp_halo_allgather": ([_P, c_int32, _P, _P, _P], None),
+    "mpbp_kernel_opts_default": ([POINTER(KernelOpts)], None),
+    "mpbp_hbm_stream": ([_P, c_int64, c_int32, _P, _P], c_int),
+    "mpbp_gtg_stencil_cheb_solve": ([POINTER(StokesParams), _P, _P, _P, c_double, c_double, c_int32, _P, _P], c_int),
+    "mpbp_kernel_opts_set_thread": ([c_void_p, c_void_p], c_int),
+    "mpbp_q13_asymmetry": ([c_int32, _P, POINTER(c_double), _P], c_int),
     "mpbp_set_march_rows": ([c_int32], c_int),
     "mpbp_set_init_diag": ([c_int32], c_int),
     "mpbp_set_f_pair": ([c_int32], c_int),
@@ -253,5 +300,5 @@ def stream_handle(stream=None):
 
 
 __all__ = ["lib", "check", "ptr", "stream_handle", "MpbpError", "Csr", "RowBlocks", "Sell", "RowPart", "StokesParams",
-           "InnerSolverC", "SchurPlan", "HALO_FN", "GATHER_FN", "byref",
+           "InnerSolverC", "SchurPlan", "KernelOpts", "kernel_opts", "kernel_options", "HALO_FN", "GATHER_FN", "byref",
            "Mg", "MgLevel"]

@@ -30,11 +30,12 @@
 // RCCL is resolved at run time (dlopen of the library the caller names -- the one torch loaded, so the
 // process holds one RCCL), which keeps libmpbp free of a link-time RCCL dependency.
 //
-// Communicators: one per process group.  mpbp_halo_create opens it; mpbp_halo_create_shared gives another halo
-// object (its own vector kinds, buffers and stream) the same communicator, reference-counted -- the partitioned
-// operator and the partitioned preconditioner of one FGMRES solve hold one communicator per rank.  Every exchange is
-// issued on the caller's stream in program order, which is the same on every rank, so graph-replayed (the captured
-// preconditioner) and eager (the operator) operations on the communicator stay in one consistent order.  A
+// Communicators: mpbp_halo_create opens one; mpbp_halo_create_shared gives another halo object (its own vector kinds,
+// buffers and stream) the same communicator, reference-counted.  The Python layer shares one communicator between the
+// partitioned PRECONDITIONERS of a process group (all their exchanges in order on the caller's stream, the same program
+// order on every rank) and gives the partitioned operator A u (DistributedMatrix) a communicator of its own: its
+// exchanges run eagerly on this object's side stream (OVERLAP) while a preconditioner's may be graph-replayed, and eager
+// side-stream and graph-replayed operations are never mixed on one communicator.  A
 // communicator whose point-to-point kernels were captured into a hipGraph is not destroyed when its last halo object
 // goes (see mpbp_halo_destroy): with RCCL 2.26.6 ncclCommDestroy then never returns.
 #include <dlfcn.h>

@@ -19,25 +19,37 @@
 namespace {
 
 thread_local char g_err[1024] = "";
-// grid rows per workgroup of the marching kernels; 0 (default): the count that fills one round of workgroups
-// (measured best at every size: 256^2 1 row -> 13.5k applies/s vs 7.6k at 4; 1024^2 4; 2048^2 16 -> 753 vs 727)
-int g_march_rows = 0;
-int g_csr_table = 1;      // CSR SpMV waves start from the row blocks' wave table when it has one (0: from row_ptr)
-int g_mg_mf_transfer = 1;   // whole-grid multigrid transfers matrix-free (0: their CSR / SELL / grouped forms)
-int g_init_diag = 1;      // fused first F sweep: 1 rebuilds the staged diagonal from thn, 0 streams diag
-int g_mg_gal_p = 1;        // ... the pressure (Gt_G) hierarchy's level 1 too, as R_0 (Gt_G (P_0 x)) (k_gal1p)
-int g_mg_gal = 2;          // tolerance-mode F hierarchies: level 1 as R_0 (F (P_0 x)): 2 one k_gal1 launch, 1 three
-                           // launches (MgGal), 0 its stored Galerkin matrix
-int g_f_direct = 0;        // tolerance-mode F sweeps on the direct kernel (one thread per cell, no LDS) instead of marching
-int g_gtg_tpb = 512;        // k_gtg_solve workgroup: 512 lanes (one tile cell + one ring cell each) or 256
-int g_gtg_fused = 1;
-int g_gtg_drhs = 1;
-int g_q13_sym = 1;          // tolerance mode, one GPU: Gt_F_G x read from the diamond's upper half (symmetric product;
-                           // the row-partitioned apply multiplies full rows: its one-GPU twin sets this to 0)         // the first fused Gt_G solve builds rhs = D Finv_v + v_p itself (no D launch)       // one-GPU Chebyshev Gt_G solves of 2..6 sweeps as one k_gtg_solve launch (0: per sweep)
-int g_f_solve = 1;         // one-GPU tolerance-mode F solves of 3 or 4 Chebyshev updates as one launch (k_fsolve)
-int g_f_tile = 1;          // one-GPU tolerance-mode F: x0 + sweep 1, and the last pair, on 2D tiles (k_ftile)
-int g_f_pair = 1;         // tolerance-mode F solves: the last two Chebyshev sweeps as one k_march2 launch (0: two)
-inline int pg_rows() { return g_march_rows; }   // rows per workgroup of the D / G / Gt_G marching kernels: as F
+// Kernel choices (mpbp_kernel_opts, include/mpbp.h): the process defaults (mpbp_set_*), and the choices of the plan
+// being applied -- mpbp_schur_apply / mpbp_mg_solve install their plan's copy for the duration of the call (OptsScope),
+// so two preconditioners with different choices coexist and a captured graph holds its own plan's choices.
+// Measured defaults: march_rows 0 = the count that fills one round of workgroups (256^2 1 row -> 13.5k applies/s vs
+// 7.6k at 4; 1024^2 4; 2048^2 16 -> 753 vs 727).
+mpbp_kernel_opts g_defaults = {
+    /*march_rows*/ 0, /*init_diag*/ 1, /*f_pair*/ 1, /*f_direct*/ 0, /*gtg_fused*/ 1, /*gtg_tpb*/ 512, /*gtg_drhs*/ 1,
+    /*q13_sym*/ 1, /*f_tile*/ 1, /*f_solve*/ 1, /*mg_galerkin_mf*/ 2, /*mg_galerkin_mf_p*/ 1, /*pg_direct*/ 1,
+    /*mg_group_rows*/ 65536, /*mg_svl*/ 1, /*mg_mf_transfer*/ 1, /*csr_table*/ 1, {0, 0, 0, 0, 0, 0, 0}};
+thread_local const mpbp_kernel_opts* t_opts = nullptr;
+inline const mpbp_kernel_opts& KO() { return t_opts ? *t_opts : g_defaults; }
+struct OptsScope {   // installs a plan's kernel choices (when it has its own) for one entry-point call
+    const mpbp_kernel_opts* prev;
+    explicit OptsScope(const mpbp_kernel_opts* o) : prev(t_opts) {
+        if (o) t_opts = o;
+    }
+    ~OptsScope() { t_opts = prev; }
+};
+inline int pg_rows() { return KO().march_rows; }
+// a plan's kernel choices must be values the setters accept
+int set_error(int code, const char* fmt, ...);
+inline int check_opts(const mpbp_kernel_opts* o, const char* who) {
+    if (!o) return MPBP_OK;
+    const bool ok = o->march_rows >= 0 && o->march_rows <= 4096 && (o->gtg_tpb == 256 || o->gtg_tpb == 512) &&
+                    o->mg_galerkin_mf >= 0 && o->mg_galerkin_mf <= 2 && o->mg_group_rows >= 0 &&
+                    (o->init_diag | o->f_pair | o->f_direct | o->gtg_fused | o->gtg_drhs | o->q13_sym | o->f_tile |
+                     o->f_solve | o->mg_galerkin_mf_p | o->pg_direct | o->mg_svl | o->mg_mf_transfer | o->csr_table) >= 0 &&
+                    (o->init_diag | o->f_pair | o->f_direct | o->gtg_fused | o->gtg_drhs | o->q13_sym | o->f_tile |
+                     o->f_solve | o->mg_galerkin_mf_p | o->pg_direct | o->mg_svl | o->mg_mf_transfer | o->csr_table) <= 1;
+    return ok ? MPBP_OK : set_error(MPBP_ERR_ARG, "%s: kernel options out of range", who);
+}   // rows per workgroup of the D / G / Gt_G marching kernels: as F
 
 int set_error(int code, const char* fmt, ...) {
     va_list ap;
@@ -1023,27 +1035,46 @@ __device__ inline void wave_lds_sync() {
 // [s, s + 64 LEN) = the wave's entries), so their HBM latency overlaps the per-row row_ptr loads' instead of
 // following it.
 // TRUST: the wave table says the wave is uniform (no row check).
-template <int LEN, bool XB, class Epi, bool TRUST = false>
+// GL (table-trusted waves whose entry offset is a multiple of 4): the chunk is copied into LDS by LDS-DMA
+// (global_load_lds_dwordx4, nontemporal) instead of through VGPRs -- the same lane-linear image, no staging registers
+// or LDS stores: 137.0-137.3 vs 138.8-141.8 us for the 1024^2 A on one box (tools/spmv_lab.py, r05h).
+__device__ inline void glds16(const void* g, void* lds) {
+    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 16, 0, 2);
+}
+template <int LEN, bool XB, class Epi, bool TRUST = false, bool GL = false>
 __device__ inline bool csr_wave_uniform(const Csr& A, const double* __restrict__ x, int32_t s, int lane,
                                         double2* vs, int2* cs, int32_t ks, int32_t ke, int32_t r, const Epi& epi,
                                         const typename Epi::P& pe) {
     constexpr int P = LEN / 2;   // pairs per row == 16-byte loads per lane
-    double2 v[P];
-    int2 cc[P];
+    if constexpr (GL) {
+        static_assert(TRUST, "LDS-DMA staging only for table-trusted waves");
+        // values: P instructions of 64 x 16 B; columns: LEN / 4 whole instructions and, for LEN = 10, half of one
 #pragma unroll
-    for (int j = 0; j < P; ++j) {
-        const int32_t k = s + 2 * (lane + 64 * j);
-        v[j] = ld_matrix<kCsrNT>(reinterpret_cast<const double2*>(A.va + k));
-        cc[j] = ld_matrix<kCsrNT>(reinterpret_cast<const int2*>(A.ci + k));
-    }
-    // (a compiler memory barrier: the loads above may not sink below the check, which would serialise them
-    // behind the row_ptr loads again; it emits no instruction and no wait)
-    asm volatile("" ::: "memory");
-    if (!TRUST && !__all(ke - ks == LEN)) return false;
+        for (int j = 0; j < P; ++j) glds16(A.va + s + 2 * (lane + 64 * j), vs + 64 * j);
 #pragma unroll
-    for (int j = 0; j < P; ++j) {
-        vs[lane + 64 * j] = v[j];
-        cs[lane + 64 * j] = cc[j];
+        for (int j = 0; j < LEN / 4; ++j) glds16(A.ci + s + 4 * (lane + 64 * j), cs + 128 * j);
+        if constexpr (LEN % 4 != 0) {
+            if (lane < 32) glds16(A.ci + s + 4 * (lane + 64 * (LEN / 4)), cs + 128 * (LEN / 4));
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        double2 v[P];
+        int2 cc[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int32_t k = s + 2 * (lane + 64 * j);
+            v[j] = ld_matrix<kCsrNT>(reinterpret_cast<const double2*>(A.va + k));
+            cc[j] = ld_matrix<kCsrNT>(reinterpret_cast<const int2*>(A.ci + k));
+        }
+        // (a compiler memory barrier: the loads above may not sink below the check, which would serialise them
+        // behind the row_ptr loads again; it emits no instruction and no wait)
+        asm volatile("" ::: "memory");
+        if (!TRUST && !__all(ke - ks == LEN)) return false;
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            vs[lane + 64 * j] = v[j];
+            cs[lane + 64 * j] = cc[j];
+        }
     }
     wave_lds_sync();
     const int p0 = lane * P;
@@ -1098,6 +1129,12 @@ __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __rest
             const int32_t r = ra + lane;
             const typename Epi::P pe = epi.pre(r);
             constexpr bool XB = true;
+            if ((s & 3) == 0) {   // 16-byte aligned column chunk: LDS-DMA staging
+                if (len == 12) csr_wave_uniform<12, XB, Epi, true, true>(A, x, s, lane, vstage[w], cstage[w], 0, 0, r, epi, pe);
+                else if (len == 10) csr_wave_uniform<10, XB, Epi, true, true>(A, x, s, lane, vstage[w], cstage[w], 0, 0, r, epi, pe);
+                else csr_wave_uniform<8, XB, Epi, true, true>(A, x, s, lane, vstage[w], cstage[w], 0, 0, r, epi, pe);
+                return;
+            }
             if (len == 12) csr_wave_uniform<12, XB, Epi, true>(A, x, s, lane, vstage[w], cstage[w], 0, 0, r, epi, pe);
             else if (len == 10) csr_wave_uniform<10, XB, Epi, true>(A, x, s, lane, vstage[w], cstage[w], 0, 0, r, epi, pe);
             else csr_wave_uniform<8, XB, Epi, true>(A, x, s, lane, vstage[w], cstage[w], 0, 0, r, epi, pe);
@@ -1191,6 +1228,31 @@ __global__ void __launch_bounds__(kBlock) k_csr_wave(Csr A, const double* __rest
         }
     }
     if (live) epi.template apply<kCsrNT>(r, acc, pe);
+}
+
+// ---------------------------------------------------- HBM calibration (measurement only) ----
+// The bench's same-run reference rates for the CSR SpMV roofline (mpbp_hbm_stream): mode 0 reads `bytes` once in order
+// (16 B per lane, nontemporal, 16 KiB per workgroup); mode 1 the SpMV's own stream shape without its x gathers -- per
+// 64-lane wave 9 KiB read in order and 64 doubles written (nontemporal), as a wave of 64 twelve-entry rows moves.
+__global__ void __launch_bounds__(kBlock) k_hbm_read(const f64x2* __restrict__ p, int64_t n16, double* sink) {
+    const int64_t base = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 1024 + threadIdx.x;
+    f64x2 acc = {0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int64_t i = base + 256 * j;
+        if (i < n16) acc += __builtin_nontemporal_load(p + i);
+    }
+    if (acc.x == 1234.5678 && acc.y == -8765.4321) sink[threadIdx.x] = acc.x;   // keeps the loads; never taken on data
+}
+__global__ void __launch_bounds__(kBlock) k_hbm_readwrite(const f64x2* __restrict__ p, int64_t nwaves, double* y) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t wv = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4 + w;
+    if (wv >= nwaves) return;
+    const f64x2* q = p + wv * 576;
+    f64x2 acc = {0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc += __builtin_nontemporal_load(q + lane + 64 * j);
+    __builtin_nontemporal_store(acc.x + acc.y, y + wv * 64 + lane);
 }
 
 // ---------------------------------------------------- CSR, segmented reduction ----
@@ -1871,6 +1933,42 @@ struct FStencilFast : FStencilDev {
     }
 };
 
+// Tolerance-mode F inner solve from x = 0 on a row partition's owned rows (the per-operator exchange schedule: the
+// multigrid level-0 smoothing and the Chebyshev / Jacobi F solves there): x0 = d0 = (c2 b) (1 / diag) with the
+// reciprocal diagonals of FStencilFast::rdiag4 over the global thn table -- the operations of the one-GPU fast first
+// sweep (k_ftile / k_fsolve level 0, k_march_init), so the partitioned fast solve starts from the same bits (the stored
+// diagonal's c2 (b / diag) does not).  One thread per owned cell, its four rows.
+struct TGlob {   // thn at wrapped grid coordinates, straight from the global table
+    const double* t;
+    int n;
+    __device__ double T(int sph, int r, int c) const {
+        r = r < 0 ? r + n : (r >= n ? r - n : r);
+        c = c < 0 ? c + n : (c >= n ? c - n : c);
+        const double v = t[r * n + c];
+        return sph ? 1.0 - v : v;
+    }
+};
+template <bool CHEB>
+__global__ void __launch_bounds__(256) k_f_fast_init(FStencilFast P, const double* __restrict__ b, double c2,
+                                                     double* __restrict__ d, const double* __restrict__ sub,
+                                                     double* __restrict__ xo) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)P.L * P.n) return;
+    const int lr = (int)(i / P.n), gc = (int)(i - (int64_t)lr * P.n);
+    const int gr = P.r0 + lr;
+    const int32_t k = gr * P.n + gc;
+    const FStencilDev::Stage sg{{P.uface[k], P.vface[k]}};
+    double rd[4];
+    P.rdiag4(gr, gc, TGlob{P.cell, P.n}, sg, rd);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+        const int64_t o = ((int64_t)f * P.L + lr) * P.n + gc;
+        const double x0 = c2 * b[o] * rd[f];
+        if constexpr (CHEB) d[o] = x0;
+        xo[o] = sub ? sub[o] - x0 : x0;
+    }
+}
+
 // ---- marching kernels: a workgroup owns a 256-column strip of `rows` consecutive grid rows and walks
 // down it with a 3-row LDS ring per staged field (+ thn).  Each step stages ONE new grid row (its loads
 // are issued before the current row is computed, so their latency hides under the arithmetic) instead
@@ -2144,7 +2242,6 @@ k_march(S P, XS xs, int nchunks, Epi epi, BS bs = BS{}) {
 // full occupancy instead of one round of marching workgroups.  Same accessors' values, same row arithmetic.
 // Measured at 1024^2 (trace means, r02o vs r02l): D 17.7 -> 13.2 us, Gt_G sweeps 13.2 / 12.1 -> 11.9 / 11.3 us, the
 // Gt_G first sweep (5 divisions per cell for the staged x0) 15.6 either way.
-int g_pg_direct = 1;   // mpbp_set_pg_direct(0): the marching kernel instead
 // (lr: the thread's local row in the partition layout, gr: the same row's wrapped global index -- the row the
 // stencil's accessors are called around; a neighbour row r maps to local row lr + (r - gr))
 template <class S, class XS>
@@ -2647,9 +2744,9 @@ int64_t march_chunks(const S& P, int rows_per_block, int64_t capacity) {
 
 template <class S, class XS, class Epi, class BS = BNone>
 int launch_march_fixed(const S& P, const XS& xs, Epi epi, int rows_per_block, hipStream_t st, const BS& bs = BS{}) {
-    // D, G, Gt_G on one GPU, and (g_f_direct) the tolerance-mode F rows: the direct kernel
+    // D, G, Gt_G on one GPU, and (KO().f_direct) the tolerance-mode F rows: the direct kernel
     if constexpr ((!std::is_base_of_v<FStencilDev, S> && !BS::on) || S::kFast) {
-        if (S::kFast ? g_f_direct != 0 : g_pg_direct != 0) {
+        if (S::kFast ? KO().f_direct != 0 : KO().pg_direct != 0) {
             // rows as march_rows: 0 all owned, 1 rows 1 .. L-2, 2 rows 0 and L-1, 3 owned + ext ghost rows each side
             const int la = P.which == 1 ? 1 : P.which == 3 ? -P.ext : 0;
             const int lb = P.which == 1 ? P.L - 1 : P.which == 3 ? P.L + P.ext : P.L;
@@ -3102,7 +3199,7 @@ int launch_fsolve(const FStencilDev& Pd, int K, const double* c1, const double* 
 // its direction (SD false): level A reads d_in on its neighbours' rows and columns.
 template <bool SUB, bool SD, class BS>
 int launch_march2_t(const FStencilFast& P, const Fused2& a, hipStream_t st, const BS& bs) {
-    const int64_t chunks = march_chunks(P, g_march_rows, march_capacity<k_march2<SUB, SD, BS>>());
+    const int64_t chunks = march_chunks(P, KO().march_rows, march_capacity<k_march2<SUB, SD, BS>>());
     if (chunks == 0) return MPBP_OK;
     const int64_t strips = (P.n + kMB - 1) / kMB;
     k_march2<SUB, SD, BS><<<(unsigned)(chunks * strips), kMB, 0, st>>>(P, a, (int)chunks, bs);
@@ -3863,14 +3960,12 @@ template <class Epi>
 int launch_rows(const mpbp_csr* A, const mpbp_rowblocks* blk, const double* x, Epi epi, hipStream_t st) {
     if (!blk || blk->count <= 0) return MPBP_OK;
     k_csr_wave<Epi><<<blk->count, kBlock, 0, st>>>(to_csr(A), x, reinterpret_cast<const int2*>(blk->pairs),
-                                                    blk->count, g_csr_table ? blk->table : nullptr, epi);
+                                                    blk->count, KO().csr_table ? blk->table : nullptr, epi);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
 // Small-level CSR products through k_csr_grp: lanes per row from the mean row length (2: <= 16 entries, 4: <= 32,
 // 8: longer), so one chunk holds a multigrid coarse row (transfers 1-16 entries, Galerkin levels 20-46).
-int g_svl_on = 1;         // multigrid levels with a stencil-values copy use it (0: SELL / CSR instead)
-int g_grp_rows = 65536;   // multigrid levels / transfers with at most this many rows use it (0: never)
 template <class Epi, class XS = XPlain>
 int launch_grp(const mpbp_csr* A, const XS& xs, Epi epi, hipStream_t st) {
     if (A->nrows <= 0) return MPBP_OK;
@@ -3885,7 +3980,7 @@ int launch_grp(const mpbp_csr* A, const XS& xs, Epi epi, hipStream_t st) {
     return avg <= 16 ? go(std::integral_constant<int, 2>{})
                      : avg <= 32 ? go(std::integral_constant<int, 4>{}) : go(std::integral_constant<int, 8>{});
 }
-inline bool use_grp(const mpbp_csr& A) { return g_grp_rows > 0 && A.nrows > 0 && A.nrows <= g_grp_rows && A.nnz > 0; }
+inline bool use_grp(const mpbp_csr& A) { return KO().mg_group_rows > 0 && A.nrows > 0 && A.nrows <= KO().mg_group_rows && A.nnz > 0; }
 int grp_spmv(const mpbp_csr* A, int32_t mode, const double* x, const double* z, double* y, hipStream_t st) {
     const XPlain xs{x};
     switch (mode) {
@@ -4000,82 +4095,93 @@ extern "C" {
 
 const char* mpbp_version(void) { return "libmpbp 0.1 (gfx950)"; }
 
+void mpbp_kernel_opts_default(mpbp_kernel_opts* out) {
+    if (out) *out = KO();
+}
+
+int mpbp_kernel_opts_set_thread(const mpbp_kernel_opts* o, const mpbp_kernel_opts** prev) {
+    if (int rc = check_opts(o, "kernel_opts_set_thread")) return rc;
+    if (prev) *prev = t_opts;
+    t_opts = o;
+    return MPBP_OK;
+}
+
 int mpbp_set_march_rows(int32_t rows) {
     if (rows < 0 || rows > 4096) return set_error(MPBP_ERR_ARG, "march rows must be 0 (auto) or in [1, 4096]");
-    g_march_rows = rows;
+    g_defaults.march_rows = rows;
     return MPBP_OK;
 }
 int mpbp_set_csr_table(int32_t on) {
-    g_csr_table = on ? 1 : 0;
+    g_defaults.csr_table = on ? 1 : 0;
     return MPBP_OK;
 }
 int mpbp_set_mg_mf_transfer(int32_t on) {
-    g_mg_mf_transfer = on ? 1 : 0;
+    g_defaults.mg_mf_transfer = on ? 1 : 0;
     return MPBP_OK;
 }
 int mpbp_set_mg_svl(int32_t on) {
-    g_svl_on = on ? 1 : 0;
+    g_defaults.mg_svl = on ? 1 : 0;
     return MPBP_OK;
 }
 int mpbp_set_mg_group_rows(int32_t rows) {
     if (rows < 0) return set_error(MPBP_ERR_ARG, "mg group rows must be >= 0");
-    g_grp_rows = rows;
+    g_defaults.mg_group_rows = rows;
     return MPBP_OK;
 }
 int mpbp_set_pg_direct(int32_t on) {
-    g_pg_direct = on ? 1 : 0;
+    g_defaults.pg_direct = on ? 1 : 0;
     return MPBP_OK;
 }
 
 int mpbp_set_mg_galerkin_mf(int32_t on) {
     if (on < 0 || on > 2) return set_error(MPBP_ERR_ARG, "mg_galerkin_mf must be 0, 1 or 2");
-    g_mg_gal = on;
+    g_defaults.mg_galerkin_mf = on;
     return MPBP_OK;
 }
 int mpbp_set_mg_galerkin_mf_p(int32_t on) {
     if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "mg_galerkin_mf_p must be 0 or 1");
-    g_mg_gal_p = on;
+    g_defaults.mg_galerkin_mf_p = on;
     return MPBP_OK;
 }
 int mpbp_set_f_direct(int32_t on) {
     if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "f_direct must be 0 or 1");
-    g_f_direct = on;
+    g_defaults.f_direct = on;
     return MPBP_OK;
 }
 int mpbp_set_gtg_fused(int32_t on) {
     if (on != 0 && on != 1 && on != 256 && on != 512) return set_error(MPBP_ERR_ARG, "gtg_fused must be 0, 1, 256 or 512");
-    g_gtg_fused = on != 0;
-    if (on == 256 || on == 512) g_gtg_tpb = on;
+    g_defaults.gtg_fused = on != 0;
+    if (on == 256 || on == 512) g_defaults.gtg_tpb = on;
     return MPBP_OK;
 }
 int mpbp_set_q13_sym(int32_t on) {
     if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "q13_sym must be 0 or 1");
-    g_q13_sym = on;
+    g_defaults.q13_sym = on;
     return MPBP_OK;
 }
 int mpbp_set_gtg_drhs(int32_t on) {
     if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "gtg_drhs must be 0 or 1");
-    g_gtg_drhs = on;
+    g_defaults.gtg_drhs = on;
     return MPBP_OK;
 }
 int mpbp_set_f_tile(int32_t on) {
     if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "f_tile must be 0 or 1");
-    g_f_tile = on;
+    g_defaults.f_tile = on;
     return MPBP_OK;
 }
 int mpbp_set_f_solve(int32_t on) {
     if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "f_solve must be 0 or 1");
-    g_f_solve = on;
+    g_defaults.f_solve = on;
     return MPBP_OK;
 }
 int mpbp_set_f_pair(int32_t on) {
     if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "f_pair must be 0 or 1");
-    g_f_pair = on;
+    g_defaults.f_pair = on;
     return MPBP_OK;
 }
 int mpbp_set_init_diag(int32_t mode) {
     if (mode != 0 && mode != 1) return set_error(MPBP_ERR_ARG, "init diag mode must be 0 or 1");
-    g_init_diag = mode;
+    g_defaults.init_diag = mode;
     return MPBP_OK;
 }
 const char* mpbp_last_error(void) { return g_err; }
@@ -4337,6 +4443,22 @@ int mpbp_spmv(const mpbp_csr* A, const mpbp_rowblocks* blocks, int32_t mode, con
     case MPBP_SPMV_RESID: return launch_rows(A, blocks, x, EpiResid{z, y}, st);
     default: return set_error(MPBP_ERR_ARG, "spmv: unknown mode %d", mode);
     }
+}
+
+int mpbp_hbm_stream(const void* src, int64_t bytes, int32_t mode, double* dst, void* stream) {
+    if (!src || !dst || bytes < 16 || (mode != 0 && mode != 1)) return set_error(MPBP_ERR_ARG, "hbm_stream: bad args");
+    const hipStream_t st = as_stream(stream);
+    if (mode == 0) {
+        const int64_t n16 = bytes / 16;
+        k_hbm_read<<<(unsigned)((n16 + 1023) / 1024), kBlock, 0, st>>>(reinterpret_cast<const f64x2*>(src), n16, dst);
+    } else {
+        const int64_t nwaves = bytes / (576 * 16);
+        if (nwaves < 1) return set_error(MPBP_ERR_ARG, "hbm_stream: mode 1 needs >= 9 KiB");
+        k_hbm_readwrite<<<(unsigned)((nwaves + 3) / 4), kBlock, 0, st>>>(reinterpret_cast<const f64x2*>(src), nwaves,
+                                                                         dst);
+    }
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
 }
 
 int mpbp_spmv_seg(const mpbp_csr* A, const mpbp_rowblocks* blocks, int32_t mode, const double* x,
@@ -4957,7 +5079,7 @@ static int make_fstencil(const mpbp_stokes_params* prm, const double* cell, cons
 namespace {
 template <class Epi>
 int launch_fstencil(const FStencilDev& P, const double* x, Epi epi, hipStream_t st, bool fast = false) {
-    return with_f_policy(P, fast, [&](const auto& Q) { return launch_march(Q, XPlain{x}, epi, g_march_rows, st); });
+    return with_f_policy(P, fast, [&](const auto& Q) { return launch_march(Q, XPlain{x}, epi, KO().march_rows, st); });
 }
 
 }  // namespace
@@ -5208,6 +5330,35 @@ __global__ void __launch_bounds__(kBlock) k_q13(int32_t n, const double* __restr
     epi(cell, acc, pe);
 }
 
+// max |Q(c, c + o) - Q(c + o, c)| over the diamond (slot s at c against slot 12 - s at c + o) and max |Q|: whether the
+// symmetric-half read (k_q13<SYM>) may stand in for the stored product.  Non-negative doubles order like their bits.
+__global__ void __launch_bounds__(kBlock) k_q13_asym(int32_t n, const double* __restrict__ vals,
+                                                     unsigned long long* out) {
+    const int32_t N = n * n;
+    const int32_t cell = blockIdx.x * kBlock + threadIdx.x;
+    double asym = 0.0, amax = 0.0;
+    if (cell < N) {
+        const int gr = cell / n, gc = cell - (cell / n) * n;
+#pragma unroll
+        for (int s = 0; s < kQSlots; ++s) amax = fmax(amax, fabs(vals[(int64_t)s * N + cell]));
+#pragma unroll
+        for (int s = 0; s < 6; ++s) {
+            int rr = gr + q13_dr(s), cc = gc + q13_dc(s);
+            rr = rr < 0 ? rr + n : rr >= n ? rr - n : rr;
+            cc = cc < 0 ? cc + n : cc >= n ? cc - n : cc;
+            asym = fmax(asym, fabs(vals[(int64_t)s * N + cell] - vals[(int64_t)(12 - s) * N + rr * n + cc]));
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        asym = fmax(asym, __shfl_xor(asym, o));
+        amax = fmax(amax, __shfl_xor(amax, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(out, (unsigned long long)__double_as_longlong(asym));
+        atomicMax(out + 1, (unsigned long long)__double_as_longlong(amax));
+    }
+}
+
 template <class Epi>
 int launch_q13(int32_t n, const double* vals, const double* x, Epi epi, hipStream_t st, bool sym = false) {
     if (sym) k_q13<Epi, true><<<grid_for((int64_t)n * n), kBlock, 0, st>>>(n, vals, x, epi);
@@ -5252,6 +5403,22 @@ int mpbp_q13_build(const mpbp_csr* Q, int32_t n, double* vals, void* stream) {
     MPBP_HIP(hipFreeAsync(bad, st));
     MPBP_HIP(hipStreamSynchronize(st));
     if (nbad) return set_error(MPBP_ERR_ARG, "q13_build: %d rows are not the 13-point diamond", nbad);
+    return MPBP_OK;
+}
+
+int mpbp_q13_asymmetry(int32_t n, const double* vals, double* out, void* stream) {
+    if (n < 5 || (int64_t)n * n > INT32_MAX / kQSlots || !vals || !out) return set_error(MPBP_ERR_ARG, "q13_asymmetry: bad args");
+    const hipStream_t st = as_stream(stream);
+    unsigned long long* dev = nullptr;
+    MPBP_HIP(hipMallocAsync((void**)&dev, 2 * sizeof(unsigned long long), st));
+    MPBP_HIP(hipMemsetAsync(dev, 0, 2 * sizeof(unsigned long long), st));
+    k_q13_asym<<<grid_for((int64_t)n * n), kBlock, 0, st>>>(n, vals, dev);
+    MPBP_HIP(hipGetLastError());
+    unsigned long long h[2] = {0, 0};
+    MPBP_HIP(hipMemcpyAsync(h, dev, sizeof(h), hipMemcpyDeviceToHost, st));
+    MPBP_HIP(hipFreeAsync(dev, st));
+    MPBP_HIP(hipStreamSynchronize(st));
+    memcpy(out, h, sizeof(h));
     return MPBP_OK;
 }
 
@@ -5338,13 +5505,13 @@ int gal_r(const MgGal& g, Epi epi, hipStream_t st) {
     return mg_transfer_mf(g.m, 0, MPBP_MG_R, g.m->levels[0].R.nrows, g.t1, epi, st);
 }
 
-// The whole level-1 product as one k_gal1 launch (g_mg_gal == 2): four fields, a grid the staged windows wrap once.
+// The whole level-1 product as one k_gal1 launch (KO().mg_galerkin_mf == 2): four fields, a grid the staged windows wrap once.
 template <class Epi>
 int gal_fused(const MgGal& g, const double* x, Epi epi, hipStream_t st, bool* done) {
     *done = false;
     const mpbp_schur_plan* p = g.fine.stencil;
     if (g.fine.sop == SOP_GTG) {   // the pressure hierarchy: one field, cell-centred (mg.FIELDS_PRESSURE)
-        if (g_mg_gal != 2 || g.m->tr_nfields != 1 || g.m->tr_ky[0] != MPBP_MG_CELL || g.m->tr_kx[0] != MPBP_MG_CELL ||
+        if (KO().mg_galerkin_mf != 2 || g.m->tr_nfields != 1 || g.m->tr_ky[0] != MPBP_MG_CELL || g.m->tr_kx[0] != MPBP_MG_CELL ||
             p->f_prm.n < 2 * kG1CW || (p->f_prm.n & 1))
             return MPBP_OK;
         PGDev Pg;
@@ -5357,7 +5524,7 @@ int gal_fused(const MgGal& g, const double* x, Epi epi, hipStream_t st, bool* do
         *done = true;
         return MPBP_OK;
     }
-    if (g_mg_gal != 2 || g.m->tr_nfields != 4 || p->f_prm.n < 2 * kG1CW || (p->f_prm.n & 1)) return MPBP_OK;
+    if (KO().mg_galerkin_mf != 2 || g.m->tr_nfields != 4 || p->f_prm.n < 2 * kG1CW || (p->f_prm.n & 1)) return MPBP_OK;
     FStencilDev Pd;
     const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &Pd);
     if (rc) return rc;
@@ -5459,6 +5626,29 @@ struct OpPair {
     OpRef in, bd;
 };
 
+// x0 (= d0 for Chebyshev) of an inner solve from x = 0 over `nrows` owned rows: the tolerance-mode F operator on a row
+// partition's owned rows takes the fast reciprocal diagonals (k_f_fast_init, the one-GPU fast first sweep's bits);
+// every other operator the stored diagonal (k_cheb_init / k_jacobi_init: c2 (b / diag)).
+int op_init(const OpRef& o, int32_t nrows, bool cheb, const double* b, const double* diag, double c2, double* d,
+            const double* sub, double* xo, hipStream_t st) {
+    const mpbp_schur_plan* p = o.stencil;
+    if (p && o.sop == SOP_F && p->f_numerics == MPBP_NUMERICS_FAST && o.which == 0) {
+        const mpbp_row_part q = stencil_part(o);
+        FStencilDev Pd;
+        const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, &Pd);
+        if (rc) return rc;
+        const FStencilFast P{Pd};
+        if ((int64_t)4 * P.L * P.n != nrows) return set_error(MPBP_ERR_ARG, "f fast init: %d rows, not the owned ones", nrows);
+        const int grid = grid_for((int64_t)P.L * P.n);
+        if (cheb) k_f_fast_init<true><<<grid, 256, 0, st>>>(P, b, c2, d, sub, xo);
+        else k_f_fast_init<false><<<grid, 256, 0, st>>>(P, b, 1.0, nullptr, sub, xo);
+        MPBP_HIP(hipGetLastError());
+        return MPBP_OK;
+    }
+    return cheb ? mpbp_cheb_init(nrows, b, diag, c2, d, sub, xo, (void*)st)
+                : mpbp_jacobi_init(nrows, b, diag, sub, xo, (void*)st);
+}
+
 // The first sweep of an inner solve can fold in the init pass (x0 = d0 = c2[0] b / diag, recomputed
 // from b and diag wherever the sweep stages x) when the operator is a whole-grid marching stencil.
 bool can_fuse_init(const OpPair& op) {
@@ -5477,17 +5667,17 @@ int op_first_sweep(const OpRef& o, bool cheb, const double* b, const double* dia
         const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, &P);
         if (rc) return rc;
         const bool fast = p->f_numerics == MPBP_NUMERICS_FAST;
-        if (fast && cheb && g_f_tile && q.halo == 0 && o.which == 0 && ftile_ok(P.n))   // x0, sweep 1 on 2D tiles
+        if (fast && cheb && KO().f_tile && q.halo == 0 && o.which == 0 && ftile_ok(P.n))   // x0, sweep 1 on 2D tiles
             return launch_ftile<true>(P, FTile{nullptr, nullptr, b, sub, xo, store_d ? d : nullptr, 0.0, c2_0, c1, c2},
                                       st);
-        if (g_init_diag == 0)
+        if (KO().init_diag == 0)
             return with_f_policy(P, fast, [&](const auto& Q) {
-                return cheb ? launch_march(Q, xs, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, g_march_rows, st)
-                            : launch_march(Q, xs, EpiJacobi{nullptr, b, nullptr, sub, xo}, g_march_rows, st);
+                return cheb ? launch_march(Q, xs, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, KO().march_rows, st)
+                            : launch_march(Q, xs, EpiJacobi{nullptr, b, nullptr, sub, xo}, KO().march_rows, st);
             });
         return with_f_policy(P, fast, [&](const auto& Q) {
-            return cheb ? launch_march_init(Q, b, xs.c2, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, g_march_rows, st)
-                        : launch_march_init(Q, b, xs.c2, EpiJacobi{nullptr, b, nullptr, sub, xo}, g_march_rows, st);
+            return cheb ? launch_march_init(Q, b, xs.c2, EpiChebFirst{b, d, c1, c2, sub, xo, store_d}, KO().march_rows, st)
+                        : launch_march_init(Q, b, xs.c2, EpiJacobi{nullptr, b, nullptr, sub, xo}, KO().march_rows, st);
         });
     }
     PGDev P;
@@ -5565,7 +5755,7 @@ OpRef mg_csr_op(const mpbp_csr& A, const mpbp_rowblocks& blk) {
 OpPair mg_level_op(const mpbp_mg_level& L) {
     const OpRef none{nullptr, nullptr, nullptr, nullptr, true, 0, SOP_NONE};
     if (use_grp(L.A)) return OpPair{OpRef{&L.A, &L.A_blocks, nullptr, nullptr, false, 0, SOP_NONE, 0, 1}, none};
-    if (L.A_svl && g_svl_on)
+    if (L.A_svl && KO().mg_svl)
         return OpPair{OpRef{&L.A, &L.A_blocks, nullptr, nullptr, false, 0, SOP_NONE, 0, 0, L.A_svl}, none};
     return OpPair{L.A_sell.nslices > 0 ? OpRef{&L.A, nullptr, &L.A_sell, nullptr, false, 0, SOP_NONE}
                                        : mg_csr_op(L.A, L.A_blocks), none};
@@ -5604,7 +5794,7 @@ int mg_transfer_mf(const mpbp_mg* m, int l, int32_t which, int32_t nrows, const 
     return MPBP_OK;
 }
 inline bool use_mf_transfer(const mpbp_mg* m, int l) {
-    return g_mg_mf_transfer && m->tr_nfields > 0 && m->tr_nfields <= 8 && l >= m->part_levels && (m->tr_n0 >> l) >= 4 &&
+    return KO().mg_mf_transfer && m->tr_nfields > 0 && m->tr_nfields <= 8 && l >= m->part_levels && (m->tr_n0 >> l) >= 4 &&
            ((m->tr_n0 >> l) << l) == m->tr_n0;
 }
 int mg_transfer(const mpbp_csr& M, const mpbp_rowblocks& blk, const mpbp_sell& S, int32_t mode, const double* x,
@@ -5663,7 +5853,7 @@ __global__ void __launch_bounds__(kDT) k_dense_cm(int32_t m, const double* __res
 // ping-pong buffer when dst is NULL), as sub - x when sub is set; *cur points at the result on return.  xch(x)
 // refreshes x's ghost rows before every sweep that reads them (a no-op on one GPU).
 // The last two sweeps of a tolerance-mode F Chebyshev solve may run as one fused launch (k_march2 / k_ftile).
-bool f_pair_ok(const mpbp_schur_plan* p) { return p->f_numerics == MPBP_NUMERICS_FAST && g_f_pair && p->f_stencil; }
+bool f_pair_ok(const mpbp_schur_plan* p) { return p->f_numerics == MPBP_NUMERICS_FAST && KO().f_pair && p->f_stencil; }
 
 template <class Xch>
 int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, double lmax, int K, bool zero,
@@ -5701,7 +5891,7 @@ int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, 
         s = 2;
     } else if (zero) {
         double* out0 = K == 1 ? (dst ? dst : other) : x;
-        int rc = mpbp_cheb_init(nrows, b, diag, c2[0], d, K == 1 ? sub : nullptr, out0, (void*)st);
+        int rc = op_init(o, nrows, true, b, diag, c2[0], d, K == 1 ? sub : nullptr, out0, st);
         if (rc) return rc;
         if (K == 1) {
             *cur = out0;
@@ -5712,7 +5902,7 @@ int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, 
     // tolerance-mode F level 0 on one GPU: the last two sweeps as one tiled launch (k_ftile); a restart of two sweeps
     // reads d as +0.0 there, so it needs no memset either
     const bool tpair = K - s >= 2 && o.stencil && o.sop == SOP_F && op.bd.empty && !o.stencil->halo && o.which == 0 &&
-                       f_pair_ok(o.stencil) && g_f_tile && ftile_ok(o.stencil->f_prm.n);
+                       f_pair_ok(o.stencil) && KO().f_tile && ftile_ok(o.stencil->f_prm.n);
     // restart from the iterate in *cur: d = 0 -- read as +0.0 by the grouped kernel's first sweep, else zeroed
     bool dzero = !zero && (((op.in.grp || op.in.svl) && op.bd.empty) || (tpair && s == K - 2));
     if (!zero && !dzero) MPBP_HIP(hipMemsetAsync(d, 0, sizeof(double) * (size_t)nrows, st));
@@ -5747,7 +5937,7 @@ int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, 
 // Level 1 as R_0 (F (P_0 x)): tolerance-mode F stencil level 0 on one GPU, matrix-free transfers, level 1 smoothed.
 bool mg_gal_ok(const mpbp_mg* m, const MgFine& f) {
     const OpRef& o = f.op.in;
-    return g_mg_gal && o.stencil && (o.sop == SOP_F || (o.sop == SOP_GTG && g_mg_gal_p)) &&
+    return KO().mg_galerkin_mf && o.stencil && (o.sop == SOP_F || (o.sop == SOP_GTG && KO().mg_galerkin_mf_p)) &&
            o.stencil->f_numerics == MPBP_NUMERICS_FAST && o.which == 0 && f.op.bd.empty && !f.halo && !o.stencil->halo &&
            m->nlevels > 2 && use_mf_transfer(m, 0) && f.r && f.d;
 }
@@ -5848,13 +6038,18 @@ template <int H>
 int launch_gtg_solve_t(const GtGStencilDev& S, const double* b, const double* diag, const ChebK& ck, double* out,
                        hipStream_t st, GtgD dv = GtgD{}) {
     const bool part = S.h != 0;
+    // every staged cell of a tile (tile + H + 1 each side) must wrap onto the grid at most once (the staging's periodic
+    // fold subtracts n once): refuse smaller grids here, whatever the caller checked (gtg_fused_ok)
+    if (S.n < kGTW + kGTH + 2 * H)
+        return set_error(MPBP_ERR_ARG, "gtg_solve: a %d-sweep fused solve needs n >= %d (n = %d)", H + 1,
+                         kGTW + kGTH + 2 * H, S.n);
     const int rows = part ? S.L + 2 * S.ext : S.n;
     const int64_t tiles = (int64_t)((S.n + kGTW - 1) / kGTW) * ((rows + kGTH - 1) / kGTH);
     const bool db = dv.Y != nullptr;
     if (db && part) return set_error(MPBP_ERR_ARG, "gtg_solve: the fused D right-hand side is one-GPU only");
     // 512 lanes own rings 1 .. H - 1 one cell each (140 (H - 1) + 4 H (H - 1) <= 512 cells): H <= 4
     if constexpr (H <= 4) {
-        if (g_gtg_tpb == 512) {
+        if (KO().gtg_tpb == 512) {
             if (db) k_gtg_solve<H, false, 512, true><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, ck, out, dv);
             else if (part) k_gtg_solve<H, true, 512, false><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, ck, out, dv);
             else k_gtg_solve<H, false, 512, false><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, ck, out, dv);
@@ -5874,7 +6069,7 @@ int launch_gtg_solve_t(const GtGStencilDev& S, const double* b, const double* di
 // part: under a row partition (the CA schedule's solves), else one GPU.
 bool gtg_fused_ok(const mpbp_schur_plan* p, bool part = false) {
     const mpbp_inner_solver& in = p->inner_P;
-    return g_gtg_fused && p->pg_stencil && (p->halo != nullptr) == part && in.kind == MPBP_INNER_CHEBYSHEV &&
+    return KO().gtg_fused && p->pg_stencil && (p->halo != nullptr) == part && in.kind == MPBP_INNER_CHEBYSHEV &&
            in.sweeps >= 2 && in.sweeps <= 6 && in.lmax > in.lmin && in.lmin >= 0.0 &&
            p->f_prm.n >= kGTW + kGTH + 2 * (in.sweeps - 1);
 }
@@ -5907,6 +6102,36 @@ int gtg_solve_fused(const mpbp_schur_plan* p, const double* b, double* out, hipS
     }
 }
 
+}  // namespace
+
+extern "C" int mpbp_gtg_stencil_cheb_solve(const mpbp_stokes_params* prm, const double* cell, const double* b,
+                                           const double* diag, double lmin, double lmax, int32_t sweeps,
+                                           double* x_out, void* stream) {
+    if (!prm || !cell || !b || !diag || !x_out || b == x_out || sweeps < 2 || sweeps > 6 || !(lmax > lmin) ||
+        !(lmin >= 0.0))
+        return set_error(MPBP_ERR_ARG, "gtg_stencil_cheb_solve: bad args (2..6 sweeps, 0 <= lmin < lmax)");
+    PGDev P;
+    const int rc = make_pgstencil(prm, cell, nullptr, &P);
+    if (rc) return rc;
+    ChebK ck{};
+    double c1[64] = {}, c2[64] = {};
+    cheb_coeffs(lmin, lmax, sweeps, c1, c2);
+    for (int s = 0; s < sweeps; ++s) {
+        ck.c1[s] = c1[s];
+        ck.c2[s] = c2[s];
+    }
+    const GtGStencilDev S{P};
+    const hipStream_t st = as_stream(stream);
+    switch (sweeps - 1) {
+    case 1: return launch_gtg_solve_t<1>(S, b, diag, ck, x_out, st);
+    case 2: return launch_gtg_solve_t<2>(S, b, diag, ck, x_out, st);
+    case 3: return launch_gtg_solve_t<3>(S, b, diag, ck, x_out, st);
+    case 4: return launch_gtg_solve_t<4>(S, b, diag, ck, x_out, st);
+    default: return launch_gtg_solve_t<5>(S, b, diag, ck, x_out, st);
+    }
+}
+
+namespace {
 // The first sweep of a Gt_G Chebyshev solve staging a precomputed x0 = d0 (one GPU, matrix-free Gt_G).
 int gtg_first_sweep_x0(const mpbp_schur_plan* p, const double* x0, const double* b, double c1, double c2, double* d,
                        const double* sub, double* xo, int store_d, hipStream_t st) {
@@ -5932,7 +6157,7 @@ int f_pair(const mpbp_schur_plan* p, int ext, const double* x_in, const double* 
         rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &P);
     }
     if (rc) return rc;
-    if (ext < 0 && g_f_tile && ftile_ok(P.n))   // one GPU: the pair on 2D tiles
+    if (ext < 0 && KO().f_tile && ftile_ok(P.n))   // one GPU: the pair on 2D tiles
         return launch_ftile<false>(P, FTile{x_in, dir, b, sub, x_out, nullptr, c1a, c2a, c1b, c2b}, st, bs);
     return launch_march2(P, Fused2{x_in, dir, b, sub, x_out, nullptr, c1a, c2a, c1b, c2b}, st, bs);
 }
@@ -5982,7 +6207,7 @@ int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag
         return set_error(MPBP_ERR_ARG, "unknown inner solver %d", in.kind);
     }
     // tolerance-mode F on one GPU: the whole solve as one launch
-    if (cheb && f_pair_ok(c.p) && g_f_solve && op.in.stencil && op.in.sop == SOP_F && op.bd.empty && op.in.which == 0 &&
+    if (cheb && f_pair_ok(c.p) && KO().f_solve && op.in.stencil && op.in.sop == SOP_F && op.bd.empty && op.in.which == 0 &&
         !c.p->halo && fsolve_ok(K, c.p->f_prm.n)) {
         FStencilDev P;
         int rc = make_fstencil(&c.p->f_prm, c.p->f_cell, c.p->f_uface, c.p->f_vface, nullptr, &P);
@@ -6003,8 +6228,7 @@ int inner_solve(const Ctx& c, int32_t kind, const OpPair& op, const double* diag
         s = 2;
     } else {
         const double* s0 = (K == 1) ? sub : nullptr;
-        rc = cheb ? mpbp_cheb_init(nrows, b, diag, c2[0], dir, s0, cur, (void*)c.st)
-                  : mpbp_jacobi_init(nrows, b, diag, s0, cur, (void*)c.st);
+        rc = op_init(op.in, nrows, cheb, b, diag, c2[0], dir, s0, cur, c.st);
         if (rc) return rc;
     }
     // tolerance-mode F on one GPU: the last two sweeps as one fused launch
@@ -6057,16 +6281,16 @@ int f_solve_gx(const Ctx& c, const double* xp, const mpbp_inner_solver& in, doub
     rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &G);
     if (rc) return rc;
     const GxB bs{xp, G.d_p, G.inv, G.minv, G.n};
-    if (f_pair_ok(p) && g_f_solve && fsolve_ok(K, P.n))   // the whole solve as one launch
+    if (f_pair_ok(p) && KO().f_solve && fsolve_ok(K, P.n))   // the whole solve as one launch
         return profiled(p, profile, c.st, [&] { return launch_fsolve(P, K, c1, c2, nullptr, sub, dst, c.st, bs); });
     double* cur = K == 2 ? dst : pong;
-    if (p->f_numerics == MPBP_NUMERICS_FAST && g_f_tile && ftile_ok(P.n))   // x0 and sweep 1 on 2D tiles
+    if (p->f_numerics == MPBP_NUMERICS_FAST && KO().f_tile && ftile_ok(P.n))   // x0 and sweep 1 on 2D tiles
         rc = launch_ftile<true>(P, FTile{nullptr, nullptr, nullptr, K == 2 ? sub : nullptr, cur, K == 2 ? nullptr : dir,
                                          0.0, c2[0], c1[1], c2[1]}, c.st, bs);
     else
     rc = with_f_policy(P, p->f_numerics == MPBP_NUMERICS_FAST, [&](const auto& Q) {
         return launch_march_init(Q, nullptr, c2[0], EpiChebFirst{nullptr, dir, c1[1], c2[1], K == 2 ? sub : nullptr, cur,
-                                                                 K == 2 ? 0 : 1}, g_march_rows, c.st, bs);
+                                                                 K == 2 ? 0 : 1}, KO().march_rows, c.st, bs);
     });
     if (rc) return rc;
     for (int s = 2; s < K;) {
@@ -6082,7 +6306,7 @@ int f_solve_gx(const Ctx& c, const double* xp, const mpbp_inner_solver& in, doub
         else
             rc = with_f_policy(P, p->f_numerics == MPBP_NUMERICS_FAST, [&](const auto& Q) {
                 return launch_march(Q, XPlain{cur}, EpiCheb{cur, nullptr, nullptr, dir, c1[s], c2[s], last ? sub : nullptr,
-                                                            nxt, last ? 0 : 1}, g_march_rows, c.st, bs);
+                                                            nxt, last ? 0 : 1}, KO().march_rows, c.st, bs);
             });
         if (rc) return rc;
         if (rec) {
@@ -6133,7 +6357,7 @@ int ca_inner_solve(const Ctx& c, int32_t sop, const double* b, const double* dia
         if (q.halo >= d_out + K - 1) return gtg_solve_fused(p, b, dst, c.st, &q, diag_ext);
     }
     // tolerance-mode F: the whole solve as one tiled launch over the owned + d_out ghost rows
-    if (cheb && sop == SOP_F && f_pair_ok(p) && g_f_solve && fsolve_ok(K, p->f_prm.n)) {
+    if (cheb && sop == SOP_F && f_pair_ok(p) && KO().f_solve && fsolve_ok(K, p->f_prm.n)) {
         const mpbp_row_part q = stencil_part(ext_op(p, SOP_F, d_out));
         FStencilDev P;
         int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, &P);
@@ -6190,7 +6414,7 @@ int ca_f_solve_gx(const Ctx& c, const double* xp, const mpbp_inner_solver& in, d
         return make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, P);
     };
     FStencilDev P;
-    if (f_pair_ok(p) && g_f_solve && fsolve_ok(K, p->f_prm.n) && bs.h >= K) {   // the whole solve as one launch
+    if (f_pair_ok(p) && KO().f_solve && fsolve_ok(K, p->f_prm.n) && bs.h >= K) {   // the whole solve as one launch
         if ((rc = fpol(0, &P))) return rc;
         if (P.h >= K - 1)
             return profiled(p, profile, c.st, [&] { return launch_fsolve(P, K, c1, c2, nullptr, sub, dst, c.st, bs); });
@@ -6199,7 +6423,7 @@ int ca_f_solve_gx(const Ctx& c, const double* xp, const mpbp_inner_solver& in, d
     double* cur = K == 2 ? dst : pong;
     rc = with_f_policy(P, p->f_numerics == MPBP_NUMERICS_FAST, [&](const auto& Q) {
         return launch_march_init(Q, nullptr, c2[0], EpiChebFirst{nullptr, dir, c1[1], c2[1], K == 2 ? sub : nullptr, cur,
-                                                                 K == 2 ? 0 : 1}, g_march_rows, c.st, bs);
+                                                                 K == 2 ? 0 : 1}, KO().march_rows, c.st, bs);
     });
     if (rc) return rc;
     for (int s = 2; s < K;) {
@@ -6216,7 +6440,7 @@ int ca_f_solve_gx(const Ctx& c, const double* xp, const mpbp_inner_solver& in, d
             if ((rc = fpol(K - 1 - s, &P))) return rc;
             rc = with_f_policy(P, p->f_numerics == MPBP_NUMERICS_FAST, [&](const auto& Q) {
                 return launch_march(Q, XPlain{cur}, EpiCheb{cur, nullptr, nullptr, dir, c1[s], c2[s], last ? sub : nullptr,
-                                                            nxt, last ? 0 : 1}, g_march_rows, c.st, bs);
+                                                            nxt, last ? 0 : 1}, KO().march_rows, c.st, bs);
             });
         }
         if (rc) return rc;
@@ -6298,6 +6522,8 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
     for (int i = 0; i < 7; ++i)
         if (!p->wp[i]) return set_error(MPBP_ERR_ARG, "schur_apply: missing pressure workspace");
     if (!p->wu_owned || !p->diag_F || !p->diag_P) return set_error(MPBP_ERR_ARG, "schur_apply: missing operands");
+    if (int rc = check_opts(p->opts, "schur_apply")) return rc;
+    const OptsScope scope(p->opts);
     const Ctx c{p, as_stream(stream)};
     // the CA schedule needs every operator but Gt_F_G matrix-free on the marching kernel; otherwise the
     // per-sweep exchanges below (its deeper halos serve them as well)
@@ -6339,7 +6565,7 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
     rc = inner_solve(c, MPBP_VEC_VELOCITY, F, p->diag_F, p->inner_F, p->nu, v_u, Y, nullptr, U0, U1, Ud, true);
     if (rc) return rc;
     // 2.+3. fused: the first Gt_G solve builds rhs = D Finv_v + v_p itself          solve.py:259, 265
-    if (gfuse && g_gtg_drhs && p->pg_stencil && !px0) {
+    if (gfuse && KO().gtg_drhs && p->pg_stencil && !px0) {
         rc = gtg_solve_fused(p, nullptr, Pxa, c.st, nullptr, nullptr, GtgD{Y, v_p});
         if (rc) return rc;
     } else {
@@ -6361,9 +6587,9 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
     const bool qx0 = px0 && p->q13;
     if (qx0)
         rc = launch_q13(p->q13_n, p->q13, Pxa, EpiStoreX0{Pxb, p->diag_P, pc2[0], P0}, c.st,
-                        g_q13_sym && p->f_numerics == MPBP_NUMERICS_FAST);
+                        KO().q13_sym && p->f_numerics == MPBP_NUMERICS_FAST);
     else if (p->q13 && !p->halo)   // tolerance mode: the symmetric product's upper half (k_q13<SYM>)
-        rc = launch_q13(p->q13_n, p->q13, Pxa, EpiStore{Pxb}, c.st, g_q13_sym && p->f_numerics == MPBP_NUMERICS_FAST);
+        rc = launch_q13(p->q13_n, p->q13, Pxa, EpiStore{Pxb}, c.st, KO().q13_sym && p->f_numerics == MPBP_NUMERICS_FAST);
     else
         rc = two_phase(c, MPBP_VEC_PRESSURE, Pxa, Q,
                        [&](const OpRef& o) { return op_spmv(o, MPBP_SPMV_STORE, Pxa, nullptr, Pxb, c.st); });
@@ -6438,6 +6664,8 @@ int mpbp_mg_transfer_fill(int32_t n, int32_t nfields, const int32_t* kinds, int3
 
 int mpbp_mg_solve(const mpbp_mg* mg, const double* b, const double* sub, double* x_out, void* stream) {
     if (!mg || !b || !x_out || mg->nlevels < 2 || !mg->levels) return set_error(MPBP_ERR_ARG, "mg_solve: bad args");
+    if (int rc = check_opts(mg->opts, "mg_solve")) return rc;
+    const OptsScope scope(mg->opts);
     const mpbp_mg_level& L = mg->levels[0];
     if (check_csr(&L.A)) return MPBP_ERR_ARG;
     if (mg->part_levels < 0 || mg->part_levels >= mg->nlevels || (mg->part_levels > 0 && (!mg->halo || !mg->gather)))

@@ -63,7 +63,8 @@ class RowPartition:
         start = 0   # contiguous, in rank order, every rank at least one row (the halo and gather layouts assume it)
         for k, (a, b) in enumerate(self.bounds):
             if a != start or b < (0 if self.allow_empty else 1):
-                raise ValueError(f"row bounds {self.bounds}: rank {k} must start at row {start} and own >= 1 row")
+                raise ValueError(f"row bounds {self.bounds}: rank {k} must start at row {start} and own "
+                                 f"{'>= 0 rows' if self.allow_empty else '>= 1 row'}")
             start += b
         self.r0, self.L = self.bounds[self.rank]
         self.r1 = self.r0 + self.L
@@ -273,21 +274,38 @@ class RcclHalo:
     The communicator is libmpbp's own (its unique id travels over `group`); world = 1 exchanges with
     itself (the periodic wrap)."""
 
-    # one RCCL communicator per process group: the first RcclHalo of a group opens it (collective), later ones --
-    # the partitioned operator and preconditioner of one solve, the multigrid levels -- share it
-    # (mpbp_halo_create_shared, local), so a rank holds one communicator whatever it builds
+    # one RCCL communicator per process group: the first RcclHalo of a group opens it (collective), later ones -- the
+    # partitioned preconditioners and their multigrid levels -- share it (mpbp_halo_create_shared, local), so a rank
+    # holds one communicator however many preconditioners it builds.  The key is the group's global ranks (stable, unlike
+    # id(group)), and whether to share is agreed over the group (an all-reduce MIN of "this rank has a live one"): if
+    # any rank lacks it, every rank opens a new communicator together, so no rank waits in a collective the others skip.
     _by_group: dict = {}
 
     @staticmethod
     def _group_key(part: RowPartition, group):
-        return (id(group) if group is not None else "WORLD", part.world, part.rank)
+        import torch.distributed as dist
+        g = group if group is not None else dist.group.WORLD
+        return (tuple(dist.get_process_group_ranks(g)), part.world, part.rank)
+
+    @staticmethod
+    def _agree(have: bool, part: RowPartition, group) -> bool:
+        if part.world == 1:
+            return have
+        import torch.distributed as dist
+        dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+        t = torch.tensor([1 if have else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+        return bool(t.item())
 
     def __init__(self, part: RowPartition, h_u: int, h_p: int, group=None, overlap: bool = False, share: bool = True):
+        """share=False opens a communicator of this object's own (collective over `group`, every rank must pass the same
+        value); share=True attaches to the group's existing one when every rank still holds it."""
         import weakref
-        key = self._group_key(part, group)
+        key = self._group_key(part, group) if share else None
         ref = RcclHalo._by_group.get(key) if share else None
         base = ref() if ref is not None else None
-        if base is not None and base.handle:
+        have = base is not None and bool(base.handle)
+        if share and self._agree(have, part, group):
             self.handle = ctypes.c_void_p()
             check(lib().mpbp_halo_create_shared(base.handle, part.n, part.r0, part.L, h_u, h_p,
                                                 ctypes.byref(self.handle)))
@@ -591,6 +609,23 @@ def _dist_info(group):
     return dist, dist.get_world_size(group), dist.get_rank(group), dist.get_backend(group)
 
 
+def _phase_clock(out: dict):
+    """stamp(name): with MPBP_SETUP_TIMING=1, synchronise the device and record the seconds since the previous stamp
+    under `name` in `out`; otherwise nothing (no extra synchronisation in production setups)."""
+    if os.environ.get("MPBP_SETUP_TIMING", "0") != "1":
+        return lambda name: None
+    import time
+    torch.cuda.synchronize()
+    last = [time.perf_counter()]
+
+    def stamp(name):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        out[name] = out.get(name, 0.0) + (t - last[0])
+        last[0] = t
+    return stamp
+
+
 class DistributedMatrix:
     """A row-partitioned operator of the MAC-grid system: the operator matvec b = A u of apply.py:72 and the FGMRES
     operator of solve.py:285 (A @ xk, solve.py:166) over the ranks of `group`, one per GPU.
@@ -643,7 +678,10 @@ class DistributedMatrix:
         self._rccl = self._ex = None
         if self.partitioned:
             if self.halo_impl == "rccl":
-                self._rccl = RcclHalo(part, 1, 1, group, overlap=False)
+                # its own communicator: its exchanges run eagerly on the halo object's side stream (overlap), the
+                # preconditioner's in order on the caller's stream inside a replayed graph -- the two are never mixed
+                # on one communicator
+                self._rccl = RcclHalo(part, 1, 1, group, overlap=False, share=False)
                 self.kind = self._rccl.add_kind(part, nfields, self.h, overlap=overlap)
             else:
                 self._ex = HaloExchanger(part, nfields, self.h, dev, group)
@@ -704,11 +742,17 @@ class DistributedSchurPreconditioner(PlanProfiling):
     def __init__(self, n, xi, eta_n, eta_s, c=1.0, d_u=-1.0, inner_F=None, inner_P=None, group=None,
                  device=None, layout="sell", f_mode="auto", pg_mode="auto", halo="auto", self_halo=False,
                  halo_overlap=False, ca="auto", fuse_g=True, mg_min_cells=1 << 14, mg_part_levels=None,
-                 local_products=True, numerics="exact"):
+                 local_products=True, numerics="exact", kernel_opts=None):
         import torch.distributed as dist
         from .preconditioner import MultiphaseBlockPreconditioner
         from .solve import InnerSolver, _check_numerics
         self.numerics = _check_numerics(numerics)
+        # this preconditioner's kernel choices (process defaults now + overrides); q13_sym does not apply here: the
+        # partition multiplies Gt_F_G's full rows
+        self.kernel_opts = _lib.kernel_opts(kernel_opts)
+        # setup phase timings (MPBP_SETUP_TIMING=1: synchronise and stamp each phase; tools/setup_timing.py)
+        self.setup_phases = {}
+        _stamp = _phase_clock(self.setup_phases)
         dev = torch.device(device or "cuda")
         self.device = dev
         world = dist.get_world_size(group)
@@ -742,6 +786,7 @@ class DistributedSchurPreconditioner(PlanProfiling):
             D = bp.assemble_rows(_lib.OP_D, rows_p, **akw)
             G = bp.assemble_rows(_lib.OP_G, rows_u, **akw)
             F.stencil, D.stencil, G.stencil = st_F, st_D, st_G
+            _stamp("assemble_owned_rows")
             sweeps = lambda k: k.sweeps if k.kind in ("jacobi", "chebyshev") else 1   # noqa: E731
             sup = min(n, sweeps(ik_f) + sweeps(ik_p) + 2)
             grid_rows = np.unique(np.arange(part.r0 - sup, part.r1 + sup) % n) if part.L + 2 * sup < n \
@@ -751,12 +796,16 @@ class DistributedSchurPreconditioner(PlanProfiling):
             sup_u = torch.from_numpy(sup_u.astype(np.int32)).to(dev)
             Fs = bp.assemble_rows(_lib.OP_F, sup_u, global_shape=True, **akw)
             Gs = bp.assemble_rows(_lib.OP_G, sup_u, global_shape=True, **akw)
+            _stamp("assemble_support_rows")
             GtG, GtFG = bp.commutator_products(Fs, D, Gs)   # this rank's pressure rows, global columns
+            _stamp("commutator_products")
             GtG.stencil = _gtg_stencil(D, G)
             del Fs
         else:
             _, _, F, D, G = bp.get_big_A_matrix(**akw)
+            _stamp("assemble_global")
             GtG, GtFG = bp.commutator_products(F, D, G)
+            _stamp("commutator_products")
         lp = self.local_products
         if f_mode not in ("auto", "stencil", "assembled"):
             raise ValueError("f_mode must be 'auto', 'stencil' or 'assembled'")
@@ -782,6 +831,7 @@ class DistributedSchurPreconditioner(PlanProfiling):
         else:
             self.inner_P = (inner_P or InnerSolver()).resolve(GtG, GtG.diagonal())
         mg_any = "mg" in (self.inner_F.kind, self.inner_P.kind)
+        _stamp("inner_bounds")
 
         def reach(M, rows, local=False):
             sub = M if local else M.extract(rows, torch.arange(M.shape[1], dtype=torch.int32, device=dev), M.shape[1])
@@ -808,6 +858,7 @@ class DistributedSchurPreconditioner(PlanProfiling):
                 self.h_u = max(self.h_u, self.mg_F.h0)
             if isinstance(self.mg_P, PartitionedMultigrid):
                 self.h_p = max(self.h_p, self.mg_P.h0)
+        _stamp("halo_reach_and_multigrid")
         # communication-avoiding schedule (mpbp_schur_plan.ca): v's halo and x_b's halo only, deep enough for
         # every matrix-free operator to also compute the ghost rows its successors read
         if ca not in ("auto", True, False):
@@ -842,6 +893,7 @@ class DistributedSchurPreconditioner(PlanProfiling):
                 del D_ext
             else:
                 diag_P_glob = GtG.diagonal()
+        _stamp("ca_ghost_diagonals")
         if lp:   # already this rank's rows, in owned order
             own_u = torch.arange(rows_u.numel(), dtype=torch.int32, device=dev)
             own_p = torch.arange(rows_p.numel(), dtype=torch.int32, device=dev)
@@ -869,6 +921,7 @@ class DistributedSchurPreconditioner(PlanProfiling):
             self.diag_P_ext = diag_P_glob[gp].contiguous()
             del diag_P_glob, diag_F_glob
 
+        _stamp("extract_ghost_layout")
         mats = {"F": (self.F, nu), "D": (self.D, nu), "G": (self.G, np_), "P": (self.GtG, np_),
                 "Q": (self.GtFG, np_)}
         self._pieces = {}
@@ -883,6 +936,7 @@ class DistributedSchurPreconditioner(PlanProfiling):
             else:
                 self._pieces[key] = (M.plan_blocks(rows=inner) if inner else None,
                                      M.plan_blocks(rows=bnd) if bnd else None)
+        _stamp("sell_layouts")
         f64 = dict(dtype=torch.float64, device=dev)
         self._wu = [torch.zeros(nu_ext, **f64) for _ in range(4)]
         self._wu_owned = torch.zeros(nu, **f64)
@@ -906,8 +960,10 @@ class DistributedSchurPreconditioner(PlanProfiling):
                 self.mg_P.build(self._halos, (self._wp[4], self._wp[5]), self.diag_P, self.h_p, kind0=_lib.VEC_PRESSURE)
         else:
             self._cb = _lib.HALO_FN()
+        _stamp("halo_and_workspace")
         self._prof = None
         self._plan = self._make_plan(world)
+        _stamp("plan")
 
     def _make_plan(self, world):
         p = _lib.SchurPlan()
@@ -960,6 +1016,7 @@ class DistributedSchurPreconditioner(PlanProfiling):
         p.ca, p.ca_reach_q = (1 if self.ca else 0), self.ca_q
         p.fuse_g = 1 if self.fuse_g else 0
         p.f_numerics = _lib.NUMERICS_FAST if self.numerics == "fast" else _lib.NUMERICS_EXACT
+        p.opts = ctypes.pointer(self.kernel_opts)
         if self.ca:
             if self._rccl is not None and not self._rccl.overlap:   # v's two halves in one RCCL group
                 p.halo_pair = self._rccl.pair_fn
@@ -979,8 +1036,10 @@ class DistributedSchurPreconditioner(PlanProfiling):
         if out is None:
             out = torch.empty_like(v)
         check(lib().mpbp_schur_apply(ctypes.byref(self._plan), ptr(v), ptr(out), stream_handle()))
-        if self._rccl is not None:
-            self._rccl.check()
+        # every exchange and gather of the apply (its own halos and the partitioned multigrid levels') reports through
+        # _Halos: the RCCL object's status, or the first exception a host-staged callback latched
+        if self._halos is not None:
+            self._halos.check()
         return out
 
     def capture(self, v: torch.Tensor, out: torch.Tensor):

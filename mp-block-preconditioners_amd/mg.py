@@ -203,12 +203,14 @@ class Multigrid:
     sell     SELL-64 copies of the operators / transfers and the dense coarse kernel (False: CSR throughout)
     fine_sell  also a SELL copy of level 0's operator (the standalone solve's fine level)
     svl_min_rows  levels >= 1 with more rows get a stencil-values copy (StencilValues; None: never) -- used where the
-             grouped small-level kernel is not (mpbp_set_mg_group_rows)
+             grouped small-level kernel is not (kernel option mg_group_rows)
+    kernel_opts  overrides of the process-default kernel choices for this hierarchy's standalone solve (_lib.KernelOpts
+             field names)
     """
 
     def __init__(self, A: DeviceCSR, n: int, fields=FIELDS_PRESSURE, pre: int = 2, post: int = 2, cycles: int = 1,
                  ratio: float = 4.0, coarsest: int = 8, diag: torch.Tensor | None = None, sell: bool = True,
-                 fine_sell: bool = True, svl_min_rows: int | None | str = "default"):
+                 fine_sell: bool = True, svl_min_rows: int | None | str = "default", kernel_opts: dict | None = None):
         nf = len(fields)
         if A.shape != (nf * n * n, nf * n * n):
             raise ValueError(f"operator {A.shape} is not {nf} fields of a {n} x {n} grid")
@@ -281,6 +283,9 @@ class Multigrid:
         self._mg = _lib.Mg(len(self.ops), cycles, ctypes.cast(self._levels, ctypes.POINTER(_lib.MgLevel)),
                            self.coarse_inv.cstruct(), self.coarse_inv.blocks.cstruct(),
                            self.coarse_dense.data_ptr() if self.coarse_dense is not None else None)
+        # the standalone solve's kernel choices (inside a Schur apply the preconditioner's own govern)
+        self.kernel_opts = _lib.kernel_opts(kernel_opts)
+        self._mg.opts = ctypes.pointer(self.kernel_opts)
         set_transfer_kinds(self._mg, self.fields, n)
 
     def set_matrix_free_transfers(self, on: bool):

@@ -77,8 +77,11 @@ NUMERICS = ("exact", "fast")
 def _check_numerics(numerics: str) -> str:
     """'exact': the matrix-free F sweeps perform the assembly's IEEE operations in CSR order (bit-identical to the
     sequential oracle); 'fast': the same operator regrouped per coefficient and FMA-contracted with reciprocal diagonals
-    (MPBP_NUMERICS_FAST), north_star's bar -- within 1e-12 relative inf-norm of the oracle apply.  Only the
-    matrix-free F rows change; every other kernel is the same in both."""
+    (MPBP_NUMERICS_FAST), north_star's bar -- within 1e-12 relative inf-norm of the oracle apply.  What 'fast'
+    changes: the matrix-free F rows (inner solves, multigrid level-0 smoothing and residuals); on one GPU Gt_F_G x from
+    the diamond's symmetric half (kernel option q13_sym, kept only when the stored product is symmetric to 1e-14); and
+    the multigrid hierarchies' level 1 applied matrix-free as R0 (F (P0 x)) / R0 (Gt_G (P0 x)) (kernel options
+    mg_galerkin_mf / mg_galerkin_mf_p).  D, G, Gt_G and the other kernels compute the same bits in both modes."""
     if numerics not in NUMERICS:
         raise ValueError(f"numerics must be one of {NUMERICS}")
     return numerics
@@ -119,7 +122,22 @@ class DeviceEvent:
 
 
 class PlanProfiling:
-    """hipEvent pairs recorded by mpbp_schur_apply around every inner-F SpMV sweep (bench.py)."""
+    """What the Schur preconditioners share around their mpbp_schur_plan: the plan's kernel choices
+    (set_kernel_opts) and hipEvent pairs recorded by mpbp_schur_apply around every inner-F SpMV sweep (bench.py)."""
+
+    def set_kernel_opts(self, **kw):
+        """Change this preconditioner's kernel choices (mpbp_kernel_opts field names; others untouched).  The next apply
+        or capture uses them; graphs captured before keep the choices they were captured with.  Every choice computes
+        the same bits except q13_sym (tolerance mode), which stays 0 where the stored Gt_F_G is not symmetric."""
+        names = {f for f, _ in _lib.KernelOpts._fields_ if f != "reserved"}
+        for k, v in kw.items():
+            if k not in names:
+                raise ValueError(f"unknown kernel option {k!r} (known: {sorted(names)})")
+            if k == "q13_sym" and v and getattr(self, "q13_asymmetry", None) is not None:
+                a, m = self.q13_asymmetry
+                if not a <= 1e-14 * m:
+                    raise ValueError(f"q13_sym: this Gt_F_G is not symmetric (max |Q - Q^T| {a:.3g}, max |Q| {m:.3g})")
+            setattr(self.kernel_opts, k, int(v))
 
     def enable_profiling(self, capacity: int):
         evs = (ctypes.c_void_p * (2 * capacity))()
@@ -226,9 +244,13 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
 
     def __init__(self, F, D, G, GtG=None, GtFG=None, inner_F: InnerSolver | None = None,
                  inner_P: InnerSolver | None = None, device=None, layout: str = "sell", f_mode: str = "auto",
-                 pg_mode: str = "auto", q_mode: str = "auto", fuse_g: bool = True, numerics: str = "exact"):
+                 pg_mode: str = "auto", q_mode: str = "auto", fuse_g: bool = True, numerics: str = "exact",
+                 kernel_opts: dict | None = None):
         dev = torch.device(device or (F.device if isinstance(F, DeviceCSR) else "cuda"))
         self.numerics = _check_numerics(numerics)
+        # this preconditioner's kernel choices (mpbp_kernel_opts): the process defaults now, with `kernel_opts`
+        # overrides -- later mpbp_set_* calls and other preconditioners' choices do not affect it
+        self.kernel_opts = _lib.kernel_opts(kernel_opts)
         self.F, self.D, self.G = (_device_csr(M, dev) for M in (F, D, G))
         if GtG is None or GtFG is None:
             GtG, GtFG = MultiphaseBlockPreconditioner.commutator_products(self.F, self.D, self.G)
@@ -278,6 +300,15 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
         # 104 B per row instead of 156), "assembled" the CSR / SELL copy; "auto" = diamond whenever Gt_F_G is
         # the n^2 x n^2 periodic-grid product (n >= 5), else assembled.
         self.q13 = _q13_layout(self.GtFG, q_mode)
+        # tolerance mode reads Gt_F_G's symmetric half only when the stored product IS symmetric (to 1e-14 of its
+        # largest entry; G^T F G is, to rounding) -- a caller's non-symmetric Gt_F_G keeps all 13 slots
+        self.q13_asymmetry = None
+        if self.q13 is not None and self.numerics == "fast":
+            a = (ctypes.c_double * 2)()
+            check(lib().mpbp_q13_asymmetry(self.q13[0], ptr(self.q13[1]), a, stream_handle()))
+            self.q13_asymmetry = (a[0], a[1])
+            if not a[0] <= 1e-14 * a[1]:
+                self.kernel_opts.q13_sym = 0
         # the second F solve recomputes its right-hand side G x_p inside its sweeps (no G launch, W never stored)
         # when F and G are both matrix-free and F's inner solve is Chebyshev with >= 2 sweeps; same bits
         self.fuse_g = bool(fuse_g and self.f_stencil is not None and self.pg_stencil is not None
@@ -330,6 +361,7 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
             p.mg_P = ctypes.pointer(self.mg_P.cstruct())
         p.fuse_g = 1 if self.fuse_g else 0
         p.f_numerics = _lib.NUMERICS_FAST if self.numerics == "fast" else _lib.NUMERICS_EXACT
+        p.opts = ctypes.pointer(self.kernel_opts)
         return p
 
     def sell_of(self, key):

@@ -127,3 +127,42 @@ def test_ext_rows_inverts_colmap(n, world, h):
                 assert np.all(cm[gid] >= 0) and np.array_equal(gid[cm[gid]], gid)
             else:           # one rank: the periodic ghosts duplicate owned rows
                 assert np.array_equal(np.sort(np.unique(gid)), np.arange(nf * n * n))
+
+
+def test_host_staged_halo_failure_is_raised():
+    """a host-staged (torch / gloo) exchange that fails inside the C apply is latched by the callback (ctypes
+    would swallow it) and raised by _Halos.check(), which DistributedSchurPreconditioner.apply calls after every apply;
+    the latch is cleared so a later apply runs its exchanges again."""
+    from mp_block_preconditioners_amd import _lib
+    from mp_block_preconditioners_amd.distributed import _Halos
+
+    class Boom:
+        calls = 0
+
+        def begin(self, x):
+            Boom.calls += 1
+            raise OSError("peer went away")
+
+        def end(self, x):
+            pass
+
+    h = _Halos("torch", None, None, "cpu")
+    h._ex[0] = Boom()
+    x = torch.zeros(8, dtype=torch.float64)
+    h.register(x)
+    h.fn(None, 0, x.data_ptr(), _lib.HALO_BEGIN, None)
+    h.fn(None, 0, x.data_ptr(), _lib.HALO_BEGIN, None)   # latched: no second attempt inside the same apply
+    assert Boom.calls == 1
+    with pytest.raises(RuntimeError, match="peer went away"):
+        h.check()
+    h.check()                                             # cleared
+    h.fn(None, 0, x.data_ptr(), _lib.HALO_BEGIN, None)
+    assert Boom.calls == 2
+
+
+def test_row_partition_error_message():
+    from mp_block_preconditioners_amd.distributed import RowPartition
+    with pytest.raises(ValueError, match=">= 1 row"):
+        RowPartition(4, 2, 0, bounds=((0, 4), (4, 0)))
+    with pytest.raises(ValueError, match=">= 0 rows"):
+        RowPartition(4, 2, 0, bounds=((0, 4), (5, 0)), allow_empty=True)

@@ -228,12 +228,6 @@ def test_1024_mg_apply_properties():
     torch.cuda.synchronize()
     y1h = y1.cpu().numpy()
     assert _bits_equal(out, y1h)                                                          # graph == eager
-    try:
-        for setter, off in ((lib().mpbp_set_mg_svl, 0), (lib().mpbp_set_mg_group_rows, 0),
-                            (lib().mpbp_set_mg_mf_transfer, 0)):
-            check(setter(off))
-            assert _bits_equal(pc.apply(v1), y1h), setter
-    finally:
-        check(lib().mpbp_set_mg_svl(1))
-        check(lib().mpbp_set_mg_group_rows(65536))
-        check(lib().mpbp_set_mg_mf_transfer(1))
+    for opt in ("mg_svl", "mg_group_rows", "mg_mf_transfer"):   # cumulative, as each kernel form is switched off
+        pc.set_kernel_opts(**{opt: 0})
+        assert _bits_equal(pc.apply(v1), y1h), opt

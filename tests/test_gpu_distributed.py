@@ -27,10 +27,10 @@ def _worker(rank, world, port, n, layout, f_mode, kind, errfile, ca="auto", fuse
         dist.init_process_group("gloo", rank=rank, world_size=world)
         import mp_block_preconditioners_amd as mpb
         from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
-        mpb.lib().mpbp_set_march_rows(kind)
         iF, iP = mpb.InnerSolver("chebyshev", 4), mpb.InnerSolver("chebyshev", 3)
         dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, layout=layout,
-                                             f_mode=f_mode, ca=ca, fuse_g=fuse_g, numerics=numerics)
+                                             f_mode=f_mode, ca=ca, fuse_g=fuse_g, numerics=numerics,
+                                             kernel_opts={"march_rows": kind})
         assert dpc.fuse_g == bool(fuse_g and dpc.ca)
         assert (dpc.f_stencil is not None) == (f_mode != "assembled")
         if ca is True:
@@ -38,26 +38,19 @@ def _worker(rank, world, port, n, layout, f_mode, kind, errfile, ca="auto", fuse
         bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
         _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
         # the reference: the assembled one-GPU apply (exact numerics), or the one-GPU apply with the same fast rows
+        # (the partition multiplies Gt_F_G's full rows: so does the one-GPU reference, q13_sym = 0)
         pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, layout=layout,
-                                           f_mode="assembled" if numerics == "exact" else "stencil", numerics=numerics)
+                                           f_mode="assembled" if numerics == "exact" else "stencil", numerics=numerics,
+                                           kernel_opts={"q13_sym": 0})
         assert (pc.inner_F.lmin, pc.inner_F.lmax) == (dpc.inner_F.lmin, dpc.inner_F.lmax)
         v = torch.from_numpy(np.random.default_rng(5).standard_normal(pc.shape[0])).cuda()
         gids = torch.from_numpy(dpc.local_to_global_rows()).cuda()
-        mpb.lib().mpbp_set_q13_sym(0)   # the partition multiplies Gt_F_G's full rows: so does the one-GPU reference
-        try:
-            ref = pc.apply(v)[gids]
-        finally:
-            mpb.lib().mpbp_set_q13_sym(1)
+        ref = pc.apply(v)[gids]
         for _ in range(2):
+            # (the per-sweep schedule's fast F solves start from x0 = (c2 b) (1 / diag) with the fast reciprocal
+            # diagonals, k_f_fast_init, as the one-GPU fast first sweep: the same bits in both numerics)
             got = dpc.apply(v[gids].contiguous())
-            if numerics == "fast" and not dpc.ca:
-                # the per-sweep schedule starts each F solve with the stored diagonal's x0 = c2 (b / diag) (an exchange
-                # follows it), the one-GPU fast solve with x0 = c2 b (1 / diag) from its recomputed diagonal: north_star's
-                # bar, not bits
-                err = float((got - ref).abs().max() / ref.abs().max())
-                assert err <= 1e-12, err
-            else:
-                assert torch.equal(got, ref), float((got - ref).abs().max())
+            assert torch.equal(got, ref), float((got - ref).abs().max())
         dist.barrier()
         dist.destroy_process_group()
     except BaseException as e:
@@ -102,9 +95,9 @@ def test_distributed_apply_ca_schedule(world, n, layout, ca, fuse_g, tmp_path):
 
 @pytest.mark.parametrize("world,n,ca", [(2, 64, True), (3, 50, True), (2, 64, False)])
 def test_distributed_fast_numerics_matches_single_gpu(world, n, ca, tmp_path):
-    """Tolerance-mode F numerics under the row partition: the CA schedule (the default) runs the same fast rows and
-    updates per grid point as one GPU -- bit for bit; the per-sweep schedule differs only in its initial iterate's
-    diagonal (stored vs recomputed) -- within 1e-12."""
+    """Tolerance-mode F numerics under the row partition: the CA schedule (the default) and the per-sweep schedule (its
+    F solves starting from the fast reciprocal diagonals, k_f_fast_init) run the same fast rows and updates per grid
+    point as one GPU -- bit for bit."""
     errfile = str(tmp_path / "err.txt")
     _spawn(_worker, (world, _free_port(), n, "sell", "stencil", 4, errfile, ca, True, "fast"), world, errfile)
 
@@ -117,11 +110,10 @@ def _self_halo_worker(_index, port, n, halo, f_mode, pg_mode, kind, graph, errfi
         dist.init_process_group("gloo", rank=0, world_size=1)
         import mp_block_preconditioners_amd as mpb
         from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
-        mpb.lib().mpbp_set_march_rows(kind)
         iF, iP = mpb.InnerSolver(*inner[0]), mpb.InnerSolver(*inner[1])
         dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, f_mode=f_mode,
                                              pg_mode=pg_mode, halo=halo, self_halo=True, halo_overlap=overlap,
-                                             ca=ca)
+                                             ca=ca, kernel_opts={"march_rows": kind})
         if ca is True:
             assert dpc.ca
         assert dpc.partitioned and dpc.nu_ext > dpc.nu
@@ -297,8 +289,12 @@ def _inner_pair(spec):
     return mpb.InnerSolver(kf, sf), mpb.InnerSolver(kp, sp)
 
 
-def _mg_worker(rank, world, port, n, inner, min_cells, halo, errfile):
-    """The partitioned Schur apply with multigrid inner solves vs the one-GPU apply."""
+FAST_TWIN = {"mg_galerkin_mf": 0, "mg_galerkin_mf_p": 0, "q13_sym": 0}   # the partition's level-1 and Gt_F_G forms
+
+
+def _mg_worker(rank, world, port, n, inner, min_cells, halo, errfile, numerics="exact"):
+    """The partitioned Schur apply with multigrid inner solves vs the one-GPU apply (fast numerics: the one-GPU twin
+    applies level 1 from its stored Galerkin matrices and Gt_F_G's full rows, as the partition does)."""
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         torch.cuda.set_device(0)
@@ -307,7 +303,7 @@ def _mg_worker(rank, world, port, n, inner, min_cells, halo, errfile):
         from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner, PartitionedMultigrid
         iF, iP = _inner_pair(inner)
         dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, halo=halo,
-                                             self_halo=(world == 1), mg_min_cells=min_cells)
+                                             self_halo=(world == 1), mg_min_cells=min_cells, numerics=numerics)
         for m in (dpc.mg_F, dpc.mg_P):
             if m is not None:
                 assert isinstance(m, PartitionedMultigrid) and 1 <= m.part_levels <= m.g.nlevels - 1
@@ -315,7 +311,8 @@ def _mg_worker(rank, world, port, n, inner, min_cells, halo, errfile):
                     assert m.part_levels >= min(2, m.g.nlevels - 1), (m.part_levels, m.g.sizes)
         bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
         _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
-        pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP)
+        pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, numerics=numerics,
+                                           kernel_opts=FAST_TWIN if numerics == "fast" else None)
         v = torch.from_numpy(np.random.default_rng(8).standard_normal(pc.shape[0])).cuda()
         gids = torch.from_numpy(dpc.local_to_global_rows()).cuda()
         ref = pc.apply(v)[gids]
@@ -345,16 +342,17 @@ MG1 = (("mg", 1), ("mg", 1))
     (2, 64, MG1, 1 << 14, "auto"), (2, 64, MG1, 0, "auto"), (4, 64, MG1, 0, "auto"), (3, 48, MG1, 0, "auto"),
     (3, 50, MG1, 0, "auto"), (2, 64, (("mg", 2), ("chebyshev", 4)), 0, "auto"),
     (2, 64, (("chebyshev", 4), ("mg", 1)), 0, "auto"), (1, 64, MG1, 0, "rccl"), (1, 32, MG1, 0, "torch")])
-def test_partitioned_multigrid_apply_matches_single_gpu(world, n, inner, min_cells, halo, tmp_path):
+@pytest.mark.parametrize("numerics", ["exact", "fast"])
+def test_partitioned_multigrid_apply_matches_single_gpu(world, n, inner, min_cells, halo, numerics, tmp_path):
     """Row 18: multigrid inner solves under the row partition -- level 0 the apply's own matrix-free F / Gt_G, the
     Galerkin levels row-partitioned down to part_levels (ghost rows per operator), the coarser levels all-gathered and
     replicated -- bit for bit against the one-GPU apply (2-4 gloo ranks; ceil-halved partitions at n = 50; the RCCL
     self-exchange, captured)."""
     errfile = str(tmp_path / "err.txt")
-    _spawn(_mg_worker, (world, _free_port(), n, inner, min_cells, halo, errfile), world, errfile)
+    _spawn(_mg_worker, (world, _free_port(), n, inner, min_cells, halo, errfile, numerics), world, errfile)
 
 
-def _fgmres_worker(rank, world, port, n, inner, maxiter, outdir, errfile):
+def _fgmres_worker(rank, world, port, n, inner, maxiter, outdir, errfile, numerics="exact"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         torch.cuda.set_device(0)
@@ -362,7 +360,7 @@ def _fgmres_worker(rank, world, port, n, inner, maxiter, outdir, errfile):
         from mp_block_preconditioners_amd.distributed import solve_distributed
         iF, iP = _inner_pair(inner)
         res = solve_distributed(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, tol=1e-8, maxiter=maxiter,
-                                mg_min_cells=0)
+                                mg_min_cells=0, numerics=numerics)
         np.save(os.path.join(outdir, f"x_{rank}.npy"), res["x_local"].cpu().numpy())
         np.save(os.path.join(outdir, f"rows_{rank}.npy"), res["rows"])
         np.save(os.path.join(outdir, f"hist_{rank}.npy"), np.asarray(res["residuals"]))
@@ -374,19 +372,21 @@ def _fgmres_worker(rank, world, port, n, inner, maxiter, outdir, errfile):
         raise
 
 
-@pytest.mark.parametrize("world,n,inner,maxiter", [(2, 32, (("chebyshev", 4), ("chebyshev", 4)), 40),
-                                                   (3, 48, MG1, 60), (2, 64, MG1, 60)])
-def test_distributed_fgmres_matches_single_gpu(world, n, inner, maxiter, tmp_path):
+@pytest.mark.parametrize("world,n,inner,maxiter,numerics", [
+    (2, 32, (("chebyshev", 4), ("chebyshev", 4)), 40, "exact"), (3, 48, MG1, 60, "exact"), (2, 64, MG1, 60, "exact"),
+    (2, 64, MG1, 60, "fast"), (3, 48, MG1, 60, "fast"), (2, 32, (("chebyshev", 4), ("chebyshev", 4)), 40, "fast")])
+def test_distributed_fgmres_matches_single_gpu(world, n, inner, maxiter, numerics, tmp_path):
     """Row 17: FGMRES (solve.py:285) over the row partition -- the partitioned A, the partitioned preconditioner,
     reproducible inner products reduced over the ranks -- gives the one-GPU solve's residual history and iterate bit
     for bit (the manufactured problem of solve.py:52-80)."""
     import mp_block_preconditioners_amd as mpb
     errfile = str(tmp_path / "err.txt")
-    _spawn(_fgmres_worker, (world, _free_port(), n, inner, maxiter, str(tmp_path), errfile), world, errfile)
+    _spawn(_fgmres_worker, (world, _free_port(), n, inner, maxiter, str(tmp_path), errfile, numerics), world, errfile)
     bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
     A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
     iF, iP = _inner_pair(inner)
-    pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP)
+    pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, numerics=numerics,
+                                       kernel_opts=FAST_TWIN if numerics == "fast" else None)
     _, b = mpb.manufactured_problem(n, 1.0, -1.0, 1.0, 100.0, 1.0)
     hist = []
     x, info = mpb.fgmres(A, torch.from_numpy(b).cuda(), M=pc, tol=1e-8, maxiter=maxiter, residuals=hist)
@@ -401,23 +401,29 @@ def test_distributed_fgmres_matches_single_gpu(world, n, inner, maxiter, tmp_pat
         assert info == 0
 
 
-def _shared_comm_worker(_index, port, n, errfile):
-    """solve_distributed over the RCCL self-exchange: the partitioned operator and preconditioner hold ONE
-    communicator (mpbp_halo_create_shared), and the solve with maxiter / restrt left at their defaults runs."""
+def _comm_worker(_index, port, n, errfile):
+    """solve_distributed over the RCCL self-exchange: the partitioned operator A u holds a communicator of its own (its
+    eager side-stream exchanges never mix with a preconditioner's graph-replayed ones), the partitioned
+    preconditioners of the process group share one (mpbp_halo_create_shared), and the solve with maxiter / restrt left
+    at their defaults runs."""
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=0, world_size=1)
         import mp_block_preconditioners_amd as mpb
-        from mp_block_preconditioners_amd.distributed import solve_distributed
+        from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner, solve_distributed
         res = solve_distributed(n, 1.0, 100.0, 1.0, inner_F=mpb.InnerSolver("mg", 1), inner_P=mpb.InnerSolver("mg", 1),
                                 tol=1e-8, self_halo=True, halo="rccl", mg_min_cells=0)
         dA, M = res["A"], res["M"]
         assert dA._rccl is not None and M._rccl is not None
-        assert dA._rccl.comm != 0 and dA._rccl.comm == M._rccl.comm, (dA._rccl.comm, M._rccl.comm)
-        assert M._rccl.comm_refs == 2, M._rccl.comm_refs
+        assert dA._rccl.comm != 0 and M._rccl.comm != 0 and dA._rccl.comm != M._rccl.comm
+        assert M._rccl.comm_refs == 1 and dA._rccl.comm_refs == 1
         assert res["info"] == 0, (res["info"], len(res["residuals"]))
+        M2 = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, self_halo=True, halo="rccl")
+        assert M2._rccl.comm == M._rccl.comm and M._rccl.comm_refs == 2
         dA.close()
+        assert M._rccl.comm_refs == 2
+        M2.close()
         assert M._rccl.comm_refs == 1
         M.close()
         dist.destroy_process_group()
@@ -427,9 +433,9 @@ def _shared_comm_worker(_index, port, n, errfile):
         raise
 
 
-def test_solve_distributed_shares_one_communicator(tmp_path):
+def test_solve_distributed_communicators(tmp_path):
     errfile = str(tmp_path / "err.txt")
-    _spawn(_shared_comm_worker, (_free_port(), 32, errfile), 1, errfile)
+    _spawn(_comm_worker, (_free_port(), 32, errfile), 1, errfile)
 
 
 def _default_maxiter_worker(rank, world, port, n, outdir, errfile):
@@ -469,7 +475,7 @@ def test_distributed_fgmres_default_maxiter(tmp_path):
         assert np.array_equal(h, np.asarray(hist)), (r, len(h), len(hist))
 
 
-def _configs4_worker(rank, world, port, n, errfile):
+def _configs4_worker(rank, world, port, n, errfile, numerics="exact"):
     """configs[4]: the 2048^2 apply row-partitioned over 8 ranks (256 grid rows each: the 8-GPU run's geometry, CA
     ghost depths and halo sizes) on one GPU over gloo, bit for bit against the one-GPU apply."""
     try:
@@ -479,7 +485,7 @@ def _configs4_worker(rank, world, port, n, errfile):
         import mp_block_preconditioners_amd as mpb
         from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner
         iF, iP = mpb.InnerSolver("chebyshev", 4), mpb.InnerSolver("chebyshev", 4)
-        dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP)
+        dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, numerics=numerics)
         assert dpc.ca and dpc.part.L == n // world
         gids = torch.from_numpy(dpc.local_to_global_rows()).cuda()
         v = torch.from_numpy(np.random.default_rng(2048).standard_normal(5 * n * n)).cuda()
@@ -493,7 +499,8 @@ def _configs4_worker(rank, world, port, n, errfile):
             if turn == rank:
                 bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
                 _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
-                pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP)
+                pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, numerics=numerics,
+                                                   kernel_opts={"q13_sym": 0})   # (the partition's full Gt_F_G rows)
                 ref = pc.apply(v)[gids]
                 assert torch.equal(got, ref), float((got - ref).abs().max())
                 del pc, F, D, G, bp, ref
@@ -506,8 +513,10 @@ def _configs4_worker(rank, world, port, n, errfile):
         raise
 
 
-def test_configs4_2048_over_8_ranks(tmp_path):
+@pytest.mark.parametrize("numerics", ["exact", "fast"])
+def test_configs4_2048_over_8_ranks(numerics, tmp_path):
     """BASELINE configs[4] (2048^2, rows partitioned over 8 ranks) on one GPU: every rank's rows of the partitioned
-    apply equal the one-GPU apply's.  The RCCL-over-xGMI transport itself needs the 8-GPU node (bench.py --gpus 8)."""
+    apply equal the one-GPU apply's, in both numerics (fast: the bench's headline numerics).  The RCCL-over-xGMI
+    transport itself needs the 8-GPU node (bench.py --gpus 8)."""
     errfile = str(tmp_path / "err.txt")
-    _spawn(_configs4_worker, (8, _free_port(), 2048, errfile), 8, errfile)
+    _spawn(_configs4_worker, (8, _free_port(), 2048, errfile, numerics), 8, errfile)

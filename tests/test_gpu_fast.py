@@ -211,7 +211,6 @@ def test_fused_pair_equals_two_sweeps(n, kf, kp):
     second solve) performs each sweep's IEEE operations: bit-identical to two k_march sweeps, on grids that are and are
     not multiples of the 256-column strip."""
     mp = _mp()
-    from mp_block_preconditioners_amd._lib import check, lib
     bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
     _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
     pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("chebyshev", kf),
@@ -219,13 +218,10 @@ def test_fused_pair_equals_two_sweeps(n, kf, kp):
     assert pc.fuse_g
     v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda",
                     generator=torch.Generator(device="cuda").manual_seed(n))
-    try:
-        check(lib().mpbp_set_f_pair(0))
-        ref = pc.apply(v).clone()
-        check(lib().mpbp_set_f_pair(1))
-        got = pc.apply(v)
-    finally:
-        check(lib().mpbp_set_f_pair(1))
+    pc.set_kernel_opts(f_pair=0)
+    ref = pc.apply(v).clone()
+    pc.set_kernel_opts(f_pair=1)
+    got = pc.apply(v)
     assert torch.equal(got, ref), float((got - ref).abs().max())
     nofuse = mp.ApproxSchurPreconditioner(F, D, G, pc.GtG, pc.GtFG, inner_F=mp.InnerSolver("chebyshev", kf),
                                           inner_P=mp.InnerSolver("chebyshev", kp), numerics="fast", fuse_g=False)
@@ -237,7 +233,6 @@ def test_matrix_free_galerkin_level1(n):
     """Fast F hierarchies apply level 1 as R_0 (F (P_0 x)) (MgGal) instead of streaming the stored Galerkin product:
     the same operator, so the multigrid apply stays within 1e-10 of the stored-level-1 apply (and of the exact one)."""
     mp = _mp()
-    from mp_block_preconditioners_amd._lib import check, lib
     bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
     _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
     kw = dict(inner_F=mp.InnerSolver("mg", 1), inner_P=mp.InnerSolver("mg", 1))
@@ -245,15 +240,12 @@ def test_matrix_free_galerkin_level1(n):
     assert len(fast.mg_F.sizes) > 2
     v = torch.randn(fast.shape[0], dtype=torch.float64, device="cuda",
                     generator=torch.Generator(device="cuda").manual_seed(n))
-    try:
-        check(lib().mpbp_set_mg_galerkin_mf(0))
-        stored = fast.apply(v).clone()
-        check(lib().mpbp_set_mg_galerkin_mf(1))
-        got = fast.apply(v).clone()
-        check(lib().mpbp_set_mg_galerkin_mf(2))
-        one = fast.apply(v).clone()
-    finally:
-        check(lib().mpbp_set_mg_galerkin_mf(2))
+    fast.set_kernel_opts(mg_galerkin_mf=0)
+    stored = fast.apply(v).clone()
+    fast.set_kernel_opts(mg_galerkin_mf=1)
+    got = fast.apply(v).clone()
+    fast.set_kernel_opts(mg_galerkin_mf=2)
+    one = fast.apply(v).clone()
     assert 0.0 < rel_inf(got.cpu().numpy(), stored.cpu().numpy()) <= 1e-10
     assert torch.equal(one, got)   # one k_gal1 launch (the default) == the three launches, bit for bit
     exact = mp.ApproxSchurPreconditioner(F, D, G, fast.GtG, fast.GtFG, **kw)
@@ -267,10 +259,9 @@ def test_matrix_free_galerkin_level1(n):
 
 @pytest.mark.parametrize("n", [64, 72, 80, 100, 128, 256])
 def test_matrix_free_galerkin_level1_pressure(n):
-    """The pressure hierarchy's level 1 as R_0 (Gt_G (P_0 x)) (mpbp_set_mg_galerkin_mf_p): within 1e-10 of its stored
+    """The pressure hierarchy's level 1 as R_0 (Gt_G (P_0 x)) (kernel option mg_galerkin_mf_p): within 1e-10 of its stored
     Galerkin matrix, and the one-launch k_gal1p bit-identical to the three launches it fuses."""
     mp = _mp()
-    from mp_block_preconditioners_amd._lib import check, lib
     bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
     _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
     fast = mp.ApproxSchurPreconditioner(F, D, G, numerics="fast", inner_F=mp.InnerSolver("chebyshev", 4),
@@ -278,17 +269,12 @@ def test_matrix_free_galerkin_level1_pressure(n):
     assert len(fast.mg_P.sizes) > 2
     v = torch.randn(fast.shape[0], dtype=torch.float64, device="cuda",
                     generator=torch.Generator(device="cuda").manual_seed(n + 1))
-    try:
-        check(lib().mpbp_set_mg_galerkin_mf_p(0))
-        stored = fast.apply(v).clone()
-        check(lib().mpbp_set_mg_galerkin_mf_p(1))
-        check(lib().mpbp_set_mg_galerkin_mf(1))
-        three = fast.apply(v).clone()
-        check(lib().mpbp_set_mg_galerkin_mf(2))
-        one = fast.apply(v).clone()
-    finally:
-        check(lib().mpbp_set_mg_galerkin_mf(2))
-        check(lib().mpbp_set_mg_galerkin_mf_p(1))
+    fast.set_kernel_opts(mg_galerkin_mf_p=0)
+    stored = fast.apply(v).clone()
+    fast.set_kernel_opts(mg_galerkin_mf_p=1, mg_galerkin_mf=1)
+    three = fast.apply(v).clone()
+    fast.set_kernel_opts(mg_galerkin_mf=2)
+    one = fast.apply(v).clone()
     assert 0.0 < rel_inf(three.cpu().numpy(), stored.cpu().numpy()) <= 1e-10
     assert torch.equal(one, three), float((one - three).abs().max())
     out = torch.empty_like(v)
@@ -299,28 +285,29 @@ def test_matrix_free_galerkin_level1_pressure(n):
 
 
 @pytest.mark.parametrize("n", [5, 16, 100, 256])
-def test_q13_symmetric_half(n):
-    """Tolerance mode reads Gt_F_G's diamond upper half (mpbp_set_q13_sym, default 1): the apply stays within 1e-13
+@pytest.mark.parametrize("prm", PARAMS, ids=["visc", "stiff", "general", "c0"])
+def test_q13_symmetric_half(n, prm):
+    """Tolerance mode reads Gt_F_G's diamond upper half (kernel option q13_sym, default 1): the apply stays within 1e-13
     relative of the 13-slot apply (the stored product is symmetric to ~1.5e-16) and within 1e-12 of the oracle's;
     the exact mode never takes it."""
     mp = _mp()
-    from mp_block_preconditioners_amd._lib import check, lib
-    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
-    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    xi, eta_n, eta_s, c, d_u = prm
+    bp = mp.MultiphaseBlockPreconditioner(n, xi, eta_n, eta_s)
+    _, _, F, D, G = bp.get_big_A_matrix(c=c, d_u=d_u)
     kw = dict(inner_F=mp.InnerSolver("chebyshev", 4), inner_P=mp.InnerSolver("chebyshev", 4))
     fast = mp.ApproxSchurPreconditioner(F, D, G, numerics="fast", **kw)
     exact = mp.ApproxSchurPreconditioner(F, D, G, fast.GtG, fast.GtFG, **kw)
     v = torch.randn(fast.shape[0], dtype=torch.float64, device="cuda",
                     generator=torch.Generator(device="cuda").manual_seed(n + 11))
-    try:
-        check(lib().mpbp_set_q13_sym(0))
-        full = fast.apply(v).clone()
-        ex0 = exact.apply(v).clone()
-        check(lib().mpbp_set_q13_sym(1))
-        half = fast.apply(v).clone()
-        ex1 = exact.apply(v).clone()
-    finally:
-        check(lib().mpbp_set_q13_sym(1))
+    assert fast.kernel_opts.q13_sym == 1 and fast.q13_asymmetry[0] <= 1e-14 * fast.q13_asymmetry[1]
+    fast.set_kernel_opts(q13_sym=0)
+    exact.set_kernel_opts(q13_sym=0)
+    full = fast.apply(v).clone()
+    ex0 = exact.apply(v).clone()
+    fast.set_kernel_opts(q13_sym=1)
+    exact.set_kernel_opts(q13_sym=1)
+    half = fast.apply(v).clone()
+    ex1 = exact.apply(v).clone()
     assert rel_inf(half.cpu().numpy(), full.cpu().numpy()) <= 1e-13
     assert rel_inf(half.cpu().numpy(), ex0.cpu().numpy()) <= 1e-12
     assert torch.equal(ex0, ex1)

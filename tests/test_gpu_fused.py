@@ -24,7 +24,6 @@ def _need_gpu(oracle_built):
 @pytest.mark.parametrize("numerics", ["exact", "fast"])
 def test_fused_gtg_solve_equals_per_sweep(n, kp, numerics):
     import mp_block_preconditioners_amd as mp
-    from mp_block_preconditioners_amd._lib import check, lib
     bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
     _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
     pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("chebyshev", 4),
@@ -32,13 +31,10 @@ def test_fused_gtg_solve_equals_per_sweep(n, kp, numerics):
     assert pc.pg_stencil is not None
     v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda",
                     generator=torch.Generator(device="cuda").manual_seed(n * 10 + kp))
-    try:
-        check(lib().mpbp_set_gtg_fused(0))
-        ref = pc.apply(v).clone()
-        check(lib().mpbp_set_gtg_fused(1))
-        got = pc.apply(v)
-    finally:
-        check(lib().mpbp_set_gtg_fused(1))
+    pc.set_kernel_opts(gtg_fused=0)
+    ref = pc.apply(v).clone()
+    pc.set_kernel_opts(gtg_fused=1)
+    got = pc.apply(v)
     assert torch.equal(got, ref), float((got - ref).abs().max())
 
 
@@ -71,22 +67,16 @@ def test_ftile_equals_marching(n, kf, fuse_g):
     tolerance-mode operations: the apply is bit-identical with the tiles on and off (marching k_march_init, k_march,
     k_march2), with G x_p recomputed in the second solve and launched separately."""
     import mp_block_preconditioners_amd as mp
-    from mp_block_preconditioners_amd._lib import check, lib
     bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
     _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
     pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("chebyshev", kf),
                                       inner_P=mp.InnerSolver("chebyshev", 4), numerics="fast", fuse_g=fuse_g)
     v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda",
                     generator=torch.Generator(device="cuda").manual_seed(n * 10 + kf))
-    try:
-        check(lib().mpbp_set_f_solve(0))   # the whole-solve launch would take over kf = 3, 4 either way
-        check(lib().mpbp_set_f_tile(0))
-        ref = pc.apply(v).clone()
-        check(lib().mpbp_set_f_tile(1))
-        got = pc.apply(v)
-    finally:
-        check(lib().mpbp_set_f_tile(1))
-        check(lib().mpbp_set_f_solve(1))
+    pc.set_kernel_opts(f_solve=0, f_tile=0)   # (the whole-solve launch would take over kf = 3, 4 either way)
+    ref = pc.apply(v).clone()
+    pc.set_kernel_opts(f_tile=1)
+    got = pc.apply(v)
     assert torch.equal(got, ref), float((got - ref).abs().max())
 
 
@@ -99,20 +89,16 @@ def test_fsolve_equals_ftile(n, kf, fuse_g):
     on and off, with G x_p recomputed in the second solve and launched separately, on grids below, at and above its
     minimum (n >= 70 for 3 updates, 72 for 4) and not multiples of the 64 x 8 tile."""
     import mp_block_preconditioners_amd as mp
-    from mp_block_preconditioners_amd._lib import check, lib
     bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
     _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
     pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("chebyshev", kf),
                                       inner_P=mp.InnerSolver("chebyshev", 4), numerics="fast", fuse_g=fuse_g)
     v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda",
                     generator=torch.Generator(device="cuda").manual_seed(n * 10 + kf + 7))
-    try:
-        check(lib().mpbp_set_f_solve(0))
-        ref = pc.apply(v).clone()
-        check(lib().mpbp_set_f_solve(1))
-        got = pc.apply(v)
-    finally:
-        check(lib().mpbp_set_f_solve(1))
+    pc.set_kernel_opts(f_solve=0)
+    ref = pc.apply(v).clone()
+    pc.set_kernel_opts(f_solve=1)
+    got = pc.apply(v)
     assert torch.equal(got, ref), float((got - ref).abs().max())
 
 
@@ -121,48 +107,35 @@ def test_ftile_multigrid_smoothing_equals_marching(n):
     """Multigrid level 0 with fast F numerics: the pre-smoothing (x0 + one sweep) and the post-smoothing restart (two
     sweeps from d = 0, read as +0.0 instead of a memset) on tiles are bit-identical to the marching sweeps."""
     import mp_block_preconditioners_amd as mp
-    from mp_block_preconditioners_amd._lib import check, lib
     bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
     _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
     pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("mg", 1), inner_P=mp.InnerSolver("mg", 1),
                                       numerics="fast")
     v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda",
                     generator=torch.Generator(device="cuda").manual_seed(n))
-    try:
-        check(lib().mpbp_set_f_tile(0))
-        ref = pc.apply(v).clone()
-        check(lib().mpbp_set_f_tile(1))
-        got = pc.apply(v)
-    finally:
-        check(lib().mpbp_set_f_tile(1))
+    pc.set_kernel_opts(f_tile=0)
+    ref = pc.apply(v).clone()
+    pc.set_kernel_opts(f_tile=1)
+    got = pc.apply(v)
     assert torch.equal(got, ref), float((got - ref).abs().max())
 
 
 @pytest.mark.parametrize("n", [5, 17, 64, 128])
 @pytest.mark.parametrize("kf", [3, 5])
 def test_fdirect_equals_marching(n, kf):
-    """mpbp_set_f_direct(1): the per-sweep tolerance-mode F launches on the direct kernel (one thread per cell) perform
+    """Kernel option f_direct = 1: the per-sweep tolerance-mode F launches on the direct kernel (one thread per cell) perform
     the marching kernels' rows4 operations -- the apply is bit-identical (whole-solve and tile launches off)."""
     import mp_block_preconditioners_amd as mp
-    from mp_block_preconditioners_amd._lib import check, lib
     bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
     _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
     pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("chebyshev", kf),
                                       inner_P=mp.InnerSolver("chebyshev", 4), numerics="fast")
     v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda",
                     generator=torch.Generator(device="cuda").manual_seed(n * 10 + kf + 3))
-    try:
-        check(lib().mpbp_set_f_solve(0))
-        check(lib().mpbp_set_f_tile(0))
-        check(lib().mpbp_set_f_pair(0))
-        ref = pc.apply(v).clone()
-        check(lib().mpbp_set_f_direct(1))
-        got = pc.apply(v)
-    finally:
-        check(lib().mpbp_set_f_direct(0))
-        check(lib().mpbp_set_f_pair(1))
-        check(lib().mpbp_set_f_tile(1))
-        check(lib().mpbp_set_f_solve(1))
+    pc.set_kernel_opts(f_solve=0, f_tile=0, f_pair=0)
+    ref = pc.apply(v).clone()
+    pc.set_kernel_opts(f_direct=1)
+    got = pc.apply(v)
     assert torch.equal(got, ref), float((got - ref).abs().max())
 
 
@@ -172,22 +145,17 @@ def test_gtg_solve_builds_rhs_equals_d_launch(n, numerics):
     """The first fused Gt_G solve building rhs = D Finv_v + v_p per staged cell (DStencilDev::row's operations, EpiAdd's
     sum) is bit-identical to the D launch writing rhs, in both numerics, with 256- and 512-lane workgroups."""
     import mp_block_preconditioners_amd as mp
-    from mp_block_preconditioners_amd._lib import check, lib
     bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
     _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
     pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("chebyshev", 4),
                                       inner_P=mp.InnerSolver("chebyshev", 4), numerics=numerics)
     v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda",
                     generator=torch.Generator(device="cuda").manual_seed(n + 5))
-    try:
-        check(lib().mpbp_set_gtg_drhs(0))
-        ref = pc.apply(v).clone()
-        check(lib().mpbp_set_gtg_drhs(1))
-        got = pc.apply(v).clone()
-        check(lib().mpbp_set_gtg_fused(256))
-        got256 = pc.apply(v).clone()
-    finally:
-        check(lib().mpbp_set_gtg_drhs(1))
-        check(lib().mpbp_set_gtg_fused(512))
+    pc.set_kernel_opts(gtg_drhs=0)
+    ref = pc.apply(v).clone()
+    pc.set_kernel_opts(gtg_drhs=1)
+    got = pc.apply(v).clone()
+    pc.set_kernel_opts(gtg_tpb=256)
+    got256 = pc.apply(v).clone()
     assert torch.equal(got, ref), float((got - ref).abs().max())
     assert torch.equal(got256, ref), float((got256 - ref).abs().max())

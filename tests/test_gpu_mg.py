@@ -101,19 +101,17 @@ def test_hierarchy_bit_exact(n, coarsest):
 @pytest.fixture(params=[65536, 0], ids=["grp", "nogrp"])
 def group_rows(request):
     """Small multigrid levels on the grouped CSR kernel (default threshold) or on the SELL / CSR row kernels."""
-    from mp_block_preconditioners_amd._lib import check, lib
-    check(lib().mpbp_set_mg_group_rows(request.param))
-    yield request.param
-    check(lib().mpbp_set_mg_group_rows(65536))
+    from mp_block_preconditioners_amd._lib import kernel_options
+    with kernel_options(mg_group_rows=request.param):
+        yield request.param
 
 
 @pytest.fixture(params=[1, 0], ids=["mftransfer", "storedtransfer"])
 def mf_transfer(request):
     """Whole-grid transfers matrix-free (default) or from their stored CSR / SELL / grouped forms."""
-    from mp_block_preconditioners_amd._lib import check, lib
-    check(lib().mpbp_set_mg_mf_transfer(request.param))
-    yield request.param
-    check(lib().mpbp_set_mg_mf_transfer(1))
+    from mp_block_preconditioners_amd._lib import kernel_options
+    with kernel_options(mg_mf_transfer=request.param):
+        yield request.param
 
 
 @pytest.fixture(params=[False, True], ids=["rowlayouts", "svl"])

@@ -36,14 +36,11 @@ PARAMS = [(1.0, 100.0, 1.0, 1.0, -1.0, 1.0), (2.5, 1.0e4, 1.0, 0.5, -2.0, 2.5), 
 @pytest.fixture(params=[(0, 1), (0, 0), (4, 0), (1, 0), (7, 0)], ids=["direct", "auto", "march4", "march1", "march7"])
 def march_rows(request):
     """Workgroup shapes of the marching kernels, and the direct one-thread-per-cell kernel for D / G / Gt_G
-    (mpbp_set_pg_direct): results must not depend on either."""
-    from mp_block_preconditioners_amd._lib import check, lib
+    (kernel option pg_direct): results must not depend on either."""
+    from mp_block_preconditioners_amd._lib import kernel_options
     rows, direct = request.param
-    check(lib().mpbp_set_march_rows(rows))
-    check(lib().mpbp_set_pg_direct(direct))
-    yield request.param
-    check(lib().mpbp_set_march_rows(0))
-    check(lib().mpbp_set_pg_direct(1))
+    with kernel_options(march_rows=rows, pg_direct=direct):
+        yield request.param
 
 
 def _system(n, prm, tables=None):
@@ -162,19 +159,15 @@ def test_fused_first_sweep_rebuilt_diagonal(n, prm, inner, march_rows):
     one that streams the stored diagonal (k_march<XInit>) and the fully assembled apply, bit for bit -- every
     parameter identity instance of the F policy, strips with ragged last columns (n = 257, 300), n = 3."""
     import mp_block_preconditioners_amd as mp
-    from mp_block_preconditioners_amd._lib import check, lib
     F, D, G, GtG, GtFG = _system(n, prm)
     kw = dict(inner_F=mp.InnerSolver(*inner[0]), inner_P=mp.InnerSolver(*inner[1]))
     ref_pc = mp.ApproxSchurPreconditioner(F, D, G, GtG, GtFG, f_mode="assembled", pg_mode="assembled", **kw)
     pc = mp.ApproxSchurPreconditioner(F, D, G, GtG, GtFG, f_mode="stencil", pg_mode="stencil", **kw)
     v = torch.from_numpy(np.random.default_rng(n + 7).standard_normal(ref_pc.shape[0])).cuda()
     ref = ref_pc.apply(v)
-    try:
-        for mode in (1, 0):
-            check(lib().mpbp_set_init_diag(mode))
-            assert _bits(pc.apply(v), ref), (mode, rel_inf(pc.apply(v).cpu().numpy(), ref.cpu().numpy()))
-    finally:
-        check(lib().mpbp_set_init_diag(1))
+    for mode in (1, 0):
+        pc.set_kernel_opts(init_diag=mode)
+        assert _bits(pc.apply(v), ref), (mode, rel_inf(pc.apply(v).cpu().numpy(), ref.cpu().numpy()))
 
 
 @pytest.mark.parametrize("n", [3, 4, 5, 64, 257])

@@ -99,12 +99,12 @@ def test_seg_spmv_1024_against_oracle():
 
 @pytest.mark.parametrize("n", [3, 64])
 def test_wave_table_same_bits(n):
-    """The CSR SpMV started from the row blocks' wave table (default) == started from row_ptr (mpbp_set_csr_table(0)) ==
+    """The CSR SpMV started from the row blocks' wave table (default) == started from row_ptr (kernel option csr_table = 0) ==
     the oracle, bit for bit: stencil operators (uniform waves) and a ragged matrix (table flags 0), every mode."""
     mp = _mp()
     from oracle import csr_oracle as co
     from oracle.stokes_oracle import StokesSystem
-    from mp_block_preconditioners_amd._lib import check, lib
+    from mp_block_preconditioners_amd._lib import kernel_options
     osys = StokesSystem(n, products=False, **PARAMS)
     rng = np.random.default_rng(n)
     lengths = rng.integers(0, 30, size=2000)
@@ -113,19 +113,16 @@ def test_wave_table_same_bits(n):
     R = sp.csr_matrix((rng.standard_normal(rows.size), (rows, rng.integers(0, 3000, size=rows.size))),
                       shape=(lengths.size, 3000))
     R.sum_duplicates()
-    try:
-        for M in (osys.A, osys.F, osys.D, R):
-            dM = mp.DeviceCSR.from_scipy(M)
-            assert dM.blocks.table is not None
-            x, z = rng.standard_normal(M.shape[1]), rng.standard_normal(M.shape[0])
-            for mode in (0, 1, 2):
-                ref = co.spmv(M, x, z, mode=mode)
-                for on in (1, 0):
-                    check(lib().mpbp_set_csr_table(on))
+    for M in (osys.A, osys.F, osys.D, R):
+        dM = mp.DeviceCSR.from_scipy(M)
+        assert dM.blocks.table is not None
+        x, z = rng.standard_normal(M.shape[1]), rng.standard_normal(M.shape[0])
+        for mode in (0, 1, 2):
+            ref = co.spmv(M, x, z, mode=mode)
+            for on in (1, 0):
+                with kernel_options(csr_table=on):
                     got = dM.matvec(_cuda(x), mode=mode, z=_cuda(z)).cpu().numpy()
-                    assert np.array_equal(got.view(np.uint64), ref.view(np.uint64)), (M.shape, mode, on)
-    finally:
-        check(lib().mpbp_set_csr_table(1))
+                assert np.array_equal(got.view(np.uint64), ref.view(np.uint64)), (M.shape, mode, on)
 
 
 def test_row_blocks_of_another_matrix_refused():

@@ -31,11 +31,10 @@ PARAMS = [(1.0, 100.0, 1.0, 1.0, -1.0), (2.5, 1.0e4, 1.0, 0.5, -2.0), (1.0, 1.0,
 
 @pytest.fixture(params=[0, 4, 1, 3, 8], ids=["auto", "march4", "march1", "march3", "march8"])
 def stencil_kind(request):
-    """Rows per workgroup of the marching kernel (mpbp_set_march_rows): results must not depend on it."""
-    from mp_block_preconditioners_amd._lib import check, lib
-    check(lib().mpbp_set_march_rows(request.param))
-    yield request.param
-    check(lib().mpbp_set_march_rows(0))
+    """Rows per workgroup of the marching kernel (kernel option march_rows): results must not depend on it."""
+    from mp_block_preconditioners_amd._lib import kernel_options
+    with kernel_options(march_rows=request.param):
+        yield request.param
 
 
 @pytest.mark.parametrize("n", [3, 4, 17, 64, 255, 300])

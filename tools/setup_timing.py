@@ -18,7 +18,7 @@ sys.path.insert(0, ROOT)
 def worker(rank, world, port, n, order, q):
     import torch
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MPBP_SETUP_TIMING="1")
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import mp_block_preconditioners_amd as mpb
@@ -30,9 +30,11 @@ def worker(rank, world, port, n, order, q):
         dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=mpb.InnerSolver("chebyshev", 4),
                                              inner_P=mpb.InnerSolver("chebyshev", 4), numerics=numerics)
         torch.cuda.synchronize()
-        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        names = sorted(dpc.setup_phases)
+        el = torch.tensor([time.perf_counter() - t0] + [dpc.setup_phases[k] for k in names], dtype=torch.float64)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        out[f"{len(out) + 1}_{numerics}"] = float(el.item())
+        out[f"{len(out) + 1}_{numerics}"] = {"total": float(el[0]), "phases_max_over_ranks": {
+            k: round(float(v), 4) for k, v in zip(names, el[1:].tolist())}}
         dpc.close()
         del dpc
         torch.cuda.empty_cache()
@@ -45,7 +47,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--n", type=int, default=2048)
-    ap.add_argument("--order", default="exact,fast,fast", help="numerics of the successive builds")
+    ap.add_argument("--order", default="exact,fast,exact,fast", help="numerics of the successive builds")
     a = ap.parse_args()
     import torch.multiprocessing as mp
     with socket.socket() as s:
