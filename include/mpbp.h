@@ -604,6 +604,19 @@ int64_t mpbp_rdot_part_size(int64_t n, int32_t k);
  * on |w_out| (bound_w[0] = max |w| over all ranks) -- identical on every rank, so the sums stay reproducible.
  * 1 <= k <= 256; part: mpbp_rdot_part_size(n, k) doubles.  Replaces the reference's pyamg fgmres orthogonalisation
  * step (solve.py:285; pyamg is absent, see oracle/krylov_oracle.py). */
+/* DCGS2 (FGMRES with delayed re-orthogonalisation, two basis passes per iteration).  mpbp_rdot2: the exact fold sums of
+ * V[i] . u (acc[3i .. 3i+2]) and V[i] . w (acc[3k + 3i ..]) for i < k in ONE pass over V (k <= 256; part:
+ * mpbp_rdot_part_size(n, 2k) doubles); bounds as mpbp_rdot (bound_u, bound_w: max |u|, max |w| bounds).
+ * mpbp_dcgs2_update, iteration j (V[0..j-1] orthonormal, V[j] = u_j projected once, acc = mpbp_rdot2 of V[0..j] with
+ * u = V[j] and w): hu[0..j], hw[0..j] the finished products, P = {r, 1/r, c, bound}: r = sqrt(hu[j] - s.s) (j = 0: 1),
+ * c = (hw[j] - s.z) / r; then V[j] <- (V[j] - V[0..j-1]^T s) / r and, upd_w != 0, V[j+1] <- (w - V[0..j-1]^T z) - V[j] c
+ * (s = hu[0..j-1], z = hw[0..j-1]); P[3] = (bound_w + sum |z_i| + |c|)(1 + 2^-40) bounds |V[j+1]|.  r = 0 marks a
+ * breakdown (V[j] then 0).  All scalars in a fixed order on the device: rank-independent given reduced fold sums. */
+int mpbp_rdot2(const double* V, int64_t ld, int32_t k, const double* u, const double* w, int64_t n, int64_t n_total,
+               const double* bound_v, const double* bound_u, const double* bound_w, double* part, double* acc,
+               void* stream);
+int mpbp_dcgs2_update(double* V, int64_t ld, int32_t j, const double* acc, const double* bound_w, const double* w,
+                      int64_t n, int32_t upd_w, double* hu, double* hw, double* P, void* stream);
 int mpbp_gs_update_rdot(const double* V, int64_t ld, int32_t k, const double* h, const double* w, int64_t n,
                         int64_t n_total, const double* bound_v, const double* bound_w, double* w_out, double* part,
                         double* acc, void* stream);

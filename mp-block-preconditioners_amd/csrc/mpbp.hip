@@ -4739,6 +4739,140 @@ __global__ void __launch_bounds__(kBlock) k_rdot(const double* __restrict__ V, i
         part[c * (3 * (int64_t)k) + 3 * i0 + threadIdx.x] = a;
     }
 }
+// ---- DCGS2 (Gram-Schmidt with delayed re-orthogonalisation: Swirydowicz et al. 2020, Bielich et al. 2022) ----
+// FGMRES iteration j holds q_0 .. q_{j-1} (orthonormal) and u_j (= V[j], projected once, not normalised); one pass over
+// the basis forms the block product [V[0..j]] . [u_j, w] (w = A M u_j) -- the fold sums of both columns (k_rdot2) --
+// and one more pass (k_dcgs2_update) re-orthogonalises and normalises u_j into q_j and projects w once into u_{j+1}:
+// two passes over the basis per iteration instead of CGS2's four.  Scalars (k_dcgs2_coeffs, one thread, fixed order):
+//   s = V[0..j-1] . u_j, alpha = u_j . u_j, z = V[0..j-1] . w, beta = u_j . w,
+//   r = sqrt(alpha - s.s), q_j = (u_j - V s) / r, c = (beta - s.z) / r = q_j . w, u_{j+1} = w - V z - q_j c
+// (j = 0: q_0 = u_0 is the normalised residual, r = 1).  Arnoldi: A Z[j] = w = V z + q_j c + u_{j+1}, and
+// u_{j+1} = V' s' + r' q_{j+1} one iteration later, so column j of H is z + s', c + s'_j, r' (one iteration lagged).
+// Bounds for the binned sums: |q_i| <= 1 (unit vectors), |u_{j+1}| <= (max|w| + sum |z_i| + |c|) (1 + 2^-40).
+__global__ void __launch_bounds__(kBlock) k_rdot2(const double* __restrict__ V, int64_t ld, int k,
+                                                  const double* __restrict__ u, const double* __restrict__ w, int64_t n,
+                                                  int64_t ntot, const double* __restrict__ bound_v,
+                                                  const double* __restrict__ bound_u, const double* __restrict__ bound_w,
+                                                  double* part) {
+    const int64_t c = blockIdx.x;
+    const double bu = bound_u[0], bw = bound_w[0];
+    __shared__ double red[kRdVec * 2 * kRdFolds][kBlock / 64];
+    const int lane = threadIdx.x & 63, wv_ = threadIdx.x >> 6;
+    for (int i0 = 0; i0 < k; i0 += kRdVec) {   // the chunk's u and w re-read per group from L2; V streamed once
+        const int nv = min(kRdVec, k - i0);
+        double sig[kRdVec][2][kRdFolds], acc[kRdVec][2][kRdFolds];
+#pragma unroll
+        for (int v = 0; v < kRdVec; ++v) {
+            const double b = v < nv ? bound_v[i0 + v] : 0.0;
+            rd_sigmas(b * bu, ntot, sig[v][0]);
+            rd_sigmas(b * bw, ntot, sig[v][1]);
+#pragma unroll
+            for (int f = 0; f < kRdFolds; ++f) acc[v][0][f] = acc[v][1][f] = 0.0;
+        }
+        for (int uu = 0; uu < kGsPer; uu += kGsBatch) {
+            double uv[kGsBatch], wv[kGsBatch], vv[kRdVec][kGsBatch];
+#pragma unroll
+            for (int q = 0; q < kGsBatch; ++q) {
+                const int64_t e = c * kGsChunk + (int64_t)(uu + q) * kBlock + threadIdx.x;
+                const bool ok = e < n;
+                const int64_t ee = ok ? e : 0;
+                uv[q] = ok ? u[ee] : 0.0;
+                wv[q] = ok ? w[ee] : 0.0;
+#pragma unroll
+                for (int v = 0; v < kRdVec; ++v) vv[v][q] = (v < nv && ok) ? V[(int64_t)(i0 + v) * ld + ee] : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < kGsBatch; ++q)
+#pragma unroll
+                for (int v = 0; v < kRdVec; ++v) {
+                    rd_fold(vv[v][q] * uv[q], sig[v][0], acc[v][0]);
+                    rd_fold(vv[v][q] * wv[q], sig[v][1], acc[v][1]);
+                }
+        }
+#pragma unroll
+        for (int v = 0; v < kRdVec; ++v)
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                for (int f = 0; f < kRdFolds; ++f) {
+                    double a = acc[v][r][f];
+                    for (int off = 32; off > 0; off >>= 1) a += __shfl_down(a, off, 64);
+                    if (lane == 0) red[(v * 2 + r) * kRdFolds + f][wv_] = a;
+                }
+        __syncthreads();
+        if (threadIdx.x < nv * 2 * kRdFolds) {
+            const int t = threadIdx.x, v = t / (2 * kRdFolds), r = (t / kRdFolds) & 1, f = t % kRdFolds;
+            double a = 0.0;
+            for (int q = 0; q < kBlock / 64; ++q) a += red[t][q];
+            part[c * (6 * (int64_t)k) + r * 3 * (int64_t)k + 3 * (i0 + v) + f] = a;
+        }
+        __syncthreads();
+    }
+}
+// hu[0..j], hw[0..j] from the fold sums (acc: 3 (j+1) for u, then 3 (j+1) for w); P = {r, 1 / r, c, bound of u_{j+1}}.
+__global__ void k_dcgs2_coeffs(int j, const double* __restrict__ acc, const double* __restrict__ bound_w,
+                               double* __restrict__ hu, double* __restrict__ hw, double* __restrict__ P) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const int k = j + 1;
+    double ss = 0.0, sz = 0.0, b = bound_w[0];
+    for (int i = 0; i < k; ++i) {
+        hu[i] = (acc[3 * i] + acc[3 * i + 1]) + acc[3 * i + 2];
+        hw[i] = (acc[3 * k + 3 * i] + acc[3 * k + 3 * i + 1]) + acc[3 * k + 3 * i + 2];
+    }
+    for (int i = 0; i < j; ++i) {
+        ss = ss + hu[i] * hu[i];
+        sz = sz + hu[i] * hw[i];
+        b = b + fabs(hw[i]);
+    }
+    double r = 1.0, rinv = 1.0;
+    if (j > 0) {
+        const double d = hu[j] - ss;
+        r = d > 0.0 ? sqrt(d) : 0.0;
+        rinv = r > 0.0 ? 1.0 / r : 0.0;
+    }
+    const double cc = (hw[j] - sz) * rinv;
+    b = (b + fabs(cc)) * (1.0 + 0x1p-40);
+    P[0] = r;
+    P[1] = rinv;
+    P[2] = cc;
+    P[3] = b;
+}
+// V[j] <- q_j = (V[j] - V[0..j-1]^T s) / r; V[j + 1] <- u_{j+1} = (w - V[0..j-1]^T z) - q_j c (both sums in basis order
+// from 0.0, k_gs_update's operations; upd_w = 0: q_j only).
+__global__ void __launch_bounds__(kBlock) k_dcgs2_update(double* __restrict__ V, int64_t ld, int j,
+                                                         const double* __restrict__ hu, const double* __restrict__ hw,
+                                                         const double* __restrict__ P, const double* __restrict__ w,
+                                                         int64_t n, int upd_w) {
+    __shared__ double ss[256], zs[256];
+    for (int i = threadIdx.x; i < j; i += kBlock) {
+        ss[i] = hu[i];
+        zs[i] = hw[i];
+    }
+    __syncthreads();
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= n) return;
+    double su = 0.0, sw = 0.0;
+    int i = 0;
+    for (; i + 8 <= j; i += 8) {
+        double v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = V[(int64_t)(i + q) * ld + e];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            su += v[q] * ss[i + q];
+            sw += v[q] * zs[i + q];
+        }
+    }
+    for (; i < j; ++i) {
+        const double v = V[(int64_t)i * ld + e];
+        su += v * ss[i];
+        sw += v * zs[i];
+    }
+    const double qv = (V[(int64_t)j * ld + e] - su) * P[1];
+    V[(int64_t)j * ld + e] = qv;
+    if (upd_w) V[(int64_t)(j + 1) * ld + e] = (w[e] - sw) - qv * P[2];
+}
+
 // CGS2's first update and second projection in one kernel: wo = w - V^T h (k_gs_update's operations, same bits) and
 // the exact fold sums of V[i] . wo (k_rdot's pre-rounding).  The extractors cannot wait for max|wo|, so they come from
 // the a-priori bound B = (max|w| + sum_i bound_v[i] |h[i]|) (1 + 2^-40) >= max|wo| -- the same in every workgroup and
@@ -4916,6 +5050,37 @@ int mpbp_rdot(const double* V, int64_t ld, int32_t k, const double* w, int64_t n
     k_rdot<<<grid, kBlock, 0, st>>>(V, ld, k, w, n, n_total, bound_v, bound_w, part);
     MPBP_HIP(hipGetLastError());
     k_rdot_sum<<<3 * k, kBlock, 0, st>>>(part, nchunks, 3 * k, acc);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int mpbp_rdot2(const double* V, int64_t ld, int32_t k, const double* u, const double* w, int64_t n, int64_t n_total,
+               const double* bound_v, const double* bound_u, const double* bound_w, double* part, double* acc,
+               void* stream) {
+    if (!V || !u || !w || !bound_v || !bound_u || !bound_w || !part || !acc || k < 1 || k > 256 || n < 0 || ld < n ||
+        n_total < n)
+        return set_error(MPBP_ERR_ARG, "rdot2: bad args (1 <= k <= 256, ld >= n, n_total >= n)");
+    const hipStream_t st = as_stream(stream);
+    if (n == 0) {
+        MPBP_HIP(hipMemsetAsync(acc, 0, sizeof(double) * 6 * (size_t)k, st));
+        return MPBP_OK;
+    }
+    const int64_t nchunks = (n + kGsChunk - 1) / kGsChunk;
+    k_rdot2<<<(unsigned)nchunks, kBlock, 0, st>>>(V, ld, k, u, w, n, n_total, bound_v, bound_u, bound_w, part);
+    MPBP_HIP(hipGetLastError());
+    k_rdot_sum<<<6 * k, kBlock, 0, st>>>(part, nchunks, 6 * k, acc);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int mpbp_dcgs2_update(double* V, int64_t ld, int32_t j, const double* acc, const double* bound_w, const double* w,
+                      int64_t n, int32_t upd_w, double* hu, double* hw, double* P, void* stream) {
+    if (!V || !acc || !bound_w || !hu || !hw || !P || (upd_w && !w) || j < 0 || j > 255 || n < 1 || ld < n)
+        return set_error(MPBP_ERR_ARG, "dcgs2_update: bad args (0 <= j <= 255, ld >= n)");
+    const hipStream_t st = as_stream(stream);
+    k_dcgs2_coeffs<<<1, 64, 0, st>>>(j, acc, bound_w, hu, hw, P);
+    MPBP_HIP(hipGetLastError());
+    k_dcgs2_update<<<grid_for(n), kBlock, 0, st>>>(V, ld, j, hu, hw, P, w, n, upd_w);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
@@ -5632,8 +5797,10 @@ struct OpPair {
 int op_init(const OpRef& o, int32_t nrows, bool cheb, const double* b, const double* diag, double c2, double* d,
             const double* sub, double* xo, hipStream_t st) {
     const mpbp_schur_plan* p = o.stencil;
-    if (p && o.sop == SOP_F && p->f_numerics == MPBP_NUMERICS_FAST && o.which == 0) {
-        const mpbp_row_part q = stencil_part(o);
+    if (p && o.sop == SOP_F && p->f_numerics == MPBP_NUMERICS_FAST && o.which != 3) {
+        mpbp_row_part q = stencil_part(o);   // (the interior / boundary split of the sweeps: the init covers every owned row)
+        q.which = 0;
+        q.ext = 0;
         FStencilDev Pd;
         const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, &Pd);
         if (rc) return rc;

@@ -508,6 +508,27 @@ class KrylovKernels:
         check(lib().mpbp_rdot_finish(k, ptr(self.acc), ptr(self.h), stream_handle()))
         return self.h[:k]
 
+    # -- DCGS2 (two basis passes per iteration; fgmres(ortho="dcgs2")) --------------------------------------------------
+    def block_folds(self, V, ld, k, u, w, vb, bu, bw) -> torch.Tensor:
+        """The exact fold sums of V[:k] . u and V[:k] . w in one pass over V (k <= 256), summed over every rank:
+        acc2[:3k] for u, acc2[3k:6k] for w (mpbp_rdot2)."""
+        if not hasattr(self, "acc2"):
+            f64 = dict(dtype=torch.float64, device=self.device)
+            self.part2 = torch.empty(max(1, int(lib().mpbp_rdot_part_size(self.n, 2 * min(self.kmax, _KCHUNK)))), **f64)
+            self.acc2 = torch.empty(6 * _KCHUNK, **f64)
+            self.hu, self.hw = torch.empty(_KCHUNK, **f64), torch.empty(_KCHUNK, **f64)
+            self.P = torch.empty(4, **f64)
+        check(lib().mpbp_rdot2(ptr(V), ld, k, ptr(u), ptr(w), self.n, self.n_total, ptr(vb), ptr(bu), ptr(bw),
+                               ptr(self.part2), ptr(self.acc2), stream_handle()))
+        return self._reduce(self.acc2[: 6 * k], "sum")
+
+    def dcgs2_update(self, V, ld, j, acc, bw, w, upd_w=True):
+        """Iteration j's scalars and updates (mpbp_dcgs2_update): V[j] <- q_j, V[j+1] <- u_{j+1} (upd_w); returns the
+        device tensors (hu[:j+1], hw[:j+1], P = [r, 1/r, c, bound of u_{j+1}])."""
+        check(lib().mpbp_dcgs2_update(ptr(V), ld, j, ptr(acc), ptr(bw), ptr(w), self.n, 1 if upd_w else 0, ptr(self.hu),
+                                      ptr(self.hw), ptr(self.P), stream_handle()))
+        return self.hu[: j + 1], self.hw[: j + 1], self.P
+
     def update(self, V, ld, k, h, w, out):
         """out = w - V[:k]^T h (out may be w), the basis rows in chunks of 256 (a fixed order)."""
         src = w
@@ -541,16 +562,18 @@ _VB_SLACK = 1.0 + 2.0 ** -50   # |fl(w / s)| <= fl(max|w| / s) (1 + 2^-50): the 
 
 
 def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=None, residuals=None,
-           capture_M=True, group=None, kernels=None, fused_cgs2=False):
+           capture_M=True, group=None, kernels=None, fused_cgs2=False, ortho="dcgs2"):
     """Flexible GMRES with right preconditioning, all vectors in HBM.
 
     Same call shape as pyamg.krylov.fgmres (solve.py:207, 237, 285): convergence when the
     residual 2-norm falls below ``tol * ||r0||``; returns (x, info) with info 0 on convergence
     and the iteration count otherwise.  ``callback(xk)`` receives the current iterate as a CUDA
     tensor after every inner iteration (the reference's true-residual printer, solve.py:161-170).
-    Orthogonalisation is classical Gram-Schmidt with one re-orthogonalisation pass (CGS2: two
-    batched projections per iteration instead of j dependent dot products), each pass one sweep over
-    the basis through libmpbp (``KrylovKernels``: reproducible inner products, ``mpbp_gs_update``).
+    Orthogonalisation (``ortho``): "dcgs2" (default) -- classical Gram-Schmidt with the re-orthogonalisation pass
+    delayed into the next iteration's block product (Swirydowicz et al. 2020, Bielich et al. 2022): two sweeps over the
+    basis per iteration (``mpbp_rdot2``, ``mpbp_dcgs2_update``), H's column j completed one iteration later; "cgs2" --
+    two full CGS passes per iteration (four sweeps: ``mpbp_rdot`` + ``mpbp_gs_update`` twice).  Both with reproducible
+    inner products (``KrylovKernels``); restarts longer than 255 take CGS2.
     pyamg is not installed here, so iteration counts against pyamg itself are unpinned.
 
     group: the process group of a row partition -- b, x0 and the vectors A and M take and return are the rank's
@@ -606,6 +629,10 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
         except NotImplementedError:   # e.g. a partitioned apply over the host-staged (gloo) halo: eager
             pass
     K = kernels if kernels is not None else KrylovKernels(n, m + 1, b.device, group)
+    if ortho not in ("dcgs2", "cgs2"):
+        raise ValueError("ortho must be 'dcgs2' or 'cgs2'")
+    if ortho == "dcgs2" and m + 1 <= 256 and hasattr(K, "block_folds") and not fused_cgs2:
+        return _fgmres_dcgs2(Aop, Mop, b, x0, tol, m, maxiter, callback, residuals, K)
     fused = fused_cgs2 and hasattr(K, "update_dots")
     f64 = dict(dtype=b.dtype, device=b.device)
     x = torch.zeros_like(b) if x0 is None else (
@@ -719,6 +746,122 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
         normr = norm(r, 0)
         if normr <= target:
             return x, 0
+    return x, it
+
+
+def _fgmres_dcgs2(Aop, Mop, b, x0, tol, m, maxiter, callback, residuals, K):
+    """fgmres's restart cycles with DCGS2 orthogonalisation (see fgmres).  Iteration j of a cycle: w = A M u_j (queued
+    speculatively in iteration j - 1), max |w|, ONE block product [V[0..j]] . [u_j, w] (fold sums, one sum-reduction), the
+    scalars and both updates on the device (V[j] <- q_j, V[j+1] <- u_{j+1}), one pinned copy of s, z, r, c to the host,
+    which completes H's column j - 1 (z + s, c + s_j, r) and its Givens rotation -- the residual estimate is one
+    iteration behind the iteration that formed the column.  Z[j] = M u_j keeps the raw vector: A Z = V H holds with it."""
+    n = b.numel()
+    f64 = dict(dtype=b.dtype, device=b.device)
+    x = torch.zeros_like(b) if x0 is None else (
+        x0.clone() if isinstance(x0, torch.Tensor) else torch.from_numpy(np.asarray(x0, dtype=np.float64)).to(b.device))
+    bnd = torch.empty(2, **f64)            # [max |r| (norms), max |w|]
+
+    def norm(v, slot):
+        K.amax(v, bnd[slot:slot + 1])
+        a = K.fold_sums(v, n, 1, v, bnd[slot:slot + 1], bnd[slot:slot + 1])
+        return math.sqrt(_finish(a.cpu().tolist()))
+
+    def lincomb(xv, Zm, k, y):
+        ny = torch.from_numpy(-np.asarray(y[:k], dtype=np.float64)).to(b.device)
+        return K.update(Zm, n, k, ny, xv, torch.empty_like(xv))
+
+    r = b - Aop(x)
+    normr = norm(r, 0)
+    if residuals is not None:
+        residuals[:] = [normr]
+    normb = norm(b, 1) or 1.0
+    if normr < tol * normb:
+        return x, 0
+    target = tol * normr if normr != 0.0 else tol
+    it = 0
+    w = torch.empty_like(b)
+    V = torch.empty(m + 1, n, **f64)
+    Z = torch.empty(m, n, **f64)
+    vb = torch.ones(m + 1, **f64)          # |q_i| <= 1; vb[j] = the raw u_j's a-priori bound while it is raw
+    on_gpu = b.is_cuda
+    hbuf = torch.empty(2 * m + 8, dtype=torch.float64, pin_memory=on_gpu)
+    ev = torch.cuda.Event() if on_gpu else None
+
+    def head(j):
+        Z[j] = Mop(V[j]) if Mop is not None else V[j]
+        w.copy_(Aop(Z[j]))
+
+    while it < maxiter:
+        beta = normr
+        H = np.zeros((m + 1, m))
+        cs, sn = np.zeros(m), np.zeros(m)
+        g = np.zeros(m + 1)
+        g[0] = beta
+        torch.div(r, beta, out=V[0])
+        vb.fill_(1.0)
+        k = 0                                   # completed columns
+        zc = None                               # column j - 1's first-pass part (z, c), completed in iteration j
+        head(0)
+        done = False
+        for j in range(m + 1):
+            form = j < m and it + (1 if j > 0 else 0) < maxiter   # column j will be formed (w = A M u_j is needed)
+            ubound = vb[j:j + 1]
+            if form:
+                K.amax(w, bnd[1:2])
+            else:
+                bnd[1:2].zero_()                # (no w: its products are not used)
+            acc = K.block_folds(V, n, j + 1, V[j], w, vb, ubound, bnd[1:2])
+            hu, hw, P = K.dcgs2_update(V, n, j, acc, bnd[1:2], w, upd_w=form)
+            vb[j:j + 1] = 1.0                   # V[j] is the unit vector q_j now
+            if form:
+                vb[j + 1:j + 2] = P[3:4]        # the raw u_{j+1}'s a-priori bound
+            hbuf[: 2 * j + 6].copy_(torch.cat([hu, hw, P]), non_blocking=on_gpu)
+            if on_gpu:
+                ev.record()
+            if form and j + 1 < m and it + (1 if j > 0 else 0) + 1 < maxiter:
+                head(j + 1)                     # speculative: queued behind the copy, runs while the host works
+            if on_gpu:
+                ev.synchronize()
+            host = hbuf[: 2 * j + 6].tolist()
+            s_, z_ = host[:j], host[j + 1: 2 * j + 1]
+            rj, cj = host[2 * j + 2], host[2 * j + 4]
+            if j > 0:                           # complete column j - 1: H = (z + s, c + s_{j-1}, r)
+                zp, cp = zc
+                col = j - 1
+                for i in range(col):
+                    H[i, col] = zp[i] + s_[i]
+                H[col, col] = cp + s_[col]
+                H[j, col] = rj
+                for i in range(col):            # previous Givens rotations
+                    t = cs[i] * H[i, col] + sn[i] * H[i + 1, col]
+                    H[i + 1, col] = -sn[i] * H[i, col] + cs[i] * H[i + 1, col]
+                    H[i, col] = t
+                den = math.hypot(H[col, col], H[col + 1, col])
+                cs[col], sn[col] = (1.0, 0.0) if den == 0.0 else (H[col, col] / den, H[col + 1, col] / den)
+                H[col, col] = cs[col] * H[col, col] + sn[col] * H[col + 1, col]
+                H[col + 1, col] = 0.0
+                g[col + 1] = -sn[col] * g[col]
+                g[col] = cs[col] * g[col]
+                k = j
+                it += 1
+                res = abs(g[col + 1])
+                if residuals is not None:
+                    residuals.append(res)
+                if callback is not None:
+                    callback(lincomb(x, Z, k, _solve_upper(H, g, k)))
+                if res <= target or it >= maxiter or rj == 0.0:
+                    done = True
+                    break
+            if not form:
+                break
+            zc = (z_, cj)
+        x = lincomb(x, Z, k, _solve_upper(H, g, k))
+        r = b - Aop(x)
+        normr = norm(r, 0)
+        if normr <= target:
+            return x, 0
+        if not done and k == 0:
+            break
     return x, it
 
 

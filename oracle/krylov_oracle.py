@@ -9,8 +9,13 @@ Arnoldi with Givens rotations over dot products and axpys.  mp-block-preconditio
 * ``mpbp_gs_update`` -- w - V^T h with the basis vectors added in order;
 
 * ``mpbp_gs_update_rdot`` -- CGS2's first update and second projection fused, the extractors from an a-priori bound;
+* ``mpbp_rdot2`` / ``mpbp_dcgs2_update`` -- DCGS2's block product and its scalars and two updates (delayed
+  re-orthogonalisation: Swirydowicz, Langou, Ananthan, Yang, Thomas, "Low synchronization Gram-Schmidt and GMRES
+  algorithms", NLAA 2020; Bielich et al., "Low-synch Gram-Schmidt with delayed reorthogonalization for Krylov solvers",
+  Parallel Computing 2022);
 
-restated here in numpy: ``rd_sigmas`` / ``rdot_folds`` / ``rdot`` / ``gs_update`` / ``gs_update_rdot``.  Because every fold sum is exact,
+restated here in numpy: ``rd_sigmas`` / ``rdot_folds`` / ``rdot`` / ``gs_update`` / ``gs_update_rdot`` / ``rdot2_folds`` /
+``dcgs2_coeffs`` / ``dcgs2_update``.  Because every fold sum is exact,
 numpy's (pairwise) sum gives the same bits as the GPU's tree of partial sums, whatever the split of the vector.
 ``TorchKrylov`` has the KrylovKernels interface over CPU torch tensors (and a gloo group), so tests can drive the
 product's fgmres host logic -- the distributed reductions, bounds, Givens rotations -- on the CPU.
@@ -105,6 +110,46 @@ def gs_update_rdot(V, k, h, w, ntot, bv, bw):
     return r, rdot_folds(np.atleast_2d(V)[:k], r, ntot, bv, update_bound(bw, bv, h, k))
 
 
+def rdot2_folds(V, u, w, ntot, bv, bu: float, bw: float) -> np.ndarray:
+    """mpbp_rdot2: the fold sums of V[i] . u (first 3k) and V[i] . w (next 3k)."""
+    return np.concatenate([rdot_folds(V, u, ntot, bv, bu), rdot_folds(V, w, ntot, bv, bw)])
+
+
+def dcgs2_coeffs(j: int, acc, bw: float):
+    """mpbp.hip k_dcgs2_coeffs: (hu[0..j], hw[0..j], P = [r, 1/r, c, bound of u_{j+1}]) in the kernel's order."""
+    k = j + 1
+    a = np.asarray(acc, dtype=np.float64)
+    hu = [(float(a[3 * i]) + float(a[3 * i + 1])) + float(a[3 * i + 2]) for i in range(k)]
+    hw = [(float(a[3 * k + 3 * i]) + float(a[3 * k + 3 * i + 1])) + float(a[3 * k + 3 * i + 2]) for i in range(k)]
+    ss, sz, b = 0.0, 0.0, float(bw)
+    for i in range(j):
+        ss = ss + hu[i] * hu[i]
+        sz = sz + hu[i] * hw[i]
+        b = b + abs(hw[i])
+    r, rinv = 1.0, 1.0
+    if j > 0:
+        d = hu[j] - ss
+        r = math.sqrt(d) if d > 0.0 else 0.0
+        rinv = 1.0 / r if r > 0.0 else 0.0
+    c = (hw[j] - sz) * rinv
+    b = (b + abs(c)) * (1.0 + 2.0 ** -40)
+    return np.asarray(hu), np.asarray(hw), np.asarray([r, rinv, c, b])
+
+
+def dcgs2_update(V: np.ndarray, j: int, hu, hw, P, w, upd_w=True):
+    """mpbp.hip k_dcgs2_update on a (>= j + 2) x n basis, in place: V[j] <- (V[j] - sum_i V[i] s_i) / r,
+    V[j + 1] <- (w - sum_i V[i] z_i) - V[j] c, the sums over i < j in order from 0.0."""
+    su = np.zeros(V.shape[1])
+    sw = np.zeros(V.shape[1])
+    for i in range(j):
+        su = su + V[i] * hu[i]
+        sw = sw + V[i] * hw[i]
+    q = (V[j] - su) * P[1]
+    V[j] = q
+    if upd_w:
+        V[j + 1] = (np.asarray(w, dtype=np.float64) - sw) - q * P[2]
+
+
 class TorchKrylov:
     """KrylovKernels' interface (solve.py) on CPU torch float64 tensors, optionally over a gloo group."""
 
@@ -150,6 +195,21 @@ class TorchKrylov:
             r = gs_update(Vm[i0:i0 + kc], kc, h.numpy()[i0:i0 + kc], r)
         out.copy_(torch.from_numpy(r))
         return out
+
+    def block_folds(self, V, ld, k, u, w, vb, bu, bw):
+        Vm = V[:k, : self.n].numpy()
+        a = rdot2_folds(Vm, u.numpy()[: self.n], w.numpy()[: self.n], self.n_total, vb.numpy()[:k], float(bu[0]),
+                        float(bw[0]))
+        if not hasattr(self, "acc2"):
+            self.acc2 = torch.zeros(6 * 256, dtype=torch.float64)
+        self.acc2[: 6 * k] = torch.from_numpy(a)
+        return self._reduce(self.acc2[: 6 * k], "sum")
+
+    def dcgs2_update(self, V, ld, j, acc, bw, w, upd_w=True):
+        hu, hw, P = dcgs2_coeffs(j, acc.numpy(), float(bw[0]))
+        Vm = V.numpy()   # a view: updated in place
+        dcgs2_update(Vm, j, hu, hw, P, w.numpy() if upd_w else None, upd_w)
+        return torch.from_numpy(hu), torch.from_numpy(hw), torch.from_numpy(P)
 
     def update_dots(self, V, ld, k, h, w, vb, wb):
         """w <- w - V[:k]^T h in place, then h2 = V[:k] w under the a-priori bound (KrylovKernels.update_dots)."""

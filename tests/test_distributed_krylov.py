@@ -22,7 +22,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, maxiter, restrt, outdir, errfile, fused=False):
+def _worker(rank, world, port, n, maxiter, restrt, outdir, errfile, fused=False, ortho="dcgs2"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -76,7 +76,7 @@ def _worker(rank, world, port, n, maxiter, restrt, outdir, errfile, fused=False)
         hist = []
         K = TorchKrylov(own, (restrt or maxiter) + 1, group=group if world > 1 else None)
         x, info = fgmres(Aop, b, M=Mop, tol=1e-12, maxiter=maxiter, restrt=restrt, residuals=hist,
-                         group=group if world > 1 else None, kernels=K, fused_cgs2=fused)
+                         group=group if world > 1 else None, kernels=K, fused_cgs2=fused, ortho=ortho)
         np.save(os.path.join(outdir, f"x_{world}_{rank}.npy"), x.numpy())
         np.save(os.path.join(outdir, f"rows_{world}_{rank}.npy"), rows5)
         np.save(os.path.join(outdir, f"hist_{world}_{rank}.npy"), np.asarray(hist))
@@ -88,9 +88,9 @@ def _worker(rank, world, port, n, maxiter, restrt, outdir, errfile, fused=False)
         raise
 
 
-def _run(world, n, maxiter, restrt, outdir, errfile, fused=False):
+def _run(world, n, maxiter, restrt, outdir, errfile, fused=False, ortho="dcgs2"):
     try:
-        mp.spawn(_worker, args=(world, _free_port(), n, maxiter, restrt, outdir, errfile, fused), nprocs=world,
+        mp.spawn(_worker, args=(world, _free_port(), n, maxiter, restrt, outdir, errfile, fused, ortho), nprocs=world,
                  join=True)
     except Exception:
         msg = open(errfile).read() if os.path.exists(errfile) else ""
@@ -104,15 +104,55 @@ def _run(world, n, maxiter, restrt, outdir, errfile, fused=False):
     return x, hists[0]
 
 
-@pytest.mark.parametrize("n,maxiter,restrt,fused", [(12, 25, None, False), (13, 30, 12, False), (12, 25, None, True)])
-def test_distributed_fgmres_matches_one_rank(n, maxiter, restrt, fused, tmp_path, oracle_built):
+@pytest.mark.parametrize("n,maxiter,restrt,fused,ortho", [(12, 25, None, False, "dcgs2"), (13, 30, 12, False, "dcgs2"),
+                                                          (12, 25, None, False, "cgs2"), (13, 30, 12, False, "cgs2"),
+                                                          (12, 25, None, True, "cgs2")])
+def test_distributed_fgmres_matches_one_rank(n, maxiter, restrt, fused, ortho, tmp_path, oracle_built):
     """FGMRES with the partitioned A and the partitioned preconditioner on 2 and 3 gloo ranks: the residual history
-    and the iterate are bit-identical to the one-rank run (reproducible inner products), restarts included -- also with
-    CGS2's first update and second projection fused (update_dots: the extractor bound from global quantities)."""
+    and the iterate are bit-identical to the one-rank run (reproducible inner products), restarts included -- with DCGS2
+    (the delayed re-orthogonalisation: its block products, scalars and a-priori bounds from global quantities), CGS2,
+    and CGS2's first update and second projection fused (update_dots)."""
     errfile = str(tmp_path / "err.txt")
-    x1, h1 = _run(1, n, maxiter, restrt, str(tmp_path), errfile, fused)
+    x1, h1 = _run(1, n, maxiter, restrt, str(tmp_path), errfile, fused, ortho)
     assert len(h1) == maxiter + 1 and h1[-1] < h1[0]
     for world in (2, 3):
-        xw, hw = _run(world, n, maxiter, restrt, str(tmp_path), errfile, fused)
+        xw, hw = _run(world, n, maxiter, restrt, str(tmp_path), errfile, fused, ortho)
         assert np.array_equal(hw, h1), (world, np.max(np.abs(hw - h1)))
         assert np.array_equal(xw.view(np.uint64), x1.view(np.uint64)), world
+
+
+def test_dcgs2_and_cgs2_converge_alike(oracle_built):
+    """The delayed re-orthogonalisation reaches the tolerance in the iterations CGS2 needs (within 2) on the CPU oracle
+    kernels -- the reference's manufactured (consistent) problem, solve.py:52-80 -- and its residual estimate is the
+    true residual (unrestarted and restarted every 8 iterations)."""
+    from mp_block_preconditioners_amd.solve import fgmres
+    from mp_block_preconditioners_amd.utils import manufactured_problem
+    from oracle import csr_oracle as co
+    from oracle.krylov_oracle import TorchKrylov
+    from oracle.schur_oracle import Inner, approx_schur_apply, diagonal, gershgorin
+    from oracle.stokes_oracle import StokesSystem
+    n = 16
+    s = StokesSystem(n, **PARAMS)
+    _, bb = manufactured_problem(n, PARAMS["c"], PARAMS["d_u"], PARAMS["xi"], PARAMS["eta_n"], PARAMS["eta_s"])
+    b = torch.from_numpy(np.ascontiguousarray(bb))
+    lF, lP = gershgorin(s.F, diagonal(s.F)), gershgorin(s.GtG, diagonal(s.GtG))
+    iF, iP = Inner("chebyshev", 6, lF / 30, lF), Inner("chebyshev", 6, lP / 30, lP)
+
+    def Aop(x):
+        return torch.from_numpy(co.spmv(s.A, x.numpy()))
+
+    def Mop(v):
+        return torch.from_numpy(approx_schur_apply(s.F, s.D, s.G, s.GtG, s.GtFG, v.numpy(), iF, iP))
+    out = {}
+    for ortho in ("cgs2", "dcgs2"):
+        for restrt in (None, 8):
+            hist = []
+            K = TorchKrylov(b.numel(), (restrt or 150) + 1)
+            x, info = fgmres(Aop, b, M=Mop, tol=1e-8, maxiter=150, restrt=restrt, residuals=hist, kernels=K,
+                             ortho=ortho)
+            true = float(np.linalg.norm(b.numpy() - Aop(x).numpy()))
+            assert info == 0 and true <= 1e-8 * hist[0], (ortho, restrt, info, true / hist[0])
+            assert abs(true - hist[-1]) <= 1e-3 * hist[-1] or restrt, (ortho, true, hist[-1])
+            out[(ortho, restrt)] = len(hist) - 1
+    for restrt in (None, 8):
+        assert abs(out[("dcgs2", restrt)] - out[("cgs2", restrt)]) <= 2, out

@@ -168,10 +168,92 @@ def test_fgmres_fused_cgs2_matches_two_pass():
     out = {}
     for fused in (True, False):
         hist = []
-        x, info = mp.fgmres(A, bd, M=pc, tol=1e-10, maxiter=100, residuals=hist, fused_cgs2=fused)
+        x, info = mp.fgmres(A, bd, M=pc, tol=1e-10, maxiter=100, residuals=hist, fused_cgs2=fused, ortho="cgs2")
         assert info == 0
         out[fused] = (x, hist)
     (x1, h1), (x2, h2) = out[True], out[False]
     assert abs(len(h1) - len(h2)) <= 1
     assert np.allclose(h1[: min(len(h1), len(h2))], h2[: min(len(h1), len(h2))], rtol=1e-6, atol=0)
     assert float((x1 - x2).abs().max()) <= 1e-8 * float(x2.abs().max())
+
+
+@pytest.mark.parametrize("j,n", [(0, 1), (0, 1000), (1, 4097), (3, 100_003), (9, 5000), (31, 70_001), (40, 4096),
+                                 (12, 5_242_880)])
+def test_dcgs2_step_matches_oracle_bit_for_bit(j, n):
+    """DCGS2's iteration j on the GPU -- mpbp_rdot2 (both columns' fold sums in one pass over V[0..j]) and
+    mpbp_dcgs2_update (the scalars r, c, the bound, then V[j] <- q_j and V[j+1] <- u_{j+1}) -- against
+    oracle/krylov_oracle.py's rdot2_folds / dcgs2_coeffs / dcgs2_update, bit for bit."""
+    from oracle.krylov_oracle import dcgs2_coeffs, dcgs2_update, rdot2_folds
+    check, lib, ptr, sh = _lib()
+    rng = np.random.default_rng(j * 13 + n)
+    Q, _ = np.linalg.qr(rng.standard_normal((n, j))) if 0 < j <= n else (np.zeros((n, 0)), None)
+    V = np.zeros((j + 2, n))
+    V[:j] = Q.T[:j]
+    u = rng.standard_normal(n)
+    u = u / np.linalg.norm(u) if j == 0 else u - 0.9 * (Q @ (Q.T @ u))   # j > 0: partly projected, not unit
+    V[j] = u
+    w = rng.standard_normal(n) * 3.0
+    vb = np.ones(j + 2)
+    vb[j] = 1.0 if j == 0 else float(np.max(np.abs(u))) * (1 + 2.0 ** -40)
+    wb = float(np.max(np.abs(w)))
+    dV, dw = torch.from_numpy(V.copy()).cuda(), torch.from_numpy(w).cuda()
+    dvb = torch.from_numpy(vb).cuda()
+    dwb = torch.tensor([wb], dtype=torch.float64, device="cuda")
+    part = torch.empty(max(1, int(lib().mpbp_rdot_part_size(n, 2 * (j + 1)))), dtype=torch.float64, device="cuda")
+    acc = torch.empty(6 * (j + 1), dtype=torch.float64, device="cuda")
+    check(lib().mpbp_rdot2(ptr(dV), n, j + 1, ptr(dV[j]), ptr(dw), n, n, ptr(dvb), ptr(dvb[j:j + 1]), ptr(dwb),
+                           ptr(part), ptr(acc), sh()))
+    ref_acc = rdot2_folds(V[: j + 1], V[j], w, n, vb[: j + 1], vb[j], wb)
+    assert np.array_equal(acc.cpu().numpy().view(np.uint64), ref_acc.view(np.uint64))
+    hu = torch.empty(256, dtype=torch.float64, device="cuda")
+    hw = torch.empty(256, dtype=torch.float64, device="cuda")
+    P = torch.empty(4, dtype=torch.float64, device="cuda")
+    check(lib().mpbp_dcgs2_update(ptr(dV), n, j, ptr(acc), ptr(dwb), ptr(dw), n, 1, ptr(hu), ptr(hw), ptr(P), sh()))
+    rhu, rhw, rP = dcgs2_coeffs(j, ref_acc, wb)
+    dcgs2_update(V, j, rhu, rhw, rP, w)
+    assert np.array_equal(hu[: j + 1].cpu().numpy().view(np.uint64), rhu.view(np.uint64))
+    assert np.array_equal(hw[: j + 1].cpu().numpy().view(np.uint64), rhw.view(np.uint64))
+    assert np.array_equal(P.cpu().numpy().view(np.uint64), rP.view(np.uint64))
+    assert np.array_equal(dV.cpu().numpy().view(np.uint64), V.view(np.uint64))
+    # what the step means: q_j unit and orthogonal to V[0..j-1]; u_{j+1} orthogonal to V[0..j] (one CGS pass); the bound
+    assert abs(np.linalg.norm(V[j]) - 1.0) < 1e-12
+    if j:
+        assert np.max(np.abs(V[:j] @ V[j])) < 1e-12
+    assert np.max(np.abs(V[: j + 1] @ V[j + 1])) < 1e-10 * np.linalg.norm(w)
+    assert np.max(np.abs(V[j + 1])) <= rP[3]
+
+
+@pytest.mark.parametrize("n,inner", [(64, "mg:1"), (256, "mg:1"), (256, "chebyshev:4")])
+def test_fgmres_dcgs2_matches_cgs2(n, inner):
+    """FGMRES with DCGS2 (the default: two basis passes per iteration) and with CGS2 (four): the reference's
+    manufactured problem (solve.py:52-80) converges in the same iterations (within 2), to the same solution within the
+    tolerance, and each is deterministic."""
+    import mp_block_preconditioners_amd as mp
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    kind, k = inner.split(":")
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver(kind, int(k)), inner_P=mp.InnerSolver(kind, int(k)),
+                                      numerics="fast")
+    _, b = mp.manufactured_problem(n, 1.0, -1.0, 1.0, 100.0, 1.0)
+    bd = torch.from_numpy(b).cuda()
+    out = {}
+    for ortho in ("dcgs2", "cgs2", "dcgs2"):
+        hist = []
+        x, info = mp.fgmres(A, bd, M=pc, tol=1e-8, maxiter=150, residuals=hist, ortho=ortho)
+        if ortho in out:
+            assert torch.equal(x, out[ortho][0]) and hist == out[ortho][1]   # deterministic
+        out[ortho] = (x, hist, info)
+    (xd, hd, id_), (xc, hc, ic) = out["dcgs2"], out["cgs2"]
+    assert id_ == ic
+    if ic == 0:
+        assert abs(len(hd) - len(hc)) <= 2, (len(hd), len(hc))
+        true = float(torch.linalg.vector_norm(bd - A.matvec(xd)))
+        assert true <= 1.01e-8 * hd[0]
+        assert float((xd - xc).abs().max()) <= 1e-6 * float(xc.abs().max())
+    else:   # chebyshev:4 stalls (DESIGN.md section 7): both reach maxiter without converging.  Once the Krylov space
+        # stops growing, DCGS2's r = sqrt(alpha - s.s) cancels to 0 (u_j within ~1e-7 of span(V)): the cycle ends
+        # there and restarts from the true residual, where CGS2 goes on normalising rounding noise
+        assert ic == id_ == 150 and len(hc) == 151 and len(hd) == 151
+        for x in (xd, xc):
+            true = float(torch.linalg.vector_norm(bd - A.matvec(x)))
+            assert true <= hd[0]
