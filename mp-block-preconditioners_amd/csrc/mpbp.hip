@@ -5765,12 +5765,16 @@ int op_cheb(const OpRef& o, const double* xin, const double* b, const double* dg
             const double* sub, double* xo, hipStream_t st, int store_d, bool dzero = false) {
     if (o.empty) return MPBP_OK;
     if (o.gal) {
-        if (dzero) return set_error(MPBP_ERR_ARG, "cheb: a zero direction is only supported on the grouped CSR path");
-        bool done = false;
-        const int rf = gal_fused(*o.gal, xin, EpiCheb{xin, b, dg, d, c1, c2, sub, xo, store_d}, st, &done);
-        if (rf || done) return rf;
-        const int rc = gal_fp(*o.gal, xin, st);
-        return rc ? rc : gal_r(*o.gal, EpiCheb{xin, b, dg, d, c1, c2, sub, xo, store_d}, st);
+        // (dzero: a restart's first sweep reads d as +0.0 -- no memset of the direction)
+        auto run = [&](const auto& epi) {
+            bool done = false;
+            const int rf = gal_fused(*o.gal, xin, epi, st, &done);
+            if (rf || done) return rf;
+            const int rc = gal_fp(*o.gal, xin, st);
+            return rc ? rc : gal_r(*o.gal, epi, st);
+        };
+        const EpiCheb e{xin, b, dg, d, c1, c2, sub, xo, store_d};
+        return dzero ? run(EpiZeroD<EpiCheb>{e}) : run(e);
     }
     if (o.grp) return grp_cheb(o.csr, xin, b, dg, c1, c2, d, sub, xo, st, store_d, dzero);
     if (o.svl) return svl_cheb(o.svl, o.csr, xin, b, dg, c1, c2, d, sub, xo, st, store_d, dzero);
@@ -6071,7 +6075,7 @@ int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, 
     const bool tpair = K - s >= 2 && o.stencil && o.sop == SOP_F && op.bd.empty && !o.stencil->halo && o.which == 0 &&
                        f_pair_ok(o.stencil) && KO().f_tile && ftile_ok(o.stencil->f_prm.n);
     // restart from the iterate in *cur: d = 0 -- read as +0.0 by the grouped kernel's first sweep, else zeroed
-    bool dzero = !zero && (((op.in.grp || op.in.svl) && op.bd.empty) || (tpair && s == K - 2));
+    bool dzero = !zero && (((op.in.grp || op.in.svl || op.in.gal) && op.bd.empty) || (tpair && s == K - 2));
     if (!zero && !dzero) MPBP_HIP(hipMemsetAsync(d, 0, sizeof(double) * (size_t)nrows, st));
     for (; s < K; ++s) {
         if (tpair && s == K - 2) {

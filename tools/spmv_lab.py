@@ -10,6 +10,8 @@ product kernel's.
 """
 import argparse
 import ctypes
+
+import numpy as np
 import json
 import os
 import subprocess
@@ -68,12 +70,41 @@ def main():
     def sh():
         return stream_handle()
 
-    def lab_csr(mode, nt):
+    def lab_csr(mode, nt, table=None):
+        t = tb if table is None else table
         return lambda: L.lab_csr(mode, nt, P(A.val.data_ptr()), P(A.col_idx.data_ptr()), P(x.data_ptr()),
-                                 A.shape[1], P(tb.data_ptr()), blk.count, P(y.data_ptr()), sh())
+                                 A.shape[1], P(t.data_ptr()), blk.count, P(y.data_ptr()), sh())
+
+    # block orders: the product's (fields interleaved block by block across the 5 stacked fields), plain row order,
+    # and the fields interleaved in chunks of q consecutive blocks (fewer concurrent streams, x gathers still near)
+    from mp_block_preconditioners_amd.csr import RowBlockList
+    flat = A.plan_blocks(groups=1)
+    fp = flat.pairs.cpu().numpy().reshape(-1, 2)
+    nf = 5
+    per = fp.shape[0] // nf
+    tables = {"roworder": flat.table}
+    for q in (4, 16):
+        order = []
+        for c0 in range(0, per, q):
+            for f in range(nf):
+                order.extend(range(f * per + c0, f * per + min(c0 + q, per)))
+        order.extend(range(nf * per, fp.shape[0]))
+        pq = np.ascontiguousarray(fp[np.asarray(order)].reshape(-1))
+        tables[f"chunk{q}"] = RowBlockList(torch.from_numpy(pq).cuda(), A.row_ptr_host, pq).table
+
+    # placement probes: the same product kernel with x / y in buffers allocated at other times (after 1.3 GB of other
+    # allocations, and behind a 2 GiB spacer) -- does where x and y live change the rate (Infinity-Cache residency)?
+    x_late = x.clone()
+    spacer = torch.empty(2 * 1024 ** 3 // 8, dtype=torch.float64, device="cuda")
+    x_far = torch.empty_like(x)
+    x_far.copy_(x)
+    y_late = torch.empty_like(y)
 
     variants = {
         "product_k_csr_wave": (lambda: A.matvec(x, out=y), nbytes, True),
+        "product_x_late": (lambda: A.matvec(x_late, out=y), nbytes, True),
+        "product_x_far": (lambda: A.matvec(x_far, out=y), nbytes, True),
+        "product_y_late": (lambda: A.matvec(x, out=y_late), nbytes, False),
         "lab_reg_nt": (lab_csr(0, 1), nbytes, True),
         "lab_reg_default": (lab_csr(0, 0), nbytes, True),
         "lab_glds_nt": (lab_csr(1, 1), nbytes, True),
@@ -81,6 +112,9 @@ def main():
         "lab_glds_nt_noswizzle": (lab_csr(2, 1), nbytes, True),
         "lab_glds_aux3": (lab_csr(3, 1), nbytes, True),
         "lab_glds_aux1": (lab_csr(4, 1), nbytes, True),
+        "lab_glds_roworder": (lab_csr(1, 1, tables["roworder"]), nbytes, True),
+        "lab_glds_chunk4": (lab_csr(1, 1, tables["chunk4"]), nbytes, True),
+        "lab_glds_chunk16": (lab_csr(1, 1, tables["chunk16"]), nbytes, True),
         "read_stream_nt": (lambda: L.lab_read(P(buf.data_ptr()), nbytes, 1, P(sink.data_ptr()), sh()), nbytes, False),
         "read_stream_default": (lambda: L.lab_read(P(buf.data_ptr()), nbytes, 0, P(sink.data_ptr()), sh()), nbytes,
                                 False),
@@ -137,6 +171,14 @@ def main():
                       "b2b_us_mean": round(sum(r["b2b_us"]) / len(r["b2b_us"]), 2),
                       "warm_gbs_best": round(nb / w / 1e3, 1), "frac_of_8000_best": round(nb / w / 1e3 / 8000, 3)}
     print(json.dumps({"summary": summ}), flush=True)
+    # the bench's own SpMV section (bench.spmv_bench) on the same matrix, in this process
+    sys.path.insert(0, ROOT)
+    from bench import spmv_bench
+    del buf, flush, spacer
+    torch.cuda.empty_cache()
+    r = spmv_bench(A, gen)
+    print(json.dumps({"bench_spmv_section": {k: r[k] for k in ("csr_us", "csr_us_graph", "csr_us_eager", "sell_us")},
+                      "calibration": r.get("calibration")}), flush=True)
 
 
 if __name__ == "__main__":
