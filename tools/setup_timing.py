@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def worker(rank, world, port, n, order, q):
+def worker(rank, world, port, n, order, q, keep_cache=False):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MPBP_SETUP_TIMING="1")
@@ -35,9 +35,12 @@ def worker(rank, world, port, n, order, q):
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         out[f"{len(out) + 1}_{numerics}"] = {"total": float(el[0]), "phases_max_over_ranks": {
             k: round(float(v), 4) for k, v in zip(names, el[1:].tolist())}}
+        if rank == 0:   # progress (a silent multi-minute run looks hung to the GPU harness)
+            print(json.dumps({"build": len(out), "numerics": numerics, **out[f"{len(out)}_{numerics}"]}), flush=True)
         dpc.close()
         del dpc
-        torch.cuda.empty_cache()
+        if not keep_cache:
+            torch.cuda.empty_cache()
     if rank == 0:
         q.put(out)
     dist.destroy_process_group()
@@ -48,21 +51,30 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--n", type=int, default=2048)
     ap.add_argument("--order", default="exact,fast,exact,fast", help="numerics of the successive builds")
+    ap.add_argument("--fresh", action="store_true", help="every build in a fresh set of rank processes")
+    ap.add_argument("--keep-cache", action="store_true", help="no torch.cuda.empty_cache() between builds")
     a = ap.parse_args()
     import torch.multiprocessing as mp
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
-    q = ctx.Queue()
     order = a.order.split(",")
-    procs = [ctx.Process(target=worker, args=(r, a.world, port, a.n, order, q)) for r in range(a.world)]
-    for p in procs:
-        p.start()
-    res = q.get(timeout=600)
-    for p in procs:
-        p.join(timeout=120)
+    res = {}
+    for batch in ([[o] for o in order] if a.fresh else [order]):
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        q = ctx.Queue()
+        procs = [ctx.Process(target=worker, args=(r, a.world, port, a.n, batch, q, a.keep_cache))
+                 for r in range(a.world)]
+        for p in procs:
+            p.start()
+        out = q.get(timeout=600)
+        for p in procs:
+            p.join(timeout=120)
+        for k, v in out.items():
+            res[f"{len(res) + 1}_{k.split('_', 1)[1]}"] = v
     print(json.dumps({"n": a.n, "world": a.world, "backend": "gloo, every rank on one GPU",
+                      "processes": "a fresh set per build" if a.fresh else "one set for all builds",
+                      "empty_cache_between_builds": not a.keep_cache,
                       "setup_seconds_max_over_ranks": res,
                       "note": "DistributedSchurPreconditioner construction: rank-local F / D / G rows, commutator "
                               "products of the owned rows, Chebyshev bounds, CA ghost diagonals, halo plan"}), flush=True)
