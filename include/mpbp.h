@@ -403,6 +403,11 @@ int mpbp_cheb_step(const mpbp_csr* A, const mpbp_rowblocks* blocks, const double
 int mpbp_cheb_coeffs(double lmin, double lmax, int32_t sweeps, double* c1, double* c2);
 /* out = M^-1 v with M the block upper-triangular approximate-commutator preconditioner
  * (solve.py:257-277): v, out are device vectors of nu + np owned entries. */
+/* Multigrid level 1 of the plan's F (kind MPBP_VEC_VELOCITY) or Gt_G (MPBP_VEC_PRESSURE) hierarchy, y = op(A_1 x) (modes
+ * as mpbp_spmv), as the ONE fused matrix-free launch the tolerance-mode multigrid apply runs (k_gal1 / k_gal1p:
+ * R_0 (A_0 (P_0 x))).  One GPU, plan f_numerics FAST, kernel option mg_galerkin_mf = 2 (else MPBP_ERR_ARG).  For timing. */
+int mpbp_mg_level1_apply(const mpbp_schur_plan* p, int32_t kind, int32_t mode, const double* x, const double* z,
+                         double* y, void* stream);
 int mpbp_schur_apply(const mpbp_schur_plan* plan, const double* v, double* out, void* stream);
 
 /* ---- SELL-64 (the apply's HBM layout; built once from CSR) --------------------------------- */

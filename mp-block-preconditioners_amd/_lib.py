@@ -205,6 +205,7 @@ _SIGNATURES = {
     "mpbp_halo_add_gather": ([_P, c_int32, c_int32, _P, _P], c_int),
     "mpbp_halo_allgather": ([_P, c_int32, _P, _P, _P], None),
     "mpbp_kernel_opts_default": ([POINTER(KernelOpts)], None),
+    "mpbp_mg_level1_apply": ([POINTER(SchurPlan), c_int32, c_int32, _P, _P, _P, _P], c_int),
     "mpbp_rdot2": ([_P, c_int64, c_int32, _P, _P, c_int64, c_int64, _P, _P, _P, _P, _P, _P], c_int),
     "mpbp_dcgs2_update": ([_P, c_int64, c_int32, _P, _P, _P, c_int64, c_int32, _P, _P, _P, _P], c_int),
     "mpbp_hbm_stream": ([_P, c_int64, c_int32, _P, _P], c_int),

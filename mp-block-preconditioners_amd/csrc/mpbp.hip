@@ -3070,8 +3070,13 @@ k_fsolve(FStencilFast P, FSolve a, BS bs) {
     // the owned cells: slot 0, 1 the tile cells, slot 1 + r ring r (r = 1 .. H; slot H + 1 only needs x0)
     int cr[NS + 1], cc[NS + 1];
     bool own[NS + 1];
-    cr[0] = r0 + lr; cc[0] = c0 + lc; own[0] = true;
-    cr[1] = r0 + 4 + lr; cc[1] = c0 + lc; own[1] = true;
+#ifndef MPBP_FS_ADJ
+#define MPBP_FS_ADJ 0
+#endif
+    // MPBP_FS_ADJ (experiment): a lane's two tile cells in adjacent rows (2 lr, 2 lr + 1), so their stencils share
+    // loads of x and thn from LDS; 0: rows lr and lr + 4
+    cr[0] = r0 + (MPBP_FS_ADJ ? 2 * lr : lr); cc[0] = c0 + lc; own[0] = true;
+    cr[1] = r0 + (MPBP_FS_ADJ ? 2 * lr + 1 : 4 + lr); cc[1] = c0 + lc; own[1] = true;
 #pragma unroll
     for (int r = 1; r <= H; ++r) {
         own[1 + r] = tid < 140 + 8 * r;
@@ -6685,6 +6690,36 @@ int schur_apply_ca(const Ctx& c, const double* v, double* out) {
 }
 
 }  // namespace
+
+// Multigrid level 1 of the plan's F (kind MPBP_VEC_VELOCITY) or Gt_G (MPBP_VEC_PRESSURE) hierarchy applied matrix-free
+// as ONE fused launch (k_gal1 / k_gal1p: R_0 (A_0 (P_0 x))), y = op(A_1 x) with the modes of mpbp_spmv -- the kernel the
+// tolerance-mode multigrid apply runs for its level-1 sweeps and residuals, exposed for timing (bench.py mg_apply).
+extern "C" int mpbp_mg_level1_apply(const mpbp_schur_plan* p, int32_t kind, int32_t mode, const double* x,
+                                    const double* z, double* y, void* stream) {
+    if (!p || !x || !y || (mode != MPBP_SPMV_STORE && !z)) return set_error(MPBP_ERR_ARG, "mg_level1_apply: bad args");
+    if (int rc = check_opts(p->opts, "mg_level1_apply")) return rc;
+    const OptsScope scope(p->opts);
+    const mpbp_mg* m = kind == MPBP_VEC_VELOCITY ? p->mg_F : kind == MPBP_VEC_PRESSURE ? p->mg_P : nullptr;
+    if (!m || p->halo || p->f_numerics != MPBP_NUMERICS_FAST || KO().mg_galerkin_mf != 2)
+        return set_error(MPBP_ERR_ARG, "mg_level1_apply: a one-GPU fast plan with that multigrid hierarchy, "
+                                       "kernel option mg_galerkin_mf = 2");
+    const int sop = kind == MPBP_VEC_VELOCITY ? SOP_F : SOP_GTG;
+    if ((sop == SOP_F && !p->f_stencil) || (sop == SOP_GTG && (!p->pg_stencil || !KO().mg_galerkin_mf_p)))
+        return set_error(MPBP_ERR_ARG, "mg_level1_apply: the level-0 operator is not matrix-free");
+    const OpPair fine = make_stencil_op(p, sop, false);
+    const MgGal g{m, fine.in, nullptr, nullptr};
+    const hipStream_t st = as_stream(stream);
+    bool done = false;
+    int rc = MPBP_OK;
+    switch (mode) {
+    case MPBP_SPMV_STORE: rc = gal_fused(g, x, EpiStore{y}, st, &done); break;
+    case MPBP_SPMV_ADD: rc = gal_fused(g, x, EpiAdd{z, y}, st, &done); break;
+    case MPBP_SPMV_RESID: rc = gal_fused(g, x, EpiResid{z, y}, st, &done); break;
+    default: return set_error(MPBP_ERR_ARG, "mg_level1_apply: unknown mode %d", mode);
+    }
+    if (rc) return rc;
+    return done ? MPBP_OK : set_error(MPBP_ERR_ARG, "mg_level1_apply: the grid / transfer kinds do not take the fused kernel");
+}
 
 extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, double* out, void* stream) {
     if (!p || !v || !out) return set_error(MPBP_ERR_ARG, "schur_apply: bad args");

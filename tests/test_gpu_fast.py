@@ -383,3 +383,38 @@ def test_q13_symmetric_half(n, prm):
     assert rel_inf(half.cpu().numpy(), full.cpu().numpy()) <= 1e-13
     assert rel_inf(half.cpu().numpy(), ex0.cpu().numpy()) <= 1e-12
     assert torch.equal(ex0, ex1)
+
+
+@pytest.mark.parametrize("n", [96, 128, 256])
+def test_mg_level1_apply_abi(n):
+    """mpbp_mg_level1_apply: the fused level-1 launch (k_gal1 for F, k_gal1p for Gt_G) the bench times, through the
+    C-ABI.  Within 1e-12 of the stored Galerkin matrix of the same level (another summation order of the same product),
+    its add / residual modes the store mode's bits plus / minus z, and MPBP_ERR_ARG without a launch on an exact plan or
+    with the fused kernel switched off."""
+    import ctypes
+    from mp_block_preconditioners_amd._lib import ERR_ARG, VEC_PRESSURE, VEC_VELOCITY, check, lib, ptr, stream_handle
+    mp = _mp()
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    kw = dict(inner_F=mp.InnerSolver("mg", 1), inner_P=mp.InnerSolver("mg", 1))
+    fast = mp.ApproxSchurPreconditioner(F, D, G, numerics="fast", **kw)
+    gen = torch.Generator(device="cuda").manual_seed(n + 7)
+    for kind, mg in ((VEC_VELOCITY, fast.mg_F), (VEC_PRESSURE, fast.mg_P)):
+        M1 = mg.ops[1]
+        x, z = (torch.randn(M1.shape[0], dtype=torch.float64, device="cuda", generator=gen) for _ in range(2))
+        ys = [torch.full_like(x, 7.0) for _ in range(3)]
+        for mode, y in enumerate(ys):
+            check(lib().mpbp_mg_level1_apply(ctypes.byref(fast._plan), kind, mode, ptr(x), ptr(z), ptr(y),
+                                             stream_handle()))
+        ref = M1.matvec(x)
+        assert rel_inf(ys[0].cpu().numpy(), ref.cpu().numpy()) <= 1e-12
+        assert torch.equal(ys[1], ys[0] + z) and torch.equal(ys[2], z - ys[0])
+    exact = mp.ApproxSchurPreconditioner(F, D, G, fast.GtG, fast.GtFG, **kw)
+    y = torch.full_like(x, 7.0)
+    assert lib().mpbp_mg_level1_apply(ctypes.byref(exact._plan), VEC_VELOCITY, 0, ptr(x), None, ptr(y),
+                                      stream_handle()) == ERR_ARG
+    fast.set_kernel_opts(mg_galerkin_mf=1)
+    assert lib().mpbp_mg_level1_apply(ctypes.byref(fast._plan), VEC_VELOCITY, 0, ptr(x), None, ptr(y),
+                                      stream_handle()) == ERR_ARG
+    torch.cuda.synchronize()
+    assert bool((y == 7.0).all())
