@@ -488,7 +488,8 @@ typedef struct mpbp_kernel_opts {
     int32_t mg_svl;            /* multigrid levels with a stencil-values copy use it (1, default) */
     int32_t mg_mf_transfer;    /* whole-grid multigrid transfers matrix-free when the kinds are known (1, default) */
     int32_t csr_table;         /* CSR SpMV waves start from the row blocks' wave table when present (1, default) */
-    int32_t reserved[7];
+    int32_t f_tpb;             /* k_fsolve workgroup lanes: 256 (default) or 512 */
+    int32_t reserved[6];
 } mpbp_kernel_opts;
 /* *out = the calling thread's current choices: its mpbp_kernel_opts_set_thread scope, else the process defaults. */
 void mpbp_kernel_opts_default(mpbp_kernel_opts* out);
@@ -506,7 +507,7 @@ int mpbp_set_gtg_drhs(int32_t on);
 int mpbp_set_q13_sym(int32_t on);
 int mpbp_set_gtg_fused(int32_t on);   /* also 256 / 512: on, with that many lanes per workgroup */
 int mpbp_set_f_tile(int32_t on);
-int mpbp_set_f_solve(int32_t on);
+int mpbp_set_f_solve(int32_t on);    /* also 256 / 512: on, with that many lanes per k_fsolve workgroup */
 int mpbp_set_mg_galerkin_mf(int32_t on);
 int mpbp_set_mg_galerkin_mf_p(int32_t on);
 int mpbp_set_pg_direct(int32_t on);

@@ -27,7 +27,7 @@ thread_local char g_err[1024] = "";
 mpbp_kernel_opts g_defaults = {
     /*march_rows*/ 0, /*init_diag*/ 1, /*f_pair*/ 1, /*f_direct*/ 0, /*gtg_fused*/ 1, /*gtg_tpb*/ 512, /*gtg_drhs*/ 1,
     /*q13_sym*/ 1, /*f_tile*/ 1, /*f_solve*/ 1, /*mg_galerkin_mf*/ 2, /*mg_galerkin_mf_p*/ 1, /*pg_direct*/ 1,
-    /*mg_group_rows*/ 65536, /*mg_svl*/ 1, /*mg_mf_transfer*/ 1, /*csr_table*/ 1, {0, 0, 0, 0, 0, 0, 0}};
+    /*mg_group_rows*/ 65536, /*mg_svl*/ 1, /*mg_mf_transfer*/ 1, /*csr_table*/ 1, /*f_tpb*/ 256, {0, 0, 0, 0, 0, 0}};
 thread_local const mpbp_kernel_opts* t_opts = nullptr;
 inline const mpbp_kernel_opts& KO() { return t_opts ? *t_opts : g_defaults; }
 struct OptsScope {   // installs a plan's kernel choices (when it has its own) for one entry-point call
@@ -43,6 +43,7 @@ int set_error(int code, const char* fmt, ...);
 inline int check_opts(const mpbp_kernel_opts* o, const char* who) {
     if (!o) return MPBP_OK;
     const bool ok = o->march_rows >= 0 && o->march_rows <= 4096 && (o->gtg_tpb == 256 || o->gtg_tpb == 512) &&
+                    (o->f_tpb == 256 || o->f_tpb == 512) &&
                     o->mg_galerkin_mf >= 0 && o->mg_galerkin_mf <= 2 && o->mg_group_rows >= 0 &&
                     (o->init_diag | o->f_pair | o->f_direct | o->gtg_fused | o->gtg_drhs | o->q13_sym | o->f_tile |
                      o->f_solve | o->mg_galerkin_mf_p | o->pg_direct | o->mg_svl | o->mg_mf_transfer | o->csr_table) >= 0 &&
@@ -3004,11 +3005,25 @@ __device__ inline void fs_ring_cell(int r, int j, int r0, int c0, int& vr, int& 
 // PART (row partition, the CA schedule): the tiles cover the owned rows and P.ext ghost rows each side; b and x are
 // in the partition's ghost layout (P.xrow, P.out_row), the thn tables global.  Rows past b's ghost depth (padding of
 // the last tile row and its halo, which no output reads) load a clamped row.
-template <int H, bool SUB, bool PART, class BS>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8)))
+// TPB = 256: a lane owns two tile cells (rows lr, lr + 4) and cell t of every ring.  TPB = 512 (kernel option
+// f_tpb): one tile cell and at most one ring cell per lane (rings 1 .. H numbered across the workgroup), so the
+// per-lane state (d, 1 / diag, b, faces of each owned cell) halves and twice the waves share a CU; every cell keeps
+// one owning lane for all its levels, so the results are the same bits.
+template <int TPB>
+struct FsWpe { static constexpr int v = 2; };
+#ifndef MPBP_FS512_WPE
+#define MPBP_FS512_WPE 4
+#endif
+template <>
+struct FsWpe<512> { static constexpr int v = MPBP_FS512_WPE; };
+template <int H, bool SUB, bool PART, class BS, int TPB = 256>
+__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(FsWpe<TPB>::v, 8)))
 k_fsolve(FStencilFast P, FSolve a, BS bs) {
     using T = FsTile<H>;
-    constexpr int NS = H + 1;   // owned cells with updates after x0: the two tile cells and rings 1 .. H - 1
+    static_assert(TPB == 256 || (TPB == 512 && 140 * H + 4 * H * (H + 1) <= 512), "512 lanes own one ring cell each");
+    constexpr int NT = TPB == 256 ? 2 : 1;        // tile cells per lane
+    constexpr int NSL = TPB == 256 ? H + 2 : 2;   // owned cells per lane (256: the tile's two, then ring r at 1 + r)
+    constexpr int NS = TPB == 256 ? H + 1 : 2;    // ... with updates after x0 (256: ring H only needs x0)
     constexpr int PW = T::RW + 1, PN = PW * (T::RH + 1);   // BS: x_p over the tile + H, + its west / north neighbours
     __shared__ double ts[T::TN];
     __shared__ double xa[4 * T::N], xb[4 * T::N];
@@ -3030,11 +3045,11 @@ k_fsolve(FStencilFast P, FSolve a, BS bs) {
         }
     };
     {
-        constexpr int IT = (T::TN + 255) / 256;
+        constexpr int IT = (T::TN + TPB - 1) / TPB;
         double v[IT];
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            const int i = tid + it * 256;
+            const int i = tid + it * TPB;
             if (i < T::TN) {
                 const int sr = i / T::TW, sc = i - sr * T::TW;
                 v[it] = P.cell[P.wrap(rbt + sr) * n + P.wrap(cbt + sc)];
@@ -3042,16 +3057,16 @@ k_fsolve(FStencilFast P, FSolve a, BS bs) {
         }
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            const int i = tid + it * 256;
+            const int i = tid + it * TPB;
             if (i < T::TN) ts[i] = v[it];
         }
     }
     if constexpr (BS::on) {
-        constexpr int IT = (PN + 255) / 256;
+        constexpr int IT = (PN + TPB - 1) / TPB;
         double v[IT];
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            const int i = tid + it * 256;
+            const int i = tid + it * TPB;
             if (i < PN) {
                 const int sr = i / PW, sc = i - sr * PW;
                 const int pr = in_row(rb - 1 + sr, PART ? bs.h : 0);
@@ -3060,37 +3075,63 @@ k_fsolve(FStencilFast P, FSolve a, BS bs) {
         }
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            const int i = tid + it * 256;
+            const int i = tid + it * TPB;
             if (i < PN) ps[i] = v[it];
+        }
+    }
+    const int lr = tid >> 6, lc = tid & 63;
+    // the owned cells and their rings (0: a tile cell; ring r lives through level H - r)
+    int cr[NSL], cc[NSL], rr[NSL];
+    bool own[NSL];
+#pragma unroll
+    for (int m = 0; m < NT; ++m) {
+        cr[m] = r0 + lr + 4 * m; cc[m] = c0 + lc; own[m] = true; rr[m] = 0;
+    }
+    if constexpr (TPB == 256) {
+#pragma unroll
+        for (int r = 1; r <= H; ++r) {
+            own[1 + r] = tid < 140 + 8 * r;
+            rr[1 + r] = r;
+            fs_ring_cell(r, own[1 + r] ? tid : 0, r0, c0, cr[1 + r], cc[1 + r]);
+        }
+    } else {
+        int r = 0, j = tid;   // rings 1 .. H numbered ring 1 first: lane t owns cell t of that sequence
+#pragma unroll
+        for (int q = 1; q <= H; ++q)
+            if (r == 0) {
+                if (j < 140 + 8 * q) r = q;
+                else j -= 140 + 8 * q;
+            }
+        own[1] = r != 0;
+        rr[1] = r;
+        fs_ring_cell(r ? r : 1, r ? j : 0, r0, c0, cr[1], cc[1]);
+    }
+    // every owned cell's faces and b (BNone) are loaded here, behind the staging loads and ahead of the barrier: one
+    // global-memory latency for the whole level 0 instead of one per cell
+    double fl[NSL][2], bl[BS::on ? 1 : NSL][4];
+#pragma unroll
+    for (int sl = 0; sl < NSL; ++sl) {
+        if (!own[sl]) continue;
+        const int gr = P.wrap(cr[sl]), gc = P.wrap(cc[sl]);
+        const int32_t k = gr * n + gc;
+        fl[sl][0] = P.uface[k];
+        fl[sl][1] = P.vface[k];
+        if constexpr (!BS::on) {
+            const int br = in_row(cr[sl], P.h);
+#pragma unroll
+            for (int f = 0; f < 4; ++f) bl[sl][f] = a.b[(PART ? ext_row(4, f, br, P.L, P.h, n) : (f * n + br) * n) + gc];
         }
     }
     __syncthreads();
     const TTileT<T::TW> tt{ts, rbt, cbt};
-    const int lr = tid >> 6, lc = tid & 63;
-    // the owned cells: slot 0, 1 the tile cells, slot 1 + r ring r (r = 1 .. H; slot H + 1 only needs x0)
-    int cr[NS + 1], cc[NS + 1];
-    bool own[NS + 1];
-#ifndef MPBP_FS_ADJ
-#define MPBP_FS_ADJ 0
-#endif
-    // MPBP_FS_ADJ (experiment): a lane's two tile cells in adjacent rows (2 lr, 2 lr + 1), so their stencils share
-    // loads of x and thn from LDS; 0: rows lr and lr + 4
-    cr[0] = r0 + (MPBP_FS_ADJ ? 2 * lr : lr); cc[0] = c0 + lc; own[0] = true;
-    cr[1] = r0 + (MPBP_FS_ADJ ? 2 * lr + 1 : 4 + lr); cc[1] = c0 + lc; own[1] = true;
-#pragma unroll
-    for (int r = 1; r <= H; ++r) {
-        own[1 + r] = tid < 140 + 8 * r;
-        fs_ring_cell(r, own[1 + r] ? tid : 0, r0, c0, cr[1 + r], cc[1 + r]);
-    }
     double d[NS][4], rd[NS][4], bv[NS][4], fc[NS][2];
     // level 0: x0 = d0 = c2_0 b / diag over the tile + H
 #pragma unroll
-    for (int sl = 0; sl <= NS; ++sl) {
+    for (int sl = 0; sl < NSL; ++sl) {
         if (!own[sl]) continue;
         const int vr = cr[sl], vc = cc[sl];
         const int gr = P.wrap(vr), gc = P.wrap(vc);
-        const int32_t k = gr * n + gc;
-        const FStencilDev::Stage sg{{P.uface[k], P.vface[k]}};
+        const FStencilDev::Stage sg{{fl[sl][0], fl[sl][1]}};
         double b4[4], r4[4];
         P.rdiag4(vr, vc, tt, sg, r4);
         if constexpr (BS::on) {   // b = G x_p, x_p and thn from LDS at virtual coordinates
@@ -3099,9 +3140,8 @@ k_fsolve(FStencilFast P, FSolve a, BS bs) {
 #pragma unroll
             for (int f = 0; f < 4; ++f) b4[f] = bs.b_at(f, vr, vc, gc == 0, gr == 0, tt, q);
         } else {
-            const int br = in_row(vr, P.h);
 #pragma unroll
-            for (int f = 0; f < 4; ++f) b4[f] = a.b[(PART ? ext_row(4, f, br, P.L, P.h, n) : (f * n + br) * n) + gc];
+            for (int f = 0; f < 4; ++f) b4[f] = bl[sl][f];
         }
         const int si = (vr - rb) * T::RW + (vc - cb);
 #pragma unroll
@@ -3122,14 +3162,27 @@ k_fsolve(FStencilFast P, FSolve a, BS bs) {
     // levels 1 .. H
     double* cur = xa;
     double* nxt = xb;
+    double sv[NT][4];   // SUB: the tile cells' sub entries, loaded at the start of level H (its stencil work hides them)
 #pragma unroll
     for (int l = 1; l <= H; ++l) {
         __syncthreads();
         const XTileT<T::RW, T::RH> xt{cur, rb, cb};
         const double c1 = a.c1[l - 1], c2 = a.c2[l - 1];
+        if constexpr (SUB) {
+            if (l == H) {
+#pragma unroll
+                for (int m = 0; m < NT; ++m) {
+                    const int vr = cr[m], vc = cc[m];
+                    if (vr >= hi || vc >= n) continue;
+#pragma unroll
+                    for (int f = 0; f < 4; ++f)
+                        sv[m][f] = a.sub[PART ? P.out_row(f, vr - P.r0, vc) : f * nn + vr * n + vc];
+                }
+            }
+        }
 #pragma unroll
         for (int sl = 0; sl < NS; ++sl) {
-            if (sl >= 2 && (sl - 1 > H - l || !own[sl])) continue;   // ring r = sl - 1 lives through level H - r
+            if (sl >= NT && (!own[sl] || rr[sl] > H - l)) continue;   // ring r lives through level H - r
             const int vr = cr[sl], vc = cc[sl];
             if (l == H && (vr >= hi || vc >= n)) continue;            // a tile past the last row / column
             double acc[4], rdx[4];
@@ -3145,7 +3198,8 @@ k_fsolve(FStencilFast P, FSolve a, BS bs) {
                     d[sl][f] = dn;
                 } else {
                     const int32_t o = PART ? P.out_row(f, vr - P.r0, vc) : f * nn + vr * n + vc;
-                    a.x_out[o] = SUB ? a.sub[o] - x : x;
+                    if constexpr (SUB) a.x_out[o] = sv[sl < NT ? sl : 0][f] - x;   // (level H: tile cells only)
+                    else a.x_out[o] = x;
                 }
             }
         }
@@ -3162,8 +3216,13 @@ template <int H, bool PART, class BS>
 int launch_fsolve_t(const FStencilFast& P, const FSolve& a, hipStream_t st, const BS& bs) {
     const int rows = PART ? P.L + 2 * P.ext : P.n;
     const int64_t tiles = (int64_t)((P.n + kFTW - 1) / kFTW) * ((rows + kFTH - 1) / kFTH);
-    if (a.sub) k_fsolve<H, true, PART, BS><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
-    else k_fsolve<H, false, PART, BS><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
+    if (KO().f_tpb == 512) {
+        if (a.sub) k_fsolve<H, true, PART, BS, 512><<<(unsigned)tiles, 512, 0, st>>>(P, a, bs);
+        else k_fsolve<H, false, PART, BS, 512><<<(unsigned)tiles, 512, 0, st>>>(P, a, bs);
+    } else {
+        if (a.sub) k_fsolve<H, true, PART, BS><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
+        else k_fsolve<H, false, PART, BS><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
+    }
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
@@ -3535,22 +3594,37 @@ __global__ void __launch_bounds__(TPB) k_gtg_solve(GtGStencilDev P, const double
             for (int it = 0; it < IT; ++it)
                 if (tid + it * TPB < TN) ts[tid + it * TPB] = tv[it];
         }
-        __syncthreads();
-        const TTileT<TW> tD{ts, rb - 1, cb - 1};
-        for (int i = tid; i < G::N; i += TPB) {
+        // every staged cell's Y, v_p and diagonal loaded ahead of the barrier: one memory latency, not one per cell
+        constexpr int IY = (G::N + TPB - 1) / TPB;
+        double yl[IY][8], vpl[IY], dgl[IY];
+#pragma unroll
+        for (int it = 0; it < IY; ++it) {
+            const int i = tid + it * TPB;
+            if (i >= G::N) break;
             const int rr = i / G::RW, cc = i - rr * G::RW;
-            const int vr = rb + rr, vc = cb + cc, gr = P.wrap(vr), gc = P.wrap(vc);
+            const int gr = P.wrap(rb + rr), gc = P.wrap(cb + cc);
             const int ge = gc == n - 1 ? 0 : gc + 1, gs = gr == n - 1 ? 0 : gr + 1;
             const int32_t k = gr * n + gc;
-            double yv[8];
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
-                yv[4 * q + 0] = dv.Y[2 * q * nn + gr * n + ge];         // u at the east face
-                yv[4 * q + 1] = dv.Y[2 * q * nn + k];                   // u at the cell's west face
-                yv[4 * q + 2] = dv.Y[(2 * q + 1) * nn + k];             // v at its north face
-                yv[4 * q + 3] = dv.Y[(2 * q + 1) * nn + gs * n + gc];   // v at the south face
+                yl[it][4 * q + 0] = dv.Y[2 * q * nn + gr * n + ge];         // u at the east face
+                yl[it][4 * q + 1] = dv.Y[2 * q * nn + k];                   // u at the cell's west face
+                yl[it][4 * q + 2] = dv.Y[(2 * q + 1) * nn + k];             // v at its north face
+                yl[it][4 * q + 3] = dv.Y[(2 * q + 1) * nn + gs * n + gc];   // v at the south face
             }
-            const double vpk = dv.vp[k], dgk = diag[k];
+            vpl[it] = dv.vp[k];
+            dgl[it] = diag[k];
+        }
+        __syncthreads();
+        const TTileT<TW> tD{ts, rb - 1, cb - 1};
+#pragma unroll
+        for (int it = 0; it < IY; ++it) {
+            const int i = tid + it * TPB;
+            if (i >= G::N) break;
+            const int rr = i / G::RW, cc = i - rr * G::RW;
+            const int vr = rb + rr, vc = cb + cc, gr = P.wrap(vr), gc = P.wrap(vc);
+            const double* yv = yl[it];
+            const double vpk = vpl[it], dgk = dgl[it];
             const bool lastc = gc == n - 1, lastr = gr == n - 1;   // the wrapped neighbour sorts first (DStencilDev)
             double acc = 0.0;
 #pragma unroll
@@ -3768,6 +3842,19 @@ __global__ void __launch_bounds__(256) k_gal1(FStencilFast P, MgFields tr, const
         for (int it = 0; it < IT; ++it)
             if (tid + it * 256 < PN) ts[tid + it * 256] = vt[it];
     }
+    // the faces of this lane's t1 cells, loaded ahead (their latency behind the P_0 stage, not in the F stage)
+    constexpr int IF = (FN + 255) / 256;
+    double fu[IF], fv[IF];
+#pragma unroll
+    for (int it = 0; it < IF; ++it) {
+        const int i = tid + it * 256;
+        if (i < FN) {
+            const int r = i / kG1FW, c = i - r * kG1FW;
+            const int32_t k = P.wrap(fr0 - 1 + r) * n + P.wrap(fc0 - 1 + c);
+            fu[it] = P.uface[k];
+            fv[it] = P.vface[k];
+        }
+    }
     __syncthreads();
     // t0 = P_0 x on the fine block + 2
     for (int i = tid; i < PN; i += 256) {
@@ -3796,12 +3883,14 @@ __global__ void __launch_bounds__(256) k_gal1(FStencilFast P, MgFields tr, const
     {
         const TTileT<kG1PW> tt{ts, fr0 - 2, fc0 - 2};
         const XTileT<kG1PW, kG1PH> xt{t0, fr0 - 2, fc0 - 2};
-        for (int i = tid; i < FN; i += 256) {
+#pragma unroll
+        for (int it = 0; it < IF; ++it) {
+            const int i = tid + it * 256;
+            if (i >= FN) break;
             const int r = i / kG1FW, c = i - r * kG1FW;
             const int vr = fr0 - 1 + r, vc = fc0 - 1 + c;
-            const int32_t k = P.wrap(vr) * n + P.wrap(vc);
             double acc[4], rd[4];
-            P.template rows4<false>(vr, vc, tt, xt, FStencilDev::Cell{{P.uface[k], P.vface[k]}}, acc, rd);
+            P.template rows4<false>(vr, vc, tt, xt, FStencilDev::Cell{{fu[it], fv[it]}}, acc, rd);
 #pragma unroll
             for (int f = 0; f < 4; ++f) t1[f * FN + i] = acc[f];
         }
@@ -4175,8 +4264,9 @@ int mpbp_set_f_tile(int32_t on) {
     return MPBP_OK;
 }
 int mpbp_set_f_solve(int32_t on) {
-    if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "f_solve must be 0 or 1");
-    g_defaults.f_solve = on;
+    if (on != 0 && on != 1 && on != 256 && on != 512) return set_error(MPBP_ERR_ARG, "f_solve must be 0, 1, 256 or 512");
+    g_defaults.f_solve = on != 0;
+    if (on == 256 || on == 512) g_defaults.f_tpb = on;
     return MPBP_OK;
 }
 int mpbp_set_f_pair(int32_t on) {
@@ -4836,14 +4926,16 @@ __global__ void k_dcgs2_coeffs(int j, const double* __restrict__ acc, const doub
         rinv = r > 0.0 ? 1.0 / r : 0.0;
     }
     const double cc = (hw[j] - sz) * rinv;
-    b = (b + fabs(cc)) * (1.0 + 0x1p-40);
+    b = ((b + fabs(cc)) * rinv) * (1.0 + 0x1p-40);   // u_{j+1} is stored scaled by 1 / r (k_dcgs2_update)
     P[0] = r;
     P[1] = rinv;
     P[2] = cc;
     P[3] = b;
 }
-// V[j] <- q_j = (V[j] - V[0..j-1]^T s) / r; V[j + 1] <- u_{j+1} = (w - V[0..j-1]^T z) - q_j c (both sums in basis order
-// from 0.0, k_gs_update's operations; upd_w = 0: q_j only).
+// V[j] <- q_j = (V[j] - V[0..j-1]^T s) / r; V[j + 1] <- u_{j+1} = ((w - V[0..j-1]^T z) - q_j c) / r (both sums in basis
+// order from 0.0, k_gs_update's operations; upd_w = 0: q_j only).  w = A M u_j was formed from the raw u_j (norm ~ r):
+// scaling u_{j+1} by 1 / r keeps the raw vectors at the size of A M q_j instead of growing by ||A M|| per iteration
+// (the Arnoldi column then belongs to Z[j] / r, fgmres's bookkeeping).
 __global__ void __launch_bounds__(kBlock) k_dcgs2_update(double* __restrict__ V, int64_t ld, int j,
                                                          const double* __restrict__ hu, const double* __restrict__ hw,
                                                          const double* __restrict__ P, const double* __restrict__ w,
@@ -4875,7 +4967,7 @@ __global__ void __launch_bounds__(kBlock) k_dcgs2_update(double* __restrict__ V,
     }
     const double qv = (V[(int64_t)j * ld + e] - su) * P[1];
     V[(int64_t)j * ld + e] = qv;
-    if (upd_w) V[(int64_t)(j + 1) * ld + e] = (w[e] - sw) - qv * P[2];
+    if (upd_w) V[(int64_t)(j + 1) * ld + e] = ((w[e] - sw) - qv * P[2]) * P[1];
 }
 
 // CGS2's first update and second projection in one kernel: wo = w - V^T h (k_gs_update's operations, same bits) and

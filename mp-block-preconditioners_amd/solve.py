@@ -752,9 +752,11 @@ def fgmres(A, b, x0=None, tol=1e-5, restrt=None, maxiter=None, M=None, callback=
 def _fgmres_dcgs2(Aop, Mop, b, x0, tol, m, maxiter, callback, residuals, K):
     """fgmres's restart cycles with DCGS2 orthogonalisation (see fgmres).  Iteration j of a cycle: w = A M u_j (queued
     speculatively in iteration j - 1), max |w|, ONE block product [V[0..j]] . [u_j, w] (fold sums, one sum-reduction), the
-    scalars and both updates on the device (V[j] <- q_j, V[j+1] <- u_{j+1}), one pinned copy of s, z, r, c to the host,
-    which completes H's column j - 1 (z + s, c + s_j, r) and its Givens rotation -- the residual estimate is one
-    iteration behind the iteration that formed the column.  Z[j] = M u_j keeps the raw vector: A Z = V H holds with it."""
+    scalars and both updates on the device (V[j] <- q_j, V[j+1] <- u_{j+1} / r_j), one pinned copy of s, z, r, c to the
+    host, which completes H's column j - 1 (z / r + s, c / r + s_j, r') and its Givens rotation -- the residual
+    estimate is one iteration behind the iteration that formed the column.  Z[j] = M u_j keeps the raw vector (norm
+    ~ r_j): the Arnoldi relation A Z' = V H holds for Z'[j] = Z[j] / r_j, so the solution update scales y_j by 1 / r_j
+    (w = A Z[j] is scaled by the same 1 / r_j inside the update: the raw vectors stay at the size of A M q_j)."""
     n = b.numel()
     f64 = dict(dtype=b.dtype, device=b.device)
     x = torch.zeros_like(b) if x0 is None else (
@@ -767,7 +769,7 @@ def _fgmres_dcgs2(Aop, Mop, b, x0, tol, m, maxiter, callback, residuals, K):
         return math.sqrt(_finish(a.cpu().tolist()))
 
     def lincomb(xv, Zm, k, y):
-        ny = torch.from_numpy(-np.asarray(y[:k], dtype=np.float64)).to(b.device)
+        ny = torch.from_numpy(-(np.asarray(y[:k], dtype=np.float64) * zsc[:k])).to(b.device)
         return K.update(Zm, n, k, ny, xv, torch.empty_like(xv))
 
     r = b - Aop(x)
@@ -799,6 +801,7 @@ def _fgmres_dcgs2(Aop, Mop, b, x0, tol, m, maxiter, callback, residuals, K):
         g[0] = beta
         torch.div(r, beta, out=V[0])
         vb.fill_(1.0)
+        zsc = np.ones(m)                        # Z'[i] = Z[i] * zsc[i] (1 / r_i)
         k = 0                                   # completed columns
         zc = None                               # column j - 1's first-pass part (z, c), completed in iteration j
         head(0)
@@ -824,13 +827,15 @@ def _fgmres_dcgs2(Aop, Mop, b, x0, tol, m, maxiter, callback, residuals, K):
                 ev.synchronize()
             host = hbuf[: 2 * j + 6].tolist()
             s_, z_ = host[:j], host[j + 1: 2 * j + 1]
-            rj, cj = host[2 * j + 2], host[2 * j + 4]
-            if j > 0:                           # complete column j - 1: H = (z + s, c + s_{j-1}, r)
-                zp, cp = zc
+            rj, rinvj, cj = host[2 * j + 2], host[2 * j + 3], host[2 * j + 4]
+            if j < m:
+                zsc[j] = rinvj
+            if j > 0:                           # complete column j - 1: H = (z / r + s, c / r + s_{j-1}, r')
+                zp, cp, ip = zc
                 col = j - 1
                 for i in range(col):
-                    H[i, col] = zp[i] + s_[i]
-                H[col, col] = cp + s_[col]
+                    H[i, col] = zp[i] * ip + s_[i]
+                H[col, col] = cp * ip + s_[col]
                 H[j, col] = rj
                 for i in range(col):            # previous Givens rotations
                     t = cs[i] * H[i, col] + sn[i] * H[i + 1, col]
@@ -854,7 +859,7 @@ def _fgmres_dcgs2(Aop, Mop, b, x0, tol, m, maxiter, callback, residuals, K):
                     break
             if not form:
                 break
-            zc = (z_, cj)
+            zc = (z_, cj, rinvj)
         x = lincomb(x, Z, k, _solve_upper(H, g, k))
         r = b - Aop(x)
         normr = norm(r, 0)

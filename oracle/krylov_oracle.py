@@ -132,13 +132,13 @@ def dcgs2_coeffs(j: int, acc, bw: float):
         r = math.sqrt(d) if d > 0.0 else 0.0
         rinv = 1.0 / r if r > 0.0 else 0.0
     c = (hw[j] - sz) * rinv
-    b = (b + abs(c)) * (1.0 + 2.0 ** -40)
+    b = ((b + abs(c)) * rinv) * (1.0 + 2.0 ** -40)
     return np.asarray(hu), np.asarray(hw), np.asarray([r, rinv, c, b])
 
 
 def dcgs2_update(V: np.ndarray, j: int, hu, hw, P, w, upd_w=True):
     """mpbp.hip k_dcgs2_update on a (>= j + 2) x n basis, in place: V[j] <- (V[j] - sum_i V[i] s_i) / r,
-    V[j + 1] <- (w - sum_i V[i] z_i) - V[j] c, the sums over i < j in order from 0.0."""
+    V[j + 1] <- ((w - sum_i V[i] z_i) - V[j] c) / r, the sums over i < j in order from 0.0."""
     su = np.zeros(V.shape[1])
     sw = np.zeros(V.shape[1])
     for i in range(j):
@@ -147,7 +147,7 @@ def dcgs2_update(V: np.ndarray, j: int, hu, hw, P, w, upd_w=True):
     q = (V[j] - su) * P[1]
     V[j] = q
     if upd_w:
-        V[j + 1] = (np.asarray(w, dtype=np.float64) - sw) - q * P[2]
+        V[j + 1] = ((np.asarray(w, dtype=np.float64) - sw) - q * P[2]) * P[1]
 
 
 class TorchKrylov:

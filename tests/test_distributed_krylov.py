@@ -156,3 +156,34 @@ def test_dcgs2_and_cgs2_converge_alike(oracle_built):
             out[(ortho, restrt)] = len(hist) - 1
     for restrt in (None, 8):
         assert abs(out[("dcgs2", restrt)] - out[("cgs2", restrt)]) <= 2, out
+
+
+@pytest.mark.parametrize("n", [16, 32])
+def test_dcgs2_stalling_run_stays_finite(oracle_built, n):
+    """A run that does not converge (no preconditioner, eta_n = 1e4, 150 iterations without restart): the raw Krylov
+    vectors of the delayed scheme are rescaled by 1 / r every iteration (k_dcgs2_update), so they do not grow by
+    ||A|| per iteration and overflow -- the residual estimate stays finite, equals the true residual and tracks CGS2's
+    (round 5 bench: NaN from iteration 23 before the rescaling)."""
+    from mp_block_preconditioners_amd.solve import fgmres
+    from mp_block_preconditioners_amd.utils import manufactured_problem
+    from oracle import csr_oracle as co
+    from oracle.krylov_oracle import TorchKrylov
+    from oracle.stokes_oracle import StokesSystem
+    p = dict(PARAMS, eta_n=1e4)
+    s = StokesSystem(n, **p)
+    _, bb = manufactured_problem(n, p["c"], p["d_u"], p["xi"], p["eta_n"], p["eta_s"])
+    b = torch.from_numpy(np.ascontiguousarray(bb))
+
+    def Aop(x):
+        return torch.from_numpy(co.spmv(s.A, x.numpy()))
+    out = {}
+    for ortho in ("cgs2", "dcgs2"):
+        hist = []
+        x, info = fgmres(Aop, b, tol=1e-8, maxiter=150, residuals=hist, kernels=TorchKrylov(b.numel(), 151),
+                         ortho=ortho)
+        h = np.asarray(hist) / hist[0]
+        assert info == 150 and np.isfinite(h).all() and len(h) == 151, ortho
+        true = float(np.linalg.norm(b.numpy() - Aop(x).numpy())) / hist[0]
+        assert abs(true - h[-1]) <= 1e-6 * h[-1], (ortho, true, h[-1])
+        out[ortho] = h
+    assert np.all(np.abs(np.log(out["dcgs2"] / out["cgs2"])) <= np.log(1.5)), np.max(out["dcgs2"] / out["cgs2"])
