@@ -147,7 +147,7 @@ def main():
                          "0 on the marching kernels")
     ap.add_argument("--f-solve", type=int, default=None,
                     help="fast numerics: 1 (default) runs each F solve of 3 or 4 updates as one k_fsolve launch, "
-                         "0 as k_ftile launches; 256 / 512: one launch with that many lanes per workgroup")
+                         "0 as k_ftile launches")
     ap.add_argument("--solve-numerics", default=None, choices=["fast", "exact"],
                     help="N > 1: numerics of the partitioned multigrid apply and the distributed FGMRES section "
                          "(default: --numerics)")

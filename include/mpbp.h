@@ -488,8 +488,7 @@ typedef struct mpbp_kernel_opts {
     int32_t mg_svl;            /* multigrid levels with a stencil-values copy use it (1, default) */
     int32_t mg_mf_transfer;    /* whole-grid multigrid transfers matrix-free when the kinds are known (1, default) */
     int32_t csr_table;         /* CSR SpMV waves start from the row blocks' wave table when present (1, default) */
-    int32_t f_tpb;             /* k_fsolve workgroup lanes: 256 (default) or 512 */
-    int32_t reserved[6];
+    int32_t reserved[7];
 } mpbp_kernel_opts;
 /* *out = the calling thread's current choices: its mpbp_kernel_opts_set_thread scope, else the process defaults. */
 void mpbp_kernel_opts_default(mpbp_kernel_opts* out);
@@ -507,7 +506,7 @@ int mpbp_set_gtg_drhs(int32_t on);
 int mpbp_set_q13_sym(int32_t on);
 int mpbp_set_gtg_fused(int32_t on);   /* also 256 / 512: on, with that many lanes per workgroup */
 int mpbp_set_f_tile(int32_t on);
-int mpbp_set_f_solve(int32_t on);    /* also 256 / 512: on, with that many lanes per k_fsolve workgroup */
+int mpbp_set_f_solve(int32_t on);
 int mpbp_set_mg_galerkin_mf(int32_t on);
 int mpbp_set_mg_galerkin_mf_p(int32_t on);
 int mpbp_set_pg_direct(int32_t on);
@@ -524,6 +523,12 @@ int mpbp_mg_transfer_count(int32_t n, int32_t nfields, const int32_t* kinds, int
                            void* stream);
 int mpbp_mg_transfer_fill(int32_t n, int32_t nfields, const int32_t* kinds, int32_t which, const int32_t* row_ptr,
                           int32_t* col_idx, double* val, void* stream);
+/* The same transfer's rows `rows` (device, global row ids; any order) only, output row i = row rows[i], global columns:
+ * a rank's band of a row-partitioned hierarchy without the whole-grid transfer.  Setup. */
+int mpbp_mg_transfer_rows_count(int32_t n, int32_t nfields, const int32_t* kinds, int32_t which, const int32_t* rows,
+                                int32_t nrows, int32_t* row_nnz, void* stream);
+int mpbp_mg_transfer_rows_fill(int32_t n, int32_t nfields, const int32_t* kinds, int32_t which, const int32_t* rows,
+                               int32_t nrows, const int32_t* row_ptr, int32_t* col_idx, double* val, void* stream);
 /* x_out = mg->cycles V-cycles for levels[0].A x = b from x = 0 (sub - x when sub != NULL).  Graph-capturable.
  * Row-partitioned hierarchies (part_levels > 0): b, sub, x_out hold the rank's owned rows of level 0. */
 int mpbp_mg_solve(const mpbp_mg* mg, const double* b, const double* sub, double* x_out, void* stream);

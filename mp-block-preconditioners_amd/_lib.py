@@ -84,7 +84,7 @@ class KernelOpts(Structure):
                 ("gtg_fused", c_int32), ("gtg_tpb", c_int32), ("gtg_drhs", c_int32), ("q13_sym", c_int32),
                 ("f_tile", c_int32), ("f_solve", c_int32), ("mg_galerkin_mf", c_int32), ("mg_galerkin_mf_p", c_int32),
                 ("pg_direct", c_int32), ("mg_group_rows", c_int32), ("mg_svl", c_int32), ("mg_mf_transfer", c_int32),
-                ("csr_table", c_int32), ("f_tpb", c_int32), ("reserved", c_int32 * 6)]
+                ("csr_table", c_int32), ("reserved", c_int32 * 7)]
 
 
 def kernel_opts(overrides=None) -> KernelOpts:
@@ -236,6 +236,8 @@ _SIGNATURES = {
     "mpbp_q13_spmv": ([c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "mpbp_mg_transfer_count": ([c_int32, c_int32, _P, c_int32, _P, _P], c_int),
     "mpbp_mg_transfer_fill": ([c_int32, c_int32, _P, c_int32, _P, _P, _P, _P], c_int),
+    "mpbp_mg_transfer_rows_count": ([c_int32, c_int32, _P, c_int32, _P, c_int32, _P, _P], c_int),
+    "mpbp_mg_transfer_rows_fill": ([c_int32, c_int32, _P, c_int32, _P, c_int32, _P, _P, _P, _P], c_int),
     "mpbp_mg_solve": ([POINTER(Mg), _P, _P, _P, _P], c_int),
     "mpbp_gather": ([c_int32, _P, _P, _P, _P], c_int),
     "mpbp_scatter": ([c_int32, _P, _P, _P, _P], c_int),

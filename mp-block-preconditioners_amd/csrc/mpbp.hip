@@ -27,7 +27,7 @@ thread_local char g_err[1024] = "";
 mpbp_kernel_opts g_defaults = {
     /*march_rows*/ 0, /*init_diag*/ 1, /*f_pair*/ 1, /*f_direct*/ 0, /*gtg_fused*/ 1, /*gtg_tpb*/ 512, /*gtg_drhs*/ 1,
     /*q13_sym*/ 1, /*f_tile*/ 1, /*f_solve*/ 1, /*mg_galerkin_mf*/ 2, /*mg_galerkin_mf_p*/ 1, /*pg_direct*/ 1,
-    /*mg_group_rows*/ 65536, /*mg_svl*/ 1, /*mg_mf_transfer*/ 1, /*csr_table*/ 1, /*f_tpb*/ 256, {0, 0, 0, 0, 0, 0}};
+    /*mg_group_rows*/ 65536, /*mg_svl*/ 1, /*mg_mf_transfer*/ 1, /*csr_table*/ 1, {0, 0, 0, 0, 0, 0, 0}};
 thread_local const mpbp_kernel_opts* t_opts = nullptr;
 inline const mpbp_kernel_opts& KO() { return t_opts ? *t_opts : g_defaults; }
 struct OptsScope {   // installs a plan's kernel choices (when it has its own) for one entry-point call
@@ -43,7 +43,6 @@ int set_error(int code, const char* fmt, ...);
 inline int check_opts(const mpbp_kernel_opts* o, const char* who) {
     if (!o) return MPBP_OK;
     const bool ok = o->march_rows >= 0 && o->march_rows <= 4096 && (o->gtg_tpb == 256 || o->gtg_tpb == 512) &&
-                    (o->f_tpb == 256 || o->f_tpb == 512) &&
                     o->mg_galerkin_mf >= 0 && o->mg_galerkin_mf <= 2 && o->mg_group_rows >= 0 &&
                     (o->init_diag | o->f_pair | o->f_direct | o->gtg_fused | o->gtg_drhs | o->q13_sym | o->f_tile |
                      o->f_solve | o->mg_galerkin_mf_p | o->pg_direct | o->mg_svl | o->mg_mf_transfer | o->csr_table) >= 0 &&
@@ -726,10 +725,12 @@ __global__ void __launch_bounds__(kBlock) k_mg_transfer_spmv(MgFields F, MgDiv d
 }
 
 // which: MPBP_MG_P (rows = fine unknowns) or MPBP_MG_R (rows = coarse unknowns); n = fine grid size.
+// rl (optional): the global rows to build, output row i = rl[i] (a rank's band of a row-partitioned hierarchy)
 __global__ void k_mg_transfer(MgFields F, int32_t n, int32_t which, int64_t nrows, const int32_t* rp,
-                              int32_t* row_nnz, int32_t* ci, double* va) {
-    const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (row >= nrows) return;
+                              int32_t* row_nnz, int32_t* ci, double* va, const int32_t* rl = nullptr) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nrows) return;
+    const int64_t row = rl ? (int64_t)rl[i] : i;
     const int nc = n / 2;
     const int nr = which == MPBP_MG_P ? n : nc;       // grid size of the rows' level
     const int nk = which == MPBP_MG_P ? nc : n;       // ... and of the columns' level
@@ -742,11 +743,11 @@ __global__ void k_mg_transfer(MgFields F, int32_t n, int32_t which, int64_t nrow
     const int my = which == MPBP_MG_P ? mg_p1d(F.ky[fld], nc, r, yi, yw) : mg_r1d(F.ky[fld], n, r, yi, yw);
     const int mx = which == MPBP_MG_P ? mg_p1d(F.kx[fld], nc, c, xi, xw) : mg_r1d(F.kx[fld], n, c, xi, xw);
     if (row_nnz) {
-        row_nnz[row] = my * mx;
+        row_nnz[i] = my * mx;
         return;
     }
     const int64_t off = (int64_t)fld * nk * nk;
-    int32_t k = rp[row];
+    int32_t k = rp[i];
     for (int a = 0; a < my; ++a)
         for (int b = 0; b < mx; ++b) {
             ci[k] = (int32_t)(off + (int64_t)yi[a] * nk + xi[b]);
@@ -877,7 +878,7 @@ struct EpiChebT {
     // BX: `sub` is loaded in the epilogue itself instead of ahead of the row -- the fused
     // second solve's last sweep otherwise spills (128 VGPRs + 24 B scratch): 40.9 -> 38.9 us per launch
     // (2541-2565 -> 2573-2640 applies/s, A/B on one box)
-    static constexpr bool kSubLate = BX;
+    static constexpr bool kSubLate = BX, kBX = BX;
     __device__ P pre_lite(int32_t r) const { return {0.0, BX ? 0.0 : ld_stream(b + r), 0.0, ld_stream(d + r), (has_sub() && !kSubLate) ? ld_stream(sub + r) : 0.0}; }
     template <bool NT = false>
     __device__ void apply(int32_t r, double acc, const P& p) const {
@@ -1368,7 +1369,13 @@ template <class Epi>
 struct EpiZeroD : Epi {   // Epi = EpiCheb: d read as +0.0 (never loaded)
     using P = typename Epi::P;
     __device__ P pre(int32_t r) const {
-        return {this->xin[r], ld_stream(this->b + r), this->diag[r], 0.0, this->sub ? ld_stream(this->sub + r) : 0.0};
+        return {this->xin[r], ld_stream(this->b + r), this->diag ? this->diag[r] : 0.0, 0.0,
+                this->sub ? ld_stream(this->sub + r) : 0.0};
+    }
+    // the stencil kernels' form (x and the diagonal from the stencil itself)
+    __device__ P pre_lite(int32_t r) const {
+        return {0.0, Epi::kBX ? 0.0 : ld_stream(this->b + r), 0.0, 0.0,
+                (this->has_sub() && !Epi::kSubLate) ? ld_stream(this->sub + r) : 0.0};
     }
 };
 // The first Chebyshev sweep from x = 0 with the init pass folded in (XS = XInit gathers x0 = c2_0 (b / diag) at every
@@ -2778,6 +2785,16 @@ int launch_march_fixed(const S& P, const XS& xs, Epi epi, int rows_per_block, hi
 // computes the tile from LDS, reusing those diagonals, and writes x_out (and d_out when SD).  Every workgroup is
 // independent.  Each level performs the IEEE operations of the marching kernels' tolerance-mode rows and updates, so
 // k_ftile is bit-identical to k_march_init + (k_march or) k_march2.  One GPU, whole grid.
+// The LDS-tiled stencil kernels read each operand with its own ds_read_b64 (2 LDS cycles per wave on gfx950) instead
+// of letting the compiler pair neighbouring slots into ds_read2_b64 (8 cycles: half the bytes per clock).
+#ifndef MPBP_LDS_SINGLE
+#define MPBP_LDS_SINGLE 1
+#endif
+#if MPBP_LDS_SINGLE && defined(__HIP_DEVICE_COMPILE__)   // (a device-code attribute: the host pass has no such feature)
+#define MPBP_LDS_READS __attribute__((target("no-load-store-opt")))
+#else
+#define MPBP_LDS_READS
+#endif
 constexpr int kFTW = 64, kFTH = 8, kFSW = kFTW + 4, kFSH = kFTH + 4, kFSN = kFSW * kFSH;
 template <int W, int H>
 struct XTileT {  // 4 fields over a W x H block of LDS ([4][H][W]), slot (0, 0) = virtual grid cell (rb, cb)
@@ -2819,7 +2836,7 @@ struct FTile {
 };
 
 template <bool INIT, bool SUB, bool SD, class BS>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) k_ftile(FStencilFast P, FTile a, BS bs) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) MPBP_LDS_READS k_ftile(FStencilFast P, FTile a, BS bs) {
     __shared__ double xs[INIT ? 1 : 4 * kFSN];   // !INIT: x_in over the tile + 2 halo
     __shared__ double ts[kFSN];                   // thn over the tile + 2 halo
     __shared__ double xl[4 * kFAN];               // level A's x over the tile + 1 halo
@@ -3005,25 +3022,13 @@ __device__ inline void fs_ring_cell(int r, int j, int r0, int c0, int& vr, int& 
 // PART (row partition, the CA schedule): the tiles cover the owned rows and P.ext ghost rows each side; b and x are
 // in the partition's ghost layout (P.xrow, P.out_row), the thn tables global.  Rows past b's ghost depth (padding of
 // the last tile row and its halo, which no output reads) load a clamped row.
-// TPB = 256: a lane owns two tile cells (rows lr, lr + 4) and cell t of every ring.  TPB = 512 (kernel option
-// f_tpb): one tile cell and at most one ring cell per lane (rings 1 .. H numbered across the workgroup), so the
-// per-lane state (d, 1 / diag, b, faces of each owned cell) halves and twice the waves share a CU; every cell keeps
-// one owning lane for all its levels, so the results are the same bits.
-template <int TPB>
-struct FsWpe { static constexpr int v = 2; };
-#ifndef MPBP_FS512_WPE
-#define MPBP_FS512_WPE 4
-#endif
-template <>
-struct FsWpe<512> { static constexpr int v = MPBP_FS512_WPE; };
-template <int H, bool SUB, bool PART, class BS, int TPB = 256>
-__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(FsWpe<TPB>::v, 8)))
+template <int H, bool SUB, bool PART, class BS>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) MPBP_LDS_READS
 k_fsolve(FStencilFast P, FSolve a, BS bs) {
     using T = FsTile<H>;
-    static_assert(TPB == 256 || (TPB == 512 && 140 * H + 4 * H * (H + 1) <= 512), "512 lanes own one ring cell each");
-    constexpr int NT = TPB == 256 ? 2 : 1;        // tile cells per lane
-    constexpr int NSL = TPB == 256 ? H + 2 : 2;   // owned cells per lane (256: the tile's two, then ring r at 1 + r)
-    constexpr int NS = TPB == 256 ? H + 1 : 2;    // ... with updates after x0 (256: ring H only needs x0)
+    constexpr int NT = 2;       // tile cells per lane
+    constexpr int NSL = H + 2;  // owned cells per lane: the tile's two (rows lr, lr + 4), then ring r at slot 1 + r
+    constexpr int NS = H + 1;   // ... with updates after x0 (ring H only needs x0)
     constexpr int PW = T::RW + 1, PN = PW * (T::RH + 1);   // BS: x_p over the tile + H, + its west / north neighbours
     __shared__ double ts[T::TN];
     __shared__ double xa[4 * T::N], xb[4 * T::N];
@@ -3045,11 +3050,11 @@ k_fsolve(FStencilFast P, FSolve a, BS bs) {
         }
     };
     {
-        constexpr int IT = (T::TN + TPB - 1) / TPB;
+        constexpr int IT = (T::TN + 255) / 256;
         double v[IT];
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            const int i = tid + it * TPB;
+            const int i = tid + it * 256;
             if (i < T::TN) {
                 const int sr = i / T::TW, sc = i - sr * T::TW;
                 v[it] = P.cell[P.wrap(rbt + sr) * n + P.wrap(cbt + sc)];
@@ -3057,16 +3062,16 @@ k_fsolve(FStencilFast P, FSolve a, BS bs) {
         }
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            const int i = tid + it * TPB;
+            const int i = tid + it * 256;
             if (i < T::TN) ts[i] = v[it];
         }
     }
     if constexpr (BS::on) {
-        constexpr int IT = (PN + TPB - 1) / TPB;
+        constexpr int IT = (PN + 255) / 256;
         double v[IT];
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            const int i = tid + it * TPB;
+            const int i = tid + it * 256;
             if (i < PN) {
                 const int sr = i / PW, sc = i - sr * PW;
                 const int pr = in_row(rb - 1 + sr, PART ? bs.h : 0);
@@ -3075,7 +3080,7 @@ k_fsolve(FStencilFast P, FSolve a, BS bs) {
         }
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-            const int i = tid + it * TPB;
+            const int i = tid + it * 256;
             if (i < PN) ps[i] = v[it];
         }
     }
@@ -3087,24 +3092,11 @@ k_fsolve(FStencilFast P, FSolve a, BS bs) {
     for (int m = 0; m < NT; ++m) {
         cr[m] = r0 + lr + 4 * m; cc[m] = c0 + lc; own[m] = true; rr[m] = 0;
     }
-    if constexpr (TPB == 256) {
 #pragma unroll
-        for (int r = 1; r <= H; ++r) {
-            own[1 + r] = tid < 140 + 8 * r;
-            rr[1 + r] = r;
-            fs_ring_cell(r, own[1 + r] ? tid : 0, r0, c0, cr[1 + r], cc[1 + r]);
-        }
-    } else {
-        int r = 0, j = tid;   // rings 1 .. H numbered ring 1 first: lane t owns cell t of that sequence
-#pragma unroll
-        for (int q = 1; q <= H; ++q)
-            if (r == 0) {
-                if (j < 140 + 8 * q) r = q;
-                else j -= 140 + 8 * q;
-            }
-        own[1] = r != 0;
-        rr[1] = r;
-        fs_ring_cell(r ? r : 1, r ? j : 0, r0, c0, cr[1], cc[1]);
+    for (int r = 1; r <= H; ++r) {
+        own[1 + r] = tid < 140 + 8 * r;
+        rr[1 + r] = r;
+        fs_ring_cell(r, own[1 + r] ? tid : 0, r0, c0, cr[1 + r], cc[1 + r]);
     }
     // every owned cell's faces and b (BNone) are loaded here, behind the staging loads and ahead of the barrier: one
     // global-memory latency for the whole level 0 instead of one per cell
@@ -3216,13 +3208,8 @@ template <int H, bool PART, class BS>
 int launch_fsolve_t(const FStencilFast& P, const FSolve& a, hipStream_t st, const BS& bs) {
     const int rows = PART ? P.L + 2 * P.ext : P.n;
     const int64_t tiles = (int64_t)((P.n + kFTW - 1) / kFTW) * ((rows + kFTH - 1) / kFTH);
-    if (KO().f_tpb == 512) {
-        if (a.sub) k_fsolve<H, true, PART, BS, 512><<<(unsigned)tiles, 512, 0, st>>>(P, a, bs);
-        else k_fsolve<H, false, PART, BS, 512><<<(unsigned)tiles, 512, 0, st>>>(P, a, bs);
-    } else {
-        if (a.sub) k_fsolve<H, true, PART, BS><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
-        else k_fsolve<H, false, PART, BS><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
-    }
+    if (a.sub) k_fsolve<H, true, PART, BS><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
+    else k_fsolve<H, false, PART, BS><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
@@ -3559,7 +3546,7 @@ struct GtgD {
     const double* vp;   // v's pressure part
 };
 template <int H, bool PART, int TPB, bool DB>
-__global__ void __launch_bounds__(TPB) k_gtg_solve(GtGStencilDev P, const double* __restrict__ b,
+__global__ void __launch_bounds__(TPB) MPBP_LDS_READS k_gtg_solve(GtGStencilDev P, const double* __restrict__ b,
                                                    const double* __restrict__ diag, ChebK ck, double* __restrict__ out,
                                                    GtgD dv) {
     using G = GtgTile<H>;
@@ -3801,7 +3788,7 @@ __device__ inline double g1_r(const double* tf, int cr, int cc, int n, int rb, i
 }
 // MAC: the F hierarchy's kinds (u: rows cell-, columns node-centred; v: the reverse) at compile time
 template <class Epi, bool MAC = false>
-__global__ void __launch_bounds__(256) k_gal1(FStencilFast P, MgFields tr, const double* __restrict__ x, Epi epi) {
+__global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1(FStencilFast P, MgFields tr, const double* __restrict__ x, Epi epi) {
     constexpr int CN = kG1CW * kG1CH, PN = kG1PW * kG1PH, FN = kG1FW * kG1FH;
     __shared__ double xs[4 * CN];
     __shared__ double ts[PN];
@@ -3937,7 +3924,7 @@ __global__ void __launch_bounds__(256) k_gal1(FStencilFast P, MgFields tr, const
 constexpr int kG1PH2 = 8;                                     // coarse tile rows (pressure)
 constexpr int kGPFH = 2 * kG1PH2 + 2, kGPPH = kGPFH + 2;       // fine t1 / t0 rows
 template <class Epi>
-__global__ void __launch_bounds__(256) k_gal1p(GtGStencilDev P, const double* __restrict__ x, Epi epi) {
+__global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, const double* __restrict__ x, Epi epi) {
     constexpr int CH = kG1PH2 + 4, CN = kG1CW * CH, PN = kG1PW * kGPPH, FN = kG1FW * kGPFH;
     __shared__ double xs[CN];
     __shared__ double ts[PN];
@@ -4264,9 +4251,8 @@ int mpbp_set_f_tile(int32_t on) {
     return MPBP_OK;
 }
 int mpbp_set_f_solve(int32_t on) {
-    if (on != 0 && on != 1 && on != 256 && on != 512) return set_error(MPBP_ERR_ARG, "f_solve must be 0, 1, 256 or 512");
-    g_defaults.f_solve = on != 0;
-    if (on == 256 || on == 512) g_defaults.f_tpb = on;
+    if (on != 0 && on != 1) return set_error(MPBP_ERR_ARG, "f_solve must be 0 or 1");
+    g_defaults.f_solve = on;
     return MPBP_OK;
 }
 int mpbp_set_f_pair(int32_t on) {
@@ -5461,15 +5447,17 @@ int mpbp_gtg_stencil_jacobi_step(const mpbp_stokes_params* prm, const double* ce
                         as_stream(stream));
 }
 
+// dzero: d is +0.0 (a restart: multigrid post-smoothing), read as such instead of loaded -- no memset launch
 static int gtg_stencil_cheb_impl(const mpbp_stokes_params* prm, const double* cell, const mpbp_row_part* part,
                                  const double* x_in, const double* b, double c1, double c2, double* d,
-                                 const double* sub, double* x_out, void* stream, int store_d) {
+                                 const double* sub, double* x_out, void* stream, int store_d, bool dzero = false) {
     PGDev P;
     int rc = make_pgstencil(prm, cell, part, &P);
     if (rc) return rc;
     if (!x_in || !b || !d || !x_out || x_in == x_out) return set_error(MPBP_ERR_ARG, "gtg_stencil_cheb_step: bad vectors");
-    return launch_march(GtGStencilDev{P}, XPlain{x_in}, EpiCheb{x_in, b, nullptr, d, c1, c2, sub, x_out, store_d},
-                        pg_rows(), as_stream(stream));
+    const EpiCheb e{x_in, b, nullptr, d, c1, c2, sub, x_out, store_d};
+    if (dzero) return launch_march(GtGStencilDev{P}, XPlain{x_in}, EpiZeroD<EpiCheb>{e}, pg_rows(), as_stream(stream));
+    return launch_march(GtGStencilDev{P}, XPlain{x_in}, e, pg_rows(), as_stream(stream));
 }
 
 int mpbp_gtg_stencil_cheb_step(const mpbp_stokes_params* prm, const double* cell, const mpbp_row_part* part,
@@ -5875,14 +5863,15 @@ int op_cheb(const OpRef& o, const double* xin, const double* b, const double* dg
     }
     if (o.grp) return grp_cheb(o.csr, xin, b, dg, c1, c2, d, sub, xo, st, store_d, dzero);
     if (o.svl) return svl_cheb(o.svl, o.csr, xin, b, dg, c1, c2, d, sub, xo, st, store_d, dzero);
-    if (dzero) return set_error(MPBP_ERR_ARG, "cheb: a zero direction is only supported on the grouped CSR path");
+    if (dzero && !(o.stencil && o.sop == SOP_GTG))
+        return set_error(MPBP_ERR_ARG, "cheb: a zero direction needs the grouped / stencil-values / Gt_G stencil path");
     if (o.stencil) {
         const mpbp_schur_plan* p = o.stencil;
         const mpbp_row_part q = stencil_part(o);
         if (o.sop == SOP_F)
             return f_stencil_cheb_impl(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, &q, xin, b, c1, c2, d, sub,
                                        xo, (void*)st, store_d, p->f_numerics == MPBP_NUMERICS_FAST);
-        return gtg_stencil_cheb_impl(&p->f_prm, p->f_cell, &q, xin, b, c1, c2, d, sub, xo, (void*)st, store_d);
+        return gtg_stencil_cheb_impl(&p->f_prm, p->f_cell, &q, xin, b, c1, c2, d, sub, xo, (void*)st, store_d, dzero);
     }
     return o.sell ? sell_cheb_impl(o.sell, xin, b, dg, c1, c2, d, sub, xo, (void*)st, store_d)
                   : cheb_step_impl(o.csr, o.blk, xin, b, dg, c1, c2, d, sub, xo, (void*)st, store_d);
@@ -6172,7 +6161,8 @@ int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, 
     const bool tpair = K - s >= 2 && o.stencil && o.sop == SOP_F && op.bd.empty && !o.stencil->halo && o.which == 0 &&
                        f_pair_ok(o.stencil) && KO().f_tile && ftile_ok(o.stencil->f_prm.n);
     // restart from the iterate in *cur: d = 0 -- read as +0.0 by the grouped kernel's first sweep, else zeroed
-    bool dzero = !zero && (((op.in.grp || op.in.svl || op.in.gal) && op.bd.empty) || (tpair && s == K - 2));
+    bool dzero = !zero && (((op.in.grp || op.in.svl || op.in.gal || (o.stencil && o.sop == SOP_GTG)) && op.bd.empty) ||
+                           (tpair && s == K - 2));
     if (!zero && !dzero) MPBP_HIP(hipMemsetAsync(d, 0, sizeof(double) * (size_t)nrows, st));
     for (; s < K; ++s) {
         if (tpair && s == K - 2) {
@@ -6956,6 +6946,34 @@ int mpbp_mg_transfer_fill(int32_t n, int32_t nfields, const int32_t* kinds, int3
         return set_error(MPBP_ERR_ARG, "mg_transfer: bad args");
     const int64_t rows = mg_rows(n, nfields, which);
     k_mg_transfer<<<grid_for(rows), kBlock, 0, as_stream(stream)>>>(F, n, which, rows, row_ptr, nullptr, col_idx, val);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int mpbp_mg_transfer_rows_count(int32_t n, int32_t nfields, const int32_t* kinds, int32_t which, const int32_t* rows,
+                                int32_t nrows, int32_t* row_nnz, void* stream) {
+    MgFields F;
+    const int rc = mg_fields(n, nfields, kinds, &F);
+    if (rc) return rc;
+    if (nrows < 0 || (nrows && (!rows || !row_nnz)) || (which != MPBP_MG_P && which != MPBP_MG_R))
+        return set_error(MPBP_ERR_ARG, "mg_transfer_rows: bad args");
+    if (nrows == 0) return MPBP_OK;
+    k_mg_transfer<<<grid_for(nrows), kBlock, 0, as_stream(stream)>>>(F, n, which, nrows, nullptr, row_nnz, nullptr,
+                                                                     nullptr, rows);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
+int mpbp_mg_transfer_rows_fill(int32_t n, int32_t nfields, const int32_t* kinds, int32_t which, const int32_t* rows,
+                               int32_t nrows, const int32_t* row_ptr, int32_t* col_idx, double* val, void* stream) {
+    MgFields F;
+    const int rc = mg_fields(n, nfields, kinds, &F);
+    if (rc) return rc;
+    if (nrows < 0 || (nrows && (!rows || !row_ptr || !col_idx || !val)) || (which != MPBP_MG_P && which != MPBP_MG_R))
+        return set_error(MPBP_ERR_ARG, "mg_transfer_rows: bad args");
+    if (nrows == 0) return MPBP_OK;
+    k_mg_transfer<<<grid_for(nrows), kBlock, 0, as_stream(stream)>>>(F, n, which, nrows, row_ptr, nullptr, col_idx, val,
+                                                                     rows);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }

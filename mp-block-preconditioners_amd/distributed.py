@@ -457,6 +457,239 @@ def level_partitions(part: RowPartition, sizes) -> list[RowPartition]:
     return parts
 
 
+def _csr_rows(M: DeviceCSR, idx: torch.Tensor) -> DeviceCSR:
+    """Rows idx (local row numbers of M, device) of M in that order: entries and their order kept, columns as they are."""
+    rp = M.row_ptr.to(torch.int64)
+    idx = idx.to(torch.int64)
+    lens = rp[idx + 1] - rp[idx]
+    nrp = torch.zeros(idx.numel() + 1, dtype=torch.int64, device=rp.device)
+    torch.cumsum(lens, 0, out=nrp[1:])
+    owner = torch.repeat_interleave(torch.arange(idx.numel(), device=rp.device), lens)
+    src = rp[idx][owner] + (torch.arange(int(nrp[-1]), device=rp.device) - nrp[:-1][owner])
+    return DeviceCSR(nrp.to(torch.int32), M.col_idx[src].contiguous(), M.val[src].contiguous(), (idx.numel(), M.shape[1]))
+
+
+def _positions(keys: torch.Tensor, v: torch.Tensor) -> torch.Tensor:
+    """Positions of the values v in the sorted `keys` (every value must be a key)."""
+    k = keys.to(torch.int64)
+    vv = v.to(torch.int64)
+    pos = torch.searchsorted(k, vv)
+    if v.numel() and (int(pos.max()) >= k.numel() or not bool((k[pos] == vv).all())):
+        raise ValueError("a row / column outside this rank's band")
+    return pos
+
+
+def _relabel_cols(M: DeviceCSR, keys: torch.Tensor) -> DeviceCSR:
+    """M with every column replaced by its position in the sorted `keys`: the same entries in the same order (the
+    relabelling is monotone), as a product's left operand indexing the rows `keys` of the right one."""
+    return DeviceCSR(M.row_ptr, _positions(keys, M.col_idx).to(torch.int32), M.val, (M.shape[0], keys.numel()))
+
+
+def _allgather_csr(M: DeviceCSR, rows: torch.Tensor, nrows: int, group) -> DeviceCSR:
+    """The whole operator from every rank's rows: M holds the global rows `rows` of this rank (global columns); the
+    result has every one of the `nrows` rows in global order, each row's entries in their order."""
+    import torch.distributed as dist
+    dev = M.val.device
+    cdev = dev if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    world = dist.get_world_size(group)
+    lens = (M.row_ptr[1:] - M.row_ptr[:-1]).to(torch.int64)
+    meta = torch.tensor([rows.numel(), M.col_idx.numel()], dtype=torch.int64, device=cdev)
+    metas = [torch.empty_like(meta) for _ in range(world)]
+    dist.all_gather(metas, meta, group=group)
+    cnt = [(int(m[0]), int(m[1])) for m in metas]
+
+    def gather(t, k, dtype):
+        size = max(max(c[k] for c in cnt), 1)
+        buf = torch.zeros(size, dtype=dtype, device=cdev)
+        buf[: t.numel()] = t.to(device=cdev, dtype=dtype)
+        outs = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(outs, buf, group=group)
+        return torch.cat([o[: c[k]] for o, c in zip(outs, cnt)]).to(dev)
+    r_all, l_all = gather(rows, 0, torch.int64), gather(lens, 0, torch.int64)
+    c_all, v_all = gather(M.col_idx, 1, torch.int64), gather(M.val, 1, torch.float64)
+    perm = torch.argsort(r_all)
+    if r_all.numel() != nrows or not bool((r_all[perm] == torch.arange(nrows, device=dev)).all()):
+        raise ValueError("the ranks' rows do not cover the level exactly once")
+    start = torch.zeros(nrows + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(l_all, 0, out=start[1:])
+    ls = l_all[perm]
+    rp = torch.zeros(nrows + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(ls, 0, out=rp[1:])
+    owner = torch.repeat_interleave(torch.arange(nrows, device=dev), ls)
+    src = start[perm][owner] + (torch.arange(int(rp[-1]), device=dev) - rp[:-1][owner])
+    return DeviceCSR(rp.to(torch.int32), c_all[src].to(torch.int32).contiguous(), v_all[src].contiguous(),
+                     (nrows, M.shape[1]))
+
+
+def mg_part_cap(sizes, part: RowPartition, nfields: int, min_cells: int = 1 << 14,
+                max_part_levels: int | None = None) -> int:
+    """The levels [0, cap) a row-partitioned hierarchy may split by size alone: PartitionedMultigrid's rule without
+    the ghost-depth test (which can only stop it earlier)."""
+    nl = len(sizes)
+    parts = level_partitions(part, sizes)
+    cap = nl - 1 if max_part_levels is None else max(1, min(nl - 1, max_part_levels))
+    for l in range(1, nl - 1):
+        q = parts[l]
+        if l >= cap or nfields * q.n * q.n // part.world < min_cells or q.min_rows < 1:
+            return l
+    return nl - 1
+
+
+def mg_bands(sizes, fields, part: RowPartition, cap: int, device) -> list:
+    """S_l, l = 0 .. cap: the rows of level l (sorted global ids, device int32) a rank forms to have its owned rows of
+    every level down to `cap`: S_cap = the owned rows, S_l = the owned rows and every fine row the restriction of
+    S_{l+1} reads (A_{l+1} = R_l (A_l P_l) row by row needs exactly those rows of A_l)."""
+    from .mg import transfer_rows
+    nf = len(fields)
+    parts = level_partitions(part, sizes)
+    own = [torch.from_numpy(q.owned_rows(nf).astype(np.int32)).to(device) for q in parts[: cap + 1]]
+    S = [None] * (cap + 1)
+    S[cap] = own[cap]
+    for l in range(cap - 1, -1, -1):
+        R = transfer_rows(sizes[l], fields, _lib.MG_R, S[l + 1])
+        S[l] = torch.unique(torch.cat([own[l], R.col_idx])).to(torch.int32)
+    return S
+
+
+class LocalHierarchy:
+    """The multigrid levels one rank of a row partition needs, formed from its own rows: no global operator on any
+    rank (setup memory O(N / world + ghosts) down to the replicated coarse levels).
+
+    A0 holds the rows S[0] (mg_bands) of level 0's operator with their global columns (assembled, or the rank-local
+    product rows of Gt_G).  Level l + 1's band is R_l[S_{l+1}] (A_l[S_l] P_l) with the restriction's columns relabelled
+    into S_l and A_l's into the fine rows it reaches (monotone relabellings: each product row performs the global
+    SpGEMM's operations in its order -- the one-GPU hierarchy's rows bit for bit), the transfers' rows built for those
+    rows only (mpbp_mg_transfer_rows_*).  replicated(P) all-gathers the ranks' owned rows of level P and coarsens
+    that level as mg.Multigrid does (the levels below are small): the same operators as the one-GPU hierarchy's."""
+
+    def __init__(self, A0: DeviceCSR, S: list, sizes, fields, part: RowPartition, group=None, pre=2, post=2,
+                 cycles=1, ratio=4.0, coarsest=8):
+        from .mg import transfer_rows
+        self.device = A0.val.device
+        self.sizes, self.fields, self.n, self.nf = list(sizes), tuple(fields), int(sizes[0]), len(fields)
+        self.nlevels = len(self.sizes)
+        self.pre, self.post, self.cycles, self.ratio, self.coarsest = pre, post, cycles, ratio, coarsest
+        self.S, self.part, self.group = S, part, group
+        if A0.shape[0] != S[0].numel():
+            raise ValueError("A0 must hold the band rows S[0]")
+        self.band = [A0]
+        for l in range(len(S) - 1):
+            A = self.band[l]
+            C = torch.unique(A.col_idx)
+            AP = spgemm(_relabel_cols(A, C), transfer_rows(self.sizes[l], self.fields, _lib.MG_P, C))
+            R = transfer_rows(self.sizes[l], self.fields, _lib.MG_R, S[l + 1])
+            self.band.append(spgemm(_relabel_cols(R, S[l]), AP))
+            del AP, R
+        self._rep = {}
+
+    def op_rows(self, l: int, rows: torch.Tensor) -> DeviceCSR:
+        return _csr_rows(self.band[l], _positions(self.S[l], rows))
+
+    def R_rows(self, l: int, rows: torch.Tensor) -> DeviceCSR:
+        from .mg import transfer_rows
+        return transfer_rows(self.sizes[l], self.fields, _lib.MG_R, rows)
+
+    def P_rows(self, l: int, rows: torch.Tensor) -> DeviceCSR:
+        from .mg import transfer_rows
+        return transfer_rows(self.sizes[l], self.fields, _lib.MG_P, rows)
+
+    def diag_rows(self, l: int, rows: torch.Tensor) -> torch.Tensor:
+        return _row_diagonal(self.op_rows(l, rows), rows)
+
+    def bounds(self, l: int, rows: torch.Tensor):
+        """(lmin, lmax) of level l's smoother: the Gershgorin bound is the maximum over the ranks of their owned rows'
+        (every row's sum is the global operator's): the one-GPU hierarchy's bound, exactly."""
+        import torch.distributed as dist
+        lm = self.op_rows(l, rows).gershgorin(self.diag_rows(l, rows)) if rows.numel() else 0.0
+        cdev = self.device if dist.get_backend(self.group) == "nccl" else "cpu"
+        t = torch.tensor([lm], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        lmax = float(t.item())
+        return lmax / self.ratio, lmax
+
+    def replicated(self, P: int):
+        """mg.Multigrid of level P's whole operator (every rank's owned rows of it, all-gathered): levels P .. end."""
+        if P not in self._rep:
+            from .mg import Multigrid
+            q = level_partitions(self.part, self.sizes)[P]
+            own = torch.from_numpy(q.owned_rows(self.nf).astype(np.int32)).to(self.device)
+            full = _allgather_csr(self.op_rows(P, own), own, self.nf * self.sizes[P] ** 2, self.group)
+            if P == self.nlevels - 1:   # only the coarsest level: its dense inverse
+                self._rep[P] = _CoarsestLevel(full, self.ratio)
+            else:
+                sub = Multigrid(full, self.sizes[P], self.fields, pre=self.pre, post=self.post, cycles=self.cycles,
+                                ratio=self.ratio, coarsest=self.coarsest, fine_sell=True)
+                if sub.sizes != self.sizes[P:]:
+                    raise AssertionError(f"coarse levels {sub.sizes} != {self.sizes[P:]}")
+                self._rep[P] = sub
+        return self._rep[P]
+
+
+class _CoarsestLevel:
+    """The coarsest level alone (a hierarchy partitioned down to it): its operator, buffers and dense pseudo-inverse, as
+    mg.Multigrid holds its last level (the same struct fields, the same inverse)."""
+
+    def __init__(self, A: DeviceCSR, ratio: float):
+        from .mg import dense_inverse_csr
+        dev = A.val.device
+        d = A.diagonal()
+        lmax = A.gershgorin(d)
+        self.bounds = [(lmax / ratio, lmax)]
+        self.A, self.diag = A, d
+        self.coarse_inv, inv = dense_inverse_csr(A)
+        self.coarse_dense = torch.from_numpy(np.ascontiguousarray(inv.T)).to(dev)
+        self.work = [[torch.zeros(A.shape[0], dtype=torch.float64, device=dev) for _ in range(5)]]
+        self._levels = (_lib.MgLevel * 1)()
+        L = self._levels[0]
+        L.nrows = A.shape[0]
+        L.lmin, L.lmax = self.bounds[0]
+        L.A, L.A_blocks, L.diag = A.cstruct(), A.blocks.cstruct(), d.data_ptr()
+        L.R = L.P = _lib.Csr(0, 0, 0, None, None, None)
+        L.R_blocks = L.P_blocks = _lib.RowBlocks(None, 0)
+        L.x, L.t, L.r, L.d, L.b = (w.data_ptr() for w in self.work[0])
+
+
+class _GlobalLevels:
+    """LocalHierarchy's interface over a whole mg.Multigrid (every rank holds the global hierarchy)."""
+
+    def __init__(self, g):
+        self.g = g
+        self.device, self.sizes, self.fields, self.n = g.device, g.sizes, g.fields, g.n
+        self.nlevels, self.pre, self.post, self.cycles = g.nlevels, g.pre, g.post, g.cycles
+
+    def _rows(self, M, rows):
+        return M.extract(rows, torch.arange(M.shape[1], dtype=torch.int32, device=self.device), M.shape[1])
+
+    def op_rows(self, l, rows):
+        return self._rows(self.g.ops[l], rows)
+
+    def R_rows(self, l, rows):
+        return self._rows(self.g.R[l], rows)
+
+    def P_rows(self, l, rows):
+        return self._rows(self.g.P[l], rows)
+
+    def diag_rows(self, l, rows):
+        return self.g.diags[l][rows.long()].contiguous()
+
+    def bounds(self, l, rows):
+        return self.g.bounds[l]
+
+    def replicated(self, P):
+        return _Shifted(self.g, P)
+
+
+class _Shifted:
+    """Levels P .. end of a whole hierarchy, numbered from 0 (LocalHierarchy.replicated's form)."""
+
+    def __init__(self, g, P):
+        self.g, self.P = g, P
+        self._levels = g._levels[P:]
+        self.work = g.work[P:]
+        self.bounds = g.bounds[P:]
+        self.coarse_inv, self.coarse_dense = g.coarse_inv, g.coarse_dense
+
+
 class PartitionedMultigrid:
     """A multigrid hierarchy (mg.Multigrid, built on every rank from the global operator -- setup only) split over a
     row partition for the partitioned Schur apply (solve.py:266 / 274's pointer, under north_star's row partition).
@@ -472,6 +705,8 @@ class PartitionedMultigrid:
 
     def __init__(self, g, part: RowPartition, nfields: int, group=None, min_cells: int = 1 << 14,
                  max_part_levels: int | None = None):
+        # g: a LocalHierarchy (this rank's rows only) or a whole mg.Multigrid (every rank holds it)
+        g = g if isinstance(g, LocalHierarchy) else _GlobalLevels(g)
         self.g, self.part0, self.nf, self.group = g, part, nfields, group
         dev = g.device
         self.device = dev
@@ -482,10 +717,9 @@ class PartitionedMultigrid:
         def owned(l):
             return torch.from_numpy(self.parts[l].owned_rows(nfields).astype(np.int32)).to(dev)
 
-        def depth(M, rows, l):   # ghost rows of level l read by M's rows `rows` (M's columns at level l)
+        def depth(full, l):   # ghost rows of level l read by the rows `full` (global columns at level l)
             if world == 1:
                 return 1
-            full = M.extract(rows, torch.arange(M.shape[1], dtype=torch.int32, device=dev), M.shape[1])
             q = self.parts[l]
             return ghost_depth(full.col_idx, q.n, q.r0, q.L)
 
@@ -497,15 +731,15 @@ class PartitionedMultigrid:
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
             return int(t.item())
 
-        self.h0 = reduce_max(max(1, depth(g.R[0], owned(1), 0)))   # level 0 ghosts the restriction reads
+        self.h0 = reduce_max(max(1, depth(g.R_rows(0, owned(1)), 0)))   # level 0 ghosts the restriction reads
         self.h = [self.h0]
         P = nl - 1
         cap = nl - 1 if max_part_levels is None else max(1, min(nl - 1, max_part_levels))
         for l in range(1, nl - 1):
             q = self.parts[l]
             cells = nfields * q.n * q.n // world
-            hl = reduce_max(max(1, depth(g.ops[l], owned(l), l), depth(g.R[l], owned(l + 1), l),
-                                depth(g.P[l - 1], owned(l - 1), l)))
+            hl = reduce_max(max(1, depth(g.op_rows(l, owned(l)), l), depth(g.R_rows(l, owned(l + 1)), l),
+                                depth(g.P_rows(l - 1, owned(l - 1)), l)))
             if l >= cap or cells < min_cells or q.min_rows < hl:
                 P = l
                 break
@@ -519,6 +753,7 @@ class PartitionedMultigrid:
         halo kind (the Schur apply's velocity / pressure kind; None: a new one); A0: level 0's local operator for the
         standalone solve (mpbp_mg_solve; None inside the Schur apply, whose level 0 is its own operator)."""
         g, nf, P, dev = self.g, self.nf, self.part_levels, self.device
+        rep = g.replicated(P)   # levels P .. end, whole on every rank
         if h0 < self.h0:
             raise ValueError(f"level 0 ghost depth {h0} < the restriction's {self.h0}")
         self.h[0] = h0
@@ -536,14 +771,15 @@ class PartitionedMultigrid:
         for l in range(g.nlevels):
             L = self._levels[l]
             L.pre, L.post = g.pre, g.post
-            L.lmin, L.lmax = g.bounds[l]
-            if l >= P:   # replicated: the global level as it stands
-                G = g._levels[l]
+            if l >= P:   # replicated: the whole level
+                G = rep._levels[l - P]
                 for name, _ in _lib.MgLevel._fields_:
                     setattr(L, name, getattr(G, name))
+                L.lmin, L.lmax = rep.bounds[l - P]
                 continue
             q = self.parts[l]
             rows = self._owned(l)
+            L.lmin, L.lmax = g.bounds(l, rows)
             ext = q.n_ext(nf, self.h[l])
             cm = torch.from_numpy(q.colmap(nf, self.h[l])).to(dev)
             if l + 1 < P:
@@ -551,10 +787,13 @@ class PartitionedMultigrid:
                 cm_next = torch.from_numpy(qn.colmap(nf, self.h[l + 1])).to(dev)
                 ext_next = qn.n_ext(nf, self.h[l + 1])
             else:
-                ncoarse = g.ops[l + 1].shape[0]
+                ncoarse = nf * g.sizes[l + 1] ** 2
                 cm_next, ext_next = torch.arange(ncoarse, dtype=torch.int32, device=dev), ncoarse
-            R = g.R[l].extract(self._owned(l + 1), cm, ext)
-            Pm = g.P[l].extract(rows, cm_next, ext_next)
+
+            def local(M, cmap, ncols):   # all rows of M (global columns) with the columns into the ghost layout
+                return M.extract(torch.arange(M.shape[0], dtype=torch.int32, device=dev), cmap, ncols)
+            R = local(g.R_rows(l, self._owned(l + 1)), cm, ext)
+            Pm = local(g.P_rows(l, rows), cm_next, ext_next)
             own = q.n_owned(nf)
             L.nrows = own
             if l == 0:
@@ -568,8 +807,8 @@ class PartitionedMultigrid:
                 r = torch.zeros(ext, **f64)
                 d, bb = torch.zeros(own, **f64), torch.zeros(own, **f64)
             else:
-                A = g.ops[l].extract(rows, cm, ext)
-                dg = g.diags[l][rows.long()].contiguous()
+                A = local(g.op_rows(l, rows), cm, ext)
+                dg = g.diag_rows(l, rows)
                 L.A, L.A_blocks, L.diag = A.cstruct(), A.blocks.cstruct(), dg.data_ptr()
                 SA = sell_copy(A)
                 L.A_sell = SA.cstruct() if SA is not None else empty_sell
@@ -587,14 +826,14 @@ class PartitionedMultigrid:
             halos.register(x, t, r, d, bb)
         # the gather level's r (the rank's rows, written by the restriction) and b (the whole level) are the global
         # level's full-size buffers
-        Gw = g.work[P]
+        Gw = rep.work[0]
         halos.register(*Gw)
-        self._keep = keep
+        self._keep = keep + [rep]
         self._halos = halos
         self._mg = _lib.Mg(g.nlevels, g.cycles if cycles is None else cycles,
                            ctypes.cast(self._levels, ctypes.POINTER(_lib.MgLevel)),
-                           g.coarse_inv.cstruct(), g.coarse_inv.blocks.cstruct(),
-                           g.coarse_dense.data_ptr() if g.coarse_dense is not None else None,
+                           rep.coarse_inv.cstruct(), rep.coarse_inv.blocks.cstruct(),
+                           rep.coarse_dense.data_ptr() if rep.coarse_dense is not None else None,
                            P, self.gather_kind, halos.fn, halos.ctx, halos.gather_fn)
         from .mg import set_transfer_kinds
         set_transfer_kinds(self._mg, g.fields, g.n)   # (matrix-free transfers on the replicated levels only)
@@ -769,11 +1008,10 @@ class DistributedSchurPreconditioner(PlanProfiling):
         rows_u = torch.from_numpy(part.owned_rows(N_VEL_FIELDS).astype(np.int32)).to(dev)
         rows_p = torch.from_numpy(part.owned_rows(N_P_FIELDS).astype(np.int32)).to(dev)
         ik_f, ik_p = inner_F or InnerSolver(), inner_P or InnerSolver()
-        mg_req = "mg" in (ik_f.kind, ik_p.kind)
-        # the commutator products: with Jacobi / Chebyshev inner solves only this rank's pressure rows of Gt_G and
-        # Gt_F_G (a product's row depends on that row of D alone: the same bits as the global product's row, for a
-        # 1 / world share of the SpGEMM work); multigrid builds its Galerkin hierarchy from the whole Gt_G
-        self.local_products = bool(local_products) and not mg_req and world > 1
+        # the commutator products: only this rank's pressure rows of Gt_G and Gt_F_G (a product's row depends on that
+        # row of D alone: the same bits as the global product's row, for a 1 / world share of the SpGEMM work);
+        # multigrid inner solves form their levels from this rank's band of rows too (LocalHierarchy)
+        self.local_products = bool(local_products) and world > 1
         akw = dict(c=c, d_u=d_u)
         Gs = None
         if self.local_products:
@@ -848,11 +1086,29 @@ class DistributedSchurPreconditioner(PlanProfiling):
             if ca is True:
                 raise ValueError("ca=True needs Jacobi / Chebyshev inner solves (multigrid exchanges per operator)")
             kw = dict(group=group, min_cells=mg_min_cells, max_part_levels=mg_part_levels)
+
+            def local_mg(ik, fields):
+                # this rank's band of level 0 (mg_bands), then its Galerkin levels (LocalHierarchy): no global operator
+                from .mg import level_sizes
+                sizes = level_sizes(n, ik.coarsest)
+                cap = mg_part_cap(sizes, part, len(fields), mg_min_cells, mg_part_levels)
+                S = mg_bands(sizes, fields, part, cap, dev)
+                if fields is FIELDS_VELOCITY:
+                    A0 = bp.assemble_rows(_lib.OP_F, S[0], **akw)
+                else:   # Gt_G's band rows = (-D) G on them, G on the velocity rows those rows of D reach
+                    Db = bp.assemble_rows(_lib.OP_D, S[0], **akw)
+                    Gb = bp.assemble_rows(_lib.OP_G, torch.unique(Db.col_idx), global_shape=True, **akw)
+                    A0 = spgemm(Db, Gb, alpha=-1.0)
+                    del Db, Gb
+                return LocalHierarchy(A0, S, sizes, fields, part, group, pre=ik.pre, post=ik.post,
+                                      cycles=int(ik.sweeps), ratio=ik.smooth_ratio, coarsest=ik.coarsest)
             if self.inner_F.kind == "mg":
-                gF = self.inner_F.multigrid(F, n, FIELDS_VELOCITY, F.diagonal())
+                gF = local_mg(self.inner_F, FIELDS_VELOCITY) if lp else \
+                    self.inner_F.multigrid(F, n, FIELDS_VELOCITY, F.diagonal())
                 self.mg_F = PartitionedMultigrid(gF, part, N_VEL_FIELDS, **kw) if self.partitioned else gF
             if self.inner_P.kind == "mg":
-                gP = self.inner_P.multigrid(GtG, n, FIELDS_PRESSURE, GtG.diagonal())
+                gP = local_mg(self.inner_P, FIELDS_PRESSURE) if lp else \
+                    self.inner_P.multigrid(GtG, n, FIELDS_PRESSURE, GtG.diagonal())
                 self.mg_P = PartitionedMultigrid(gP, part, N_P_FIELDS, **kw) if self.partitioned else gP
             if isinstance(self.mg_F, PartitionedMultigrid):
                 self.h_u = max(self.h_u, self.mg_F.h0)

@@ -53,6 +53,23 @@ def transfer(n: int, fields, which: int, device) -> DeviceCSR:
     return DeviceCSR(rp, ci, va, (rows, cols))
 
 
+def transfer_rows(n: int, fields, which: int, rows: torch.Tensor) -> DeviceCSR:
+    """Rows `rows` (device int32 global ids) of transfer(n, fields, which) with their global columns, the same entries
+    (mpbp_mg_transfer_rows_*): a rank's band of a row-partitioned hierarchy."""
+    kinds = np.ascontiguousarray(np.asarray(fields, dtype=np.int32).reshape(-1))
+    nf = len(fields)
+    cols = nf * ((n // 2) ** 2 if which == _lib.MG_P else n * n)
+    rows = rows.to(torch.int32).contiguous()
+    m = rows.numel()
+    row_nnz = torch.empty(max(m, 1), dtype=torch.int32, device=rows.device)[:m]
+    check(lib().mpbp_mg_transfer_rows_count(n, nf, kinds.ctypes.data_as(ctypes.c_void_p), which, ptr(rows), m,
+                                            ptr(row_nnz), stream_handle()))
+    rp, ci, va = csr_from_row_nnz(row_nnz, (m, cols), rows.device)
+    check(lib().mpbp_mg_transfer_rows_fill(n, nf, kinds.ctypes.data_as(ctypes.c_void_p), which, ptr(rows), m, ptr(rp),
+                                           ptr(ci), ptr(va), stream_handle()))
+    return DeviceCSR(rp, ci, va, (m, cols))
+
+
 def sell_copy(A: DeviceCSR) -> DeviceSELL | None:
     """SELL-64 copy of A when every row has < 256 entries (the layout's row-length byte), else None."""
     rp = A.row_ptr_host

@@ -300,7 +300,8 @@ def _mg_worker(rank, world, port, n, inner, min_cells, halo, errfile, numerics="
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         import mp_block_preconditioners_amd as mpb
-        from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner, PartitionedMultigrid
+        from mp_block_preconditioners_amd.distributed import (DistributedSchurPreconditioner, LocalHierarchy,
+                                                              PartitionedMultigrid)
         iF, iP = _inner_pair(inner)
         dpc = DistributedSchurPreconditioner(n, 1.0, 100.0, 1.0, inner_F=iF, inner_P=iP, halo=halo,
                                              self_halo=(world == 1), mg_min_cells=min_cells, numerics=numerics)
@@ -309,6 +310,10 @@ def _mg_worker(rank, world, port, n, inner, min_cells, halo, errfile, numerics="
                 assert isinstance(m, PartitionedMultigrid) and 1 <= m.part_levels <= m.g.nlevels - 1
                 if min_cells == 0 and world > 1:   # every level but the coarsest partitioned (where rows allow)
                     assert m.part_levels >= min(2, m.g.nlevels - 1), (m.part_levels, m.g.sizes)
+                if world > 1:   # rank-local levels: this rank's band of rows, no global operator
+                    assert isinstance(m.g, LocalHierarchy)
+                    if min_cells:
+                        assert m.g.band[0].shape[0] < m.nf * m.g.sizes[0] ** 2, (m.g.band[0].shape, m.g.sizes)
         bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
         _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
         pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, numerics=numerics,
@@ -347,7 +352,8 @@ def test_partitioned_multigrid_apply_matches_single_gpu(world, n, inner, min_cel
     """Row 18: multigrid inner solves under the row partition -- level 0 the apply's own matrix-free F / Gt_G, the
     Galerkin levels row-partitioned down to part_levels (ghost rows per operator), the coarser levels all-gathered and
     replicated -- bit for bit against the one-GPU apply (2-4 gloo ranks; ceil-halved partitions at n = 50; the RCCL
-    self-exchange, captured)."""
+    self-exchange, captured).  With 2+ ranks every level is formed from the rank's own band of rows (LocalHierarchy:
+    rank-local Galerkin products, level part_levels all-gathered from the ranks' rows)."""
     errfile = str(tmp_path / "err.txt")
     _spawn(_mg_worker, (world, _free_port(), n, inner, min_cells, halo, errfile, numerics), world, errfile)
 

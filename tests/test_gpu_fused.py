@@ -83,13 +83,11 @@ def test_ftile_equals_marching(n, kf, fuse_g):
 @pytest.mark.parametrize("n", [3, 5, 64, 70, 71, 72, 76, 100, 128, 255, 256, 300])
 @pytest.mark.parametrize("kf", [2, 3, 4, 5])
 @pytest.mark.parametrize("fuse_g", [True, False])
-@pytest.mark.parametrize("tpb", [256, 512])
-def test_fsolve_equals_ftile(n, kf, fuse_g, tpb):
+def test_fsolve_equals_ftile(n, kf, fuse_g):
     """k_fsolve (a whole fast F solve of 3 or 4 updates in one tiled launch: x0 and every sweep over a shrinking halo,
     each cell's state in its owning lane) performs the k_ftile launches' operations: the apply is bit-identical with it
     on and off, with G x_p recomputed in the second solve and launched separately, on grids below, at and above its
-    minimum (n >= 70 for 3 updates, 72 for 4) and not multiples of the 64 x 8 tile; with 256 lanes per workgroup (two
-    tile cells and a cell of every ring each) and with 512 (kernel option f_tpb: one tile cell, at most one ring cell)."""
+    minimum (n >= 70 for 3 updates, 72 for 4) and not multiples of the 64 x 8 tile."""
     import mp_block_preconditioners_amd as mp
     bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
     _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
@@ -99,7 +97,7 @@ def test_fsolve_equals_ftile(n, kf, fuse_g, tpb):
                     generator=torch.Generator(device="cuda").manual_seed(n * 10 + kf + 7))
     pc.set_kernel_opts(f_solve=0)
     ref = pc.apply(v).clone()
-    pc.set_kernel_opts(f_solve=1, f_tpb=tpb)
+    pc.set_kernel_opts(f_solve=1)
     got = pc.apply(v)
     assert torch.equal(got, ref), float((got - ref).abs().max())
 
