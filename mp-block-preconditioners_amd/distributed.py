@@ -563,8 +563,9 @@ class LocalHierarchy:
     that level as mg.Multigrid does (the levels below are small): the same operators as the one-GPU hierarchy's."""
 
     def __init__(self, A0: DeviceCSR, S: list, sizes, fields, part: RowPartition, group=None, pre=2, post=2,
-                 cycles=1, ratio=4.0, coarsest=8):
+                 cycles=1, ratio=4.0, coarsest=8, stamp=None):
         from .mg import transfer_rows
+        stamp = stamp or (lambda name: None)
         self.device = A0.val.device
         self.sizes, self.fields, self.n, self.nf = list(sizes), tuple(fields), int(sizes[0]), len(fields)
         self.nlevels = len(self.sizes)
@@ -580,7 +581,9 @@ class LocalHierarchy:
             R = transfer_rows(self.sizes[l], self.fields, _lib.MG_R, S[l + 1])
             self.band.append(spgemm(_relabel_cols(R, S[l]), AP))
             del AP, R
+            stamp(f"mg_band_level{l + 1}")
         self._rep = {}
+        self.stamp = stamp
 
     def op_rows(self, l: int, rows: torch.Tensor) -> DeviceCSR:
         return _csr_rows(self.band[l], _positions(self.S[l], rows))
@@ -614,6 +617,7 @@ class LocalHierarchy:
             q = level_partitions(self.part, self.sizes)[P]
             own = torch.from_numpy(q.owned_rows(self.nf).astype(np.int32)).to(self.device)
             full = _allgather_csr(self.op_rows(P, own), own, self.nf * self.sizes[P] ** 2, self.group)
+            self.stamp("mg_gather_level")
             if P == self.nlevels - 1:   # only the coarsest level: its dense inverse
                 self._rep[P] = _CoarsestLevel(full, self.ratio)
             else:
@@ -622,6 +626,7 @@ class LocalHierarchy:
                 if sub.sizes != self.sizes[P:]:
                     raise AssertionError(f"coarse levels {sub.sizes} != {self.sizes[P:]}")
                 self._rep[P] = sub
+            self.stamp("mg_replicated_levels")
         return self._rep[P]
 
 
@@ -1093,6 +1098,7 @@ class DistributedSchurPreconditioner(PlanProfiling):
                 sizes = level_sizes(n, ik.coarsest)
                 cap = mg_part_cap(sizes, part, len(fields), mg_min_cells, mg_part_levels)
                 S = mg_bands(sizes, fields, part, cap, dev)
+                _stamp("mg_bands")
                 if fields is FIELDS_VELOCITY:
                     A0 = bp.assemble_rows(_lib.OP_F, S[0], **akw)
                 else:   # Gt_G's band rows = (-D) G on them, G on the velocity rows those rows of D reach
@@ -1100,8 +1106,9 @@ class DistributedSchurPreconditioner(PlanProfiling):
                     Gb = bp.assemble_rows(_lib.OP_G, torch.unique(Db.col_idx), global_shape=True, **akw)
                     A0 = spgemm(Db, Gb, alpha=-1.0)
                     del Db, Gb
+                _stamp("mg_band_level0")
                 return LocalHierarchy(A0, S, sizes, fields, part, group, pre=ik.pre, post=ik.post,
-                                      cycles=int(ik.sweeps), ratio=ik.smooth_ratio, coarsest=ik.coarsest)
+                                      cycles=int(ik.sweeps), ratio=ik.smooth_ratio, coarsest=ik.coarsest, stamp=_stamp)
             if self.inner_F.kind == "mg":
                 gF = local_mg(self.inner_F, FIELDS_VELOCITY) if lp else \
                     self.inner_F.multigrid(F, n, FIELDS_VELOCITY, F.diagonal())
@@ -1212,8 +1219,10 @@ class DistributedSchurPreconditioner(PlanProfiling):
             # multigrid under the partition: level 0 is the apply's own F / Gt_G with its ping / pong buffers
             if isinstance(self.mg_F, PartitionedMultigrid):
                 self.mg_F.build(self._halos, (self._wu[1], self._wu[2]), self.diag_F, self.h_u, kind0=_lib.VEC_VELOCITY)
+                _stamp("mg_build_F")
             if isinstance(self.mg_P, PartitionedMultigrid):
                 self.mg_P.build(self._halos, (self._wp[4], self._wp[5]), self.diag_P, self.h_p, kind0=_lib.VEC_PRESSURE)
+                _stamp("mg_build_P")
         else:
             self._cb = _lib.HALO_FN()
         _stamp("halo_and_workspace")
