@@ -469,20 +469,26 @@ def _csr_rows(M: DeviceCSR, idx: torch.Tensor) -> DeviceCSR:
     return DeviceCSR(nrp.to(torch.int32), M.col_idx[src].contiguous(), M.val[src].contiguous(), (idx.numel(), M.shape[1]))
 
 
-def _positions(keys: torch.Tensor, v: torch.Tensor) -> torch.Tensor:
-    """Positions of the values v in the sorted `keys` (every value must be a key)."""
+def _positions(keys: torch.Tensor, v: torch.Tensor, bad: torch.Tensor | None = None) -> torch.Tensor:
+    """Positions of the values v in the sorted `keys` (every value must be a key).  bad (a device bool, optional):
+    OR-ed with "some value is not a key" and left for the caller to check once (no device synchronisation here);
+    without it the check is made at once."""
     k = keys.to(torch.int64)
     vv = v.to(torch.int64)
     pos = torch.searchsorted(k, vv)
-    if v.numel() and (int(pos.max()) >= k.numel() or not bool((k[pos] == vv).all())):
-        raise ValueError("a row / column outside this rank's band")
+    if v.numel():
+        miss = (pos >= k.numel()) | (k[pos.clamp(max=max(k.numel() - 1, 0))] != vv)
+        if bad is not None:
+            bad |= miss.any()
+        elif bool(miss.any()):
+            raise ValueError("a row / column outside this rank's band")
     return pos
 
 
-def _relabel_cols(M: DeviceCSR, keys: torch.Tensor) -> DeviceCSR:
+def _relabel_cols(M: DeviceCSR, keys: torch.Tensor, bad: torch.Tensor | None = None) -> DeviceCSR:
     """M with every column replaced by its position in the sorted `keys`: the same entries in the same order (the
     relabelling is monotone), as a product's left operand indexing the rows `keys` of the right one."""
-    return DeviceCSR(M.row_ptr, _positions(keys, M.col_idx).to(torch.int32), M.val, (M.shape[0], keys.numel()))
+    return DeviceCSR(M.row_ptr, _positions(keys, M.col_idx, bad).to(torch.int32), M.val, (M.shape[0], keys.numel()))
 
 
 def _allgather_csr(M: DeviceCSR, rows: torch.Tensor, nrows: int, group) -> DeviceCSR:
@@ -574,14 +580,17 @@ class LocalHierarchy:
         if A0.shape[0] != S[0].numel():
             raise ValueError("A0 must hold the band rows S[0]")
         self.band = [A0]
+        bad = torch.zeros((), dtype=torch.bool, device=self.device)   # checked once (each sync costs under contention)
         for l in range(len(S) - 1):
             A = self.band[l]
             C = torch.unique(A.col_idx)
-            AP = spgemm(_relabel_cols(A, C), transfer_rows(self.sizes[l], self.fields, _lib.MG_P, C))
+            AP = spgemm(_relabel_cols(A, C, bad), transfer_rows(self.sizes[l], self.fields, _lib.MG_P, C))
             R = transfer_rows(self.sizes[l], self.fields, _lib.MG_R, S[l + 1])
-            self.band.append(spgemm(_relabel_cols(R, S[l]), AP))
+            self.band.append(spgemm(_relabel_cols(R, S[l], bad), AP))
             del AP, R
             stamp(f"mg_band_level{l + 1}")
+        if bool(bad):
+            raise ValueError("LocalHierarchy: a restriction row reads outside its band (mg_bands)")
         self._rep = {}
         self.stamp = stamp
 
