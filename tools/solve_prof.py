@@ -3,7 +3,8 @@
 Runs the solve `--reps` times on one preconditioner (its hipGraph captured once, as bench.py does) and prints one JSON
 line per run: wall seconds, iterations, and -- for the first run after torch.cuda.empty_cache() -- what the basis
 allocation costs.  Run it under `rocprofv3 --kernel-trace --stats` for the per-kernel split (apply graph, CSR A,
-rdot / gs_update passes, small launches)."""
+the orthogonalisation's passes, small launches).  --ortho: dcgs2 (the default: rdot2 + dcgs2_update, two basis passes
+per iteration), cgs2 (rdot + gs_update twice: four passes), cgs2_fused (the fused update + projection kernel)."""
 import argparse
 import json
 import os
@@ -20,7 +21,7 @@ def main():
     ap.add_argument("--inner", default="mg:1")
     ap.add_argument("--numerics", default="fast")
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--cgs2", default="fused,apart", help="FGMRES orthogonalisations to time, in order")
+    ap.add_argument("--ortho", default="dcgs2,cgs2", help="FGMRES orthogonalisations to time, in order")
     args = ap.parse_args()
     import torch
     import mp_block_preconditioners_amd as mp
@@ -50,15 +51,16 @@ def main():
         A.matvec(v)
     torch.cuda.synchronize()
     a_ms = (time.perf_counter() - t0) / 10 * 1e3
-    for r, mode in ((r, mode) for mode in args.cgs2.split(",") for r in range(args.reps)):
+    for r, mode in ((r, mode) for mode in args.ortho.split(",") for r in range(args.reps)):
         torch.cuda.empty_cache()
         hist = []
         t0 = time.perf_counter()
-        x, info = mp.fgmres(A, bd, M=M, tol=1e-8, maxiter=150, residuals=hist, fused_cgs2=mode == "fused")
+        x, info = mp.fgmres(A, bd, M=M, tol=1e-8, maxiter=150, residuals=hist, fused_cgs2=mode == "cgs2_fused",
+                            ortho="dcgs2" if mode == "dcgs2" else "cgs2")
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         it = len(hist) - 1
-        print(json.dumps({"cgs2": mode, "rep": r, "seconds": el, "iterations": it, "converged": info == 0, "apply_ms": apply_ms,
+        print(json.dumps({"ortho": mode, "rep": r, "seconds": el, "iterations": it, "converged": info == 0, "apply_ms": apply_ms,
                           "A_ms": a_ms, "other_ms_per_iteration": (el * 1e3 - it * (apply_ms + a_ms)) / max(it, 1)}),
               flush=True)
         del x
