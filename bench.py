@@ -27,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0    # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+_KEEP_ALIVE = []         # objects whose lifetime must span the run (an installed kernel_options scope)
 
 
 def parse_inner(s):
@@ -178,6 +179,8 @@ def main():
                          "self-exchange over RCCL (measures the multi-GPU code path's overhead on one GPU)")
     ap.add_argument("--halo-overlap", action="store_true",
                     help="RCCL halo group on a side stream overlapping the interior rows (default: in order)")
+    ap.add_argument("--kernel-opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="a kernel choice (mpbp_kernel_opts field) for every plan of the run; repeatable")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-spmv", action="store_true")
@@ -258,6 +261,11 @@ def main():
     if args.svl_min_rows is not None:
         from mp_block_preconditioners_amd import mg as _mg
         _mg.SVL_MIN_ROWS = None if args.svl_min_rows < 0 else args.svl_min_rows
+    if args.kernel_opt:   # this thread's kernel choices for the whole run: every plan made from here starts from them
+        from mp_block_preconditioners_amd._lib import kernel_options
+        ko = kernel_options(**{k: int(v) for k, v in (o.split("=", 1) for o in args.kernel_opt)})
+        ko.__enter__()
+        _KEEP_ALIVE.append(ko)
 
     if args.weak:
         n = int(round((args.n or 1024) * math.sqrt(world)))

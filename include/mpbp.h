@@ -488,7 +488,9 @@ typedef struct mpbp_kernel_opts {
     int32_t mg_svl;            /* multigrid levels with a stencil-values copy use it (1, default) */
     int32_t mg_mf_transfer;    /* whole-grid multigrid transfers matrix-free when the kinds are known (1, default) */
     int32_t csr_table;         /* CSR SpMV waves start from the row blocks' wave table when present (1, default) */
-    int32_t reserved[7];
+    int32_t mg_fuse_l0;        /* tolerance-mode F hierarchies, one GPU: level 0's pre-smoothing, residual and restriction
+                                  as ONE k_fpre launch, and the prolongation inside the post-smoothing pair (1, default) */
+    int32_t reserved[6];
 } mpbp_kernel_opts;
 /* *out = the calling thread's current choices: its mpbp_kernel_opts_set_thread scope, else the process defaults. */
 void mpbp_kernel_opts_default(mpbp_kernel_opts* out);

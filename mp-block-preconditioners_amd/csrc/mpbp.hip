@@ -27,7 +27,7 @@ thread_local char g_err[1024] = "";
 mpbp_kernel_opts g_defaults = {
     /*march_rows*/ 0, /*init_diag*/ 1, /*f_pair*/ 1, /*f_direct*/ 0, /*gtg_fused*/ 1, /*gtg_tpb*/ 512, /*gtg_drhs*/ 1,
     /*q13_sym*/ 1, /*f_tile*/ 1, /*f_solve*/ 1, /*mg_galerkin_mf*/ 2, /*mg_galerkin_mf_p*/ 1, /*pg_direct*/ 1,
-    /*mg_group_rows*/ 65536, /*mg_svl*/ 1, /*mg_mf_transfer*/ 1, /*csr_table*/ 1, {0, 0, 0, 0, 0, 0, 0}};
+    /*mg_group_rows*/ 65536, /*mg_svl*/ 1, /*mg_mf_transfer*/ 1, /*csr_table*/ 1, /*mg_fuse_l0*/ 1, {0, 0, 0, 0, 0, 0}};
 thread_local const mpbp_kernel_opts* t_opts = nullptr;
 inline const mpbp_kernel_opts& KO() { return t_opts ? *t_opts : g_defaults; }
 struct OptsScope {   // installs a plan's kernel choices (when it has its own) for one entry-point call
@@ -45,9 +45,11 @@ inline int check_opts(const mpbp_kernel_opts* o, const char* who) {
     const bool ok = o->march_rows >= 0 && o->march_rows <= 4096 && (o->gtg_tpb == 256 || o->gtg_tpb == 512) &&
                     o->mg_galerkin_mf >= 0 && o->mg_galerkin_mf <= 2 && o->mg_group_rows >= 0 &&
                     (o->init_diag | o->f_pair | o->f_direct | o->gtg_fused | o->gtg_drhs | o->q13_sym | o->f_tile |
-                     o->f_solve | o->mg_galerkin_mf_p | o->pg_direct | o->mg_svl | o->mg_mf_transfer | o->csr_table) >= 0 &&
+                     o->f_solve | o->mg_galerkin_mf_p | o->pg_direct | o->mg_svl | o->mg_mf_transfer | o->csr_table |
+                     o->mg_fuse_l0) >= 0 &&
                     (o->init_diag | o->f_pair | o->f_direct | o->gtg_fused | o->gtg_drhs | o->q13_sym | o->f_tile |
-                     o->f_solve | o->mg_galerkin_mf_p | o->pg_direct | o->mg_svl | o->mg_mf_transfer | o->csr_table) <= 1;
+                     o->f_solve | o->mg_galerkin_mf_p | o->pg_direct | o->mg_svl | o->mg_mf_transfer | o->csr_table |
+                     o->mg_fuse_l0) <= 1;
     return ok ? MPBP_OK : set_error(MPBP_ERR_ARG, "%s: kernel options out of range", who);
 }   // rows per workgroup of the D / G / Gt_G marching kernels: as F
 
@@ -2839,13 +2841,17 @@ struct FTile {
     double* d_out;        // SD
     double c1a, c2a, c1b, c2b;   // INIT: c2a = c2_0 (c1a unused)
     int dzero = 0;        // !INIT: d_{s-1} is +0.0 (a restart: multigrid post-smoothing), d_in is not read
+    const double* xc = nullptr;   // !INIT: x_in + P_0 xc (the coarse correction of a multigrid level 0, the F
+                                  // hierarchy's MAC kinds) is the iterate -- the prolongation launch folded in
 };
 
-template <bool INIT, bool SUB, bool SD, class BS>
+template <int KY, int KX>
+__device__ inline double g1_p(const double* xf, int gr, int gc, int nc, int rb, int cb);
+template <bool INIT, bool SUB, bool SD, class BS, bool PRO = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) MPBP_LDS_READS k_ftile(FStencilFast P, FTile a, BS bs) {
     __shared__ double xs[INIT ? 1 : 4 * kFSN];   // !INIT: x_in over the tile + 2 halo
     __shared__ double ts[kFSN];                   // thn over the tile + 2 halo
-    __shared__ double xl[4 * kFAN];               // level A's x over the tile + 1 halo
+    __shared__ double xl[4 * kFAN];               // level A's x over the tile + 1 halo (PRO: first the coarse window)
     const int n = P.n;
     const int tx = (n + kFTW - 1) / kFTW;
     const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -2853,10 +2859,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))
     const int rb = r0 - 2, cb = c0 - 2;
     const int tid = threadIdx.x;
     const int nn = n * n;
+    // PRO: the coarse correction over [r0 / 2 - 2, r0 / 2 + 6) x [c0 / 2 - 2, c0 / 2 + 34) of 4 fields (k_gal1's window)
+    constexpr int CW = kFTW / 2 + 4, CH = kFTH / 2 + 4, CN = CW * CH;
+    static_assert(!PRO || 4 * CN <= 4 * kFAN, "the coarse window fits the level-A buffer");
+    const int nc = n >> 1, ncc = nc * nc, cr0 = r0 >> 1, cc0 = c0 >> 1;
     // stage thn (and x_in) over rows r0-2 .. r0+9, columns c0-2 .. c0+65: every load issued before the first LDS store
     {
-        constexpr int IT = (kFSN + 255) / 256, NF = INIT ? 1 : 5;
-        double v[IT][NF];
+        constexpr int IT = (kFSN + 255) / 256, NF = INIT ? 1 : 5, IC = PRO ? (4 * CN + 255) / 256 : 1;
+        double v[IT][NF], vc[IC];
+        if constexpr (PRO) {
+            auto wrapc = [&](int q) { return q < 0 ? q + nc : (q >= nc ? q - nc : q); };
+#pragma unroll
+            for (int it = 0; it < IC; ++it) {
+                const int i = tid + it * 256;
+                if (i < 4 * CN) {
+                    const int f = i / CN, j = i - f * CN, r = j / CW, c = j - r * CW;
+                    vc[it] = a.xc[f * ncc + wrapc(cr0 - 2 + r) * nc + wrapc(cc0 - 2 + c)];
+                }
+            }
+        }
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
             const int i = tid + it * 256;
@@ -2870,14 +2891,31 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))
                 }
             }
         }
+        if constexpr (PRO) {
+#pragma unroll
+            for (int it = 0; it < IC; ++it)
+                if (tid + it * 256 < 4 * CN) xl[tid + it * 256] = vc[it];
+            __syncthreads();
+        }
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
             const int i = tid + it * 256;
             if (i < kFSN) {
                 ts[i] = v[it][0];
                 if constexpr (!INIT) {
+                    if constexpr (PRO) {   // x_in + P_0 xc: k_mg_transfer_spmv's prolongation and EpiAdd's sum
+                        const int sr = i / kFSW, sc = i - sr * kFSW;
+                        const int gr = P.wrap(rb + sr), gc = P.wrap(cb + sc);
 #pragma unroll
-                    for (int f = 0; f < 4; ++f) xs[f * kFSN + i] = v[it][1 + f];
+                        for (int f = 0; f < 4; ++f) {
+                            const double pc = (f & 1) ? g1_p<MPBP_MG_NODE, MPBP_MG_CELL>(xl + f * CN, gr, gc, nc, cr0 - 2, cc0 - 2)
+                                                      : g1_p<MPBP_MG_CELL, MPBP_MG_NODE>(xl + f * CN, gr, gc, nc, cr0 - 2, cc0 - 2);
+                            xs[f * kFSN + i] = pc + v[it][1 + f];
+                        }
+                    } else {
+#pragma unroll
+                        for (int f = 0; f < 4; ++f) xs[f * kFSN + i] = v[it][1 + f];
+                    }
                 }
             }
         }
@@ -2971,6 +3009,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))
 template <bool INIT, bool SUB, bool SD, class BS>
 int launch_ftile_t(const FStencilFast& P, const FTile& a, hipStream_t st, const BS& bs) {
     const int64_t tiles = (int64_t)((P.n + kFTW - 1) / kFTW) * ((P.n + kFTH - 1) / kFTH);
+    if constexpr (!INIT && !BS::on) {
+        if (a.xc) {
+            k_ftile<INIT, SUB, SD, BS, true><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
+            MPBP_HIP(hipGetLastError());
+            return MPBP_OK;
+        }
+    }
     k_ftile<INIT, SUB, SD, BS><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
@@ -2983,7 +3028,7 @@ int launch_ftile(const FStencilDev& Pd, const FTile& a, hipStream_t st, const BS
     const FStencilFast P{Pd};
     if (P.h != 0 || P.which != 0 || !ftile_ok(P.n)) return set_error(MPBP_ERR_ARG, "ftile: one GPU, whole grid, n >= 76");
     if (!a.x_out || (!INIT && (!a.x_in || (!a.d_in && !a.dzero) || a.x_in == a.x_out)) || (!BS::on && !a.b) ||
-        (a.d_out && (a.d_out == a.d_in || a.d_out == a.x_in)))
+        (a.d_out && (a.d_out == a.d_in || a.d_out == a.x_in)) || (a.xc && (INIT || BS::on || (P.n & 1))))
         return set_error(MPBP_ERR_ARG, "ftile: bad vectors");
     const bool sub = a.sub != nullptr, sd = a.d_out != nullptr;
     return sub ? (sd ? launch_ftile_t<INIT, true, true>(P, a, st, bs) : launch_ftile_t<INIT, true, false>(P, a, st, bs))
@@ -3921,6 +3966,166 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1(FStencilFast P, MgF
             for (int b = 0; b < mx; ++b) acc += (yw[a] * xw[b]) * tr1[slot(xi[b], fc0 - 1, n)];
         }
         epi(row, acc, pe);
+    }
+}
+
+// ---- multigrid level 0 of a tolerance-mode F hierarchy: pre-smoothing, residual and restriction in one launch ----
+// k_fpre (the V-cycle's descent at level 0, V(2, .) from x = 0): on k_fsolve's 64 x 8 tiles with H = 3 levels -- x0 =
+// c2_0 b / diag over the tile + 3, the Chebyshev sweep x1 over the tile + 2 (written out on the tile: the iterate the
+// post-smoothing continues from), the residual r = b - F x1 over the tile + 1 (in LDS), then R_0 r on the tile's 32 x 4
+// coarse cells into the coarse right-hand side.  Each value is built by the operations of the launches it replaces
+// (k_ftile<INIT>'s x0 and sweep, the residual sweep's tolerance-mode rows and EpiResid, k_mg_transfer_spmv's restriction
+// lists and product order): bit-identical to them.  HBM: b, thn and faces in, x1 and the coarse rhs out -- the residual
+// is never written.
+template <int KY, int KX, int W>
+__device__ inline double g1_rw(const double* tf, int cr, int cc, int n, int rb, int cb) {
+    constexpr int MY = KY == MPBP_MG_CELL ? 4 : 3, MX = KX == MPBP_MG_CELL ? 4 : 3;
+    int yi[4], xi[4];
+    double yw[4], xw[4];
+    mg_r1d_fast(KY, n, cr, yi, yw);
+    mg_r1d_fast(KX, n, cc, xi, xw);
+    double acc = 0.0;
+#pragma unroll
+    for (int a = 0; a < MY; ++a) {
+        const double* tr1 = tf + g1_slot(yi[a], rb, n) * W;
+#pragma unroll
+        for (int b = 0; b < MX; ++b) acc += (yw[a] * xw[b]) * tr1[g1_slot(xi[b], cb, n)];
+    }
+    return acc;
+}
+struct FPre {
+    const double* b;   // the level's right-hand side
+    double* x_out;     // x1 (the pre-smoothed iterate)
+    double* bc;        // the coarse right-hand side R_0 (b - F x1)
+    double c2_0, c1, c2;
+};
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) MPBP_LDS_READS
+k_fpre(FStencilFast P, FPre a) {
+    constexpr int H = 3;
+    using T = FsTile<H>;
+    // slots: the two tile cells (0, 1), rings 1 .. 3 (2 .. 4); ring 1 lives through the residual level, ring 2
+    // through the sweep, ring 3 is x0 only -- state (d, 1 / diag) for slots 0 .. 3
+    constexpr int NT = 2, NSL = H + 2, NS = H + 1;
+    __shared__ double ts[T::TN];
+    __shared__ double xa[4 * T::N], xb[4 * T::N];
+    const int n = P.n, nn = n * n, nc = n >> 1, ncc = nc * nc;
+    const int tx = (n + kFTW - 1) / kFTW;
+    const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int r0 = (bk / tx) * kFTH, c0 = (bk % tx) * kFTW;
+    const int rbt = r0 - H - 1, cbt = c0 - H - 1, rb = r0 - H, cb = c0 - H;
+    const int tid = threadIdx.x;
+    {
+        constexpr int IT = (T::TN + 255) / 256;
+        double v[IT];
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256;
+            if (i < T::TN) {
+                const int sr = i / T::TW, sc = i - sr * T::TW;
+                v[it] = P.cell[P.wrap(rbt + sr) * n + P.wrap(cbt + sc)];
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256;
+            if (i < T::TN) ts[i] = v[it];
+        }
+    }
+    const int lr = tid >> 6, lc = tid & 63;
+    int cr[NSL], cc[NSL], rr[NSL];
+    bool own[NSL];
+#pragma unroll
+    for (int m = 0; m < NT; ++m) {
+        cr[m] = r0 + lr + 4 * m; cc[m] = c0 + lc; own[m] = true; rr[m] = 0;
+    }
+#pragma unroll
+    for (int r = 1; r <= H; ++r) {
+        own[1 + r] = tid < 140 + 8 * r;
+        rr[1 + r] = r;
+        fs_ring_cell(r, own[1 + r] ? tid : 0, r0, c0, cr[1 + r], cc[1 + r]);
+    }
+    double fl[NSL][2], bl[NSL][4];
+#pragma unroll
+    for (int sl = 0; sl < NSL; ++sl) {
+        if (!own[sl]) continue;
+        const int gr = P.wrap(cr[sl]), gc = P.wrap(cc[sl]);
+        const int32_t k = gr * n + gc;
+        fl[sl][0] = P.uface[k];
+        fl[sl][1] = P.vface[k];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) bl[sl][f] = a.b[(f * n + gr) * n + gc];
+    }
+    __syncthreads();
+    const TTileT<T::TW> tt{ts, rbt, cbt};
+    double d[NS][4], rd[NS][4];
+    // level 0: x0 = d0 = c2_0 b / diag over the tile + 3
+#pragma unroll
+    for (int sl = 0; sl < NSL; ++sl) {
+        if (!own[sl]) continue;
+        const int vr = cr[sl], vc = cc[sl];
+        const FStencilDev::Stage sg{{fl[sl][0], fl[sl][1]}};
+        double r4[4];
+        P.rdiag4(vr, vc, tt, sg, r4);
+        const int si = (vr - rb) * T::RW + (vc - cb);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            const double x0 = a.c2_0 * bl[sl][f] * r4[f];
+            xa[f * T::N + si] = x0;
+            if (sl < NS) {
+                d[sl][f] = x0;
+                rd[sl][f] = r4[f];
+            }
+        }
+    }
+    __syncthreads();
+    // level 1: the sweep over the tile + 2 (x1 into xb; the tile's cells also to memory)
+    {
+        const XTileT<T::RW, T::RH> xt{xa, rb, cb};
+#pragma unroll
+        for (int sl = 0; sl < NS; ++sl) {
+            if (sl >= NT && (!own[sl] || rr[sl] > 2)) continue;
+            const int vr = cr[sl], vc = cc[sl];
+            double acc[4], rdx[4];
+            P.template rows4<false>(vr, vc, tt, xt, FStencilDev::Cell{{fl[sl][0], fl[sl][1]}}, acc, rdx);
+            const int si = (vr - rb) * T::RW + (vc - cb);
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                const double z = (bl[sl][f] - acc[f]) * rd[sl][f];
+                const double dn = a.c1 * d[sl][f] + a.c2 * z;
+                const double x = xa[f * T::N + si] + dn;
+                xb[f * T::N + si] = x;
+                if (sl < NT && vr < n && vc < n) a.x_out[f * nn + vr * n + vc] = x;
+            }
+        }
+    }
+    __syncthreads();
+    // level 2: r = b - F x1 over the tile + 1 (into xa)
+    {
+        const XTileT<T::RW, T::RH> xt{xb, rb, cb};
+#pragma unroll
+        for (int sl = 0; sl < NS; ++sl) {
+            if (sl >= NT && (!own[sl] || rr[sl] > 1)) continue;
+            const int vr = cr[sl], vc = cc[sl];
+            double acc[4], rdx[4];
+            P.template rows4<false>(vr, vc, tt, xt, FStencilDev::Cell{{fl[sl][0], fl[sl][1]}}, acc, rdx);
+            const int si = (vr - rb) * T::RW + (vc - cb);
+#pragma unroll
+            for (int f = 0; f < 4; ++f) xa[f * T::N + si] = bl[sl][f] - acc[f];
+        }
+    }
+    __syncthreads();
+    // R_0 r on the tile's coarse rows (4 fields x 128 cells; the F hierarchy's MAC kinds): lane t, cell t & 127 of
+    // fields (t >> 7) and (t >> 7) + 2
+    const int cell = tid & (kG1W * kG1H - 1), fp = tid >> 7;
+    const int crr = (r0 >> 1) + cell / kG1W, ccc = (c0 >> 1) + cell % kG1W;
+    if (crr < nc && ccc < nc) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int f = fp + 2 * h;
+            const double acc = fp ? g1_rw<MPBP_MG_NODE, MPBP_MG_CELL, T::RW>(xa + f * T::N, crr, ccc, n, rb, cb)
+                                  : g1_rw<MPBP_MG_CELL, MPBP_MG_NODE, T::RW>(xa + f * T::N, crr, ccc, n, rb, cb);
+            a.bc[f * ncc + crr * nc + ccc] = acc;
+        }
     }
 }
 
@@ -6206,6 +6411,39 @@ bool mg_gal_ok(const mpbp_mg* m, const MgFine& f) {
            m->nlevels > 2 && use_mf_transfer(m, 0) && f.r && f.d;
 }
 
+// Level 0's descent as ONE k_fpre launch (pre-smoothing V(2, .) from x = 0, residual, restriction): tolerance-mode
+// matrix-free F on one GPU, the whole grid, the F hierarchy's MAC transfers matrix-free, a grid the tile's staging
+// wraps onto at most once (kernel option mg_fuse_l0).
+bool fpre_ok(const mpbp_mg* m, const MgFine& f) {
+    const OpRef& o = f.op.in;
+    if (!KO().mg_fuse_l0 || !o.stencil || o.sop != SOP_F || o.which != 0 || !f.op.bd.empty || f.halo || o.stencil->halo)
+        return false;
+    const mpbp_schur_plan* p = o.stencil;
+    if (p->f_numerics != MPBP_NUMERICS_FAST || !p->f_stencil || m->part_levels > 0 || !use_mf_transfer(m, 0) ||
+        m->tr_nfields != 4)
+        return false;
+    for (int fl = 0; fl < 4; ++fl)
+        if (m->tr_ky[fl] != ((fl & 1) ? MPBP_MG_NODE : MPBP_MG_CELL) || m->tr_kx[fl] != ((fl & 1) ? MPBP_MG_CELL : MPBP_MG_NODE))
+            return false;
+    const int n = p->f_prm.n;
+    return (n & 1) == 0 && m->tr_n0 == n && fsolve_ok_n<3>(n);
+}
+int launch_fpre(const mpbp_schur_plan* p, const double* b, double lmin, double lmax, double* x_out, double* bc,
+                hipStream_t st) {
+    FStencilDev Pd;
+    const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &Pd);
+    if (rc) return rc;
+    const FStencilFast P{Pd};
+    if (P.h != 0 || P.which != 0 || !fsolve_ok_n<3>(P.n) || (P.n & 1) || !b || !x_out || !bc)
+        return set_error(MPBP_ERR_ARG, "fpre: one GPU, whole even grid n >= 72");
+    double c1[2] = {}, c2[2] = {};
+    cheb_coeffs(lmin, lmax, 2, c1, c2);
+    const int64_t tiles = (int64_t)((P.n + kFTW - 1) / kFTW) * ((P.n + kFTH - 1) / kFTH);
+    k_fpre<<<(unsigned)tiles, 256, 0, st>>>(P, FPre{b, x_out, bc, c2[0], c1[1], c2[1]});
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
 // One V-cycle on level l for A_l x = b.  Level 0 uses `fine` (operator and buffers); coarser levels their
 // mpbp_mg_level.  *res receives the result's buffer (dst when given).  Row partition (m->part_levels > 0): levels
 // l < part_levels hold owned rows (vectors read by an operator carry ghost rows, refreshed by mg_exchange); the
@@ -6231,19 +6469,29 @@ int mg_vcycle(const mpbp_mg* m, int l, const MgFine& fine, const double* b, bool
     double* d = top ? fine.d : L.d;
     double* cur = xin;
     auto xch = [&](double* v) { mg_exchange(m, l, fine, v, st); };
-    int rc = mg_smooth(o, L.nrows, diag, L.lmin, L.lmax, L.pre, zero, b, &cur, alt, d, nullptr, nullptr, st, xch);
-    if (rc) return rc;
-    alt = cur == bx ? bt : bx;
-    // r = b - A x ; b_c = R r
-    xch(cur);
-    rc = pair_spmv(o, MPBP_SPMV_RESID, cur, b, r, st);
-    if (rc) return rc;
     const mpbp_mg_level& C = m->levels[l + 1];
     const bool gather = m->part_levels > 0 && l + 1 == m->part_levels;
-    if (l < m->part_levels) xch(r);
-    rc = use_mf_transfer(m, l) ? mg_transfer_mf(m, l, MPBP_MG_R, L.R.nrows, r, EpiStore{gather ? C.r : C.b}, st)
-                               : mg_transfer(L.R, L.R_blocks, L.R_sell, MPBP_SPMV_STORE, r, nullptr, gather ? C.r : C.b, st);
-    if (rc) return rc;
+    int rc = MPBP_OK;
+    if (top && zero && L.pre == 2 && fpre_ok(m, fine)) {
+        // x0, sweep 1, r = b - A x and b_c = R r in one launch; x1 where the smoothing would leave it (the free buffer)
+        cur = alt;
+        rc = launch_fpre(o.in.stencil, b, L.lmin, L.lmax, cur, C.b, st);
+        if (rc) return rc;
+        alt = cur == bx ? bt : bx;
+    } else {
+        rc = mg_smooth(o, L.nrows, diag, L.lmin, L.lmax, L.pre, zero, b, &cur, alt, d, nullptr, nullptr, st, xch);
+        if (rc) return rc;
+        alt = cur == bx ? bt : bx;
+        // r = b - A x ; b_c = R r
+        xch(cur);
+        rc = pair_spmv(o, MPBP_SPMV_RESID, cur, b, r, st);
+        if (rc) return rc;
+        if (l < m->part_levels) xch(r);
+        rc = use_mf_transfer(m, l) ? mg_transfer_mf(m, l, MPBP_MG_R, L.R.nrows, r, EpiStore{gather ? C.r : C.b}, st)
+                                   : mg_transfer(L.R, L.R_blocks, L.R_sell, MPBP_SPMV_STORE, r, nullptr, gather ? C.r : C.b,
+                                                 st);
+        if (rc) return rc;
+    }
     if (gather) {
         if (!m->gather) return set_error(MPBP_ERR_ARG, "mg: a partitioned hierarchy needs its gather callback");
         m->gather(m->halo_ctx, m->gather_kind, C.r, C.b, (void*)st);
@@ -6262,6 +6510,24 @@ int mg_vcycle(const mpbp_mg* m, int l, const MgFine& fine, const double* b, bool
     if (rc) return rc;
     // x += P x_c (row-wise in place), then post-smoothing from x
     mg_exchange(m, l + 1, fine, xc, st);
+    if (top && L.post == 2 && fpre_ok(m, fine) && f_pair_ok(o.in.stencil) && KO().f_tile && ftile_ok(o.in.stencil->f_prm.n)) {
+        // the prolongation folded into the post-smoothing pair's staging (k_ftile<PRO>: x + P_0 x_c per staged cell,
+        // the prolongation launch's operations), the restart's direction read as +0.0 -- mg_smooth's tile pair
+        double c1[2] = {}, c2[2] = {};
+        cheb_coeffs(L.lmin, L.lmax, 2, c1, c2);
+        double* out = dst ? dst : alt;
+        const mpbp_schur_plan* p = o.in.stencil;
+        FStencilDev P;
+        rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &P);
+        if (rc) return rc;
+        FTile a{cur, d, b, sub, out, nullptr, c1[0], c2[0], c1[1], c2[1]};
+        a.dzero = 1;
+        a.xc = xc;
+        rc = launch_ftile<false>(P, a, st);
+        if (rc) return rc;
+        *res = out;
+        return MPBP_OK;
+    }
     rc = use_mf_transfer(m, l) ? mg_transfer_mf(m, l, MPBP_MG_P, L.P.nrows, xc, EpiAdd{cur, cur}, st)
                                : mg_transfer(L.P, L.P_blocks, L.P_sell, MPBP_SPMV_ADD, xc, cur, cur, st);
     if (rc) return rc;
