@@ -3838,8 +3838,10 @@ __device__ inline double g1_r(const double* tf, int cr, int cc, int n, int rb, i
     return acc;
 }
 // MAC: the F hierarchy's kinds (u: rows cell-, columns node-centred; v: the reverse) at compile time
-template <class Epi, bool MAC = false>
-__global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1(FStencilFast P, MgFields tr, const double* __restrict__ x, Epi epi) {
+// XS: the coarse x as staged -- XPlain (x itself) or XInit (x0 = c2_0 (b / diag): a pre-smoothing's first sweep with the
+// init pass folded in, as the grouped small levels do; the epilogue then EpiChebFirstGrp)
+template <class Epi, bool MAC = false, class XS = XPlain>
+__global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1(FStencilFast P, MgFields tr, XS xin, Epi epi) {
     constexpr int CN = kG1CW * kG1CH, PN = kG1PW * kG1PH, FN = kG1FW * kG1FH;
     __shared__ double xs[4 * CN];
     __shared__ double ts[PN];
@@ -3856,13 +3858,14 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1(FStencilFast P, MgF
     auto slot = [](int i, int base, int m) { int l = i - base; return l < 0 ? l + m : (l >= m ? l - m : l); };
     {   // stage the coarse x (4 fields) and thn, every load before the first LDS store
         constexpr int IX = (4 * CN + 255) / 256, IT = (PN + 255) / 256;
-        double vx[IX], vt[IT];
+        typename XS::Raw vx[IX];
+        double vt[IT];
 #pragma unroll
         for (int it = 0; it < IX; ++it) {
             const int i = tid + it * 256;
             if (i < 4 * CN) {
                 const int f = i / CN, j = i - f * CN, r = j / kG1CW, c = j - r * kG1CW;
-                vx[it] = x[f * ncc + wrapc(cr0 - 2 + r) * nc + wrapc(cc0 - 2 + c)];
+                vx[it] = xin.load(f * ncc + wrapc(cr0 - 2 + r) * nc + wrapc(cc0 - 2 + c));
             }
         }
 #pragma unroll
@@ -3875,7 +3878,7 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1(FStencilFast P, MgF
         }
 #pragma unroll
         for (int it = 0; it < IX; ++it)
-            if (tid + it * 256 < 4 * CN) xs[tid + it * 256] = vx[it];
+            if (tid + it * 256 < 4 * CN) xs[tid + it * 256] = xin.value(vx[it]);
 #pragma unroll
         for (int it = 0; it < IT; ++it)
             if (tid + it * 256 < PN) ts[tid + it * 256] = vt[it];
@@ -4134,8 +4137,8 @@ k_fpre(FStencilFast P, FPre a) {
 // matrix-free level-0 sweep's operations), the transfers' by k_mg_transfer_spmv's: bit-identical to the three launches.
 constexpr int kG1PH2 = 8;                                     // coarse tile rows (pressure)
 constexpr int kGPFH = 2 * kG1PH2 + 2, kGPPH = kGPFH + 2;       // fine t1 / t0 rows
-template <class Epi>
-__global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, const double* __restrict__ x, Epi epi) {
+template <class Epi, class XS = XPlain>
+__global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, XS xin, Epi epi) {
     constexpr int CH = kG1PH2 + 4, CN = kG1CW * CH, PN = kG1PW * kGPPH, FN = kG1FW * kGPFH;
     __shared__ double xs[CN];
     __shared__ double ts[PN];
@@ -4150,13 +4153,14 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, c
     auto wrapc = [&](int a) { return a < 0 ? a + nc : (a >= nc ? a - nc : a); };
     {
         constexpr int IX = (CN + 255) / 256, IT = (PN + 255) / 256;
-        double vx[IX], vt[IT];
+        typename XS::Raw vx[IX];
+        double vt[IT];
 #pragma unroll
         for (int it = 0; it < IX; ++it) {
             const int i = tid + it * 256;
             if (i < CN) {
                 const int r = i / kG1CW, c = i - r * kG1CW;
-                vx[it] = x[wrapc(cr0 - 2 + r) * nc + wrapc(cc0 - 2 + c)];
+                vx[it] = xin.load(wrapc(cr0 - 2 + r) * nc + wrapc(cc0 - 2 + c));
             }
         }
 #pragma unroll
@@ -4169,7 +4173,7 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, c
         }
 #pragma unroll
         for (int it = 0; it < IX; ++it)
-            if (tid + it * 256 < CN) xs[tid + it * 256] = vx[it];
+            if (tid + it * 256 < CN) xs[tid + it * 256] = xin.value(vx[it]);
 #pragma unroll
         for (int it = 0; it < IT; ++it)
             if (tid + it * 256 < PN) ts[tid + it * 256] = vt[it];
@@ -5967,25 +5971,29 @@ int gal_r(const MgGal& g, Epi epi, hipStream_t st) {
 }
 
 // The whole level-1 product as one k_gal1 launch (KO().mg_galerkin_mf == 2): four fields, a grid the staged windows wrap once.
-template <class Epi>
-int gal_fused(const MgGal& g, const double* x, Epi epi, hipStream_t st, bool* done) {
+// gal_fused_ok: whether gal_fused takes the one-launch form for this level (else the caller runs the three launches)
+bool gal_fused_ok(const MgGal& g) {
+    const mpbp_schur_plan* p = g.fine.stencil;
+    if (KO().mg_galerkin_mf != 2 || p->f_prm.n < 2 * kG1CW || (p->f_prm.n & 1)) return false;
+    if (g.fine.sop == SOP_GTG) return g.m->tr_nfields == 1 && g.m->tr_ky[0] == MPBP_MG_CELL && g.m->tr_kx[0] == MPBP_MG_CELL;
+    return g.m->tr_nfields == 4;
+}
+template <class Epi, class XS = XPlain>
+int gal_fused(const MgGal& g, XS x, Epi epi, hipStream_t st, bool* done) {
     *done = false;
     const mpbp_schur_plan* p = g.fine.stencil;
+    if (!gal_fused_ok(g)) return MPBP_OK;
     if (g.fine.sop == SOP_GTG) {   // the pressure hierarchy: one field, cell-centred (mg.FIELDS_PRESSURE)
-        if (KO().mg_galerkin_mf != 2 || g.m->tr_nfields != 1 || g.m->tr_ky[0] != MPBP_MG_CELL || g.m->tr_kx[0] != MPBP_MG_CELL ||
-            p->f_prm.n < 2 * kG1CW || (p->f_prm.n & 1))
-            return MPBP_OK;
         PGDev Pg;
         const int rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &Pg);
         if (rc) return rc;
         const int nc = p->f_prm.n / 2;
         const int64_t tiles = (int64_t)((nc + kG1W - 1) / kG1W) * ((nc + kG1PH2 - 1) / kG1PH2);
-        k_gal1p<Epi><<<(unsigned)tiles, 256, 0, st>>>(GtGStencilDev{Pg}, x, epi);
+        k_gal1p<Epi, XS><<<(unsigned)tiles, 256, 0, st>>>(GtGStencilDev{Pg}, x, epi);
         MPBP_HIP(hipGetLastError());
         *done = true;
         return MPBP_OK;
     }
-    if (KO().mg_galerkin_mf != 2 || g.m->tr_nfields != 4 || p->f_prm.n < 2 * kG1CW || (p->f_prm.n & 1)) return MPBP_OK;
     FStencilDev Pd;
     const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &Pd);
     if (rc) return rc;
@@ -6000,8 +6008,8 @@ int gal_fused(const MgGal& g, const double* x, Epi epi, hipStream_t st, bool* do
     bool mac = true;   // the F hierarchy's MAC kinds (mg.FIELDS_VELOCITY)
     for (int f = 0; f < 4; ++f)
         mac = mac && F.ky[f] == ((f & 1) ? MPBP_MG_NODE : MPBP_MG_CELL) && F.kx[f] == ((f & 1) ? MPBP_MG_CELL : MPBP_MG_NODE);
-    if (mac) k_gal1<Epi, true><<<(unsigned)tiles, 256, 0, st>>>(FStencilFast{Pd}, F, x, epi);
-    else k_gal1<Epi, false><<<(unsigned)tiles, 256, 0, st>>>(FStencilFast{Pd}, F, x, epi);
+    if (mac) k_gal1<Epi, true, XS><<<(unsigned)tiles, 256, 0, st>>>(FStencilFast{Pd}, F, x, epi);
+    else k_gal1<Epi, false, XS><<<(unsigned)tiles, 256, 0, st>>>(FStencilFast{Pd}, F, x, epi);
     MPBP_HIP(hipGetLastError());
     *done = true;
     return MPBP_OK;
@@ -6013,9 +6021,9 @@ int op_spmv(const OpRef& o, int32_t mode, const double* x, const double* z, doub
         bool done = false;
         int rf = MPBP_OK;
         switch (mode) {
-        case MPBP_SPMV_STORE: rf = gal_fused(*o.gal, x, EpiStore{y}, st, &done); break;
-        case MPBP_SPMV_ADD: rf = gal_fused(*o.gal, x, EpiAdd{z, y}, st, &done); break;
-        case MPBP_SPMV_RESID: rf = gal_fused(*o.gal, x, EpiResid{z, y}, st, &done); break;
+        case MPBP_SPMV_STORE: rf = gal_fused(*o.gal, XPlain{x}, EpiStore{y}, st, &done); break;
+        case MPBP_SPMV_ADD: rf = gal_fused(*o.gal, XPlain{x}, EpiAdd{z, y}, st, &done); break;
+        case MPBP_SPMV_RESID: rf = gal_fused(*o.gal, XPlain{x}, EpiResid{z, y}, st, &done); break;
         default: break;
         }
         if (rf || done) return rf;
@@ -6064,7 +6072,7 @@ int op_cheb(const OpRef& o, const double* xin, const double* b, const double* dg
         // (dzero: a restart's first sweep reads d as +0.0 -- no memset of the direction)
         auto run = [&](const auto& epi) {
             bool done = false;
-            const int rf = gal_fused(*o.gal, xin, epi, st, &done);
+            const int rf = gal_fused(*o.gal, XPlain{xin}, epi, st, &done);
             if (rf || done) return rf;
             const int rc = gal_fp(*o.gal, xin, st);
             return rc ? rc : gal_r(*o.gal, epi, st);
@@ -6354,6 +6362,21 @@ int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, 
         const int rc = grp_cheb_first(o.csr, b, diag, c2[0], c1[1], c2[1], d, K == 2 ? sub : nullptr, out1, st,
                                       K == 2 ? 0 : 1);
         if (rc) return rc;
+        other = x;
+        x = out1;
+        s = 2;
+    } else if (zero && K >= 2 && op.bd.empty && o.gal && KO().mg_fuse_l0 && gal_fused_ok(*o.gal)) {
+        // matrix-free level 1 (k_gal1 / k_gal1p): the first sweep stages x0 = c2[0] b / diag itself (XInit) and its
+        // epilogue takes the row's own x0 as iterate and direction -- no init launch, k_cheb_init's bits
+        double* out1 = K == 2 ? (dst ? dst : other) : other;
+        EpiChebFirstGrp e;
+        static_cast<EpiChebFirst&>(e) = EpiChebFirst{b, d, c1[1], c2[1], K == 2 ? sub : nullptr, out1, K == 2 ? 0 : 1};
+        e.diag = diag;
+        e.c2_0 = c2[0];
+        bool done = false;
+        const int rc = gal_fused(*o.gal, XInit{b, diag, c2[0]}, e, st, &done);
+        if (rc) return rc;
+        if (!done) return set_error(MPBP_ERR_ARG, "mg: the fused level-1 first sweep did not launch");
         other = x;
         x = out1;
         s = 2;
@@ -7066,9 +7089,9 @@ extern "C" int mpbp_mg_level1_apply(const mpbp_schur_plan* p, int32_t kind, int3
     bool done = false;
     int rc = MPBP_OK;
     switch (mode) {
-    case MPBP_SPMV_STORE: rc = gal_fused(g, x, EpiStore{y}, st, &done); break;
-    case MPBP_SPMV_ADD: rc = gal_fused(g, x, EpiAdd{z, y}, st, &done); break;
-    case MPBP_SPMV_RESID: rc = gal_fused(g, x, EpiResid{z, y}, st, &done); break;
+    case MPBP_SPMV_STORE: rc = gal_fused(g, XPlain{x}, EpiStore{y}, st, &done); break;
+    case MPBP_SPMV_ADD: rc = gal_fused(g, XPlain{x}, EpiAdd{z, y}, st, &done); break;
+    case MPBP_SPMV_RESID: rc = gal_fused(g, XPlain{x}, EpiResid{z, y}, st, &done); break;
     default: return set_error(MPBP_ERR_ARG, "mg_level1_apply: unknown mode %d", mode);
     }
     if (rc) return rc;
