@@ -3788,6 +3788,161 @@ __global__ void __launch_bounds__(TPB) MPBP_LDS_READS k_gtg_solve(GtGStencilDev 
     }
 }
 
+// ---- multigrid level 0 of the pressure hierarchy (matrix-free Gt_G): descent and ascent in one launch each ----
+// k_gpre: x0 = c2_0 (b / diag) over the tile + 3, the Chebyshev sweep x1 over the tile + 2 (written on the tile), the
+// residual r = b - Gt_G x1 over the tile + 1 (in LDS) and R_0 r on the tile's 32 x 4 coarse cells (cell-centred both
+// ways).  k_gpost: x = x_in + P_0 x_c staged over the tile + 2, two Chebyshev sweeps from d = +0.0 (the restart of the
+// post-smoothing), the last writing the tile (sub - x when sub is set).  k_gtg_solve's 512-lane layout (one tile cell
+// and at most one ring cell per lane, the cell's five entries built once from thn), its rows and updates, the
+// transfers' k_mg_transfer_spmv lists and orders, EpiResid's and EpiAdd's sums: bit-identical to the launches they
+// replace (the first / plain / zero-direction sweeps, the residual, the restriction, the prolongation).
+template <int KY, int KX, int W>
+__device__ inline double g1_rw(const double* tf, int cr, int cc, int n, int rb, int cb);
+template <bool PRE, bool SUB>
+__global__ void __launch_bounds__(512) MPBP_LDS_READS
+k_gtg_level0(GtGStencilDev P, const double* __restrict__ b, const double* __restrict__ diag, const double* __restrict__ xin,
+             const double* __restrict__ xc, const double* __restrict__ sub, ChebK ck, double* __restrict__ x_out,
+             double* __restrict__ bc) {
+    constexpr int H = PRE ? 3 : 2;   // staged halo: the tile + H
+    using G = GtgTile<H>;
+    constexpr int CW = kGTW / 2 + 4, CH = kGTH / 2 + 4, CN = CW * CH;   // k_gpost's coarse window (k_gal1's geometry)
+    __shared__ double ts[G::N], bs[G::N], xa[G::N], xb[G::N];
+    __shared__ double cs[PRE ? 1 : CN];
+    const int n = P.n, nc = n >> 1;
+    const int tx = (n + kGTW - 1) / kGTW;
+    const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int r0 = (bk / tx) * kGTH, c0 = (bk % tx) * kGTW;
+    const int rb = r0 - H, cb = c0 - H;
+    const int cr0 = r0 >> 1, cc0 = c0 >> 1;
+    const int tid = threadIdx.x;
+    auto wrapc = [&](int q) { return q < 0 ? q + nc : (q >= nc ? q - nc : q); };
+    {
+        constexpr int IT = (G::N + 511) / 512, IC = PRE ? 1 : (CN + 511) / 512;
+        double bv[IT], tv[IT], wv[IT], cv[IC];
+        if constexpr (!PRE) {
+#pragma unroll
+            for (int it = 0; it < IC; ++it) {
+                const int i = tid + it * 512;
+                if (i < CN) {
+                    const int r = i / CW, c = i - r * CW;
+                    cv[it] = xc[wrapc(cr0 - 2 + r) * nc + wrapc(cc0 - 2 + c)];
+                }
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 512;
+            if (i < G::N) {
+                const int rr = i / G::RW, cc = i - rr * G::RW;
+                const int32_t k = P.wrap(rb + rr) * n + P.wrap(cb + cc);
+                bv[it] = b[k];
+                tv[it] = P.cell[k];
+                wv[it] = PRE ? diag[k] : xin[k];
+            }
+        }
+        if constexpr (!PRE) {
+#pragma unroll
+            for (int it = 0; it < IC; ++it)
+                if (tid + it * 512 < CN) cs[tid + it * 512] = cv[it];
+            __syncthreads();
+        }
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 512;
+            if (i < G::N) {
+                ts[i] = tv[it];
+                bs[i] = bv[it];
+                if constexpr (PRE) {
+                    xa[i] = ck.c2[0] * (bv[it] / wv[it]);   // x0 (k_cheb_init's expression, XInit's)
+                } else {                                     // x_in + P_0 x_c (the prolongation's sum)
+                    const int rr = i / G::RW, cc = i - rr * G::RW;
+                    const double pc = g1_p<MPBP_MG_CELL, MPBP_MG_CELL>(cs, P.wrap(rb + rr), P.wrap(cb + cc), nc, cr0 - 2,
+                                                                       cc0 - 2);
+                    xa[i] = pc + wv[it];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const TTileT<G::RW> ta{ts, rb, cb};
+    const int lr = tid >> 6, lc = tid & 63;
+    // slot 0: the tile cell; slot 1: ring cell t of rings 1 .. H - 1 numbered ring 1 first
+    int cr[2], cc[2], si[2], rr[2];
+    bool own[2], edge[2];
+    double e[2][5], bo[2], d[2];
+    cr[0] = r0 + lr; cc[0] = c0 + lc; own[0] = true; rr[0] = 0;
+    {
+        int r = 0, j = tid;
+#pragma unroll
+        for (int q = 1; q < H; ++q)
+            if (r == 0) {
+                if (j < 140 + 8 * q) r = q;
+                else j -= 140 + 8 * q;
+            }
+        own[1] = r != 0;
+        rr[1] = r;
+        fs_ring_cell(r ? r : 1, r ? j : 0, r0, c0, cr[1], cc[1]);
+    }
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+        const int vr = cr[sl], vc = cc[sl], gr = P.wrap(vr), gc = P.wrap(vc);
+        si[sl] = (vr - rb) * G::RW + (vc - cb);
+        edge[sl] = __builtin_amdgcn_readfirstlane(__any(own[sl] && (gr == 0 || gr == n - 1 || gc == 0 ||
+                                                                    gc == n - 1))) != 0;
+        if (own[sl]) {
+            P.entries(vr, vc, gr, gc, ta, e[sl]);
+            bo[sl] = bs[si[sl]];
+            d[sl] = PRE ? xa[si[sl]] : 0.0;   // PRE: d0 = x0; post: the restart's +0.0
+        }
+    }
+    double* cur = xa;
+    double* nxt = xb;
+    constexpr int L = PRE ? 2 : 2;   // PRE: the sweep, then the residual; post: two sweeps
+#pragma unroll
+    for (int l = 1; l <= L; ++l) {
+        if (l > 1) __syncthreads();
+        const double c1 = ck.c1[l], c2 = ck.c2[l];
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl) {
+            // PRE: ring rr lives through level 3 - rr (the residual at level 2 covers the tile + 1); post: 2 - rr
+            if (sl == 1 && (!own[1] || rr[1] > (PRE ? 3 : 2) - l)) continue;
+            const int vr = cr[sl], vc = cc[sl];
+            const int i = si[sl];
+            const double p[5] = {e[sl][0] * cur[i - G::RW], e[sl][1] * cur[i - 1], e[sl][2] * cur[i],
+                                 e[sl][3] * cur[i + 1], e[sl][4] * cur[i + G::RW]};
+            const int gr = P.wrap(vr), gc = P.wrap(vc);
+            const Wrap wr{gr == 0, gr == n - 1, gc == 0, gc == n - 1};
+            const double acc = edge[sl] ? add5<true>(0.0, p, wr) : add5<false>(0.0, p, wr);
+            if (PRE && l == 2) {   // the residual (EpiResid)
+                nxt[i] = bo[sl] - acc;
+                continue;
+            }
+            const double z = (bo[sl] - acc) / e[sl][2];
+            const double dn = c1 * d[sl] + c2 * z;
+            const double x = cur[i] + dn;
+            nxt[i] = x;
+            d[sl] = dn;
+            const bool out = PRE ? (l == 1) : (l == L);
+            if (sl == 0 && out && vr < n && vc < n) {
+                const int32_t o = vr * n + vc;
+                x_out[o] = (SUB && !PRE) ? sub[o] - x : x;
+            }
+        }
+        double* t = cur;
+        cur = nxt;
+        nxt = t;
+    }
+    if constexpr (PRE) {   // R_0 r on the tile's coarse cells (cur holds r over the tile + 1)
+        __syncthreads();
+        constexpr int CTW = kGTW / 2, CTH = kGTH / 2;   // the tile's coarse cells
+        if (tid < CTW * CTH) {
+            const int crr = cr0 + tid / CTW, ccc = cc0 + tid % CTW;
+            if (crr < nc && ccc < nc)
+                bc[crr * nc + ccc] = g1_rw<MPBP_MG_CELL, MPBP_MG_CELL, G::RW>(cur, crr, ccc, n, rb, cb);
+        }
+    }
+}
+
 // ---- multigrid level 1 of a tolerance-mode F hierarchy in one launch (k_gal1) ----
 // A_1 x = R_0 (F (P_0 x)) (MgGal) with the two fine-size intermediates kept in LDS: a workgroup owns a 32 x 4 tile of
 // coarse cells (a 64 x 8 fine block), stages the coarse x of its four fields over the tile + 2 and thn over the fine
@@ -6467,6 +6622,51 @@ int launch_fpre(const mpbp_schur_plan* p, const double* b, double lmin, double l
     return MPBP_OK;
 }
 
+// The pressure hierarchy's level 0 the same way (k_gtg_level0): matrix-free Gt_G on one GPU, the whole grid, its
+// cell-centred transfers matrix-free, a grid the staging wraps onto at most once (kernel option mg_fuse_l0).
+bool gpre_ok(const mpbp_mg* m, const MgFine& f) {
+    const OpRef& o = f.op.in;
+    if (!KO().mg_fuse_l0 || !o.stencil || o.sop != SOP_GTG || o.which != 0 || !f.op.bd.empty || f.halo || o.stencil->halo)
+        return false;
+    const mpbp_schur_plan* p = o.stencil;
+    if (!p->pg_stencil || m->part_levels > 0 || !use_mf_transfer(m, 0) || m->tr_nfields != 1 ||
+        m->tr_ky[0] != MPBP_MG_CELL || m->tr_kx[0] != MPBP_MG_CELL)
+        return false;
+    const int n = p->f_prm.n;
+    return (n & 1) == 0 && m->tr_n0 == n && n >= kGTW + kGTH + 6;
+}
+// pre: x0, sweep 1 (x_out), r = b - A x1, b_c = R_0 r; post: x = x_in + P_0 x_c, two sweeps from d = 0 (x_out, or
+// sub - x when sub is set)
+int launch_gtg_level0(bool pre, const mpbp_schur_plan* p, const double* b, const double* diag, const double* xin,
+                      const double* xc, const double* sub, double lmin, double lmax, double* x_out, double* bc,
+                      hipStream_t st) {
+    PGDev Pg;
+    const int rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &Pg);
+    if (rc) return rc;
+    const GtGStencilDev S{Pg};
+    if (S.n < kGTW + kGTH + 6 || (S.n & 1) || !b || !x_out || (pre && (!diag || !bc)) || (!pre && (!xin || !xc)))
+        return set_error(MPBP_ERR_ARG, "gtg_level0: one GPU, whole even grid n >= 78, vectors");
+    double c1[2] = {}, c2[2] = {};
+    cheb_coeffs(lmin, lmax, 2, c1, c2);
+    ChebK ck{};
+    if (pre) {
+        ck.c2[0] = c2[0];
+        ck.c1[1] = c1[1];
+        ck.c2[1] = c2[1];
+    } else {   // the post-smoothing's sweeps s = 0, 1 as levels 1, 2
+        ck.c1[1] = c1[0];
+        ck.c2[1] = c2[0];
+        ck.c1[2] = c1[1];
+        ck.c2[2] = c2[1];
+    }
+    const int64_t tiles = (int64_t)((S.n + kGTW - 1) / kGTW) * ((S.n + kGTH - 1) / kGTH);
+    if (pre) k_gtg_level0<true, false><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, nullptr, nullptr, nullptr, ck, x_out, bc);
+    else if (sub) k_gtg_level0<false, true><<<(unsigned)tiles, 512, 0, st>>>(S, b, nullptr, xin, xc, sub, ck, x_out, nullptr);
+    else k_gtg_level0<false, false><<<(unsigned)tiles, 512, 0, st>>>(S, b, nullptr, xin, xc, nullptr, ck, x_out, nullptr);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
 // One V-cycle on level l for A_l x = b.  Level 0 uses `fine` (operator and buffers); coarser levels their
 // mpbp_mg_level.  *res receives the result's buffer (dst when given).  Row partition (m->part_levels > 0): levels
 // l < part_levels hold owned rows (vectors read by an operator carry ghost rows, refreshed by mg_exchange); the
@@ -6501,6 +6701,11 @@ int mg_vcycle(const mpbp_mg* m, int l, const MgFine& fine, const double* b, bool
         rc = launch_fpre(o.in.stencil, b, L.lmin, L.lmax, cur, C.b, st);
         if (rc) return rc;
         alt = cur == bx ? bt : bx;
+    } else if (top && zero && L.pre == 2 && gpre_ok(m, fine)) {   // the same for the pressure hierarchy
+        cur = alt;
+        rc = launch_gtg_level0(true, o.in.stencil, b, diag, nullptr, nullptr, nullptr, L.lmin, L.lmax, cur, C.b, st);
+        if (rc) return rc;
+        alt = cur == bx ? bt : bx;
     } else {
         rc = mg_smooth(o, L.nrows, diag, L.lmin, L.lmax, L.pre, zero, b, &cur, alt, d, nullptr, nullptr, st, xch);
         if (rc) return rc;
@@ -6533,6 +6738,13 @@ int mg_vcycle(const mpbp_mg* m, int l, const MgFine& fine, const double* b, bool
     if (rc) return rc;
     // x += P x_c (row-wise in place), then post-smoothing from x
     mg_exchange(m, l + 1, fine, xc, st);
+    if (top && L.post == 2 && gpre_ok(m, fine)) {   // x + P_0 x_c and the two post-smoothing sweeps in one launch
+        double* out = dst ? dst : alt;
+        rc = launch_gtg_level0(false, o.in.stencil, b, nullptr, cur, xc, sub, L.lmin, L.lmax, out, nullptr, st);
+        if (rc) return rc;
+        *res = out;
+        return MPBP_OK;
+    }
     if (top && L.post == 2 && fpre_ok(m, fine) && f_pair_ok(o.in.stencil) && KO().f_tile && ftile_ok(o.in.stencil->f_prm.n)) {
         // the prolongation folded into the post-smoothing pair's staging (k_ftile<PRO>: x + P_0 x_c per staged cell,
         // the prolongation launch's operations), the restart's direction read as +0.0 -- mg_smooth's tile pair

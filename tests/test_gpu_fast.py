@@ -422,17 +422,19 @@ def test_mg_level1_apply_abi(n):
 
 @pytest.mark.parametrize("n", [72, 100, 128, 256])
 @pytest.mark.parametrize("cycles", [1, 2])
-def test_fused_level0_descent_equals_launches(n, cycles):
+@pytest.mark.parametrize("numerics", ["fast", "exact"])
+def test_fused_level0_descent_equals_launches(n, cycles, numerics):
     """Kernel option mg_fuse_l0 (default on): the F hierarchy's level-0 descent -- x0 and the pre-smoothing sweep,
     r = b - F x1 and R_0 r -- as ONE k_fpre launch, and the ascent's prolongation x + P_0 x_c inside the post-smoothing
     tile pair, perform the operations of the launches they replace, so the multigrid apply is bit-identical either way
     (one V-cycle and two: the second starts from x != 0 and keeps the descent's launches), eagerly and replayed; on
-    grids not a multiple of the 64 x 8 tile too."""
+    grids not a multiple of the 64 x 8 tile too.  The pressure hierarchy's level 0 likewise (k_gtg_level0: descent
+    and ascent, n >= 78), in both numerics (its Gt_G rows are the same in both; exact mode keeps the F launches)."""
     mp = _mp()
     bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
     _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
-    pc = mp.ApproxSchurPreconditioner(F, D, G, numerics="fast", inner_F=mp.InnerSolver("mg", cycles),
-                                      inner_P=mp.InnerSolver("mg", 1))
+    pc = mp.ApproxSchurPreconditioner(F, D, G, numerics=numerics, inner_F=mp.InnerSolver("mg", cycles),
+                                      inner_P=mp.InnerSolver("mg", cycles))
     assert pc.kernel_opts.mg_fuse_l0 == 1
     v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda",
                     generator=torch.Generator(device="cuda").manual_seed(n + cycles))
