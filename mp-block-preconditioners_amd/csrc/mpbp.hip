@@ -1458,7 +1458,8 @@ __global__ void __launch_bounds__(kBlock) k_svl(Svl V, Csr A, int32_t nrows, XS 
     __syncthreads();
     // interior: one thread per pair of horizontally adjacent cells (reach is even, so W = m - 2 reach is even and a
     // pair starts on an even row id): 16-byte value loads, two rows' products, two ordered sums
-    const int W = V.m - 2 * V.R, W2 = W >> 1;
+    const int W = V.m - 2 * V.R;
+    const int W2 = W >> 1;
     const int32_t per = W2 * W;                        // pairs per field
     const int32_t ni = V.nf * per;
     // the edge rows' latency-bound CSR chains in the first-dispatched workgroups (round-robin over the XCDs), the
@@ -3992,6 +3993,57 @@ __device__ inline double g1_r(const double* tf, int cr, int cc, int n, int rb, i
     }
     return acc;
 }
+// Interior tiles (no staged window wraps and no 1D list takes its periodic special case): P_0's and R_0's rows in
+// window coordinates straight from the fine / coarse parity -- the same entries, weights, order and products as
+// mg_p1d_fast / mg_r1d_fast give there, without their wrap tests, sorted-order selects and runtime weights.  A node
+// kind's one-entry row (even fine index) takes a second entry of weight 0: its products are +-0 added to a sum that
+// started from +0.0 (never -0.0), so the sum's bits are unchanged for finite x.  With t1 in t0's LDS (occupancy 2 -> 3
+// workgroups per CU): k_gal1 45 -> 33 us, multigrid apply 1.610 -> 1.510 ms (A/B on one box, profiles/r05zd_ab.txt).
+template <int K>
+__device__ inline void g1_p1d_in(int r, int& lo, double& w0, double& w1) {
+    const bool odd = r & 1;
+    if constexpr (K == MPBP_MG_CELL) {   // even: c_{i-1} (1/4), c_i (3/4); odd: c_i (3/4), c_{i+1} (1/4)
+        lo = (r >> 1) + (odd ? 1 : 0);
+        w0 = odd ? 0.75 : 0.25;
+        w1 = odd ? 0.25 : 0.75;
+    } else {                             // even: c_i (1); odd: c_i, c_{i+1} (1/2 each)
+        lo = (r >> 1) + 1;
+        w0 = odd ? 0.5 : 1.0;
+        w1 = odd ? 0.5 : 0.0;
+    }
+}
+// P_0's row at window fine (r, c) of the block + 2 (the coarse window starts two coarse cells before the tile)
+template <int KY, int KX>
+__device__ inline double g1_p_in(const double* xf, int r, int c) {
+    int ry, cx;
+    double y0, y1, x0, x1;
+    g1_p1d_in<KY>(r, ry, y0, y1);
+    g1_p1d_in<KX>(c, cx, x0, x1);
+    const double* q = xf + ry * kG1CW + cx;
+    double acc = 0.0;
+    acc += (y0 * x0) * q[0];
+    acc += (y0 * x1) * q[1];
+    acc += (y1 * x0) * q[kG1CW];
+    acc += (y1 * x1) * q[kG1CW + 1];
+    return acc;
+}
+// R_0's row at tile coarse (lr, lc) over t1's window (fine block + 1): 2 lr + 0 .. 3 (cell) / 0 .. 2 (node)
+template <int KY, int KX>
+__device__ inline double g1_r_in(const double* tf, int lr, int lc) {
+    constexpr int MY = KY == MPBP_MG_CELL ? 4 : 3, MX = KX == MPBP_MG_CELL ? 4 : 3;
+    constexpr double WC[4] = {0.25, 0.75, 0.75, 0.25}, WN[3] = {0.5, 1.0, 0.5};
+    const double* q = tf + (2 * lr) * kG1FW + 2 * lc;
+    double acc = 0.0;
+#pragma unroll
+    for (int a = 0; a < MY; ++a)
+#pragma unroll
+        for (int b = 0; b < MX; ++b)
+            acc += ((KY == MPBP_MG_CELL ? WC[a] : WN[a]) * (KX == MPBP_MG_CELL ? WC[b] : WN[b])) * q[a * kG1FW + b];
+    return acc;
+}
+template <bool INNER, class Epi, bool MAC, class XS>
+__device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& tr, const XS& xin, const Epi& epi,
+                                         double* xs, double* ts, double* t0, double* t1, int cr0, int cc0);
 // MAC: the F hierarchy's kinds (u: rows cell-, columns node-centred; v: the reverse) at compile time
 // XS: the coarse x as staged -- XPlain (x itself) or XInit (x0 = c2_0 (b / diag): a pre-smoothing's first sweep with the
 // init pass folded in, as the grouped small levels do; the epilogue then EpiChebFirstGrp)
@@ -4001,11 +4053,25 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1(FStencilFast P, MgF
     __shared__ double xs[4 * CN];
     __shared__ double ts[PN];
     __shared__ double t0[4 * PN];
-    __shared__ double t1[4 * FN];
-    const int n = P.n, nc = n >> 1, ncc = nc * nc;
+    double* t1 = t0;
+    static_assert(FN <= PN, "t1 fits t0");
+    const int nc = P.n >> 1;
     const int tx = (nc + kG1W - 1) / kG1W;
     const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
     const int cr0 = (bk / tx) * kG1H, cc0 = (bk % tx) * kG1W;     // the coarse tile
+    if constexpr (MAC) {
+        if (cr0 >= 2 && cr0 + kG1H + 2 <= nc && cc0 >= 2 && cc0 + kG1W + 2 <= nc) {
+            gal1_run<true, Epi, MAC, XS>(P, tr, xin, epi, xs, ts, t0, t1, cr0, cc0);
+            return;
+        }
+    }
+    gal1_run<false, Epi, MAC, XS>(P, tr, xin, epi, xs, ts, t0, t1, cr0, cc0);
+}
+template <bool INNER, class Epi, bool MAC, class XS>
+__device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& tr, const XS& xin, const Epi& epi,
+                                         double* xs, double* ts, double* t0, double* t1, int cr0, int cc0) {
+    constexpr int CN = kG1CW * kG1CH, PN = kG1PW * kG1PH, FN = kG1FW * kG1FH;
+    const int n = P.n, nc = n >> 1, ncc = nc * nc;
     const int fr0 = 2 * cr0, fc0 = 2 * cc0;                      // its fine block
     const int tid = threadIdx.x;
     auto wrapc = [&](int a) { return a < 0 ? a + nc : (a >= nc ? a - nc : a); };
@@ -4056,6 +4122,13 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1(FStencilFast P, MgF
     for (int i = tid; i < PN; i += 256) {
         const int r = i / kG1PW, c = i - r * kG1PW;
         const int gr = P.wrap(fr0 - 2 + r), gc = P.wrap(fc0 - 2 + c);
+        if constexpr (MAC && INNER) {
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+                t0[f * PN + i] = (f & 1) ? g1_p_in<MPBP_MG_NODE, MPBP_MG_CELL>(xs + f * CN, r, c)
+                                         : g1_p_in<MPBP_MG_CELL, MPBP_MG_NODE>(xs + f * CN, r, c);
+            continue;
+        }
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
             if constexpr (MAC) {
@@ -4079,16 +4152,24 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1(FStencilFast P, MgF
     {
         const TTileT<kG1PW> tt{ts, fr0 - 2, fc0 - 2};
         const XTileT<kG1PW, kG1PH> xt{t0, fr0 - 2, fc0 - 2};
+        // t1 takes t0's LDS (63 -> 42 KB per workgroup: 3 resident per CU instead of 2): rows kept in registers until
+        // every lane has read its t0 neighbours
+        double tv[IF][4];
 #pragma unroll
         for (int it = 0; it < IF; ++it) {
             const int i = tid + it * 256;
             if (i >= FN) break;
             const int r = i / kG1FW, c = i - r * kG1FW;
-            const int vr = fr0 - 1 + r, vc = fc0 - 1 + c;
-            double acc[4], rd[4];
-            P.template rows4<false>(vr, vc, tt, xt, FStencilDev::Cell{{fu[it], fv[it]}}, acc, rd);
+            double rd[4];
+            P.template rows4<false>(fr0 - 1 + r, fc0 - 1 + c, tt, xt, FStencilDev::Cell{{fu[it], fv[it]}}, tv[it], rd);
+        }
+        __syncthreads();
 #pragma unroll
-            for (int f = 0; f < 4; ++f) t1[f * FN + i] = acc[f];
+        for (int it = 0; it < IF; ++it) {
+            const int i = tid + it * 256;
+            if (i >= FN) break;
+#pragma unroll
+            for (int f = 0; f < 4; ++f) t1[f * FN + i] = tv[it][f];
         }
     }
     __syncthreads();
@@ -4102,8 +4183,13 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1(FStencilFast P, MgF
                 const int f = fp + 2 * h;
                 const int32_t row = f * ncc + cr * nc + cc;
                 const typename Epi::P pe = epi.pre(row);
-                const double acc = fp ? g1_r<MPBP_MG_NODE, MPBP_MG_CELL>(t1 + f * FN, cr, cc, n, fr0 - 1, fc0 - 1)
-                                      : g1_r<MPBP_MG_CELL, MPBP_MG_NODE>(t1 + f * FN, cr, cc, n, fr0 - 1, fc0 - 1);
+                double acc;
+                if constexpr (INNER)
+                    acc = fp ? g1_r_in<MPBP_MG_NODE, MPBP_MG_CELL>(t1 + f * FN, cr - cr0, cc - cc0)
+                             : g1_r_in<MPBP_MG_CELL, MPBP_MG_NODE>(t1 + f * FN, cr - cr0, cc - cc0);
+                else
+                    acc = fp ? g1_r<MPBP_MG_NODE, MPBP_MG_CELL>(t1 + f * FN, cr, cc, n, fr0 - 1, fc0 - 1)
+                             : g1_r<MPBP_MG_CELL, MPBP_MG_NODE>(t1 + f * FN, cr, cc, n, fr0 - 1, fc0 - 1);
                 epi(row, acc, pe);
             }
         }
@@ -4298,7 +4384,8 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, X
     __shared__ double xs[CN];
     __shared__ double ts[PN];
     __shared__ double t0[PN];
-    __shared__ double t1[FN];
+    double* t1 = t0;   // (k_gal1's aliasing: 34.7 -> 25 KB per workgroup)
+    static_assert(FN <= PN, "t1 fits t0");
     const int n = P.n, nc = n >> 1;
     const int tx = (nc + kG1W - 1) / kG1W;
     const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -4334,14 +4421,20 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, X
             if (tid + it * 256 < PN) ts[tid + it * 256] = vt[it];
     }
     __syncthreads();
+    const bool inner = cr0 >= 2 && cr0 + kG1PH2 + 2 <= nc && cc0 >= 2 && cc0 + kG1W + 2 <= nc;   // (k_gal1's g1_*_in)
     for (int i = tid; i < PN; i += 256) {   // t0 = P_0 x on the fine block + 2
         const int r = i / kG1PW, c = i - r * kG1PW;
-        t0[i] = g1_p<MPBP_MG_CELL, MPBP_MG_CELL>(xs, P.wrap(fr0 - 2 + r), P.wrap(fc0 - 2 + c), nc, cr0 - 2, cc0 - 2);
+        t0[i] = inner ? g1_p_in<MPBP_MG_CELL, MPBP_MG_CELL>(xs, r, c)
+                      : g1_p<MPBP_MG_CELL, MPBP_MG_CELL>(xs, P.wrap(fr0 - 2 + r), P.wrap(fc0 - 2 + c), nc, cr0 - 2, cc0 - 2);
     }
     __syncthreads();
     {   // t1 = Gt_G t0 on the fine block + 1
         const TTileT<kG1PW> ta{ts, fr0 - 2, fc0 - 2};
-        for (int i0 = 0; i0 < FN; i0 += 256) {
+        constexpr int IT1 = (FN + 255) / 256;
+        double tv[IT1];
+#pragma unroll
+        for (int it = 0; it < IT1; ++it) {
+            const int i0 = it * 256;
             const int i = i0 + tid;
             const bool live = i < FN;
             const int ii = live ? i : 0;
@@ -4356,8 +4449,12 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, X
             const double pr[5] = {e[0] * t0[si - kG1PW], e[1] * t0[si - 1], e[2] * t0[si], e[3] * t0[si + 1],
                                   e[4] * t0[si + kG1PW]};
             const Wrap wr{gr == 0, gr == n - 1, gc == 0, gc == n - 1};
-            t1[i] = edge ? add5<true>(0.0, pr, wr) : add5<false>(0.0, pr, wr);
+            tv[it] = edge ? add5<true>(0.0, pr, wr) : add5<false>(0.0, pr, wr);
         }
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < IT1; ++it)
+            if (it * 256 + tid < FN) t1[it * 256 + tid] = tv[it];
     }
     __syncthreads();
     {   // R_0 t1 on the tile's 256 coarse rows, each to the epilogue
@@ -4365,7 +4462,8 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, X
         if (cr < nc && cc < nc) {
             const int32_t row = cr * nc + cc;
             const typename Epi::P pe = epi.pre(row);
-            epi(row, g1_r<MPBP_MG_CELL, MPBP_MG_CELL>(t1, cr, cc, n, fr0 - 1, fc0 - 1), pe);
+            epi(row, inner ? g1_r_in<MPBP_MG_CELL, MPBP_MG_CELL>(t1, cr - cr0, cc - cc0)
+                           : g1_r<MPBP_MG_CELL, MPBP_MG_CELL>(t1, cr, cc, n, fr0 - 1, fc0 - 1), pe);
         }
     }
 }
@@ -4472,7 +4570,8 @@ int check_svl(const mpbp_svl* V, const mpbp_csr* A) {
 template <class Epi, class XS = XPlain>
 int launch_svl(const mpbp_svl* V, const mpbp_csr* A, const XS& xs, Epi epi, hipStream_t st) {
     const int64_t w = V->m - 2 * V->reach;
-    const int64_t threads = (((int64_t)V->n_edge * kSvEdgeG + kBlock - 1) / kBlock) * kBlock + V->nfields * (w / 2) * w;
+    const int64_t per = (w / 2) * w;
+    const int64_t threads = (((int64_t)V->n_edge * kSvEdgeG + kBlock - 1) / kBlock) * kBlock + V->nfields * per;
     if (threads <= 0) return MPBP_OK;
     k_svl<XS, Epi><<<(unsigned)((threads + kBlock - 1) / kBlock), kBlock, 0, st>>>(to_svl(V), to_csr(A), A->nrows, xs,
                                                                                     epi);
