@@ -2846,8 +2846,18 @@ struct FTile {
                                   // hierarchy's MAC kinds) is the iterate -- the prolongation launch folded in
 };
 
+// multigrid level 1's tile and windows (k_gal1; the level-0 fused kernels stage the same windows)
+constexpr int kG1W = 32, kG1H = 4;                          // coarse tile
+constexpr int kG1FW = 2 * kG1W + 2, kG1FH = 2 * kG1H + 2;   // t1: fine [2 c0 - 1, 2 c0 + 2 W + 1)
+constexpr int kG1PW = kG1FW + 2, kG1PH = kG1FH + 2;         // t0 and thn: one more fine cell each side
+constexpr int kG1CW = kG1W + 4, kG1CH = kG1H + 4;           // coarse x: [c0 - 2, c0 + W + 2)
 template <int KY, int KX>
 __device__ inline double g1_p(const double* xf, int gr, int gc, int nc, int rb, int cb);
+template <int KY, int KX>
+__device__ inline double g1_p_in(const double* xf, int r, int c);
+template <int KY, int KX, int W, int OFF>
+__device__ inline double g1_rw_in(const double* tf, int lr, int lc);
+__device__ inline bool g1_inner(int cr0, int cc0, int th, int tw, int nc);
 template <bool INIT, bool SUB, bool SD, class BS, bool PRO = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) MPBP_LDS_READS k_ftile(FStencilFast P, FTile a, BS bs) {
     __shared__ double xs[INIT ? 1 : 4 * kFSN];   // !INIT: x_in over the tile + 2 halo
@@ -2863,6 +2873,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))
     // PRO: the coarse correction over [r0 / 2 - 2, r0 / 2 + 6) x [c0 / 2 - 2, c0 / 2 + 34) of 4 fields (k_gal1's window)
     constexpr int CW = kFTW / 2 + 4, CH = kFTH / 2 + 4, CN = CW * CH;
     static_assert(!PRO || 4 * CN <= 4 * kFAN, "the coarse window fits the level-A buffer");
+    static_assert(CW == kG1CW && kFSW == kG1PW && kFSH == kG1PH, "g1_p_in's window geometry");
     const int nc = n >> 1, ncc = nc * nc, cr0 = r0 >> 1, cc0 = c0 >> 1;
     // stage thn (and x_in) over rows r0-2 .. r0+9, columns c0-2 .. c0+65: every load issued before the first LDS store
     {
@@ -2907,10 +2918,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))
                     if constexpr (PRO) {   // x_in + P_0 xc: k_mg_transfer_spmv's prolongation and EpiAdd's sum
                         const int sr = i / kFSW, sc = i - sr * kFSW;
                         const int gr = P.wrap(rb + sr), gc = P.wrap(cb + sc);
+                        const bool inner = g1_inner(cr0, cc0, kFTH / 2, kFTW / 2, nc);   // (window coordinates)
 #pragma unroll
                         for (int f = 0; f < 4; ++f) {
-                            const double pc = (f & 1) ? g1_p<MPBP_MG_NODE, MPBP_MG_CELL>(xl + f * CN, gr, gc, nc, cr0 - 2, cc0 - 2)
-                                                      : g1_p<MPBP_MG_CELL, MPBP_MG_NODE>(xl + f * CN, gr, gc, nc, cr0 - 2, cc0 - 2);
+                            const double pc =
+                                inner ? ((f & 1) ? g1_p_in<MPBP_MG_NODE, MPBP_MG_CELL>(xl + f * CN, sr, sc)
+                                                 : g1_p_in<MPBP_MG_CELL, MPBP_MG_NODE>(xl + f * CN, sr, sc))
+                                      : ((f & 1) ? g1_p<MPBP_MG_NODE, MPBP_MG_CELL>(xl + f * CN, gr, gc, nc, cr0 - 2, cc0 - 2)
+                                                 : g1_p<MPBP_MG_CELL, MPBP_MG_NODE>(xl + f * CN, gr, gc, nc, cr0 - 2, cc0 - 2));
                             xs[f * kFSN + i] = pc + v[it][1 + f];
                         }
                     } else {
@@ -3597,8 +3612,12 @@ struct GtgD {
     const double* Y;    // Finv_v: u_n, v_n, u_s, v_s
     const double* vp;   // v's pressure part
 };
+#ifndef MPBP_GTG_WPE
+#define MPBP_GTG_WPE 1
+#endif
 template <int H, bool PART, int TPB, bool DB>
-__global__ void __launch_bounds__(TPB) MPBP_LDS_READS k_gtg_solve(GtGStencilDev P, const double* __restrict__ b,
+__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB == 512 ? MPBP_GTG_WPE : 1, 8)))
+MPBP_LDS_READS k_gtg_solve(GtGStencilDev P, const double* __restrict__ b,
                                                    const double* __restrict__ diag, ChebK ck, double* __restrict__ out,
                                                    GtgD dv) {
     using G = GtgTile<H>;
@@ -3807,6 +3826,7 @@ k_gtg_level0(GtGStencilDev P, const double* __restrict__ b, const double* __rest
     constexpr int H = PRE ? 3 : 2;   // staged halo: the tile + H
     using G = GtgTile<H>;
     constexpr int CW = kGTW / 2 + 4, CH = kGTH / 2 + 4, CN = CW * CH;   // k_gpost's coarse window (k_gal1's geometry)
+    static_assert(CW == kG1CW, "g1_p_in's window stride");
     __shared__ double ts[G::N], bs[G::N], xa[G::N], xb[G::N];
     __shared__ double cs[PRE ? 1 : CN];
     const int n = P.n, nc = n >> 1;
@@ -3857,8 +3877,10 @@ k_gtg_level0(GtGStencilDev P, const double* __restrict__ b, const double* __rest
                     xa[i] = ck.c2[0] * (bv[it] / wv[it]);   // x0 (k_cheb_init's expression, XInit's)
                 } else {                                     // x_in + P_0 x_c (the prolongation's sum)
                     const int rr = i / G::RW, cc = i - rr * G::RW;
-                    const double pc = g1_p<MPBP_MG_CELL, MPBP_MG_CELL>(cs, P.wrap(rb + rr), P.wrap(cb + cc), nc, cr0 - 2,
-                                                                       cc0 - 2);
+                    const double pc = g1_inner(cr0, cc0, kGTH / 2, kGTW / 2, nc)
+                                          ? g1_p_in<MPBP_MG_CELL, MPBP_MG_CELL>(cs, rr, cc)
+                                          : g1_p<MPBP_MG_CELL, MPBP_MG_CELL>(cs, P.wrap(rb + rr), P.wrap(cb + cc), nc,
+                                                                             cr0 - 2, cc0 - 2);
                     xa[i] = pc + wv[it];
                 }
             }
@@ -3939,7 +3961,9 @@ k_gtg_level0(GtGStencilDev P, const double* __restrict__ b, const double* __rest
         if (tid < CTW * CTH) {
             const int crr = cr0 + tid / CTW, ccc = cc0 + tid % CTW;
             if (crr < nc && ccc < nc)
-                bc[crr * nc + ccc] = g1_rw<MPBP_MG_CELL, MPBP_MG_CELL, G::RW>(cur, crr, ccc, n, rb, cb);
+                bc[crr * nc + ccc] = g1_inner(cr0, cc0, CTH, CTW, nc)
+                                         ? g1_rw_in<MPBP_MG_CELL, MPBP_MG_CELL, G::RW, 2>(cur, crr - cr0, ccc - cc0)
+                                         : g1_rw<MPBP_MG_CELL, MPBP_MG_CELL, G::RW>(cur, crr, ccc, n, rb, cb);
         }
     }
 }
@@ -3951,10 +3975,7 @@ k_gtg_level0(GtGStencilDev P, const double* __restrict__ b, const double* __rest
 // tolerance-mode rows), and R_0 t1 on its coarse rows, handing each to the level's epilogue.  Each value is built by
 // the operations of the three launches it replaces (k_mg_transfer_spmv's 1D lists and product order, FStencilFast::rows4),
 // so the result is bit-identical; HBM: x, thn and the epilogue operands once, no fine vector written or read.
-constexpr int kG1W = 32, kG1H = 4;                          // coarse tile
-constexpr int kG1FW = 2 * kG1W + 2, kG1FH = 2 * kG1H + 2;   // t1: fine [2 c0 - 1, 2 c0 + 2 W + 1)
-constexpr int kG1PW = kG1FW + 2, kG1PH = kG1FH + 2;         // t0 and thn: one more fine cell each side
-constexpr int kG1CW = kG1W + 4, kG1CH = kG1H + 4;           // coarse x: [c0 - 2, c0 + W + 2)
+// (k_gal1's tile and window geometry: constants above)
 // a grid index to its slot in a staged window starting at virtual index `base` (the window is < the grid)
 __device__ inline int g1_slot(int i, int base, int m) { int l = i - base; return l < 0 ? l + m : (l >= m ? l - m : l); }
 // P_0's row at fine (gr, gc) of a field with compile-time kinds: k_mg_transfer_spmv's list order and products
@@ -4027,19 +4048,28 @@ __device__ inline double g1_p_in(const double* xf, int r, int c) {
     acc += (y1 * x1) * q[kG1CW + 1];
     return acc;
 }
-// R_0's row at tile coarse (lr, lc) over t1's window (fine block + 1): 2 lr + 0 .. 3 (cell) / 0 .. 2 (node)
-template <int KY, int KX>
-__device__ inline double g1_r_in(const double* tf, int lr, int lc) {
+// R_0's row at tile coarse (lr, lc) over a fine window of row stride W whose slot OFF holds fine index 2 c0 - 1 (the
+// tile's first coarse cell's first restriction entry): 2 lr + OFF + 0 .. 3 (cell) / 0 .. 2 (node)
+template <int KY, int KX, int W, int OFF>
+__device__ inline double g1_rw_in(const double* tf, int lr, int lc) {
     constexpr int MY = KY == MPBP_MG_CELL ? 4 : 3, MX = KX == MPBP_MG_CELL ? 4 : 3;
     constexpr double WC[4] = {0.25, 0.75, 0.75, 0.25}, WN[3] = {0.5, 1.0, 0.5};
-    const double* q = tf + (2 * lr) * kG1FW + 2 * lc;
+    const double* q = tf + (2 * lr + OFF) * W + 2 * lc + OFF;
     double acc = 0.0;
 #pragma unroll
     for (int a = 0; a < MY; ++a)
 #pragma unroll
         for (int b = 0; b < MX; ++b)
-            acc += ((KY == MPBP_MG_CELL ? WC[a] : WN[a]) * (KX == MPBP_MG_CELL ? WC[b] : WN[b])) * q[a * kG1FW + b];
+            acc += ((KY == MPBP_MG_CELL ? WC[a] : WN[a]) * (KX == MPBP_MG_CELL ? WC[b] : WN[b])) * q[a * W + b];
     return acc;
+}
+// ... over t1's window (fine block + 1)
+template <int KY, int KX>
+__device__ inline double g1_r_in(const double* tf, int lr, int lc) { return g1_rw_in<KY, KX, kG1FW, 0>(tf, lr, lc); }
+// a tile whose transfers' windows neither wrap nor reach a 1D list's periodic special case (coarse tile of TH x TW
+// cells at (cr0, cc0), windows two coarse cells beyond it)
+__device__ inline bool g1_inner(int cr0, int cc0, int th, int tw, int nc) {
+    return cr0 >= 2 && cr0 + th + 2 <= nc && cc0 >= 2 && cc0 + tw + 2 <= nc;
 }
 template <bool INNER, class Epi, bool MAC, class XS>
 __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& tr, const XS& xin, const Epi& epi,
@@ -4060,7 +4090,7 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1(FStencilFast P, MgF
     const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
     const int cr0 = (bk / tx) * kG1H, cc0 = (bk % tx) * kG1W;     // the coarse tile
     if constexpr (MAC) {
-        if (cr0 >= 2 && cr0 + kG1H + 2 <= nc && cc0 >= 2 && cc0 + kG1W + 2 <= nc) {
+        if (g1_inner(cr0, cc0, kG1H, kG1W, nc)) {
             gal1_run<true, Epi, MAC, XS>(P, tr, xin, epi, xs, ts, t0, t1, cr0, cc0);
             return;
         }
@@ -4366,8 +4396,14 @@ k_fpre(FStencilFast P, FPre a) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int f = fp + 2 * h;
-            const double acc = fp ? g1_rw<MPBP_MG_NODE, MPBP_MG_CELL, T::RW>(xa + f * T::N, crr, ccc, n, rb, cb)
-                                  : g1_rw<MPBP_MG_CELL, MPBP_MG_NODE, T::RW>(xa + f * T::N, crr, ccc, n, rb, cb);
+            const bool inner = g1_inner(r0 >> 1, c0 >> 1, kFTH / 2, kFTW / 2, nc);   // (window coordinates, slot 2 =
+                                                                                     // fine 2 c0 - 1: rb = r0 - 3)
+            const int lr = crr - (r0 >> 1), lc = ccc - (c0 >> 1);
+            const double acc =
+                inner ? (fp ? g1_rw_in<MPBP_MG_NODE, MPBP_MG_CELL, T::RW, 2>(xa + f * T::N, lr, lc)
+                            : g1_rw_in<MPBP_MG_CELL, MPBP_MG_NODE, T::RW, 2>(xa + f * T::N, lr, lc))
+                      : (fp ? g1_rw<MPBP_MG_NODE, MPBP_MG_CELL, T::RW>(xa + f * T::N, crr, ccc, n, rb, cb)
+                            : g1_rw<MPBP_MG_CELL, MPBP_MG_NODE, T::RW>(xa + f * T::N, crr, ccc, n, rb, cb));
             a.bc[f * ncc + crr * nc + ccc] = acc;
         }
     }
@@ -4421,7 +4457,7 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, X
             if (tid + it * 256 < PN) ts[tid + it * 256] = vt[it];
     }
     __syncthreads();
-    const bool inner = cr0 >= 2 && cr0 + kG1PH2 + 2 <= nc && cc0 >= 2 && cc0 + kG1W + 2 <= nc;   // (k_gal1's g1_*_in)
+    const bool inner = g1_inner(cr0, cc0, kG1PH2, kG1W, nc);   // (k_gal1's g1_*_in)
     for (int i = tid; i < PN; i += 256) {   // t0 = P_0 x on the fine block + 2
         const int r = i / kG1PW, c = i - r * kG1PW;
         t0[i] = inner ? g1_p_in<MPBP_MG_CELL, MPBP_MG_CELL>(xs, r, c)
