@@ -490,7 +490,10 @@ typedef struct mpbp_kernel_opts {
     int32_t csr_table;         /* CSR SpMV waves start from the row blocks' wave table when present (1, default) */
     int32_t mg_fuse_l0;        /* tolerance-mode F hierarchies, one GPU: level 0's pre-smoothing, residual and restriction
                                   as ONE k_fpre launch, and the prolongation inside the post-smoothing pair (1, default) */
-    int32_t reserved[6];
+    int32_t mg_coarse_tree;    /* tolerance-mode hierarchies: the coarsest level's dense inverse applied with its row sums
+                                  split over the workgroup and combined by a tree (1; default 0: another order of the
+                                  ill-conditioned coarsest F inverse's sums moves the apply by ~5e-13) */
+    int32_t reserved[5];
 } mpbp_kernel_opts;
 /* *out = the calling thread's current choices: its mpbp_kernel_opts_set_thread scope, else the process defaults. */
 void mpbp_kernel_opts_default(mpbp_kernel_opts* out);

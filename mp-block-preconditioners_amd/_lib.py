@@ -84,7 +84,8 @@ class KernelOpts(Structure):
                 ("gtg_fused", c_int32), ("gtg_tpb", c_int32), ("gtg_drhs", c_int32), ("q13_sym", c_int32),
                 ("f_tile", c_int32), ("f_solve", c_int32), ("mg_galerkin_mf", c_int32), ("mg_galerkin_mf_p", c_int32),
                 ("pg_direct", c_int32), ("mg_group_rows", c_int32), ("mg_svl", c_int32), ("mg_mf_transfer", c_int32),
-                ("csr_table", c_int32), ("mg_fuse_l0", c_int32), ("reserved", c_int32 * 6)]
+                ("csr_table", c_int32), ("mg_fuse_l0", c_int32), ("mg_coarse_tree", c_int32),
+                ("reserved", c_int32 * 5)]
 
 
 def kernel_opts(overrides=None) -> KernelOpts:

@@ -27,7 +27,8 @@ thread_local char g_err[1024] = "";
 mpbp_kernel_opts g_defaults = {
     /*march_rows*/ 0, /*init_diag*/ 1, /*f_pair*/ 1, /*f_direct*/ 0, /*gtg_fused*/ 1, /*gtg_tpb*/ 512, /*gtg_drhs*/ 1,
     /*q13_sym*/ 1, /*f_tile*/ 1, /*f_solve*/ 1, /*mg_galerkin_mf*/ 2, /*mg_galerkin_mf_p*/ 1, /*pg_direct*/ 1,
-    /*mg_group_rows*/ 65536, /*mg_svl*/ 1, /*mg_mf_transfer*/ 1, /*csr_table*/ 1, /*mg_fuse_l0*/ 1, {0, 0, 0, 0, 0, 0}};
+    /*mg_group_rows*/ 65536, /*mg_svl*/ 1, /*mg_mf_transfer*/ 1, /*csr_table*/ 1, /*mg_fuse_l0*/ 1,
+    /*mg_coarse_tree*/ 0, {0, 0, 0, 0, 0}};
 thread_local const mpbp_kernel_opts* t_opts = nullptr;
 inline const mpbp_kernel_opts& KO() { return t_opts ? *t_opts : g_defaults; }
 struct OptsScope {   // installs a plan's kernel choices (when it has its own) for one entry-point call
@@ -46,10 +47,10 @@ inline int check_opts(const mpbp_kernel_opts* o, const char* who) {
                     o->mg_galerkin_mf >= 0 && o->mg_galerkin_mf <= 2 && o->mg_group_rows >= 0 &&
                     (o->init_diag | o->f_pair | o->f_direct | o->gtg_fused | o->gtg_drhs | o->q13_sym | o->f_tile |
                      o->f_solve | o->mg_galerkin_mf_p | o->pg_direct | o->mg_svl | o->mg_mf_transfer | o->csr_table |
-                     o->mg_fuse_l0) >= 0 &&
+                     o->mg_fuse_l0 | o->mg_coarse_tree) >= 0 &&
                     (o->init_diag | o->f_pair | o->f_direct | o->gtg_fused | o->gtg_drhs | o->q13_sym | o->f_tile |
                      o->f_solve | o->mg_galerkin_mf_p | o->pg_direct | o->mg_svl | o->mg_mf_transfer | o->csr_table |
-                     o->mg_fuse_l0) <= 1;
+                     o->mg_fuse_l0 | o->mg_coarse_tree) <= 1;
     return ok ? MPBP_OK : set_error(MPBP_ERR_ARG, "%s: kernel options out of range", who);
 }   // rows per workgroup of the D / G / Gt_G marching kernels: as F
 
@@ -4134,6 +4135,18 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
         for (int it = 0; it < IT; ++it)
             if (tid + it * 256 < PN) ts[tid + it * 256] = vt[it];
     }
+#if MPBP_GAL_PREPE
+    // experiment: the epilogue's operands of this lane's two coarse rows loaded here, behind the three stages
+    typename Epi::P pe2[2] = {};
+    if constexpr (MAC) {
+        const int cell = tid & (kG1W * kG1H - 1), fp = tid >> 7;
+        const int cr = cr0 + cell / kG1W, cc = cc0 + cell % kG1W;
+        if (cr < nc && cc < nc) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) pe2[h] = epi.pre((fp + 2 * h) * ncc + cr * nc + cc);
+        }
+    }
+#endif
     // the faces of this lane's t1 cells, loaded ahead (their latency behind the P_0 stage, not in the F stage)
     constexpr int IF = (FN + 255) / 256;
     double fu[IF], fv[IF];
@@ -4212,7 +4225,11 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
             for (int h = 0; h < 2; ++h) {
                 const int f = fp + 2 * h;
                 const int32_t row = f * ncc + cr * nc + cc;
+#if MPBP_GAL_PREPE
+                const typename Epi::P pe = pe2[h];
+#else
                 const typename Epi::P pe = epi.pre(row);
+#endif
                 double acc;
                 if constexpr (INNER)
                     acc = fp ? g1_r_in<MPBP_MG_NODE, MPBP_MG_CELL>(t1 + f * FN, cr - cr0, cc - cc0)
@@ -4458,6 +4475,13 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, X
     }
     __syncthreads();
     const bool inner = g1_inner(cr0, cc0, kG1PH2, kG1W, nc);   // (k_gal1's g1_*_in)
+#if MPBP_GAL_PREPE
+    typename Epi::P pe1{};
+    {
+        const int cr = cr0 + tid / kG1W, cc = cc0 + tid % kG1W;
+        if (cr < nc && cc < nc) pe1 = epi.pre(cr * nc + cc);
+    }
+#endif
     for (int i = tid; i < PN; i += 256) {   // t0 = P_0 x on the fine block + 2
         const int r = i / kG1PW, c = i - r * kG1PW;
         t0[i] = inner ? g1_p_in<MPBP_MG_CELL, MPBP_MG_CELL>(xs, r, c)
@@ -4497,7 +4521,11 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, X
         const int cr = cr0 + tid / kG1W, cc = cc0 + tid % kG1W;
         if (cr < nc && cc < nc) {
             const int32_t row = cr * nc + cc;
+#if MPBP_GAL_PREPE
+            const typename Epi::P pe = pe1;
+#else
             const typename Epi::P pe = epi.pre(row);
+#endif
             epi(row, inner ? g1_r_in<MPBP_MG_CELL, MPBP_MG_CELL>(t1, cr - cr0, cc - cc0)
                            : g1_r<MPBP_MG_CELL, MPBP_MG_CELL>(t1, cr, cc, n, fr0 - 1, fc0 - 1), pe);
         }
@@ -6614,6 +6642,40 @@ __global__ void __launch_bounds__(kDT) k_dense_cm(int32_t m, const double* __res
     if (t < kDR && r0 + t < m) y[r0 + t] = acc;
 }
 
+// The same product in tolerance mode (kernel option mg_coarse_tree): a workgroup owns kDR rows and every thread sums the
+// products of its 16 columns of one row in registers as it loads them (no LDS round trip per product); the row's 64
+// partial sums are then added pairwise in LDS.  One memory round trip and a 6-deep tree instead of the ordered row sum's
+// m dependent additions (~1e-16 relative from the exact mode's k_dense_cm, which keeps the CSR row's bits).
+__global__ void __launch_bounds__(kDT) k_dense_tree(int32_t m, const double* __restrict__ Mt,
+                                                   const double* __restrict__ b, double* __restrict__ y) {
+    constexpr int CPT = kDK * kDR / kDT;   // 16 columns per thread and slab
+    constexpr int NP = kDT / kDR;          // 64 partial sums per row
+    __shared__ double part[kDR * NP];
+    const int32_t r0 = blockIdx.x * kDR;
+    const int t = threadIdx.x, row = r0 + t % kDR, k = t / kDR;   // thread t: row t % 16, columns k + 64 u
+    double acc = 0.0;
+    for (int32_t j0 = 0; j0 < m; j0 += kDK) {
+        double v[CPT], bv[CPT];
+#pragma unroll
+        for (int u = 0; u < CPT; ++u) {
+            const int32_t c = j0 + k + NP * u;
+            const bool in = c < m && row < m;
+            v[u] = in ? Mt[(size_t)c * m + row] : 0.0;   // (lanes of a wave: 16 rows x 4 columns, 128-byte runs)
+            bv[u] = c < m ? b[c] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < CPT; ++u) acc += v[u] * bv[u];
+    }
+    part[(t % kDR) * NP + k] = acc;
+    __syncthreads();
+#pragma unroll
+    for (int w = NP / 2; w >= 1; w >>= 1) {   // rows' partials pairwise: t < 16 w lanes, row t % 16
+        if (t < kDR * w) part[(t % kDR) * NP + t / kDR] += part[(t % kDR) * NP + t / kDR + w];
+        __syncthreads();
+    }
+    if (t < kDR && r0 + t < m) y[r0 + t] = part[t * NP];
+}
+
 // K Chebyshev-Jacobi sweeps on [lmin, lmax].  zero: from x = 0 (the first sweep is the init pass: d = x =
 // c2[0] b / diag), else from the iterate in *cur (d starts at 0).  The last sweep writes `dst` (or the free
 // ping-pong buffer when dst is NULL), as sub - x when sub is set; *cur points at the result on return.  xch(x)
@@ -6862,7 +6924,11 @@ int mg_vcycle(const mpbp_mg* m, int l, const MgFine& fine, const double* b, bool
     double* xc = C.x;
     if (l + 1 == m->nlevels - 1) {
         if (m->coarse_dense) {
-            k_dense_cm<<<grid_for(C.nrows, kDR), kDT, 0, st>>>(C.nrows, m->coarse_dense, C.b, xc);
+            // tolerance-mode hierarchies (the fine operator a fast-numerics stencil plan): the tree-summed product
+            const bool tree = KO().mg_coarse_tree && fine.op.in.stencil &&
+                              fine.op.in.stencil->f_numerics == MPBP_NUMERICS_FAST;
+            if (tree) k_dense_tree<<<grid_for(C.nrows, kDR), kDT, 0, st>>>(C.nrows, m->coarse_dense, C.b, xc);
+            else k_dense_cm<<<grid_for(C.nrows, kDR), kDT, 0, st>>>(C.nrows, m->coarse_dense, C.b, xc);
             MPBP_HIP(hipGetLastError());
         } else {
             rc = mpbp_spmv(&m->coarse_inv, &m->coarse_inv_blocks, MPBP_SPMV_STORE, C.b, nullptr, xc, (void*)st);

@@ -128,7 +128,8 @@ class PlanProfiling:
     def set_kernel_opts(self, **kw):
         """Change this preconditioner's kernel choices (mpbp_kernel_opts field names; others untouched).  The next apply
         or capture uses them; graphs captured before keep the choices they were captured with.  Every choice computes
-        the same bits except q13_sym (tolerance mode), which stays 0 where the stored Gt_F_G is not symmetric."""
+        the same bits except q13_sym and mg_coarse_tree (tolerance mode; q13_sym stays 0 where the stored Gt_F_G is not
+        symmetric)."""
         names = {f for f, _ in _lib.KernelOpts._fields_ if f != "reserved"}
         for k, v in kw.items():
             if k not in names:

@@ -329,6 +329,36 @@ def test_matrix_free_galerkin_level1(n):
     assert torch.equal(out, got)
 
 
+@pytest.mark.parametrize("n", [64, 256, 512])
+def test_mg_coarse_tree_sum(n):
+    """Kernel option mg_coarse_tree (opt-in): tolerance-mode hierarchies apply the coarsest level's dense inverse with
+    each row's sum split over the workgroup and combined by a tree -- within 1e-12 of the ordered-sum apply (the
+    coarsest F inverse is ill-conditioned: another order moves the apply by ~5e-13 at 256^2), eagerly and replayed; the
+    exact mode keeps the ordered sum (its apply is bit-identical with the option on or off)."""
+    mp = _mp()
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    kw = dict(inner_F=mp.InnerSolver("mg", 1), inner_P=mp.InnerSolver("mg", 1))
+    fast = mp.ApproxSchurPreconditioner(F, D, G, numerics="fast", **kw)
+    exact = mp.ApproxSchurPreconditioner(F, D, G, fast.GtG, fast.GtFG, **kw)
+    v = torch.randn(fast.shape[0], dtype=torch.float64, device="cuda",
+                    generator=torch.Generator(device="cuda").manual_seed(n + 5))
+    assert fast.kernel_opts.mg_coarse_tree == 0
+    ordered = fast.apply(v).clone()
+    ex0 = exact.apply(v).clone()
+    fast.set_kernel_opts(mg_coarse_tree=1)
+    exact.set_kernel_opts(mg_coarse_tree=1)
+    tree = fast.apply(v).clone()
+    assert torch.equal(exact.apply(v), ex0)
+    assert rel_inf(tree.cpu().numpy(), ordered.cpu().numpy()) <= 1e-12
+    assert rel_inf(tree.cpu().numpy(), ex0.cpu().numpy()) <= 1e-10
+    out = torch.empty_like(v)
+    g = fast.capture(v, out)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, tree)
+
+
 @pytest.mark.parametrize("n", [64, 72, 80, 100, 128, 256])
 def test_matrix_free_galerkin_level1_pressure(n):
     """The pressure hierarchy's level 1 as R_0 (Gt_G (P_0 x)) (kernel option mg_galerkin_mf_p): within 1e-10 of its stored
