@@ -3809,6 +3809,181 @@ MPBP_LDS_READS k_gtg_solve(GtGStencilDev P, const double* __restrict__ b,
     }
 }
 
+#if MPBP_GTG_PS
+// Experiment: k_gtg_solve (512 lanes, one GPU) as a persistent loop over tiles -- each workgroup walks its XCD's run of
+// tiles and issues the next tile's global loads (b, thn, diag; DB: thn, Y, v_p, diag) right after staging the current
+// one, so their latency hides behind the current tile's levels instead of opening every tile.  Same operations per
+// tile as k_gtg_solve (bit-identical).
+#ifndef MPBP_GTG_PS_WPE
+#define MPBP_GTG_PS_WPE 1
+#endif
+template <int H, bool DB>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MPBP_GTG_PS_WPE, 8))) MPBP_LDS_READS
+k_gtg_solve_ps(GtGStencilDev P, const double* __restrict__ b,
+                                                                    const double* __restrict__ diag, ChebK ck,
+                                                                    double* __restrict__ out, GtgD dv, int ntiles) {
+    constexpr int TPB = 512;
+    using G = GtgTile<H>;
+    constexpr int TW = DB ? G::RW + 2 : G::RW, TN = DB ? TW * (G::RH + 2) : G::N;
+    static_assert(140 * (H - 1) + 4 * H * (H - 1) <= 512, "512 lanes own at most one ring cell each");
+    __shared__ double ts[TN], bs[G::N], xa[G::N], xb[G::N];
+    const int n = P.n, nn = n * n;
+    const int tx = (n + kGTW - 1) / kGTW;
+    const int tid = threadIdx.x;
+    // this workgroup's tiles: XCD x = blockIdx % 8 owns the x-th eighth of the tiles, its workgroups take turns
+    const int per = (ntiles + 7) / 8, xcd = blockIdx.x & 7, nbx = (int)gridDim.x >> 3;
+    const int tend = min(ntiles, (xcd + 1) * per);
+    int tile = xcd * per + (int)(blockIdx.x >> 3);
+    constexpr int IT = (G::N + TPB - 1) / TPB, ITT = (TN + TPB - 1) / TPB;
+    double tv[ITT], bv[DB ? 1 : IT], dgl[IT], vpl[DB ? IT : 1], yl[DB ? IT : 1][8];
+    auto load = [&](int tl) {
+        const int r0 = (tl / tx) * kGTH, c0 = (tl % tx) * kGTW, rb = r0 - H, cb = c0 - H;
+#pragma unroll
+        for (int it = 0; it < ITT; ++it) {
+            const int i = tid + it * TPB;
+            if (i < TN) {
+                const int rr = i / TW, cc = i - rr * TW;
+                tv[it] = DB ? P.cell[P.wrap(rb - 1 + rr) * n + P.wrap(cb - 1 + cc)]
+                            : P.cell[P.wrap(rb + rr) * n + P.wrap(cb + cc)];
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * TPB;
+            if (i >= G::N) break;
+            const int rr = i / G::RW, cc = i - rr * G::RW;
+            const int gr = P.wrap(rb + rr), gc = P.wrap(cb + cc);
+            const int32_t k = gr * n + gc;
+            if constexpr (DB) {
+                const int ge = gc == n - 1 ? 0 : gc + 1, gs = gr == n - 1 ? 0 : gr + 1;
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    yl[it][4 * q + 0] = dv.Y[2 * q * nn + gr * n + ge];
+                    yl[it][4 * q + 1] = dv.Y[2 * q * nn + k];
+                    yl[it][4 * q + 2] = dv.Y[(2 * q + 1) * nn + k];
+                    yl[it][4 * q + 3] = dv.Y[(2 * q + 1) * nn + gs * n + gc];
+                }
+                vpl[it] = dv.vp[k];
+            } else {
+                bv[it] = b[k];
+            }
+            dgl[it] = diag[k];
+        }
+    };
+    if (tile < tend) load(tile);
+    for (; tile < tend; tile += nbx) {
+        const int r0 = (tile / tx) * kGTH, c0 = (tile % tx) * kGTW;
+        const int rb = r0 - H, cb = c0 - H;
+        __syncthreads();   // the previous tile's levels have read the buffers
+#pragma unroll
+        for (int it = 0; it < ITT; ++it)
+            if (tid + it * TPB < TN) ts[tid + it * TPB] = tv[it];
+        if constexpr (DB) {
+            __syncthreads();
+            const TTileT<TW> tD{ts, rb - 1, cb - 1};
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                const int i = tid + it * TPB;
+                if (i >= G::N) break;
+                const int rr = i / G::RW, cc = i - rr * G::RW;
+                const int vr = rb + rr, vc = cb + cc, gr = P.wrap(vr), gc = P.wrap(vc);
+                const double* yv = yl[it];
+                const bool lastc = gc == n - 1, lastr = gr == n - 1;
+                double acc = 0.0;
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const double t0 = tD.T(q, vr, vc), tE = tD.T(q, vr, vc + 1), tWv = tD.T(q, vr, vc - 1);
+                    const double tN = tD.T(q, vr - 1, vc), tS = tD.T(q, vr + 1, vc);
+                    const double uE = (P.inv * (0.5 * (t0 + tE))) * yv[4 * q + 0];
+                    const double uC = (P.minv * (0.5 * (t0 + tWv))) * yv[4 * q + 1];
+                    const double vC = (P.inv * (0.5 * (t0 + tN))) * yv[4 * q + 2];
+                    const double vS = (P.minv * (0.5 * (t0 + tS))) * yv[4 * q + 3];
+                    acc += lastc ? uE : uC;
+                    acc += lastc ? uC : uE;
+                    acc += lastr ? vS : vC;
+                    acc += lastr ? vC : vS;
+                }
+                const double bvv = acc + vpl[it];
+                bs[i] = bvv;
+                xa[i] = ck.c2[0] * (bvv / dgl[it]);
+            }
+        } else {
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                const int i = tid + it * TPB;
+                if (i < G::N) {
+                    bs[i] = bv[it];
+                    xa[i] = ck.c2[0] * (bv[it] / dgl[it]);
+                }
+            }
+        }
+        __syncthreads();
+        if (tile + nbx < tend) load(tile + nbx);   // the next tile's operands, in flight under this tile's levels
+        const TTileT<TW> ta{ts, DB ? rb - 1 : rb, DB ? cb - 1 : cb};
+        const int lr = tid >> 6, lc = tid & 63;
+        int cr[2], cc[2], si[2], rr[2];
+        bool own[2], edge[2];
+        double e[2][5], bo[2], d[2];
+        cr[0] = r0 + lr; cc[0] = c0 + lc; own[0] = true; rr[0] = 0;
+        {
+            int r = 0, j = tid;
+#pragma unroll
+            for (int q = 1; q < H; ++q)
+                if (r == 0) {
+                    if (j < 140 + 8 * q) r = q;
+                    else j -= 140 + 8 * q;
+                }
+            own[1] = r != 0;
+            rr[1] = r;
+            fs_ring_cell(r ? r : 1, r ? j : 0, r0, c0, cr[1], cc[1]);
+        }
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl) {
+            const int vr = cr[sl], vc = cc[sl], gr = P.wrap(vr), gc = P.wrap(vc);
+            si[sl] = (vr - rb) * G::RW + (vc - cb);
+            edge[sl] = __builtin_amdgcn_readfirstlane(__any(own[sl] && (gr == 0 || gr == n - 1 || gc == 0 ||
+                                                                        gc == n - 1))) != 0;
+            if (own[sl]) {
+                P.entries(vr, vc, gr, gc, ta, e[sl]);
+                bo[sl] = bs[si[sl]];
+                d[sl] = xa[si[sl]];
+            }
+        }
+        double* cur = xa;
+        double* nxt = xb;
+#pragma unroll
+        for (int l = 1; l <= H; ++l) {
+            if (l > 1) __syncthreads();
+            const double c1 = ck.c1[l], c2 = ck.c2[l];
+#pragma unroll
+            for (int sl = 0; sl < 2; ++sl) {
+                if (sl >= 1 && (!own[sl] || rr[sl] > H - l)) continue;
+                const int vr = cr[sl], vc = cc[sl];
+                if (l == H && (vr >= n || vc >= n)) continue;
+                const int i = si[sl];
+                const double p[5] = {e[sl][0] * cur[i - G::RW], e[sl][1] * cur[i - 1], e[sl][2] * cur[i],
+                                     e[sl][3] * cur[i + 1], e[sl][4] * cur[i + G::RW]};
+                const int gr = P.wrap(vr), gc = P.wrap(vc);
+                const Wrap wr{gr == 0, gr == n - 1, gc == 0, gc == n - 1};
+                const double acc = edge[sl] ? add5<true>(0.0, p, wr) : add5<false>(0.0, p, wr);
+                const double z = (bo[sl] - acc) / e[sl][2];
+                const double dn = c1 * d[sl] + c2 * z;
+                const double x = cur[i] + dn;
+                if (l < H) {
+                    nxt[i] = x;
+                    d[sl] = dn;
+                } else {
+                    out[vr * n + vc] = x;
+                }
+            }
+            double* t = cur;
+            cur = nxt;
+            nxt = t;
+        }
+    }
+}
+#endif
+
 // ---- multigrid level 0 of the pressure hierarchy (matrix-free Gt_G): descent and ascent in one launch each ----
 // k_gpre: x0 = c2_0 (b / diag) over the tile + 3, the Chebyshev sweep x1 over the tile + 2 (written on the tile), the
 // residual r = b - Gt_G x1 over the tile + 1 (in LDS) and R_0 r on the tile's 32 x 4 coarse cells (cell-centred both
@@ -7016,6 +7191,25 @@ int launch_gtg_solve_t(const GtGStencilDev& S, const double* b, const double* di
     // 512 lanes own rings 1 .. H - 1 one cell each (140 (H - 1) + 4 H (H - 1) <= 512 cells): H <= 4
     if constexpr (H <= 4) {
         if (KO().gtg_tpb == 512) {
+#if MPBP_GTG_PS
+            if (!part) {
+                static int nb[2] = {0, 0};
+                int& q = nb[db ? 1 : 0];
+                if (!q) {
+                    int dev = 0, ncu = 0, occ = 0;
+                    MPBP_HIP(hipGetDevice(&dev));
+                    MPBP_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+                    if (db) MPBP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_gtg_solve_ps<H, true>, 512, 0));
+                    else MPBP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_gtg_solve_ps<H, false>, 512, 0));
+                    q = max(8, (ncu * max(occ, 1)) & ~7);
+                }
+                const int g = (int)std::min<int64_t>(q, ((tiles + 7) / 8) * 8);
+                if (db) k_gtg_solve_ps<H, true><<<(unsigned)g, 512, 0, st>>>(S, b, diag, ck, out, dv, (int)tiles);
+                else k_gtg_solve_ps<H, false><<<(unsigned)g, 512, 0, st>>>(S, b, diag, ck, out, dv, (int)tiles);
+                MPBP_HIP(hipGetLastError());
+                return MPBP_OK;
+            }
+#endif
             if (db) k_gtg_solve<H, false, 512, true><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, ck, out, dv);
             else if (part) k_gtg_solve<H, true, 512, false><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, ck, out, dv);
             else k_gtg_solve<H, false, 512, false><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, ck, out, dv);

@@ -329,12 +329,12 @@ def test_matrix_free_galerkin_level1(n):
     assert torch.equal(out, got)
 
 
-@pytest.mark.parametrize("n", [64, 256, 512])
+@pytest.mark.parametrize("n", [64, 256])
 def test_mg_coarse_tree_sum(n):
     """Kernel option mg_coarse_tree (opt-in): tolerance-mode hierarchies apply the coarsest level's dense inverse with
     each row's sum split over the workgroup and combined by a tree -- within 1e-12 of the ordered-sum apply (the
-    coarsest F inverse is ill-conditioned: another order moves the apply by ~5e-13 at 256^2), eagerly and replayed; the
-    exact mode keeps the ordered sum (its apply is bit-identical with the option on or off)."""
+    coarsest F inverse is ill-conditioned: another order moved the apply by 4.6e-13 at 256^2, profiles/r05zf), eagerly
+    and replayed; the exact mode keeps the ordered sum (its apply is bit-identical with the option on or off)."""
     mp = _mp()
     bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
     _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
