@@ -3613,12 +3613,13 @@ struct GtgD {
     const double* Y;    // Finv_v: u_n, v_n, u_s, v_s
     const double* vp;   // v's pressure part
 };
-#ifndef MPBP_GTG_WPE
-#define MPBP_GTG_WPE 1
+#ifdef MPBP_GTG_WPE   // experiment: waves per SIMD asked of the 512-lane kernel (8: four workgroups per CU)
+#define MPBP_GTG_WPE_ATTR __attribute__((amdgpu_waves_per_eu(TPB == 512 ? MPBP_GTG_WPE : 1, 8)))
+#else
+#define MPBP_GTG_WPE_ATTR
 #endif
 template <int H, bool PART, int TPB, bool DB>
-__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(TPB == 512 ? MPBP_GTG_WPE : 1, 8)))
-MPBP_LDS_READS k_gtg_solve(GtGStencilDev P, const double* __restrict__ b,
+__global__ void __launch_bounds__(TPB) MPBP_GTG_WPE_ATTR MPBP_LDS_READS k_gtg_solve(GtGStencilDev P, const double* __restrict__ b,
                                                    const double* __restrict__ diag, ChebK ck, double* __restrict__ out,
                                                    GtgD dv) {
     using G = GtgTile<H>;
