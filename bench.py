@@ -196,6 +196,9 @@ def main():
                     help="N > 1: every rank forms the whole Gt_G / Gt_F_G (the default forms its own pressure rows)")
     ap.add_argument("--eager-partitioned", action="store_true",
                     help="N > 1: launch the partitioned apply eagerly instead of replaying its hipGraph")
+    ap.add_argument("--detail-json", default=None, metavar="PATH",
+                    help="also write the full record (every note and timing description) to PATH; stdout keeps the "
+                         "compact line")
     args = ap.parse_args()
 
     # --gpus N > 1 without a launcher: start the N ranks as a child process BEFORE anything touches the GPU
@@ -530,7 +533,10 @@ def main():
             "time_to_solution": time_to_solution(solve, n),
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
+        if args.detail_json:   # the verbose record (every note and timing description) beside the printed line
+            with open(args.detail_json, "w") as f:
+                json.dump(line, f, indent=1)
+        print(json.dumps(compact_line(line)), flush=True)
     if partitioned:
         pc.close()
         dist.destroy_process_group()
@@ -549,6 +555,95 @@ def time_to_solution(solve, n):
                                      "iterations": b["iterations"], "apply_ms": b.get("apply_ms"),
                                      "true_rel_residual": b.get("true_rel_residual")}
     return out or None
+
+
+def _r(x, nd=4):
+    """A float rounded to nd significant digits (the printed line's precision; the detail file keeps every digit)."""
+    if isinstance(x, float) and math.isfinite(x) and x != 0.0:
+        return float(f"{x:.{nd}g}")
+    return x
+
+
+def _roof(r, keep=()):
+    """A roofline object without its prose: the contract's fields plus the kernel, bytes and launch time."""
+    if not isinstance(r, dict):
+        return r
+    out = {k: _r(r[k]) if k in ("achieved", "frac", "avg_launch_us") else r[k]
+           for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "bytes_per_launch",
+                     "avg_launch_us", "launches_timed", "launches_per_apply", *keep) if k in r}
+    if isinstance(out.get("kernel"), str):   # the template instance and its one-line role, not the paragraph
+        out["kernel"] = out["kernel"].split(" (")[0]
+    if isinstance(out.get("traffic"), float):
+        out["traffic"] = round(out["traffic"])
+    return out
+
+
+def compact_line(line):
+    """The printed JSON line: the contract's keys first, every section without prose, null fields dropped, and
+    north_star's CSR SpMV target (roofline_csr_spmv) LAST -- so the whole line, and that object in any case, stays
+    inside the last 8 KB of stdout that the driver records.  --detail-json writes the full record."""
+    out = {k: v for k, v in line.items() if k not in (
+        "roofline", "roofline_second_f_solve", "spmv_A", "roofline_csr_spmv", "mg_apply", "host_buffer_matvec",
+        "solve_level", "time_to_solution", "cpu_baseline")}
+    cfg = dict(out.get("config") or {})
+    cfg.pop("before_timed_loop", None)
+    if isinstance(cfg.get("f_numerics"), str):
+        cfg["f_numerics"] = cfg["f_numerics"].split(" (")[0]
+    out["config"] = cfg
+    out["roofline"] = _roof(line.get("roofline"))
+    if line.get("roofline") and line["roofline"].get("timing"):
+        out["roofline"]["timing"] = "HIP events on the apply stream around each k_fsolve launch (eager pass, K applies)"
+    r2 = line.get("roofline_second_f_solve")
+    if isinstance(r2, dict) and r2.get("launches_timed"):
+        out["roofline_second_f_solve"] = {"frac": _r(r2["frac"]), "bytes_per_launch": r2["bytes_per_launch"],
+                                          "avg_launch_us": _r(r2["avg_launch_us"])}
+    out["cpu_baseline"] = line.get("cpu_baseline")
+    if isinstance(out["cpu_baseline"], dict):
+        cb = dict(out["cpu_baseline"])
+        if isinstance(cb.get("scipy"), dict):
+            cb["scipy"] = {k: _r(cb["scipy"][k]) for k in ("value", "rel_inf_vs_gpu") if k in cb["scipy"]}
+        cb["value"] = _r(cb["value"])
+        out["cpu_baseline"] = cb
+    mg = line.get("mg_apply")
+    if isinstance(mg, dict) and "error" not in mg:
+        out["mg_apply"] = {"value": _r(mg["value"]), "unit": mg["unit"], "ms_per_step": _r(mg["ms_per_step"]),
+                           "inner": "mg:1/mg:1", "f_numerics": mg.get("f_numerics"), "launch": mg.get("launch"),
+                           "setup_seconds": _r(mg.get("setup_seconds"), 3),
+                           "levels": f"{mg['levels_F'][0]}^2..{mg['levels_F'][-1]}^2",
+                           "roofline": _roof(mg.get("roofline"))}
+        if isinstance(mg.get("roofline_stored_level1"), dict):
+            s = mg["roofline_stored_level1"]
+            out["mg_apply"]["roofline_stored_level1"] = {"kernel": s["kernel"].split(" (")[0], "frac": _r(s["frac"]),
+                                                         "avg_launch_us": _r(s["avg_launch_us"])}
+    elif mg is not None:
+        out["mg_apply"] = mg
+    if isinstance(line.get("host_buffer_matvec"), dict):
+        out["host_buffer_matvec"] = {"value": _r(line["host_buffer_matvec"]["value"]), "unit": "applies/s",
+                                     "note": "host ndarray in and out over PCIe per call"}
+    sl = line.get("solve_level")
+    if isinstance(sl, dict) and sl.get("runs") is not None:
+        cols = ("n", "eta_n", "preconditioner", "iterations", "converged", "seconds", "apply_ms", "true_rel_residual")
+        out["solve_level"] = {"tol": sl["tol"], "maxiter": sl["maxiter"], "problem": "solve.py:52-80, x0 = 0",
+                              "f_numerics": sl.get("f_numerics"), "cols": list(cols),
+                              "runs": [[_r(r.get(c)) for c in cols] for r in sl["runs"]]}
+    tts = line.get("time_to_solution")
+    if isinstance(tts, dict):
+        out["time_to_solution"] = {k: {kk: _r(vv) for kk, vv in v.items() if vv is not None} for k, v in tts.items()}
+    sp, rc = line.get("spmv_A"), line.get("roofline_csr_spmv")
+    if isinstance(rc, dict):
+        cal = rc.get("same_run_stream") or {}
+        out["roofline_csr_spmv"] = {
+            **_roof(rc),
+            "back_to_back_us": _r(rc.get("back_to_back_us")), "frac_back_to_back": _r(rc.get("frac_back_to_back")),
+            "sell_frac": _r(sp["sell_gbs"] / HBM_PEAK_GBS) if isinstance(sp, dict) and "sell_gbs" in sp else None,
+            "same_run_stream": {"read_frac": _r(cal["read"]["frac_of_peak"]),
+                                "spmv_shape_frac": _r(cal["spmv_shape"]["frac_of_peak"]),
+                                "memory_clock": cal.get("memory_clock")} if cal else None,
+            "frac_of_measured_stream": _r(rc.get("frac_of_measured_stream")),
+            "timing": "HIP event pair around each of 20 launches"}
+    contract = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+                "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline")
+    return {k: v for k, v in out.items() if v is not None or k in contract}
 
 
 def _progress(rank, msg):

@@ -493,7 +493,10 @@ typedef struct mpbp_kernel_opts {
     int32_t mg_coarse_tree;    /* tolerance-mode hierarchies: the coarsest level's dense inverse applied with its row sums
                                   split over the workgroup and combined by a tree (1; default 0: another order of the
                                   ill-conditioned coarsest F inverse's sums moves the apply by ~5e-13) */
-    int32_t reserved[5];
+    int32_t f_solve_tile;      /* tolerance-mode whole F solves (k_fsolve): 0 the 64 x 8 tile, halo rings owned by the
+                                  first lanes; 1 (default) a 32 x 16 tile, each ring dealt out evenly over the four waves, the
+                                  rows' level-invariant terms computed once (k_fsolve_w).  Both compute the same bits */
+    int32_t reserved[4];
 } mpbp_kernel_opts;
 /* *out = the calling thread's current choices: its mpbp_kernel_opts_set_thread scope, else the process defaults. */
 void mpbp_kernel_opts_default(mpbp_kernel_opts* out);

@@ -85,7 +85,7 @@ class KernelOpts(Structure):
                 ("f_tile", c_int32), ("f_solve", c_int32), ("mg_galerkin_mf", c_int32), ("mg_galerkin_mf_p", c_int32),
                 ("pg_direct", c_int32), ("mg_group_rows", c_int32), ("mg_svl", c_int32), ("mg_mf_transfer", c_int32),
                 ("csr_table", c_int32), ("mg_fuse_l0", c_int32), ("mg_coarse_tree", c_int32),
-                ("reserved", c_int32 * 5)]
+                ("f_solve_tile", c_int32), ("reserved", c_int32 * 4)]
 
 
 def kernel_opts(overrides=None) -> KernelOpts:
@@ -101,6 +101,11 @@ def kernel_opts(overrides=None) -> KernelOpts:
     return o
 
 
+# every KernelOpts a kernel_options block has installed and not yet restored: the C thread-local pointer refers to the
+# struct, so it must outlive the block even when __exit__ never runs (an abandoned generator, a by-hand __enter__)
+_INSTALLED: list = []
+
+
 class kernel_options:
     """Context manager: kernel choices for this thread inside the block -- the current ones with `overrides` applied
     (mpbp_kernel_opts_set_thread): the plan-less entry points (mpbp_spmv, mpbp_f_stencil_*, mpbp_pg_stencil_*, ...)
@@ -110,13 +115,23 @@ class kernel_options:
     def __init__(self, **overrides):
         self.opts = kernel_opts(overrides)
         self._prev = ctypes.c_void_p()
+        self._active = False
 
     def __enter__(self):
+        if self._active:   # a second entry would overwrite _prev: the earlier choice could never be restored
+            raise RuntimeError("kernel_options: this block is already active (use a new instance to nest)")
         check(lib().mpbp_kernel_opts_set_thread(ctypes.byref(self.opts), ctypes.byref(self._prev)))
+        self._active = True
+        _INSTALLED.append(self.opts)
         return self.opts
 
     def __exit__(self, *exc):
         check(lib().mpbp_kernel_opts_set_thread(self._prev, None))
+        self._active = False
+        for i, o in enumerate(_INSTALLED):
+            if o is self.opts:
+                del _INSTALLED[i]
+                break
         return False
 
 

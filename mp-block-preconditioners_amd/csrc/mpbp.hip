@@ -28,7 +28,7 @@ mpbp_kernel_opts g_defaults = {
     /*march_rows*/ 0, /*init_diag*/ 1, /*f_pair*/ 1, /*f_direct*/ 0, /*gtg_fused*/ 1, /*gtg_tpb*/ 512, /*gtg_drhs*/ 1,
     /*q13_sym*/ 1, /*f_tile*/ 1, /*f_solve*/ 1, /*mg_galerkin_mf*/ 2, /*mg_galerkin_mf_p*/ 1, /*pg_direct*/ 1,
     /*mg_group_rows*/ 65536, /*mg_svl*/ 1, /*mg_mf_transfer*/ 1, /*csr_table*/ 1, /*mg_fuse_l0*/ 1,
-    /*mg_coarse_tree*/ 0, {0, 0, 0, 0, 0}};
+    /*mg_coarse_tree*/ 0, /*f_solve_tile*/ 1, {0, 0, 0, 0}};
 thread_local const mpbp_kernel_opts* t_opts = nullptr;
 inline const mpbp_kernel_opts& KO() { return t_opts ? *t_opts : g_defaults; }
 struct OptsScope {   // installs a plan's kernel choices (when it has its own) for one entry-point call
@@ -44,6 +44,7 @@ int set_error(int code, const char* fmt, ...);
 inline int check_opts(const mpbp_kernel_opts* o, const char* who) {
     if (!o) return MPBP_OK;
     const bool ok = o->march_rows >= 0 && o->march_rows <= 4096 && (o->gtg_tpb == 256 || o->gtg_tpb == 512) &&
+                    o->f_solve_tile >= 0 && o->f_solve_tile <= 1 &&
                     o->mg_galerkin_mf >= 0 && o->mg_galerkin_mf <= 2 && o->mg_group_rows >= 0 &&
                     (o->init_diag | o->f_pair | o->f_direct | o->gtg_fused | o->gtg_drhs | o->q13_sym | o->f_tile |
                      o->f_solve | o->mg_galerkin_mf_p | o->pg_direct | o->mg_svl | o->mg_mf_transfer | o->csr_table |
@@ -1897,6 +1898,38 @@ struct FStencilFast : FStencilDev {
         return k;
     }
     __device__ double aco(int p) const { return d_u * (p ? eta_s : eta_n) * idx2; }
+    // a cell's level-invariant row terms beside Co: the identity weights c thn_p at its u / v face, per phase
+    struct W4 { double wu[2], wv[2]; };
+    __device__ W4 weights(const Cell& cl) const {
+        return {{c * cl.face[0], c * (1.0 - cl.face[0])}, {c * cl.face[1], c * (1.0 - cl.face[1])}};
+    }
+    // the four rows (u_n, v_n, u_s, v_s) of cell (gr, gc) from its coefficients k and weights w (rows4's arithmetic)
+    template <class XA>
+    __device__ void rows4_co(int gr, int gc, const Co& k, const W4& w, const XA& xa, double* acc) const {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int fu = 2 * p, fv = 2 * p + 1;
+            auto ph = [&](double t) { return p ? 1.0 - t : t; };
+            const double a = aco(p);
+            const double A1 = ph(k.w), A2 = ph(k.c), B1 = ph(k.nn), KC = ph(k.kc), KS = ph(k.ks), KE = ph(k.ke);
+            const double uC = xa.X(fu, gr, gc), uN = xa.X(fu, gr - 1, gc), uS = xa.X(fu, gr + 1, gc);
+            const double uW = xa.X(fu, gr, gc - 1), uE = xa.X(fu, gr, gc + 1), uNE = xa.X(fu, gr - 1, gc + 1);
+            const double vC = xa.X(fv, gr, gc), vN = xa.X(fv, gr - 1, gc), vS = xa.X(fv, gr + 1, gc);
+            const double vW = xa.X(fv, gr, gc - 1), vE = xa.X(fv, gr, gc + 1), vSW = xa.X(fv, gr + 1, gc - 1);
+            const double uo = xa.X(fu ^ 2, gr, gc), vo = xa.X(fv ^ 2, gr, gc);
+            const double tn = (uN - uC) + (vC - vW), tc = (uE - uC) + (vS - vC);
+            double br = KC * tn;
+            br = __builtin_fma(A1, (uW - uC) + (vW - vSW), br);
+            br = __builtin_fma(A2, tc, br);
+            br = __builtin_fma(KS, (uS - uC) + (vSW - vS), br);
+            acc[fu] = __builtin_fma(a, br, __builtin_fma(w.wu[p], uC, k.xu * (uC - uo)));
+            double bv = B1 * ((vN - vC) + (uN - uNE));
+            bv = __builtin_fma(KC, -tn, bv);
+            bv = __builtin_fma(KE, (vE - vC) + (uNE - uE), bv);
+            bv = __builtin_fma(A2, tc, bv);
+            acc[fv] = __builtin_fma(a, bv, __builtin_fma(w.wv[p], vC, k.xv * (vC - vo)));
+        }
+    }
     // the four rows (u_n, v_n, u_s, v_s) of cell (gr, gc) and their reciprocal diagonals
     // RD = false: the diagonals are the caller's (k_ftile level B reuses level A's, computed by the same operations)
     template <bool RD = true, class TA, class XA>
@@ -1934,6 +1967,17 @@ struct FStencilFast : FStencilDev {
             acc[fv] = __builtin_fma(a, bv, __builtin_fma(wv, vC, k.xv * (vC - vo)));
             if constexpr (RD)
                 rd[fv] = rcp_nr(__builtin_fma(-a, (B1 + A2) + (KC + KE), wv + k.xv));
+        }
+    }
+    // the reciprocal diagonals from a cell's coefficients and weights (rdiag4's arithmetic)
+    __device__ void rdiag4_co(const Co& k, const W4& w, double* rd) const {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            auto ph = [&](double t) { return p ? 1.0 - t : t; };
+            const double a = aco(p);
+            const double A1 = ph(k.w), A2 = ph(k.c), B1 = ph(k.nn), KC = ph(k.kc), KS = ph(k.ks), KE = ph(k.ke);
+            rd[2 * p] = rcp_nr(__builtin_fma(-a, (A1 + A2) + (KC + KS), w.wu[p] + k.xu));
+            rd[2 * p + 1] = rcp_nr(__builtin_fma(-a, (B1 + A2) + (KC + KE), w.wv[p] + k.xv));
         }
     }
     // the reciprocal diagonals of the four rows at a staged point (k_march_init: x0 = c2 b / diag)
@@ -3281,6 +3325,275 @@ int launch_fsolve_t(const FStencilFast& P, const FSolve& a, hipStream_t st, cons
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
+// ---- k_fsolve on narrower tiles with the halo rings spread evenly over the waves (kernel option f_solve_tile) ----
+// The same whole-solve launch as k_fsolve, the same operations per cell and level (bit-identical), on a TW x TH tile
+// (32 x 16: 10 % fewer cell-levels than 64 x 8 -- 2 680 instead of 2 968 per 512 outputs at H = 3 -- because the
+// halo rings are shorter).  A level's time is set by the wave with the most owned cells it updates, so ring r's cells
+// are dealt out in four equal contiguous runs, one per wave: rings 1 .. H - 1 share one slot (lanes 0 .. 51 of every
+// wave at 32 x 16, H = 3), ring H (x0 only) a second.  Per wave and level: x0 on 4 cells (k_fsolve 64 x 8: 5), then
+// 3, 3, 2 stencil cells (4, 3, 2), and three cells' state in registers instead of four.  The level-invariant part of
+// the rows is computed once: the node averages K(r, c) into an LDS table (FStencilFast::coeffs' kc / ks / ke are
+// K(r, c), K(r + 1, c), K(r, c + 1), the same sums in the same order), and each owned cell keeps its XI couplings and
+// identity weights in registers (in place of its two face values), so a level reads 6 coefficients instead of 8
+// thn values and skips ~27 of the row's ~115 fp64 operations.  (An in-place variant -- one x image, a second barrier
+// per level, 34 KB of LDS for three workgroups per CU -- spilled ~700 B per lane at the 168-VGPR cap and ran 4.5x
+// slower: removed.)
+template <int TW, int TH, int H>
+struct FsGeom {
+    static constexpr int RW = TW + 2 * H, RH = TH + 2 * H, N = RW * RH;   // x levels: the tile + H
+    static constexpr int TSW = RW + 2, TSH = RH + 2, TSN = TSW * TSH;     // thn: the tile + H + 1
+    static constexpr int NT = TW * TH / 256;                             // tile cells per lane
+    static constexpr int ring(int r) { return 2 * TW + 2 * TH + 8 * r - 4; }
+    static constexpr int q(int r) { return ring(r) / 4; }               // ring r's cells per wave
+    static constexpr int qa() {                                          // slot A: rings 1 .. H - 1, per wave
+        int s = 0;
+        for (int r = 1; r < H; ++r) s += q(r);
+        return s;
+    }
+};
+template <int TW, int TH>
+__device__ inline void fs_ring_cell_t(int r, int j, int r0, int c0, int& vr, int& vc) {
+    const int w = TW + 2 * r;
+    if (j < 2 * w) {
+        vr = j < w ? r0 - r : r0 + TH - 1 + r;
+        vc = c0 - r + (j < w ? j : j - w);
+    } else {
+        const int k = j - 2 * w;
+        vr = r0 - r + 1 + (k >> 1);
+        vc = (k & 1) ? c0 + TW - 1 + r : c0 - r;
+    }
+}
+template <int TW, int TH, int H, bool SUB, bool PART, class BS>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) MPBP_LDS_READS
+k_fsolve_w(FStencilFast P, FSolve a, BS bs) {
+    using T = FsGeom<TW, TH, H>;
+    static_assert(TW * TH == 256 * T::NT && TW % 32 == 0, "whole rows of 32 lanes, NT cells per lane");
+    static_assert((2 * TW + 2 * TH - 4) % 4 == 0, "every ring splits into four equal runs");
+    static_assert(T::qa() <= 64 && T::q(H) <= 64, "one ring slot for rings 1 .. H - 1 and one for ring H");
+    constexpr int NT = T::NT;
+    constexpr int NSL = NT + 2;   // owned cells per lane: NT tile cells, slot A (rings 1 .. H - 1), slot B (ring H)
+    constexpr int NS = NT + 1;    // ... with updates after x0 (ring H only needs x0)
+    constexpr int PW = T::RW + 1, PN = PW * (T::RH + 1);   // BS: x_p over the tile + H, + its west / north neighbours
+    constexpr int KW = T::RW + 1, KN = KW * (T::RH + 1);   // node averages K(r, c) of the tile + H, + 1 row / column
+    __shared__ double ts[T::TSN];
+    __shared__ double kt[KN];
+    __shared__ double xa[4 * T::N], xb[4 * T::N];
+    __shared__ double ps[BS::on ? PN : 1];
+    const int n = P.n, nn = n * n;
+    const int tx = (n + TW - 1) / TW;
+    const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int lo = PART ? P.r0 - P.ext : 0, hi = PART ? P.r0 + P.L + P.ext : n;   // output rows [lo, hi)
+    const int r0 = lo + (bk / tx) * TH, c0 = (bk % tx) * TW;
+    const int rbt = r0 - H - 1, cbt = c0 - H - 1, rb = r0 - H, cb = c0 - H;
+    const int tid = threadIdx.x;
+    auto in_row = [&](int vr, int h) {
+        if constexpr (PART) {
+            const int lr = vr - P.r0;
+            return lr < -h ? -h : (lr >= P.L + h ? P.L + h - 1 : lr);
+        } else {
+            return P.wrap(vr);
+        }
+    };
+    {
+        constexpr int IT = (T::TSN + 255) / 256;
+        double v[IT];
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256;
+            if (i < T::TSN) {
+                const int sr = i / T::TSW, sc = i - sr * T::TSW;
+                v[it] = P.cell[P.wrap(rbt + sr) * n + P.wrap(cbt + sc)];
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256;
+            if (i < T::TSN) ts[i] = v[it];
+        }
+    }
+    if constexpr (BS::on) {
+        constexpr int IT = (PN + 255) / 256;
+        double v[IT];
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256;
+            if (i < PN) {
+                const int sr = i / PW, sc = i - sr * PW;
+                const int pr = in_row(rb - 1 + sr, PART ? bs.h : 0);
+                v[it] = bs.xp[(PART ? ext_row(1, 0, pr, P.L, bs.h, n) : pr * n) + P.wrap(cb - 1 + sc)];
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = tid + it * 256;
+            if (i < PN) ps[i] = v[it];
+        }
+    }
+    const int lane = tid & 63, wv = tid >> 6;
+    int cr[NSL], cc[NSL], rr[NSL];
+    bool own[NSL];
+#pragma unroll
+    for (int m = 0; m < NT; ++m) {   // tile cell m: row (tid / TW) + m (256 / TW), column tid % TW
+        cr[m] = r0 + tid / TW + m * (256 / TW); cc[m] = c0 + tid % TW; own[m] = true; rr[m] = 0;
+    }
+    {   // slot A: rings 1 .. H - 1 in consecutive lane ranges; slot B: ring H
+        int r = 0, j = 0, base = 0;
+#pragma unroll
+        for (int q = 1; q < H; ++q) {
+            if (r == 0 && lane < base + T::q(q)) {
+                r = q;
+                j = wv * T::q(q) + lane - base;
+            }
+            base += T::q(q);
+        }
+        own[NT] = r != 0;
+        rr[NT] = r;
+        fs_ring_cell_t<TW, TH>(r ? r : 1, j, r0, c0, cr[NT], cc[NT]);
+        own[NT + 1] = lane < T::q(H);
+        rr[NT + 1] = H;
+        fs_ring_cell_t<TW, TH>(H, own[NT + 1] ? wv * T::q(H) + lane : 0, r0, c0, cr[NT + 1], cc[NT + 1]);
+    }
+    double fl[NSL][2], bl[BS::on ? 1 : NSL][4];
+#pragma unroll
+    for (int sl = 0; sl < NSL; ++sl) {
+        if (!own[sl]) continue;
+        const int gr = P.wrap(cr[sl]), gc = P.wrap(cc[sl]);
+        const int32_t k = gr * n + gc;
+        fl[sl][0] = P.uface[k];
+        fl[sl][1] = P.vface[k];
+        if constexpr (!BS::on) {
+            const int br = in_row(cr[sl], P.h);
+#pragma unroll
+            for (int f = 0; f < 4; ++f) bl[sl][f] = a.b[(PART ? ext_row(4, f, br, P.L, P.h, n) : (f * n + br) * n) + gc];
+        }
+    }
+    __syncthreads();
+    const TTileT<T::TSW> tt{ts, rbt, cbt};
+    // the node averages every level reads (FStencilFast::coeffs' kc of cell (r, c), ks of (r - 1, c), ke of (r, c - 1):
+    // the same sum in the same order), computed once; first read after level 1's barrier
+    {
+        constexpr int IK = (KN + 255) / 256;
+#pragma unroll
+        for (int it = 0; it < IK; ++it) {
+            const int i = tid + it * 256;
+            if (i < KN) {
+                const int r = rb + i / KW, c = cb + i % KW;
+                kt[i] = 0.25 * ((tt.T(0, r - 1, c - 1) + tt.T(0, r - 1, c)) + (tt.T(0, r, c - 1) + tt.T(0, r, c)));
+            }
+        }
+    }
+    // per owned cell: d, its reciprocal diagonals, b, and the level-invariant row terms (XI couplings xu / xv, weights)
+    double d[NS][4], rd[NS][4], bv[NS][4], kx[NS][2];
+    typename FStencilFast::W4 wt[NS];
+    // level 0: x0 = d0 = c2_0 b / diag over the tile + H
+#pragma unroll
+    for (int sl = 0; sl < NSL; ++sl) {
+        if (!own[sl]) continue;
+        const int vr = cr[sl], vc = cc[sl];
+        const int gr = P.wrap(vr), gc = P.wrap(vc);
+        const FStencilDev::Cell cl{{fl[sl][0], fl[sl][1]}};
+        const typename FStencilFast::Co k = P.coeffs(P.nb(tt, vr, vc));
+        const typename FStencilFast::W4 w = P.weights(cl);
+        double b4[4], r4[4];
+        P.rdiag4_co(k, w, r4);
+        if constexpr (BS::on) {
+            const int pi = (vr - rb + 1) * PW + (vc - cb + 1);
+            const typename BS::Q q{ps[pi], ps[pi - 1], ps[pi - PW]};
+#pragma unroll
+            for (int f = 0; f < 4; ++f) b4[f] = bs.b_at(f, vr, vc, gc == 0, gr == 0, tt, q);
+        } else {
+#pragma unroll
+            for (int f = 0; f < 4; ++f) b4[f] = bl[sl][f];
+        }
+        const int si = (vr - rb) * T::RW + (vc - cb);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            const double x0 = a.c2_0 * b4[f] * r4[f];
+            xa[f * T::N + si] = x0;
+            if (sl < NS) {
+                d[sl][f] = x0;
+                rd[sl][f] = r4[f];
+                bv[sl][f] = b4[f];
+            }
+        }
+        if (sl < NS) {
+            kx[sl][0] = k.xu;
+            kx[sl][1] = k.xv;
+            wt[sl] = w;
+        }
+    }
+    double* cur = xa;
+    double* nxt = xb;
+    double sv[NT][4];
+#pragma unroll
+    for (int l = 1; l <= H; ++l) {
+        __syncthreads();
+        const XTileT<T::RW, T::RH> xt{cur, rb, cb};
+        const double c1 = a.c1[l - 1], c2 = a.c2[l - 1];
+        if constexpr (SUB) {
+            if (l == H) {
+#pragma unroll
+                for (int m = 0; m < NT; ++m) {
+                    const int vr = cr[m], vc = cc[m];
+                    if (vr >= hi || vc >= n) continue;
+#pragma unroll
+                    for (int f = 0; f < 4; ++f)
+                        sv[m][f] = a.sub[PART ? P.out_row(f, vr - P.r0, vc) : f * nn + vr * n + vc];
+                }
+            }
+        }
+#pragma unroll
+        for (int sl = 0; sl < NS; ++sl) {
+            if (sl >= NT && (!own[sl] || rr[sl] > H - l)) continue;   // ring r lives through level H - r
+            const int vr = cr[sl], vc = cc[sl];
+            if (l == H && (vr >= hi || vc >= n)) continue;            // a tile past the last row / column
+            typename FStencilFast::Co k;
+            k.w = tt.T(0, vr, vc - 1);
+            k.c = tt.T(0, vr, vc);
+            k.nn = tt.T(0, vr - 1, vc);
+            const int ki = (vr - rb) * KW + (vc - cb);
+            k.kc = kt[ki];
+            k.ks = kt[ki + KW];
+            k.ke = kt[ki + 1];
+            k.xu = kx[sl][0];
+            k.xv = kx[sl][1];
+            double acc[4];
+            P.rows4_co(vr, vc, k, wt[sl], xt, acc);
+            const int si = (vr - rb) * T::RW + (vc - cb);
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                const double z = (bv[sl][f] - acc[f]) * rd[sl][f];
+                const double dn = c1 * d[sl][f] + c2 * z;
+                if (l < H) {
+                    nxt[f * T::N + si] = cur[f * T::N + si] + dn;
+                    d[sl][f] = dn;
+                } else {
+                    const double x = cur[f * T::N + si] + dn;
+                    const int32_t o = PART ? P.out_row(f, vr - P.r0, vc) : f * nn + vr * n + vc;
+                    if constexpr (SUB) a.x_out[o] = sv[sl < NT ? sl : 0][f] - x;
+                    else a.x_out[o] = x;
+                }
+            }
+        }
+        double* t = cur;
+        cur = nxt;
+        nxt = t;
+    }
+}
+// Grids the narrow tile's staged thn (tile + H + 1 each side) wraps onto at most once.
+template <int TW, int TH, int H>
+inline bool fsolve_w_ok_n(int n) { return n >= FsGeom<TW, TH, H>::TSW && n >= FsGeom<TW, TH, H>::TSH; }
+template <int H, bool PART, class BS>
+int launch_fsolve_w(const FStencilFast& P, const FSolve& a, hipStream_t st, const BS& bs) {
+    constexpr int TW = 32, TH = 16;
+    const int rows = PART ? P.L + 2 * P.ext : P.n;
+    const int64_t tiles = (int64_t)((P.n + TW - 1) / TW) * ((rows + TH - 1) / TH);
+    if (a.sub) k_fsolve_w<TW, TH, H, true, PART, BS><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
+    else k_fsolve_w<TW, TH, H, false, PART, BS><<<(unsigned)tiles, 256, 0, st>>>(P, a, bs);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
 // K = 3 or 4 Chebyshev updates (x0 and H = K - 1 stencil sweeps); columns wrap at most once per tile.
 inline bool fsolve_ok(int K, int n) { return (K == 3 && fsolve_ok_n<2>(n)) || (K == 4 && fsolve_ok_n<3>(n)); }
 // One GPU, whole grid (P.h == 0), or a row partition's owned rows + P.ext ghost rows (P.which == 3), b's ghost depth
@@ -3305,6 +3618,16 @@ int launch_fsolve(const FStencilDev& Pd, int K, const double* c1, const double* 
         a.c2[l - 1] = c2[l];
     }
     constexpr bool bpart = BS::on && BS::part;   // GxBPart launches only the partitioned kernel, GxB the other
+    if (KO().f_solve_tile) {   // 32 x 16 tiles, rings spread over the waves, level-invariant terms cached
+        if (!(K == 3 ? fsolve_w_ok_n<32, 16, 2>(P.n) : fsolve_w_ok_n<32, 16, 3>(P.n)))
+            return set_error(MPBP_ERR_ARG, "fsolve: grid smaller than the 32 x 16 tile's staging");
+        if constexpr (BS::on) {
+            return K == 3 ? launch_fsolve_w<2, bpart>(P, a, st, bs) : launch_fsolve_w<3, bpart>(P, a, st, bs);
+        } else {
+            if (part) return K == 3 ? launch_fsolve_w<2, true>(P, a, st, bs) : launch_fsolve_w<3, true>(P, a, st, bs);
+            return K == 3 ? launch_fsolve_w<2, false>(P, a, st, bs) : launch_fsolve_w<3, false>(P, a, st, bs);
+        }
+    }
     if constexpr (BS::on) {
         return K == 3 ? launch_fsolve_t<2, bpart>(P, a, st, bs) : launch_fsolve_t<3, bpart>(P, a, st, bs);
     } else {
@@ -3613,13 +3936,8 @@ struct GtgD {
     const double* Y;    // Finv_v: u_n, v_n, u_s, v_s
     const double* vp;   // v's pressure part
 };
-#ifdef MPBP_GTG_WPE   // experiment: waves per SIMD asked of the 512-lane kernel (8: four workgroups per CU)
-#define MPBP_GTG_WPE_ATTR __attribute__((amdgpu_waves_per_eu(TPB == 512 ? MPBP_GTG_WPE : 1, 8)))
-#else
-#define MPBP_GTG_WPE_ATTR
-#endif
 template <int H, bool PART, int TPB, bool DB>
-__global__ void __launch_bounds__(TPB) MPBP_GTG_WPE_ATTR MPBP_LDS_READS k_gtg_solve(GtGStencilDev P, const double* __restrict__ b,
+__global__ void __launch_bounds__(TPB) MPBP_LDS_READS k_gtg_solve(GtGStencilDev P, const double* __restrict__ b,
                                                    const double* __restrict__ diag, ChebK ck, double* __restrict__ out,
                                                    GtgD dv) {
     using G = GtgTile<H>;
@@ -3810,180 +4128,6 @@ __global__ void __launch_bounds__(TPB) MPBP_GTG_WPE_ATTR MPBP_LDS_READS k_gtg_so
     }
 }
 
-#if MPBP_GTG_PS
-// Experiment: k_gtg_solve (512 lanes, one GPU) as a persistent loop over tiles -- each workgroup walks its XCD's run of
-// tiles and issues the next tile's global loads (b, thn, diag; DB: thn, Y, v_p, diag) right after staging the current
-// one, so their latency hides behind the current tile's levels instead of opening every tile.  Same operations per
-// tile as k_gtg_solve (bit-identical).
-#ifndef MPBP_GTG_PS_WPE
-#define MPBP_GTG_PS_WPE 1
-#endif
-template <int H, bool DB>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MPBP_GTG_PS_WPE, 8))) MPBP_LDS_READS
-k_gtg_solve_ps(GtGStencilDev P, const double* __restrict__ b,
-                                                                    const double* __restrict__ diag, ChebK ck,
-                                                                    double* __restrict__ out, GtgD dv, int ntiles) {
-    constexpr int TPB = 512;
-    using G = GtgTile<H>;
-    constexpr int TW = DB ? G::RW + 2 : G::RW, TN = DB ? TW * (G::RH + 2) : G::N;
-    static_assert(140 * (H - 1) + 4 * H * (H - 1) <= 512, "512 lanes own at most one ring cell each");
-    __shared__ double ts[TN], bs[G::N], xa[G::N], xb[G::N];
-    const int n = P.n, nn = n * n;
-    const int tx = (n + kGTW - 1) / kGTW;
-    const int tid = threadIdx.x;
-    // this workgroup's tiles: XCD x = blockIdx % 8 owns the x-th eighth of the tiles, its workgroups take turns
-    const int per = (ntiles + 7) / 8, xcd = blockIdx.x & 7, nbx = (int)gridDim.x >> 3;
-    const int tend = min(ntiles, (xcd + 1) * per);
-    int tile = xcd * per + (int)(blockIdx.x >> 3);
-    constexpr int IT = (G::N + TPB - 1) / TPB, ITT = (TN + TPB - 1) / TPB;
-    double tv[ITT], bv[DB ? 1 : IT], dgl[IT], vpl[DB ? IT : 1], yl[DB ? IT : 1][8];
-    auto load = [&](int tl) {
-        const int r0 = (tl / tx) * kGTH, c0 = (tl % tx) * kGTW, rb = r0 - H, cb = c0 - H;
-#pragma unroll
-        for (int it = 0; it < ITT; ++it) {
-            const int i = tid + it * TPB;
-            if (i < TN) {
-                const int rr = i / TW, cc = i - rr * TW;
-                tv[it] = DB ? P.cell[P.wrap(rb - 1 + rr) * n + P.wrap(cb - 1 + cc)]
-                            : P.cell[P.wrap(rb + rr) * n + P.wrap(cb + cc)];
-            }
-        }
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int i = tid + it * TPB;
-            if (i >= G::N) break;
-            const int rr = i / G::RW, cc = i - rr * G::RW;
-            const int gr = P.wrap(rb + rr), gc = P.wrap(cb + cc);
-            const int32_t k = gr * n + gc;
-            if constexpr (DB) {
-                const int ge = gc == n - 1 ? 0 : gc + 1, gs = gr == n - 1 ? 0 : gr + 1;
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    yl[it][4 * q + 0] = dv.Y[2 * q * nn + gr * n + ge];
-                    yl[it][4 * q + 1] = dv.Y[2 * q * nn + k];
-                    yl[it][4 * q + 2] = dv.Y[(2 * q + 1) * nn + k];
-                    yl[it][4 * q + 3] = dv.Y[(2 * q + 1) * nn + gs * n + gc];
-                }
-                vpl[it] = dv.vp[k];
-            } else {
-                bv[it] = b[k];
-            }
-            dgl[it] = diag[k];
-        }
-    };
-    if (tile < tend) load(tile);
-    for (; tile < tend; tile += nbx) {
-        const int r0 = (tile / tx) * kGTH, c0 = (tile % tx) * kGTW;
-        const int rb = r0 - H, cb = c0 - H;
-        __syncthreads();   // the previous tile's levels have read the buffers
-#pragma unroll
-        for (int it = 0; it < ITT; ++it)
-            if (tid + it * TPB < TN) ts[tid + it * TPB] = tv[it];
-        if constexpr (DB) {
-            __syncthreads();
-            const TTileT<TW> tD{ts, rb - 1, cb - 1};
-#pragma unroll
-            for (int it = 0; it < IT; ++it) {
-                const int i = tid + it * TPB;
-                if (i >= G::N) break;
-                const int rr = i / G::RW, cc = i - rr * G::RW;
-                const int vr = rb + rr, vc = cb + cc, gr = P.wrap(vr), gc = P.wrap(vc);
-                const double* yv = yl[it];
-                const bool lastc = gc == n - 1, lastr = gr == n - 1;
-                double acc = 0.0;
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const double t0 = tD.T(q, vr, vc), tE = tD.T(q, vr, vc + 1), tWv = tD.T(q, vr, vc - 1);
-                    const double tN = tD.T(q, vr - 1, vc), tS = tD.T(q, vr + 1, vc);
-                    const double uE = (P.inv * (0.5 * (t0 + tE))) * yv[4 * q + 0];
-                    const double uC = (P.minv * (0.5 * (t0 + tWv))) * yv[4 * q + 1];
-                    const double vC = (P.inv * (0.5 * (t0 + tN))) * yv[4 * q + 2];
-                    const double vS = (P.minv * (0.5 * (t0 + tS))) * yv[4 * q + 3];
-                    acc += lastc ? uE : uC;
-                    acc += lastc ? uC : uE;
-                    acc += lastr ? vS : vC;
-                    acc += lastr ? vC : vS;
-                }
-                const double bvv = acc + vpl[it];
-                bs[i] = bvv;
-                xa[i] = ck.c2[0] * (bvv / dgl[it]);
-            }
-        } else {
-#pragma unroll
-            for (int it = 0; it < IT; ++it) {
-                const int i = tid + it * TPB;
-                if (i < G::N) {
-                    bs[i] = bv[it];
-                    xa[i] = ck.c2[0] * (bv[it] / dgl[it]);
-                }
-            }
-        }
-        __syncthreads();
-        if (tile + nbx < tend) load(tile + nbx);   // the next tile's operands, in flight under this tile's levels
-        const TTileT<TW> ta{ts, DB ? rb - 1 : rb, DB ? cb - 1 : cb};
-        const int lr = tid >> 6, lc = tid & 63;
-        int cr[2], cc[2], si[2], rr[2];
-        bool own[2], edge[2];
-        double e[2][5], bo[2], d[2];
-        cr[0] = r0 + lr; cc[0] = c0 + lc; own[0] = true; rr[0] = 0;
-        {
-            int r = 0, j = tid;
-#pragma unroll
-            for (int q = 1; q < H; ++q)
-                if (r == 0) {
-                    if (j < 140 + 8 * q) r = q;
-                    else j -= 140 + 8 * q;
-                }
-            own[1] = r != 0;
-            rr[1] = r;
-            fs_ring_cell(r ? r : 1, r ? j : 0, r0, c0, cr[1], cc[1]);
-        }
-#pragma unroll
-        for (int sl = 0; sl < 2; ++sl) {
-            const int vr = cr[sl], vc = cc[sl], gr = P.wrap(vr), gc = P.wrap(vc);
-            si[sl] = (vr - rb) * G::RW + (vc - cb);
-            edge[sl] = __builtin_amdgcn_readfirstlane(__any(own[sl] && (gr == 0 || gr == n - 1 || gc == 0 ||
-                                                                        gc == n - 1))) != 0;
-            if (own[sl]) {
-                P.entries(vr, vc, gr, gc, ta, e[sl]);
-                bo[sl] = bs[si[sl]];
-                d[sl] = xa[si[sl]];
-            }
-        }
-        double* cur = xa;
-        double* nxt = xb;
-#pragma unroll
-        for (int l = 1; l <= H; ++l) {
-            if (l > 1) __syncthreads();
-            const double c1 = ck.c1[l], c2 = ck.c2[l];
-#pragma unroll
-            for (int sl = 0; sl < 2; ++sl) {
-                if (sl >= 1 && (!own[sl] || rr[sl] > H - l)) continue;
-                const int vr = cr[sl], vc = cc[sl];
-                if (l == H && (vr >= n || vc >= n)) continue;
-                const int i = si[sl];
-                const double p[5] = {e[sl][0] * cur[i - G::RW], e[sl][1] * cur[i - 1], e[sl][2] * cur[i],
-                                     e[sl][3] * cur[i + 1], e[sl][4] * cur[i + G::RW]};
-                const int gr = P.wrap(vr), gc = P.wrap(vc);
-                const Wrap wr{gr == 0, gr == n - 1, gc == 0, gc == n - 1};
-                const double acc = edge[sl] ? add5<true>(0.0, p, wr) : add5<false>(0.0, p, wr);
-                const double z = (bo[sl] - acc) / e[sl][2];
-                const double dn = c1 * d[sl] + c2 * z;
-                const double x = cur[i] + dn;
-                if (l < H) {
-                    nxt[i] = x;
-                    d[sl] = dn;
-                } else {
-                    out[vr * n + vc] = x;
-                }
-            }
-            double* t = cur;
-            cur = nxt;
-            nxt = t;
-        }
-    }
-}
-#endif
 
 // ---- multigrid level 0 of the pressure hierarchy (matrix-free Gt_G): descent and ascent in one launch each ----
 // k_gpre: x0 = c2_0 (b / diag) over the tile + 3, the Chebyshev sweep x1 over the tile + 2 (written on the tile), the
@@ -4311,18 +4455,6 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
         for (int it = 0; it < IT; ++it)
             if (tid + it * 256 < PN) ts[tid + it * 256] = vt[it];
     }
-#if MPBP_GAL_PREPE
-    // experiment: the epilogue's operands of this lane's two coarse rows loaded here, behind the three stages
-    typename Epi::P pe2[2] = {};
-    if constexpr (MAC) {
-        const int cell = tid & (kG1W * kG1H - 1), fp = tid >> 7;
-        const int cr = cr0 + cell / kG1W, cc = cc0 + cell % kG1W;
-        if (cr < nc && cc < nc) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) pe2[h] = epi.pre((fp + 2 * h) * ncc + cr * nc + cc);
-        }
-    }
-#endif
     // the faces of this lane's t1 cells, loaded ahead (their latency behind the P_0 stage, not in the F stage)
     constexpr int IF = (FN + 255) / 256;
     double fu[IF], fv[IF];
@@ -4401,11 +4533,7 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
             for (int h = 0; h < 2; ++h) {
                 const int f = fp + 2 * h;
                 const int32_t row = f * ncc + cr * nc + cc;
-#if MPBP_GAL_PREPE
-                const typename Epi::P pe = pe2[h];
-#else
                 const typename Epi::P pe = epi.pre(row);
-#endif
                 double acc;
                 if constexpr (INNER)
                     acc = fp ? g1_r_in<MPBP_MG_NODE, MPBP_MG_CELL>(t1 + f * FN, cr - cr0, cc - cc0)
@@ -4651,13 +4779,6 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, X
     }
     __syncthreads();
     const bool inner = g1_inner(cr0, cc0, kG1PH2, kG1W, nc);   // (k_gal1's g1_*_in)
-#if MPBP_GAL_PREPE
-    typename Epi::P pe1{};
-    {
-        const int cr = cr0 + tid / kG1W, cc = cc0 + tid % kG1W;
-        if (cr < nc && cc < nc) pe1 = epi.pre(cr * nc + cc);
-    }
-#endif
     for (int i = tid; i < PN; i += 256) {   // t0 = P_0 x on the fine block + 2
         const int r = i / kG1PW, c = i - r * kG1PW;
         t0[i] = inner ? g1_p_in<MPBP_MG_CELL, MPBP_MG_CELL>(xs, r, c)
@@ -4697,11 +4818,7 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, X
         const int cr = cr0 + tid / kG1W, cc = cc0 + tid % kG1W;
         if (cr < nc && cc < nc) {
             const int32_t row = cr * nc + cc;
-#if MPBP_GAL_PREPE
-            const typename Epi::P pe = pe1;
-#else
             const typename Epi::P pe = epi.pre(row);
-#endif
             epi(row, inner ? g1_r_in<MPBP_MG_CELL, MPBP_MG_CELL>(t1, cr - cr0, cc - cc0)
                            : g1_r<MPBP_MG_CELL, MPBP_MG_CELL>(t1, cr, cc, n, fr0 - 1, fc0 - 1), pe);
         }
@@ -7192,25 +7309,6 @@ int launch_gtg_solve_t(const GtGStencilDev& S, const double* b, const double* di
     // 512 lanes own rings 1 .. H - 1 one cell each (140 (H - 1) + 4 H (H - 1) <= 512 cells): H <= 4
     if constexpr (H <= 4) {
         if (KO().gtg_tpb == 512) {
-#if MPBP_GTG_PS
-            if (!part) {
-                static int nb[2] = {0, 0};
-                int& q = nb[db ? 1 : 0];
-                if (!q) {
-                    int dev = 0, ncu = 0, occ = 0;
-                    MPBP_HIP(hipGetDevice(&dev));
-                    MPBP_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-                    if (db) MPBP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_gtg_solve_ps<H, true>, 512, 0));
-                    else MPBP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_gtg_solve_ps<H, false>, 512, 0));
-                    q = max(8, (ncu * max(occ, 1)) & ~7);
-                }
-                const int g = (int)std::min<int64_t>(q, ((tiles + 7) / 8) * 8);
-                if (db) k_gtg_solve_ps<H, true><<<(unsigned)g, 512, 0, st>>>(S, b, diag, ck, out, dv, (int)tiles);
-                else k_gtg_solve_ps<H, false><<<(unsigned)g, 512, 0, st>>>(S, b, diag, ck, out, dv, (int)tiles);
-                MPBP_HIP(hipGetLastError());
-                return MPBP_OK;
-            }
-#endif
             if (db) k_gtg_solve<H, false, 512, true><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, ck, out, dv);
             else if (part) k_gtg_solve<H, true, 512, false><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, ck, out, dv);
             else k_gtg_solve<H, false, 512, false><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, ck, out, dv);

@@ -1338,12 +1338,14 @@ class DistributedSchurPreconditioner(PlanProfiling):
 
 
 def solve_distributed(n, xi, etan, etas, c=1.0, d=-1.0, b_vec=None, inner_F=None, inner_P=None, tol=1e-8,
-                      maxiter=150, restrt=None, group=None, self_halo=False, **pc_kw):
+                      maxiter=150, restrt=None, group=None, self_halo=False, keep_operators=False, **pc_kw):
     """solve.py:240-286 over a row partition (one rank per GPU): FGMRES (solve.fgmres over `group`) on the partitioned
     operator A (DistributedMatrix) with the partitioned approximate-commutator preconditioner
     (DistributedSchurPreconditioner).  b_vec: the global right-hand side on the host (default: the manufactured problem
     of solve.py:52-80).  The solve is the one-GPU solve's, bit for bit (reproducible inner products).  Returns a dict:
-    x_local (this rank's rows of the iterate, CUDA), rows (their global ids), info, residuals, A, M."""
+    x_local (this rank's rows of the iterate, CUDA), rows (their global ids), info, residuals, A, M.  Unless
+    keep_operators, A and M are closed before the return (their RCCL communicators destroyed here, at the same point on
+    every rank, also when the solve raises -- not whenever the garbage collector of each rank gets to them)."""
     import torch.distributed as dist
     from .preconditioner import MultiphaseBlockPreconditioner
     from .solve import fgmres
@@ -1360,14 +1362,22 @@ def solve_distributed(n, xi, etan, etas, c=1.0, d=-1.0, b_vec=None, inner_F=None
                                halo=pc_kw.get("halo", "auto"))
     del bp
     torch.cuda.empty_cache()
-    M = DistributedSchurPreconditioner(n, xi, etan, etas, c=c, d_u=d, inner_F=inner_F, inner_P=inner_P, group=group,
-                                       self_halo=self_halo, **pc_kw)
-    if b_vec is None:
-        _, b_vec = manufactured_problem(n, c, d, xi, etan, etas)
-    rows = dA.local_to_global_rows()
-    assert np.array_equal(rows, M.local_to_global_rows())
-    b = torch.from_numpy(np.ascontiguousarray(np.asarray(b_vec, dtype=np.float64)[rows])).cuda()
-    kgroup = (group if group is not None else dist.group.WORLD) if world > 1 else None
-    hist = []
-    x, info = fgmres(dA, b, M=M, tol=tol, maxiter=maxiter, restrt=restrt, residuals=hist, group=kgroup)
+    M = None
+    try:
+        M = DistributedSchurPreconditioner(n, xi, etan, etas, c=c, d_u=d, inner_F=inner_F, inner_P=inner_P,
+                                           group=group, self_halo=self_halo, **pc_kw)
+        if b_vec is None:
+            _, b_vec = manufactured_problem(n, c, d, xi, etan, etas)
+        rows = dA.local_to_global_rows()
+        assert np.array_equal(rows, M.local_to_global_rows())
+        b = torch.from_numpy(np.ascontiguousarray(np.asarray(b_vec, dtype=np.float64)[rows])).cuda()
+        kgroup = (group if group is not None else dist.group.WORLD) if world > 1 else None
+        hist = []
+        x, info = fgmres(dA, b, M=M, tol=tol, maxiter=maxiter, restrt=restrt, residuals=hist, group=kgroup)
+        torch.cuda.synchronize()
+    finally:
+        if not keep_operators:
+            dA.close()
+            if M is not None:
+                M.close()
     return {"x_local": x, "rows": rows, "info": info, "residuals": hist, "A": dA, "M": M}

@@ -61,6 +61,9 @@ def transfer_rows(n: int, fields, which: int, rows: torch.Tensor) -> DeviceCSR:
     cols = nf * ((n // 2) ** 2 if which == _lib.MG_P else n * n)
     rows = rows.to(torch.int32).contiguous()
     m = rows.numel()
+    nrows = nf * (n * n if which == _lib.MG_P else (n // 2) ** 2)
+    if m and (int(rows.min()) < 0 or int(rows.max()) >= nrows):   # the kernel derives (field, row, column) from the id
+        raise ValueError(f"transfer_rows: row ids must lie in [0, {nrows}) for {nf} fields of the {n}^2 level")
     row_nnz = torch.empty(max(m, 1), dtype=torch.int32, device=rows.device)[:m]
     check(lib().mpbp_mg_transfer_rows_count(n, nf, kinds.ctypes.data_as(ctypes.c_void_p), which, ptr(rows), m,
                                             ptr(row_nnz), stream_handle()))

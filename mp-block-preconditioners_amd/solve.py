@@ -829,6 +829,10 @@ def _fgmres_dcgs2(Aop, Mop, b, x0, tol, m, maxiter, callback, residuals, K):
             host = hbuf[: 2 * j + 6].tolist()
             s_, z_ = host[:j], host[j + 1: 2 * j + 1]
             rj, rinvj, cj = host[2 * j + 2], host[2 * j + 3], host[2 * j + 4]
+            # r_j = sqrt(hu_j - s.s) forced to 0 while the raw u_j is not zero: the difference cancelled because the
+            # basis lost orthogonality (a stalling solve), not a happy breakdown -- the column's estimate |g| = 0 would
+            # be false, so the iteration records the true residual of the restart the cycle ends with instead
+            lost = j > 0 and rj == 0.0 and host[j] > 0.0
             if j < m:
                 zsc[j] = rinvj
             if j > 0:                           # complete column j - 1: H = (z / r + s, c / r + s_{j-1}, r')
@@ -851,7 +855,7 @@ def _fgmres_dcgs2(Aop, Mop, b, x0, tol, m, maxiter, callback, residuals, K):
                 k = j
                 it += 1
                 res = abs(g[col + 1])
-                if residuals is not None:
+                if residuals is not None and not lost:
                     residuals.append(res)
                 if callback is not None:
                     callback(lincomb(x, Z, k, _solve_upper(H, g, k)))
@@ -864,6 +868,8 @@ def _fgmres_dcgs2(Aop, Mop, b, x0, tol, m, maxiter, callback, residuals, K):
         x = lincomb(x, Z, k, _solve_upper(H, g, k))
         r = b - Aop(x)
         normr = norm(r, 0)
+        if lost and residuals is not None:
+            residuals.append(normr)
         if normr <= target:
             return x, 0
         if not done and k == 0:

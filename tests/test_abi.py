@@ -131,3 +131,22 @@ def test_wave_table_flags():
             want = int(L[0]) if (rb - a >= 64 and np.all(L == L[0]) and L[0] in (8, 10, 12) and rp[a] % 2 == 0) else 0
             assert (int(t[b, 7]) >> (8 * w)) & 255 == want, (b, w)
     assert (int(t[0, 7]) & 255) == 12 and ((int(t[0, 7]) >> 8) & 255) == (10 if rp[64] % 2 == 0 else 0)
+
+
+def test_kernel_options_block_lifetime_and_reentry():
+    """kernel_options (host-only, mpbp_kernel_opts_set_thread): the installed struct stays referenced while the block is
+    active -- the C thread-local pointer refers to it -- and a second entry of the same instance is refused, so the
+    previous choice can always be restored."""
+    from mp_block_preconditioners_amd import _lib
+    base = _lib.kernel_opts()
+    ko = _lib.kernel_options(march_rows=7)
+    with ko as o:
+        assert any(x is o for x in _lib._INSTALLED)
+        assert _lib.kernel_opts().march_rows == 7
+        with pytest.raises(RuntimeError):
+            ko.__enter__()
+        with _lib.kernel_options(march_rows=3):
+            assert _lib.kernel_opts().march_rows == 3
+        assert _lib.kernel_opts().march_rows == 7
+    assert not any(x is o for x in _lib._INSTALLED)
+    assert _lib.kernel_opts().march_rows == base.march_rows

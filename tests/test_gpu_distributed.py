@@ -419,7 +419,7 @@ def _comm_worker(_index, port, n, errfile):
         import mp_block_preconditioners_amd as mpb
         from mp_block_preconditioners_amd.distributed import DistributedSchurPreconditioner, solve_distributed
         res = solve_distributed(n, 1.0, 100.0, 1.0, inner_F=mpb.InnerSolver("mg", 1), inner_P=mpb.InnerSolver("mg", 1),
-                                tol=1e-8, self_halo=True, halo="rccl", mg_min_cells=0)
+                                tol=1e-8, self_halo=True, halo="rccl", mg_min_cells=0, keep_operators=True)
         dA, M = res["A"], res["M"]
         assert dA._rccl is not None and M._rccl is not None
         assert dA._rccl.comm != 0 and M._rccl.comm != 0 and dA._rccl.comm != M._rccl.comm

@@ -83,11 +83,13 @@ def test_ftile_equals_marching(n, kf, fuse_g):
 @pytest.mark.parametrize("n", [3, 5, 64, 70, 71, 72, 76, 100, 128, 255, 256, 300])
 @pytest.mark.parametrize("kf", [2, 3, 4, 5])
 @pytest.mark.parametrize("fuse_g", [True, False])
-def test_fsolve_equals_ftile(n, kf, fuse_g):
+@pytest.mark.parametrize("tile", [0, 1], ids=["64x8", "32x16"])
+def test_fsolve_equals_ftile(n, kf, fuse_g, tile):
     """k_fsolve (a whole fast F solve of 3 or 4 updates in one tiled launch: x0 and every sweep over a shrinking halo,
     each cell's state in its owning lane) performs the k_ftile launches' operations: the apply is bit-identical with it
     on and off, with G x_p recomputed in the second solve and launched separately, on grids below, at and above its
-    minimum (n >= 70 for 3 updates, 72 for 4) and not multiples of the 64 x 8 tile."""
+    minimum (n >= 70 for 3 updates, 72 for 4) and not multiples of the 64 x 8 tile -- in each tile form (kernel option
+    f_solve_tile: the 64 x 8 tile, and the 32 x 16 tile with the rings spread over the waves and cached row terms)."""
     import mp_block_preconditioners_amd as mp
     bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
     _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
@@ -97,7 +99,7 @@ def test_fsolve_equals_ftile(n, kf, fuse_g):
                     generator=torch.Generator(device="cuda").manual_seed(n * 10 + kf + 7))
     pc.set_kernel_opts(f_solve=0)
     ref = pc.apply(v).clone()
-    pc.set_kernel_opts(f_solve=1)
+    pc.set_kernel_opts(f_solve=1, f_solve_tile=tile)
     got = pc.apply(v)
     assert torch.equal(got, ref), float((got - ref).abs().max())
 

@@ -254,6 +254,7 @@ def test_fgmres_dcgs2_matches_cgs2(n, inner):
         # stops growing, DCGS2's r = sqrt(alpha - s.s) cancels to 0 (u_j within ~1e-7 of span(V)): the cycle ends
         # there and restarts from the true residual, where CGS2 goes on normalising rounding noise
         assert ic == id_ == 150 and len(hc) == 151 and len(hd) == 151
+        assert min(hd) > 0.0 and min(hc) > 0.0   # a cancelled r_j records the restart's true residual, not a false 0
         for x in (xd, xc):
             true = float(torch.linalg.vector_norm(bd - A.matvec(x)))
             assert true <= hd[0]

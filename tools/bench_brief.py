@@ -28,6 +28,7 @@ for f in sys.argv[1:]:
                 print(f"  {k}: {b[k]}")
         sl = b.get("solve_level")
         if sl:
-            for x in sl["runs"]:
+            for row in sl["runs"]:
+                x = dict(zip(sl["cols"], row)) if isinstance(row, list) else row
                 print(f"    solve n={x['n']} eta={x['eta_n']:g} {x['preconditioner']}: {x['iterations']} it "
                       f"{x['seconds']:.3f} s apply {x['apply_ms']} ms conv={x['converged']}")

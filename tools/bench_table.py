@@ -10,6 +10,6 @@ for f in sys.argv[1:]:
         continue
     d = json.loads(line)
     r = d["roofline"]
-    sp = d.get("spmv_A") or {}
+    cs = d.get("roofline_csr_spmv") or {}
     print(f"{f:60s} {d['value']:8.1f} applies/s  sweep {r['avg_launch_us']:6.2f} us  frac {r['frac']:.3f}  "
-          f"sell {sp.get('sell_gbs', 0):7.1f} GB/s  csr {sp.get('csr_gbs', 0):7.1f} GB/s")
+          f"csr {cs.get('achieved', 0):7.1f} GB/s (frac {cs.get('frac', 0):.3f}, sell frac {cs.get('sell_frac') or 0:.3f})")
