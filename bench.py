@@ -28,6 +28,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0    # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 _KEEP_ALIVE = []         # objects whose lifetime must span the run (an installed kernel_options scope)
+MG_KW = {}               # --mg-coarsest: InnerSolver keyword arguments of every multigrid inner solve the run builds
 
 
 def parse_inner(s):
@@ -196,6 +197,8 @@ def main():
                     help="N > 1: every rank forms the whole Gt_G / Gt_F_G (the default forms its own pressure rows)")
     ap.add_argument("--eager-partitioned", action="store_true",
                     help="N > 1: launch the partitioned apply eagerly instead of replaying its hipGraph")
+    ap.add_argument("--mg-coarsest", type=int, default=None,
+                    help="multigrid sections: coarsening stops at n <= this (InnerSolver.coarsest; default 16)")
     ap.add_argument("--detail-json", default=None, metavar="PATH",
                     help="also write the full record (every note and timing description) to PATH; stdout keeps the "
                          "compact line")
@@ -270,6 +273,8 @@ def main():
         ko.__enter__()
         _KEEP_ALIVE.append(ko)
 
+    if args.mg_coarsest is not None:
+        MG_KW["coarsest"] = args.mg_coarsest
     if args.weak:
         n = int(round((args.n or 1024) * math.sqrt(world)))
     else:
@@ -692,7 +697,7 @@ def partitioned_solver_section(args, n, rank, world, dist, torch, backend):
     # smoothing from the fast reciprocal diagonals as one GPU does (k_f_fast_init), so the residual histories are
     # comparable bit for bit in both numerics
     snum = args.solve_numerics or args.numerics
-    mg1 = dict(inner_F=mp.InnerSolver("mg", 1), inner_P=mp.InnerSolver("mg", 1))
+    mg1 = dict(inner_F=mp.InnerSolver("mg", 1, **MG_KW), inner_P=mp.InnerSolver("mg", 1, **MG_KW))
     out = {}
     t0 = time.perf_counter()
     M = DistributedSchurPreconditioner(n, args.xi, args.eta_n, args.eta_s, numerics=snum, **mg1)
@@ -968,7 +973,8 @@ def mg_apply_bench(F, D, G, steps, warmup, gen, reps=20, numerics="exact"):
     from mp_block_preconditioners_amd._lib import check, lib, ptr, stream_handle
     from mp_block_preconditioners_amd.solve import DeviceEvent
     t0 = time.perf_counter()
-    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("mg", 1), inner_P=mp.InnerSolver("mg", 1),
+    pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=mp.InnerSolver("mg", 1, **MG_KW),
+                                      inner_P=mp.InnerSolver("mg", 1, **MG_KW),
                                       numerics=numerics)
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
@@ -1086,7 +1092,7 @@ def inner_pair(mp, name):
 
     def mk(s):
         kind, _, k = s.partition(":")
-        return mp.InnerSolver(kind, int(k or 4), **(mgkw if kind == "mg" else {}))
+        return mp.InnerSolver(kind, int(k or 4), **({**MG_KW, **mgkw} if kind == "mg" else {}))
     return mk(f), mk(p or f)
 
 

@@ -1903,9 +1903,13 @@ struct FStencilFast : FStencilDev {
     __device__ W4 weights(const Cell& cl) const {
         return {{c * cl.face[0], c * (1.0 - cl.face[0])}, {c * cl.face[1], c * (1.0 - cl.face[1])}};
     }
-    // the four rows (u_n, v_n, u_s, v_s) of cell (gr, gc) from its coefficients k and weights w (rows4's arithmetic)
+    // the four rows (u_n, v_n, u_s, v_s) of cell (gr, gc) from its coefficients k and weights w.  The XI coupling
+    // xu (u_C - u_o) of the s phase is the n phase's negated (u_s - u_n = -(u_n - u_s) and xu (-y) = -(xu y) exactly in
+    // round-to-nearest): one difference and one product serve both phases.
     template <class XA>
     __device__ void rows4_co(int gr, int gc, const Co& k, const W4& w, const XA& xa, double* acc) const {
+        const double xdu = k.xu * (xa.X(0, gr, gc) - xa.X(2, gr, gc));
+        const double xdv = k.xv * (xa.X(1, gr, gc) - xa.X(3, gr, gc));
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
             const int fu = 2 * p, fv = 2 * p + 1;
@@ -1916,36 +1920,6 @@ struct FStencilFast : FStencilDev {
             const double uW = xa.X(fu, gr, gc - 1), uE = xa.X(fu, gr, gc + 1), uNE = xa.X(fu, gr - 1, gc + 1);
             const double vC = xa.X(fv, gr, gc), vN = xa.X(fv, gr - 1, gc), vS = xa.X(fv, gr + 1, gc);
             const double vW = xa.X(fv, gr, gc - 1), vE = xa.X(fv, gr, gc + 1), vSW = xa.X(fv, gr + 1, gc - 1);
-            const double uo = xa.X(fu ^ 2, gr, gc), vo = xa.X(fv ^ 2, gr, gc);
-            const double tn = (uN - uC) + (vC - vW), tc = (uE - uC) + (vS - vC);
-            double br = KC * tn;
-            br = __builtin_fma(A1, (uW - uC) + (vW - vSW), br);
-            br = __builtin_fma(A2, tc, br);
-            br = __builtin_fma(KS, (uS - uC) + (vSW - vS), br);
-            acc[fu] = __builtin_fma(a, br, __builtin_fma(w.wu[p], uC, k.xu * (uC - uo)));
-            double bv = B1 * ((vN - vC) + (uN - uNE));
-            bv = __builtin_fma(KC, -tn, bv);
-            bv = __builtin_fma(KE, (vE - vC) + (uNE - uE), bv);
-            bv = __builtin_fma(A2, tc, bv);
-            acc[fv] = __builtin_fma(a, bv, __builtin_fma(w.wv[p], vC, k.xv * (vC - vo)));
-        }
-    }
-    // the four rows (u_n, v_n, u_s, v_s) of cell (gr, gc) and their reciprocal diagonals
-    // RD = false: the diagonals are the caller's (k_ftile level B reuses level A's, computed by the same operations)
-    template <bool RD = true, class TA, class XA>
-    __device__ void rows4(int gr, int gc, const TA& ta, const XA& xa, const Cell& cl, double* acc, double* rd) const {
-        const Co k = coeffs(nb(ta, gr, gc));
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            const int fu = 2 * p, fv = 2 * p + 1;
-            auto ph = [&](double t) { return p ? 1.0 - t : t; };
-            const double a = aco(p);
-            const double A1 = ph(k.w), A2 = ph(k.c), B1 = ph(k.nn), KC = ph(k.kc), KS = ph(k.ks), KE = ph(k.ke);
-            const double uC = xa.X(fu, gr, gc), uN = xa.X(fu, gr - 1, gc), uS = xa.X(fu, gr + 1, gc);
-            const double uW = xa.X(fu, gr, gc - 1), uE = xa.X(fu, gr, gc + 1), uNE = xa.X(fu, gr - 1, gc + 1);
-            const double vC = xa.X(fv, gr, gc), vN = xa.X(fv, gr - 1, gc), vS = xa.X(fv, gr + 1, gc);
-            const double vW = xa.X(fv, gr, gc - 1), vE = xa.X(fv, gr, gc + 1), vSW = xa.X(fv, gr + 1, gc - 1);
-            const double uo = xa.X(fu ^ 2, gr, gc), vo = xa.X(fv ^ 2, gr, gc);
             // the node (r, c) and centre (r, c) terms are shared by the u and v rows: the v row's are -tn (the same
             // differences negated: exact) and tc (the same sum, operands swapped: exact)
             const double tn = (uN - uC) + (vC - vW), tc = (uE - uC) + (vS - vC);
@@ -1954,20 +1928,23 @@ struct FStencilFast : FStencilDev {
             br = __builtin_fma(A1, (uW - uC) + (vW - vSW), br);
             br = __builtin_fma(A2, tc, br);
             br = __builtin_fma(KS, (uS - uC) + (vSW - vS), br);
-            const double wu = c * ph(cl.face[0]);
-            acc[fu] = __builtin_fma(a, br, __builtin_fma(wu, uC, k.xu * (uC - uo)));
-            if constexpr (RD)
-                rd[fu] = rcp_nr(__builtin_fma(-a, (A1 + A2) + (KC + KS), wu + k.xu));
+            acc[fu] = __builtin_fma(a, br, __builtin_fma(w.wu[p], uC, p ? -xdu : xdu));
             // v row: u1 = uN, u2 = uNE, u3 = uC, u4 = uE
             double bv = B1 * ((vN - vC) + (uN - uNE));
             bv = __builtin_fma(KC, -tn, bv);
             bv = __builtin_fma(KE, (vE - vC) + (uNE - uE), bv);
             bv = __builtin_fma(A2, tc, bv);
-            const double wv = c * ph(cl.face[1]);
-            acc[fv] = __builtin_fma(a, bv, __builtin_fma(wv, vC, k.xv * (vC - vo)));
-            if constexpr (RD)
-                rd[fv] = rcp_nr(__builtin_fma(-a, (B1 + A2) + (KC + KE), wv + k.xv));
+            acc[fv] = __builtin_fma(a, bv, __builtin_fma(w.wv[p], vC, p ? -xdv : xdv));
         }
+    }
+    // the four rows (u_n, v_n, u_s, v_s) of cell (gr, gc) and their reciprocal diagonals
+    // RD = false: the diagonals are the caller's (k_ftile level B reuses level A's, computed by the same operations)
+    template <bool RD = true, class TA, class XA>
+    __device__ void rows4(int gr, int gc, const TA& ta, const XA& xa, const Cell& cl, double* acc, double* rd) const {
+        const Co k = coeffs(nb(ta, gr, gc));
+        const W4 w = weights(cl);
+        rows4_co(gr, gc, k, w, xa, acc);
+        if constexpr (RD) rdiag4_co(k, w, rd);
     }
     // the reciprocal diagonals from a cell's coefficients and weights (rdiag4's arithmetic)
     __device__ void rdiag4_co(const Co& k, const W4& w, double* rd) const {

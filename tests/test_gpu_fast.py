@@ -174,7 +174,10 @@ def test_256_fast_multigrid_apply(inner):
     v = torch.randn(fast.shape[0], dtype=torch.float64, device="cuda",
                     generator=torch.Generator(device="cuda").manual_seed(9))
     err = rel_inf(fast.apply(v).cpu().numpy(), exact.apply(v).cpu().numpy())
-    assert 0.0 < err <= 1e-10, err   # ~200 launches incl. the coarsest pseudo-inverses (cf. test_1024_mg_apply_properties)
+    print(f"256^2 {inner}: fast vs exact {err:.3e}")
+    # north_star's bar: measured 2.5e-13 (mg:1) and 3.4e-13 (mg:2 / mg:1) on round 6's library, against the exact apply,
+    # which is the oracle's bits (tests/test_gpu_mg.py); the apply's own one-ulp conditioning floor here is ~5e-13
+    assert 0.0 < err <= TOL_APPLY, err
 
 
 def _oracle_mg_apply(S, pc, v):
@@ -223,6 +226,7 @@ def test_256_fast_multigrid_apply_vs_mg_oracle(eta_n, inner, oracle_256):
         exact = mp.ApproxSchurPreconditioner(F, D, G, pc.GtG, pc.GtFG, inner_F=iF, inner_P=iP)
         vu = v * (1.0 + np.where(np.random.default_rng(7).random(v.size) < 0.5, -1.0, 1.0) * 2.0 ** -52)
         floor = rel_inf(exact.apply(_cuda(vu)).cpu().numpy(), ref)
+        print(f"256^2 eta {eta_n:g} {inner}: fast vs oracle {err:.3e}, one-ulp floor {floor:.3e}")
         assert 0.0 < err <= 1e-11, (err, floor)
 
 
@@ -245,6 +249,7 @@ def test_1024_fast_multigrid_apply_at_the_conditioning_floor():
     ref = exact.apply(v).cpu().numpy()
     floor = rel_inf(exact.apply(v_ulp).cpu().numpy(), ref)
     err = rel_inf(fast.apply(v).cpu().numpy(), ref)
+    print(f"1024^2 mg:1: fast vs exact {err:.3e}, one-ulp floor {floor:.3e}")
     assert floor > 0.0
     assert err <= max(TOL_APPLY, 4.0 * floor), (err, floor)
 
@@ -303,7 +308,8 @@ def test_fused_pair_equals_two_sweeps(n, kf, kp):
 @pytest.mark.parametrize("n", [64, 72, 100, 128, 256])
 def test_matrix_free_galerkin_level1(n):
     """Fast F hierarchies apply level 1 as R_0 (F (P_0 x)) (MgGal) instead of streaming the stored Galerkin product:
-    the same operator, so the multigrid apply stays within 1e-10 of the stored-level-1 apply (and of the exact one)."""
+    the same operator, so the multigrid apply stays within north_star's 1e-12 of the stored-level-1 apply (and of the
+    exact one)."""
     mp = _mp()
     bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
     _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
@@ -318,10 +324,13 @@ def test_matrix_free_galerkin_level1(n):
     got = fast.apply(v).clone()
     fast.set_kernel_opts(mg_galerkin_mf=2)
     one = fast.apply(v).clone()
-    assert 0.0 < rel_inf(got.cpu().numpy(), stored.cpu().numpy()) <= 1e-10
+    e_stored = rel_inf(got.cpu().numpy(), stored.cpu().numpy())
+    assert 0.0 < e_stored <= TOL_APPLY   # measured 2.5e-14 (n = 72) .. 2.9e-13 (n = 256)
     assert torch.equal(one, got)   # one k_gal1 launch (the default) == the three launches, bit for bit
     exact = mp.ApproxSchurPreconditioner(F, D, G, fast.GtG, fast.GtFG, **kw)
-    assert rel_inf(got.cpu().numpy(), exact.apply(v).cpu().numpy()) <= 1e-10
+    e_exact = rel_inf(got.cpu().numpy(), exact.apply(v).cpu().numpy())
+    print(f"level-1 F n={n}: vs stored {e_stored:.3e}, vs exact {e_exact:.3e}")
+    assert e_exact <= TOL_APPLY   # measured 3.4e-14 .. 4.6e-13
     out = torch.empty_like(v)
     g = fast.capture(v, out)
     g.replay()
@@ -361,7 +370,7 @@ def test_mg_coarse_tree_sum(n):
 
 @pytest.mark.parametrize("n", [64, 72, 80, 100, 128, 256])
 def test_matrix_free_galerkin_level1_pressure(n):
-    """The pressure hierarchy's level 1 as R_0 (Gt_G (P_0 x)) (kernel option mg_galerkin_mf_p): within 1e-10 of its stored
+    """The pressure hierarchy's level 1 as R_0 (Gt_G (P_0 x)) (kernel option mg_galerkin_mf_p): within 1e-12 of its stored
     Galerkin matrix, and the one-launch k_gal1p bit-identical to the three launches it fuses."""
     mp = _mp()
     bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
@@ -377,7 +386,9 @@ def test_matrix_free_galerkin_level1_pressure(n):
     three = fast.apply(v).clone()
     fast.set_kernel_opts(mg_galerkin_mf=2)
     one = fast.apply(v).clone()
-    assert 0.0 < rel_inf(three.cpu().numpy(), stored.cpu().numpy()) <= 1e-10
+    e_stored = rel_inf(three.cpu().numpy(), stored.cpu().numpy())
+    print(f"level-1 P n={n}: vs stored {e_stored:.3e}")
+    assert 0.0 < e_stored <= TOL_APPLY   # measured 1.5e-14 .. 3.0e-13
     assert torch.equal(one, three), float((one - three).abs().max())
     out = torch.empty_like(v)
     g = fast.capture(v, out)

@@ -9,8 +9,9 @@ at 1024^2 -- BASELINE configs[2] (eta_n = 100) and configs[3] (eta_n / eta_s = 1
   levels); this is their oracle check at the size they run at.
 * fast numerics (the bench's): against the same oracle output.  Bar: max(1e-12, 4 x floor), floor = the EXACT apply's
   own response to a one-ulp relative perturbation of its input (the exact GPU apply is the oracle's bits, checked in
-  the first test).  No evaluation order other than the oracle's can sit closer to the oracle than that floor; measured
-  floors are ~2.7e-12 at eta_n = 100 (profiles/r05j_mg_parity_study.jsonl).  The measured error and floor are printed.
+  the first test).  No evaluation order other than the oracle's can sit closer to the oracle than that floor.  Measured
+  (round 6, profiles/r06e_fast_tests_measured.txt): eta_n = 100 error 5.4e-12, floor 2.7e-12; eta ratio 1e4 error
+  5.2e-12, floor 6.1e-12.  The measured error and floor are printed.
 The oracle side costs about a minute of one host core per eta (assembly + products ~35 s, the F hierarchy ~25 s)."""
 import numpy as np
 import pytest
