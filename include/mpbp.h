@@ -496,7 +496,10 @@ typedef struct mpbp_kernel_opts {
     int32_t f_solve_tile;      /* tolerance-mode whole F solves (k_fsolve): 0 the 64 x 8 tile, halo rings owned by the
                                   first lanes; 1 (default) a 32 x 16 tile, each ring dealt out evenly over the four waves, the
                                   rows' level-invariant terms computed once (k_fsolve_w).  Both compute the same bits */
-    int32_t reserved[4];
+    int32_t q13_mf;            /* tolerance mode, one GPU, matrix-free F / D / G: x_b = Gt_F_G x_a applied as its factors
+                                  -(D (F (G x_a))) on 32 x 16 tiles (k_qmf; 42 instead of 76 MB per apply at 1024^2),
+                                  not the stored product (1); 0: the stored product (k_q13) */
+    int32_t reserved[3];
 } mpbp_kernel_opts;
 /* *out = the calling thread's current choices: its mpbp_kernel_opts_set_thread scope, else the process defaults. */
 void mpbp_kernel_opts_default(mpbp_kernel_opts* out);

@@ -28,7 +28,7 @@ mpbp_kernel_opts g_defaults = {
     /*march_rows*/ 0, /*init_diag*/ 1, /*f_pair*/ 1, /*f_direct*/ 0, /*gtg_fused*/ 1, /*gtg_tpb*/ 512, /*gtg_drhs*/ 1,
     /*q13_sym*/ 1, /*f_tile*/ 1, /*f_solve*/ 1, /*mg_galerkin_mf*/ 2, /*mg_galerkin_mf_p*/ 1, /*pg_direct*/ 1,
     /*mg_group_rows*/ 65536, /*mg_svl*/ 1, /*mg_mf_transfer*/ 1, /*csr_table*/ 1, /*mg_fuse_l0*/ 1,
-    /*mg_coarse_tree*/ 0, /*f_solve_tile*/ 1, {0, 0, 0, 0}};
+    /*mg_coarse_tree*/ 0, /*f_solve_tile*/ 1, /*q13_mf*/ 0, {0, 0, 0}};
 thread_local const mpbp_kernel_opts* t_opts = nullptr;
 inline const mpbp_kernel_opts& KO() { return t_opts ? *t_opts : g_defaults; }
 struct OptsScope {   // installs a plan's kernel choices (when it has its own) for one entry-point call
@@ -48,10 +48,10 @@ inline int check_opts(const mpbp_kernel_opts* o, const char* who) {
                     o->mg_galerkin_mf >= 0 && o->mg_galerkin_mf <= 2 && o->mg_group_rows >= 0 &&
                     (o->init_diag | o->f_pair | o->f_direct | o->gtg_fused | o->gtg_drhs | o->q13_sym | o->f_tile |
                      o->f_solve | o->mg_galerkin_mf_p | o->pg_direct | o->mg_svl | o->mg_mf_transfer | o->csr_table |
-                     o->mg_fuse_l0 | o->mg_coarse_tree) >= 0 &&
+                     o->mg_fuse_l0 | o->mg_coarse_tree | o->q13_mf) >= 0 &&
                     (o->init_diag | o->f_pair | o->f_direct | o->gtg_fused | o->gtg_drhs | o->q13_sym | o->f_tile |
                      o->f_solve | o->mg_galerkin_mf_p | o->pg_direct | o->mg_svl | o->mg_mf_transfer | o->csr_table |
-                     o->mg_fuse_l0 | o->mg_coarse_tree) <= 1;
+                     o->mg_fuse_l0 | o->mg_coarse_tree | o->q13_mf) <= 1;
     return ok ? MPBP_OK : set_error(MPBP_ERR_ARG, "%s: kernel options out of range", who);
 }   // rows per workgroup of the D / G / Gt_G marching kernels: as F
 
@@ -6419,6 +6419,148 @@ int launch_q13(int32_t n, const double* vals, const double* x, Epi epi, hipStrea
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
+
+// ---- x_b = Gt_F_G x_a matrix-free, tolerance mode (k_qmf, kernel option q13_mf) ----
+// solve.py:247-249 forms Gt_F_G = ((-D) F) G once and the apply multiplies it (k_q13: 7 or 13 stored diamond values
+// per row, 75-126 MB per apply at 1024^2).  Here the product is applied as its three factors on a 32 x 16 tile of
+// pressure cells: y = G x_a on the tile + 1 (its four velocity rows, GxBT::b_at's entries: d_p (+-inv g) with g the
+// face's thn average), z = F y on the tile's cells plus their east / south faces (the tolerance-mode rows,
+// FStencilFast::rows4_co), then x_b = -(D z) (DStencilDev's entries: +-inv times the face average).  x_a and thn are
+// staged over the tile + 2, y and z live in LDS (z over y), only the faces of the z cells and x_b touch memory
+// besides: HBM 8 B x_a + 24 B thn / faces + 8 B x_b per cell = 42 MB at 1024^2, against k_q13<SYM>'s 76 MB.  The same
+// operator as the stored product; its sums in another order (a few ulp per entry, within north_star's 1e-12 on the
+// apply: tests/test_gpu_fast.py, test_gpu_q13.py).  One GPU, whole grid, fast numerics, matrix-free F / D / G.
+constexpr int kQmW = 32, kQmH = 16;
+constexpr int kQxW = kQmW + 4, kQxH = kQmH + 4, kQxN = kQxW * kQxH;   // x_a, thn: the tile + 2
+constexpr int kQyW = kQmW + 3, kQyH = kQmH + 3, kQyN = kQyW * kQyH;   // y = G x_a: rows / columns -1 .. +TW+1
+constexpr int kQzW = kQmW + 1, kQzH = kQmH + 1, kQzN = kQzW * kQzH;   // z = F y: the tile's cells + east / south
+template <class Epi>
+__global__ void __launch_bounds__(256) MPBP_LDS_READS k_qmf(FStencilFast P, PGDev G, const double* __restrict__ xa,
+                                                            Epi epi) {
+    __shared__ double ts[kQxN], xs[kQxN];
+    __shared__ double ys[4 * kQyN];   // y; then z (4 * kQzN <= 4 * kQyN)
+    const int n = P.n;
+    const int tx = (n + kQmW - 1) / kQmW;
+    const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int r0 = (bk / tx) * kQmH, c0 = (bk % tx) * kQmW;
+    const int tid = threadIdx.x;
+    constexpr int IX = (kQxN + 255) / 256, IZ = (kQzN + 255) / 256;
+    {   // x_a and thn over the tile + 2; the faces of this lane's z cells -- every load before the first LDS store
+        double vt[IX], vx[IX];
+#pragma unroll
+        for (int it = 0; it < IX; ++it) {
+            const int i = tid + it * 256;
+            if (i < kQxN) {
+                const int sr = i / kQxW, sc = i - sr * kQxW;
+                const int32_t k = P.wrap(r0 - 2 + sr) * n + P.wrap(c0 - 2 + sc);
+                vt[it] = P.cell[k];
+                vx[it] = xa[k];
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < IX; ++it) {
+            const int i = tid + it * 256;
+            if (i < kQxN) {
+                ts[i] = vt[it];
+                xs[i] = vx[it];
+            }
+        }
+    }
+    double fu[IZ], fv[IZ];
+#pragma unroll
+    for (int it = 0; it < IZ; ++it) {
+        const int i = tid + it * 256;
+        if (i < kQzN) {
+            const int zr = i / kQzW, zc = i - zr * kQzW;
+            const int32_t k = P.wrap(r0 + zr) * n + P.wrap(c0 + zc);
+            fu[it] = P.uface[k];
+            fv[it] = P.vface[k];
+        }
+    }
+    __syncthreads();
+    const TTileT<kQxW> tt{ts, r0 - 2, c0 - 2};
+    const XTileT<kQxW, 1> xt{xs, r0 - 2, c0 - 2};
+    // y = G x_a: velocity rows (u_n, v_n, u_s, v_s) at (r, c) -- u on the cell's west face, v on its north face
+    for (int i = tid; i < kQyN; i += 256) {
+        const int vr = r0 - 1 + i / kQyW, vc = c0 - 1 + i % kQyW;
+        const double xc = xt.X(0, vr, vc), xw = xt.X(0, vr, vc - 1), xn = xt.X(0, vr - 1, vc);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const double t0 = tt.T(p, vr, vc);
+            const double gu = 0.5 * (t0 + tt.T(p, vr, vc - 1)), gv = 0.5 * (t0 + tt.T(p, vr - 1, vc));
+            ys[(2 * p) * kQyN + i] = (G.d_p * (G.minv * gu)) * xw + (G.d_p * (G.inv * gu)) * xc;
+            ys[(2 * p + 1) * kQyN + i] = (G.d_p * (G.inv * gv)) * xn + (G.d_p * (G.minv * gv)) * xc;
+        }
+    }
+    __syncthreads();
+    // z = F y on the tile's cells and their east / south neighbours (held in registers, then over y)
+    double zv[IZ][4];
+    {
+        const XTileT<kQyW, kQyH> yt{ys, r0 - 1, c0 - 1};
+#pragma unroll
+        for (int it = 0; it < IZ; ++it) {
+            const int i = tid + it * 256;
+            if (i >= kQzN) break;
+            const int vr = r0 + i / kQzW, vc = c0 + i % kQzW;
+            const typename FStencilFast::Co k = P.coeffs(P.nb(tt, vr, vc));
+            P.rows4_co(vr, vc, k, P.weights(FStencilDev::Cell{{fu[it], fv[it]}}), yt, zv[it]);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < IZ; ++it) {
+        const int i = tid + it * 256;
+        if (i >= kQzN) break;
+#pragma unroll
+        for (int f = 0; f < 4; ++f) ys[f * kQzN + i] = zv[it][f];
+    }
+    __syncthreads();
+    // x_b = -(D z) on the tile (the pressure row: u at the west / east faces, v at the north / south faces, per phase)
+    const XTileT<kQzW, kQzH> zt{ys, r0, c0};
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        const int vr = r0 + tid / kQmW + 8 * m, vc = c0 + tid % kQmW;
+        if (vr >= n || vc >= n) continue;
+        const int32_t row = vr * n + vc;
+        const typename Epi::P pe = epi.pre(row);
+        double acc = 0.0;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const double t0 = tt.T(q, vr, vc);
+            const double uC = (G.minv * (0.5 * (t0 + tt.T(q, vr, vc - 1)))) * zt.X(2 * q, vr, vc);
+            const double uE = (G.inv * (0.5 * (t0 + tt.T(q, vr, vc + 1)))) * zt.X(2 * q, vr, vc + 1);
+            const double vC = (G.inv * (0.5 * (t0 + tt.T(q, vr - 1, vc)))) * zt.X(2 * q + 1, vr, vc);
+            const double vS = (G.minv * (0.5 * (t0 + tt.T(q, vr + 1, vc)))) * zt.X(2 * q + 1, vr + 1, vc);
+            acc += uC;
+            acc += uE;
+            acc += vC;
+            acc += vS;
+        }
+        epi(row, -acc, pe);
+    }
+}
+// whole grid, one GPU: the staged window (tile + 2) wraps at most once
+inline bool qmf_ok_n(int n) { return n >= kQxW && n >= kQxH; }
+// The plan's Gt_F_G product by k_qmf: kernel option q13_mf, tolerance mode, one GPU, matrix-free F (fast rows) and D / G.
+bool qmf_ok(const mpbp_schur_plan* p) {
+    return KO().q13_mf && p->f_numerics == MPBP_NUMERICS_FAST && p->f_stencil && p->pg_stencil && !p->halo &&
+           p->f_cell && p->f_uface && p->f_vface && qmf_ok_n(p->f_prm.n);
+}
+template <class Epi>
+int launch_qmf(const mpbp_schur_plan* p, const double* xa, Epi epi, hipStream_t st) {
+    FStencilDev Pd;
+    int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &Pd);
+    if (rc) return rc;
+    PGDev G;
+    rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &G);
+    if (rc) return rc;
+    const FStencilFast P{Pd};
+    if (!qmf_ok_n(P.n) || !xa || xa == epi.y) return set_error(MPBP_ERR_ARG, "qmf: whole grid n >= 36, vectors");
+    const int64_t tiles = (int64_t)((P.n + kQmW - 1) / kQmW) * ((P.n + kQmH - 1) / kQmH);
+    k_qmf<Epi><<<(unsigned)tiles, 256, 0, st>>>(P, G, xa, epi);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -7850,10 +7992,15 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
     }
     // 4. x_b = Gt_F_G @ x_a                                                solve.py:267
     //    (one GPU: the diamond layout when the plan has it)
-    const bool qx0 = px0 && p->q13;
-    if (qx0)
+    const bool qmf = qmf_ok(p);   // tolerance mode: the product as its factors, matrix-free (k_qmf)
+    const bool qx0 = px0 && (p->q13 || qmf);
+    if (qx0 && qmf)
+        rc = launch_qmf(p, Pxa, EpiStoreX0{Pxb, p->diag_P, pc2[0], P0}, c.st);
+    else if (qx0)
         rc = launch_q13(p->q13_n, p->q13, Pxa, EpiStoreX0{Pxb, p->diag_P, pc2[0], P0}, c.st,
                         KO().q13_sym && p->f_numerics == MPBP_NUMERICS_FAST);
+    else if (qmf)
+        rc = launch_qmf(p, Pxa, EpiStore{Pxb}, c.st);
     else if (p->q13 && !p->halo)   // tolerance mode: the symmetric product's upper half (k_q13<SYM>)
         rc = launch_q13(p->q13_n, p->q13, Pxa, EpiStore{Pxb}, c.st, KO().q13_sym && p->f_numerics == MPBP_NUMERICS_FAST);
     else

@@ -16,6 +16,7 @@ is not formed here (``S`` is None) -- the approximate-commutator preconditioner 
 from __future__ import annotations
 
 import ctypes
+import weakref
 
 import numpy as np
 import torch
@@ -201,6 +202,9 @@ class MultiphaseBlockPreconditioner:
         GtF = spgemm(D, F, alpha=-1.0)
         GtFG = spgemm(GtF, G, alpha=1.0)
         del GtF
+        # provenance: the matrix-free Gt_F_G apply (kernel option q13_mf) may stand in for this product only when it
+        # IS the product of the operators the preconditioner holds (weak references: the tag keeps nothing alive)
+        GtFG._product_of = tuple(weakref.ref(M) for M in (F, D, G))
         sd, sg = getattr(D, "stencil", None), getattr(G, "stencil", None)
         if isinstance(sd, PGStencil) and sd.op == _lib.PG_D and isinstance(sg, PGStencil) and sg.op == _lib.PG_G \
                 and sd.same_grid(sg):

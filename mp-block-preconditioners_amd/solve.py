@@ -128,12 +128,15 @@ class PlanProfiling:
     def set_kernel_opts(self, **kw):
         """Change this preconditioner's kernel choices (mpbp_kernel_opts field names; others untouched).  The next apply
         or capture uses them; graphs captured before keep the choices they were captured with.  Every choice computes
-        the same bits except q13_sym and mg_coarse_tree (tolerance mode; q13_sym stays 0 where the stored Gt_F_G is not
-        symmetric)."""
+        the same bits except q13_sym, q13_mf and mg_coarse_tree (tolerance mode; q13_sym stays 0 where the stored Gt_F_G
+        is not symmetric, q13_mf where it is not the product of the preconditioner's own F, D, G)."""
         names = {f for f, _ in _lib.KernelOpts._fields_ if f != "reserved"}
         for k, v in kw.items():
             if k not in names:
                 raise ValueError(f"unknown kernel option {k!r} (known: {sorted(names)})")
+            if k == "q13_mf" and v and not getattr(self, "gtfg_is_product", False):
+                raise ValueError("q13_mf: this preconditioner's Gt_F_G is not known to be ((-D) F) G of its own "
+                                 "F, D, G (pass GtFG from commutator_products of the same operators, or none)")
             if k == "q13_sym" and v and getattr(self, "q13_asymmetry", None) is not None:
                 a, m = self.q13_asymmetry
                 if not a <= 1e-14 * m:
@@ -256,6 +259,12 @@ class ApproxSchurPreconditioner(PlanProfiling, spla.LinearOperator):
         if GtG is None or GtFG is None:
             GtG, GtFG = MultiphaseBlockPreconditioner.commutator_products(self.F, self.D, self.G)
         self.GtG, self.GtFG = _device_csr(GtG, dev), _device_csr(GtFG, dev)
+        # Gt_F_G is the product of this preconditioner's own F, D, G (commutator_products of these objects): only then
+        # may tolerance mode apply it matrix-free as -(D (F (G x))) (kernel option q13_mf)
+        tag = getattr(self.GtFG, "_product_of", None)
+        self.gtfg_is_product = tag is not None and all(r() is M for r, M in zip(tag, (self.F, self.D, self.G)))
+        if not self.gtfg_is_product:
+            self.kernel_opts.q13_mf = 0
         nu, np_ = self.F.shape[0], self.GtG.shape[0]
         if self.F.shape != (nu, nu) or self.D.shape != (np_, nu) or self.G.shape != (nu, np_) \
                 or self.GtFG.shape != (np_, np_):

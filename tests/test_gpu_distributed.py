@@ -41,7 +41,7 @@ def _worker(rank, world, port, n, layout, f_mode, kind, errfile, ca="auto", fuse
         # (the partition multiplies Gt_F_G's full rows: so does the one-GPU reference, q13_sym = 0)
         pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, layout=layout,
                                            f_mode="assembled" if numerics == "exact" else "stencil", numerics=numerics,
-                                           kernel_opts={"q13_sym": 0})
+                                           kernel_opts={"q13_sym": 0, "q13_mf": 0})
         assert (pc.inner_F.lmin, pc.inner_F.lmax) == (dpc.inner_F.lmin, dpc.inner_F.lmax)
         v = torch.from_numpy(np.random.default_rng(5).standard_normal(pc.shape[0])).cuda()
         gids = torch.from_numpy(dpc.local_to_global_rows()).cuda()
@@ -289,7 +289,7 @@ def _inner_pair(spec):
     return mpb.InnerSolver(kf, sf), mpb.InnerSolver(kp, sp)
 
 
-FAST_TWIN = {"mg_galerkin_mf": 0, "mg_galerkin_mf_p": 0, "q13_sym": 0}   # the partition's level-1 and Gt_F_G forms
+FAST_TWIN = {"mg_galerkin_mf": 0, "mg_galerkin_mf_p": 0, "q13_sym": 0, "q13_mf": 0}   # the partition's level-1 and Gt_F_G forms
 
 
 def _mg_worker(rank, world, port, n, inner, min_cells, halo, errfile, numerics="exact"):
@@ -506,7 +506,7 @@ def _configs4_worker(rank, world, port, n, errfile, numerics="exact"):
                 bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
                 _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
                 pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, numerics=numerics,
-                                                   kernel_opts={"q13_sym": 0})   # (the partition's full Gt_F_G rows)
+                                                   kernel_opts={"q13_sym": 0, "q13_mf": 0})   # (the partition's full Gt_F_G rows)
                 ref = pc.apply(v)[gids]
                 assert torch.equal(got, ref), float((got - ref).abs().max())
                 del pc, F, D, G, bp, ref

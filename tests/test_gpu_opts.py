@@ -40,9 +40,10 @@ def test_two_preconditioners_with_different_kernel_choices(n):
     before = bytes(kernel_opts())
     kw = dict(inner_F=mp.InnerSolver("chebyshev", 4), inner_P=mp.InnerSolver("chebyshev", 4), numerics="fast")
     slow = {"f_solve": 0, "f_tile": 0, "gtg_fused": 0, "gtg_drhs": 0}
-    A = mp.ApproxSchurPreconditioner(F, D, G, GtG, GtFG, **kw)
-    B = mp.ApproxSchurPreconditioner(F, D, G, GtG, GtFG, **kw, kernel_opts={**slow, "q13_sym": 0})
-    C = mp.ApproxSchurPreconditioner(F, D, G, GtG, GtFG, **kw, kernel_opts=slow)
+    # (the stored Gt_F_G in both reads: q13_mf = 0, the matrix-free product being a third form)
+    A = mp.ApproxSchurPreconditioner(F, D, G, GtG, GtFG, **kw, kernel_opts={"q13_mf": 0})
+    B = mp.ApproxSchurPreconditioner(F, D, G, GtG, GtFG, **kw, kernel_opts={**slow, "q13_sym": 0, "q13_mf": 0})
+    C = mp.ApproxSchurPreconditioner(F, D, G, GtG, GtFG, **kw, kernel_opts={**slow, "q13_mf": 0})
     assert bytes(kernel_opts()) == before
     assert A.kernel_opts.f_solve == 1 and B.kernel_opts.f_solve == 0 and B.kernel_opts.q13_sym == 0
     v = torch.randn(A.shape[0], dtype=torch.float64, device="cuda",
@@ -108,12 +109,16 @@ def test_nonsymmetric_gtfg_keeps_full_rows():
     Q = DeviceCSR(GtFG.row_ptr, GtFG.col_idx, val, GtFG.shape)
     bad = mp.ApproxSchurPreconditioner(F, D, G, GtG, Q, **kw)
     assert bad.kernel_opts.q13_sym == 0 and bad.q13_asymmetry[0] > 1e-14 * bad.q13_asymmetry[1]
-    full = mp.ApproxSchurPreconditioner(F, D, G, GtG, Q, **kw, kernel_opts={"q13_sym": 0})
+    full = mp.ApproxSchurPreconditioner(F, D, G, GtG, Q, **kw, kernel_opts={"q13_sym": 0, "q13_mf": 0})
     v = torch.randn(sym.shape[0], dtype=torch.float64, device="cuda",
                     generator=torch.Generator(device="cuda").manual_seed(2))
     assert torch.equal(bad.apply(v), full.apply(v))
     with pytest.raises(ValueError, match="not symmetric"):
         bad.set_kernel_opts(q13_sym=1)
+    # a caller's Gt_F_G that is not the product of these F, D, G is never replaced by the matrix-free product
+    assert not bad.gtfg_is_product and bad.kernel_opts.q13_mf == 0 and sym.gtfg_is_product
+    with pytest.raises(ValueError, match="q13_mf"):
+        bad.set_kernel_opts(q13_mf=1)
 
 
 @pytest.mark.parametrize("sweeps", [2, 4, 6])

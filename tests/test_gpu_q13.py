@@ -27,6 +27,16 @@ def _bits(a, b):
 PARAMS = [(1.0, 100.0, 1.0, 1.0, -1.0, 1.0), (2.5, 1.0e4, 1.0, 0.5, -2.0, 2.5)]
 
 
+def _mp():
+    import mp_block_preconditioners_amd as mp
+    return mp
+
+
+def _rel(a, b):
+    a, b = a.cpu().numpy(), b.cpu().numpy()
+    return float(np.max(np.abs(a - b)) / np.max(np.abs(b)))
+
+
 def _products(n, prm):
     import mp_block_preconditioners_amd as mp
     xi, eta_n, eta_s, c, d_u, d_p = prm
@@ -84,3 +94,34 @@ def test_apply_with_diamond_matches_assembled(n, layout):
     assert a.q13 is None and b.q13 is not None
     v = torch.from_numpy(np.random.default_rng(3).standard_normal(a.shape[0])).cuda()
     assert _bits(a.apply(v), b.apply(v))
+
+
+@pytest.mark.parametrize("n", [36, 64, 100, 256])
+@pytest.mark.parametrize("prm", [(1.0, 100.0, 1.0, 1.0, -1.0), (1.0, 1.0e4, 1.0, 1.0, -1.0), (2.5, 3.0, 0.5, 0.7, -2.0)],
+                         ids=["visc", "stiff", "general"])
+def test_gtfg_matrix_free_product(n, prm):
+    """Kernel option q13_mf (tolerance mode, one GPU): x_b = Gt_F_G x_a applied as -(D (F (G x_a))) on tiles (k_qmf)
+    instead of the stored product: the apply stays within north_star's 1e-12 relative inf-norm of the stored-product
+    apply and of the exact (oracle-identical) apply, and its hipGraph replay equals the eager apply bit for bit."""
+    xi, eta_n, eta_s, c, d_u = prm
+    mp = _mp()
+    bp = mp.MultiphaseBlockPreconditioner(n, xi, eta_n, eta_s)
+    _, _, F, D, G = bp.get_big_A_matrix(c=c, d_u=d_u)
+    kw = dict(inner_F=mp.InnerSolver("chebyshev", 4), inner_P=mp.InnerSolver("chebyshev", 4))
+    fast = mp.ApproxSchurPreconditioner(F, D, G, numerics="fast", **kw)
+    exact = mp.ApproxSchurPreconditioner(F, D, G, fast.GtG, fast.GtFG, **kw)
+    v = torch.randn(fast.shape[0], dtype=torch.float64, device="cuda",
+                    generator=torch.Generator(device="cuda").manual_seed(n + 3))
+    fast.set_kernel_opts(q13_mf=0)
+    stored = fast.apply(v).clone()
+    fast.set_kernel_opts(q13_mf=1)
+    mf = fast.apply(v).clone()
+    e_stored = _rel(mf, stored)
+    e_exact = _rel(mf, exact.apply(v))
+    print(f"q13_mf n={n} {prm}: vs stored {e_stored:.3e}, vs exact {e_exact:.3e}")
+    assert 0.0 < e_stored <= 1e-12 and e_exact <= 1e-12, (e_stored, e_exact)
+    out = torch.empty_like(v)
+    g = fast.capture(v, out)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, mf)
