@@ -77,8 +77,9 @@ def sweep_bytes(pc, layout, kind, sweeps, fused_init, f_tile=False, f_solve=Fals
     fuse_g = bool(getattr(pc, "fuse_g", False))
     out = []
     if stencil and fast and cheb and f_solve:
-        kname = ("k_fsolve (a whole F Chebyshev solve -- x0 and %d sweeps -- in one launch on 64 x 8 tiles, "
-                 "matrix-free, tolerance mode)" % (sweeps - 1))
+        w = int(getattr(getattr(pc, "kernel_opts", None), "f_solve_tile", 0)) == 1
+        kname = ("%s (a whole F Chebyshev solve -- x0 and %d sweeps -- in one launch on %s tiles, matrix-free, "
+                 "tolerance mode)" % ("k_fsolve_w" if w else "k_fsolve", sweeps - 1, "32 x 16" if w else "64 x 8"))
         for solve in (1, 2):
             gx = fuse_g and solve == 2
             rhs = nF // 4 * 8 if gx else nF * 8            # x_p (one field) or b (four)
@@ -597,7 +598,7 @@ def compact_line(line):
     out["config"] = cfg
     out["roofline"] = _roof(line.get("roofline"))
     if line.get("roofline") and line["roofline"].get("timing"):
-        out["roofline"]["timing"] = "HIP events on the apply stream around each k_fsolve launch (eager pass, K applies)"
+        out["roofline"]["timing"] = "HIP events on the apply stream around each whole-F-solve launch (eager pass, K applies)"
     r2 = line.get("roofline_second_f_solve")
     if isinstance(r2, dict) and r2.get("launches_timed"):
         out["roofline_second_f_solve"] = {"frac": _r(r2["frac"]), "bytes_per_launch": r2["bytes_per_launch"],

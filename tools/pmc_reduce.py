@@ -43,8 +43,9 @@ def main():
                "sell": ("k_sell_rows<(anonymous namespace)::EpiCheb>", grid),   # grid 4N: F rows, not Gt_G
                # round 4: the whole-solve F launch (the first solve: b streamed, no sub; the second: G x_p, sub), the
                # fused Gt_G solve and Gt_F_G on the diamond -- every kernel of the default apply but D
-               "fsolve": (("k_fsolve<3, false, false, (anonymous namespace)::BNone>",), None),
-               "fsolve_gx": (("k_fsolve<3, true, false, (anonymous namespace)::GxBT<false> >",), None),
+               # (round 6: k_fsolve_w, the 32 x 16 tile form -- kernel option f_solve_tile 1, the default)
+               "fsolve": (("k_fsolve_w<32, 16, 3, false, false, (anonymous namespace)::BNone>",), None),
+               "fsolve_gx": (("k_fsolve_w<32, 16, 3, true, false, (anonymous namespace)::GxBT<false> >",), None),
                "gtg_solve_drhs": (("k_gtg_solve<3, false, 512, true>",), None),      # the first: rhs = D Y + v_p inside
                "gtg_solve": (("k_gtg_solve<3, false, 512, false>",), None),
                "q13": (("k_q13<(anonymous namespace)::EpiStore, ",), None)}
