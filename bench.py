@@ -767,10 +767,10 @@ def partitioned_solver_section(args, n, rank, world, dist, torch, backend):
         bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
         A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
         # the partitioned hierarchy applies its level 1 from the stored Galerkin product; a one-GPU fast hierarchy
-        # defaults to R0 (F (P0 x)) (the same operator, other roundings): compare against the stored form, with
-        # Gt_F_G's full rows as the partition multiplies them
+        # defaults to R0 (F (P0 x)) (the same operator, other roundings): compare against the stored form (Gt_F_G's
+        # symmetric half on both sides)
         pc1 = mp.ApproxSchurPreconditioner(F, D, G, numerics=snum, **mg1,
-                                           kernel_opts={"mg_galerkin_mf": 0, "mg_galerkin_mf_p": 0, "q13_sym": 0, "q13_mf": 0})
+                                           kernel_opts={"mg_galerkin_mf": 0, "mg_galerkin_mf_p": 0, "q13_mf": 0})
         h1 = []
         mp.fgmres(A, torch.from_numpy(b).cuda(), M=pc1, tol=1e-8, maxiter=150, residuals=h1)
         same[0] = 1 if np.array_equal(np.asarray(h1), np.asarray(hist)) else 0
@@ -808,9 +808,9 @@ def single_gpu_check(dpc, n, args, iF, iP, rank, dist, torch):
     t0 = time.perf_counter()
     bp = mp.MultiphaseBlockPreconditioner(n, args.xi, args.eta_n, args.eta_s)
     _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
-    # (the partition multiplies Gt_F_G's full rows: the one-GPU twin does too, q13_sym = 0)
+    # (the one-GPU default apply: the partition reads Gt_F_G's symmetric half over its row block as one GPU does)
     pc = mp.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, layout=args.layout, f_mode=args.f_mode,
-                                      pg_mode=args.pg_mode, numerics=args.numerics, kernel_opts={"q13_sym": 0, "q13_mf": 0})
+                                      pg_mode=args.pg_mode, numerics=args.numerics, kernel_opts={"q13_mf": 0})
     del F, D, G
     vg = torch.from_numpy(np.random.default_rng(2048).standard_normal(pc.shape[0])).cuda()
     gids = torch.from_numpy(dpc.local_to_global_rows()).cuda()

@@ -280,8 +280,10 @@ typedef struct mpbp_schur_plan {
     const double* diag_P_ext;        /* device, np_ext: diag(Gt_G) on owned + ghost rows */
     mpbp_halo_pair_fn halo_pair;     /* optional (CA schedule): both halves of v in one exchange
                                         (mpbp_halo_exchange_pair); NULL: two halo calls */
-    const double* q13;               /* optional (one GPU): Gt_F_G in the 13-point diamond layout
-                                        (mpbp_q13_build), used instead of GtFG / Qs_* when set */
+    const double* q13;               /* optional: Gt_F_G in the 13-point diamond layout (mpbp_q13_build), used
+                                        instead of GtFG / Qs_* when set.  Row partition (tolerance mode, q13_sym):
+                                        the diamond of grid rows p_part.r0 - 2 .. r0 + rows - 1 (mpbp_q13_build_rows),
+                                        read as its symmetric upper half -- the one-GPU k_q13<SYM> bits per row */
     int32_t q13_n;                   /* its grid size n */
     const mpbp_mg* mg_F;             /* inner_F.kind == MPBP_INNER_MG: F's hierarchy (level 0 = F; row-partitioned
                                         with part_levels >= 1 when halo is set) */
@@ -348,6 +350,9 @@ int mpbp_svl_cheb_step(const mpbp_svl* V, const mpbp_csr* A, const double* x_in,
 /* out[0] = max |Q(c, c + o) - Q(c + o, c)| over the diamond, out[1] = max |Q| (host doubles; synchronises the stream):
  * whether tolerance mode may read the symmetric half (mpbp_kernel_opts.q13_sym) for this product.  Setup. */
 int mpbp_q13_asymmetry(int32_t n, const double* vals, double* out, void* stream);
+/* mpbp_q13_build for a block of whole grid rows of Gt_F_G (a row partition's rows r0 - 2 .. r0 + L - 1, with global
+ * columns): Q's row i is grid row (row0 + i / n) mod n; vals[13 * Q->nrows], slot-major.  Setup: synchronises. */
+int mpbp_q13_build_rows(const mpbp_csr* Q, int32_t n, int32_t row0, double* vals, void* stream);
 int mpbp_q13_spmv(int32_t n, const double* vals, int32_t mode, const double* x, const double* z, double* y,
                   void* stream);
 

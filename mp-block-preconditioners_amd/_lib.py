@@ -247,6 +247,7 @@ _SIGNATURES = {
     "mpbp_set_mg_mf_transfer": ([c_int32], c_int),
     "mpbp_set_csr_table": ([c_int32], c_int),
     "mpbp_q13_build": ([POINTER(Csr), c_int32, c_void_p, c_void_p], c_int),
+    "mpbp_q13_build_rows": ([POINTER(Csr), c_int32, c_int32, c_void_p, c_void_p], c_int),
     "mpbp_svl_spmv": ([POINTER(Svl), POINTER(Csr), c_int32, _P, _P, _P, _P], c_int),
     "mpbp_svl_cheb_step": ([POINTER(Svl), POINTER(Csr), _P, _P, _P, c_double, c_double, _P, _P, _P, _P], c_int),
     "mpbp_q13_spmv": ([c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p], c_int),

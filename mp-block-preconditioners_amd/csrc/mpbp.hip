@@ -6300,11 +6300,14 @@ __device__ inline int q13_off(int d, int n) {   // periodic offset folded into [
     return (d >= -2 && d <= 2) ? d : 99;
 }
 
-__global__ void k_q13_fill(Csr Q, int32_t n, double* vals, int* bad) {
-    const int32_t N = n * n;
+// row0 (a row partition's block, mpbp_q13_build_rows): Q's row r is grid row (row0 + r / n) mod n, column r % n;
+// vals holds Q->nrows cells per slot
+__global__ void k_q13_fill(Csr Q, int32_t N, int32_t n, double* vals, int* bad, int32_t row0 = 0) {
     const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= N) return;
-    const int gr = r / n, gc = r - (r / n) * n;
+    int gr = row0 + r / n;
+    gr = ((gr % n) + n) % n;
+    const int gc = r - (r / n) * n;
     unsigned seen = 0;
     bool ok = Q.rp[r + 1] - Q.rp[r] == kQSlots;
     for (int32_t k = Q.rp[r]; ok && k < Q.rp[r + 1]; ++k) {
@@ -6364,6 +6367,61 @@ __global__ void __launch_bounds__(kBlock) k_q13(int32_t n, const double* __restr
             key[s] = rr * n + cc;
             pr[s] = v[s] * x[key[s]];
         }
+#pragma unroll
+        for (int round = 0; round < kQSlots; ++round) {
+#pragma unroll
+            for (int i = round & 1; i + 1 < kQSlots; i += 2) {
+                const bool sw = key[i] > key[i + 1];
+                const int32_t ka = key[i], kb = key[i + 1];
+                const double pa = pr[i], pb = pr[i + 1];
+                key[i] = sw ? kb : ka;
+                key[i + 1] = sw ? ka : kb;
+                pr[i] = sw ? pb : pa;
+                pr[i + 1] = sw ? pa : pb;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < kQSlots; ++s) acc += pr[s];
+    }
+    epi(cell, acc, pe);
+}
+
+// The symmetric-half read on a row partition (the owned grid rows [r0, r0 + L) of every rank): vals holds the diamond
+// of grid rows r0 - 2 .. r0 + L - 1 (L + 2 rows: the lower slots of the first owned rows come from the two rows above),
+// x the owned rows with h >= 2 ghost rows each side (ext_row layout).  Every value, product and the order of the sum
+// (slot order, or for cells whose diamond wraps the periodic edge the wrapped global column order) are k_q13<SYM>'s:
+// the rank's rows of the one-GPU result bit for bit.
+template <class Epi>
+__global__ void __launch_bounds__(kBlock) k_q13p(int32_t n, int32_t r0, int32_t L, int32_t h,
+                                                 const double* __restrict__ vals, const double* __restrict__ x, Epi epi) {
+    const int32_t M = (L + 2) * n;   // cells per slot of the row block
+    const int32_t cell = xcd_swizzle(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
+    if (cell >= L * n) return;
+    const typename Epi::P pe = epi.pre(cell);
+    const int lr = cell / n, gc = cell - (cell / n) * n, gr = r0 + lr;
+    const int32_t bc = (lr + 2) * n + gc;   // the cell in the row block
+    auto wrapc = [&](int c) { return c < 0 ? c + n : c >= n ? c - n : c; };
+    double v[kQSlots];
+#pragma unroll
+    for (int s = 6; s < kQSlots; ++s) v[s] = vals[(int64_t)s * M + bc];
+#pragma unroll
+    for (int s = 0; s < 6; ++s) v[s] = vals[(int64_t)(12 - s) * M + (lr + 2 + q13_dr(s)) * n + wrapc(gc + q13_dc(s))];
+    double pr[kQSlots];
+    int32_t key[kQSlots];
+#pragma unroll
+    for (int s = 0; s < kQSlots; ++s) {
+        const int cc = wrapc(gc + q13_dc(s));
+        int rr = gr + q13_dr(s);
+        rr = rr < 0 ? rr + n : rr >= n ? rr - n : rr;
+        key[s] = rr * n + cc;
+        pr[s] = v[s] * x[ext_row(1, 0, lr + q13_dr(s), L, h, n) + cc];
+    }
+    double acc = 0.0;
+    const bool wraps = gr < 2 || gr >= n - 2 || gc < 2 || gc >= n - 2;
+    if (!__any(wraps)) {
+#pragma unroll
+        for (int s = 0; s < kQSlots; ++s) acc += pr[s];
+    } else {
 #pragma unroll
         for (int round = 0; round < kQSlots; ++round) {
 #pragma unroll
@@ -6591,13 +6649,33 @@ int mpbp_q13_build(const mpbp_csr* Q, int32_t n, double* vals, void* stream) {
     int* bad = nullptr;
     MPBP_HIP(hipMallocAsync((void**)&bad, sizeof(int), st));
     MPBP_HIP(hipMemsetAsync(bad, 0, sizeof(int), st));
-    k_q13_fill<<<grid_for((int64_t)n * n), kBlock, 0, st>>>(to_csr(Q), n, vals, bad);
+    k_q13_fill<<<grid_for((int64_t)n * n), kBlock, 0, st>>>(to_csr(Q), n * n, n, vals, bad);
     MPBP_HIP(hipGetLastError());
     int nbad = 0;
     MPBP_HIP(hipMemcpyAsync(&nbad, bad, sizeof(int), hipMemcpyDeviceToHost, st));
     MPBP_HIP(hipFreeAsync(bad, st));
     MPBP_HIP(hipStreamSynchronize(st));
     if (nbad) return set_error(MPBP_ERR_ARG, "q13_build: %d rows are not the 13-point diamond", nbad);
+    return MPBP_OK;
+}
+
+int mpbp_q13_build_rows(const mpbp_csr* Q, int32_t n, int32_t row0, double* vals, void* stream) {
+    int rc = check_csr(Q);
+    if (rc) return rc;
+    if (n < 5 || Q->nrows < n || Q->nrows % n || Q->nrows > (n + 2) * n || (int64_t)Q->nrows > INT32_MAX / kQSlots ||
+        Q->ncols != n * n || !vals)
+        return set_error(MPBP_ERR_ARG, "q13_build_rows: needs whole grid rows of an n^2-column operator, n >= 5");
+    const hipStream_t st = as_stream(stream);
+    int* bad = nullptr;
+    MPBP_HIP(hipMallocAsync((void**)&bad, sizeof(int), st));
+    MPBP_HIP(hipMemsetAsync(bad, 0, sizeof(int), st));
+    k_q13_fill<<<grid_for((int64_t)Q->nrows), kBlock, 0, st>>>(to_csr(Q), Q->nrows, n, vals, bad, row0);
+    MPBP_HIP(hipGetLastError());
+    int nbad = 0;
+    MPBP_HIP(hipMemcpyAsync(&nbad, bad, sizeof(int), hipMemcpyDeviceToHost, st));
+    MPBP_HIP(hipFreeAsync(bad, st));
+    MPBP_HIP(hipStreamSynchronize(st));
+    if (nbad) return set_error(MPBP_ERR_ARG, "q13_build_rows: %d rows are not the 13-point diamond", nbad);
     return MPBP_OK;
 }
 
@@ -6926,6 +7004,20 @@ int two_phase(const Ctx& c, int32_t kind, const double* x_ext, const OpPair& op,
     if (rc) return rc;
     if (p->halo) p->halo(p->halo_ctx, kind, const_cast<double*>(x_ext), MPBP_HALO_END, (void*)c.st);
     return launch(op.bd);
+}
+
+// Tolerance mode on a row partition: Gt_F_G x_a from the diamond's upper half over the rank's row block (k_q13p; the
+// plan's q13 then holds grid rows p_part.r0 - 2 .. r0 + rows - 1, mpbp_q13_build_rows), x_a's ghost rows complete.
+bool q13p_ok(const mpbp_schur_plan* p) {
+    return p->q13 && p->halo && KO().q13_sym && p->f_numerics == MPBP_NUMERICS_FAST && p->q13_n >= 5 &&
+           p->p_part.halo >= 2 && p->p_part.rows >= 1 && p->np == p->p_part.rows * p->q13_n;
+}
+template <class Epi>
+int launch_q13p(const mpbp_schur_plan* p, const double* x_ext, Epi epi, hipStream_t st) {
+    const int32_t n = p->q13_n, L = p->p_part.rows;
+    k_q13p<Epi><<<grid_for((int64_t)L * n), kBlock, 0, st>>>(n, p->p_part.r0, L, p->p_part.halo, p->q13, x_ext, epi);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
 }
 
 // ---- geometric multigrid inner solve (MPBP_INNER_MG) ----
@@ -7872,9 +7964,14 @@ int schur_apply_ca(const Ctx& c, const double* v, double* out) {
     rc = ca_inner_solve(c, SOP_GTG, Prhs, p->diag_P_ext, p->inner_P, p->np_ext, Pxa, nullptr, P0, P1, Pd, d_xa, false);
     if (rc) return rc;
     // 4. x_b = Gt_F_G x_a on the owned rows (its columns reach q ghost rows)  solve.py:267
-    const OpPair Q = make_op(p, p->GtFG, p->Q_int, p->Q_bnd, p->Qs_int, p->Qs_bnd);
-    rc = op_spmv(Q.in, MPBP_SPMV_STORE, Pxa, nullptr, Pxb, c.st);
-    if (!rc) rc = op_spmv(Q.bd, MPBP_SPMV_STORE, Pxa, nullptr, Pxb, c.st);
+    //    (tolerance mode: the diamond's upper half over the rank's row block, as k_q13<SYM> on one GPU)
+    if (q13p_ok(p)) {
+        rc = launch_q13p(p, Pxa, EpiStore{Pxb}, c.st);
+    } else {
+        const OpPair Q = make_op(p, p->GtFG, p->Q_int, p->Q_bnd, p->Qs_int, p->Qs_bnd);
+        rc = op_spmv(Q.in, MPBP_SPMV_STORE, Pxa, nullptr, Pxb, c.st);
+        if (!rc) rc = op_spmv(Q.bd, MPBP_SPMV_STORE, Pxa, nullptr, Pxb, c.st);
+    }
     if (rc) return rc;
     ca_exchange(c, MPBP_VEC_PRESSURE, Pxb);
     // 5. x_p = Gt_G^-1 x_b on owned + d_xp ghost rows                         solve.py:271
@@ -8003,7 +8100,10 @@ extern "C" int mpbp_schur_apply(const mpbp_schur_plan* p, const double* v, doubl
         rc = launch_qmf(p, Pxa, EpiStore{Pxb}, c.st);
     else if (p->q13 && !p->halo)   // tolerance mode: the symmetric product's upper half (k_q13<SYM>)
         rc = launch_q13(p->q13_n, p->q13, Pxa, EpiStore{Pxb}, c.st, KO().q13_sym && p->f_numerics == MPBP_NUMERICS_FAST);
-    else
+    else if (q13p_ok(p)) {         // ... and on a row partition: x_a's ghost rows first, then the rank's rows
+        ca_exchange(c, MPBP_VEC_PRESSURE, Pxa);
+        rc = launch_q13p(p, Pxa, EpiStore{Pxb}, c.st);
+    } else
         rc = two_phase(c, MPBP_VEC_PRESSURE, Pxa, Q,
                        [&](const OpRef& o) { return op_spmv(o, MPBP_SPMV_STORE, Pxa, nullptr, Pxb, c.st); });
     if (rc) return rc;

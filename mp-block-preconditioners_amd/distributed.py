@@ -978,6 +978,41 @@ class DistributedMatrix:
         return self.part.owned_rows(self.nfields)
 
 
+def _csr_vstack(A: DeviceCSR, B: DeviceCSR) -> DeviceCSR:
+    """The rows of A, then the rows of B (same column count), as one CSR."""
+    rp = torch.cat([A.row_ptr[:-1], B.row_ptr + A.nnz])
+    return DeviceCSR(rp.contiguous(), torch.cat([A.col_idx, B.col_idx]), torch.cat([A.val, B.val]),
+                     (A.shape[0] + B.shape[0], A.shape[1]))
+
+
+def _q13_block(Q: DeviceCSR, n: int, part, group, red_dev):
+    """(n, vals, symmetric) for a row partition: Gt_F_G's diamond over grid rows r0 - 2 .. r0 + L - 1 (Q: those rows
+    with global columns, mpbp_q13_build_rows) and whether the product is symmetric to 1e-14 of its largest entry over
+    every rank's owned rows (slot s at a cell against slot 12 - s at its neighbour (dr_s, dc_s) -- mpbp_q13_asymmetry's
+    test, reduced over the ranks).  None when Q's rows are not the 13-point diamond."""
+    import torch.distributed as dist
+    L = part.L
+    vals = torch.empty(13 * (L + 2) * n, dtype=torch.float64, device=Q.device)
+    if lib().mpbp_q13_build_rows(ctypes.byref(Q.cstruct()), n, part.r0 - 2, ptr(vals), stream_handle()) != 0:
+        ok = torch.tensor([0.0], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MAX, group=group)   # (the same collective on every rank)
+        dist.all_reduce(ok, op=dist.ReduceOp.MAX, group=group)
+        return None
+    V = vals.view(13, L + 2, n)
+    amax = V[:, 2:, :].abs().max()
+    asym = torch.zeros((), dtype=torch.float64, device=Q.device)
+    dr = (-2, -1, -1, -1, 0, 0)
+    dc = (0, -1, 0, 1, -2, -1)
+    for s in range(6):
+        nb = torch.roll(V[12 - s, 2 + dr[s]: 2 + dr[s] + L, :], shifts=-dc[s], dims=1)
+        asym = torch.maximum(asym, (V[s, 2:, :] - nb).abs().max())
+    a = torch.stack([asym, amax]).to(red_dev)
+    dist.all_reduce(a[0:1], op=dist.ReduceOp.MAX, group=group)
+    dist.all_reduce(a[1:2], op=dist.ReduceOp.MAX, group=group)
+    a = a.cpu()
+    return n, vals, bool(a[0] <= 1e-14 * a[1])
+
+
 class DistributedSchurPreconditioner(PlanProfiling):
     """The approximate-commutator apply over a row partition of the grid (one rank per GPU).
 
@@ -1000,8 +1035,8 @@ class DistributedSchurPreconditioner(PlanProfiling):
         from .preconditioner import MultiphaseBlockPreconditioner
         from .solve import InnerSolver, _check_numerics
         self.numerics = _check_numerics(numerics)
-        # this preconditioner's kernel choices (process defaults now + overrides); q13_sym does not apply here: the
-        # partition multiplies Gt_F_G's full rows
+        # this preconditioner's kernel choices (process defaults now + overrides): tolerance mode reads Gt_F_G's
+        # symmetric half over the rank's row block (q13_sym, as one GPU); q13_mf is one-GPU only
         self.kernel_opts = _lib.kernel_opts(kernel_opts)
         # setup phase timings (MPBP_SETUP_TIMING=1: synchronise and stamp each phase; tools/setup_timing.py)
         self.setup_phases = {}
@@ -1052,12 +1087,37 @@ class DistributedSchurPreconditioner(PlanProfiling):
             GtG, GtFG = bp.commutator_products(Fs, D, Gs)   # this rank's pressure rows, global columns
             _stamp("commutator_products")
             GtG.stencil = _gtg_stencil(D, G)
+            # tolerance mode: the two pressure grid rows above the owned block too (their products' rows, bit for bit
+            # the global product's), so the symmetric-half read has the lower slots of the first owned rows
+            q_rows = None
+            if self.numerics == "fast" and part.ghosts and part.L < n:
+                q_rows = GtFG
+                for k in (1, 2):   # (one grid row per assembly: the wrapped rows need not ascend)
+                    row = torch.from_numpy((((part.r0 - k) % n) * n + np.arange(n)).astype(np.int32)).to(dev)
+                    D1 = bp.assemble_rows(_lib.OP_D, row, **akw)
+                    q_rows = _csr_vstack(spgemm(spgemm(D1, Fs, alpha=-1.0), Gs, alpha=1.0), q_rows)
+                del D1
             del Fs
         else:
             _, _, F, D, G = bp.get_big_A_matrix(**akw)
             _stamp("assemble_global")
             GtG, GtFG = bp.commutator_products(F, D, G)
             _stamp("commutator_products")
+            q_rows = None
+            if self.numerics == "fast" and part.ghosts:   # grid rows r0 - 2 .. r0 + L - 1 of the global product
+                blk = np.concatenate([((part.r0 + k) % n) * n + np.arange(n) for k in range(-2, part.L)]).astype(np.int32)
+                q_rows = GtFG.extract(torch.from_numpy(blk).to(dev),
+                                      torch.arange(GtFG.shape[1], dtype=torch.int32, device=dev), GtFG.shape[1])
+        # Gt_F_G's diamond over the rank's row block, read from its symmetric upper half (k_q13p) when the product is
+        # symmetric to 1e-14 of its largest entry -- decided over all ranks, as one GPU decides over the whole grid
+        self.q13 = None
+        if q_rows is not None and n >= 5:
+            self.q13 = _q13_block(q_rows, n, part, group, dev if backend == "nccl" else "cpu")
+            if self.q13 is None or not self.q13[2]:
+                self.kernel_opts.q13_sym = 0
+        else:
+            self.kernel_opts.q13_sym = 0
+        del q_rows
         lp = self.local_products
         if f_mode not in ("auto", "stencil", "assembled"):
             raise ValueError("f_mode must be 'auto', 'stencil' or 'assembled'")
@@ -1288,6 +1348,8 @@ class DistributedSchurPreconditioner(PlanProfiling):
         # then one launch per sweep
         p.halo_first = 1 if (self._rccl is not None and not self._rccl.overlap) else 0
         p.ca, p.ca_reach_q = (1 if self.ca else 0), self.ca_q
+        if self.q13 is not None:
+            p.q13, p.q13_n = self.q13[1].data_ptr(), self.q13[0]
         p.fuse_g = 1 if self.fuse_g else 0
         p.f_numerics = _lib.NUMERICS_FAST if self.numerics == "fast" else _lib.NUMERICS_EXACT
         p.opts = ctypes.pointer(self.kernel_opts)

@@ -35,13 +35,15 @@ def _worker(rank, world, port, n, layout, f_mode, kind, errfile, ca="auto", fuse
         assert (dpc.f_stencil is not None) == (f_mode != "assembled")
         if ca is True:
             assert dpc.ca and dpc.h_u == dpc.ca_q + 2 + 1 + 3, (dpc.h_u, dpc.ca_q)
+        if numerics == "fast" and n >= 5:   # Gt_F_G's symmetric half over the rank's row block (k_q13p), as one GPU
+            assert dpc.q13 is not None and dpc.kernel_opts.q13_sym == 1
         bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
         _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
         # the reference: the assembled one-GPU apply (exact numerics), or the one-GPU apply with the same fast rows
-        # (the partition multiplies Gt_F_G's full rows: so does the one-GPU reference, q13_sym = 0)
+        # (the partition reads Gt_F_G's symmetric half over its row block, as the one-GPU default does)
         pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, layout=layout,
                                            f_mode="assembled" if numerics == "exact" else "stencil", numerics=numerics,
-                                           kernel_opts={"q13_sym": 0, "q13_mf": 0})
+                                           kernel_opts={"q13_mf": 0})
         assert (pc.inner_F.lmin, pc.inner_F.lmax) == (dpc.inner_F.lmin, dpc.inner_F.lmax)
         v = torch.from_numpy(np.random.default_rng(5).standard_normal(pc.shape[0])).cuda()
         gids = torch.from_numpy(dpc.local_to_global_rows()).cuda()
@@ -289,7 +291,7 @@ def _inner_pair(spec):
     return mpb.InnerSolver(kf, sf), mpb.InnerSolver(kp, sp)
 
 
-FAST_TWIN = {"mg_galerkin_mf": 0, "mg_galerkin_mf_p": 0, "q13_sym": 0, "q13_mf": 0}   # the partition's level-1 and Gt_F_G forms
+FAST_TWIN = {"mg_galerkin_mf": 0, "mg_galerkin_mf_p": 0}   # the partition's level-1 form (its stored Galerkin product)
 
 
 def _mg_worker(rank, world, port, n, inner, min_cells, halo, errfile, numerics="exact"):
@@ -506,7 +508,7 @@ def _configs4_worker(rank, world, port, n, errfile, numerics="exact"):
                 bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
                 _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
                 pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, numerics=numerics,
-                                                   kernel_opts={"q13_sym": 0, "q13_mf": 0})   # (the partition's full Gt_F_G rows)
+                                                   kernel_opts={"q13_mf": 0})   # (the stored Gt_F_G, as the partition)
                 ref = pc.apply(v)[gids]
                 assert torch.equal(got, ref), float((got - ref).abs().max())
                 del pc, F, D, G, bp, ref
