@@ -504,7 +504,10 @@ typedef struct mpbp_kernel_opts {
     int32_t q13_mf;            /* tolerance mode, one GPU, matrix-free F / D / G: x_b = Gt_F_G x_a applied as its factors
                                   -(D (F (G x_a))) on 32 x 16 tiles (k_qmf; 42 instead of 76 MB per apply at 1024^2),
                                   not the stored product (1); 0: the stored product (k_q13) */
-    int32_t reserved[3];
+    int32_t mg_fuse_small;     /* whole-grid multigrid levels l >= 1 on k_csr_grp rows (<= mg_group_rows) with matrix-free
+                                  transfers and a coarse level of <= 1024 rows: residual + restriction as ONE launch
+                                  (k_grp_rr; 1, default; the same bits as 0) */
+    int32_t reserved[2];
 } mpbp_kernel_opts;
 /* *out = the calling thread's current choices: its mpbp_kernel_opts_set_thread scope, else the process defaults. */
 void mpbp_kernel_opts_default(mpbp_kernel_opts* out);

@@ -85,7 +85,8 @@ class KernelOpts(Structure):
                 ("f_tile", c_int32), ("f_solve", c_int32), ("mg_galerkin_mf", c_int32), ("mg_galerkin_mf_p", c_int32),
                 ("pg_direct", c_int32), ("mg_group_rows", c_int32), ("mg_svl", c_int32), ("mg_mf_transfer", c_int32),
                 ("csr_table", c_int32), ("mg_fuse_l0", c_int32), ("mg_coarse_tree", c_int32),
-                ("f_solve_tile", c_int32), ("q13_mf", c_int32), ("reserved", c_int32 * 3)]
+                ("f_solve_tile", c_int32), ("q13_mf", c_int32), ("mg_fuse_small", c_int32),
+                ("reserved", c_int32 * 2)]
 
 
 def kernel_opts(overrides=None) -> KernelOpts:

@@ -28,7 +28,7 @@ mpbp_kernel_opts g_defaults = {
     /*march_rows*/ 0, /*init_diag*/ 1, /*f_pair*/ 1, /*f_direct*/ 0, /*gtg_fused*/ 1, /*gtg_tpb*/ 512, /*gtg_drhs*/ 1,
     /*q13_sym*/ 1, /*f_tile*/ 1, /*f_solve*/ 1, /*mg_galerkin_mf*/ 2, /*mg_galerkin_mf_p*/ 1, /*pg_direct*/ 1,
     /*mg_group_rows*/ 65536, /*mg_svl*/ 1, /*mg_mf_transfer*/ 1, /*csr_table*/ 1, /*mg_fuse_l0*/ 1,
-    /*mg_coarse_tree*/ 0, /*f_solve_tile*/ 1, /*q13_mf*/ 0, {0, 0, 0}};
+    /*mg_coarse_tree*/ 0, /*f_solve_tile*/ 1, /*q13_mf*/ 0, /*mg_fuse_small*/ 1, {0, 0}};
 thread_local const mpbp_kernel_opts* t_opts = nullptr;
 inline const mpbp_kernel_opts& KO() { return t_opts ? *t_opts : g_defaults; }
 struct OptsScope {   // installs a plan's kernel choices (when it has its own) for one entry-point call
@@ -48,10 +48,10 @@ inline int check_opts(const mpbp_kernel_opts* o, const char* who) {
                     o->mg_galerkin_mf >= 0 && o->mg_galerkin_mf <= 2 && o->mg_group_rows >= 0 &&
                     (o->init_diag | o->f_pair | o->f_direct | o->gtg_fused | o->gtg_drhs | o->q13_sym | o->f_tile |
                      o->f_solve | o->mg_galerkin_mf_p | o->pg_direct | o->mg_svl | o->mg_mf_transfer | o->csr_table |
-                     o->mg_fuse_l0 | o->mg_coarse_tree | o->q13_mf) >= 0 &&
+                     o->mg_fuse_l0 | o->mg_coarse_tree | o->q13_mf | o->mg_fuse_small) >= 0 &&
                     (o->init_diag | o->f_pair | o->f_direct | o->gtg_fused | o->gtg_drhs | o->q13_sym | o->f_tile |
                      o->f_solve | o->mg_galerkin_mf_p | o->pg_direct | o->mg_svl | o->mg_mf_transfer | o->csr_table |
-                     o->mg_fuse_l0 | o->mg_coarse_tree | o->q13_mf) <= 1;
+                     o->mg_fuse_l0 | o->mg_coarse_tree | o->q13_mf | o->mg_fuse_small) <= 1;
     return ok ? MPBP_OK : set_error(MPBP_ERR_ARG, "%s: kernel options out of range", who);
 }   // rows per workgroup of the D / G / Gt_G marching kernels: as F
 
@@ -704,27 +704,40 @@ __device__ inline int mg_r1d_fast(int kind, int nf, int i, int* idx, double* w) 
 struct MgDiv {
     DivU per, nr;   // rows per field, grid size of the rows' level
 };
+// Row `row` of T = P (rows = fine unknowns) or R (rows = coarse unknowns) of the n x n fine grid: its field, the 1D
+// lists of both directions and the columns' field offset (nk = the columns' grid size).  The one place the matrix-free
+// transfers build a row, so every kernel that folds a transfer in takes the same lists in the same order.
+struct MgRow {
+    int my, mx, nk, off;
+    int yi[4], xi[4];
+    double yw[4], xw[4];
+};
+__device__ inline void mg_row(const MgFields& F, const MgDiv& dv, int32_t n, int32_t which, int32_t row, MgRow& T) {
+    const int nc = n / 2;
+    const int nr = which == MPBP_MG_P ? n : nc;
+    T.nk = which == MPBP_MG_P ? nc : n;
+    const uint32_t per = (uint32_t)nr * (uint32_t)nr;
+    const int fld = (int)divu((uint32_t)row, dv.per);
+    const uint32_t cell = (uint32_t)row - (uint32_t)fld * per;
+    const int r = (int)divu(cell, dv.nr), c = (int)(cell - (uint32_t)r * (uint32_t)nr);
+    T.my = which == MPBP_MG_P ? mg_p1d_fast(F.ky[fld], nc, r, T.yi, T.yw) : mg_r1d_fast(F.ky[fld], n, r, T.yi, T.yw);
+    T.mx = which == MPBP_MG_P ? mg_p1d_fast(F.kx[fld], nc, c, T.xi, T.xw) : mg_r1d_fast(F.kx[fld], n, c, T.xi, T.xw);
+    T.off = fld * T.nk * T.nk;
+}
 template <class Epi>
 __global__ void __launch_bounds__(kBlock) k_mg_transfer_spmv(MgFields F, MgDiv dv, int32_t n, int32_t which,
                                                              int32_t nrows, const double* __restrict__ x, Epi epi) {
     const int32_t row = (int32_t)(blockIdx.x * kBlock + threadIdx.x);
     if (row >= nrows) return;
     const typename Epi::P pe = epi.pre(row);
-    const int nc = n / 2;
-    const int nr = which == MPBP_MG_P ? n : nc;
-    const int nk = which == MPBP_MG_P ? nc : n;
-    const uint32_t per = (uint32_t)nr * (uint32_t)nr;
-    const int fld = (int)divu((uint32_t)row, dv.per);
-    const uint32_t cell = (uint32_t)row - (uint32_t)fld * per;
-    const int r = (int)divu(cell, dv.nr), c = (int)(cell - (uint32_t)r * (uint32_t)nr);
-    int yi[4], xi[4];
-    double yw[4], xw[4];
-    const int my = which == MPBP_MG_P ? mg_p1d_fast(F.ky[fld], nc, r, yi, yw) : mg_r1d_fast(F.ky[fld], n, r, yi, yw);
-    const int mx = which == MPBP_MG_P ? mg_p1d_fast(F.kx[fld], nc, c, xi, xw) : mg_r1d_fast(F.kx[fld], n, c, xi, xw);
-    const int32_t off = fld * nk * nk;
+    MgRow T;
+    mg_row(F, dv, n, which, row, T);
     double acc = 0.0;
-    for (int a = 0; a < my; ++a)
-        for (int b = 0; b < mx; ++b) acc += (yw[a] * xw[b]) * x[off + yi[a] * nk + xi[b]];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)   // (constant trip counts keep the lists in registers)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            if (a < T.my && b < T.mx) acc += (T.yw[a] * T.xw[b]) * x[T.off + T.yi[a] * T.nk + T.xi[b]];
     epi(row, acc, pe);
 }
 
@@ -4889,6 +4902,73 @@ int grp_cheb_first(const mpbp_csr* A, const double* b, const double* dg, double 
     return launch_grp(A, XInit{b, dg, c2_0}, e, st);
 }
 
+// ---- small multigrid levels with their transfers folded in (kernel option mg_fuse_small) ----
+// b_c = R (b - A x) in one launch, one wave per coarse row I: four lanes per fine row of R's row (<= 4 x 4 of them)
+// gather that row's CSR entries at once and the slot's first lane adds the products left to right from 0.0 (k_csr_grp's
+// sum) and forms b_j - sum (EpiResid); the wave's first lane then adds R's products (yw xw) r_j in list order
+// (k_mg_transfer_spmv's restriction).  The residual and restriction launches' operations, bit for bit, without r's
+// store and reload.  A fine row shared by neighbouring coarse rows is recomputed by each (up to 4x), so it pays only
+// where the two launches are latency-bound: coarse levels of <= kRrMaxCoarse rows (1024^2, mg:1, profiles/
+// r06l_mg_apply_kernel_trace.md: 7.3 vs 5.0 + 4.9 us into 1024 coarse rows, 6.6 vs ~9.8 into 256; into 4096, 10.4 vs
+// 5.1 + 4.9; into 16384, 32 vs 11 + 5).  Folding the prolongation into the first post-smoothing sweep's gathers
+// (x + P x_c per gathered column: five loads instead of one) measured slower than its two launches at every level
+// (10-31 vs 9-17 us) and is not kept.
+constexpr int32_t kRrMaxCoarse = 1024;
+constexpr int kRrL = 4, kRrJ = 12, kRrCap = kRrL * kRrJ;   // lanes per fine row, entries per lane and chunk
+__device__ inline int sel4(const int* v, int i) { return i == 0 ? v[0] : i == 1 ? v[1] : i == 2 ? v[2] : v[3]; }
+__global__ void __launch_bounds__(kBlock) k_grp_rr(Csr A, MgFields F, MgDiv dv, int32_t n, int32_t ncr,
+                                                  const double* __restrict__ x, const double* __restrict__ b,
+                                                  double* __restrict__ bc) {
+    constexpr int WPB = kBlock / 64;
+    __shared__ double prod[WPB * 16 * kRrCap];
+    __shared__ double rs[WPB * 16];
+    const int w = threadIdx.x / 64, lane = threadIdx.x % 64, s = lane / kRrL, k = lane % kRrL;
+    const int32_t I = blockIdx.x * WPB + w;   // wave-uniform: a wave past the last coarse row leaves whole
+    if (I >= ncr) return;
+    MgRow R;
+    mg_row(F, dv, n, MPBP_MG_R, I, R);
+    const bool live = s < R.my * R.mx;
+    const int a = live ? (s >= R.mx) + (s >= 2 * R.mx) + (s >= 3 * R.mx) : 0, c = s - a * R.mx;
+    const int32_t j = live ? R.off + sel4(R.yi, a) * n + sel4(R.xi, c) : 0;
+    const int32_t ks = A.rp[j], ke = live ? A.rp[j + 1] : ks;
+    const double bj = (live && k == 0) ? b[j] : 0.0;
+    double* pr = prod + (w * 16 + s) * kRrCap;
+    double acc = 0.0;
+    for (int32_t cb = ks; cb < ke; cb += kRrCap) {
+        double v[kRrJ];
+        int32_t ci[kRrJ];
+#pragma unroll
+        for (int u = 0; u < kRrJ; ++u) {
+            const int32_t e = cb + k + kRrL * u;
+            const bool in = e < ke;
+            v[u] = in ? A.va[e] : 0.0;
+            ci[u] = in ? A.ci[e] : 0;
+        }
+        double p[kRrJ];
+#pragma unroll
+        for (int u = 0; u < kRrJ; ++u) p[u] = v[u] * x[ci[u]];
+        if (cb != ks) wave_lds_sync();   // the previous chunk's sums have read their slots
+#pragma unroll
+        for (int u = 0; u < kRrJ; ++u) pr[k + kRrL * u] = p[u];
+        wave_lds_sync();
+        if (k == 0) {
+            const int32_t cnt = min(ke - cb, (int32_t)kRrCap);
+            for (int32_t e = 0; e < cnt; ++e) acc += pr[e];
+        }
+    }
+    if (live && k == 0) rs[w * 16 + s] = bj - acc;
+    wave_lds_sync();
+    if (lane == 0) {
+        double r = 0.0;
+#pragma unroll
+        for (int ya = 0; ya < 4; ++ya)
+#pragma unroll
+            for (int xb = 0; xb < 4; ++xb)
+                if (ya < R.my && xb < R.mx) r += (R.yw[ya] * R.xw[xb]) * rs[w * 16 + ya * R.mx + xb];
+        bc[I] = r;
+    }
+}
+
 // Products through the stencil-values layout (k_svl).
 inline Svl to_svl(const mpbp_svl* V) {
     return Svl{V->nfields, V->m, V->reach, V->slots, V->delta, V->vals, V->edge_rows, V->n_edge};
@@ -7072,28 +7152,49 @@ void mg_exchange(const mpbp_mg* m, int l, const MgFine& f, double* x, hipStream_
         m->halo(m->halo_ctx, m->levels[l].halo_kind, x, MPBP_HALO_END, (void*)st);
     }
 }
+MgFields mg_fields(const mpbp_mg* m) {
+    MgFields F{};
+    F.nfields = m->tr_nfields;
+    for (int f = 0; f < m->tr_nfields; ++f) {
+        F.ky[f] = m->tr_ky[f];
+        F.kx[f] = m->tr_kx[f];
+    }
+    return F;
+}
+inline MgDiv mg_div(int32_t nr) { return MgDiv{divu((uint32_t)nr * (uint32_t)nr), divu((uint32_t)nr)}; }
 // Level l's restriction (which = MPBP_MG_R) or prolongation (MPBP_MG_P) matrix-free when the hierarchy names its
 // field kinds and the level is whole-grid (not row-partitioned); 1: launched, 0: not applicable.
 template <class Epi>
 int mg_transfer_mf(const mpbp_mg* m, int l, int32_t which, int32_t nrows, const double* x, Epi epi, hipStream_t st) {
     const int32_t n = m->tr_n0 >> l, nr = which == MPBP_MG_P ? n : n / 2;
-    k_mg_transfer_spmv<Epi><<<grid_for(nrows), kBlock, 0, st>>>(
-        [&] {
-            MgFields F{};
-            F.nfields = m->tr_nfields;
-            for (int f = 0; f < m->tr_nfields; ++f) {
-                F.ky[f] = m->tr_ky[f];
-                F.kx[f] = m->tr_kx[f];
-            }
-            return F;
-        }(),
-        MgDiv{divu((uint32_t)nr * (uint32_t)nr), divu((uint32_t)nr)}, n, which, nrows, x, epi);
+    k_mg_transfer_spmv<Epi><<<grid_for(nrows), kBlock, 0, st>>>(mg_fields(m), mg_div(nr), n, which, nrows, x, epi);
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
 }
 inline bool use_mf_transfer(const mpbp_mg* m, int l) {
     return KO().mg_mf_transfer && m->tr_nfields > 0 && m->tr_nfields <= 8 && l >= m->part_levels && (m->tr_n0 >> l) >= 4 &&
            ((m->tr_n0 >> l) << l) == m->tr_n0;
+}
+// Kernel option mg_fuse_small (k_grp_rr): level l >= 1 of a hierarchy held whole on this GPU (one GPU, or a level every
+// rank replicates), its operator on k_csr_grp rows, its transfers matrix-free with the level sizes the transfers imply,
+// the coarse level at most kRrMaxCoarse rows.
+bool mg_small_ok(const mpbp_mg* m, int l, const OpPair& o) {
+    if (!KO().mg_fuse_small || l < 1 || l < m->part_levels || l + 1 >= m->nlevels || !o.in.grp || !o.in.csr ||
+        o.in.gal || !o.bd.empty || !use_mf_transfer(m, l))
+        return false;
+    const int64_t n = m->tr_n0 >> l, rows = (int64_t)m->tr_nfields * n * n;
+    const mpbp_csr& A = *o.in.csr;
+    return A.nrows == rows && A.ncols == rows && m->levels[l].nrows == rows && m->levels[l + 1].nrows == rows / 4 &&
+           rows / 4 <= kRrMaxCoarse;
+}
+int launch_grp_rr(const mpbp_mg* m, int l, const mpbp_csr* A, const double* x, const double* b, double* bc,
+                  hipStream_t st) {
+    const int32_t n = m->tr_n0 >> l, ncr = m->tr_nfields * (n / 2) * (n / 2);
+    constexpr int WPB = kBlock / 64;
+    k_grp_rr<<<(unsigned)((ncr + WPB - 1) / WPB), kBlock, 0, st>>>(to_csr(A), mg_fields(m), mg_div(n / 2), n, ncr, x, b,
+                                                                 bc);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
 }
 int mg_transfer(const mpbp_csr& M, const mpbp_rowblocks& blk, const mpbp_sell& S, int32_t mode, const double* x,
                 const double* z, double* y, hipStream_t st) {
@@ -7395,6 +7496,7 @@ int mg_vcycle(const mpbp_mg* m, int l, const MgFine& fine, const double* b, bool
     auto xch = [&](double* v) { mg_exchange(m, l, fine, v, st); };
     const mpbp_mg_level& C = m->levels[l + 1];
     const bool gather = m->part_levels > 0 && l + 1 == m->part_levels;
+    const bool small = mg_small_ok(m, l, o);   // (never a gathering level: l >= part_levels)
     int rc = MPBP_OK;
     if (top && zero && L.pre == 2 && fpre_ok(m, fine)) {
         // x0, sweep 1, r = b - A x and b_c = R r in one launch; x1 where the smoothing would leave it (the free buffer)
@@ -7411,14 +7513,17 @@ int mg_vcycle(const mpbp_mg* m, int l, const MgFine& fine, const double* b, bool
         rc = mg_smooth(o, L.nrows, diag, L.lmin, L.lmax, L.pre, zero, b, &cur, alt, d, nullptr, nullptr, st, xch);
         if (rc) return rc;
         alt = cur == bx ? bt : bx;
-        // r = b - A x ; b_c = R r
-        xch(cur);
-        rc = pair_spmv(o, MPBP_SPMV_RESID, cur, b, r, st);
-        if (rc) return rc;
-        if (l < m->part_levels) xch(r);
-        rc = use_mf_transfer(m, l) ? mg_transfer_mf(m, l, MPBP_MG_R, L.R.nrows, r, EpiStore{gather ? C.r : C.b}, st)
-                                   : mg_transfer(L.R, L.R_blocks, L.R_sell, MPBP_SPMV_STORE, r, nullptr, gather ? C.r : C.b,
-                                                 st);
+        if (small) {   // r = b - A x and b_c = R r in one launch (k_grp_rr)
+            rc = launch_grp_rr(m, l, o.in.csr, cur, b, C.b, st);
+        } else {       // r = b - A x ; b_c = R r
+            xch(cur);
+            rc = pair_spmv(o, MPBP_SPMV_RESID, cur, b, r, st);
+            if (rc) return rc;
+            if (l < m->part_levels) xch(r);
+            rc = use_mf_transfer(m, l) ? mg_transfer_mf(m, l, MPBP_MG_R, L.R.nrows, r, EpiStore{gather ? C.r : C.b}, st)
+                                       : mg_transfer(L.R, L.R_blocks, L.R_sell, MPBP_SPMV_STORE, r, nullptr,
+                                                     gather ? C.r : C.b, st);
+        }
         if (rc) return rc;
     }
     if (gather) {

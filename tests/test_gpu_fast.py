@@ -489,3 +489,31 @@ def test_fused_level0_descent_equals_launches(n, cycles, numerics):
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("n", [64, 128, 256])
+@pytest.mark.parametrize("cycles", [1, 2])
+@pytest.mark.parametrize("numerics", ["fast", "exact"])
+def test_small_level_fusion_equals_launches(n, cycles, numerics):
+    """Kernel option mg_fuse_small (default on): on the grouped small levels (l >= 1, <= mg_group_rows rows, matrix-free
+    transfers, <= 1024 coarse rows) the residual and restriction run as ONE k_grp_rr launch -- the operations of the two
+    launches it replaces, so the Schur apply with multigrid inner solves is bit-identical either way, eagerly and
+    replayed (tests/test_gpu_mg.py pins both forms against oracle/mg_oracle.py)."""
+    mp = _mp()
+    bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
+    _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
+    pc = mp.ApproxSchurPreconditioner(F, D, G, numerics=numerics, inner_F=mp.InnerSolver("mg", cycles),
+                                      inner_P=mp.InnerSolver("mg", cycles))
+    assert pc.kernel_opts.mg_fuse_small == 1
+    v = torch.randn(pc.shape[0], dtype=torch.float64, device="cuda",
+                    generator=torch.Generator(device="cuda").manual_seed(3 * n + cycles))
+    fused = pc.apply(v).clone()
+    pc.set_kernel_opts(mg_fuse_small=0)
+    ref = pc.apply(v).clone()
+    assert torch.equal(fused, ref), float((fused - ref).abs().max())
+    pc.set_kernel_opts(mg_fuse_small=1)
+    out = torch.empty_like(v)
+    g = pc.capture(v, out)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)

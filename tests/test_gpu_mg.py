@@ -114,6 +114,14 @@ def mf_transfer(request):
         yield request.param
 
 
+@pytest.fixture(params=[1, 0], ids=["fusesmall", "nofusesmall"])
+def fuse_small(request):
+    """Small grouped levels' residual + restriction as one launch (k_grp_rr; default) or as two."""
+    from mp_block_preconditioners_amd._lib import kernel_options
+    with kernel_options(mg_fuse_small=request.param):
+        yield request.param
+
+
 @pytest.fixture(params=[False, True], ids=["rowlayouts", "svl"])
 def svl_all(request, monkeypatch):
     """Every coarse level with a stencil-values copy (mg.SVL_MIN_ROWS = 0), or the default (none at these sizes)."""
@@ -173,10 +181,11 @@ def test_stencil_values_spmv_bit_exact(n):
 
 @pytest.mark.parametrize("sell", [True, False], ids=["sell", "csr"])
 @pytest.mark.parametrize("n,cycles,pre,post", [(16, 1, 2, 2), (32, 2, 2, 2), (64, 1, 1, 3), (64, 3, 2, 1)])
-def test_mg_solve_bit_exact(n, cycles, pre, post, sell, group_rows, svl_all, mf_transfer):
+def test_mg_solve_bit_exact(n, cycles, pre, post, sell, group_rows, svl_all, mf_transfer, fuse_small):
     """V-cycles vs the oracle: with the SELL-64 copies of every level and the dense coarse kernel (default), and
     with the CSR forms throughout; the small levels and transfers on the grouped CSR kernel (several lanes per row,
-    the row's sum in order) or on the row kernels."""
+    the row's sum in order) or on the row kernels; the small grouped levels' residual + restriction in one launch
+    (mg_fuse_small) or in two."""
     mp = _mp()
     from oracle import mg_oracle as mo
     _, (A, F, D, G), S = _system(n)
