@@ -174,7 +174,7 @@ typedef struct mpbp_inner_solver {
 typedef struct mpbp_mg_level {
     int32_t nrows;
     int32_t pre, post;               /* Chebyshev-Jacobi smoothing sweeps (>= 1) */
-    int32_t reserved;
+    int32_t part_r0;                 /* row partition: the first grid row this rank owns of every field of the level */
     double lmin, lmax;               /* smoothing interval of diag(A)^-1 A */
     mpbp_csr A;
     mpbp_rowblocks A_blocks;
@@ -193,7 +193,7 @@ typedef struct mpbp_mg_level {
      * x / t / r hold owned + ghost rows (the ext layout), R's columns index that layout and P's the next level's
      * (or, at the last partitioned level, the whole next level) */
     int32_t halo_kind;
-    int32_t reserved2;
+    int32_t part_h;                  /* row partition: ghost rows each side of this level's x / t / r (0: whole level) */
     /* optional stencil-values copy of A (NULL: none; used for levels above the grouped kernel's row limit) */
     const mpbp_svl* A_svl;
 } mpbp_mg_level;

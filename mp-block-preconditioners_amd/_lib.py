@@ -65,11 +65,11 @@ class Svl(Structure):
 
 
 class MgLevel(Structure):
-    _fields_ = [("nrows", c_int32), ("pre", c_int32), ("post", c_int32), ("reserved", c_int32),
+    _fields_ = [("nrows", c_int32), ("pre", c_int32), ("post", c_int32), ("part_r0", c_int32),
                 ("lmin", c_double), ("lmax", c_double), ("A", Csr), ("A_blocks", RowBlocks), ("diag", c_void_p),
                 ("R", Csr), ("R_blocks", RowBlocks), ("P", Csr), ("P_blocks", RowBlocks),
                 ("x", c_void_p), ("t", c_void_p), ("r", c_void_p), ("d", c_void_p), ("b", c_void_p),
-                ("A_sell", Sell), ("R_sell", Sell), ("P_sell", Sell), ("halo_kind", c_int32), ("reserved2", c_int32),
+                ("A_sell", Sell), ("R_sell", Sell), ("P_sell", Sell), ("halo_kind", c_int32), ("part_h", c_int32),
                 ("A_svl", POINTER(Svl))]
 
 

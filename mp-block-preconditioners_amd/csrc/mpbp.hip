@@ -4382,14 +4382,39 @@ __device__ inline double g1_r_in(const double* tf, int lr, int lc) { return g1_r
 __device__ inline bool g1_inner(int cr0, int cc0, int th, int tw, int nc) {
     return cr0 >= 2 && cr0 + th + 2 <= nc && cc0 >= 2 && cc0 + tw + 2 <= nc;
 }
-template <bool INNER, class Epi, bool MAC, class XS>
+// Level 1 under a row partition (PART): this rank owns coarse rows [r0, r0 + L) of every field and its level-1 vectors
+// hold them followed by h ghost rows above and below (ext_row's layout).  The tiles cover the owned rows only; every
+// value is computed in global coordinates exactly as on one GPU (the same windows, lists and rows), so the rank's rows
+// are the one-GPU launch's bits.
+struct G1Part {
+    int r0 = 0, L = 0, h = 0;
+};
+// level-1 x index of (field f, coarse row gr -- unwrapped, within two rows of the tile --, wrapped column c); window
+// rows past the ghosts (a partial last tile's) are clamped: they feed only outputs the tile does not own
+template <bool PART>
+__device__ inline int32_t g1_xidx(const G1Part& q, int nf, int f, int gr, int c, int nc) {
+    if constexpr (!PART) {
+        (void)q; (void)nf;
+        return (f * nc + (gr < 0 ? gr + nc : (gr >= nc ? gr - nc : gr))) * nc + c;
+    } else {
+        const int lr = min(max(gr - q.r0, -q.h), q.L + q.h - 1);
+        return ext_row(nf, f, lr, q.L, q.h, nc) + c;
+    }
+}
+// the level-1 row of an owned output (f, cr, cc)
+template <bool PART>
+__device__ inline int32_t g1_orow(const G1Part& q, int f, int cr, int cc, int nc) {
+    return PART ? (f * q.L + cr - q.r0) * nc + cc : (f * nc + cr) * nc + cc;
+}
+template <bool INNER, class Epi, bool MAC, class XS, bool PART>
 __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& tr, const XS& xin, const Epi& epi,
-                                         double* xs, double* ts, double* t0, double* t1, int cr0, int cc0);
+                                         double* xs, double* ts, double* t0, double* t1, int cr0, int cc0,
+                                         const G1Part& q);
 // MAC: the F hierarchy's kinds (u: rows cell-, columns node-centred; v: the reverse) at compile time
 // XS: the coarse x as staged -- XPlain (x itself) or XInit (x0 = c2_0 (b / diag): a pre-smoothing's first sweep with the
 // init pass folded in, as the grouped small levels do; the epilogue then EpiChebFirstGrp)
-template <class Epi, bool MAC = false, class XS = XPlain>
-__global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1(FStencilFast P, MgFields tr, XS xin, Epi epi) {
+template <class Epi, bool MAC = false, class XS = XPlain, bool PART = false>
+__global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1(FStencilFast P, MgFields tr, XS xin, Epi epi, G1Part q) {
     constexpr int CN = kG1CW * kG1CH, PN = kG1PW * kG1PH, FN = kG1FW * kG1FH;
     __shared__ double xs[4 * CN];
     __shared__ double ts[PN];
@@ -4399,20 +4424,21 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1(FStencilFast P, MgF
     const int nc = P.n >> 1;
     const int tx = (nc + kG1W - 1) / kG1W;
     const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
-    const int cr0 = (bk / tx) * kG1H, cc0 = (bk % tx) * kG1W;     // the coarse tile
+    const int cr0 = (PART ? q.r0 : 0) + (bk / tx) * kG1H, cc0 = (bk % tx) * kG1W;     // the coarse tile
     if constexpr (MAC) {
         if (g1_inner(cr0, cc0, kG1H, kG1W, nc)) {
-            gal1_run<true, Epi, MAC, XS>(P, tr, xin, epi, xs, ts, t0, t1, cr0, cc0);
+            gal1_run<true, Epi, MAC, XS, PART>(P, tr, xin, epi, xs, ts, t0, t1, cr0, cc0, q);
             return;
         }
     }
-    gal1_run<false, Epi, MAC, XS>(P, tr, xin, epi, xs, ts, t0, t1, cr0, cc0);
+    gal1_run<false, Epi, MAC, XS, PART>(P, tr, xin, epi, xs, ts, t0, t1, cr0, cc0, q);
 }
-template <bool INNER, class Epi, bool MAC, class XS>
+template <bool INNER, class Epi, bool MAC, class XS, bool PART>
 __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& tr, const XS& xin, const Epi& epi,
-                                         double* xs, double* ts, double* t0, double* t1, int cr0, int cc0) {
+                                         double* xs, double* ts, double* t0, double* t1, int cr0, int cc0,
+                                         const G1Part& q) {
     constexpr int CN = kG1CW * kG1CH, PN = kG1PW * kG1PH, FN = kG1FW * kG1FH;
-    const int n = P.n, nc = n >> 1, ncc = nc * nc;
+    const int n = P.n, nc = n >> 1;
     const int fr0 = 2 * cr0, fc0 = 2 * cc0;                      // its fine block
     const int tid = threadIdx.x;
     auto wrapc = [&](int a) { return a < 0 ? a + nc : (a >= nc ? a - nc : a); };
@@ -4427,7 +4453,7 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
             const int i = tid + it * 256;
             if (i < 4 * CN) {
                 const int f = i / CN, j = i - f * CN, r = j / kG1CW, c = j - r * kG1CW;
-                vx[it] = xin.load(f * ncc + wrapc(cr0 - 2 + r) * nc + wrapc(cc0 - 2 + c));
+                vx[it] = xin.load(g1_xidx<PART>(q, 4, f, cr0 - 2 + r, wrapc(cc0 - 2 + c), nc));
             }
         }
 #pragma unroll
@@ -4518,11 +4544,11 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
     if constexpr (MAC) {   // lane t: cell t & 127 of fields (t >> 7) and (t >> 7) + 2 -- one kind pair per wave
         const int cell = tid & (kG1W * kG1H - 1), fp = tid >> 7;
         const int cr = cr0 + cell / kG1W, cc = cc0 + cell % kG1W;
-        if (cr < nc && cc < nc) {
+        if (cr < (PART ? q.r0 + q.L : nc) && cc < nc) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int f = fp + 2 * h;
-                const int32_t row = f * ncc + cr * nc + cc;
+                const int32_t row = g1_orow<PART>(q, f, cr, cc, nc);
                 const typename Epi::P pe = epi.pre(row);
                 double acc;
                 if constexpr (INNER)
@@ -4539,8 +4565,8 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
     for (int j = tid; j < 4 * kG1W * kG1H; j += 256) {
         const int f = j / (kG1W * kG1H), cell = j - f * (kG1W * kG1H);
         const int cr = cr0 + cell / kG1W, cc = cc0 + cell % kG1W;
-        if (cr >= nc || cc >= nc) continue;
-        const int32_t row = f * ncc + cr * nc + cc;
+        if (cr >= (PART ? q.r0 + q.L : nc) || cc >= nc) continue;
+        const int32_t row = g1_orow<PART>(q, f, cr, cc, nc);
         const typename Epi::P pe = epi.pre(row);
         int yi[4], xi[4];
         double yw[4], xw[4];
@@ -4725,8 +4751,8 @@ k_fpre(FStencilFast P, FPre a) {
 // matrix-free level-0 sweep's operations), the transfers' by k_mg_transfer_spmv's: bit-identical to the three launches.
 constexpr int kG1PH2 = 8;                                     // coarse tile rows (pressure)
 constexpr int kGPFH = 2 * kG1PH2 + 2, kGPPH = kGPFH + 2;       // fine t1 / t0 rows
-template <class Epi, class XS = XPlain>
-__global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, XS xin, Epi epi) {
+template <class Epi, class XS = XPlain, bool PART = false>
+__global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, XS xin, Epi epi, G1Part q) {
     constexpr int CH = kG1PH2 + 4, CN = kG1CW * CH, PN = kG1PW * kGPPH, FN = kG1FW * kGPFH;
     __shared__ double xs[CN];
     __shared__ double ts[PN];
@@ -4736,7 +4762,7 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, X
     const int n = P.n, nc = n >> 1;
     const int tx = (nc + kG1W - 1) / kG1W;
     const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
-    const int cr0 = (bk / tx) * kG1PH2, cc0 = (bk % tx) * kG1W;
+    const int cr0 = (PART ? q.r0 : 0) + (bk / tx) * kG1PH2, cc0 = (bk % tx) * kG1W;
     const int fr0 = 2 * cr0, fc0 = 2 * cc0;
     const int tid = threadIdx.x;
     auto wrapc = [&](int a) { return a < 0 ? a + nc : (a >= nc ? a - nc : a); };
@@ -4749,7 +4775,7 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, X
             const int i = tid + it * 256;
             if (i < CN) {
                 const int r = i / kG1CW, c = i - r * kG1CW;
-                vx[it] = xin.load(wrapc(cr0 - 2 + r) * nc + wrapc(cc0 - 2 + c));
+                vx[it] = xin.load(g1_xidx<PART>(q, 1, 0, cr0 - 2 + r, wrapc(cc0 - 2 + c), nc));
             }
         }
 #pragma unroll
@@ -4806,8 +4832,8 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, X
     __syncthreads();
     {   // R_0 t1 on the tile's 256 coarse rows, each to the epilogue
         const int cr = cr0 + tid / kG1W, cc = cc0 + tid % kG1W;
-        if (cr < nc && cc < nc) {
-            const int32_t row = cr * nc + cc;
+        if (cr < (PART ? q.r0 + q.L : nc) && cc < nc) {
+            const int32_t row = g1_orow<PART>(q, 0, cr, cc, nc);
             const typename Epi::P pe = epi.pre(row);
             epi(row, inner ? g1_r_in<MPBP_MG_CELL, MPBP_MG_CELL>(t1, cr - cr0, cc - cc0)
                            : g1_r<MPBP_MG_CELL, MPBP_MG_CELL>(t1, cr, cc, n, fr0 - 1, fc0 - 1), pe);
@@ -6860,9 +6886,26 @@ int gal_r(const MgGal& g, Epi epi, hipStream_t st) {
 
 // The whole level-1 product as one k_gal1 launch (KO().mg_galerkin_mf == 2): four fields, a grid the staged windows wrap once.
 // gal_fused_ok: whether gal_fused takes the one-launch form for this level (else the caller runs the three launches)
+// Under a row partition (g.m->part_levels > 0) level 1 is either the whole replicated level (part_levels == 1: the
+// one-GPU launch on every rank) or row-partitioned (> 1: the PART launch over the owned coarse rows, its x read with
+// >= 2 ghost rows each side -- the windows' reach).
+bool gal_part(const MgGal& g, G1Part* q) {
+    *q = G1Part{};
+    if (g.m->part_levels <= 1) return true;
+    const mpbp_mg_level& L1 = g.m->levels[1];
+    const int nc = g.fine.stencil->f_prm.n / 2, nf = g.fine.sop == SOP_GTG ? 1 : 4;
+    if (L1.nrows == nf * nc * nc && L1.part_r0 == 0) return true;   // one rank: its owned rows are the whole level
+    if (nc <= 0 || L1.nrows % (nf * nc) || L1.part_h < 2 || L1.part_r0 < 0) return false;
+    q->r0 = L1.part_r0;
+    q->L = L1.nrows / (nf * nc);
+    q->h = L1.part_h;
+    return q->L >= q->h && q->r0 + q->L <= nc;
+}
 bool gal_fused_ok(const MgGal& g) {
     const mpbp_schur_plan* p = g.fine.stencil;
     if (KO().mg_galerkin_mf != 2 || p->f_prm.n < 2 * kG1CW || (p->f_prm.n & 1)) return false;
+    G1Part q;
+    if (!gal_part(g, &q)) return false;
     if (g.fine.sop == SOP_GTG) return g.m->tr_nfields == 1 && g.m->tr_ky[0] == MPBP_MG_CELL && g.m->tr_kx[0] == MPBP_MG_CELL;
     return g.m->tr_nfields == 4;
 }
@@ -6871,13 +6914,17 @@ int gal_fused(const MgGal& g, XS x, Epi epi, hipStream_t st, bool* done) {
     *done = false;
     const mpbp_schur_plan* p = g.fine.stencil;
     if (!gal_fused_ok(g)) return MPBP_OK;
+    G1Part q;
+    gal_part(g, &q);
+    const bool part = q.L > 0;
     if (g.fine.sop == SOP_GTG) {   // the pressure hierarchy: one field, cell-centred (mg.FIELDS_PRESSURE)
         PGDev Pg;
         const int rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &Pg);
         if (rc) return rc;
         const int nc = p->f_prm.n / 2;
-        const int64_t tiles = (int64_t)((nc + kG1W - 1) / kG1W) * ((nc + kG1PH2 - 1) / kG1PH2);
-        k_gal1p<Epi, XS><<<(unsigned)tiles, 256, 0, st>>>(GtGStencilDev{Pg}, x, epi);
+        const int64_t tiles = (int64_t)((nc + kG1W - 1) / kG1W) * (((part ? q.L : nc) + kG1PH2 - 1) / kG1PH2);
+        if (part) k_gal1p<Epi, XS, true><<<(unsigned)tiles, 256, 0, st>>>(GtGStencilDev{Pg}, x, epi, q);
+        else k_gal1p<Epi, XS><<<(unsigned)tiles, 256, 0, st>>>(GtGStencilDev{Pg}, x, epi, q);
         MPBP_HIP(hipGetLastError());
         *done = true;
         return MPBP_OK;
@@ -6892,12 +6939,14 @@ int gal_fused(const MgGal& g, XS x, Epi epi, hipStream_t st, bool* done) {
         F.kx[f] = g.m->tr_kx[f];
     }
     const int nc = p->f_prm.n / 2;
-    const int64_t tiles = (int64_t)((nc + kG1W - 1) / kG1W) * ((nc + kG1H - 1) / kG1H);
+    const int64_t tiles = (int64_t)((nc + kG1W - 1) / kG1W) * (((part ? q.L : nc) + kG1H - 1) / kG1H);
     bool mac = true;   // the F hierarchy's MAC kinds (mg.FIELDS_VELOCITY)
     for (int f = 0; f < 4; ++f)
         mac = mac && F.ky[f] == ((f & 1) ? MPBP_MG_NODE : MPBP_MG_CELL) && F.kx[f] == ((f & 1) ? MPBP_MG_CELL : MPBP_MG_NODE);
-    if (mac) k_gal1<Epi, true, XS><<<(unsigned)tiles, 256, 0, st>>>(FStencilFast{Pd}, F, x, epi);
-    else k_gal1<Epi, false, XS><<<(unsigned)tiles, 256, 0, st>>>(FStencilFast{Pd}, F, x, epi);
+    if (part && !mac) return set_error(MPBP_ERR_ARG, "mg: a row-partitioned matrix-free level 1 needs the MAC kinds");
+    if (part) k_gal1<Epi, true, XS, true><<<(unsigned)tiles, 256, 0, st>>>(FStencilFast{Pd}, F, x, epi, q);
+    else if (mac) k_gal1<Epi, true, XS><<<(unsigned)tiles, 256, 0, st>>>(FStencilFast{Pd}, F, x, epi, q);
+    else k_gal1<Epi, false, XS><<<(unsigned)tiles, 256, 0, st>>>(FStencilFast{Pd}, F, x, epi, q);
     MPBP_HIP(hipGetLastError());
     *done = true;
     return MPBP_OK;
@@ -7322,9 +7371,11 @@ int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, 
         other = x;
         x = out1;
         s = 2;
-    } else if (zero && K >= 2 && op.bd.empty && o.gal && KO().mg_fuse_l0 && gal_fused_ok(*o.gal)) {
+    } else if (zero && K >= 2 && op.bd.empty && o.gal && KO().mg_fuse_l0 && gal_fused_ok(*o.gal) &&
+               o.gal->m->part_levels <= 1) {
         // matrix-free level 1 (k_gal1 / k_gal1p): the first sweep stages x0 = c2[0] b / diag itself (XInit) and its
-        // epilogue takes the row's own x0 as iterate and direction -- no init launch, k_cheb_init's bits
+        // epilogue takes the row's own x0 as iterate and direction -- no init launch, k_cheb_init's bits.  Not on a
+        // row-partitioned level 1 (b and diag hold the owned rows; the ghosts' x0 comes from the init and exchange)
         double* out1 = K == 2 ? (dst ? dst : other) : other;
         EpiChebFirstGrp e;
         static_cast<EpiChebFirst&>(e) = EpiChebFirst{b, d, c1[1], c2[1], K == 2 ? sub : nullptr, out1, K == 2 ? 0 : 1};
@@ -7383,12 +7434,20 @@ int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, 
     return MPBP_OK;
 }
 
-// Level 1 as R_0 (F (P_0 x)): tolerance-mode F stencil level 0 on one GPU, matrix-free transfers, level 1 smoothed.
+// Level 1 as R_0 (F (P_0 x)): tolerance-mode F (or Gt_G) stencil level 0, level 1 smoothed.  mg_galerkin_mf 1: the three
+// launches (one GPU, matrix-free level-0 transfers); 2 (default): the one-launch form where the grid allows it
+// (gal_fused_ok: even n >= 72), else the stored Galerkin level -- on one GPU and under a row partition alike (level 0's
+// interior / boundary rows and its halo; level 1 replicated whole or its owned rows), so both run the same level 1.
 bool mg_gal_ok(const mpbp_mg* m, const MgFine& f) {
     const OpRef& o = f.op.in;
-    return KO().mg_galerkin_mf && o.stencil && (o.sop == SOP_F || (o.sop == SOP_GTG && KO().mg_galerkin_mf_p)) &&
-           o.stencil->f_numerics == MPBP_NUMERICS_FAST && o.which == 0 && f.op.bd.empty && !f.halo && !o.stencil->halo &&
-           m->nlevels > 2 && use_mf_transfer(m, 0) && f.r && f.d;
+    if (!KO().mg_galerkin_mf || !o.stencil || !(o.sop == SOP_F || (o.sop == SOP_GTG && KO().mg_galerkin_mf_p)) ||
+        o.stencil->f_numerics != MPBP_NUMERICS_FAST || m->nlevels <= 2 || !f.r || !f.d)
+        return false;
+    const MgGal g{m, o, f.r, f.d};
+    if (m->part_levels == 0)
+        return o.which == 0 && f.op.bd.empty && !f.halo && !o.stencil->halo && use_mf_transfer(m, 0) &&
+               (KO().mg_galerkin_mf == 1 || gal_fused_ok(g));
+    return f.halo && o.stencil->halo && m->tr_nfields > 0 && m->tr_n0 == o.stencil->f_prm.n && gal_fused_ok(g);
 }
 
 // Level 0's descent as ONE k_fpre launch (pre-smoothing V(2, .) from x = 0, residual, restriction): tolerance-mode

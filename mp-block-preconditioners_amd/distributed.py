@@ -836,6 +836,7 @@ class PartitionedMultigrid:
             keep += [R, Pm, SR, SP]
             L.x, L.t, L.r, L.d, L.b = (v.data_ptr() for v in (x, t, r, d, bb))
             L.halo_kind = self.kinds[l]
+            L.part_r0, L.part_h = q.r0, self.h[l]   # (the matrix-free level 1's owned window, k_gal1 / k_gal1p)
             self.work.append((x, t, r, d, bb))
             halos.register(x, t, r, d, bb)
         # the gather level's r (the rank's rows, written by the restriction) and b (the whole level) are the global

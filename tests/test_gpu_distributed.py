@@ -291,12 +291,10 @@ def _inner_pair(spec):
     return mpb.InnerSolver(kf, sf), mpb.InnerSolver(kp, sp)
 
 
-FAST_TWIN = {"mg_galerkin_mf": 0, "mg_galerkin_mf_p": 0}   # the partition's level-1 form (its stored Galerkin product)
-
-
 def _mg_worker(rank, world, port, n, inner, min_cells, halo, errfile, numerics="exact"):
-    """The partitioned Schur apply with multigrid inner solves vs the one-GPU apply (fast numerics: the one-GPU twin
-    applies level 1 from its stored Galerkin matrices and Gt_F_G's full rows, as the partition does)."""
+    """The partitioned Schur apply with multigrid inner solves vs the one-GPU apply with its default kernel choices
+    (fast numerics at n >= 72: level 1 matrix-free in one launch on both sides -- k_gal1 / k_gal1p over the rank's owned
+    coarse rows under the partition)."""
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         torch.cuda.set_device(0)
@@ -318,14 +316,19 @@ def _mg_worker(rank, world, port, n, inner, min_cells, halo, errfile, numerics="
                         assert m.g.band[0].shape[0] < m.nf * m.g.sizes[0] ** 2, (m.g.band[0].shape, m.g.sizes)
         bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
         _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
-        pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, numerics=numerics,
-                                           kernel_opts=FAST_TWIN if numerics == "fast" else None)
+        pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, numerics=numerics)
         v = torch.from_numpy(np.random.default_rng(8).standard_normal(pc.shape[0])).cuda()
         gids = torch.from_numpy(dpc.local_to_global_rows()).cuda()
         ref = pc.apply(v)[gids]
         for _ in range(2):
             got = dpc.apply(v[gids].contiguous())
             assert torch.equal(got, ref), float((got - ref).abs().max())
+        if numerics == "fast" and n >= 72:   # the matrix-free level 1 ran: the stored one gives other bits
+            dpc.kernel_opts.mg_galerkin_mf = 0
+            stored = dpc.apply(v[gids].contiguous())
+            assert not torch.equal(stored, ref)
+            assert float((stored - ref).abs().max()) <= 1e-10 * float(ref.abs().max())
+            dpc.kernel_opts.mg_galerkin_mf = 2
         if halo == "rccl":   # in-order RCCL halo: the partitioned MG apply captured into a hipGraph
             vin, out = v[gids].contiguous(), torch.zeros_like(ref)
             g = dpc.capture(vin, out)
@@ -348,14 +351,18 @@ MG1 = (("mg", 1), ("mg", 1))
 @pytest.mark.parametrize("world,n,inner,min_cells,halo", [
     (2, 64, MG1, 1 << 14, "auto"), (2, 64, MG1, 0, "auto"), (4, 64, MG1, 0, "auto"), (3, 48, MG1, 0, "auto"),
     (3, 50, MG1, 0, "auto"), (2, 64, (("mg", 2), ("chebyshev", 4)), 0, "auto"),
-    (2, 64, (("chebyshev", 4), ("mg", 1)), 0, "auto"), (1, 64, MG1, 0, "rccl"), (1, 32, MG1, 0, "torch")])
+    (2, 64, (("chebyshev", 4), ("mg", 1)), 0, "auto"), (1, 64, MG1, 0, "rccl"), (1, 32, MG1, 0, "torch"),
+    (2, 128, MG1, 0, "auto"), (4, 128, MG1, 0, "auto"), (3, 100, MG1, 0, "auto"), (2, 128, MG1, 1 << 14, "auto"),
+    (1, 128, MG1, 0, "rccl")])
 @pytest.mark.parametrize("numerics", ["exact", "fast"])
 def test_partitioned_multigrid_apply_matches_single_gpu(world, n, inner, min_cells, halo, numerics, tmp_path):
     """Row 18: multigrid inner solves under the row partition -- level 0 the apply's own matrix-free F / Gt_G, the
     Galerkin levels row-partitioned down to part_levels (ghost rows per operator), the coarser levels all-gathered and
     replicated -- bit for bit against the one-GPU apply (2-4 gloo ranks; ceil-halved partitions at n = 50; the RCCL
     self-exchange, captured).  With 2+ ranks every level is formed from the rank's own band of rows (LocalHierarchy:
-    rank-local Galerkin products, level part_levels all-gathered from the ranks' rows)."""
+    rank-local Galerkin products, level part_levels all-gathered from the ranks' rows).  Fast numerics against the
+    one-GPU default: at n >= 72 both apply level 1 matrix-free in one launch (the partition over each rank's owned
+    coarse rows and ghost rows, or the replicated level when it is the gather level), below it both the stored level."""
     errfile = str(tmp_path / "err.txt")
     _spawn(_mg_worker, (world, _free_port(), n, inner, min_cells, halo, errfile, numerics), world, errfile)
 
@@ -382,7 +389,8 @@ def _fgmres_worker(rank, world, port, n, inner, maxiter, outdir, errfile, numeri
 
 @pytest.mark.parametrize("world,n,inner,maxiter,numerics", [
     (2, 32, (("chebyshev", 4), ("chebyshev", 4)), 40, "exact"), (3, 48, MG1, 60, "exact"), (2, 64, MG1, 60, "exact"),
-    (2, 64, MG1, 60, "fast"), (3, 48, MG1, 60, "fast"), (2, 32, (("chebyshev", 4), ("chebyshev", 4)), 40, "fast")])
+    (2, 64, MG1, 60, "fast"), (3, 48, MG1, 60, "fast"), (2, 32, (("chebyshev", 4), ("chebyshev", 4)), 40, "fast"),
+    (2, 128, MG1, 60, "fast")])
 def test_distributed_fgmres_matches_single_gpu(world, n, inner, maxiter, numerics, tmp_path):
     """Row 17: FGMRES (solve.py:285) over the row partition -- the partitioned A, the partitioned preconditioner,
     reproducible inner products reduced over the ranks -- gives the one-GPU solve's residual history and iterate bit
@@ -393,8 +401,7 @@ def test_distributed_fgmres_matches_single_gpu(world, n, inner, maxiter, numeric
     bp = mpb.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
     A, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
     iF, iP = _inner_pair(inner)
-    pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, numerics=numerics,
-                                       kernel_opts=FAST_TWIN if numerics == "fast" else None)
+    pc = mpb.ApproxSchurPreconditioner(F, D, G, inner_F=iF, inner_P=iP, numerics=numerics)
     _, b = mpb.manufactured_problem(n, 1.0, -1.0, 1.0, 100.0, 1.0)
     hist = []
     x, info = mpb.fgmres(A, torch.from_numpy(b).cuda(), M=pc, tol=1e-8, maxiter=maxiter, residuals=hist)

@@ -326,7 +326,9 @@ def test_matrix_free_galerkin_level1(n):
     one = fast.apply(v).clone()
     e_stored = rel_inf(got.cpu().numpy(), stored.cpu().numpy())
     assert 0.0 < e_stored <= TOL_APPLY   # measured 2.5e-14 (n = 72) .. 2.9e-13 (n = 256)
-    assert torch.equal(one, got)   # one k_gal1 launch (the default) == the three launches, bit for bit
+    # the default (2): one k_gal1 launch == the three launches, bit for bit; where the grid does not take the fused
+    # kernel (n < 72), the stored level (as the row partition does there)
+    assert torch.equal(one, got if n >= 72 else stored)
     exact = mp.ApproxSchurPreconditioner(F, D, G, fast.GtG, fast.GtFG, **kw)
     e_exact = rel_inf(got.cpu().numpy(), exact.apply(v).cpu().numpy())
     print(f"level-1 F n={n}: vs stored {e_stored:.3e}, vs exact {e_exact:.3e}")
@@ -335,7 +337,7 @@ def test_matrix_free_galerkin_level1(n):
     g = fast.capture(v, out)
     g.replay()
     torch.cuda.synchronize()
-    assert torch.equal(out, got)
+    assert torch.equal(out, one)
 
 
 @pytest.mark.parametrize("n", [64, 256])
@@ -389,7 +391,8 @@ def test_matrix_free_galerkin_level1_pressure(n):
     e_stored = rel_inf(three.cpu().numpy(), stored.cpu().numpy())
     print(f"level-1 P n={n}: vs stored {e_stored:.3e}")
     assert 0.0 < e_stored <= TOL_APPLY   # measured 1.5e-14 .. 3.0e-13
-    assert torch.equal(one, three), float((one - three).abs().max())
+    ref = three if n >= 72 else stored   # (n < 72: the stored level, as test_matrix_free_galerkin_level1)
+    assert torch.equal(one, ref), float((one - ref).abs().max())
     out = torch.empty_like(v)
     g = fast.capture(v, out)
     g.replay()

@@ -19,9 +19,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def worker(rank, world, port, n, order, q, keep_cache=False, inner="chebyshev:4", local_products=True):
+def worker(rank, world, port, n, order, q, keep_cache=False, inner="chebyshev:4", local_products=True, threads=0):
     import torch
     import torch.distributed as dist
+    if threads:   # host threads per rank (the ranks share the box's cores)
+        torch.set_num_threads(threads)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MPBP_SETUP_TIMING="1")
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -43,8 +45,12 @@ def worker(rank, world, port, n, order, q, keep_cache=False, inner="chebyshev:4"
         el = torch.tensor([time.perf_counter() - t0, torch.cuda.max_memory_allocated() - base,
                            torch.cuda.memory_allocated() - base] + [dpc.setup_phases[k] for k in names],
                           dtype=torch.float64)
+        mine = {"total": round(time.perf_counter() - t0, 4), **{k: round(v, 4) for k, v in dpc.setup_phases.items()}}
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        out[f"{len(out) + 1}_{numerics}"] = {"total": float(el[0]), "peak_mem_gb": round(float(el[1]) / 1e9, 3),
+        out[f"{len(out) + 1}_{numerics}"] = {"phases_per_rank": per_rank, "total": float(el[0]),
+                                             "peak_mem_gb": round(float(el[1]) / 1e9, 3),
                                              "kept_mem_gb": round(float(el[2]) / 1e9, 3), "phases_max_over_ranks": {
             k: round(float(v), 4) for k, v in zip(names, el[3:].tolist())}}
         if rank == 0:   # progress (a silent multi-minute run looks hung to the GPU harness)
@@ -66,6 +72,7 @@ def main():
     ap.add_argument("--fresh", action="store_true", help="every build in a fresh set of rank processes")
     ap.add_argument("--keep-cache", action="store_true", help="no torch.cuda.empty_cache() between builds")
     ap.add_argument("--inner", default="chebyshev:4", help="both inner solves, kind:k (e.g. mg:1)")
+    ap.add_argument("--threads", type=int, default=0, help="torch host threads per rank (0: torch's default)")
     ap.add_argument("--global-products", action="store_true",
                     help="every rank forms the global operators (and multigrid hierarchy) and extracts its rows")
     a = ap.parse_args()
@@ -79,7 +86,7 @@ def main():
             port = s.getsockname()[1]
         q = ctx.Queue()
         procs = [ctx.Process(target=worker, args=(r, a.world, port, a.n, batch, q, a.keep_cache, a.inner,
-                                                  not a.global_products))
+                                                  not a.global_products, a.threads))
                  for r in range(a.world)]
         for p in procs:
             p.start()
@@ -92,6 +99,7 @@ def main():
                       "processes": "a fresh set per build" if a.fresh else "one set for all builds",
                       "empty_cache_between_builds": not a.keep_cache, "inner": a.inner,
                       "products": "global on every rank" if a.global_products else "rank-local",
+                      "host_threads_per_rank": a.threads or "torch default",
                       "setup_seconds_max_over_ranks": res,
                       "note": "DistributedSchurPreconditioner construction: rank-local F / D / G rows, commutator "
                               "products of the owned rows, Chebyshev bounds or the multigrid levels, CA ghost "
