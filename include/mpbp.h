@@ -494,7 +494,8 @@ typedef struct mpbp_kernel_opts {
     int32_t mg_mf_transfer;    /* whole-grid multigrid transfers matrix-free when the kinds are known (1, default) */
     int32_t csr_table;         /* CSR SpMV waves start from the row blocks' wave table when present (1, default) */
     int32_t mg_fuse_l0;        /* tolerance-mode F hierarchies, one GPU: level 0's pre-smoothing, residual and restriction
-                                  as ONE k_fpre launch, and the prolongation inside the post-smoothing pair (1, default) */
+                                  as ONE k_fpre launch, and the prolongation inside the post-smoothing pair; the matrix-free
+                                  level 1's prolongation inside its first post-smoothing sweep (k_gal1 / k_gal1p <PRO>) (1, default) */
     int32_t mg_coarse_tree;    /* tolerance-mode hierarchies: the coarsest level's dense inverse applied with its row sums
                                   split over the workgroup and combined by a tree (1; default 0: another order of the
                                   ill-conditioned coarsest F inverse's sums moves the apply by ~5e-13) */

@@ -4406,19 +4406,27 @@ template <bool PART>
 __device__ inline int32_t g1_orow(const G1Part& q, int f, int cr, int cc, int nc) {
     return PART ? (f * q.L + cr - q.r0) * nc + cc : (f * nc + cr) * nc + cc;
 }
-template <bool INNER, class Epi, bool MAC, class XS, bool PART>
+// PRO (the post-smoothing's first sweep after level 2's correction): the staged x is x + P_1 x_c, level 2's window
+// [cr0 / 2 - 2, cr0 / 2 + kG1QH - 2) x [cc0 / 2 - 2, cc0 / 2 + kG1QW - 2) staged first (k_ftile<PRO>'s scheme one level
+// down: the same P rows in window coordinates, k_mg_transfer_spmv's lists and EpiAdd's sum), and the epilogue's iterate
+// is the row's own staged value -- the prolongation launch folded in, bit-identical.
+constexpr int kG1QW = kG1W / 2 + 4, kG1QH = kG1H / 2 + 4;   // level-2 window of a k_gal1 tile (row stride kG1CW)
+template <bool INNER, class Epi, bool MAC, class XS, bool PART, bool PRO>
 __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& tr, const XS& xin, const Epi& epi,
                                          double* xs, double* ts, double* t0, double* t1, int cr0, int cc0,
-                                         const G1Part& q);
+                                         const G1Part& q, const double* xc, double* xq);
 // MAC: the F hierarchy's kinds (u: rows cell-, columns node-centred; v: the reverse) at compile time
 // XS: the coarse x as staged -- XPlain (x itself) or XInit (x0 = c2_0 (b / diag): a pre-smoothing's first sweep with the
 // init pass folded in, as the grouped small levels do; the epilogue then EpiChebFirstGrp)
-template <class Epi, bool MAC = false, class XS = XPlain, bool PART = false>
-__global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1(FStencilFast P, MgFields tr, XS xin, Epi epi, G1Part q) {
+template <class Epi, bool MAC = false, class XS = XPlain, bool PART = false, bool PRO = false>
+__global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1(FStencilFast P, MgFields tr, XS xin, Epi epi, G1Part q,
+                                                              const double* __restrict__ xc = nullptr) {
     constexpr int CN = kG1CW * kG1CH, PN = kG1PW * kG1PH, FN = kG1FW * kG1FH;
+    static_assert(!PRO || (MAC && !PART), "the folded prolongation: MAC kinds, whole level");
     __shared__ double xs[4 * CN];
     __shared__ double ts[PN];
     __shared__ double t0[4 * PN];
+    __shared__ double xq[PRO ? 4 * kG1CW * kG1QH : 1];
     double* t1 = t0;
     static_assert(FN <= PN, "t1 fits t0");
     const int nc = P.n >> 1;
@@ -4427,16 +4435,16 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1(FStencilFast P, MgF
     const int cr0 = (PART ? q.r0 : 0) + (bk / tx) * kG1H, cc0 = (bk % tx) * kG1W;     // the coarse tile
     if constexpr (MAC) {
         if (g1_inner(cr0, cc0, kG1H, kG1W, nc)) {
-            gal1_run<true, Epi, MAC, XS, PART>(P, tr, xin, epi, xs, ts, t0, t1, cr0, cc0, q);
+            gal1_run<true, Epi, MAC, XS, PART, PRO>(P, tr, xin, epi, xs, ts, t0, t1, cr0, cc0, q, xc, xq);
             return;
         }
     }
-    gal1_run<false, Epi, MAC, XS, PART>(P, tr, xin, epi, xs, ts, t0, t1, cr0, cc0, q);
+    gal1_run<false, Epi, MAC, XS, PART, PRO>(P, tr, xin, epi, xs, ts, t0, t1, cr0, cc0, q, xc, xq);
 }
-template <bool INNER, class Epi, bool MAC, class XS, bool PART>
+template <bool INNER, class Epi, bool MAC, class XS, bool PART, bool PRO>
 __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& tr, const XS& xin, const Epi& epi,
                                          double* xs, double* ts, double* t0, double* t1, int cr0, int cc0,
-                                         const G1Part& q) {
+                                         const G1Part& q, const double* xc, double* xq) {
     constexpr int CN = kG1CW * kG1CH, PN = kG1PW * kG1PH, FN = kG1FW * kG1FH;
     const int n = P.n, nc = n >> 1;
     const int fr0 = 2 * cr0, fc0 = 2 * cc0;                      // its fine block
@@ -4464,9 +4472,47 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
                 vt[it] = P.cell[P.wrap(fr0 - 2 + r) * n + P.wrap(fc0 - 2 + c)];
             }
         }
+        const int n2 = nc >> 1;
+        if constexpr (PRO) {   // level 2's window first: the staged x needs it
+            auto wrap2 = [&](int a) { return a < 0 ? a + n2 : (a >= n2 ? a - n2 : a); };
+            constexpr int QF = kG1QW * kG1QH, IQ = (4 * QF + 255) / 256;
+            double vq[IQ];
 #pragma unroll
-        for (int it = 0; it < IX; ++it)
-            if (tid + it * 256 < 4 * CN) xs[tid + it * 256] = xin.value(vx[it]);
+            for (int it = 0; it < IQ; ++it) {
+                const int i = tid + it * 256;
+                if (i < 4 * QF) {
+                    const int f = i / QF, j = i - f * QF, r = j / kG1QW, c = j - r * kG1QW;
+                    vq[it] = xc[(f * n2 + wrap2((cr0 >> 1) - 2 + r)) * n2 + wrap2((cc0 >> 1) - 2 + c)];
+                }
+            }
+#pragma unroll
+            for (int it = 0; it < IQ; ++it) {
+                const int i = tid + it * 256;
+                if (i < 4 * QF) {
+                    const int f = i / QF, j = i - f * QF, r = j / kG1QW, c = j - r * kG1QW;
+                    xq[(f * kG1QH + r) * kG1CW + c] = vq[it];
+                }
+            }
+            __syncthreads();
+        }
+        const bool inner2 = PRO && g1_inner(cr0 >> 1, cc0 >> 1, kG1H / 2, kG1W / 2, n2);
+#pragma unroll
+        for (int it = 0; it < IX; ++it) {
+            const int i = tid + it * 256;
+            if (i >= 4 * CN) continue;
+            double v = xin.value(vx[it]);
+            if constexpr (PRO) {   // x + P_1 x_c (EpiAdd: the row sum, then + x)
+                const int f = i / CN, j = i - f * CN, r = j / kG1CW, c = j - r * kG1CW;
+                const double* xf = xq + f * kG1QH * kG1CW;
+                const int gr = wrapc(cr0 - 2 + r), gc = wrapc(cc0 - 2 + c), rb = (cr0 >> 1) - 2, cb = (cc0 >> 1) - 2;
+                const double pc = inner2 ? ((f & 1) ? g1_p_in<MPBP_MG_NODE, MPBP_MG_CELL>(xf, r, c)
+                                                    : g1_p_in<MPBP_MG_CELL, MPBP_MG_NODE>(xf, r, c))
+                                         : ((f & 1) ? g1_p<MPBP_MG_NODE, MPBP_MG_CELL>(xf, gr, gc, n2, rb, cb)
+                                                    : g1_p<MPBP_MG_CELL, MPBP_MG_NODE>(xf, gr, gc, n2, rb, cb));
+                v = pc + v;
+            }
+            xs[i] = v;
+        }
 #pragma unroll
         for (int it = 0; it < IT; ++it)
             if (tid + it * 256 < PN) ts[tid + it * 256] = vt[it];
@@ -4549,7 +4595,14 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
             for (int h = 0; h < 2; ++h) {
                 const int f = fp + 2 * h;
                 const int32_t row = g1_orow<PART>(q, f, cr, cc, nc);
-                const typename Epi::P pe = epi.pre(row);
+                typename Epi::P pe;
+                if constexpr (PRO) {   // the iterate is the staged x + P_1 x_c at the row
+                    pe = epi.pre_lite(row);
+                    set_x(pe, xs[f * CN + (cr - cr0 + 2) * kG1CW + (cc - cc0 + 2)]);
+                    set_diag(pe, epi.diag[row]);
+                } else {
+                    pe = epi.pre(row);
+                }
                 double acc;
                 if constexpr (INNER)
                     acc = fp ? g1_r_in<MPBP_MG_NODE, MPBP_MG_CELL>(t1 + f * FN, cr - cr0, cc - cc0)
@@ -4751,12 +4804,17 @@ k_fpre(FStencilFast P, FPre a) {
 // matrix-free level-0 sweep's operations), the transfers' by k_mg_transfer_spmv's: bit-identical to the three launches.
 constexpr int kG1PH2 = 8;                                     // coarse tile rows (pressure)
 constexpr int kGPFH = 2 * kG1PH2 + 2, kGPPH = kGPFH + 2;       // fine t1 / t0 rows
-template <class Epi, class XS = XPlain, bool PART = false>
-__global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, XS xin, Epi epi, G1Part q) {
+// PRO: as k_gal1's (x + P_1 x_c staged, level 2's window of the 16 x 4 level-2 cells under the tile first)
+constexpr int kG1PQH = kG1PH2 / 2 + 4;   // level-2 window rows (columns kG1QW, row stride kG1CW)
+template <class Epi, class XS = XPlain, bool PART = false, bool PRO = false>
+__global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, XS xin, Epi epi, G1Part q,
+                                                               const double* __restrict__ xc = nullptr) {
     constexpr int CH = kG1PH2 + 4, CN = kG1CW * CH, PN = kG1PW * kGPPH, FN = kG1FW * kGPFH;
     __shared__ double xs[CN];
     __shared__ double ts[PN];
     __shared__ double t0[PN];
+    __shared__ double xq[PRO ? kG1CW * kG1PQH : 1];
+    static_assert(!PRO || !PART, "the folded prolongation: whole level");
     double* t1 = t0;   // (k_gal1's aliasing: 34.7 -> 25 KB per workgroup)
     static_assert(FN <= PN, "t1 fits t0");
     const int n = P.n, nc = n >> 1;
@@ -4786,9 +4844,45 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, X
                 vt[it] = P.cell[P.wrap(fr0 - 2 + r) * n + P.wrap(fc0 - 2 + c)];
             }
         }
+        const int n2 = nc >> 1;
+        if constexpr (PRO) {   // level 2's window first
+            auto wrap2 = [&](int a) { return a < 0 ? a + n2 : (a >= n2 ? a - n2 : a); };
+            constexpr int QN = kG1QW * kG1PQH, IQ = (QN + 255) / 256;
+            double vq[IQ];
 #pragma unroll
-        for (int it = 0; it < IX; ++it)
-            if (tid + it * 256 < CN) xs[tid + it * 256] = xin.value(vx[it]);
+            for (int it = 0; it < IQ; ++it) {
+                const int i = tid + it * 256;
+                if (i < QN) {
+                    const int r = i / kG1QW, c = i - r * kG1QW;
+                    vq[it] = xc[wrap2((cr0 >> 1) - 2 + r) * n2 + wrap2((cc0 >> 1) - 2 + c)];
+                }
+            }
+#pragma unroll
+            for (int it = 0; it < IQ; ++it) {
+                const int i = tid + it * 256;
+                if (i < QN) {
+                    const int r = i / kG1QW, c = i - r * kG1QW;
+                    xq[r * kG1CW + c] = vq[it];
+                }
+            }
+            __syncthreads();
+        }
+        const bool inner2 = PRO && g1_inner(cr0 >> 1, cc0 >> 1, kG1PH2 / 2, kG1W / 2, n2);
+#pragma unroll
+        for (int it = 0; it < IX; ++it) {
+            const int i = tid + it * 256;
+            if (i >= CN) continue;
+            double v = xin.value(vx[it]);
+            if constexpr (PRO) {   // x + P_1 x_c (EpiAdd: the row sum, then + x)
+                const int r = i / kG1CW, c = i - r * kG1CW;
+                const double pc =
+                    inner2 ? g1_p_in<MPBP_MG_CELL, MPBP_MG_CELL>(xq, r, c)
+                           : g1_p<MPBP_MG_CELL, MPBP_MG_CELL>(xq, wrapc(cr0 - 2 + r), wrapc(cc0 - 2 + c), n2,
+                                                              (cr0 >> 1) - 2, (cc0 >> 1) - 2);
+                v = pc + v;
+            }
+            xs[i] = v;
+        }
 #pragma unroll
         for (int it = 0; it < IT; ++it)
             if (tid + it * 256 < PN) ts[tid + it * 256] = vt[it];
@@ -4834,7 +4928,14 @@ __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1p(GtGStencilDev P, X
         const int cr = cr0 + tid / kG1W, cc = cc0 + tid % kG1W;
         if (cr < (PART ? q.r0 + q.L : nc) && cc < nc) {
             const int32_t row = g1_orow<PART>(q, 0, cr, cc, nc);
-            const typename Epi::P pe = epi.pre(row);
+            typename Epi::P pe;
+            if constexpr (PRO) {   // the iterate is the staged x + P_1 x_c at the row
+                pe = epi.pre_lite(row);
+                set_x(pe, xs[(cr - cr0 + 2) * kG1CW + (cc - cc0 + 2)]);
+                set_diag(pe, epi.diag[row]);
+            } else {
+                pe = epi.pre(row);
+            }
             epi(row, inner ? g1_r_in<MPBP_MG_CELL, MPBP_MG_CELL>(t1, cr - cr0, cc - cc0)
                            : g1_r<MPBP_MG_CELL, MPBP_MG_CELL>(t1, cr, cc, n, fr0 - 1, fc0 - 1), pe);
         }
@@ -6952,6 +7053,45 @@ int gal_fused(const MgGal& g, XS x, Epi epi, hipStream_t st, bool* done) {
     return MPBP_OK;
 }
 
+MgFields mg_fields(const mpbp_mg* m);
+// The post-smoothing's first sweep on a matrix-free level 1 with level 2's correction folded in (k_gal1<PRO>,
+// k_gal1p<PRO>): x = x_in + P_1 x_c staged, then the sweep from d = 0 -- the prolongation launch and that sweep's
+// operations.  One GPU (or a replicated level 1), the F hierarchy's MAC kinds, the one-launch form.
+bool gal_pro_ok(const MgGal& g) {
+    G1Part q;
+    if (!gal_fused_ok(g) || !gal_part(g, &q) || q.L || g.m->nlevels < 3 || !KO().mg_fuse_l0) return false;
+    const int nf = g.fine.sop == SOP_GTG ? 1 : 4;   // (gal_fused_ok: the pressure hierarchy's one cell-centred field)
+    if (nf == 4)
+        for (int f = 0; f < 4; ++f)
+            if (g.m->tr_ky[f] != ((f & 1) ? MPBP_MG_NODE : MPBP_MG_CELL) ||
+                g.m->tr_kx[f] != ((f & 1) ? MPBP_MG_CELL : MPBP_MG_NODE))
+                return false;
+    const int n = g.fine.stencil->f_prm.n, n2 = n / 4;
+    return n % 4 == 0 && n2 >= kG1QW && g.m->levels[2].nrows == nf * n2 * n2;
+}
+int gal_pro(const MgGal& g, const double* x, const double* xc, const EpiZeroD<EpiCheb>& epi, hipStream_t st) {
+    const mpbp_schur_plan* p = g.fine.stencil;
+    const int nc = p->f_prm.n / 2;
+    if (g.fine.sop == SOP_GTG) {
+        PGDev Pg;
+        const int rc = make_pgstencil(&p->f_prm, p->f_cell, nullptr, &Pg);
+        if (rc) return rc;
+        const int64_t tiles = (int64_t)((nc + kG1W - 1) / kG1W) * ((nc + kG1PH2 - 1) / kG1PH2);
+        k_gal1p<EpiZeroD<EpiCheb>, XPlain, false, true><<<(unsigned)tiles, 256, 0, st>>>(GtGStencilDev{Pg}, XPlain{x},
+                                                                                         epi, G1Part{}, xc);
+        MPBP_HIP(hipGetLastError());
+        return MPBP_OK;
+    }
+    FStencilDev Pd;
+    const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &Pd);
+    if (rc) return rc;
+    const int64_t tiles = (int64_t)((nc + kG1W - 1) / kG1W) * ((nc + kG1H - 1) / kG1H);
+    k_gal1<EpiZeroD<EpiCheb>, true, XPlain, false, true><<<(unsigned)tiles, 256, 0, st>>>(
+        FStencilFast{Pd}, mg_fields(g.m), XPlain{x}, epi, G1Part{}, xc);
+    MPBP_HIP(hipGetLastError());
+    return MPBP_OK;
+}
+
 int op_spmv(const OpRef& o, int32_t mode, const double* x, const double* z, double* y, hipStream_t st) {
     if (o.empty) return MPBP_OK;
     if (o.gal) {
@@ -7340,14 +7480,15 @@ bool f_pair_ok(const mpbp_schur_plan* p) { return p->f_numerics == MPBP_NUMERICS
 template <class Xch>
 int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, double lmax, int K, bool zero,
               const double* b, double** cur, double* alt, double* d, double* dst, const double* sub, hipStream_t st,
-              Xch&& xch) {
+              Xch&& xch, int s0 = 0) {
     double c1[64] = {}, c2[64] = {};
     if (K < 1 || K > 64) return set_error(MPBP_ERR_ARG, "mg: smoothing sweeps must be in [1, 64]");
     cheb_coeffs(lmin, lmax, K, c1, c2);
     const OpRef& o = op.in;
     double* x = *cur;
     double* other = alt;
-    int s = 0;
+    int s = s0;   // s0 > 0: sweeps 0 .. s0 - 1 already ran from *cur's predecessor (d holds their direction)
+    if (s0 && (zero || s0 >= K)) return set_error(MPBP_ERR_ARG, "mg: a smoothing resumed at sweep %d of %d", s0, K);
     if (zero && K >= 2 && op.bd.empty && o.stencil && !o.stencil->halo && o.which == 0 &&
         (o.sop == SOP_F || o.sop == SOP_GTG)) {
         // whole-grid stencil level (level 0 of the Schur apply's hierarchies): the first sweep stages
@@ -7403,9 +7544,9 @@ int mg_smooth(const OpPair& op, int32_t nrows, const double* diag, double lmin, 
     const bool tpair = K - s >= 2 && o.stencil && o.sop == SOP_F && op.bd.empty && !o.stencil->halo && o.which == 0 &&
                        f_pair_ok(o.stencil) && KO().f_tile && ftile_ok(o.stencil->f_prm.n);
     // restart from the iterate in *cur: d = 0 -- read as +0.0 by the grouped kernel's first sweep, else zeroed
-    bool dzero = !zero && (((op.in.grp || op.in.svl || op.in.gal || (o.stencil && o.sop == SOP_GTG)) && op.bd.empty) ||
+    bool dzero = !zero && !s0 && (((op.in.grp || op.in.svl || op.in.gal || (o.stencil && o.sop == SOP_GTG)) && op.bd.empty) ||
                            (tpair && s == K - 2));
-    if (!zero && !dzero) MPBP_HIP(hipMemsetAsync(d, 0, sizeof(double) * (size_t)nrows, st));
+    if (!zero && !dzero && !s0) MPBP_HIP(hipMemsetAsync(d, 0, sizeof(double) * (size_t)nrows, st));
     for (; s < K; ++s) {
         if (tpair && s == K - 2) {
             double* out = dst ? dst : other;
@@ -7630,6 +7771,21 @@ int mg_vcycle(const mpbp_mg* m, int l, const MgFine& fine, const double* b, bool
         rc = launch_ftile<false>(P, a, st);
         if (rc) return rc;
         *res = out;
+        return MPBP_OK;
+    }
+    if (o.in.gal && L.post >= 1 && L.post <= 64 && gal_pro_ok(*o.in.gal)) {
+        // level 1 (matrix-free F): x + P_1 x_c staged by the first post-smoothing sweep (k_gal1<PRO>), the remaining
+        // sweeps as mg_smooth's
+        double c1[64] = {}, c2[64] = {};
+        cheb_coeffs(L.lmin, L.lmax, L.post, c1, c2);
+        const bool last = L.post == 1;
+        double* x1 = last && dst ? dst : alt;
+        const EpiCheb e{cur, b, diag, d, c1[0], c2[0], last ? sub : nullptr, x1, last ? 0 : 1};
+        rc = gal_pro(*o.in.gal, cur, xc, EpiZeroD<EpiCheb>{e}, st);
+        if (rc) return rc;
+        if (!last) rc = mg_smooth(o, L.nrows, diag, L.lmin, L.lmax, L.post, false, b, &x1, cur, d, dst, sub, st, xch, 1);
+        if (rc) return rc;
+        *res = x1;
         return MPBP_OK;
     }
     rc = use_mf_transfer(m, l) ? mg_transfer_mf(m, l, MPBP_MG_P, L.P.nrows, xc, EpiAdd{cur, cur}, st)

@@ -473,7 +473,9 @@ def test_fused_level0_descent_equals_launches(n, cycles, numerics):
     tile pair, perform the operations of the launches they replace, so the multigrid apply is bit-identical either way
     (one V-cycle and two: the second starts from x != 0 and keeps the descent's launches), eagerly and replayed; on
     grids not a multiple of the 64 x 8 tile too.  The pressure hierarchy's level 0 likewise (k_gtg_level0: descent
-    and ascent, n >= 78), in both numerics (its Gt_G rows are the same in both; exact mode keeps the F launches)."""
+    and ascent, n >= 78), in both numerics (its Gt_G rows are the same in both; exact mode keeps the F launches).  And
+    the matrix-free level 1's ascent in both hierarchies: x + P_1 x_c staged by its first post-smoothing sweep
+    (k_gal1<PRO> / k_gal1p<PRO>, fast, n >= 80 and a multiple of 4)."""
     mp = _mp()
     bp = mp.MultiphaseBlockPreconditioner(n, 1.0, 100.0, 1.0)
     _, _, F, D, G = bp.get_big_A_matrix(c=1.0, d_u=-1.0)
