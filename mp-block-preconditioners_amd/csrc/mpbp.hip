@@ -2885,10 +2885,10 @@ struct FTile {
 constexpr int kG1W = 32, kG1H = 4;                          // coarse tile
 constexpr int kG1FW = 2 * kG1W + 2, kG1FH = 2 * kG1H + 2;   // t1: fine [2 c0 - 1, 2 c0 + 2 W + 1)
 constexpr int kG1PW = kG1FW + 2, kG1PH = kG1FH + 2;         // t0 and thn: one more fine cell each side
-constexpr int kG1CW = kG1W + 4, kG1CH = kG1H + 4;           // coarse x: [c0 - 2, c0 + W + 2)
-template <int KY, int KX>
+constexpr int kG1CW = kG1W + 4;                             // coarse x: [c0 - 2, c0 + W + 2)
+template <int KY, int KX, int S = kG1CW>
 __device__ inline double g1_p(const double* xf, int gr, int gc, int nc, int rb, int cb);
-template <int KY, int KX>
+template <int KY, int KX, int S = kG1CW>
 __device__ inline double g1_p_in(const double* xf, int r, int c);
 template <int KY, int KX, int W, int OFF>
 __device__ inline double g1_rw_in(const double* tf, int lr, int lc);
@@ -4280,17 +4280,19 @@ k_gtg_level0(GtGStencilDev P, const double* __restrict__ b, const double* __rest
 }
 
 // ---- multigrid level 1 of a tolerance-mode F hierarchy in one launch (k_gal1) ----
-// A_1 x = R_0 (F (P_0 x)) (MgGal) with the two fine-size intermediates kept in LDS: a workgroup owns a 32 x 4 tile of
-// coarse cells (a 64 x 8 fine block), stages the coarse x of its four fields over the tile + 2 and thn over the fine
-// block + 2, builds t0 = P_0 x on the fine block + 2 (68 x 12), t1 = F t0 on the fine block + 1 (66 x 10, the
-// tolerance-mode rows), and R_0 t1 on its coarse rows, handing each to the level's epilogue.  Each value is built by
-// the operations of the three launches it replaces (k_mg_transfer_spmv's 1D lists and product order, FStencilFast::rows4),
-// so the result is bit-identical; HBM: x, thn and the epilogue operands once, no fine vector written or read.
-// (k_gal1's tile and window geometry: constants above)
+// A_1 x = R_0 (F (P_0 x)) (MgGal) with the two fine-size intermediates kept in LDS: a workgroup owns a 16 x 8 tile of
+// coarse cells (a 32 x 16 fine block; kGF* below), stages the coarse x of its four fields over the tile + 2 and thn
+// over the fine block + 2, builds t0 = P_0 x on the fine block + 2 (36 x 20), t1 = F t0 on the fine block + 1 (34 x 18,
+// the tolerance-mode rows), and R_0 t1 on its coarse rows, handing each to the level's epilogue.  Each value is built
+// by the operations of the three launches it replaces (k_mg_transfer_spmv's 1D lists and product order,
+// FStencilFast::rows4), so the result is bit-identical; HBM: x, thn and the epilogue operands once, no fine vector
+// written or read.  (The 32 x 4 tile of kG1* above -- the level-0 fused kernels' coarse windows -- took 42 KB of LDS,
+// three workgroups per CU: 33.1 vs 28.5 us per launch, profiles/r06s_ab_gal1_tile.txt.)
 // a grid index to its slot in a staged window starting at virtual index `base` (the window is < the grid)
 __device__ inline int g1_slot(int i, int base, int m) { int l = i - base; return l < 0 ? l + m : (l >= m ? l - m : l); }
 // P_0's row at fine (gr, gc) of a field with compile-time kinds: k_mg_transfer_spmv's list order and products
-template <int KY, int KX>
+// (S: the coarse window's row stride)
+template <int KY, int KX, int S>
 __device__ inline double g1_p(const double* xf, int gr, int gc, int nc, int rb, int cb) {
     int yi[2], xi[2];
     double yw[2], xw[2];
@@ -4299,7 +4301,7 @@ __device__ inline double g1_p(const double* xf, int gr, int gc, int nc, int rb, 
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
         if (a >= my) break;
-        const double* xr = xf + g1_slot(yi[a], rb, nc) * kG1CW;
+        const double* xr = xf + g1_slot(yi[a], rb, nc) * S;
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
             if (b >= mx) break;
@@ -4308,8 +4310,8 @@ __device__ inline double g1_p(const double* xf, int gr, int gc, int nc, int rb, 
     }
     return acc;
 }
-// R_0's row at coarse (cr, cc): 4 (cell) x 3 or 4 entries, compile-time counts
-template <int KY, int KX>
+// R_0's row at coarse (cr, cc): 4 (cell) x 3 or 4 entries, compile-time counts (S: the fine window's row stride)
+template <int KY, int KX, int S = kG1FW>
 __device__ inline double g1_r(const double* tf, int cr, int cc, int n, int rb, int cb) {
     constexpr int MY = KY == MPBP_MG_CELL ? 4 : 3, MX = KX == MPBP_MG_CELL ? 4 : 3;
     int yi[4], xi[4];
@@ -4319,7 +4321,7 @@ __device__ inline double g1_r(const double* tf, int cr, int cc, int n, int rb, i
     double acc = 0.0;
 #pragma unroll
     for (int a = 0; a < MY; ++a) {
-        const double* tr1 = tf + g1_slot(yi[a], rb, n) * kG1FW;
+        const double* tr1 = tf + g1_slot(yi[a], rb, n) * S;
 #pragma unroll
         for (int b = 0; b < MX; ++b) acc += (yw[a] * xw[b]) * tr1[g1_slot(xi[b], cb, n)];
     }
@@ -4345,18 +4347,18 @@ __device__ inline void g1_p1d_in(int r, int& lo, double& w0, double& w1) {
     }
 }
 // P_0's row at window fine (r, c) of the block + 2 (the coarse window starts two coarse cells before the tile)
-template <int KY, int KX>
+template <int KY, int KX, int S>
 __device__ inline double g1_p_in(const double* xf, int r, int c) {
     int ry, cx;
     double y0, y1, x0, x1;
     g1_p1d_in<KY>(r, ry, y0, y1);
     g1_p1d_in<KX>(c, cx, x0, x1);
-    const double* q = xf + ry * kG1CW + cx;
+    const double* q = xf + ry * S + cx;
     double acc = 0.0;
     acc += (y0 * x0) * q[0];
     acc += (y0 * x1) * q[1];
-    acc += (y1 * x0) * q[kG1CW];
-    acc += (y1 * x1) * q[kG1CW + 1];
+    acc += (y1 * x0) * q[S];
+    acc += (y1 * x1) * q[S + 1];
     return acc;
 }
 // R_0's row at tile coarse (lr, lc) over a fine window of row stride W whose slot OFF holds fine index 2 c0 - 1 (the
@@ -4375,8 +4377,8 @@ __device__ inline double g1_rw_in(const double* tf, int lr, int lc) {
     return acc;
 }
 // ... over t1's window (fine block + 1)
-template <int KY, int KX>
-__device__ inline double g1_r_in(const double* tf, int lr, int lc) { return g1_rw_in<KY, KX, kG1FW, 0>(tf, lr, lc); }
+template <int KY, int KX, int S = kG1FW>
+__device__ inline double g1_r_in(const double* tf, int lr, int lc) { return g1_rw_in<KY, KX, S, 0>(tf, lr, lc); }
 // a tile whose transfers' windows neither wrap nor reach a 1D list's periodic special case (coarse tile of TH x TW
 // cells at (cr0, cc0), windows two coarse cells beyond it)
 __device__ inline bool g1_inner(int cr0, int cc0, int th, int tw, int nc) {
@@ -4407,10 +4409,17 @@ __device__ inline int32_t g1_orow(const G1Part& q, int f, int cr, int cc, int nc
     return PART ? (f * q.L + cr - q.r0) * nc + cc : (f * nc + cr) * nc + cc;
 }
 // PRO (the post-smoothing's first sweep after level 2's correction): the staged x is x + P_1 x_c, level 2's window
-// [cr0 / 2 - 2, cr0 / 2 + kG1QH - 2) x [cc0 / 2 - 2, cc0 / 2 + kG1QW - 2) staged first (k_ftile<PRO>'s scheme one level
+// [cr0 / 2 - 2, cr0 / 2 + kGFQH - 2) x [cc0 / 2 - 2, cc0 / 2 + kGFQW - 2) staged first (k_ftile<PRO>'s scheme one level
 // down: the same P rows in window coordinates, k_mg_transfer_spmv's lists and EpiAdd's sum), and the epilogue's iterate
 // is the row's own staged value -- the prolongation launch folded in, bit-identical.
-constexpr int kG1QW = kG1W / 2 + 4, kG1QH = kG1H / 2 + 4;   // level-2 window of a k_gal1 tile (row stride kG1CW)
+// k_gal1's own tile: 16 x 8 coarse cells (a 32 x 16 fine block) -- its windows and t0 take 36.5 KB of LDS, so four
+// workgroups share a CU (the 32 x 4 tile's 42 KB held three), and F's rows on the block + 1 are 612 instead of 660
+constexpr int kGFW = 16, kGFH = 8;
+constexpr int kGFCW = kGFW + 4, kGFCH = kGFH + 4;               // coarse x: [c0 - 2, c0 + W + 2)
+constexpr int kGFFW = 2 * kGFW + 2, kGFFH = 2 * kGFH + 2;       // t1: fine block + 1
+constexpr int kGFPW = kGFFW + 2, kGFPH = kGFFH + 2;             // t0 and thn: fine block + 2
+constexpr int kGFQW = kGFW / 2 + 4, kGFQH = kGFH / 2 + 4;       // PRO: level 2's window (row stride kGFQW)
+constexpr int kG1QW = kG1W / 2 + 4;                             // (k_gal1p's level-2 window columns)
 template <bool INNER, class Epi, bool MAC, class XS, bool PART, bool PRO>
 __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& tr, const XS& xin, const Epi& epi,
                                          double* xs, double* ts, double* t0, double* t1, int cr0, int cc0,
@@ -4421,20 +4430,20 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
 template <class Epi, bool MAC = false, class XS = XPlain, bool PART = false, bool PRO = false>
 __global__ void __launch_bounds__(256) MPBP_LDS_READS k_gal1(FStencilFast P, MgFields tr, XS xin, Epi epi, G1Part q,
                                                               const double* __restrict__ xc = nullptr) {
-    constexpr int CN = kG1CW * kG1CH, PN = kG1PW * kG1PH, FN = kG1FW * kG1FH;
+    constexpr int CN = kGFCW * kGFCH, PN = kGFPW * kGFPH, FN = kGFFW * kGFFH;
     static_assert(!PRO || (MAC && !PART), "the folded prolongation: MAC kinds, whole level");
     __shared__ double xs[4 * CN];
     __shared__ double ts[PN];
     __shared__ double t0[4 * PN];
-    __shared__ double xq[PRO ? 4 * kG1CW * kG1QH : 1];
+    __shared__ double xq[PRO ? 4 * kGFQW * kGFQH : 1];
     double* t1 = t0;
     static_assert(FN <= PN, "t1 fits t0");
     const int nc = P.n >> 1;
-    const int tx = (nc + kG1W - 1) / kG1W;
+    const int tx = (nc + kGFW - 1) / kGFW;
     const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
-    const int cr0 = (PART ? q.r0 : 0) + (bk / tx) * kG1H, cc0 = (bk % tx) * kG1W;     // the coarse tile
+    const int cr0 = (PART ? q.r0 : 0) + (bk / tx) * kGFH, cc0 = (bk % tx) * kGFW;     // the coarse tile
     if constexpr (MAC) {
-        if (g1_inner(cr0, cc0, kG1H, kG1W, nc)) {
+        if (g1_inner(cr0, cc0, kGFH, kGFW, nc)) {
             gal1_run<true, Epi, MAC, XS, PART, PRO>(P, tr, xin, epi, xs, ts, t0, t1, cr0, cc0, q, xc, xq);
             return;
         }
@@ -4445,7 +4454,7 @@ template <bool INNER, class Epi, bool MAC, class XS, bool PART, bool PRO>
 __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& tr, const XS& xin, const Epi& epi,
                                          double* xs, double* ts, double* t0, double* t1, int cr0, int cc0,
                                          const G1Part& q, const double* xc, double* xq) {
-    constexpr int CN = kG1CW * kG1CH, PN = kG1PW * kG1PH, FN = kG1FW * kG1FH;
+    constexpr int CN = kGFCW * kGFCH, PN = kGFPW * kGFPH, FN = kGFFW * kGFFH;
     const int n = P.n, nc = n >> 1;
     const int fr0 = 2 * cr0, fc0 = 2 * cc0;                      // its fine block
     const int tid = threadIdx.x;
@@ -4460,7 +4469,7 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
         for (int it = 0; it < IX; ++it) {
             const int i = tid + it * 256;
             if (i < 4 * CN) {
-                const int f = i / CN, j = i - f * CN, r = j / kG1CW, c = j - r * kG1CW;
+                const int f = i / CN, j = i - f * CN, r = j / kGFCW, c = j - r * kGFCW;
                 vx[it] = xin.load(g1_xidx<PART>(q, 4, f, cr0 - 2 + r, wrapc(cc0 - 2 + c), nc));
             }
         }
@@ -4468,20 +4477,20 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
         for (int it = 0; it < IT; ++it) {
             const int i = tid + it * 256;
             if (i < PN) {
-                const int r = i / kG1PW, c = i - r * kG1PW;
+                const int r = i / kGFPW, c = i - r * kGFPW;
                 vt[it] = P.cell[P.wrap(fr0 - 2 + r) * n + P.wrap(fc0 - 2 + c)];
             }
         }
         const int n2 = nc >> 1;
         if constexpr (PRO) {   // level 2's window first: the staged x needs it
             auto wrap2 = [&](int a) { return a < 0 ? a + n2 : (a >= n2 ? a - n2 : a); };
-            constexpr int QF = kG1QW * kG1QH, IQ = (4 * QF + 255) / 256;
+            constexpr int QF = kGFQW * kGFQH, IQ = (4 * QF + 255) / 256;
             double vq[IQ];
 #pragma unroll
             for (int it = 0; it < IQ; ++it) {
                 const int i = tid + it * 256;
                 if (i < 4 * QF) {
-                    const int f = i / QF, j = i - f * QF, r = j / kG1QW, c = j - r * kG1QW;
+                    const int f = i / QF, j = i - f * QF, r = j / kGFQW, c = j - r * kGFQW;
                     vq[it] = xc[(f * n2 + wrap2((cr0 >> 1) - 2 + r)) * n2 + wrap2((cc0 >> 1) - 2 + c)];
                 }
             }
@@ -4489,26 +4498,26 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
             for (int it = 0; it < IQ; ++it) {
                 const int i = tid + it * 256;
                 if (i < 4 * QF) {
-                    const int f = i / QF, j = i - f * QF, r = j / kG1QW, c = j - r * kG1QW;
-                    xq[(f * kG1QH + r) * kG1CW + c] = vq[it];
+                    const int f = i / QF, j = i - f * QF, r = j / kGFQW, c = j - r * kGFQW;
+                    xq[(f * kGFQH + r) * kGFQW + c] = vq[it];
                 }
             }
             __syncthreads();
         }
-        const bool inner2 = PRO && g1_inner(cr0 >> 1, cc0 >> 1, kG1H / 2, kG1W / 2, n2);
+        const bool inner2 = PRO && g1_inner(cr0 >> 1, cc0 >> 1, kGFH / 2, kGFW / 2, n2);
 #pragma unroll
         for (int it = 0; it < IX; ++it) {
             const int i = tid + it * 256;
             if (i >= 4 * CN) continue;
             double v = xin.value(vx[it]);
             if constexpr (PRO) {   // x + P_1 x_c (EpiAdd: the row sum, then + x)
-                const int f = i / CN, j = i - f * CN, r = j / kG1CW, c = j - r * kG1CW;
-                const double* xf = xq + f * kG1QH * kG1CW;
+                const int f = i / CN, j = i - f * CN, r = j / kGFCW, c = j - r * kGFCW;
+                const double* xf = xq + f * kGFQH * kGFQW;
                 const int gr = wrapc(cr0 - 2 + r), gc = wrapc(cc0 - 2 + c), rb = (cr0 >> 1) - 2, cb = (cc0 >> 1) - 2;
-                const double pc = inner2 ? ((f & 1) ? g1_p_in<MPBP_MG_NODE, MPBP_MG_CELL>(xf, r, c)
-                                                    : g1_p_in<MPBP_MG_CELL, MPBP_MG_NODE>(xf, r, c))
-                                         : ((f & 1) ? g1_p<MPBP_MG_NODE, MPBP_MG_CELL>(xf, gr, gc, n2, rb, cb)
-                                                    : g1_p<MPBP_MG_CELL, MPBP_MG_NODE>(xf, gr, gc, n2, rb, cb));
+                const double pc = inner2 ? ((f & 1) ? g1_p_in<MPBP_MG_NODE, MPBP_MG_CELL, kGFQW>(xf, r, c)
+                                                    : g1_p_in<MPBP_MG_CELL, MPBP_MG_NODE, kGFQW>(xf, r, c))
+                                         : ((f & 1) ? g1_p<MPBP_MG_NODE, MPBP_MG_CELL, kGFQW>(xf, gr, gc, n2, rb, cb)
+                                                    : g1_p<MPBP_MG_CELL, MPBP_MG_NODE, kGFQW>(xf, gr, gc, n2, rb, cb));
                 v = pc + v;
             }
             xs[i] = v;
@@ -4524,7 +4533,7 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
     for (int it = 0; it < IF; ++it) {
         const int i = tid + it * 256;
         if (i < FN) {
-            const int r = i / kG1FW, c = i - r * kG1FW;
+            const int r = i / kGFFW, c = i - r * kGFFW;
             const int32_t k = P.wrap(fr0 - 1 + r) * n + P.wrap(fc0 - 1 + c);
             fu[it] = P.uface[k];
             fv[it] = P.vface[k];
@@ -4533,20 +4542,21 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
     __syncthreads();
     // t0 = P_0 x on the fine block + 2
     for (int i = tid; i < PN; i += 256) {
-        const int r = i / kG1PW, c = i - r * kG1PW;
+        const int r = i / kGFPW, c = i - r * kGFPW;
         const int gr = P.wrap(fr0 - 2 + r), gc = P.wrap(fc0 - 2 + c);
         if constexpr (MAC && INNER) {
 #pragma unroll
             for (int f = 0; f < 4; ++f)
-                t0[f * PN + i] = (f & 1) ? g1_p_in<MPBP_MG_NODE, MPBP_MG_CELL>(xs + f * CN, r, c)
-                                         : g1_p_in<MPBP_MG_CELL, MPBP_MG_NODE>(xs + f * CN, r, c);
+                t0[f * PN + i] = (f & 1) ? g1_p_in<MPBP_MG_NODE, MPBP_MG_CELL, kGFCW>(xs + f * CN, r, c)
+                                         : g1_p_in<MPBP_MG_CELL, MPBP_MG_NODE, kGFCW>(xs + f * CN, r, c);
             continue;
         }
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
             if constexpr (MAC) {
-                t0[f * PN + i] = (f & 1) ? g1_p<MPBP_MG_NODE, MPBP_MG_CELL>(xs + f * CN, gr, gc, nc, cr0 - 2, cc0 - 2)
-                                         : g1_p<MPBP_MG_CELL, MPBP_MG_NODE>(xs + f * CN, gr, gc, nc, cr0 - 2, cc0 - 2);
+                t0[f * PN + i] = (f & 1)
+                    ? g1_p<MPBP_MG_NODE, MPBP_MG_CELL, kGFCW>(xs + f * CN, gr, gc, nc, cr0 - 2, cc0 - 2)
+                    : g1_p<MPBP_MG_CELL, MPBP_MG_NODE, kGFCW>(xs + f * CN, gr, gc, nc, cr0 - 2, cc0 - 2);
                 continue;
             }
             int yi[4], xi[4];
@@ -4554,7 +4564,7 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
             const int my = mg_p1d_fast(tr.ky[f], nc, gr, yi, yw), mx = mg_p1d_fast(tr.kx[f], nc, gc, xi, xw);
             double acc = 0.0;
             for (int a = 0; a < my; ++a) {
-                const double* xr = xs + f * CN + slot(yi[a], cr0 - 2, nc) * kG1CW;
+                const double* xr = xs + f * CN + slot(yi[a], cr0 - 2, nc) * kGFCW;
                 for (int b = 0; b < mx; ++b) acc += (yw[a] * xw[b]) * xr[slot(xi[b], cc0 - 2, nc)];
             }
             t0[f * PN + i] = acc;
@@ -4563,8 +4573,8 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
     __syncthreads();
     // t1 = F t0 on the fine block + 1
     {
-        const TTileT<kG1PW> tt{ts, fr0 - 2, fc0 - 2};
-        const XTileT<kG1PW, kG1PH> xt{t0, fr0 - 2, fc0 - 2};
+        const TTileT<kGFPW> tt{ts, fr0 - 2, fc0 - 2};
+        const XTileT<kGFPW, kGFPH> xt{t0, fr0 - 2, fc0 - 2};
         // t1 takes t0's LDS (63 -> 42 KB per workgroup: 3 resident per CU instead of 2): rows kept in registers until
         // every lane has read its t0 neighbours
         double tv[IF][4];
@@ -4572,7 +4582,7 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
         for (int it = 0; it < IF; ++it) {
             const int i = tid + it * 256;
             if (i >= FN) break;
-            const int r = i / kG1FW, c = i - r * kG1FW;
+            const int r = i / kGFFW, c = i - r * kGFFW;
             double rd[4];
             P.template rows4<false>(fr0 - 1 + r, fc0 - 1 + c, tt, xt, FStencilDev::Cell{{fu[it], fv[it]}}, tv[it], rd);
         }
@@ -4588,8 +4598,8 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
     __syncthreads();
     // R_0 t1 on the tile's coarse rows (4 fields x 128 cells), each to the epilogue
     if constexpr (MAC) {   // lane t: cell t & 127 of fields (t >> 7) and (t >> 7) + 2 -- one kind pair per wave
-        const int cell = tid & (kG1W * kG1H - 1), fp = tid >> 7;
-        const int cr = cr0 + cell / kG1W, cc = cc0 + cell % kG1W;
+        const int cell = tid & (kGFW * kGFH - 1), fp = tid >> 7;
+        const int cr = cr0 + cell / kGFW, cc = cc0 + cell % kGFW;
         if (cr < (PART ? q.r0 + q.L : nc) && cc < nc) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
@@ -4598,26 +4608,26 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
                 typename Epi::P pe;
                 if constexpr (PRO) {   // the iterate is the staged x + P_1 x_c at the row
                     pe = epi.pre_lite(row);
-                    set_x(pe, xs[f * CN + (cr - cr0 + 2) * kG1CW + (cc - cc0 + 2)]);
+                    set_x(pe, xs[f * CN + (cr - cr0 + 2) * kGFCW + (cc - cc0 + 2)]);
                     set_diag(pe, epi.diag[row]);
                 } else {
                     pe = epi.pre(row);
                 }
                 double acc;
                 if constexpr (INNER)
-                    acc = fp ? g1_r_in<MPBP_MG_NODE, MPBP_MG_CELL>(t1 + f * FN, cr - cr0, cc - cc0)
-                             : g1_r_in<MPBP_MG_CELL, MPBP_MG_NODE>(t1 + f * FN, cr - cr0, cc - cc0);
+                    acc = fp ? g1_r_in<MPBP_MG_NODE, MPBP_MG_CELL, kGFFW>(t1 + f * FN, cr - cr0, cc - cc0)
+                             : g1_r_in<MPBP_MG_CELL, MPBP_MG_NODE, kGFFW>(t1 + f * FN, cr - cr0, cc - cc0);
                 else
-                    acc = fp ? g1_r<MPBP_MG_NODE, MPBP_MG_CELL>(t1 + f * FN, cr, cc, n, fr0 - 1, fc0 - 1)
-                             : g1_r<MPBP_MG_CELL, MPBP_MG_NODE>(t1 + f * FN, cr, cc, n, fr0 - 1, fc0 - 1);
+                    acc = fp ? g1_r<MPBP_MG_NODE, MPBP_MG_CELL, kGFFW>(t1 + f * FN, cr, cc, n, fr0 - 1, fc0 - 1)
+                             : g1_r<MPBP_MG_CELL, MPBP_MG_NODE, kGFFW>(t1 + f * FN, cr, cc, n, fr0 - 1, fc0 - 1);
                 epi(row, acc, pe);
             }
         }
         return;
     }
-    for (int j = tid; j < 4 * kG1W * kG1H; j += 256) {
-        const int f = j / (kG1W * kG1H), cell = j - f * (kG1W * kG1H);
-        const int cr = cr0 + cell / kG1W, cc = cc0 + cell % kG1W;
+    for (int j = tid; j < 4 * kGFW * kGFH; j += 256) {
+        const int f = j / (kGFW * kGFH), cell = j - f * (kGFW * kGFH);
+        const int cr = cr0 + cell / kGFW, cc = cc0 + cell % kGFW;
         if (cr >= (PART ? q.r0 + q.L : nc) || cc >= nc) continue;
         const int32_t row = g1_orow<PART>(q, f, cr, cc, nc);
         const typename Epi::P pe = epi.pre(row);
@@ -4626,7 +4636,7 @@ __device__ __forceinline__ void gal1_run(const FStencilFast& P, const MgFields& 
         const int my = mg_r1d_fast(tr.ky[f], n, cr, yi, yw), mx = mg_r1d_fast(tr.kx[f], n, cc, xi, xw);
         double acc = 0.0;
         for (int a = 0; a < my; ++a) {
-            const double* tr1 = t1 + f * FN + slot(yi[a], fr0 - 1, n) * kG1FW;
+            const double* tr1 = t1 + f * FN + slot(yi[a], fr0 - 1, n) * kGFFW;
             for (int b = 0; b < mx; ++b) acc += (yw[a] * xw[b]) * tr1[slot(xi[b], fc0 - 1, n)];
         }
         epi(row, acc, pe);
@@ -7040,7 +7050,7 @@ int gal_fused(const MgGal& g, XS x, Epi epi, hipStream_t st, bool* done) {
         F.kx[f] = g.m->tr_kx[f];
     }
     const int nc = p->f_prm.n / 2;
-    const int64_t tiles = (int64_t)((nc + kG1W - 1) / kG1W) * (((part ? q.L : nc) + kG1H - 1) / kG1H);
+    const int64_t tiles = (int64_t)((nc + kGFW - 1) / kGFW) * (((part ? q.L : nc) + kGFH - 1) / kGFH);
     bool mac = true;   // the F hierarchy's MAC kinds (mg.FIELDS_VELOCITY)
     for (int f = 0; f < 4; ++f)
         mac = mac && F.ky[f] == ((f & 1) ? MPBP_MG_NODE : MPBP_MG_CELL) && F.kx[f] == ((f & 1) ? MPBP_MG_CELL : MPBP_MG_NODE);
@@ -7085,7 +7095,7 @@ int gal_pro(const MgGal& g, const double* x, const double* xc, const EpiZeroD<Ep
     FStencilDev Pd;
     const int rc = make_fstencil(&p->f_prm, p->f_cell, p->f_uface, p->f_vface, nullptr, &Pd);
     if (rc) return rc;
-    const int64_t tiles = (int64_t)((nc + kG1W - 1) / kG1W) * ((nc + kG1H - 1) / kG1H);
+    const int64_t tiles = (int64_t)((nc + kGFW - 1) / kGFW) * ((nc + kGFH - 1) / kGFH);
     k_gal1<EpiZeroD<EpiCheb>, true, XPlain, false, true><<<(unsigned)tiles, 256, 0, st>>>(
         FStencilFast{Pd}, mg_fields(g.m), XPlain{x}, epi, G1Part{}, xc);
     MPBP_HIP(hipGetLastError());
