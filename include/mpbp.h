@@ -508,7 +508,8 @@ typedef struct mpbp_kernel_opts {
     int32_t mg_fuse_small;     /* whole-grid multigrid levels l >= 1 on k_csr_grp rows (<= mg_group_rows) with matrix-free
                                   transfers and a coarse level of <= 1024 rows: residual + restriction as ONE launch
                                   (k_grp_rr; 1, default; the same bits as 0) */
-    int32_t reserved[2];
+    int32_t gtg_solve_tile;    /* fused Gt_G solves (k_gtg_solve): 1 (default) 32 x 16 tiles, 0 the 64 x 8 tile; the same bits */
+    int32_t reserved[1];
 } mpbp_kernel_opts;
 /* *out = the calling thread's current choices: its mpbp_kernel_opts_set_thread scope, else the process defaults. */
 void mpbp_kernel_opts_default(mpbp_kernel_opts* out);

@@ -86,7 +86,7 @@ class KernelOpts(Structure):
                 ("pg_direct", c_int32), ("mg_group_rows", c_int32), ("mg_svl", c_int32), ("mg_mf_transfer", c_int32),
                 ("csr_table", c_int32), ("mg_fuse_l0", c_int32), ("mg_coarse_tree", c_int32),
                 ("f_solve_tile", c_int32), ("q13_mf", c_int32), ("mg_fuse_small", c_int32),
-                ("reserved", c_int32 * 2)]
+                ("gtg_solve_tile", c_int32), ("reserved", c_int32 * 1)]
 
 
 def kernel_opts(overrides=None) -> KernelOpts:

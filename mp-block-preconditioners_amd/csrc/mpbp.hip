@@ -28,7 +28,7 @@ mpbp_kernel_opts g_defaults = {
     /*march_rows*/ 0, /*init_diag*/ 1, /*f_pair*/ 1, /*f_direct*/ 0, /*gtg_fused*/ 1, /*gtg_tpb*/ 512, /*gtg_drhs*/ 1,
     /*q13_sym*/ 1, /*f_tile*/ 1, /*f_solve*/ 1, /*mg_galerkin_mf*/ 2, /*mg_galerkin_mf_p*/ 1, /*pg_direct*/ 1,
     /*mg_group_rows*/ 65536, /*mg_svl*/ 1, /*mg_mf_transfer*/ 1, /*csr_table*/ 1, /*mg_fuse_l0*/ 1,
-    /*mg_coarse_tree*/ 0, /*f_solve_tile*/ 1, /*q13_mf*/ 0, /*mg_fuse_small*/ 1, {0, 0}};
+    /*mg_coarse_tree*/ 0, /*f_solve_tile*/ 1, /*q13_mf*/ 0, /*mg_fuse_small*/ 1, /*gtg_solve_tile*/ 1, {0}};
 thread_local const mpbp_kernel_opts* t_opts = nullptr;
 inline const mpbp_kernel_opts& KO() { return t_opts ? *t_opts : g_defaults; }
 struct OptsScope {   // installs a plan's kernel choices (when it has its own) for one entry-point call
@@ -48,10 +48,10 @@ inline int check_opts(const mpbp_kernel_opts* o, const char* who) {
                     o->mg_galerkin_mf >= 0 && o->mg_galerkin_mf <= 2 && o->mg_group_rows >= 0 &&
                     (o->init_diag | o->f_pair | o->f_direct | o->gtg_fused | o->gtg_drhs | o->q13_sym | o->f_tile |
                      o->f_solve | o->mg_galerkin_mf_p | o->pg_direct | o->mg_svl | o->mg_mf_transfer | o->csr_table |
-                     o->mg_fuse_l0 | o->mg_coarse_tree | o->q13_mf | o->mg_fuse_small) >= 0 &&
+                     o->mg_fuse_l0 | o->mg_coarse_tree | o->q13_mf | o->mg_fuse_small | o->gtg_solve_tile) >= 0 &&
                     (o->init_diag | o->f_pair | o->f_direct | o->gtg_fused | o->gtg_drhs | o->q13_sym | o->f_tile |
                      o->f_solve | o->mg_galerkin_mf_p | o->pg_direct | o->mg_svl | o->mg_mf_transfer | o->csr_table |
-                     o->mg_fuse_l0 | o->mg_coarse_tree | o->q13_mf | o->mg_fuse_small) <= 1;
+                     o->mg_fuse_l0 | o->mg_coarse_tree | o->q13_mf | o->mg_fuse_small | o->gtg_solve_tile) <= 1;
     return ok ? MPBP_OK : set_error(MPBP_ERR_ARG, "%s: kernel options out of range", who);
 }   // rows per workgroup of the D / G / Gt_G marching kernels: as F
 
@@ -3900,9 +3900,11 @@ constexpr int kGTW = kFTW, kGTH = kFTH;   // the 64 x 8 tile and ring numbering 
 struct ChebK {
     double c1[8], c2[8];   // sweep s's coefficients (c2[0]: the initial iterate's)
 };
-template <int H>
-struct GtgTile {
-    static constexpr int RW = kGTW + 2 * H, RH = kGTH + 2 * H, N = RW * RH;
+template <int H, int GW = kGTW, int GH = kGTH>
+struct GtgTile {   // a GW x GH tile of cells with H halo levels
+    static constexpr int RW = GW + 2 * H, RH = GH + 2 * H, N = RW * RH;
+    static constexpr int ring(int r) { return 2 * GW + 2 * GH - 4 + 8 * r; }   // cells of halo ring r
+    static constexpr int rings(int h) { return h < 1 ? 0 : ring(h) + rings(h - 1); }
 };
 template <int H>
 struct TTile {   // thn of the staged tile; (r, c) in the tile's virtual grid coordinates
@@ -3926,22 +3928,24 @@ struct GtgD {
     const double* Y;    // Finv_v: u_n, v_n, u_s, v_s
     const double* vp;   // v's pressure part
 };
-template <int H, bool PART, int TPB, bool DB>
+template <int H, bool PART, int TPB, bool DB, int GW = kGTW, int GH = kGTH>
 __global__ void __launch_bounds__(TPB) MPBP_LDS_READS k_gtg_solve(GtGStencilDev P, const double* __restrict__ b,
                                                    const double* __restrict__ diag, ChebK ck, double* __restrict__ out,
                                                    GtgD dv) {
-    using G = GtgTile<H>;
-    constexpr int TW = DB ? G::RW + 2 : G::RW, TN = DB ? TW * (G::RH + 2) : G::N;   // staged thn
-    constexpr int NM = TPB == 256 ? 2 : 1;           // tile cells per lane
+    using G = GtgTile<H, GW, GH>;
+    constexpr int SW = DB ? G::RW + 2 : G::RW, TN = DB ? SW * (G::RH + 2) : G::N;   // staged thn
+    constexpr int NM = GW * GH / TPB;                // tile cells per lane
     constexpr int NR = TPB == 256 ? H - 1 : 1;       // ring slots per lane (rings 1 .. H - 1)
     constexpr int NS = NM + NR;
-    static_assert(TPB == 256 || 140 * (H - 1) + 4 * H * (H - 1) <= 512, "512 lanes own at most one ring cell each");
+    static_assert(NM * TPB == GW * GH && TPB % GW == 0, "whole tile rows per lane group");
+    static_assert(TPB == 512 || G::ring(H - 1) <= 256, "256 lanes own one cell of each ring");
+    static_assert(TPB == 256 || G::rings(H - 1) <= 512, "512 lanes own at most one ring cell each");
     __shared__ double ts[TN], bs[G::N], xa[G::N], xb[G::N];
     const int n = P.n;
-    const int tx = (n + kGTW - 1) / kGTW;
+    const int tx = (n + GW - 1) / GW;
     const int bk = xcd_swizzle(blockIdx.x, gridDim.x);
     const int lo = PART ? P.r0 - P.ext : 0, hi = PART ? P.r0 + P.L + P.ext : n;   // output rows [lo, hi)
-    const int r0 = lo + (bk / tx) * kGTH, c0 = (bk % tx) * kGTW;
+    const int r0 = lo + (bk / tx) * GH, c0 = (bk % tx) * GW;
     const int rb = r0 - H, cb = c0 - H;   // virtual coordinates of staged cell 0
     const int tid = threadIdx.x;
     // level 0 over the whole staged region: thn, b, x0 = c2_0 (b / diag); every load issued before the first LDS store
@@ -3954,7 +3958,7 @@ __global__ void __launch_bounds__(TPB) MPBP_LDS_READS k_gtg_solve(GtGStencilDev 
             for (int it = 0; it < IT; ++it) {
                 const int i = tid + it * TPB;
                 if (i < TN) {
-                    const int rr = i / TW, cc = i - rr * TW;
+                    const int rr = i / SW, cc = i - rr * SW;
                     tv[it] = P.cell[P.wrap(rb - 1 + rr) * n + P.wrap(cb - 1 + cc)];
                 }
             }
@@ -3984,7 +3988,7 @@ __global__ void __launch_bounds__(TPB) MPBP_LDS_READS k_gtg_solve(GtGStencilDev 
             dgl[it] = diag[k];
         }
         __syncthreads();
-        const TTileT<TW> tD{ts, rb - 1, cb - 1};
+        const TTileT<SW> tD{ts, rb - 1, cb - 1};
 #pragma unroll
         for (int it = 0; it < IY; ++it) {
             const int i = tid + it * TPB;
@@ -4044,33 +4048,33 @@ __global__ void __launch_bounds__(TPB) MPBP_LDS_READS k_gtg_solve(GtGStencilDev 
     }
     __syncthreads();
     // the owned cells (slot 0, 1: the tile's; slot 1 + r: ring r), their entries, b and d0 = x0
-    const TTileT<TW> ta{ts, DB ? rb - 1 : rb, DB ? cb - 1 : cb};
-    const int lr = tid >> 6, lc = tid & 63;
+    const TTileT<SW> ta{ts, DB ? rb - 1 : rb, DB ? cb - 1 : cb};
+    const int lr = tid / GW, lc = tid % GW;
     int cr[NS], cc[NS], si[NS], rr[NS];
     bool own[NS], edge[NS];
     double e[NS][5], bo[NS], d[NS];
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
-        cr[m] = r0 + lr + 4 * m; cc[m] = c0 + lc; own[m] = true; rr[m] = 0;
+        cr[m] = r0 + lr + (TPB / GW) * m; cc[m] = c0 + lc; own[m] = true; rr[m] = 0;
     }
     if constexpr (TPB == 256) {
 #pragma unroll
         for (int r = 1; r < H; ++r) {
-            own[NM + r - 1] = tid < 140 + 8 * r;
+            own[NM + r - 1] = tid < G::ring(r);
             rr[NM + r - 1] = r;
-            fs_ring_cell(r, own[NM + r - 1] ? tid : 0, r0, c0, cr[NM + r - 1], cc[NM + r - 1]);
+            fs_ring_cell_t<GW, GH>(r, own[NM + r - 1] ? tid : 0, r0, c0, cr[NM + r - 1], cc[NM + r - 1]);
         }
     } else if constexpr (NR > 0) {
         int r = 0, j = tid;   // rings 1 .. H - 1 numbered ring 1 first: lane t owns cell t of that sequence
 #pragma unroll
         for (int q = 1; q < H; ++q)
             if (r == 0) {
-                if (j < 140 + 8 * q) r = q;
-                else j -= 140 + 8 * q;
+                if (j < G::ring(q)) r = q;
+                else j -= G::ring(q);
             }
         own[NM] = r != 0;
         rr[NM] = r;
-        fs_ring_cell(r ? r : 1, r ? j : 0, r0, c0, cr[NM], cc[NM]);
+        fs_ring_cell_t<GW, GH>(r ? r : 1, r ? j : 0, r0, c0, cr[NM], cc[NM]);
     }
 #pragma unroll
     for (int sl = 0; sl < NS; ++sl) {
@@ -7834,36 +7838,47 @@ int d_rhs_x0(const mpbp_schur_plan* p, const double* Y, const double* v_p, doubl
 }
 
 // x = Gt_G^-1 b by the plan's Chebyshev inner solve in one k_gtg_solve launch (one GPU, matrix-free Gt_G, 2..6 sweeps).
-template <int H>
-int launch_gtg_solve_t(const GtGStencilDev& S, const double* b, const double* diag, const ChebK& ck, double* out,
-                       hipStream_t st, GtgD dv = GtgD{}) {
+template <int H, int GW, int GH>
+int launch_gtg_solve_g(const GtGStencilDev& S, const double* b, const double* diag, const ChebK& ck, double* out,
+                       hipStream_t st, GtgD dv) {
     const bool part = S.h != 0;
     // every staged cell of a tile (tile + H + 1 each side) must wrap onto the grid at most once (the staging's periodic
-    // fold subtracts n once): refuse smaller grids here, whatever the caller checked (gtg_fused_ok)
-    if (S.n < kGTW + kGTH + 2 * H)
-        return set_error(MPBP_ERR_ARG, "gtg_solve: a %d-sweep fused solve needs n >= %d (n = %d)", H + 1,
-                         kGTW + kGTH + 2 * H, S.n);
+    // fold subtracts n once): refuse smaller grids here, whatever the caller checked (gtg_fused_ok) -- one bound for
+    // both tiles (the 64 x 8 tile's, the larger), so the tile option never changes which grids the fused solve takes
+    constexpr int kMin = kGTW + kGTH + 2 * H;
+    static_assert(GW + GH + 2 * H <= kMin, "the documented bound covers this tile");
+    if (S.n < kMin)
+        return set_error(MPBP_ERR_ARG, "gtg_solve: a %d-sweep fused solve needs n >= %d (n = %d)", H + 1, kMin, S.n);
     const int rows = part ? S.L + 2 * S.ext : S.n;
-    const int64_t tiles = (int64_t)((S.n + kGTW - 1) / kGTW) * ((rows + kGTH - 1) / kGTH);
+    const int64_t tiles = (int64_t)((S.n + GW - 1) / GW) * ((rows + GH - 1) / GH);
     const bool db = dv.Y != nullptr;
     if (db && part) return set_error(MPBP_ERR_ARG, "gtg_solve: the fused D right-hand side is one-GPU only");
-    // 512 lanes own rings 1 .. H - 1 one cell each (140 (H - 1) + 4 H (H - 1) <= 512 cells): H <= 4
-    if constexpr (H <= 4) {
+    // 512 lanes own rings 1 .. H - 1 one cell each (GtgTile::rings(H - 1) <= 512 cells)
+    if constexpr (GtgTile<H, GW, GH>::rings(H - 1) <= 512) {
         if (KO().gtg_tpb == 512) {
-            if (db) k_gtg_solve<H, false, 512, true><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, ck, out, dv);
-            else if (part) k_gtg_solve<H, true, 512, false><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, ck, out, dv);
-            else k_gtg_solve<H, false, 512, false><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, ck, out, dv);
+            if (db) k_gtg_solve<H, false, 512, true, GW, GH><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, ck, out, dv);
+            else if (part)
+                k_gtg_solve<H, true, 512, false, GW, GH><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, ck, out, dv);
+            else k_gtg_solve<H, false, 512, false, GW, GH><<<(unsigned)tiles, 512, 0, st>>>(S, b, diag, ck, out, dv);
             MPBP_HIP(hipGetLastError());
             return MPBP_OK;
         }
     }
     {
-        if (db) k_gtg_solve<H, false, 256, true><<<(unsigned)tiles, 256, 0, st>>>(S, b, diag, ck, out, dv);
-        else if (part) k_gtg_solve<H, true, 256, false><<<(unsigned)tiles, 256, 0, st>>>(S, b, diag, ck, out, dv);
-        else k_gtg_solve<H, false, 256, false><<<(unsigned)tiles, 256, 0, st>>>(S, b, diag, ck, out, dv);
+        if (db) k_gtg_solve<H, false, 256, true, GW, GH><<<(unsigned)tiles, 256, 0, st>>>(S, b, diag, ck, out, dv);
+        else if (part) k_gtg_solve<H, true, 256, false, GW, GH><<<(unsigned)tiles, 256, 0, st>>>(S, b, diag, ck, out, dv);
+        else k_gtg_solve<H, false, 256, false, GW, GH><<<(unsigned)tiles, 256, 0, st>>>(S, b, diag, ck, out, dv);
     }
     MPBP_HIP(hipGetLastError());
     return MPBP_OK;
+}
+// kernel option gtg_solve_tile: 32 x 16 tiles (1) -- shorter halo rings, fewer staged and halo cells per output, as
+// k_fsolve_w -- or the 64 x 8 tile (0); every cell's operations are the same, so are the bits
+template <int H>
+int launch_gtg_solve_t(const GtGStencilDev& S, const double* b, const double* diag, const ChebK& ck, double* out,
+                       hipStream_t st, GtgD dv = GtgD{}) {
+    return KO().gtg_solve_tile ? launch_gtg_solve_g<H, 32, 16>(S, b, diag, ck, out, st, dv)
+                               : launch_gtg_solve_g<H, kGTW, kGTH>(S, b, diag, ck, out, st, dv);
 }
 // The tile's staged cells must wrap onto the grid at most once each way (P.wrap), so n >= a tile plus its halos.
 // part: under a row partition (the CA schedule's solves), else one GPU.
