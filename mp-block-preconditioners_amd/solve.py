@@ -824,6 +824,7 @@ def _fgmres_dcgs2(Aop, Mop, b, x0, tol, m, maxiter, callback, residuals, K):
         zc = None                               # column j - 1's first-pass part (z, c), completed in iteration j
         head(0)
         done = False
+        cyc = []                                # this cycle's residual estimates
         for j in range(m + 1):
             form = j < m and it + (1 if j > 0 else 0) < maxiter   # column j will be formed (w = A M u_j is needed)
             ubound = vb[j:j + 1]
@@ -839,8 +840,14 @@ def _fgmres_dcgs2(Aop, Mop, b, x0, tol, m, maxiter, callback, residuals, K):
             hbuf[: 2 * j + 6].copy_(torch.cat([hu, hw, P]), non_blocking=on_gpu)
             if on_gpu:
                 ev.record()
-            if form and j + 1 < m and it + (1 if j > 0 else 0) + 1 < maxiter:
-                head(j + 1)                     # speculative: queued behind the copy, runs while the host works
+            nxt = form and j + 1 < m and it + (1 if j > 0 else 0) + 1 < maxiter
+            # head(j + 1) is speculative: queued behind the copy, it runs while the host completes column j - 1.  When
+            # the estimates' rate says that column is likely the last (the next estimate within 2x of the target), it
+            # waits for the host instead: a converged solve then skips one apply (an mg:4 / mg:1 apply is 4.3 ms at
+            # 1024^2) for one host round trip when it does not converge.  Only the timing changes, never the values.
+            late = nxt and len(cyc) >= 2 and cyc[-2] > 0.0 and cyc[-1] * (cyc[-1] / cyc[-2]) <= 2.0 * target
+            if nxt and not late:
+                head(j + 1)
             if on_gpu:
                 ev.synchronize()
             host = hbuf[: 2 * j + 6].tolist()
@@ -872,6 +879,7 @@ def _fgmres_dcgs2(Aop, Mop, b, x0, tol, m, maxiter, callback, residuals, K):
                 k = j
                 it += 1
                 res = abs(g[col + 1])
+                cyc.append(res)
                 if residuals is not None and not lost:
                     residuals.append(res)
                 if callback is not None:
@@ -881,6 +889,8 @@ def _fgmres_dcgs2(Aop, Mop, b, x0, tol, m, maxiter, callback, residuals, K):
                     break
             if not form:
                 break
+            if late:
+                head(j + 1)                     # the deferred speculation: the cycle goes on
             zc = (z_, cj, rinvj)
         x = lincomb(x, Z, k, _solve_upper(H, g, k))
         r = b - Aop(x)
