@@ -824,7 +824,7 @@ def _fgmres_dcgs2(Aop, Mop, b, x0, tol, m, maxiter, callback, residuals, K):
         zc = None                               # column j - 1's first-pass part (z, c), completed in iteration j
         head(0)
         done = False
-        cyc = []                                # this cycle's residual estimates
+        cyc = [beta]                            # this cycle's residual estimates, from its initial residual
         for j in range(m + 1):
             form = j < m and it + (1 if j > 0 else 0) < maxiter   # column j will be formed (w = A M u_j is needed)
             ubound = vb[j:j + 1]
@@ -842,10 +842,11 @@ def _fgmres_dcgs2(Aop, Mop, b, x0, tol, m, maxiter, callback, residuals, K):
                 ev.record()
             nxt = form and j + 1 < m and it + (1 if j > 0 else 0) + 1 < maxiter
             # head(j + 1) is speculative: queued behind the copy, it runs while the host completes column j - 1.  When
-            # the estimates' rate says that column is likely the last (the next estimate within 2x of the target), it
-            # waits for the host instead: a converged solve then skips one apply (an mg:4 / mg:1 apply is 4.3 ms at
-            # 1024^2) for one host round trip when it does not converge.  Only the timing changes, never the values.
-            late = nxt and len(cyc) >= 2 and cyc[-2] > 0.0 and cyc[-1] * (cyc[-1] / cyc[-2]) <= 2.0 * target
+            # the estimates' rate says that column may be the last (the next estimate within 10x of the target), it
+            # waits for the host instead: a converged solve then skips one apply (an mg:8 / mg:1 apply is ~8 ms at
+            # 1024^2) for one host round trip (~0.25 ms) when it does not converge.  Only the timing changes, never
+            # the values.
+            late = nxt and len(cyc) >= 2 and cyc[-2] > 0.0 and cyc[-1] * (cyc[-1] / cyc[-2]) <= 10.0 * target
             if nxt and not late:
                 head(j + 1)
             if on_gpu:
